@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Benchmark: SAC gradient-steps/s on Humanoid-v5 shapes (BASELINE.json `metric`).
+
+One "step" = one full SAC update (sac_imp.py:74-152): device random.sample over the
+HBM replay ring (1M rows by default), gather, target, twin-critic fwd/bwd + Adam,
+actor fwd/bwd + Adam, alpha update, Polyak — on synthetic Humanoid-shaped data
+(obs 376, act 17, hidden 512, batch 256 per GPU; random-init weights).
+
+Single GPU:   python bench.py [--steps K --warmup W]
+N GPUs:       python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+              (data parallel: per-GPU replay shard, per-GPU batch 256, critic and actor
+              gradients all-reduced over RCCL; value = N * iterations/s, i.e.
+              batch-256-equivalent gradient steps per second, weak scaling).
+
+Prints ONE JSON line (rank 0).  Extra objects: `roofline` (dominant kernel = the
+grouped fp32 MFMA GEMM, timed with HIP events on its launch stream) and
+`cpu_baseline` (the oracle's torch-CPU port of the reference update + deque replay
+on this host's cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "humanoid-walking-with-sac_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+S_DIM, A_DIM, HIDDEN, BATCH = 376, 17, 512, 256
+PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_HBM_GBS = 8000.0
+
+
+def necessary_flops(S, A, H, B):
+    """GEMM FLOPs the update needs (excludes the reference's wasted
+    actor-pass Q dW and state columns of Q-fc1 dX)."""
+    Qf = (S + A) * H + H * H + H
+    Pf = S * H + H * H + 2 * H * A
+    Qdx = H + H * H + H * A
+    Pbw = Pf + H * H + 2 * H * A
+    return 2 * B * ((Pf + 2 * Qf) + 2 * (2 * Qf + H + H * H) + (Pf + 2 * Qf + 2 * Qdx + Pbw))
+
+
+def synth(n, seed):
+    rng = np.random.default_rng(seed)
+    s = rng.standard_normal((n, S_DIM), dtype=np.float32)
+    s2 = rng.standard_normal((n, S_DIM), dtype=np.float32)
+    a = rng.uniform(-0.4, 0.4, size=(n, A_DIM)).astype(np.float32)
+    r = rng.standard_normal(n, dtype=np.float32)
+    d = (rng.random(n) < 0.02).astype(np.uint8)
+    return s, a, r, s2, d
+
+
+def init_agent(ctx, seed):
+    """Xavier-uniform weights, zero biases (networks_model1.py:22-25,60-63)."""
+    rng = np.random.default_rng(seed)
+    from sacmi.core import net_keys
+    shapes = {"policy": {"fc1": (HIDDEN, S_DIM), "fc2": (HIDDEN, HIDDEN), "mean": (A_DIM, HIDDEN),
+                         "log_std": (A_DIM, HIDDEN)},
+              "q": {"fc1": (HIDDEN, S_DIM + A_DIM), "fc2": (HIDDEN, HIDDEN), "fc3": (1, HIDDEN)}}
+    q_sd = {}
+    for net in ("policy", "q1", "q2"):
+        shp = shapes["policy" if net == "policy" else "q"]
+        sd = {}
+        for key, _layer, part in net_keys(net):
+            lname = key.split(".")[0]
+            o, i = shp[lname]
+            if part == 0:
+                b = np.sqrt(6.0 / (o + i))
+                sd[key] = rng.uniform(-b, b, size=(o, i)).astype(np.float32)
+            else:
+                sd[key] = np.zeros(o, np.float32)
+        ctx.set_net(net, sd)
+        q_sd[net] = sd
+    ctx.set_net("q1_target", q_sd["q1"])
+    ctx.set_net("q2_target", q_sd["q2"])
+
+
+def gemm_roofline(ctx, batch, iters=20):
+    sites = ctx.profile_step(batch, iters)
+    g = [(n, ms, f) for (n, ms, f) in sites if n.startswith("gemm_") or n == "heads_sample"]
+    tot_ms = sum(ms for _, ms, _ in sites)
+    gemm = [(n, ms, f) for (n, ms, f) in sites if n.startswith("gemm_")]
+    gms = sum(ms for _, ms, _ in gemm)
+    gfl = sum(f for _, _, f in gemm)
+    launches = len(gemm)
+    avg_ms = gms / launches
+    achieved = (gfl / launches) / (avg_ms * 1e-3) / 1e12
+    return dict(sites=sites, step_ms_eager=tot_ms, gemm_ms=gms, gemm_flops=gfl,
+                launches=launches, avg_launch_ms=avg_ms, achieved_tflops=achieved), g
+
+
+def cpu_baseline(rows, seconds=15.0, warmup=5):
+    """The reference update on CPU (oracle torch port, fp32) + the reference's deque
+    replay data path, timed on this host's cores for a bounded number of steps."""
+    import random
+    from oracle.replay_ref import DequeReplay
+    from oracle.sac_step import OracleSAC, SacConfig, init_params
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = SacConfig(S_DIM, A_DIM, HIDDEN)
+    agent = OracleSAC(cfg, init_params(cfg, 0), dtype=torch.float32)
+    s, a, r, s2, d = rows
+    buf = DequeReplay(capacity=len(r))
+    for i in range(len(r)):
+        buf.push(s[i], a[i], float(r[i]), s2[i], bool(d[i]))
+    random.seed(0)
+    gen = torch.Generator().manual_seed(0)
+
+    def one():
+        bs, ba, br, bs2, bd = buf.sample(BATCH)
+        e1 = torch.randn(BATCH, A_DIM, generator=gen).numpy()
+        e2 = torch.randn(BATCH, A_DIM, generator=gen).numpy()
+        agent.step(bs, ba, br, bs2, bd, e1, e2)
+
+    for _ in range(warmup):
+        one()
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        one()
+        n += 1
+    dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return dict(value=n / dt, unit="grad-steps/s", cores=threads, kind="port",
+                sample=f"{n} updates (after {warmup} warm-up) in {dt:.1f}s; oracle torch-CPU fp32 "
+                       f"port of sac_imp.update_parameters + deque/random.sample replay over "
+                       f"{len(r)} rows (float32 rows); {threads} threads on {cpu}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--fill", type=int, default=1_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--profile-only", action="store_true",
+                    help="just run warmup+steps (for rocprofv3 runs)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        from sacmi.dp import run_dp_bench
+        return run_dp_bench(args, rank, world, local_rank)
+
+    from sacmi import Config, Context
+    torch.cuda.init()
+    fill = args.fill
+    ctx = Context(Config(S_DIM, A_DIM, HIDDEN, max_batch=args.batch, capacity=fill, seed=1), 0)
+    init_agent(ctx, 0)
+    t_fill = time.perf_counter()
+    chunk = 100_000
+    rows_keep = None
+    for c0 in range(0, fill, chunk):
+        rows = synth(min(chunk, fill - c0), 1000 + c0)
+        ctx.push(*rows)
+        if rows_keep is None:
+            rows_keep = rows
+    t_fill = time.perf_counter() - t_fill
+
+    for _ in range(args.warmup):
+        ctx.step_async(args.batch)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.step_async(args.batch)
+    losses = ctx.fetch_losses(args.steps)      # D2H of every loss, inside the timed region
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert losses.shape == (args.steps, 3) and np.all(np.isfinite(losses)), losses[-3:]
+    if args.profile_only:
+        print(json.dumps({"steps": args.steps, "ms_per_step": 1e3 * dt / args.steps}))
+        return
+    sps = args.steps / dt
+
+    # API-faithful mode: losses synced every step (sac_imp.py:140-144 .item())
+    n_sync = max(20, args.steps // 4)
+    t1 = time.perf_counter()
+    for _ in range(n_sync):
+        ctx.step(args.batch)
+    sync_sps = n_sync / (time.perf_counter() - t1)
+
+    roof = None
+    if not args.no_roofline:
+        info, _ = gemm_roofline(ctx, args.batch)
+        roof = {"bound": "mfma", "achieved": round(info["achieved_tflops"], 3),
+                "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(info["achieved_tflops"] / PEAK_FP32_MFMA_TFLOPS, 4),
+                "traffic": None, "kernel": "k_gemm<32,32,4> (grouped fp32 MFMA GEMM)",
+                "launches_per_step": info["launches"],
+                "avg_launch_us": round(info["avg_launch_ms"] * 1e3, 3),
+                "gemm_flops_per_step": info["gemm_flops"],
+                "eager_step_us": round(info["step_ms_eager"] * 1e3, 2),
+                "sites_us": {n: round(ms * 1e3, 2) for (n, ms, _) in info["sites"]}}
+    flops = necessary_flops(S_DIM, A_DIM, HIDDEN, args.batch)
+    cpu = None
+    if not args.no_cpu_baseline:
+        n_cpu = min(fill, 1_000_000)
+        cpu_rows = tuple(x[:n_cpu] for x in synth(n_cpu, 7))
+        cpu = cpu_baseline(cpu_rows, seconds=args.cpu_seconds)
+    out = {
+        "metric": "SAC gradient-steps/sec, Humanoid-v5 batch=256 (obs 376, act 17, hidden 512)",
+        "value": round(sps, 2), "unit": "grad-steps/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 / sps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": "BASELINE configs[1]: Humanoid-v5 shapes, hidden=512, batch=256, "
+                               "uniform replay (HBM ring, device random.sample)",
+                   "state_dim": S_DIM, "action_dim": A_DIM, "hidden": HIDDEN,
+                   "global_batch": args.batch, "replay_fill": fill, "parallelism": "single GPU"},
+        "api_faithful_steps_per_s": round(sync_sps, 2),
+        "mfma_util_step": round(flops * sps / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
+        "necessary_gflop_per_step": round(flops / 1e9, 4),
+        "roofline": roof, "cpu_baseline": cpu,
+        "fill_seconds": round(t_fill, 2),
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

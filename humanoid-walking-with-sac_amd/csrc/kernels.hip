@@ -1,0 +1,562 @@
+// HIP/CDNA4 kernels of the SAC gradient step (gfx950).
+//
+// GEMMs: fp32-in / fp32-accumulate MFMA (v_mfma_f32_16x16x4_f32, exact-f32 fma
+// chain) — the reference computes in fp32 (sac_imp.py:81-85 FloatTensor), gfx950
+// has no xf32, so this is the native full-precision matrix path.
+//
+// Fragment mapping of v_mfma_f32_16x16x4_f32 (cdna_hip_programming.md §3):
+//   lane l supplies A[i = l&15][kk = l>>4] and B[kk = l>>4][j = l&15];
+//   D[row = (l>>4)*4 + r][col = l&15] lands in accumulator register r.
+// A 16-deep K chunk is consumed in 4 MFMA steps s = 0..3; lane group g = l>>4 feeds
+// k = k0 + 4g + s to BOTH operands, so each lane fetches 4 consecutive k of its row
+// with ONE 16-byte load when the operand is K-contiguous (nn.Linear weights,
+// row-major activations) and 4 coalesced 64-byte row segments otherwise.
+// Workgroups split K across their waves and reduce through LDS in a fixed wave
+// order: no float atomics anywhere, results are bitwise reproducible.
+#include "sacmi_internal.h"
+
+#include <cmath>
+#include <cstdio>
+
+namespace sacmi {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+#define HIP_LAUNCH_CHECK()                                                          \
+  do {                                                                              \
+    hipError_t e_ = hipGetLastError();                                              \
+    if (e_ != hipSuccess) {                                                         \
+      fprintf(stderr, "sacmi: launch failed %s (%s:%d)\n", hipGetErrorString(e_),   \
+              __FILE__, __LINE__);                                                  \
+    }                                                                               \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// operand fetch: NT 16-row subtiles x 4 consecutive k (k = k0 + 4g .. +3)
+template <int NT>
+__device__ __forceinline__ void fetch_op(const float* __restrict__ P, int ld, int kc, int row0,
+                                         int nrows, int k0, int K, int lane, float (&v)[NT][4]) {
+  const int r = lane & 15;
+  const int k = k0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    int row = row0 + t * 16 + r;
+    row = row < nrows ? row : nrows - 1;
+    if (kc) {
+      if (k < K) {
+        const float4 x = *reinterpret_cast<const float4*>(P + (size_t)row * ld + k);
+        v[t][0] = x.x;
+        v[t][1] = (k + 1 < K) ? x.y : 0.f;
+        v[t][2] = (k + 2 < K) ? x.z : 0.f;
+        v[t][3] = (k + 3 < K) ? x.w : 0.f;
+      } else {
+        v[t][0] = v[t][1] = v[t][2] = v[t][3] = 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int kk = (k + s < K) ? (k + s) : (K - 1);
+        const float x = P[(size_t)kk * ld + row];
+        v[t][s] = (k + s < K) ? x : 0.f;
+      }
+    }
+  }
+}
+
+template <int MT, int NT>
+__device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[MT][4],
+                                           const float (&b)[NT][4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+}
+
+// Each wave accumulates chunks wave, wave+KSPLIT, ... of a TM x TN tile and writes
+// its partial sums to red[wave][TM][TN+1].
+template <int TM, int TN, int KSPLIT>
+__device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red) {
+  constexpr int MT = TM / 16, NT = TN / 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = (d.K + 15) >> 4;
+  float a0[MT][4], b0[NT][4], a1[MT][4], b1[NT][4];
+  int c = wave;
+  if (c < nch) {
+    fetch_op<MT>(d.A, d.lda, d.a_kc, m0, d.M, c * 16, d.K, lane, a0);
+    fetch_op<NT>(d.B, d.ldb, d.b_kc, n0, d.N, c * 16, d.K, lane, b0);
+  }
+  for (;;) {
+    if (c >= nch) break;
+    if (c + KSPLIT < nch) {
+      fetch_op<MT>(d.A, d.lda, d.a_kc, m0, d.M, (c + KSPLIT) * 16, d.K, lane, a1);
+      fetch_op<NT>(d.B, d.ldb, d.b_kc, n0, d.N, (c + KSPLIT) * 16, d.K, lane, b1);
+    }
+    mfma_chunk<MT, NT>(acc, a0, b0);
+    c += KSPLIT;
+    if (c >= nch) break;
+    if (c + KSPLIT < nch) {
+      fetch_op<MT>(d.A, d.lda, d.a_kc, m0, d.M, (c + KSPLIT) * 16, d.K, lane, a0);
+      fetch_op<NT>(d.B, d.ldb, d.b_kc, n0, d.N, (c + KSPLIT) * 16, d.K, lane, b0);
+    }
+    mfma_chunk<MT, NT>(acc, a1, b1);
+    c += KSPLIT;
+  }
+  float* my = red + wave * TM * (TN + 1);
+  const int rq = (lane >> 4) * 4, cc = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) my[(i * 16 + rq + r) * (TN + 1) + j * 16 + cc] = acc[i][j][r];
+}
+
+template <int TM, int TN, int KSPLIT>
+__device__ __forceinline__ float reduce_partials(const float* red, int row, int col) {
+  float s = red[row * (TN + 1) + col];
+#pragma unroll
+  for (int w = 1; w < KSPLIT; ++w) s += red[w * TM * (TN + 1) + row * (TN + 1) + col];
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// grouped GEMM: one launch runs every independent GEMM of one dependency level
+template <int TM, int TN, int KSPLIT>
+__global__ __launch_bounds__(64 * KSPLIT) void k_gemm(GemmBatch batch) {
+  __shared__ float red[KSPLIT * TM * (TN + 1)];
+  const int bid = blockIdx.x;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  const int m0 = (t / d.tiles_n) * TM, n0 = (t % d.tiles_n) * TN;
+  gemm_core<TM, TN, KSPLIT>(d, m0, n0, red);
+  __syncthreads();
+  for (int e = threadIdx.x; e < TM * TN; e += 64 * KSPLIT) {
+    const int row = e / TN, col = e % TN;
+    const int m = m0 + row, n = n0 + col;
+    if (m >= d.M || n >= d.N) continue;
+    float v = reduce_partials<TM, TN, KSPLIT>(red, row, col);
+    if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
+    else if (d.epi == EPI_MASK) v = d.aux[(size_t)m * d.ldaux + n] > 0.f ? v : 0.f;
+    d.C[(size_t)m * d.ldc + n] = v;
+  }
+}
+
+void launch_gemm(const GemmBatch& b, hipStream_t s) {
+  if (b.count == 0) return;
+  hipLaunchKernelGGL((k_gemm<32, 32, 4>), dim3(b.total_tiles), dim3(256), 0, s, b);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 + Box-Muller (perf-mode policy noise)
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t counter, uint32_t elem) {
+  uint32_t c[4] = {(uint32_t)counter, (uint32_t)(counter >> 32), elem, 0x5ac3u};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float u1 = ((float)c[0] + 0.5f) * 2.3283064365386963e-10f;   // (0,1)
+  const float u2 = ((float)c[1] + 0.5f) * 2.3283064365386963e-10f;
+  return sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+}
+
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;   // math.log(math.sqrt(2*pi))
+
+// ---------------------------------------------------------------------------
+// policy heads (mean | log_std) GEMM + GaussianPolicy.sample epilogue
+// (networks_model1.py:65-99, torch distributions/normal.py:83-103)
+template <int TN, int KSPLIT>
+__global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) {
+  constexpr int TM = 16;
+  __shared__ float red[KSPLIT * TM * (TN + 1)];
+  __shared__ float lp[TM][33];
+  const int A = a.A;
+  GemmDesc d;
+  d.A = a.h; d.lda = a.ldh; d.a_kc = 1; d.M = a.rows;
+  d.B = a.Wh; d.ldb = a.ldw; d.b_kc = 1; d.N = 2 * A; d.K = a.K;
+  const int m0 = blockIdx.x * TM;
+  gemm_core<TM, TN, KSPLIT>(d, m0, 0, red);
+  __syncthreads();
+  const float alpha_unused = 0.f; (void)alpha_unused;
+  const uint64_t ctr = a.sc->noise_counter;
+  for (int e = threadIdx.x; e < TM * A; e += 64 * KSPLIT) {
+    const int row = e / A, j = e % A;
+    const int m = m0 + row;
+    float lpe = 0.f;
+    if (m < a.rows) {
+      const float mean = reduce_partials<TM, TN, KSPLIT>(red, row, j);
+      const float ls_raw = reduce_partials<TM, TN, KSPLIT>(red, row, A + j);
+      const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
+      const float sd = expf(ls);
+      float eps;
+      if (a.gen_eps) {
+        eps = philox_normal(a.seed, ctr, (uint32_t)(m * A + j));
+        a.eps[(size_t)m * A + j] = eps;
+      } else {
+        eps = a.eps[(size_t)m * A + j];
+      }
+      const float x = mean + eps * sd;
+      const float y = tanhf(x);
+      a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
+      const float dx = x - mean;
+      lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
+      lpe -= logf(a.scale * (1.f - y * y) + 1e-6f);
+      float* cr = a.cache + (size_t)m * 3 * A;
+      cr[j] = mean; cr[A + j] = ls_raw; cr[2 * A + j] = y;
+    }
+    lp[row][j] = lpe;
+  }
+  __syncthreads();
+  if (threadIdx.x < TM) {
+    const int m = m0 + threadIdx.x;
+    if (m < a.rows) {
+      float s = 0.f;
+      for (int j = 0; j < A; ++j) s += lp[threadIdx.x][j];
+      a.logp[m] = s;
+    }
+  }
+}
+
+void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {
+  const int grid = (a.rows + 15) / 16;
+  const int n = 2 * a.A;
+  if (n <= 32)
+    hipLaunchKernelGGL((k_heads_sample<32, 4>), dim3(grid), dim3(256), 0, s, a);
+  else if (n <= 48)
+    hipLaunchKernelGGL((k_heads_sample<48, 4>), dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_heads_sample<64, 4>), dim3(grid), dim3(256), 0, s, a);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// dL/da GEMM (both critics, K = 2H) + GaussianPolicy.sample backward epilogue.
+// For L_pi = mean(alpha*logp - min Q): dL/dlogp = alpha/B.  Per element with
+// u = scale*(1-y^2)+1e-6:  G = scale*dL/da + (alpha/B)*2*scale*y/u,
+//   dmean = G*(1-y^2);  dlog_std = [-20<=ls<=2] * (G*(1-y^2)*eps*std - alpha/B)
+// (the Normal.log_prob quadratic term's gradients w.r.t. mean and std cancel
+// exactly: x - mean = eps*std).
+template <int TM, int TN, int KSPLIT>
+__global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, SampleBwdArgs a) {
+  __shared__ float red[KSPLIT * TM * (TN + 1)];
+  const int m0 = blockIdx.x * TM;
+  gemm_core<TM, TN, KSPLIT>(d, m0, 0, red);
+  __syncthreads();
+  const int A = a.A;
+  const float glogp = a.sc->alpha / (float)a.B;
+  for (int e = threadIdx.x; e < TM * A; e += 64 * KSPLIT) {
+    const int row = e / A, j = e % A;
+    const int m = m0 + row;
+    if (m >= d.M) continue;
+    const float ga = reduce_partials<TM, TN, KSPLIT>(red, row, j);
+    const float* cr = a.cache + (size_t)m * 3 * A;
+    const float ls_raw = cr[A + j], y = cr[2 * A + j];
+    const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
+    const float sd = expf(ls);
+    const float eps = a.eps[(size_t)m * A + j];
+    const float omy2 = 1.f - y * y;
+    const float u = a.scale * omy2 + 1e-6f;
+    const float G = a.scale * ga + glogp * (2.f * a.scale * y / u);
+    const float dx = G * omy2;
+    float dls = dx * eps * sd - glogp;
+    if (!(ls_raw >= -20.f && ls_raw <= 2.f)) dls = 0.f;
+    a.dhead[(size_t)m * a.lddh + j] = dx;
+    a.dhead[(size_t)m * a.lddh + A + j] = dls;
+  }
+}
+
+void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s) {
+  const int grid = (d.M + 31) / 32;
+  hipLaunchKernelGGL((k_gemm_sample_bwd<32, 32, 4>), dim3(grid), dim3(256), 0, s, d, a);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// dot(h~[row], w~) over K4 float4 chunks, one wave
+__device__ __forceinline__ float wave_dot(const float* __restrict__ h, const float* __restrict__ w,
+                                          int K4, int lane) {
+  float s = 0.f;
+  for (int q = lane; q < K4; q += 64) {
+    const float4 x = reinterpret_cast<const float4*>(h)[q];
+    const float4 y = reinterpret_cast<const float4*>(w)[q];
+    s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+  }
+  return wave_sum(s);
+}
+
+// Target + critic loss rows (sac_imp.py:87-105 forward tail, mse backward).
+// One wave per row b:
+//   q_i = h2_i[b].w3_i ; qt_i = ht2_i[b].w3t_i ;  q^ = r + (1-d)*gamma*(min qt - alpha*logp')
+//   dq_i = 2 (q_i - q^) / B ;  dh2_i[b,:] = dq_i * w3_i * [h2_i > 0]
+constexpr int kRowsPerBlock = 4;
+
+__global__ __launch_bounds__(256) void k_critic_rows(CriticRowsArgs a) {
+  __shared__ float part[kRowsPerBlock][2];
+  __shared__ float red[256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x * kRowsPerBlock + w;
+  const int K4 = (a.H + 1 + 3) / 4;
+  const float alpha = a.sc->alpha;
+  float e1 = 0.f, e2 = 0.f;
+  if (b < a.B) {
+    const float* h1 = a.hq2 + (size_t)b * 2 * a.ldh;
+    const float* h2 = h1 + a.ldh;
+    const float* t1 = a.hqt2 + (size_t)b * 2 * a.ldh;
+    const float* t2 = t1 + a.ldh;
+    const float q1 = wave_dot(h1, a.w3, K4, lane);
+    const float q2 = wave_dot(h2, a.w3 + a.w3_stride, K4, lane);
+    const float qt1 = wave_dot(t1, a.w3t, K4, lane);
+    const float qt2 = wave_dot(t2, a.w3t + a.w3_stride, K4, lane);
+    const float vt = fminf(qt1, qt2) - alpha * a.logp_t[b];
+    const float qhat = a.r[b] + ((1.f - a.d[b]) * a.gamma) * vt;
+    e1 = q1 - qhat;
+    e2 = q2 - qhat;
+    const float dq1 = 2.f * e1 / (float)a.B, dq2 = 2.f * e2 / (float)a.B;
+    if (lane == 0) { a.dq[b] = dq1; a.dq[a.B + b] = dq2; }
+    float* o = a.dh2 + (size_t)b * 2 * a.H;
+    for (int h = lane; h < a.H; h += 64) {
+      o[h] = h1[h] > 0.f ? dq1 * a.w3[h] : 0.f;
+      o[a.H + h] = h2[h] > 0.f ? dq2 * a.w3[a.w3_stride + h] : 0.f;
+    }
+  }
+  if (lane == 0) { part[w][0] = e1 * e1; part[w][1] = e2 * e2; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    float s = 0.f;
+    for (int r = 0; r < kRowsPerBlock; ++r) s += part[r][threadIdx.x];
+    a.loss_part[blockIdx.x * 2 + threadIdx.x] = s;
+  }
+  // alpha gradient: d/dlog_alpha of -mean(log_alpha * (logp + te)) = -mean(logp + te)
+  if (blockIdx.x == 0 && a.auto_entropy) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < a.B; i += 256) s += a.logp_a[i] + a.target_entropy;
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o >= 1; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *a.alpha_grad = -red[0] / (float)a.B;
+  }
+}
+
+void launch_critic_rows(const CriticRowsArgs& a, hipStream_t s) {
+  const int grid = (a.B + kRowsPerBlock - 1) / kRowsPerBlock;
+  hipLaunchKernelGGL(k_critic_rows, dim3(grid), dim3(256), 0, s, a);
+  HIP_LAUNCH_CHECK();
+}
+
+// Actor rows (sac_imp.py:116-121): qa_i = ha2_i[b].w3_i with the UPDATED critics,
+// L_pi partial = alpha*logp - min(qa1, qa2); min backward splits ties 1/2 : 1/2.
+// Also advances the step counters (the critic Adam ran before this kernel, the
+// actor Adam runs after it).
+__global__ __launch_bounds__(256) void k_actor_rows(ActorRowsArgs a) {
+  __shared__ float part[kRowsPerBlock];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x * kRowsPerBlock + w;
+  const int K4 = (a.H + 1 + 3) / 4;
+  const float alpha = a.sc->alpha;
+  float lpart = 0.f;
+  if (b < a.B) {
+    const float* h1 = a.hqa2 + (size_t)b * 2 * a.ldh;
+    const float* h2 = h1 + a.ldh;
+    const float q1 = wave_dot(h1, a.w3, K4, lane);
+    const float q2 = wave_dot(h2, a.w3 + a.w3_stride, K4, lane);
+    const float qmin = fminf(q1, q2);
+    lpart = alpha * a.logp_a[b] - qmin;
+    const float g = -1.f / (float)a.B;
+    const float w1 = q1 < q2 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
+    const float dq1 = g * w1, dq2 = g * (1.f - w1);
+    float* o = a.dha2 + (size_t)b * 2 * a.H;
+    for (int h = lane; h < a.H; h += 64) {
+      o[h] = h1[h] > 0.f ? dq1 * a.w3[h] : 0.f;
+      o[a.H + h] = h2[h] > 0.f ? dq2 * a.w3[a.w3_stride + h] : 0.f;
+    }
+  }
+  if (lane == 0) part[w] = lpart;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int r = 0; r < kRowsPerBlock; ++r) s += part[r];
+    a.loss_part[blockIdx.x] = s;
+    if (blockIdx.x == 0) {
+      for (int i = 0; i < 4; ++i) a.sc->step[i] += 1.0;
+      a.sc->noise_counter += 1;
+    }
+  }
+}
+
+void launch_actor_rows(const ActorRowsArgs& a, hipStream_t s) {
+  const int grid = (a.B + kRowsPerBlock - 1) / kRowsPerBlock;
+  hipLaunchKernelGGL(k_actor_rows, dim3(grid), dim3(256), 0, s, a);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// Adam (torch.optim.Adam single-tensor semantics, torch optim/adam.py) over the
+// flat arena + optional Polyak target update (sac_imp.py:146-152) + loss
+// finalisation + alpha = exp(log_alpha) (sac_imp.py:135).
+__global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+  __shared__ float s_step_size[4], s_bc2_sqrt[4];
+  __shared__ int64_t s_prefix[5];
+  if (threadIdx.x < a.nseg) {
+    const double t = a.sc->step[a.seg[threadIdx.x].step_idx] + (double)a.step_offset;
+    const double bc1 = 1.0 - pow((double)a.beta1, t);
+    const double bc2 = 1.0 - pow((double)a.beta2, t);
+    s_step_size[threadIdx.x] = (float)((double)a.lr / bc1);
+    s_bc2_sqrt[threadIdx.x] = (float)sqrt(bc2);
+  }
+  if (threadIdx.x == 0) {
+    int64_t p = 0;
+    for (int i = 0; i < a.nseg; ++i) { s_prefix[i] = p; p += a.seg[i].n; }
+    s_prefix[a.nseg] = p;
+  }
+  __syncthreads();
+  const float om_b1 = 1.f - a.beta1;
+  const float om_b2 = 1.f - a.beta2;
+  const float omtau = 1.f - a.tau;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int sg = 0;
+    for (int q = 1; q < a.nseg; ++q)
+      if (e >= s_prefix[q]) sg = q;
+    const int64_t i = a.seg[sg].off + (e - s_prefix[sg]);
+    const float g = a.g[i] * a.grad_scale;
+    float m = a.m[i];
+    m = m + om_b1 * (g - m);
+    float v = a.v[i] * a.beta2;
+    v = v + om_b2 * g * g;
+    const float denom = sqrtf(v) / s_bc2_sqrt[sg] + a.eps;
+    const float p = a.p[i] + (-s_step_size[sg] * m) / denom;
+    a.m[i] = m; a.v[i] = v; a.p[i] = p;
+    if (a.tgt) {
+      float* t = a.tgt + (i - a.tgt_base);
+      *t = __fadd_rn(__fmul_rn(*t, omtau), __fmul_rn(p, a.tau));
+    }
+    if (i == a.log_alpha_idx && a.auto_entropy) {
+      a.sc->alpha = expf(p);
+      a.sc->alpha_is_tensor = 1;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < a.n_losses) {
+    float s = 0.f;
+    for (int w = 0; w < a.n_part; ++w) s += a.loss_part[w * a.n_losses + threadIdx.x];
+    a.sc->losses[a.loss_slot0 + threadIdx.x] = s / a.loss_div;
+  }
+}
+
+// Loss ring: copies the three losses of this update into slot (pos % ring).
+__global__ void k_loss_ring(DevScalars* sc, float* ring, int nring) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const int64_t p = sc->loss_ring_pos % nring;
+    ring[p * 3 + 0] = sc->losses[0];
+    ring[p * 3 + 1] = sc->losses[1];
+    ring[p * 3 + 2] = sc->losses[2];
+    sc->loss_ring_pos += 1;
+  }
+}
+
+void launch_adam(const AdamArgs& a, hipStream_t s) {
+  int64_t blocks = (a.total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  HIP_LAUNCH_CHECK();
+  if (a.loss_ring) {
+    hipLaunchKernelGGL(k_loss_ring, dim3(1), dim3(64), 0, s, a.sc, a.loss_ring, a.ring);
+    HIP_LAUNCH_CHECK();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// replay gather: deque positions -> ring slots -> critic input [s|1|a] and the
+// stacked policy input [s2|1|.. ; s|1|..]  (replay_buffer.py:15-19 + sac_imp.py:81-85)
+__global__ __launch_bounds__(128) void k_gather(GatherArgs a) {
+  const int b = blockIdx.x;
+  const int64_t slot = (a.sc->head + (int64_t)a.idx[b]) % a.capacity;
+  const float* so = a.obs + slot * a.ldo;
+  const float* s2 = a.obs2 + slot * a.ldo;
+  const float* ac = a.act + slot * a.lda_;
+  float* xq = a.xq + (size_t)b * a.ldx;
+  float* xt = a.x2 + (size_t)b * a.ldx;
+  float* xa = a.x2 + (size_t)(a.B + b) * a.ldx;
+  if ((a.S & 3) == 0) {
+    for (int q = threadIdx.x; q < a.S / 4; q += blockDim.x) {
+      const float4 v = reinterpret_cast<const float4*>(so)[q];
+      reinterpret_cast<float4*>(xq)[q] = v;
+      reinterpret_cast<float4*>(xa)[q] = v;
+      reinterpret_cast<float4*>(xt)[q] = reinterpret_cast<const float4*>(s2)[q];
+    }
+  } else {
+    for (int q = threadIdx.x; q < a.S; q += blockDim.x) {
+      const float v = so[q];
+      xq[q] = v; xa[q] = v; xt[q] = s2[q];
+    }
+  }
+  for (int j = threadIdx.x; j < a.A; j += blockDim.x) xq[a.S + 1 + j] = ac[j];
+  if (threadIdx.x == 0) {
+    a.r[b] = a.rew[slot];
+    a.d[b] = a.done[slot];
+  }
+}
+
+void launch_gather(const GatherArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather, dim3(a.B), dim3(128), 0, s, a);
+  HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+__global__ void k_fill(float* p, int64_t n, float v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+void launch_fill(float* p, int64_t n, float v, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(256), 0, s, p, n, v);
+  HIP_LAUNCH_CHECK();
+}
+
+__global__ void k_set_column(float* p, int rows, int ld, int col, float v) {
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += gridDim.x * blockDim.x)
+    p[(size_t)r * ld + col] = v;
+}
+void launch_set_column(float* p, int rows, int ld, int col, float v, hipStream_t s) {
+  if (rows <= 0) return;
+  int blocks = (rows + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_set_column, dim3(blocks), dim3(256), 0, s, p, rows, ld, col, v);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace sacmi

@@ -1,0 +1,924 @@
+// libsacmi host runtime: the C ABI of include/sacmi.h.
+//
+// Owns every device buffer of one agent (parameter arenas, replay ring, scratch),
+// sequences the ~20 kernels of one SAC update on one HIP stream, and caches each
+// distinct update configuration as an instantiated hipGraph so a training step is
+// one graph launch (the step is launch-latency bound at batch 256: SURVEY §7).
+#include "sacmi_internal.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+namespace sacmi {
+
+static thread_local std::string g_last_error;
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define CHECK_HIP(expr)                                                              \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      throw Error{SACMI_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+#define REQUIRE(cond, code, msg)           \
+  do {                                     \
+    if (!(cond)) throw Error{code, (msg)}; \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    n = count;
+    if (count) {
+      CHECK_HIP(hipMalloc(&p, count * sizeof(T)));
+      CHECK_HIP(hipMemset(p, 0, count * sizeof(T)));
+    }
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct GraphKey {
+  int batch, dev_idx, dev_eps, phase_mask, ring;
+  bool operator<(const GraphKey& o) const {
+    return std::tie(batch, dev_idx, dev_eps, phase_mask, ring) <
+           std::tie(o.batch, o.dev_idx, o.dev_eps, o.phase_mask, o.ring);
+  }
+};
+
+}  // namespace sacmi
+
+struct sacmi_ctx {
+  sacmi_config cfg{};
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  int S = 0, A = 0, H = 0, Bm = 0;
+  int Kx = 0, Hd = 0, Kp1 = 0, lddh = 0;
+  // layout
+  sacmi::Linear q_fc[2][3];        // [net][layer]
+  sacmi::Linear p_fc1, p_fc2, p_head;
+  int64_t q_begin = 0, q_end = 0, pi_begin = 0, la_idx = 0, total = 0;
+  // arenas
+  sacmi::DevBuf<float> P, T, G, M, V;
+  sacmi::DevBuf<sacmi::DevScalars> sc;
+  // replay
+  int ldo = 0, ldact = 0;
+  int64_t capacity = 0, len = 0, wpos = 0;
+  sacmi::DevBuf<float> obs, act, rew, obs2, done, prio;
+  sacmi::DevBuf<uint32_t> mt;      // [2][625]: random / numpy streams
+  // scratch
+  sacmi::DevBuf<int32_t> idx32;
+  sacmi::DevBuf<int64_t> idx64;
+  sacmi::DevBuf<float> xq, x2, r, d, hp1, hp2, eps, cache, logp;
+  sacmi::DevBuf<float> hq1, hq2, hqt1, hqt2, hqa1, hqa2;
+  sacmi::DevBuf<float> dq, dh2, dh1, dha2, dha1, dhead, dhp2, dhp1;
+  sacmi::DevBuf<float> lpart_c, lpart_a, ring;
+  int ring_slots = 0;
+  // act scratch
+  int act_rows = 0;
+  sacmi::DevBuf<float> ax, ah1, ah2, aeps, acache, alogp, aout;
+  // staging
+  sacmi::DevBuf<float> stage, per_scr;
+  std::map<sacmi::GraphKey, hipGraphExec_t> graphs;
+  bool use_graphs = true;
+  // profiling (sacmi_profile_step): one event per launch site
+  bool prof = false;
+  std::vector<std::string> prof_names;
+  std::vector<double> prof_flops;
+  std::vector<hipEvent_t> prof_events;
+};
+
+namespace sacmi {
+
+static void set_err(const Error& e) { g_last_error = e.msg; }
+
+template <class F>
+static int guard(F&& f) {
+  try {
+    f();
+    return SACMI_OK;
+  } catch (const Error& e) {
+    set_err(e);
+    return e.code;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return SACMI_EDEVICE;
+  }
+}
+
+static void destroy_graphs(sacmi_ctx* c) {
+  for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+  c->graphs.clear();
+}
+
+// ---------------------------------------------------------------------------
+static void build_layout(sacmi_ctx* c) {
+  const int S = c->S, A = c->A, H = c->H;
+  c->Kx = round_up(S + 1 + A, 4);
+  c->Hd = round_up(H + 1, 4);
+  c->Kp1 = round_up(S + 1, 4);
+  c->lddh = round_up(2 * A, 4);
+  int64_t off = 0;
+  auto take = [&](Linear& l, int n_out, int k_in, int ld, int bias_col, int split, bool align) {
+    if (align) off = round_up64(off, 64);
+    l.off = off; l.n_out = n_out; l.k_in = k_in; l.ld = ld; l.bias_col = bias_col; l.split = split;
+    off += (int64_t)n_out * ld;
+  };
+  c->q_begin = 0;
+  take(c->q_fc[0][0], H, S + A, c->Kx, S, S, true);
+  take(c->q_fc[1][0], H, S + A, c->Kx, S, S, false);   // adjacent: one K=2H dL/da GEMM
+  take(c->q_fc[0][1], H, H, c->Hd, H, H, true);
+  take(c->q_fc[1][1], H, H, c->Hd, H, H, true);
+  take(c->q_fc[0][2], 1, H, c->Hd, H, H, true);
+  take(c->q_fc[1][2], 1, H, c->Hd, H, H, true);
+  off = round_up64(off, 64);
+  c->q_end = off;
+  c->pi_begin = off;
+  take(c->p_fc1, H, S, c->Kp1, S, S, true);
+  take(c->p_fc2, H, H, c->Hd, H, H, true);
+  take(c->p_head, 2 * A, H, c->Hd, H, H, true);
+  off = round_up64(off, 64);
+  c->la_idx = off;
+  c->total = off + 64;
+}
+
+static Linear head_part(const sacmi_ctx* c, int which /*0 mean 1 log_std*/) {
+  Linear l = c->p_head;
+  l.n_out = c->A;
+  l.off = c->p_head.off + (int64_t)which * c->A * c->p_head.ld;
+  return l;
+}
+
+static Linear find_linear(const sacmi_ctx* c, int net, int layer) {
+  if (net == SACMI_POLICY) {
+    switch (layer) {
+      case 0: return c->p_fc1;
+      case 1: return c->p_fc2;
+      case 2: return head_part(c, 0);
+      case 3: return head_part(c, 1);
+    }
+  } else if (net >= SACMI_Q1 && net <= SACMI_Q2_TARGET) {
+    const int q = (net == SACMI_Q1 || net == SACMI_Q1_TARGET) ? 0 : 1;
+    if (layer >= 0 && layer < 3) return c->q_fc[q][layer];
+  }
+  throw Error{SACMI_EVALUE, "bad (net, layer)"};
+}
+
+static void alloc_all(sacmi_ctx* c) {
+  const int Bm = c->Bm, S = c->S, A = c->A, H = c->H;
+  c->P.alloc(c->total); c->G.alloc(c->total); c->M.alloc(c->total); c->V.alloc(c->total);
+  c->T.alloc(c->q_end);
+  c->sc.alloc(1);
+  c->ldo = round_up(S, 4);
+  c->ldact = round_up(A, 4);
+  const int64_t cap = c->capacity;
+  c->obs.alloc((size_t)cap * c->ldo);
+  c->obs2.alloc((size_t)cap * c->ldo);
+  c->act.alloc((size_t)cap * c->ldact);
+  c->rew.alloc(cap);
+  c->done.alloc(cap);
+  if (c->cfg.replay_kind == SACMI_REPLAY_PER) c->prio.alloc(cap);
+  c->mt.alloc(2 * 625);
+  c->per_scr.alloc(16);
+  c->idx32.alloc(Bm); c->idx64.alloc(Bm);
+  c->xq.alloc((size_t)Bm * c->Kx);
+  c->x2.alloc((size_t)2 * Bm * c->Kx);
+  c->r.alloc(Bm); c->d.alloc(Bm);
+  c->hp1.alloc((size_t)2 * Bm * c->Hd); c->hp2.alloc((size_t)2 * Bm * c->Hd);
+  c->eps.alloc((size_t)2 * Bm * A);
+  c->cache.alloc((size_t)2 * Bm * 3 * A);
+  c->logp.alloc((size_t)2 * Bm);
+  for (auto* b : {&c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1, &c->hqa2})
+    b->alloc((size_t)Bm * 2 * c->Hd);
+  c->dq.alloc((size_t)2 * Bm);
+  for (auto* b : {&c->dh2, &c->dh1, &c->dha2, &c->dha1}) b->alloc((size_t)Bm * 2 * H);
+  c->dhead.alloc((size_t)Bm * c->lddh);
+  c->dhp2.alloc((size_t)Bm * H); c->dhp1.alloc((size_t)Bm * H);
+  const int nb = (Bm + 3) / 4;
+  c->lpart_c.alloc((size_t)nb * 2); c->lpart_a.alloc(nb);
+  hipStream_t s = c->stream;
+  // constant-1 (bias) columns
+  launch_set_column(c->xq.p, Bm, c->Kx, S, 1.f, s);
+  launch_set_column(c->x2.p, 2 * Bm, c->Kx, S, 1.f, s);
+  launch_set_column(c->hp1.p, 2 * Bm, c->Hd, H, 1.f, s);
+  launch_set_column(c->hp2.p, 2 * Bm, c->Hd, H, 1.f, s);
+  for (auto* b : {&c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1, &c->hqa2}) {
+    launch_set_column(b->p, Bm, 2 * c->Hd, H, 1.f, s);
+    launch_set_column(b->p, Bm, 2 * c->Hd, c->Hd + H, 1.f, s);
+  }
+  CHECK_HIP(hipStreamSynchronize(s));
+}
+
+static void upload_scalars(sacmi_ctx* c, const DevScalars& h) {
+  CHECK_HIP(hipMemcpyAsync(c->sc.p, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+  CHECK_HIP(hipStreamSynchronize(c->stream));
+}
+static DevScalars download_scalars(sacmi_ctx* c) {
+  DevScalars h;
+  CHECK_HIP(hipMemcpyAsync(&h, c->sc.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  CHECK_HIP(hipStreamSynchronize(c->stream));
+  return h;
+}
+
+// ---------------------------------------------------------------------------
+// one update, enqueued on c->stream.  phase_mask bit p enables phase p.
+static GemmDesc gd(const float* A, int lda, int a_kc, const float* B, int ldb, int b_kc,
+                   float* C, int ldc, int M, int N, int K, int epi = EPI_STORE,
+                   const float* aux = nullptr, int ldaux = 0) {
+  GemmDesc d{};
+  d.A = A; d.lda = lda; d.a_kc = a_kc;
+  d.B = B; d.ldb = ldb; d.b_kc = b_kc;
+  d.C = C; d.ldc = ldc; d.M = M; d.N = N; d.K = K; d.epi = epi; d.aux = aux; d.ldaux = ldaux;
+  return d;
+}
+
+struct Level {
+  GemmBatch b{};
+  void add(const GemmDesc& d0) {
+    if (b.count >= kMaxGemms) throw Error{SACMI_ESTATE, "too many GEMMs in one level"};
+    GemmDesc d = d0;
+    const int tm = (d.M + 31) / 32, tn = (d.N + 31) / 32;
+    d.tiles_n = tn;
+    d.tile_begin = b.total_tiles;
+    b.total_tiles += tm * tn;
+    b.d[b.count++] = d;
+  }
+};
+
+static double level_flops(const GemmBatch& b) {
+  double f = 0;
+  for (int i = 0; i < b.count; ++i) f += 2.0 * b.d[i].M * (double)b.d[i].N * b.d[i].K;
+  return f;
+}
+
+// profiling mark: records an event BEFORE the launch it names
+static void mark(sacmi_ctx* c, const char* name, double flops = 0) {
+  if (!c->prof) return;
+  hipEvent_t e;
+  CHECK_HIP(hipEventCreate(&e));
+  CHECK_HIP(hipEventRecord(e, c->stream));
+  c->prof_events.push_back(e);
+  c->prof_names.push_back(name);
+  c->prof_flops.push_back(flops);
+}
+
+static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
+                           float grad_scale, bool use_ring) {
+  hipStream_t s = c->stream;
+  const int S = c->S, A = c->A, H = c->H, Kx = c->Kx, Hd = c->Hd;
+  float* P = c->P.p;
+  float* G = c->G.p;
+  const float* T = c->T.p;
+  const int nb = (B + 3) / 4;
+  auto W = [&](const Linear& l) { return P + l.off; };
+  auto Wt = [&](const Linear& l) { return T + (l.off - c->q_begin); };
+  auto dW = [&](const Linear& l) { return G + l.off; };
+  const Linear(&q)[2][3] = c->q_fc;
+
+  if (phase_mask & 1) {
+    if (dev_idx) {
+      MtSampleArgs m{};
+      m.mt = c->mt.p; m.sc = c->sc.p; m.k = B;
+      const int k = B;
+      int setsize = 21;
+      if (k > 5) setsize += (int)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
+      m.setsize = setsize; m.idx_out = c->idx32.p; m.idx64_out = c->idx64.p;
+      mark(c, "mt_sample");
+      launch_mt_sample(m, s);
+    }
+    GatherArgs g{};
+    g.idx = c->idx32.p; g.obs = c->obs.p; g.act = c->act.p; g.rew = c->rew.p; g.obs2 = c->obs2.p;
+    g.done = c->done.p; g.ldo = c->ldo; g.lda_ = c->ldact; g.capacity = c->capacity;
+    g.sc = c->sc.p; g.S = S; g.A = A; g.B = B; g.xq = c->xq.p; g.x2 = c->x2.p; g.ldx = Kx;
+    g.r = c->r.p; g.d = c->d.p;
+    mark(c, "gather");
+    launch_gather(g, s);
+
+    // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
+    Level l1;
+    l1.add(gd(c->x2.p, Kx, 1, W(c->p_fc1), c->p_fc1.ld, 1, c->hp1.p, Hd, 2 * B, H, S + 1, EPI_RELU));
+    for (int i = 0; i < 2; ++i)
+      l1.add(gd(c->xq.p, Kx, 1, W(q[i][0]), Kx, 1, c->hq1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+    mark(c, "gemm_L1_fc1", level_flops(l1.b));
+    launch_gemm(l1.b, s);
+    // L2
+    Level l2;
+    l2.add(gd(c->hp1.p, Hd, 1, W(c->p_fc2), Hd, 1, c->hp2.p, Hd, 2 * B, H, H + 1, EPI_RELU));
+    for (int i = 0; i < 2; ++i)
+      l2.add(gd(c->hq1.p + i * Hd, 2 * Hd, 1, W(q[i][1]), Hd, 1, c->hq2.p + i * Hd, 2 * Hd, B, H, H + 1, EPI_RELU));
+    mark(c, "gemm_L2_fc2", level_flops(l2.b));
+    launch_gemm(l2.b, s);
+    // heads + sample for both stacks
+    HeadSampleArgs hs{};
+    hs.h = c->hp2.p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H + 1;
+    hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = dev_eps; hs.seed = c->cfg.seed;
+    hs.sc = c->sc.p; hs.act = c->x2.p + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
+    hs.cache = c->cache.p;
+    hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
+    hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
+    mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * (H + 1));
+    launch_heads_sample(hs, s);
+    // L3/L4: target critics on [s2|1|a']
+    Level l3, l4;
+    for (int i = 0; i < 2; ++i)
+      l3.add(gd(c->x2.p, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+    mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b));
+    launch_gemm(l3.b, s);
+    for (int i = 0; i < 2; ++i)
+      l4.add(gd(c->hqt1.p + i * Hd, 2 * Hd, 1, Wt(q[i][1]), Hd, 1, c->hqt2.p + i * Hd, 2 * Hd, B, H, H + 1, EPI_RELU));
+    mark(c, "gemm_L4_tgt_fc2", level_flops(l4.b));
+    launch_gemm(l4.b, s);
+    // target / critic loss rows
+    CriticRowsArgs cr{};
+    cr.hq2 = c->hq2.p; cr.hqt2 = c->hqt2.p; cr.ldh = Hd; cr.H = H; cr.B = B;
+    cr.w3 = W(q[0][2]); cr.w3t = Wt(q[0][2]); cr.w3_stride = (int)(q[1][2].off - q[0][2].off);
+    cr.r = c->r.p; cr.d = c->d.p; cr.logp_t = c->logp.p; cr.logp_a = c->logp.p + B;
+    cr.gamma = (float)c->cfg.gamma; cr.target_entropy = (float)(-A);
+    cr.auto_entropy = c->cfg.auto_entropy; cr.sc = c->sc.p; cr.dq = c->dq.p; cr.dh2 = c->dh2.p;
+    cr.loss_part = c->lpart_c.p; cr.alpha_grad = G + c->la_idx;
+    mark(c, "critic_rows");
+    launch_critic_rows(cr, s);
+    // L5: dh1 (relu-masked), dW2~, dW3~
+    Level l5;
+    for (int i = 0; i < 2; ++i) {
+      l5.add(gd(c->dh2.p + i * H, 2 * H, 1, W(q[i][1]), Hd, 0, c->dh1.p + i * H, 2 * H, B, H, H,
+                EPI_MASK, c->hq1.p + i * Hd, 2 * Hd));
+      l5.add(gd(c->dh2.p + i * H, 2 * H, 0, c->hq1.p + i * Hd, 2 * Hd, 0, dW(q[i][1]), Hd, H, H + 1, B));
+      l5.add(gd(c->dq.p + i * B, 1, 0, c->hq2.p + i * Hd, 2 * Hd, 0, dW(q[i][2]), Hd, 1, H + 1, B));
+    }
+    mark(c, "gemm_L5_critic_bwd2", level_flops(l5.b));
+    launch_gemm(l5.b, s);
+    // L6: dW1~
+    Level l6;
+    for (int i = 0; i < 2; ++i)
+      l6.add(gd(c->dh1.p + i * H, 2 * H, 0, c->xq.p, Kx, 0, dW(q[i][0]), Kx, H, S + A + 1, B));
+    mark(c, "gemm_L6_critic_dW1", level_flops(l6.b));
+    launch_gemm(l6.b, s);
+  }
+  const float lr = (float)c->cfg.lr;
+  if (phase_mask & 2) {
+    // critic Adam (+ Polyak, + q-loss finalisation)
+    AdamArgs ad{};
+    ad.p = P; ad.g = G; ad.m = c->M.p; ad.v = c->V.p; ad.tgt = c->T.p; ad.tgt_base = c->q_begin;
+    ad.nseg = 0;
+    for (int layer = 0; layer < 3; ++layer)
+      for (int i = 0; i < 2; ++i) {
+        const Linear& l = q[i][layer];
+        ad.seg[ad.nseg++] = AdamSeg{l.off, l.numel_padded(), i == 0 ? 1 : 2};
+      }
+    ad.total = 0;
+    for (int i = 0; i < ad.nseg; ++i) ad.total += ad.seg[i].n;
+    ad.lr = lr; ad.beta1 = 0.9f; ad.beta2 = 0.999f; ad.eps = 1e-8f; ad.grad_scale = grad_scale;
+    ad.tau = (float)c->cfg.tau; ad.step_offset = 1; ad.sc = c->sc.p;
+    ad.loss_part = c->lpart_c.p; ad.n_part = nb; ad.loss_slot0 = 0; ad.n_losses = 2;
+    ad.loss_div = (float)B; ad.log_alpha_idx = -1; ad.auto_entropy = 0;
+    mark(c, "adam_critic_polyak");
+    launch_adam(ad, s);
+    // L7/L8: updated critics on [s|1|a~]
+    const float* xa = c->x2.p + (size_t)B * Kx;
+    Level l7, l8;
+    for (int i = 0; i < 2; ++i)
+      l7.add(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, c->hqa1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+    mark(c, "gemm_L7_act_fc1", level_flops(l7.b));
+    launch_gemm(l7.b, s);
+    for (int i = 0; i < 2; ++i)
+      l8.add(gd(c->hqa1.p + i * Hd, 2 * Hd, 1, W(q[i][1]), Hd, 1, c->hqa2.p + i * Hd, 2 * Hd, B, H, H + 1, EPI_RELU));
+    mark(c, "gemm_L8_act_fc2", level_flops(l8.b));
+    launch_gemm(l8.b, s);
+    ActorRowsArgs ar{};
+    ar.hqa2 = c->hqa2.p; ar.ldh = Hd; ar.H = H; ar.B = B; ar.w3 = W(q[0][2]);
+    ar.w3_stride = (int)(q[1][2].off - q[0][2].off); ar.logp_a = c->logp.p + B; ar.sc = c->sc.p;
+    ar.dha2 = c->dha2.p; ar.loss_part = c->lpart_a.p;
+    mark(c, "actor_rows");
+    launch_actor_rows(ar, s);
+    // L9: dha1
+    Level l9;
+    for (int i = 0; i < 2; ++i)
+      l9.add(gd(c->dha2.p + i * H, 2 * H, 1, W(q[i][1]), Hd, 0, c->dha1.p + i * H, 2 * H, B, H, H,
+                EPI_MASK, c->hqa1.p + i * Hd, 2 * Hd));
+    mark(c, "gemm_L9_act_dh1", level_flops(l9.b));
+    launch_gemm(l9.b, s);
+    // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
+    GemmDesc da = gd(c->dha1.p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
+    SampleBwdArgs sb{};
+    sb.cache = c->cache.p + (size_t)B * 3 * A; sb.eps = c->eps.p + (size_t)B * A;
+    sb.dhead = c->dhead.p; sb.lddh = c->lddh; sb.A = A; sb.B = B; sb.sc = c->sc.p;
+    sb.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
+    mark(c, "gemm_L10_dlda_sample_bwd", 2.0 * B * A * (2.0 * H));
+    launch_gemm_sample_bwd(da, sb, s);
+    // L11: dhp2, dW_head~
+    const float* hp2a = c->hp2.p + (size_t)B * Hd;
+    const float* hp1a = c->hp1.p + (size_t)B * Hd;
+    Level l11;
+    l11.add(gd(c->dhead.p, c->lddh, 1, W(c->p_head), Hd, 0, c->dhp2.p, H, B, H, 2 * A, EPI_MASK, hp2a, Hd));
+    l11.add(gd(c->dhead.p, c->lddh, 0, hp2a, Hd, 0, dW(c->p_head), Hd, 2 * A, H + 1, B));
+    mark(c, "gemm_L11_pi_head_bwd", level_flops(l11.b));
+    launch_gemm(l11.b, s);
+    Level l12;
+    l12.add(gd(c->dhp2.p, H, 1, W(c->p_fc2), Hd, 0, c->dhp1.p, H, B, H, H, EPI_MASK, hp1a, Hd));
+    l12.add(gd(c->dhp2.p, H, 0, hp1a, Hd, 0, dW(c->p_fc2), Hd, H, H + 1, B));
+    mark(c, "gemm_L12_pi_fc2_bwd", level_flops(l12.b));
+    launch_gemm(l12.b, s);
+    Level l13;
+    l13.add(gd(c->dhp1.p, H, 0, xa, Kx, 0, dW(c->p_fc1), c->p_fc1.ld, H, S + 1, B));
+    mark(c, "gemm_L13_pi_dW1", level_flops(l13.b));
+    launch_gemm(l13.b, s);
+  }
+  if (phase_mask & 4) {
+    AdamArgs ad{};
+    ad.p = P; ad.g = G; ad.m = c->M.p; ad.v = c->V.p; ad.tgt = nullptr;
+    ad.nseg = 0;
+    for (const Linear* l : {&c->p_fc1, &c->p_fc2, &c->p_head})
+      ad.seg[ad.nseg++] = AdamSeg{l->off, l->numel_padded(), 0};
+    if (c->cfg.auto_entropy) ad.seg[ad.nseg++] = AdamSeg{c->la_idx, 1, 3};
+    ad.total = 0;
+    for (int i = 0; i < ad.nseg; ++i) ad.total += ad.seg[i].n;
+    ad.lr = lr; ad.beta1 = 0.9f; ad.beta2 = 0.999f; ad.eps = 1e-8f; ad.grad_scale = grad_scale;
+    ad.tau = 0.f; ad.step_offset = 0; ad.sc = c->sc.p;
+    ad.loss_part = c->lpart_a.p; ad.n_part = nb; ad.loss_slot0 = 2; ad.n_losses = 1;
+    ad.loss_div = (float)B; ad.log_alpha_idx = c->la_idx; ad.auto_entropy = c->cfg.auto_entropy;
+    ad.loss_ring = use_ring ? c->ring.p : nullptr; ad.ring = c->ring_slots;
+    mark(c, "adam_actor_alpha");
+    launch_adam(ad, s);
+  }
+}
+
+static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
+                       float grad_scale, bool use_ring) {
+  if (!c->use_graphs) {
+    enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring);
+    CHECK_HIP(hipGetLastError());
+    return;
+  }
+  GraphKey key{B, dev_idx, dev_eps, phase_mask | (grad_scale != 1.f ? 8 : 0), use_ring ? c->ring_slots : 0};
+  auto it = c->graphs.find(key);
+  if (it == c->graphs.end()) {
+    hipGraph_t g;
+    CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    try {
+      enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring);
+    } catch (...) {
+      (void)hipStreamEndCapture(c->stream, &g);
+      throw;
+    }
+    CHECK_HIP(hipStreamEndCapture(c->stream, &g));
+    hipGraphExec_t ex;
+    CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    CHECK_HIP(hipGraphDestroy(g));
+    it = c->graphs.emplace(key, ex).first;
+  }
+  CHECK_HIP(hipGraphLaunch(it->second, c->stream));
+}
+
+static void check_batch(sacmi_ctx* c, int B) {
+  REQUIRE(B > 0 && B <= c->Bm, SACMI_EVALUE,
+          "batch_size must be in [1, max_batch=" + std::to_string(c->Bm) + "]");
+  REQUIRE(B <= c->len, SACMI_EVALUE, "Sample larger than population or is negative");
+}
+
+static void stage_inputs(sacmi_ctx* c, int B, const int64_t* idx, const float* eps1,
+                         const float* eps2) {
+  if (idx) {
+    std::vector<int32_t> h(B);
+    for (int i = 0; i < B; ++i) {
+      REQUIRE(idx[i] >= 0 && idx[i] < c->len, SACMI_EVALUE, "index out of range");
+      h[i] = (int32_t)idx[i];
+    }
+    CHECK_HIP(hipMemcpyAsync(c->idx32.p, h.data(), B * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+  }
+  if (eps1 || eps2) {
+    REQUIRE(eps1 && eps2, SACMI_EVALUE, "eps1 and eps2 must both be given");
+    const size_t n = (size_t)B * c->A;
+    CHECK_HIP(hipMemcpyAsync(c->eps.p, eps1, n * 4, hipMemcpyHostToDevice, c->stream));
+    CHECK_HIP(hipMemcpyAsync(c->eps.p + n, eps2, n * 4, hipMemcpyHostToDevice, c->stream));
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+  }
+}
+
+}  // namespace sacmi
+
+using namespace sacmi;
+
+// ============================================================================
+extern "C" {
+
+int sacmi_abi_version(void) { return SACMI_ABI_VERSION; }
+const char* sacmi_last_error(void) { return g_last_error.c_str(); }
+
+int sacmi_device_count(int* n) {
+  return guard([&] { CHECK_HIP(hipGetDeviceCount(n)); });
+}
+
+int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
+  return guard([&] {
+    REQUIRE(cfg && out, SACMI_EVALUE, "null argument");
+    REQUIRE(cfg->state_dim > 0 && cfg->action_dim > 0 && cfg->hidden_dim > 0, SACMI_EVALUE,
+            "dims must be positive");
+    REQUIRE(cfg->action_dim <= 32, SACMI_EVALUE, "action_dim > 32 not supported");
+    REQUIRE(cfg->max_batch > 0 && cfg->max_batch <= 65536, SACMI_EVALUE, "bad max_batch");
+    REQUIRE(cfg->capacity > 0 && cfg->capacity < (int64_t)1 << 31, SACMI_EVALUE, "bad capacity");
+    int ndev = 0;
+    CHECK_HIP(hipGetDeviceCount(&ndev));
+    REQUIRE(device >= 0 && device < ndev, SACMI_EDEVICE, "no such HIP device");
+    CHECK_HIP(hipSetDevice(device));
+    std::unique_ptr<sacmi_ctx> c(new sacmi_ctx());
+    c->cfg = *cfg;
+    c->device = device;
+    c->S = cfg->state_dim; c->A = cfg->action_dim; c->H = cfg->hidden_dim; c->Bm = cfg->max_batch;
+    c->capacity = cfg->capacity;
+    CHECK_HIP(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    c->stream = c->own_stream;
+    build_layout(c.get());
+    alloc_all(c.get());
+    c->ring_slots = 4096;
+    c->ring.alloc((size_t)c->ring_slots * 3);
+    c->stage.alloc(0);
+    DevScalars h{};
+    h.alpha = (float)cfg->alpha;
+    h.per_frame = 1;
+    upload_scalars(c.get(), h);
+    // default RNG state: MT seeded with 5489 (both streams), as a fresh generator
+    std::vector<uint32_t> k(625);
+    k[0] = 5489u;
+    for (int i = 1; i < 624; ++i) k[i] = 1812433253u * (k[i - 1] ^ (k[i - 1] >> 30)) + i;
+    k[624] = 624;
+    CHECK_HIP(hipMemcpy(c->mt.p, k.data(), 625 * 4, hipMemcpyHostToDevice));
+    CHECK_HIP(hipMemcpy(c->mt.p + 625, k.data(), 625 * 4, hipMemcpyHostToDevice));
+    const char* ng = getenv("SACMI_NO_GRAPH");
+    c->use_graphs = !(ng && ng[0] == '1');
+    *out = c.release();
+  });
+}
+
+int sacmi_destroy(sacmi_ctx* c) {
+  return guard([&] {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    destroy_graphs(c);
+    for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
+                    &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->hp1, &c->hp2, &c->eps,
+                    &c->cache, &c->logp, &c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1,
+                    &c->hqa2, &c->dq, &c->dh2, &c->dh1, &c->dha2, &c->dha1, &c->dhead, &c->dhp2,
+                    &c->dhp1, &c->lpart_c, &c->lpart_a, &c->ring, &c->ax, &c->ah1, &c->ah2,
+                    &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr})
+      b->release();
+    c->sc.release(); c->mt.release(); c->idx32.release(); c->idx64.release();
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+  });
+}
+
+int sacmi_set_stream(sacmi_ctx* c, void* stream) {
+  return guard([&] {
+    REQUIRE(c, SACMI_EVALUE, "null ctx");
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    destroy_graphs(c);
+  });
+}
+
+int sacmi_synchronize(sacmi_ctx* c) {
+  return guard([&] { CHECK_HIP(hipStreamSynchronize(c->stream)); });
+}
+
+int sacmi_tensor_numel(sacmi_ctx* c, int net, int layer, int part, int64_t* numel) {
+  return guard([&] {
+    const Linear l = find_linear(c, net, layer);
+    *numel = part == 0 ? (int64_t)l.n_out * l.k_in : (int64_t)l.n_out;
+  });
+}
+
+static float* slot_base(sacmi_ctx* c, int slot, int net) {
+  const bool target = net == SACMI_Q1_TARGET || net == SACMI_Q2_TARGET;
+  if (target) {
+    REQUIRE(slot == SACMI_SLOT_PARAM, SACMI_EVALUE, "target nets only have parameters");
+    return c->T.p - c->q_begin;
+  }
+  switch (slot) {
+    case SACMI_SLOT_PARAM: return c->P.p;
+    case SACMI_SLOT_GRAD: return c->G.p;
+    case SACMI_SLOT_ADAM_M: return c->M.p;
+    case SACMI_SLOT_ADAM_V: return c->V.p;
+  }
+  throw Error{SACMI_EVALUE, "bad slot"};
+}
+
+static void tensor_io(sacmi_ctx* c, int slot, int net, int layer, int part, float* host,
+                      const float* in, int64_t numel) {
+  const Linear l = find_linear(c, net, layer);
+  const int64_t want = part == 0 ? (int64_t)l.n_out * l.k_in : (int64_t)l.n_out;
+  REQUIRE(part == 0 || part == 1, SACMI_EVALUE, "part must be 0 (weight) or 1 (bias)");
+  REQUIRE(numel == want, SACMI_EVALUE, "tensor size mismatch");
+  float* base = slot_base(c, slot, net) + l.off;
+  std::vector<float> buf((size_t)l.n_out * l.ld);
+  CHECK_HIP(hipStreamSynchronize(c->stream));
+  CHECK_HIP(hipMemcpy(buf.data(), base, buf.size() * 4, hipMemcpyDeviceToHost));
+  for (int o = 0; o < l.n_out; ++o) {
+    float* row = buf.data() + (size_t)o * l.ld;
+    if (part == 1) {
+      if (in) row[l.bias_col] = in[o]; else host[o] = row[l.bias_col];
+    } else {
+      for (int k = 0; k < l.k_in; ++k) {
+        const int col = k < l.split ? k : k + 1;
+        if (in) row[col] = in[(size_t)o * l.k_in + k]; else host[(size_t)o * l.k_in + k] = row[col];
+      }
+    }
+  }
+  if (in) CHECK_HIP(hipMemcpy(base, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
+}
+
+int sacmi_set_tensor(sacmi_ctx* c, int slot, int net, int layer, int part, const float* host,
+                     int64_t numel) {
+  return guard([&] { tensor_io(c, slot, net, layer, part, nullptr, host, numel); });
+}
+
+int sacmi_get_tensor(sacmi_ctx* c, int slot, int net, int layer, int part, float* host,
+                     int64_t numel) {
+  return guard([&] { tensor_io(c, slot, net, layer, part, host, nullptr, numel); });
+}
+
+static void arena_scalar(sacmi_ctx* c, float* arena, int64_t idx, const double* in, double* out) {
+  float v;
+  CHECK_HIP(hipStreamSynchronize(c->stream));
+  if (in) {
+    v = (float)*in;
+    CHECK_HIP(hipMemcpy(arena + idx, &v, 4, hipMemcpyHostToDevice));
+  } else {
+    CHECK_HIP(hipMemcpy(&v, arena + idx, 4, hipMemcpyDeviceToHost));
+    *out = v;
+  }
+}
+
+static void scalar_io(sacmi_ctx* c, int which, const double* in, double* out) {
+  switch (which) {
+    case SACMI_S_LOG_ALPHA: arena_scalar(c, c->P.p, c->la_idx, in, out); return;
+    case SACMI_S_ADAM_M_LOG_ALPHA: arena_scalar(c, c->M.p, c->la_idx, in, out); return;
+    case SACMI_S_ADAM_V_LOG_ALPHA: arena_scalar(c, c->V.p, c->la_idx, in, out); return;
+    case SACMI_S_GRAD_LOG_ALPHA: arena_scalar(c, c->G.p, c->la_idx, in, out); return;
+    default: break;
+  }
+  DevScalars h = download_scalars(c);
+  switch (which) {
+    case SACMI_S_ALPHA: if (in) h.alpha = (float)*in; else *out = h.alpha; break;
+    case SACMI_S_ALPHA_IS_TENSOR: if (in) h.alpha_is_tensor = (int)*in; else *out = h.alpha_is_tensor; break;
+    case SACMI_S_STEP_POLICY: case SACMI_S_STEP_Q1: case SACMI_S_STEP_Q2: case SACMI_S_STEP_ALPHA: {
+      const int k = which - SACMI_S_STEP_POLICY;
+      if (in) h.step[k] = *in; else *out = h.step[k];
+      break;
+    }
+    case SACMI_S_PER_FRAME: if (in) h.per_frame = (int64_t)*in; else *out = (double)h.per_frame; break;
+    case SACMI_S_NOISE_COUNTER: if (in) h.noise_counter = (uint64_t)*in; else *out = (double)h.noise_counter; break;
+    default: throw Error{SACMI_EVALUE, "bad scalar id"};
+  }
+  if (in) upload_scalars(c, h);
+}
+
+int sacmi_set_scalar(sacmi_ctx* c, int which, double value) {
+  return guard([&] { scalar_io(c, which, &value, nullptr); });
+}
+int sacmi_get_scalar(sacmi_ctx* c, int which, double* value) {
+  return guard([&] { scalar_io(c, which, nullptr, value); });
+}
+
+int sacmi_push(sacmi_ctx* c, const float* s, const float* a, const float* r, const float* s2,
+               const uint8_t* d, int64_t n) {
+  return guard([&] {
+    REQUIRE(n >= 0, SACMI_EVALUE, "n < 0");
+    if (n == 0) return;
+    REQUIRE(s && a && r && s2 && d, SACMI_EVALUE, "null transition array");
+    // only the last `capacity` rows of a huge batch survive (deque(maxlen))
+    int64_t skip = n > c->capacity ? n - c->capacity : 0;
+    const int S = c->S, A = c->A;
+    std::vector<float> dn;
+    const bool was_empty = c->len == 0;
+    const int64_t cap = c->capacity;
+    int64_t w = (c->wpos + skip) % cap;   // ring slot of row `skip`
+    const int64_t pos0 = w;
+    int64_t i = skip;
+    while (i < n) {
+      const int64_t run = std::min<int64_t>(n - i, cap - w);
+      CHECK_HIP(hipMemcpy2DAsync(c->obs.p + w * c->ldo, c->ldo * 4, s + i * S, S * 4, S * 4, run,
+                                 hipMemcpyHostToDevice, c->stream));
+      CHECK_HIP(hipMemcpy2DAsync(c->obs2.p + w * c->ldo, c->ldo * 4, s2 + i * S, S * 4, S * 4, run,
+                                 hipMemcpyHostToDevice, c->stream));
+      CHECK_HIP(hipMemcpy2DAsync(c->act.p + w * c->ldact, c->ldact * 4, a + i * A, A * 4, A * 4, run,
+                                 hipMemcpyHostToDevice, c->stream));
+      CHECK_HIP(hipMemcpyAsync(c->rew.p + w, r + i, run * 4, hipMemcpyHostToDevice, c->stream));
+      dn.resize(run);
+      for (int64_t j = 0; j < run; ++j) dn[j] = d[i + j] ? 1.f : 0.f;
+      CHECK_HIP(hipMemcpyAsync(c->done.p + w, dn.data(), run * 4, hipMemcpyHostToDevice, c->stream));
+      CHECK_HIP(hipStreamSynchronize(c->stream));
+      i += run;
+      w = (w + run) % cap;
+    }
+    const int64_t added = n - skip;
+    if (c->cfg.replay_kind == SACMI_REPLAY_PER) {
+      launch_per_push(c->prio.p, c->capacity, pos0, added, was_empty ? 1 : 0, c->per_scr.p, c->stream);
+    }
+    c->wpos = (c->wpos + n) % c->capacity;
+    c->len = std::min<int64_t>(c->capacity, c->len + n);
+    DevScalars h = download_scalars(c);
+    h.len = c->len;
+    h.head = c->len < c->capacity ? 0 : c->wpos;
+    upload_scalars(c, h);
+  });
+}
+
+int sacmi_len(sacmi_ctx* c, int64_t* n) {
+  return guard([&] { *n = c->len; });
+}
+
+int sacmi_get_rows(sacmi_ctx* c, const int64_t* idx, int64_t n, float* s, float* a, float* r,
+                   float* s2, uint8_t* d) {
+  return guard([&] {
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    const int64_t head = c->len < c->capacity ? 0 : c->wpos;
+    for (int64_t i = 0; i < n; ++i) {
+      REQUIRE(idx[i] >= 0 && idx[i] < c->len, SACMI_EVALUE, "index out of range");
+      const int64_t sl = (head + idx[i]) % c->capacity;
+      if (s) CHECK_HIP(hipMemcpy(s + i * c->S, c->obs.p + sl * c->ldo, c->S * 4, hipMemcpyDeviceToHost));
+      if (s2) CHECK_HIP(hipMemcpy(s2 + i * c->S, c->obs2.p + sl * c->ldo, c->S * 4, hipMemcpyDeviceToHost));
+      if (a) CHECK_HIP(hipMemcpy(a + i * c->A, c->act.p + sl * c->ldact, c->A * 4, hipMemcpyDeviceToHost));
+      if (r) CHECK_HIP(hipMemcpy(r + i, c->rew.p + sl, 4, hipMemcpyDeviceToHost));
+      if (d) {
+        float f;
+        CHECK_HIP(hipMemcpy(&f, c->done.p + sl, 4, hipMemcpyDeviceToHost));
+        d[i] = f != 0.f;
+      }
+    }
+  });
+}
+
+int sacmi_rng_set_mt(sacmi_ctx* c, int stream, const uint32_t* key, int32_t pos) {
+  return guard([&] {
+    REQUIRE(stream == 0 || stream == 1, SACMI_EVALUE, "stream must be 0 or 1");
+    REQUIRE(pos >= 0 && pos <= 624, SACMI_EVALUE, "MT position must be in [0, 624]");
+    std::vector<uint32_t> k(key, key + 624);
+    k.push_back((uint32_t)pos);
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    CHECK_HIP(hipMemcpy(c->mt.p + 625 * stream, k.data(), 625 * 4, hipMemcpyHostToDevice));
+  });
+}
+
+int sacmi_rng_get_mt(sacmi_ctx* c, int stream, uint32_t* key, int32_t* pos) {
+  return guard([&] {
+    REQUIRE(stream == 0 || stream == 1, SACMI_EVALUE, "stream must be 0 or 1");
+    std::vector<uint32_t> k(625);
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    CHECK_HIP(hipMemcpy(k.data(), c->mt.p + 625 * stream, 625 * 4, hipMemcpyDeviceToHost));
+    std::memcpy(key, k.data(), 624 * 4);
+    *pos = (int32_t)k[624];
+  });
+}
+
+int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
+  return guard([&] {
+    REQUIRE(batch >= 0 && batch <= c->len, SACMI_EVALUE, "Sample larger than population or is negative");
+    REQUIRE(batch <= c->Bm, SACMI_EVALUE, "batch > max_batch");
+    REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
+    if (batch == 0) return;
+    MtSampleArgs m{};
+    m.mt = c->mt.p; m.sc = c->sc.p; m.k = batch;
+    int setsize = 21;
+    if (batch > 5) setsize += (int)std::pow(4.0, std::ceil(std::log((double)batch * 3) / std::log(4.0)));
+    m.setsize = setsize; m.idx_out = c->idx32.p; m.idx64_out = c->idx64.p;
+    launch_mt_sample(m, c->stream);
+    CHECK_HIP(hipGetLastError());
+    CHECK_HIP(hipMemcpyAsync(idx_out, c->idx64.p, (size_t)batch * 8, hipMemcpyDeviceToHost, c->stream));
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int sacmi_step(sacmi_ctx* c, int32_t batch, const int64_t* idx, const float* eps1,
+               const float* eps2, float* losses_out) {
+  return guard([&] {
+    check_batch(c, batch);
+    REQUIRE(idx || batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
+    stage_inputs(c, batch, idx, eps1, eps2);
+    run_update(c, batch, idx ? 0 : 1, (eps1 || eps2) ? 0 : 1, 7, 1.f, false);
+    if (losses_out) {
+      DevScalars h = download_scalars(c);
+      std::memcpy(losses_out, h.losses, 12);
+    }
+  });
+}
+
+int sacmi_step_async(sacmi_ctx* c, int32_t batch) {
+  return guard([&] {
+    check_batch(c, batch);
+    REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
+    run_update(c, batch, 1, 1, 7, 1.f, true);
+  });
+}
+
+int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_out) {
+  return guard([&] {
+    DevScalars h = download_scalars(c);
+    const int64_t avail = std::min<int64_t>(h.loss_ring_pos, c->ring_slots);
+    const int64_t n = std::min<int64_t>(avail, max_steps);
+    std::vector<float> all((size_t)c->ring_slots * 3);
+    CHECK_HIP(hipMemcpy(all.data(), c->ring.p, all.size() * 4, hipMemcpyDeviceToHost));
+    // most recent n entries, oldest first
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t logical = h.loss_ring_pos - n + i;
+      const int64_t p = logical % c->ring_slots;
+      std::memcpy(out + i * 3, all.data() + p * 3, 12);
+    }
+    *n_out = (int32_t)n;
+  });
+}
+
+int sacmi_step_phase(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scale) {
+  return guard([&] {
+    REQUIRE(phase >= 0 && phase <= 2, SACMI_EVALUE, "phase must be 0, 1 or 2");
+    if (phase == 0) check_batch(c, batch);
+    run_update(c, batch, 1, 1, 1 << phase, grad_scale, false);
+  });
+}
+
+int sacmi_grad_buffer(sacmi_ctx* c, int which, void** ptr, int64_t* numel) {
+  return guard([&] {
+    REQUIRE(which == 0 || which == 1, SACMI_EVALUE, "which must be 0 (critic) or 1 (actor)");
+    if (which == 0) { *ptr = c->G.p + c->q_begin; *numel = c->q_end - c->q_begin; }
+    else { *ptr = c->G.p + c->pi_begin; *numel = c->total - c->pi_begin; }
+  });
+}
+
+int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_out,
+                       float* ms_out, double* flops_out, int32_t max_sites, int32_t* n_sites) {
+  return guard([&] {
+    check_batch(c, batch);
+    REQUIRE(iters > 0, SACMI_EVALUE, "iters must be > 0");
+    std::vector<double> acc;
+    std::vector<std::string> names;
+    std::vector<double> fl;
+    for (int it = 0; it < iters; ++it) {
+      c->prof = true;
+      c->prof_events.clear(); c->prof_names.clear(); c->prof_flops.clear();
+      try {
+        enqueue_update(c, batch, 1, 1, 7, 1.f, false);
+        mark(c, "end");
+      } catch (...) {
+        c->prof = false;
+        throw;
+      }
+      c->prof = false;
+      CHECK_HIP(hipStreamSynchronize(c->stream));
+      const size_t n = c->prof_events.size() - 1;
+      if (acc.empty()) { acc.assign(n, 0.0); names = c->prof_names; fl = c->prof_flops; }
+      for (size_t i = 0; i < n; ++i) {
+        float ms = 0;
+        CHECK_HIP(hipEventElapsedTime(&ms, c->prof_events[i], c->prof_events[i + 1]));
+        acc[i] += ms;
+      }
+      for (auto e : c->prof_events) (void)hipEventDestroy(e);
+      c->prof_events.clear();
+    }
+    const int n = (int)std::min<size_t>(acc.size(), (size_t)max_sites);
+    for (int i = 0; i < n; ++i) {
+      std::memset(names_out + 32 * i, 0, 32);
+      std::strncpy(names_out + 32 * i, names[i].c_str(), 31);
+      ms_out[i] = (float)(acc[i] / iters);
+      flops_out[i] = fl[i];
+    }
+    *n_sites = n;
+  });
+}
+
+int sacmi_per_sample(sacmi_ctx* c, int32_t, const double*, int64_t*, float*) {
+  return guard([&] { throw Error{SACMI_ESTATE, "PER sampling not built yet"}; });
+}
+int sacmi_per_update(sacmi_ctx* c, const int64_t*, const float*, int64_t) {
+  return guard([&] { throw Error{SACMI_ESTATE, "PER not built yet"}; });
+}
+int sacmi_per_get_priorities(sacmi_ctx* c, float*, int64_t) {
+  return guard([&] { throw Error{SACMI_ESTATE, "PER not built yet"}; });
+}
+int sacmi_per_set_priorities(sacmi_ctx* c, const float*, int64_t) {
+  return guard([&] { throw Error{SACMI_ESTATE, "PER not built yet"}; });
+}
+
+int sacmi_act(sacmi_ctx* c, const float*, int32_t, int32_t, const float*, float*) {
+  return guard([&] { throw Error{SACMI_ESTATE, "act not built yet"}; });
+}
+
+}  // extern "C"

@@ -1,0 +1,221 @@
+// Internal declarations of libsacmi: device layout + kernel launchers.
+//
+// Data layout in HBM (fp32 unless noted) — see DESIGN.md §3:
+//   * Every nn.Linear is stored "bias-folded": W~ = [W | b] with one extra input
+//     column, so every activation matrix carries a constant-1 column and a single
+//     MFMA GEMM produces both y = x W^T + b (forward) and [dW | db] = dY^T x~
+//     (backward).  Row stride `ld` is padded to a multiple of 4 floats (16 B) and the
+//     pad is kept at exactly 0.
+//   * The critic input is [s | 1 | a | 0-pad] (bias column between state and
+//     action) so the policy can read its input [s | 1] from the same rows.
+//   * Trained parameters live in one flat arena ordered
+//       [q1.fc1 q2.fc1 | q1.fc2 q2.fc2 | q1.fc3 q2.fc3 | policy.fc1 policy.fc2
+//        policy.head(mean rows ; log_std rows) | log_alpha]
+//     (twin fc1 adjacent so dL/da of both critics is ONE GEMM with K = 2H); the
+//     gradient, Adam m and Adam v arenas mirror it, the target arena mirrors the
+//     critic part.  Critic grads and actor grads are each contiguous (one
+//     all-reduce each in data-parallel mode).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/sacmi.h"
+
+namespace sacmi {
+
+constexpr int kWave = 64;
+
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// One bias-folded linear layer inside an arena.
+struct Linear {
+  int64_t off = 0;   // float offset of W~ [n_out, ld]
+  int n_out = 0;     // out features
+  int k_in = 0;      // in features (reference)
+  int ld = 0;        // row stride of W~ (>= k_in + 1, %4 == 0)
+  int bias_col = 0;  // column of W~ holding the bias
+  int split = 0;     // reference cols >= split sit one column to the right
+  int kdim() const { return k_in + 1; }   // GEMM K including the bias column
+  int64_t numel_padded() const { return (int64_t)n_out * ld; }
+};
+
+// Scalars shared by kernels (device resident, one struct per context).
+struct DevScalars {
+  float alpha;          // alpha used by this update (0.2 until the first update)
+  float log_alpha_grad; // (unused slot kept for alignment)
+  float losses[3];      // q1, q2, policy of the last update
+  float pad0;
+  double step[4];       // Adam step of policy, q1, q2, alpha optimizers
+  uint64_t noise_counter;
+  int64_t len;          // replay fill
+  int64_t head;         // ring slot of deque position 0
+  int64_t per_frame;
+  int32_t alpha_is_tensor;
+  int32_t err;
+  int64_t loss_ring_pos;
+};
+
+enum Epi { EPI_STORE = 0, EPI_RELU = 1, EPI_MASK = 2 };
+
+// One GEMM of a grouped launch: C[m,n] = epi( sum_k A(m,k) B(k,n) ).
+//   A(m,k) = a_kc ? A[m*lda + k] : A[k*lda + m]
+//   B(k,n) = b_kc ? B[n*ldb + k] : B[k*ldb + n]
+//   EPI_MASK: C = acc * (aux[m*ldaux + n] > 0)   (ReLU backward)
+struct GemmDesc {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* aux;
+  int M, N, K;
+  int lda, ldb, ldc, ldaux;
+  int a_kc, b_kc, epi;
+  int tiles_n, tile_begin;
+};
+
+constexpr int kMaxGemms = 8;
+struct GemmBatch {
+  GemmDesc d[kMaxGemms];
+  int count;
+  int total_tiles;
+};
+
+// Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked
+// [target rows ; actor rows] matrix.
+struct HeadSampleArgs {
+  const float* h;        // [rows, ldh] policy hidden (h~ incl. ones col)
+  const float* Wh;       // [2A, ldw] head weights (mean rows ; log_std rows)
+  int rows, A, K, ldh, ldw;
+  float* eps;            // [rows, A] standard normals (read, or written when gen)
+  int gen_eps;           // 1: Philox noise
+  uint64_t seed;
+  const DevScalars* sc;
+  float* act;            // actions written to act[row*ldact + j]
+  int ldact;
+  float* logp;           // [rows]
+  float* cache;          // [rows, 3A]: mean | log_std(raw) | y
+  float scale, bias;
+};
+
+// Sample-backward epilogue of the dL/da GEMM.
+struct SampleBwdArgs {
+  const float* cache;    // actor rows' cache [B, 3A]
+  const float* eps;      // actor rows' eps [B, A]
+  float* dhead;          // [B, lddh] : dmean | dlog_std
+  int lddh, A, B;
+  const DevScalars* sc;
+  float scale;
+};
+
+// ---------------------------------------------------------------------------
+// launchers (kernels.hip)
+void launch_gemm(const GemmBatch& batch, hipStream_t s);
+void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
+void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s);
+
+struct CriticRowsArgs {
+  const float* hq2;   // [B, 2*ldh] critic hidden-2 (q1 | q2)
+  const float* hqt2;  // [B, 2*ldh] target hidden-2
+  int ldh, H, B;
+  const float* w3;    // q1.fc3 row (ld = ld3); q2.fc3 at + w3_stride
+  const float* w3t;   // target fc3
+  int w3_stride;
+  const float* r;     // [B]
+  const float* d;     // [B]
+  const float* logp_t;  // [B] next-state log-probs
+  const float* logp_a;  // [B] actor log-probs (for the alpha gradient)
+  float gamma;
+  float target_entropy;
+  int auto_entropy;
+  DevScalars* sc;
+  float* dq;          // [2, B]
+  float* dh2;         // [B, 2H]
+  float* loss_part;   // [nblocks, 2]
+  float* alpha_grad;  // gradient slot of log_alpha
+};
+void launch_critic_rows(const CriticRowsArgs& a, hipStream_t s);
+
+struct ActorRowsArgs {
+  const float* hqa2;  // [B, 2*ldh]
+  int ldh, H, B;
+  const float* w3;
+  int w3_stride;
+  const float* logp_a;
+  DevScalars* sc;
+  float* dha2;        // [B, 2H]
+  float* loss_part;   // [nblocks]
+};
+void launch_actor_rows(const ActorRowsArgs& a, hipStream_t s);
+
+struct AdamSeg { int64_t off, n; int step_idx; };
+struct AdamArgs {
+  float* p; const float* g; float* m; float* v;
+  float* tgt;              // Polyak target arena (mirrors p from p_tgt_base) or null
+  int64_t tgt_base;        // offset subtracted from p index to index tgt
+  int nseg; AdamSeg seg[4];
+  int64_t total;           // sum of seg n (grid-stride domain)
+  float lr, beta1, beta2, eps, grad_scale, tau;
+  int step_offset;         // t = step[idx] + step_offset
+  DevScalars* sc;
+  // loss finalisation (block 0)
+  const float* loss_part; int n_part; int loss_slot0; int n_losses; float loss_div;
+  // alpha update: index (inside p) of log_alpha or -1
+  int64_t log_alpha_idx; int auto_entropy;
+  float* loss_ring;        // [ring, 3] or null
+  int ring;
+};
+void launch_adam(const AdamArgs& a, hipStream_t s);
+
+struct GatherArgs {
+  const int32_t* idx;     // deque positions [B]
+  const float* obs; const float* act; const float* rew; const float* obs2; const float* done;
+  int ldo, lda_;          // row strides of obs/obs2 and act in the ring
+  int64_t capacity;
+  const DevScalars* sc;
+  int S, A, B;
+  float* xq; float* x2; int ldx;   // xq [B, ldx], x2 [2B, ldx]
+  float* r; float* d;
+};
+void launch_gather(const GatherArgs& a, hipStream_t s);
+
+struct MtSampleArgs {
+  uint32_t* mt;           // 624 key words + pos
+  const DevScalars* sc;   // len
+  int k;                  // batch
+  int setsize;            // random.sample branch threshold (host-computed, exact)
+  int32_t* idx_out;       // [k]
+  int64_t* idx64_out;     // [k] or null
+  int32_t* pool;          // scratch [max setsize] for the pool branch
+};
+void launch_mt_sample(const MtSampleArgs& a, hipStream_t s);
+
+void launch_fill(float* p, int64_t n, float v, hipStream_t s);
+void launch_set_column(float* p, int rows, int ld, int col, float v, hipStream_t s);
+void launch_increment_steps(DevScalars* sc, hipStream_t s);
+
+// PER
+struct PerArgs {
+  float* prio; int64_t len; int64_t cap;
+  float alpha;
+  float* probs;           // [len]
+  double* cdf;            // [len]
+  float* chunk_sums;      // scratch
+  int64_t* ichunk;        // scratch
+  const double* u;        // [k] uniforms (device)
+  uint32_t* mt;           // numpy MT state when u is generated on device
+  int gen_u;
+  int k;
+  int64_t* idx_out;
+  float* w_out;
+  DevScalars* sc;
+  float beta_start, beta_frames;
+  double* u_scratch;
+};
+void launch_per_sample(const PerArgs& a, hipStream_t s);
+void launch_per_update(float* prio, const int64_t* idx, const float* val, int64_t n, hipStream_t s);
+void launch_per_push(float* prio, int64_t cap, int64_t pos, int64_t n, int empty, float* scratch,
+                     hipStream_t s);
+
+}  // namespace sacmi

@@ -1,0 +1,157 @@
+"""ctypes bridge to libsacmi.so (the C ABI declared in include/sacmi.h).
+
+The library is the product: there is no CPU fallback.  Loading fails loudly when
+the shared object is missing or was built for another ABI version.
+
+``import torch`` happens before the library is loaded on purpose: torch ships its
+own HIP runtime (``libamdhip64.so.7``); loading it first makes the dynamic linker
+resolve libsacmi's HIP dependency to the same runtime instance, so device
+pointers and streams are shared with torch (needed for the RCCL all-reduce of the
+data-parallel path).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsacmi.so")
+ABI_VERSION = 1
+
+c_f32p = ctypes.POINTER(ctypes.c_float)
+c_f64p = ctypes.POINTER(ctypes.c_double)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_vp = ctypes.c_void_p
+
+SACMI_OK, SACMI_EVALUE, SACMI_ESTATE, SACMI_EDEVICE, SACMI_ENAN = range(5)
+REPLAY_UNIFORM, REPLAY_PER = 0, 1
+POLICY, Q1, Q2, Q1_TARGET, Q2_TARGET = range(5)
+SLOT_PARAM, SLOT_GRAD, SLOT_ADAM_M, SLOT_ADAM_V = range(4)
+(S_LOG_ALPHA, S_ALPHA, S_ALPHA_IS_TENSOR, S_STEP_POLICY, S_STEP_Q1, S_STEP_Q2, S_STEP_ALPHA,
+ S_ADAM_M_LOG_ALPHA, S_ADAM_V_LOG_ALPHA, S_GRAD_LOG_ALPHA, S_PER_FRAME,
+ S_NOISE_COUNTER) = range(12)
+
+
+class SacmiConfig(ctypes.Structure):
+    _fields_ = [
+        ("state_dim", ctypes.c_int32), ("action_dim", ctypes.c_int32),
+        ("hidden_dim", ctypes.c_int32), ("max_batch", ctypes.c_int32),
+        ("gamma", ctypes.c_double), ("tau", ctypes.c_double), ("lr", ctypes.c_double),
+        ("alpha", ctypes.c_double), ("auto_entropy", ctypes.c_int32),
+        ("replay_kind", ctypes.c_int32), ("action_low", ctypes.c_double),
+        ("action_high", ctypes.c_double), ("capacity", ctypes.c_int64),
+        ("per_alpha", ctypes.c_double), ("per_beta_start", ctypes.c_double),
+        ("per_beta_frames", ctypes.c_double), ("seed", ctypes.c_uint64),
+    ]
+
+
+# name -> (argtypes)   every function returns int status except the two noted
+_PROTOS = {
+    "sacmi_device_count": [c_i32p],
+    "sacmi_create": [ctypes.POINTER(SacmiConfig), ctypes.c_int, ctypes.POINTER(c_vp)],
+    "sacmi_destroy": [c_vp],
+    "sacmi_set_stream": [c_vp, c_vp],
+    "sacmi_synchronize": [c_vp],
+    "sacmi_tensor_numel": [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64p],
+    "sacmi_set_tensor": [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_f32p,
+                         ctypes.c_int64],
+    "sacmi_get_tensor": [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_f32p,
+                         ctypes.c_int64],
+    "sacmi_set_scalar": [c_vp, ctypes.c_int, ctypes.c_double],
+    "sacmi_get_scalar": [c_vp, ctypes.c_int, c_f64p],
+    "sacmi_push": [c_vp, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p, ctypes.c_int64],
+    "sacmi_len": [c_vp, c_i64p],
+    "sacmi_get_rows": [c_vp, c_i64p, ctypes.c_int64, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p],
+    "sacmi_rng_set_mt": [c_vp, ctypes.c_int, c_u32p, ctypes.c_int32],
+    "sacmi_rng_get_mt": [c_vp, ctypes.c_int, c_u32p, c_i32p],
+    "sacmi_sample_indices": [c_vp, ctypes.c_int32, c_i64p],
+    "sacmi_step": [c_vp, ctypes.c_int32, c_i64p, c_f32p, c_f32p, c_f32p],
+    "sacmi_step_async": [c_vp, ctypes.c_int32],
+    "sacmi_fetch_losses": [c_vp, c_f32p, ctypes.c_int32, c_i32p],
+    "sacmi_step_phase": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float],
+    "sacmi_grad_buffer": [c_vp, ctypes.c_int, ctypes.POINTER(c_vp), c_i64p],
+    "sacmi_per_sample": [c_vp, ctypes.c_int32, c_f64p, c_i64p, c_f32p],
+    "sacmi_per_update": [c_vp, c_i64p, c_f32p, ctypes.c_int64],
+    "sacmi_per_get_priorities": [c_vp, c_f32p, ctypes.c_int64],
+    "sacmi_per_set_priorities": [c_vp, c_f32p, ctypes.c_int64],
+    "sacmi_act": [c_vp, c_f32p, ctypes.c_int32, ctypes.c_int32, c_f32p, c_f32p],
+    "sacmi_profile_step": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
+                           ctypes.c_int32, c_i32p],
+}
+EXPORTS = tuple(_PROTOS) + ("sacmi_abi_version", "sacmi_last_error")
+
+_lib = None
+
+
+class SacmiError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the library; raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libsacmi.so not found at {LIB_PATH}; build it with "
+            f"`make -C humanoid-walking-with-sac_amd` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.sacmi_abi_version.restype = ctypes.c_int
+    lib.sacmi_abi_version.argtypes = []
+    lib.sacmi_last_error.restype = ctypes.c_char_p
+    lib.sacmi_last_error.argtypes = []
+    for name, args in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    v = lib.sacmi_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"libsacmi ABI {v} != expected {ABI_VERSION}; rebuild")
+    _lib = lib
+    return lib
+
+
+def check(status: int) -> None:
+    """Map a status code to the reference's exception types."""
+    if status == SACMI_OK:
+        return
+    msg = load().sacmi_last_error().decode(errors="replace")
+    if status in (SACMI_EVALUE, SACMI_ENAN):
+        raise ValueError(msg)
+    raise SacmiError(f"sacmi error {status}: {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args))
+
+
+def fptr(a):
+    return a.ctypes.data_as(c_f32p) if a is not None else None
+
+
+def dptr(a):
+    return a.ctypes.data_as(c_f64p) if a is not None else None
+
+
+def i64ptr(a):
+    return a.ctypes.data_as(c_i64p) if a is not None else None
+
+
+def u8ptr(a):
+    return a.ctypes.data_as(c_u8p) if a is not None else None
+
+
+def u32ptr(a):
+    return a.ctypes.data_as(c_u32p) if a is not None else None
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    call("sacmi_device_count", ctypes.byref(n))
+    return n.value

@@ -1,0 +1,259 @@
+"""Object wrapper over one libsacmi context (one agent on one GPU)."""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+NET_IDS = {"policy": L.POLICY, "q1": L.Q1, "q2": L.Q2, "q1_target": L.Q1_TARGET,
+           "q2_target": L.Q2_TARGET}
+# state_dict key -> (layer, part)
+POLICY_LAYERS = {"fc1": 0, "fc2": 1, "mean": 2, "log_std": 3}
+Q_LAYERS = {"fc1": 0, "fc2": 1, "fc3": 2}
+SLOTS = {"param": L.SLOT_PARAM, "grad": L.SLOT_GRAD, "m": L.SLOT_ADAM_M, "v": L.SLOT_ADAM_V}
+
+
+def net_keys(net: str):
+    layers = POLICY_LAYERS if net == "policy" else Q_LAYERS
+    for name, layer in layers.items():
+        yield f"{name}.weight", layer, 0
+        yield f"{name}.bias", layer, 1
+
+
+@dataclass
+class Config:
+    state_dim: int
+    action_dim: int
+    hidden_dim: int = 256
+    max_batch: int = 4096
+    gamma: float = 0.99
+    tau: float = 0.005
+    lr: float = 3e-4
+    alpha: float = 0.2
+    automatic_entropy_tuning: bool = True
+    replay: str = "uniform"
+    action_low: float = -0.4
+    action_high: float = 0.4
+    capacity: int = 1_000_000
+    per_alpha: float = 0.6
+    per_beta_start: float = 0.4
+    per_beta_frames: float = 100000
+    seed: int = 0
+
+    def to_c(self) -> L.SacmiConfig:
+        c = L.SacmiConfig()
+        c.state_dim, c.action_dim, c.hidden_dim = self.state_dim, self.action_dim, self.hidden_dim
+        c.max_batch = self.max_batch
+        c.gamma, c.tau, c.lr, c.alpha = self.gamma, self.tau, self.lr, self.alpha
+        c.auto_entropy = int(bool(self.automatic_entropy_tuning))
+        c.replay_kind = L.REPLAY_PER if self.replay == "per" else L.REPLAY_UNIFORM
+        c.action_low, c.action_high = self.action_low, self.action_high
+        c.capacity = int(self.capacity)
+        c.per_alpha, c.per_beta_start = self.per_alpha, self.per_beta_start
+        c.per_beta_frames = float(self.per_beta_frames)
+        c.seed = int(self.seed) & ((1 << 64) - 1)
+        return c
+
+
+def setsize(k: int) -> int:
+    """random.py:488-490 (the pool/set branch threshold of random.sample)."""
+    s = 21
+    if k > 5:
+        s += 4 ** math.ceil(math.log(k * 3, 4))
+    return s
+
+
+class Context:
+    """Owns a ``sacmi_ctx``; every method is one C-ABI call."""
+
+    def __init__(self, cfg: Config, device: int = 0):
+        self.cfg = cfg
+        self.device = device
+        self._lib = L.load()
+        h = ctypes.c_void_p()
+        ccfg = cfg.to_c()
+        L.call("sacmi_create", ctypes.byref(ccfg), int(device), ctypes.byref(h))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            L.call("sacmi_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- streams -----------------------------------------------------------------
+    def set_stream(self, stream_handle: int | None):
+        L.call("sacmi_set_stream", self._h, ctypes.c_void_p(stream_handle or 0))
+
+    def synchronize(self):
+        L.call("sacmi_synchronize", self._h)
+
+    # -- tensors -----------------------------------------------------------------
+    def numel(self, net: str, layer: int, part: int) -> int:
+        n = ctypes.c_int64()
+        L.call("sacmi_tensor_numel", self._h, NET_IDS[net], layer, part, ctypes.byref(n))
+        return n.value
+
+    def get_tensor(self, slot: str, net: str, layer: int, part: int, shape) -> np.ndarray:
+        out = np.empty(shape, np.float32)
+        L.call("sacmi_get_tensor", self._h, SLOTS[slot], NET_IDS[net], layer, part, L.fptr(out),
+               out.size)
+        return out
+
+    def set_tensor(self, slot: str, net: str, layer: int, part: int, value) -> None:
+        v = np.ascontiguousarray(value, dtype=np.float32)
+        L.call("sacmi_set_tensor", self._h, SLOTS[slot], NET_IDS[net], layer, part, L.fptr(v),
+               v.size)
+
+    def get_net(self, net: str, slot: str = "param", shapes: dict | None = None) -> dict:
+        out = {}
+        for key, layer, part in net_keys(net):
+            n = self.numel(net, layer, part)
+            shp = shapes[key] if shapes else (n,)
+            out[key] = self.get_tensor(slot, net, layer, part, shp)
+        return out
+
+    def set_net(self, net: str, sd: dict, slot: str = "param") -> None:
+        for key, layer, part in net_keys(net):
+            self.set_tensor(slot, net, layer, part, np.asarray(sd[key]))
+
+    def get_scalar(self, which: int) -> float:
+        v = ctypes.c_double()
+        L.call("sacmi_get_scalar", self._h, which, ctypes.byref(v))
+        return v.value
+
+    def set_scalar(self, which: int, value: float) -> None:
+        L.call("sacmi_set_scalar", self._h, which, float(value))
+
+    # -- replay --------------------------------------------------------------------
+    def push(self, s, a, r, s2, d) -> None:
+        S, A = self.cfg.state_dim, self.cfg.action_dim
+        s = np.ascontiguousarray(s, np.float32).reshape(-1, S)
+        n = s.shape[0]
+        a = np.ascontiguousarray(a, np.float32).reshape(n, A)
+        r = np.ascontiguousarray(r, np.float32).reshape(n)
+        s2 = np.ascontiguousarray(s2, np.float32).reshape(n, S)
+        d = np.ascontiguousarray(np.asarray(d).astype(bool), np.uint8).reshape(n)
+        L.call("sacmi_push", self._h, L.fptr(s), L.fptr(a), L.fptr(r), L.fptr(s2), L.u8ptr(d), n)
+
+    def __len__(self) -> int:
+        n = ctypes.c_int64()
+        L.call("sacmi_len", self._h, ctypes.byref(n))
+        return n.value
+
+    def get_rows(self, idx):
+        idx = np.ascontiguousarray(idx, np.int64)
+        n = idx.size
+        S, A = self.cfg.state_dim, self.cfg.action_dim
+        s = np.empty((n, S), np.float32); s2 = np.empty((n, S), np.float32)
+        a = np.empty((n, A), np.float32); r = np.empty(n, np.float32); d = np.empty(n, np.uint8)
+        L.call("sacmi_get_rows", self._h, L.i64ptr(idx), n, L.fptr(s), L.fptr(a), L.fptr(r),
+               L.fptr(s2), L.u8ptr(d))
+        return s, a, r, s2, d.astype(bool)
+
+    # -- rng -----------------------------------------------------------------------
+    def set_mt(self, stream: int, key, pos: int) -> None:
+        k = np.ascontiguousarray(key, np.uint32)
+        assert k.shape == (624,)
+        L.call("sacmi_rng_set_mt", self._h, stream, L.u32ptr(k), int(pos))
+
+    def get_mt(self, stream: int):
+        k = np.empty(624, np.uint32)
+        p = ctypes.c_int32()
+        L.call("sacmi_rng_get_mt", self._h, stream, L.u32ptr(k), ctypes.byref(p))
+        return k, p.value
+
+    def sample_indices(self, batch: int) -> np.ndarray:
+        out = np.empty(batch, np.int64)
+        L.call("sacmi_sample_indices", self._h, int(batch), L.i64ptr(out))
+        return out
+
+    # -- the update ------------------------------------------------------------------
+    def step(self, batch: int, idx=None, eps1=None, eps2=None, want_losses: bool = True):
+        A = self.cfg.action_dim
+        idx_a = None if idx is None else np.ascontiguousarray(idx, np.int64)
+        e1 = None if eps1 is None else np.ascontiguousarray(eps1, np.float32).reshape(batch, A)
+        e2 = None if eps2 is None else np.ascontiguousarray(eps2, np.float32).reshape(batch, A)
+        out = np.zeros(3, np.float32) if want_losses else None
+        L.call("sacmi_step", self._h, int(batch), L.i64ptr(idx_a), L.fptr(e1), L.fptr(e2),
+               L.fptr(out))
+        return out
+
+    def step_async(self, batch: int) -> None:
+        L.call("sacmi_step_async", self._h, int(batch))
+
+    def fetch_losses(self, max_steps: int) -> np.ndarray:
+        out = np.zeros((max_steps, 3), np.float32)
+        n = ctypes.c_int32()
+        L.call("sacmi_fetch_losses", self._h, L.fptr(out), int(max_steps), ctypes.byref(n))
+        return out[:n.value]
+
+    def step_phase(self, batch: int, phase: int, grad_scale: float = 1.0) -> None:
+        L.call("sacmi_step_phase", self._h, int(batch), int(phase), float(grad_scale))
+
+    def grad_buffer(self, which: int):
+        p = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        L.call("sacmi_grad_buffer", self._h, which, ctypes.byref(p), ctypes.byref(n))
+        return p.value, n.value
+
+    # -- PER -------------------------------------------------------------------------
+    def per_sample(self, batch: int, u=None):
+        n = min(batch, len(self))
+        idx = np.empty(n, np.int64)
+        w = np.empty(n, np.float32)
+        u_a = None if u is None else np.ascontiguousarray(u, np.float64)
+        L.call("sacmi_per_sample", self._h, int(batch), L.dptr(u_a), L.i64ptr(idx), L.fptr(w))
+        return idx, w
+
+    def per_update(self, idx, prio) -> None:
+        idx = np.ascontiguousarray(idx, np.int64)
+        p = np.ascontiguousarray(prio, np.float32).reshape(-1)
+        L.call("sacmi_per_update", self._h, L.i64ptr(idx), L.fptr(p), idx.size)
+
+    def per_priorities(self, n: int | None = None) -> np.ndarray:
+        n = self.cfg.capacity if n is None else n
+        out = np.empty(n, np.float32)
+        L.call("sacmi_per_get_priorities", self._h, L.fptr(out), n)
+        return out
+
+    def per_set_priorities(self, prio) -> None:
+        p = np.ascontiguousarray(prio, np.float32)
+        L.call("sacmi_per_set_priorities", self._h, L.fptr(p), p.size)
+
+    # -- diagnostics -------------------------------------------------------------------
+    def profile_step(self, batch: int, iters: int = 10):
+        """[(site, mean_ms, flops_per_launch)] over `iters` eager updates (HIP events)."""
+        mx = 64
+        names = ctypes.create_string_buffer(32 * mx)
+        ms = np.zeros(mx, np.float32)
+        fl = np.zeros(mx, np.float64)
+        n = ctypes.c_int32()
+        L.call("sacmi_profile_step", self._h, int(batch), int(iters), names, L.fptr(ms),
+               L.dptr(fl), mx, ctypes.byref(n))
+        raw = names.raw
+        return [(raw[32 * i:32 * i + 32].split(b"\0")[0].decode(), float(ms[i]), float(fl[i]))
+                for i in range(n.value)]
+
+    # -- act -------------------------------------------------------------------------
+    def act(self, states, deterministic: bool, eps=None) -> np.ndarray:
+        S, A = self.cfg.state_dim, self.cfg.action_dim
+        s = np.ascontiguousarray(states, np.float32).reshape(-1, S)
+        n = s.shape[0]
+        e = None if eps is None else np.ascontiguousarray(eps, np.float32).reshape(n, A)
+        out = np.empty((n, A), np.float32)
+        L.call("sacmi_act", self._h, L.fptr(s), n, int(bool(deterministic)), L.fptr(e), L.fptr(out))
+        return out

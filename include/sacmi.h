@@ -1,0 +1,189 @@
+/*
+ * sacmi.h — C ABI of the MI355X-native SAC gradient-step library (libsacmi.so).
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (FilippoCrc/Humanoid-walking-with-SAC, snapshot 2025-02-22):
+ *
+ *   sac_imp.SAC.__init__            sac_imp.py:9-52        -> sacmi_create
+ *   sac_imp.SAC.update_parameters   sac_imp.py:74-144      -> sacmi_step / sacmi_step_async
+ *   sac_imp.SAC._soft_update_...    sac_imp.py:146-152     -> (inside sacmi_step)
+ *   sac_imp.SAC.select_action       sac_imp.py:54-72       -> sacmi_act
+ *   nn.Module.state_dict / load     sac_imp.py:154-233     -> sacmi_get_tensor / sacmi_set_tensor
+ *   ReplayBuffer.push / __len__     replay_buffer.py:10-11,21-22   -> sacmi_push / sacmi_len
+ *   ReplayBuffer.sample (indices)   replay_buffer.py:13-19 -> sacmi_sample_indices (+ inside step)
+ *   ReplayBuffer.buffer (read)      sac_imp.py:199          -> sacmi_get_rows
+ *   PrioritizedReplayBuffer.sample  replay_buffer.py:48-82 -> sacmi_per_sample
+ *   PrioritizedReplayBuffer.update_priorities  replay_buffer.py:84-87 -> sacmi_per_update
+ *   random.getstate/setstate, np.random.get_state/set_state -> sacmi_rng_get_mt / sacmi_rng_set_mt
+ *
+ * Conventions
+ *   - Every call returns int status: 0 = OK, otherwise an SACMI_E* code; the message
+ *     is in sacmi_last_error() (thread-local).  The Python host maps codes to the
+ *     reference's exceptions (ValueError for SACMI_EVALUE, RuntimeError otherwise).
+ *   - One context per GPU.  All device work of a context is ordered on its HIP stream
+ *     (its own, or one supplied by sacmi_set_stream).  A context is not thread-safe.
+ *   - The library owns all device memory; every host pointer argument is copied in
+ *     or out before the call returns (except sacmi_step_async, which writes nothing
+ *     to host memory).
+ *   - Plain C types only: no torch / HIP types cross this boundary.
+ */
+#ifndef SACMI_H_
+#define SACMI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SACMI_ABI_VERSION 1
+
+enum sacmi_status {
+  SACMI_OK = 0,
+  SACMI_EVALUE = 1,    /* bad argument (maps to ValueError)          */
+  SACMI_ESTATE = 2,    /* call not valid in the current state        */
+  SACMI_EDEVICE = 3,   /* HIP runtime error / no device              */
+  SACMI_ENAN = 4,      /* non-finite value surfaced (maps to ValueError, as Normal(validate_args)) */
+};
+
+enum sacmi_replay_kind { SACMI_REPLAY_UNIFORM = 0, SACMI_REPLAY_PER = 1 };
+
+typedef struct sacmi_config {
+  int32_t state_dim;          /* S  (sac_imp.py:11)                               */
+  int32_t action_dim;         /* A  (sac_imp.py:12)                               */
+  int32_t hidden_dim;         /* H  (sac_imp.py:13, default 256)                  */
+  int32_t max_batch;          /* largest batch_size passed to step / act          */
+  double gamma;               /* 0.99  (sac_imp.py:14)                            */
+  double tau;                 /* 0.005 (sac_imp.py:15)                            */
+  double lr;                  /* 3e-4  (sac_imp.py:16)                            */
+  double alpha;               /* 0.2   (sac_imp.py:17) alpha used until the 1st update */
+  int32_t auto_entropy;       /* automatic_entropy_tuning (sac_imp.py:18)          */
+  int32_t replay_kind;        /* sacmi_replay_kind                                 */
+  double action_low;          /* action_bounds (networks_model1.py:52-55)         */
+  double action_high;
+  int64_t capacity;           /* ReplayBuffer(capacity=1e6) (replay_buffer.py:7)  */
+  double per_alpha;           /* 0.6   (replay_buffer.py:26)                      */
+  double per_beta_start;      /* 0.4                                             */
+  double per_beta_frames;     /* 1e5                                             */
+  uint64_t seed;              /* Philox seed for the policy noise (perf mode)     */
+} sacmi_config;
+
+typedef struct sacmi_ctx sacmi_ctx;
+
+/* Tensor ids for get/set.  Layout of every tensor is the reference nn.Linear /
+ * optimizer layout: weight [out, in] row-major, bias [out]. */
+enum sacmi_net { SACMI_POLICY = 0, SACMI_Q1 = 1, SACMI_Q2 = 2, SACMI_Q1_TARGET = 3,
+                 SACMI_Q2_TARGET = 4 };
+enum sacmi_slot { SACMI_SLOT_PARAM = 0, SACMI_SLOT_GRAD = 1, SACMI_SLOT_ADAM_M = 2,
+                  SACMI_SLOT_ADAM_V = 3 };
+/* layer index inside a net: policy {0: fc1, 1: fc2, 2: mean, 3: log_std};
+ * q {0: fc1, 1: fc2, 2: fc3};  part: 0 = weight, 1 = bias. */
+
+/* scalar ids for get/set_scalar */
+enum sacmi_scalar {
+  SACMI_S_LOG_ALPHA = 0,       /* log_alpha (sac_imp.py:48)                          */
+  SACMI_S_ALPHA = 1,           /* current alpha (0.2 float before the 1st update)    */
+  SACMI_S_ALPHA_IS_TENSOR = 2, /* 1 once alpha = log_alpha.exp() (sac_imp.py:135)   */
+  SACMI_S_STEP_POLICY = 3,     /* Adam 'step' of each optimizer                     */
+  SACMI_S_STEP_Q1 = 4,
+  SACMI_S_STEP_Q2 = 5,
+  SACMI_S_STEP_ALPHA = 6,
+  SACMI_S_ADAM_M_LOG_ALPHA = 7,
+  SACMI_S_ADAM_V_LOG_ALPHA = 8,
+  SACMI_S_GRAD_LOG_ALPHA = 9,
+  SACMI_S_PER_FRAME = 10,      /* PrioritizedReplayBuffer.frame (replay_buffer.py:31) */
+  SACMI_S_NOISE_COUNTER = 11,  /* Philox counter (updates drawn so far)             */
+  SACMI_S_COUNT = 12
+};
+
+/* ---- lifecycle ---------------------------------------------------------------- */
+int sacmi_abi_version(void);
+const char* sacmi_last_error(void);
+int sacmi_device_count(int* n);
+int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out);
+int sacmi_destroy(sacmi_ctx* ctx);
+/* Order all work on an external HIP stream (e.g. torch's current stream), passed
+ * as an opaque pointer; NULL returns to the context's own stream. */
+int sacmi_set_stream(sacmi_ctx* ctx, void* hip_stream);
+int sacmi_synchronize(sacmi_ctx* ctx);
+
+/* ---- parameters / optimizer state (state_dict bridge) ------------------------ */
+int sacmi_tensor_numel(sacmi_ctx* ctx, int net, int layer, int part, int64_t* numel);
+int sacmi_set_tensor(sacmi_ctx* ctx, int slot, int net, int layer, int part,
+                     const float* host, int64_t numel);
+int sacmi_get_tensor(sacmi_ctx* ctx, int slot, int net, int layer, int part,
+                     float* host, int64_t numel);
+int sacmi_set_scalar(sacmi_ctx* ctx, int which, double value);
+int sacmi_get_scalar(sacmi_ctx* ctx, int which, double* value);
+
+/* ---- replay (HBM ring, SoA) ----------------------------------------------------- */
+/* Append n transitions (copy-in).  s,s2: [n,S] f32; a: [n,A] f32; r: [n] f32;
+ * d: [n] u8.  Oldest rows are evicted past capacity (deque(maxlen)).  For PER the
+ * new rows get max(priorities) (or 1.0 when empty), replay_buffer.py:36-46. */
+int sacmi_push(sacmi_ctx* ctx, const float* s, const float* a, const float* r,
+               const float* s2, const uint8_t* d, int64_t n);
+int sacmi_len(sacmi_ctx* ctx, int64_t* n);
+/* Copy rows at deque positions idx[0..n) out (materialises ReplayBuffer.buffer). */
+int sacmi_get_rows(sacmi_ctx* ctx, const int64_t* idx, int64_t n, float* s, float* a,
+                   float* r, float* s2, uint8_t* d);
+
+/* ---- RNG bridges ----------------------------------------------------------------- */
+/* stream 0 = CPython `random` (uniform indices), stream 1 = numpy legacy
+ * RandomState (PER).  key: 624 words, pos: index 0..624. */
+int sacmi_rng_set_mt(sacmi_ctx* ctx, int stream, const uint32_t* key, int32_t pos);
+int sacmi_rng_get_mt(sacmi_ctx* ctx, int stream, uint32_t* key, int32_t* pos);
+
+/* random.sample(buffer, batch) positions, drawn on the GPU from stream 0 (advances it). */
+int sacmi_sample_indices(sacmi_ctx* ctx, int32_t batch, int64_t* idx_out);
+
+/* ---- the gradient step ----------------------------------------------------------- */
+/* One update_parameters(batch): sample (uniform: device MT stream 0 unless idx is
+ * given), gather, target, twin-critic step, actor step, alpha step, Polyak.
+ * idx:  NULL -> draw on device; else [batch] deque positions.
+ * eps1, eps2: NULL -> on-device Philox noise; else [batch, A] standard normals
+ *   (eps1 for policy.sample(next_state), eps2 for policy.sample(state)).
+ * losses_out (may be NULL): {q1_loss, q2_loss, policy_loss} — synchronises. */
+int sacmi_step(sacmi_ctx* ctx, int32_t batch, const int64_t* idx, const float* eps1,
+               const float* eps2, float* losses_out);
+/* Same work, enqueued only (no host sync, no host writes); losses stay on device
+ * in a ring of `ring` slots, fetched by sacmi_fetch_losses. */
+int sacmi_step_async(sacmi_ctx* ctx, int32_t batch);
+int sacmi_fetch_losses(sacmi_ctx* ctx, float* out, int32_t max_steps, int32_t* n_out);
+
+/* Data-parallel split of the step (one process per GPU).  phase 0: sample, gather,
+ * forward, critic backward -> critic gradient buffer; phase 1: critic Adam + Polyak,
+ * actor forward/backward -> actor gradient buffer; phase 2: actor Adam + alpha.
+ * Between phases the caller all-reduces (sum) the buffer named by
+ * sacmi_grad_buffer(which=0 critic, 1 actor); grad_scale (1/world) is applied by the
+ * Adam kernels. */
+int sacmi_step_phase(sacmi_ctx* ctx, int32_t batch, int32_t phase, float grad_scale);
+int sacmi_grad_buffer(sacmi_ctx* ctx, int which, void** device_ptr, int64_t* numel);
+
+/* ---- prioritized replay ------------------------------------------------------------ */
+/* PrioritizedReplayBuffer.sample(batch) indices + IS weights; u: NULL -> draw from
+ * MT stream 1 on device, else [min(batch,len)] uniforms in [0,1).  Advances frame. */
+int sacmi_per_sample(sacmi_ctx* ctx, int32_t batch, const double* u, int64_t* idx_out,
+                     float* weights_out);
+int sacmi_per_update(sacmi_ctx* ctx, const int64_t* idx, const float* prio, int64_t n);
+int sacmi_per_get_priorities(sacmi_ctx* ctx, float* out, int64_t n);
+int sacmi_per_set_priorities(sacmi_ctx* ctx, const float* in, int64_t n);
+
+/* ---- action selection (sac_imp.py:54-72) ----------------------------------------- */
+/* n states [n,S] -> actions [n,A]; deterministic: tanh(mean)*scale+bias;
+ * else policy.sample with eps [n,A] (NULL -> Philox). */
+int sacmi_act(sacmi_ctx* ctx, const float* s, int32_t n, int32_t deterministic,
+              const float* eps, float* a_out);
+
+/* ---- diagnostics ------------------------------------------------------------------ */
+/* Run `iters` eager (non-graph) updates with a HIP event recorded on the context's
+ * stream between consecutive kernel launches; returns, per launch site, its name
+ * (32 bytes each, NUL-padded), the mean duration in ms and the algorithmic FLOPs of
+ * one launch (GEMM sites; 0 elsewhere).  The model state advances as in sacmi_step. */
+int sacmi_profile_step(sacmi_ctx* ctx, int32_t batch, int32_t iters, char* names_out,
+                       float* ms_out, double* flops_out, int32_t max_sites, int32_t* n_sites);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SACMI_H_ */

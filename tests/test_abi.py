@@ -1,0 +1,68 @@
+"""CPU checks of the drop-in boundary: libsacmi.so loads and exports exactly the
+C ABI declared in include/sacmi.h (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "sacmi.h")
+LIB = os.path.join(ROOT, "humanoid-walking-with-sac_amd", "sacmi", "libsacmi.so")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(sacmi_\w+)\s*\(", text, re.M)))
+
+
+def test_library_built():
+    assert os.path.exists(LIB), "run __graft_entry__.build() / make first"
+
+
+def test_exports_every_header_symbol():
+    funcs = header_functions()
+    assert len(funcs) >= 25
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (sacmi_\w+)", out))
+    missing = [f for f in funcs if f not in exported]
+    assert not missing, missing
+    extra = sorted(e for e in exported if e not in funcs)
+    assert not extra, f"exported but undeclared: {extra}"
+
+
+def test_python_bridge_matches_header():
+    from sacmi import _lib as L
+    assert set(L.EXPORTS) == set(header_functions())
+
+
+def test_abi_version_and_error_string():
+    from sacmi import _lib as L
+    lib = L.load()
+    assert lib.sacmi_abi_version() == L.ABI_VERSION
+    assert isinstance(lib.sacmi_last_error(), bytes)
+
+
+def test_config_struct_layout_matches_header():
+    """The ctypes mirror must have the C struct's size (checked with gcc)."""
+    from sacmi import _lib as L
+    src = ('#include "sacmi.h"\n#include <stdio.h>\n'
+           'int main(){printf("%zu\\n", sizeof(sacmi_config));return 0;}\n')
+    tmp = os.path.join("/tmp", "sacmi_sizeof.c")
+    exe = os.path.join("/tmp", "sacmi_sizeof")
+    open(tmp, "w").write(src)
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), tmp, "-o", exe], check=True)
+    size = int(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
+    assert size == ctypes.sizeof(L.SacmiConfig)
+
+
+def test_no_device_is_a_loud_error():
+    """Without a GPU the product path must fail loudly (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from sacmi import Config, Context
+    with pytest.raises(Exception):
+        Context(Config(4, 2, 16, max_batch=8, capacity=64))

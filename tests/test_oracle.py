@@ -1,0 +1,107 @@
+"""Pin the CPU oracle to the reference's own outputs (tests/golden/*.npz, produced by
+tools/make_golden.py running the reference in the build container)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import per as P
+from oracle.pyrandom import MT19937, random_samples, sample_indices, sample_setsize
+from oracle.sac_step import NETS, OracleSAC, SacConfig, init_params, synthetic_rows
+
+
+def _z(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def test_uniform_indices_bitexact(golden_dir):
+    z = _z(golden_dir, "idx_uniform.npz")
+    for c, (seed, n, k) in enumerate(z["cases"]):
+        mt = MT19937(z[f"c{c}.key"], int(z[f"c{c}.pos"]))
+        idx = sample_indices(mt, int(n), int(k))
+        assert np.array_equal(idx, z[f"c{c}.idx"]), (seed, n, k)
+        assert mt.pos == int(z[f"c{c}.post_pos"])
+        assert np.array_equal(mt.key, z[f"c{c}.post_key"])
+
+
+def test_sample_errors_like_reference():
+    mt = MT19937(np.arange(624, dtype=np.uint32), 624)
+    with pytest.raises(ValueError, match="Sample larger than population"):
+        sample_indices(mt, 10, 11)
+    assert sample_setsize(256) == 1045 and sample_setsize(4096) == 16405
+
+
+def test_numpy_random_sample_bridge():
+    np.random.seed(5)
+    st = np.random.get_state()
+    ref = np.random.random_sample(9)
+    mt = MT19937.from_npstate(st)
+    assert np.array_equal(random_samples(mt, 9), ref)
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 127, 128, 129, 1000, 8191, 8192, 8193, 70001])
+def test_pairwise_sum_matches_numpy(n):
+    a = (np.random.default_rng(n).uniform(0, 2, n).astype(np.float32)) ** np.float32(0.6)
+    assert P.pairwise_sum_f32(a) == a.sum()
+
+
+def test_per_oracle_bitexact(golden_dir):
+    z = _z(golden_dir, "per.npz")
+    for c, (seed, n, batch, cap) in enumerate(z["cases"]):
+        L = min(int(n), int(cap))
+        probs = P.probs_from(z[f"c{c}.prio_before"], L)
+        assert np.array_equal(probs, z[f"c{c}.probs"])
+        mt = MT19937(z[f"c{c}.np_key"], int(z[f"c{c}.np_pos"]))
+        idx, w = P.sample_from_probs(probs, int(batch), mt, P.beta_at(int(z[f"c{c}.frame"])))
+        assert np.array_equal(idx, z[f"c{c}.idx"])
+        assert np.array_equal(w, z[f"c{c}.weights"])
+        assert mt.pos == int(z[f"c{c}.np_post_pos"])
+        up = P.update_priorities(z[f"c{c}.prio_before"], idx, z[f"c{c}.upd_prio"])
+        assert np.array_equal(up, z[f"c{c}.prio_after"])
+        pushed, pos, _ = P.push_priority(up, L, (int(n)) % int(cap), int(cap))
+        assert np.array_equal(pushed, z[f"c{c}.prio_after_push"])
+        assert pos == int(z[f"c{c}.pos_after_push"])
+
+
+def _golden_params(z, cfg):
+    from oracle.sac_step import param_shapes
+    return {n: {k: z[f"in.{n}.{k}"] for k in param_shapes(cfg)[n]} for n in NETS}
+
+
+def test_oracle_fp32_bitexact_small(golden_dir):
+    z = _z(golden_dir, "step_small.npz")
+    S, A, H, B, N = (int(x) for x in z["cfg"])
+    cfg = SacConfig(S, A, H)
+    orc = OracleSAC(cfg, _golden_params(z, cfg), dtype=torch.float32)
+    rows = [z[f"rows.{k}"] for k in ("s", "a", "r", "s2", "d")]
+    for t in range(2):
+        mt = MT19937(z[f"step{t}.mt_key"], int(z[f"step{t}.mt_pos"]))
+        idx = sample_indices(mt, N, B)
+        assert np.array_equal(idx, z[f"step{t}.idx"])
+        L = orc.step(*[x[idx] for x in rows], z[f"step{t}.eps1"], z[f"step{t}.eps2"])
+        assert np.array_equal([L["q1_loss"], L["q2_loss"], L["policy_loss"]], z[f"step{t}.losses"])
+        st = orc.state()
+        for k in z.files:
+            if k.startswith(f"step{t}.out."):
+                assert np.array_equal(st[k[len(f"step{t}.out."):]], z[k]), k
+
+
+def test_oracle_fp32_bitexact_humanoid(golden_dir):
+    z = _z(golden_dir, "step_humanoid.npz")
+    S, A, H, B, N = (int(x) for x in z["cfg"])
+    cfg = SacConfig(S, A, H)
+    ps, rs = (int(x) for x in z["seeds"])
+    params = init_params(cfg, ps, float(z["bias_scale"]))
+    rows = synthetic_rows(cfg, N, rs, float(z["state_scale"]))
+    orc = OracleSAC(cfg, params, dtype=torch.float32)
+    stride = int(z["stride"])
+    for t in range(2):
+        idx = z[f"step{t}.idx"]
+        L = orc.step(*[x[idx] for x in rows], z[f"step{t}.eps1"], z[f"step{t}.eps2"])
+        assert np.array_equal([L["q1_loss"], L["q2_loss"], L["policy_loss"]], z[f"step{t}.losses"])
+        st = orc.state()
+        for k in z.files:
+            pre = f"step{t}.sample."
+            if k.startswith(pre):
+                assert np.array_equal(st[k[len(pre):]].reshape(-1)[::stride], z[k]), k
