@@ -22,6 +22,8 @@ namespace sacmi {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+constexpr int kGemmKsplit = 8;
+
 #define HIP_LAUNCH_CHECK()                                                          \
   do {                                                                              \
     hipError_t e_ = hipGetLastError();                                              \
@@ -76,8 +78,33 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 }
 
 // Each wave accumulates chunks wave, wave+KSPLIT, ... of a TM x TN tile and writes
-// its partial sums to red[wave][TM][TN+1].
-template <int TM, int TN, int KSPLIT>
+// its partial sums to red[wave][TM][TN+1].  At batch 256 every operand read is a
+// dependent L2/MALL round trip (~1 us), so the wave issues the loads of G chunks at
+// once and double-buffers whole groups: up to 2G chunks are in flight while the
+// MFMAs of the previous group run.
+template <int MT, int NT, int G>
+__device__ __forceinline__ void load_group(const GemmDesc& d, int m0, int n0, int wave, int ks,
+                                           int j0, int nmine, int lane, float (&a)[G][MT][4],
+                                           float (&b)[G][NT][4]) {
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (j0 + g < nmine) {
+      const int k0 = (wave + (j0 + g) * ks) * 16;
+      fetch_op<MT>(d.A, d.lda, d.a_kc, m0, d.M, k0, d.K, lane, a[g]);
+      fetch_op<NT>(d.B, d.ldb, d.b_kc, n0, d.N, k0, d.K, lane, b[g]);
+    }
+  }
+}
+
+template <int MT, int NT, int G>
+__device__ __forceinline__ void mfma_group(f4 (&acc)[MT][NT], int j0, int nmine,
+                                           const float (&a)[G][MT][4], const float (&b)[G][NT][4]) {
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    if (j0 + g < nmine) mfma_chunk<MT, NT>(acc, a[g], b[g]);
+}
+
+template <int TM, int TN, int KSPLIT, int G = 2>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red) {
   constexpr int MT = TM / 16, NT = TN / 16;
   const int lane = threadIdx.x & 63;
@@ -89,36 +116,28 @@ __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, flo
     for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int nch = (d.K + 15) >> 4;
-  float a0[MT][4], b0[NT][4], a1[MT][4], b1[NT][4];
-  int c = wave;
-  if (c < nch) {
-    fetch_op<MT>(d.A, d.lda, d.a_kc, m0, d.M, c * 16, d.K, lane, a0);
-    fetch_op<NT>(d.B, d.ldb, d.b_kc, n0, d.N, c * 16, d.K, lane, b0);
-  }
+  const int nmine = nch > wave ? (nch - wave + KSPLIT - 1) / KSPLIT : 0;
+  float a0[G][MT][4], b0[G][NT][4], a1[G][MT][4], b1[G][NT][4];
+  int j = 0;
+  load_group<MT, NT, G>(d, m0, n0, wave, KSPLIT, 0, nmine, lane, a0, b0);
   for (;;) {
-    if (c >= nch) break;
-    if (c + KSPLIT < nch) {
-      fetch_op<MT>(d.A, d.lda, d.a_kc, m0, d.M, (c + KSPLIT) * 16, d.K, lane, a1);
-      fetch_op<NT>(d.B, d.ldb, d.b_kc, n0, d.N, (c + KSPLIT) * 16, d.K, lane, b1);
-    }
-    mfma_chunk<MT, NT>(acc, a0, b0);
-    c += KSPLIT;
-    if (c >= nch) break;
-    if (c + KSPLIT < nch) {
-      fetch_op<MT>(d.A, d.lda, d.a_kc, m0, d.M, (c + KSPLIT) * 16, d.K, lane, a0);
-      fetch_op<NT>(d.B, d.ldb, d.b_kc, n0, d.N, (c + KSPLIT) * 16, d.K, lane, b0);
-    }
-    mfma_chunk<MT, NT>(acc, a1, b1);
-    c += KSPLIT;
+    if (j >= nmine) break;
+    load_group<MT, NT, G>(d, m0, n0, wave, KSPLIT, j + G, nmine, lane, a1, b1);
+    mfma_group<MT, NT, G>(acc, j, nmine, a0, b0);
+    j += G;
+    if (j >= nmine) break;
+    load_group<MT, NT, G>(d, m0, n0, wave, KSPLIT, j + G, nmine, lane, a0, b0);
+    mfma_group<MT, NT, G>(acc, j, nmine, a1, b1);
+    j += G;
   }
   float* my = red + wave * TM * (TN + 1);
   const int rq = (lane >> 4) * 4, cc = lane & 15;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int jj = 0; jj < NT; ++jj)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) my[(i * 16 + rq + r) * (TN + 1) + j * 16 + cc] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) my[(i * 16 + rq + r) * (TN + 1) + jj * 16 + cc] = acc[i][jj][r];
 }
 
 template <int TM, int TN, int KSPLIT>
@@ -132,7 +151,7 @@ __device__ __forceinline__ float reduce_partials(const float* red, int row, int 
 // ---------------------------------------------------------------------------
 // grouped GEMM: one launch runs every independent GEMM of one dependency level
 template <int TM, int TN, int KSPLIT>
-__global__ __launch_bounds__(64 * KSPLIT) void k_gemm(GemmBatch batch) {
+__global__ __launch_bounds__(64 * KSPLIT, 4) void k_gemm(GemmBatch batch) {
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   const int bid = blockIdx.x;
   int p = 0;
@@ -156,7 +175,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm(GemmBatch batch) {
 
 void launch_gemm(const GemmBatch& b, hipStream_t s) {
   if (b.count == 0) return;
-  hipLaunchKernelGGL((k_gemm<32, 32, 4>), dim3(b.total_tiles), dim3(256), 0, s, b);
+  hipLaunchKernelGGL((k_gemm<32, 32, kGemmKsplit>), dim3(b.total_tiles), dim3(64 * kGemmKsplit), 0, s, b);
   HIP_LAUNCH_CHECK();
 }
 
@@ -243,11 +262,11 @@ void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {
   const int grid = (a.rows + 15) / 16;
   const int n = 2 * a.A;
   if (n <= 32)
-    hipLaunchKernelGGL((k_heads_sample<32, 4>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_heads_sample<32, 16>), dim3(grid), dim3(1024), 0, s, a);
   else if (n <= 48)
-    hipLaunchKernelGGL((k_heads_sample<48, 4>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_heads_sample<48, 16>), dim3(grid), dim3(1024), 0, s, a);
   else
-    hipLaunchKernelGGL((k_heads_sample<64, 4>), dim3(grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_heads_sample<64, 16>), dim3(grid), dim3(1024), 0, s, a);
   HIP_LAUNCH_CHECK();
 }
 
@@ -288,8 +307,8 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
 }
 
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s) {
-  const int grid = (d.M + 31) / 32;
-  hipLaunchKernelGGL((k_gemm_sample_bwd<32, 32, 4>), dim3(grid), dim3(256), 0, s, d, a);
+  const int grid = (d.M + 15) / 16;
+  hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16>), dim3(grid), dim3(1024), 0, s, d, a);
   HIP_LAUNCH_CHECK();
 }
 
@@ -300,16 +319,27 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// dot(h~[row], w~) over K4 float4 chunks, one wave
-__device__ __forceinline__ float wave_dot(const float* __restrict__ h, const float* __restrict__ w,
-                                          int K4, int lane) {
-  float s = 0.f;
+// NV simultaneous dots h_v . w_v over K4 float4 chunks, one wave; every load of the
+// row is issued before any reduction (one latency instead of NV).
+template <int NV>
+__device__ __forceinline__ void wave_dots(const float* const (&h)[NV], const float* const (&w)[NV],
+                                          int K4, int lane, float (&out)[NV]) {
+  float s[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) s[v] = 0.f;
+#pragma unroll 3
   for (int q = lane; q < K4; q += 64) {
-    const float4 x = reinterpret_cast<const float4*>(h)[q];
-    const float4 y = reinterpret_cast<const float4*>(w)[q];
-    s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    float4 x[NV], y[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      x[v] = reinterpret_cast<const float4*>(h[v])[q];
+      y[v] = reinterpret_cast<const float4*>(w[v])[q];
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) s[v] += x[v].x * y[v].x + x[v].y * y[v].y + x[v].z * y[v].z + x[v].w * y[v].w;
   }
-  return wave_sum(s);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) out[v] = wave_sum(s[v]);
 }
 
 // Target + critic loss rows (sac_imp.py:87-105 forward tail, mse backward).
@@ -331,10 +361,11 @@ __global__ __launch_bounds__(256) void k_critic_rows(CriticRowsArgs a) {
     const float* h2 = h1 + a.ldh;
     const float* t1 = a.hqt2 + (size_t)b * 2 * a.ldh;
     const float* t2 = t1 + a.ldh;
-    const float q1 = wave_dot(h1, a.w3, K4, lane);
-    const float q2 = wave_dot(h2, a.w3 + a.w3_stride, K4, lane);
-    const float qt1 = wave_dot(t1, a.w3t, K4, lane);
-    const float qt2 = wave_dot(t2, a.w3t + a.w3_stride, K4, lane);
+    const float* const hv[4] = {h1, h2, t1, t2};
+    const float* const wv[4] = {a.w3, a.w3 + a.w3_stride, a.w3t, a.w3t + a.w3_stride};
+    float dv[4];
+    wave_dots<4>(hv, wv, K4, lane, dv);
+    const float q1 = dv[0], q2 = dv[1], qt1 = dv[2], qt2 = dv[3];
     const float vt = fminf(qt1, qt2) - alpha * a.logp_t[b];
     const float qhat = a.r[b] + ((1.f - a.d[b]) * a.gamma) * vt;
     e1 = q1 - qhat;
@@ -388,8 +419,11 @@ __global__ __launch_bounds__(256) void k_actor_rows(ActorRowsArgs a) {
   if (b < a.B) {
     const float* h1 = a.hqa2 + (size_t)b * 2 * a.ldh;
     const float* h2 = h1 + a.ldh;
-    const float q1 = wave_dot(h1, a.w3, K4, lane);
-    const float q2 = wave_dot(h2, a.w3 + a.w3_stride, K4, lane);
+    const float* const hv[2] = {h1, h2};
+    const float* const wv[2] = {a.w3, a.w3 + a.w3_stride};
+    float dv[2];
+    wave_dots<2>(hv, wv, K4, lane, dv);
+    const float q1 = dv[0], q2 = dv[1];
     const float qmin = fminf(q1, q2);
     lpart = alpha * a.logp_a[b] - qmin;
     const float g = -1.f / (float)a.B;
@@ -422,78 +456,112 @@ void launch_actor_rows(const ActorRowsArgs& a, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // Adam (torch.optim.Adam single-tensor semantics, torch optim/adam.py) over the
-// flat arena + optional Polyak target update (sac_imp.py:146-152) + loss
-// finalisation + alpha = exp(log_alpha) (sac_imp.py:135).
+// flat arena, 4 elements per thread-iteration (every segment is a multiple of 4 floats
+// and 16-byte aligned), + optional Polyak target update (sac_imp.py:146-152) + loss
+// finalisation + the scalar log_alpha step and alpha = exp(log_alpha)
+// (sac_imp.py:128-135) + the loss ring slot of this update.
+struct AdamScalars { float step_size, bc2_sqrt; };
+
+// t*(1-tau) + p*tau as three separately rounded fp32 ops, like the reference's tensor
+// expression (sac_imp.py:149) — no FMA contraction, so the result is bit-exact.
+__device__ __forceinline__ float polyak(float t, float p, float omtau, float tau) {
+#pragma clang fp contract(off)
+  const float a = t * omtau;
+  const float b = p * tau;
+  return a + b;
+}
+
+__device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, int step_idx) {
+  const double t = a.sc->step[step_idx] + (double)a.step_offset;
+  const double bc1 = 1.0 - pow((double)a.beta1, t);
+  const double bc2 = 1.0 - pow((double)a.beta2, t);
+  return AdamScalars{(float)((double)a.lr / bc1), (float)sqrt(bc2)};
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float om_b1,
+                                          float b2, float om_b2, float eps, AdamScalars k) {
+  m = m + om_b1 * (g - m);
+  v = v * b2;
+  v = v + om_b2 * g * g;
+  const float denom = sqrtf(v) / k.bc2_sqrt + eps;
+  p = p + (-k.step_size * m) / denom;
+}
+
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
-  __shared__ float s_step_size[4], s_bc2_sqrt[4];
-  __shared__ int64_t s_prefix[5];
-  if (threadIdx.x < a.nseg) {
-    const double t = a.sc->step[a.seg[threadIdx.x].step_idx] + (double)a.step_offset;
-    const double bc1 = 1.0 - pow((double)a.beta1, t);
-    const double bc2 = 1.0 - pow((double)a.beta2, t);
-    s_step_size[threadIdx.x] = (float)((double)a.lr / bc1);
-    s_bc2_sqrt[threadIdx.x] = (float)sqrt(bc2);
-  }
+  __shared__ AdamScalars s_k[kMaxAdamSegs];
+  __shared__ int64_t s_prefix[kMaxAdamSegs + 1];
+  if (threadIdx.x < a.nseg) s_k[threadIdx.x] = adam_scalars(a, a.seg[threadIdx.x].step_idx);
   if (threadIdx.x == 0) {
     int64_t p = 0;
-    for (int i = 0; i < a.nseg; ++i) { s_prefix[i] = p; p += a.seg[i].n; }
+    for (int i = 0; i < a.nseg; ++i) { s_prefix[i] = p; p += a.seg[i].n / 4; }
     s_prefix[a.nseg] = p;
   }
   __syncthreads();
-  const float om_b1 = 1.f - a.beta1;
-  const float om_b2 = 1.f - a.beta2;
-  const float omtau = 1.f - a.tau;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.total;
+  const float om_b1 = 1.f - a.beta1, om_b2 = 1.f - a.beta2, omtau = 1.f - a.tau;
+  const int64_t total4 = s_prefix[a.nseg];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total4;
        e += (int64_t)gridDim.x * blockDim.x) {
     int sg = 0;
     for (int q = 1; q < a.nseg; ++q)
       if (e >= s_prefix[q]) sg = q;
-    const int64_t i = a.seg[sg].off + (e - s_prefix[sg]);
-    const float g = a.g[i] * a.grad_scale;
-    float m = a.m[i];
-    m = m + om_b1 * (g - m);
-    float v = a.v[i] * a.beta2;
-    v = v + om_b2 * g * g;
-    const float denom = sqrtf(v) / s_bc2_sqrt[sg] + a.eps;
-    const float p = a.p[i] + (-s_step_size[sg] * m) / denom;
-    a.m[i] = m; a.v[i] = v; a.p[i] = p;
+    const int64_t i = a.seg[sg].off + 4 * (e - s_prefix[sg]);
+    const AdamScalars k = s_k[sg];
+    float4 g = *reinterpret_cast<const float4*>(a.g + i);
+    float4 p = *reinterpret_cast<const float4*>(a.p + i);
+    float4 m = *reinterpret_cast<const float4*>(a.m + i);
+    float4 v = *reinterpret_cast<const float4*>(a.v + i);
+    g.x *= a.grad_scale; g.y *= a.grad_scale; g.z *= a.grad_scale; g.w *= a.grad_scale;
+    adam_elem(p.x, m.x, v.x, g.x, om_b1, a.beta2, om_b2, a.eps, k);
+    adam_elem(p.y, m.y, v.y, g.y, om_b1, a.beta2, om_b2, a.eps, k);
+    adam_elem(p.z, m.z, v.z, g.z, om_b1, a.beta2, om_b2, a.eps, k);
+    adam_elem(p.w, m.w, v.w, g.w, om_b1, a.beta2, om_b2, a.eps, k);
+    *reinterpret_cast<float4*>(a.p + i) = p;
+    *reinterpret_cast<float4*>(a.m + i) = m;
+    *reinterpret_cast<float4*>(a.v + i) = v;
     if (a.tgt) {
-      float* t = a.tgt + (i - a.tgt_base);
-      *t = __fadd_rn(__fmul_rn(*t, omtau), __fmul_rn(p, a.tau));
-    }
-    if (i == a.log_alpha_idx && a.auto_entropy) {
-      a.sc->alpha = expf(p);
-      a.sc->alpha_is_tensor = 1;
+      float4* tp = reinterpret_cast<float4*>(a.tgt + (i - a.tgt_base));
+      float4 t = *tp;
+      t.x = polyak(t.x, p.x, omtau, a.tau);
+      t.y = polyak(t.y, p.y, omtau, a.tau);
+      t.z = polyak(t.z, p.z, omtau, a.tau);
+      t.w = polyak(t.w, p.w, omtau, a.tau);
+      *tp = t;
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x < a.n_losses) {
+  if (blockIdx.x != 0) return;
+  if (threadIdx.x == 0 && a.log_alpha_idx >= 0 && a.auto_entropy) {
+    const AdamScalars k = adam_scalars(a, 3);
+    const int64_t i = a.log_alpha_idx;
+    float p = a.p[i], m = a.m[i], v = a.v[i];
+    adam_elem(p, m, v, a.g[i] * a.grad_scale, om_b1, a.beta2, om_b2, a.eps, k);
+    a.p[i] = p; a.m[i] = m; a.v[i] = v;
+    a.sc->alpha = expf(p);
+    a.sc->alpha_is_tensor = 1;
+  }
+  if (threadIdx.x < a.n_losses) {
     float s = 0.f;
     for (int w = 0; w < a.n_part; ++w) s += a.loss_part[w * a.n_losses + threadIdx.x];
     a.sc->losses[a.loss_slot0 + threadIdx.x] = s / a.loss_div;
   }
-}
-
-// Loss ring: copies the three losses of this update into slot (pos % ring).
-__global__ void k_loss_ring(DevScalars* sc, float* ring, int nring) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    const int64_t p = sc->loss_ring_pos % nring;
-    ring[p * 3 + 0] = sc->losses[0];
-    ring[p * 3 + 1] = sc->losses[1];
-    ring[p * 3 + 2] = sc->losses[2];
-    sc->loss_ring_pos += 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && a.loss_ring) {
+    const int64_t pos = a.sc->loss_ring_pos;
+    const int64_t q = pos % a.ring;
+    a.loss_ring[q * 3 + 0] = a.sc->losses[0];
+    a.loss_ring[q * 3 + 1] = a.sc->losses[1];
+    a.loss_ring[q * 3 + 2] = a.sc->losses[2];
+    a.sc->loss_ring_pos = pos + 1;
   }
 }
 
 void launch_adam(const AdamArgs& a, hipStream_t s) {
-  int64_t blocks = (a.total + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  int64_t total4 = 0;
+  for (int i = 0; i < a.nseg; ++i) total4 += a.seg[i].n / 4;
+  int64_t blocks = (total4 + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, s, a);
   HIP_LAUNCH_CHECK();
-  if (a.loss_ring) {
-    hipLaunchKernelGGL(k_loss_ring, dim3(1), dim3(64), 0, s, a.sc, a.loss_ring, a.ring);
-    HIP_LAUNCH_CHECK();
-  }
 }
 
 // ---------------------------------------------------------------------------

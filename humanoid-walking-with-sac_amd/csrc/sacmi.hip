@@ -36,6 +36,13 @@ struct Error {
     if (!(cond)) throw Error{code, (msg)}; \
   } while (0)
 
+// every device allocation of the process, for the host-side bounds validator
+struct AllocRec { uintptr_t base; size_t bytes; };
+static std::vector<AllocRec>& alloc_registry() {
+  static std::vector<AllocRec> r;
+  return r;
+}
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -44,10 +51,17 @@ struct DevBuf {
     n = count;
     if (count) {
       CHECK_HIP(hipMalloc(&p, count * sizeof(T)));
+      // null-stream memset: the context stream is non-blocking, so wait for the
+      // zero-fill before anything is enqueued there (init writes the 1-columns).
       CHECK_HIP(hipMemset(p, 0, count * sizeof(T)));
+      CHECK_HIP(hipDeviceSynchronize());
+      alloc_registry().push_back({(uintptr_t)p, count * sizeof(T)});
     }
   }
   void release() {
+    auto& reg = alloc_registry();
+    for (size_t i = 0; i < reg.size(); ++i)
+      if (reg[i].base == (uintptr_t)p) { reg.erase(reg.begin() + i); break; }
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
@@ -249,9 +263,40 @@ static GemmDesc gd(const float* A, int lda, int a_kc, const float* B, int ldb, i
   return d;
 }
 
+// Host-side bounds check of one GEMM before it is ever launched: every element the
+// kernel can touch (incl. the 16-byte over-read of K-contiguous fetches) must lie in
+// one registered allocation, and vector-loaded operands must be 16-byte aligned.
+static void check_span(const void* p, int64_t max_index, const char* what) {
+  if (!p) throw Error{SACMI_ESTATE, std::string("null GEMM operand ") + what};
+  const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)(max_index + 1) * 4;
+  for (const AllocRec& r : alloc_registry())
+    if (a >= r.base && e <= r.base + r.bytes) return;
+  throw Error{SACMI_ESTATE, std::string("GEMM operand out of bounds: ") + what};
+}
+
+static void validate(const GemmDesc& d) {
+  if (d.M <= 0 || d.N <= 0 || d.K <= 0) throw Error{SACMI_ESTATE, "empty GEMM"};
+  const int64_t klast = ((int64_t)(d.K - 1) / 4) * 4 + 3;
+  if (d.a_kc) {
+    if (((uintptr_t)d.A & 15) || (d.lda & 3)) throw Error{SACMI_ESTATE, "A misaligned"};
+    check_span(d.A, (int64_t)(d.M - 1) * d.lda + klast, "A");
+  } else {
+    check_span(d.A, (int64_t)(d.K - 1) * d.lda + d.M - 1, "A");
+  }
+  if (d.b_kc) {
+    if (((uintptr_t)d.B & 15) || (d.ldb & 3)) throw Error{SACMI_ESTATE, "B misaligned"};
+    check_span(d.B, (int64_t)(d.N - 1) * d.ldb + klast, "B");
+  } else {
+    check_span(d.B, (int64_t)(d.K - 1) * d.ldb + d.N - 1, "B");
+  }
+  if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + d.N - 1, "C");
+  if (d.epi == EPI_MASK) check_span(d.aux, (int64_t)(d.M - 1) * d.ldaux + d.N - 1, "aux");
+}
+
 struct Level {
   GemmBatch b{};
   void add(const GemmDesc& d0) {
+    validate(d0);
     if (b.count >= kMaxGemms) throw Error{SACMI_ESTATE, "too many GEMMs in one level"};
     GemmDesc d = d0;
     const int tm = (d.M + 31) / 32, tn = (d.N + 31) / 32;
@@ -381,10 +426,14 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     for (int layer = 0; layer < 3; ++layer)
       for (int i = 0; i < 2; ++i) {
         const Linear& l = q[i][layer];
+        REQUIRE(ad.nseg < kMaxAdamSegs, SACMI_ESTATE, "too many Adam segments");
         ad.seg[ad.nseg++] = AdamSeg{l.off, l.numel_padded(), i == 0 ? 1 : 2};
       }
     ad.total = 0;
-    for (int i = 0; i < ad.nseg; ++i) ad.total += ad.seg[i].n;
+    for (int i = 0; i < ad.nseg; ++i) {
+      REQUIRE(ad.seg[i].n % 4 == 0 && ad.seg[i].off % 4 == 0, SACMI_ESTATE, "Adam segment not float4-aligned");
+      ad.total += ad.seg[i].n;
+    }
     ad.lr = lr; ad.beta1 = 0.9f; ad.beta2 = 0.999f; ad.eps = 1e-8f; ad.grad_scale = grad_scale;
     ad.tau = (float)c->cfg.tau; ad.step_offset = 1; ad.sc = c->sc.p;
     ad.loss_part = c->lpart_c.p; ad.n_part = nb; ad.loss_slot0 = 0; ad.n_losses = 2;
@@ -417,6 +466,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     launch_gemm(l9.b, s);
     // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
     GemmDesc da = gd(c->dha1.p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
+    validate(da);
     SampleBwdArgs sb{};
     sb.cache = c->cache.p + (size_t)B * 3 * A; sb.eps = c->eps.p + (size_t)B * A;
     sb.dhead = c->dhead.p; sb.lddh = c->lddh; sb.A = A; sb.B = B; sb.sc = c->sc.p;
@@ -447,9 +497,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.nseg = 0;
     for (const Linear* l : {&c->p_fc1, &c->p_fc2, &c->p_head})
       ad.seg[ad.nseg++] = AdamSeg{l->off, l->numel_padded(), 0};
-    if (c->cfg.auto_entropy) ad.seg[ad.nseg++] = AdamSeg{c->la_idx, 1, 3};
     ad.total = 0;
-    for (int i = 0; i < ad.nseg; ++i) ad.total += ad.seg[i].n;
+    for (int i = 0; i < ad.nseg; ++i) {
+      REQUIRE(ad.seg[i].n % 4 == 0 && ad.seg[i].off % 4 == 0, SACMI_ESTATE, "Adam segment not float4-aligned");
+      ad.total += ad.seg[i].n;
+    }
     ad.lr = lr; ad.beta1 = 0.9f; ad.beta2 = 0.999f; ad.eps = 1e-8f; ad.grad_scale = grad_scale;
     ad.tau = 0.f; ad.step_offset = 0; ad.sc = c->sc.p;
     ad.loss_part = c->lpart_a.p; ad.n_part = nb; ad.loss_slot0 = 2; ad.n_losses = 1;
@@ -533,6 +585,7 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
     REQUIRE(cfg->state_dim > 0 && cfg->action_dim > 0 && cfg->hidden_dim > 0, SACMI_EVALUE,
             "dims must be positive");
     REQUIRE(cfg->action_dim <= 32, SACMI_EVALUE, "action_dim > 32 not supported");
+    REQUIRE(cfg->hidden_dim % 4 == 0, SACMI_EVALUE, "hidden_dim must be a multiple of 4");
     REQUIRE(cfg->max_batch > 0 && cfg->max_batch <= 65536, SACMI_EVALUE, "bad max_batch");
     REQUIRE(cfg->capacity > 0 && cfg->capacity < (int64_t)1 << 31, SACMI_EVALUE, "bad capacity");
     int ndev = 0;

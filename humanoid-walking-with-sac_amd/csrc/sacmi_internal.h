@@ -149,12 +149,13 @@ struct ActorRowsArgs {
 };
 void launch_actor_rows(const ActorRowsArgs& a, hipStream_t s);
 
+constexpr int kMaxAdamSegs = 8;
 struct AdamSeg { int64_t off, n; int step_idx; };
 struct AdamArgs {
   float* p; const float* g; float* m; float* v;
   float* tgt;              // Polyak target arena (mirrors p from p_tgt_base) or null
   int64_t tgt_base;        // offset subtracted from p index to index tgt
-  int nseg; AdamSeg seg[4];
+  int nseg; AdamSeg seg[kMaxAdamSegs];
   int64_t total;           // sum of seg n (grid-stride domain)
   float lr, beta1, beta2, eps, grad_scale, tau;
   int step_offset;         // t = step[idx] + step_offset

@@ -221,7 +221,7 @@ def test_polyak_bitexact_and_determinism():
         ctx = make_ctx(cfg, max_batch=64, capacity=400)
         load_params(ctx, params)
         ctx.push(*rows)
-        ctx.set_mt(0, np.arange(624, dtype=np.uint32) * 2654435761 % (2**32), 624)
+        ctx.set_mt(0, (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32), 624)
         for _ in range(3):
             before_t = {n: ctx.get_net(n) for n in ("q1_target", "q2_target")}
             ctx.step(64)                           # device indices + device noise

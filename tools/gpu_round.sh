@@ -1,0 +1,24 @@
+#!/bin/bash
+# one GPU session: tests, bench, kernel-trace profile.  Every GPU step is time-limited
+# and chained: the script stops at the first failure.
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out
+MODE=${1:-all}
+if [ "$MODE" = all ] || [ "$MODE" = test ]; then
+  timeout -k 10 500 python -m pytest tests -q -m gpu > $OUT/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest_rc=$rc" >> $OUT/pytest_gpu.log; tail -3 $OUT/pytest_gpu.log
+  [ $rc -ne 0 ] && exit $rc
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  timeout -k 10 500 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
+  rc=$?; cat $OUT/bench.json; [ $rc -ne 0 ] && { tail -20 $OUT/bench.err; exit $rc; }
+fi
+if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+  cd /tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- \
+    python3 $GRAFT_REPO_ROOT/bench.py --profile-only --steps 200 --warmup 20 --fill 200000 > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1
+  rc=$?; echo prof_rc=$rc; [ $rc -ne 0 ] && { tail -20 $GRAFT_REPO_ROOT/$OUT/prof.log; exit $rc; }
+  find $GRAFT_REPO_ROOT/$OUT/prof -name "*stats*"
+fi
