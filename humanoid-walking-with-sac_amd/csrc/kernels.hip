@@ -22,7 +22,6 @@ namespace sacmi {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGemmKsplit = 8;
 
 #define HIP_LAUNCH_CHECK()                                                          \
   do {                                                                              \
@@ -34,19 +33,19 @@ constexpr int kGemmKsplit = 8;
   } while (0)
 
 // ---------------------------------------------------------------------------
-// operand fetch: NT 16-row subtiles x 4 consecutive k (k = k0 + 4g .. +3)
-template <int NT>
-__device__ __forceinline__ void fetch_op(const float* __restrict__ P, int ld, int kc, int row0,
-                                         int nrows, int k0, int K, int lane, float (&v)[NT][4]) {
-  const int r = lane & 15;
-  const int k = k0 + 4 * (lane >> 4);
+// operand fetch: NT 16-row subtiles x 4 consecutive k (k = k0 + 4g .. +3).
+// rp[t] is the lane's row pointer of subtile t (row clamped into range):
+//   KC  (K-contiguous, element (row,k) at rp + k):     one 16-byte load
+//   !KC (row-contiguous, element (row,k) at rp + k*ld): 4 loads, each a coalesced
+//        64-byte segment across the 16 lanes of a lane group.
+template <int NT, bool KC>
+__device__ __forceinline__ void fetch_op(const float* const (&rp)[NT], int ld, int k, int K,
+                                         float (&v)[NT][4]) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    int row = row0 + t * 16 + r;
-    row = row < nrows ? row : nrows - 1;
-    if (kc) {
+    if (KC) {
       if (k < K) {
-        const float4 x = *reinterpret_cast<const float4*>(P + (size_t)row * ld + k);
+        const float4 x = *reinterpret_cast<const float4*>(rp[t] + k);
         v[t][0] = x.x;
         v[t][1] = (k + 1 < K) ? x.y : 0.f;
         v[t][2] = (k + 2 < K) ? x.z : 0.f;
@@ -58,10 +57,21 @@ __device__ __forceinline__ void fetch_op(const float* __restrict__ P, int ld, in
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int kk = (k + s < K) ? (k + s) : (K - 1);
-        const float x = P[(size_t)kk * ld + row];
+        const float x = rp[t][(size_t)kk * ld];
         v[t][s] = (k + s < K) ? x : 0.f;
       }
     }
+  }
+}
+
+template <int NT, bool KC>
+__device__ __forceinline__ void row_ptrs(const float* P, int ld, int row0, int nrows, int lane,
+                                         const float* (&rp)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    int row = row0 + t * 16 + (lane & 15);
+    row = row < nrows ? row : nrows - 1;
+    rp[t] = KC ? P + (size_t)row * ld : P + row;
   }
 }
 
@@ -79,33 +89,11 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 
 // Each wave accumulates chunks wave, wave+KSPLIT, ... of a TM x TN tile and writes
 // its partial sums to red[wave][TM][TN+1].  At batch 256 every operand read is a
-// dependent L2/MALL round trip (~1 us), so the wave issues the loads of G chunks at
-// once and double-buffers whole groups: up to 2G chunks are in flight while the
-// MFMAs of the previous group run.
-template <int MT, int NT, int G>
-__device__ __forceinline__ void load_group(const GemmDesc& d, int m0, int n0, int wave, int ks,
-                                           int j0, int nmine, int lane, float (&a)[G][MT][4],
-                                           float (&b)[G][NT][4]) {
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    if (j0 + g < nmine) {
-      const int k0 = (wave + (j0 + g) * ks) * 16;
-      fetch_op<MT>(d.A, d.lda, d.a_kc, m0, d.M, k0, d.K, lane, a[g]);
-      fetch_op<NT>(d.B, d.ldb, d.b_kc, n0, d.N, k0, d.K, lane, b[g]);
-    }
-  }
-}
-
-template <int MT, int NT, int G>
-__device__ __forceinline__ void mfma_group(f4 (&acc)[MT][NT], int j0, int nmine,
-                                           const float (&a)[G][MT][4], const float (&b)[G][NT][4]) {
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-    if (j0 + g < nmine) mfma_chunk<MT, NT>(acc, a[g], b[g]);
-}
-
-template <int TM, int TN, int KSPLIT, int G = 2>
-__device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red) {
+// dependent L2/MALL round trip (~1-2 us), so a wave issues the loads of G chunks at
+// once (with KSPLIT = 16 waves per workgroup and K <= 528 that is ALL of its chunks:
+// one exposed latency per GEMM) and only then runs their MFMAs.
+template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC>
+__device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red) {
   constexpr int MT = TM / 16, NT = TN / 16;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -114,21 +102,26 @@ __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, flo
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-
+  const float* ra[MT];
+  const float* rb[NT];
+  row_ptrs<MT, AKC>(d.A, d.lda, m0, d.M, lane, ra);
+  row_ptrs<NT, BKC>(d.B, d.ldb, n0, d.N, lane, rb);
   const int nch = (d.K + 15) >> 4;
   const int nmine = nch > wave ? (nch - wave + KSPLIT - 1) / KSPLIT : 0;
-  float a0[G][MT][4], b0[G][NT][4], a1[G][MT][4], b1[G][NT][4];
-  int j = 0;
-  load_group<MT, NT, G>(d, m0, n0, wave, KSPLIT, 0, nmine, lane, a0, b0);
-  for (;;) {
-    if (j >= nmine) break;
-    load_group<MT, NT, G>(d, m0, n0, wave, KSPLIT, j + G, nmine, lane, a1, b1);
-    mfma_group<MT, NT, G>(acc, j, nmine, a0, b0);
-    j += G;
-    if (j >= nmine) break;
-    load_group<MT, NT, G>(d, m0, n0, wave, KSPLIT, j + G, nmine, lane, a0, b0);
-    mfma_group<MT, NT, G>(acc, j, nmine, a1, b1);
-    j += G;
+  const int kl = 4 * (lane >> 4);
+  float a[G][MT][4], b[G][NT][4];
+  for (int j = 0; j < nmine; j += G) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (j + g < nmine) {
+        const int k = (wave + (j + g) * KSPLIT) * 16 + kl;
+        fetch_op<MT, AKC>(ra, d.lda, k, d.K, a[g]);
+        fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (j + g < nmine) mfma_chunk<MT, NT>(acc, a[g], b[g]);
   }
   float* my = red + wave * TM * (TN + 1);
   const int rq = (lane >> 4) * 4, cc = lane & 15;
@@ -140,6 +133,18 @@ __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, flo
       for (int r = 0; r < 4; ++r) my[(i * 16 + rq + r) * (TN + 1) + jj * 16 + cc] = acc[i][jj][r];
 }
 
+// layout dispatch (wave-uniform, once per workgroup)
+template <int TM, int TN, int KSPLIT, int G>
+__device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red) {
+  if (d.a_kc) {
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true>(d, m0, n0, red);
+    else gemm_core_l<TM, TN, KSPLIT, G, true, false>(d, m0, n0, red);
+  } else {
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true>(d, m0, n0, red);
+    else gemm_core_l<TM, TN, KSPLIT, G, false, false>(d, m0, n0, red);
+  }
+}
+
 template <int TM, int TN, int KSPLIT>
 __device__ __forceinline__ float reduce_partials(const float* red, int row, int col) {
   float s = red[row * (TN + 1) + col];
@@ -149,9 +154,10 @@ __device__ __forceinline__ float reduce_partials(const float* red, int row, int 
 }
 
 // ---------------------------------------------------------------------------
-// grouped GEMM: one launch runs every independent GEMM of one dependency level
-template <int TM, int TN, int KSPLIT>
-__global__ __launch_bounds__(64 * KSPLIT, 4) void k_gemm(GemmBatch batch) {
+// grouped GEMM: one launch runs every independent GEMM of one dependency level.
+// One workgroup (16 waves, K split 16 ways) per output tile, one workgroup per CU.
+template <int TM, int TN, int KSPLIT, int G>
+__global__ __launch_bounds__(64 * KSPLIT) void k_gemm(GemmBatch batch) {
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   const int bid = blockIdx.x;
   int p = 0;
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(64 * KSPLIT, 4) void k_gemm(GemmBatch batch) {
   const GemmDesc d = batch.d[p];
   const int t = bid - d.tile_begin;
   const int m0 = (t / d.tiles_n) * TM, n0 = (t % d.tiles_n) * TN;
-  gemm_core<TM, TN, KSPLIT>(d, m0, n0, red);
+  gemm_core<TM, TN, KSPLIT, G>(d, m0, n0, red);
   __syncthreads();
   for (int e = threadIdx.x; e < TM * TN; e += 64 * KSPLIT) {
     const int row = e / TN, col = e % TN;
@@ -173,9 +179,29 @@ __global__ __launch_bounds__(64 * KSPLIT, 4) void k_gemm(GemmBatch batch) {
   }
 }
 
-void launch_gemm(const GemmBatch& b, hipStream_t s) {
-  if (b.count == 0) return;
-  hipLaunchKernelGGL((k_gemm<32, 32, kGemmKsplit>), dim3(b.total_tiles), dim3(64 * kGemmKsplit), 0, s, b);
+template <int TM, int TN>
+static int assign_tiles(GemmBatch& b) {
+  int tot = 0;
+  for (int i = 0; i < b.count; ++i) {
+    GemmDesc& d = b.d[i];
+    d.tiles_n = (d.N + TN - 1) / TN;
+    d.tile_begin = tot;
+    tot += ((d.M + TM - 1) / TM) * d.tiles_n;
+  }
+  b.total_tiles = tot;
+  return tot;
+}
+
+void launch_gemm(const GemmBatch& b0, hipStream_t s) {
+  if (b0.count == 0) return;
+  GemmBatch b = b0;
+  // widest tile that still gives one workgroup to most CUs
+  if (assign_tiles<32, 64>(b) >= 192) {
+    hipLaunchKernelGGL((k_gemm<32, 64, 16, 2>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+  } else {
+    assign_tiles<32, 32>(b);
+    hipLaunchKernelGGL((k_gemm<32, 32, 16, 4>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+  }
   HIP_LAUNCH_CHECK();
 }
 
@@ -216,7 +242,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   d.A = a.h; d.lda = a.ldh; d.a_kc = 1; d.M = a.rows;
   d.B = a.Wh; d.ldb = a.ldw; d.b_kc = 1; d.N = 2 * A; d.K = a.K;
   const int m0 = blockIdx.x * TM;
-  gemm_core<TM, TN, KSPLIT>(d, m0, 0, red);
+  gemm_core_l<TM, TN, KSPLIT, 3, true, true>(d, m0, 0, red);
   __syncthreads();
   const float alpha_unused = 0.f; (void)alpha_unused;
   const uint64_t ctr = a.sc->noise_counter;
@@ -281,7 +307,7 @@ template <int TM, int TN, int KSPLIT>
 __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, SampleBwdArgs a) {
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   const int m0 = blockIdx.x * TM;
-  gemm_core<TM, TN, KSPLIT>(d, m0, 0, red);
+  gemm_core_l<TM, TN, KSPLIT, 4, true, false>(d, m0, 0, red);
   __syncthreads();
   const int A = a.A;
   const float glogp = a.sc->alpha / (float)a.B;
@@ -442,7 +468,11 @@ __global__ __launch_bounds__(256) void k_actor_rows(ActorRowsArgs a) {
     for (int r = 0; r < kRowsPerBlock; ++r) s += part[r];
     a.loss_part[blockIdx.x] = s;
     if (blockIdx.x == 0) {
-      for (int i = 0; i < 4; ++i) a.sc->step[i] += 1.0;
+      for (int i = 0; i < 4; ++i) {
+        a.sc->step[i] += 1.0;
+        a.sc->beta_pow[i][0] *= 0.9;     // torch Adam default betas (sac_imp.py:39-49)
+        a.sc->beta_pow[i][1] *= 0.999;
+      }
       a.sc->noise_counter += 1;
     }
   }
@@ -471,10 +501,13 @@ __device__ __forceinline__ float polyak(float t, float p, float omtau, float tau
   return a + b;
 }
 
+// bias corrections of torch Adam (bc = 1 - beta^t in double, step_size = lr/bc1),
+// from the running products beta^step kept in DevScalars (no pow on the device)
 __device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, int step_idx) {
-  const double t = a.sc->step[step_idx] + (double)a.step_offset;
-  const double bc1 = 1.0 - pow((double)a.beta1, t);
-  const double bc2 = 1.0 - pow((double)a.beta2, t);
+  double p1 = a.sc->beta_pow[step_idx][0], p2 = a.sc->beta_pow[step_idx][1];
+  if (a.step_offset) { p1 *= (double)a.beta1; p2 *= (double)a.beta2; }
+  const double bc1 = 1.0 - p1;
+  const double bc2 = 1.0 - p2;
   return AdamScalars{(float)((double)a.lr / bc1), (float)sqrt(bc2)};
 }
 

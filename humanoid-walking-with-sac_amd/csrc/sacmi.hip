@@ -112,6 +112,7 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> stage, per_scr;
   std::map<sacmi::GraphKey, hipGraphExec_t> graphs;
   bool use_graphs = true;
+  bool G_external = false;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
   // profiling (sacmi_profile_step): one event per launch site
   bool prof = false;
   std::vector<std::string> prof_names;
@@ -606,6 +607,7 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
     c->stage.alloc(0);
     DevScalars h{};
     h.alpha = (float)cfg->alpha;
+    for (int i = 0; i < 4; ++i) { h.beta_pow[i][0] = 1.0; h.beta_pow[i][1] = 1.0; }
     h.per_frame = 1;
     upload_scalars(c.get(), h);
     // default RNG state: MT seeded with 5489 (both streams), as a fresh generator
@@ -627,6 +629,12 @@ int sacmi_destroy(sacmi_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     destroy_graphs(c);
+    if (c->G_external) {
+      auto& reg = alloc_registry();
+      for (size_t i = 0; i < reg.size(); ++i)
+        if (reg[i].base == (uintptr_t)c->G.p) { reg.erase(reg.begin() + i); break; }
+      c->G.p = nullptr;
+    }
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
                     &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->hp1, &c->hp2, &c->eps,
                     &c->cache, &c->logp, &c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1,
@@ -735,7 +743,13 @@ static void scalar_io(sacmi_ctx* c, int which, const double* in, double* out) {
     case SACMI_S_ALPHA_IS_TENSOR: if (in) h.alpha_is_tensor = (int)*in; else *out = h.alpha_is_tensor; break;
     case SACMI_S_STEP_POLICY: case SACMI_S_STEP_Q1: case SACMI_S_STEP_Q2: case SACMI_S_STEP_ALPHA: {
       const int k = which - SACMI_S_STEP_POLICY;
-      if (in) h.step[k] = *in; else *out = h.step[k];
+      if (in) {
+        h.step[k] = *in;
+        h.beta_pow[k][0] = std::pow(0.9, *in);
+        h.beta_pow[k][1] = std::pow(0.999, *in);
+      } else {
+        *out = h.step[k];
+      }
       break;
     }
     case SACMI_S_PER_FRAME: if (in) h.per_frame = (int64_t)*in; else *out = (double)h.per_frame; break;
@@ -905,6 +919,26 @@ int sacmi_step_phase(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scal
     REQUIRE(phase >= 0 && phase <= 2, SACMI_EVALUE, "phase must be 0, 1 or 2");
     if (phase == 0) check_batch(c, batch);
     run_update(c, batch, 1, 1, 1 << phase, grad_scale, false);
+  });
+}
+
+int sacmi_grad_arena_numel(sacmi_ctx* c, int64_t* numel) {
+  return guard([&] { *numel = c->total; });
+}
+
+int sacmi_attach_grad_arena(sacmi_ctx* c, void* ptr, int64_t numel) {
+  return guard([&] {
+    REQUIRE(ptr && numel == c->total, SACMI_EVALUE, "grad arena must hold exactly grad_arena_numel floats");
+    REQUIRE(((uintptr_t)ptr & 15) == 0, SACMI_EVALUE, "grad arena must be 16-byte aligned");
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    CHECK_HIP(hipMemset(ptr, 0, (size_t)numel * 4));
+    CHECK_HIP(hipDeviceSynchronize());
+    c->G.release();
+    c->G.p = (float*)ptr;
+    c->G.n = (size_t)numel;
+    c->G_external = true;
+    alloc_registry().push_back({(uintptr_t)ptr, (size_t)numel * 4});
+    destroy_graphs(c);
   });
 }
 

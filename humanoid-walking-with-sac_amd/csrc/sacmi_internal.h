@@ -49,6 +49,7 @@ struct DevScalars {
   float losses[3];      // q1, q2, policy of the last update
   float pad0;
   double step[4];       // Adam step of policy, q1, q2, alpha optimizers
+  double beta_pow[4][2];  // (beta1^step, beta2^step) per optimizer (running products)
   uint64_t noise_counter;
   int64_t len;          // replay fill
   int64_t head;         // ring slot of deque position 0

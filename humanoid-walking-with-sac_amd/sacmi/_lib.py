@@ -75,6 +75,8 @@ _PROTOS = {
     "sacmi_fetch_losses": [c_vp, c_f32p, ctypes.c_int32, c_i32p],
     "sacmi_step_phase": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float],
     "sacmi_grad_buffer": [c_vp, ctypes.c_int, ctypes.POINTER(c_vp), c_i64p],
+    "sacmi_grad_arena_numel": [c_vp, c_i64p],
+    "sacmi_attach_grad_arena": [c_vp, c_vp, ctypes.c_int64],
     "sacmi_per_sample": [c_vp, ctypes.c_int32, c_f64p, c_i64p, c_f32p],
     "sacmi_per_update": [c_vp, c_i64p, c_f32p, ctypes.c_int64],
     "sacmi_per_get_priorities": [c_vp, c_f32p, ctypes.c_int64],

@@ -204,6 +204,14 @@ class Context:
     def step_phase(self, batch: int, phase: int, grad_scale: float = 1.0) -> None:
         L.call("sacmi_step_phase", self._h, int(batch), int(phase), float(grad_scale))
 
+    def grad_arena_numel(self) -> int:
+        n = ctypes.c_int64()
+        L.call("sacmi_grad_arena_numel", self._h, ctypes.byref(n))
+        return n.value
+
+    def attach_grad_arena(self, device_ptr: int, numel: int) -> None:
+        L.call("sacmi_attach_grad_arena", self._h, ctypes.c_void_p(device_ptr), int(numel))
+
     def grad_buffer(self, which: int):
         p = ctypes.c_void_p()
         n = ctypes.c_int64()

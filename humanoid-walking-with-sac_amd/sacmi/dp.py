@@ -1,0 +1,129 @@
+"""Data-parallel SAC updates: one process per GPU, RCCL gradient all-reduce.
+
+SURVEY §8(e): every loss of ``update_parameters`` is a batch mean, so with equal
+per-rank batches the mean of the per-rank gradients equals the gradient of the
+concatenated global batch.  Each rank samples from its own HBM replay shard; the
+update is split where the reference has an ordering constraint (the actor must see
+the post-Adam critics, sac_imp.py:101-125):
+
+  phase 0  sample, gather, forward, critic backward   -> critic gradient buffer
+           all_reduce(SUM) critic grads                 (RCCL over xGMI)
+  phase 1  critic Adam (x 1/world) + Polyak, actor forward/backward -> actor buffer
+           all_reduce(SUM) [policy grads | dL/dlog_alpha]
+  phase 2  actor Adam (x 1/world) + alpha
+
+Every rank applies the identical reduced gradient with the identical deterministic
+kernels, so replicas stay bitwise identical.  The collectives run on tensors that
+alias the library's gradient arena (torch allocates it, libsacmi adopts it), ordered
+on torch's current stream, on which the library also runs.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+class GpuBackend:
+    """libsacmi context whose gradient arena is a torch tensor on ``device``."""
+
+    def __init__(self, ctx, device: torch.device):
+        self.ctx = ctx
+        n = ctx.grad_arena_numel()
+        self.arena = torch.zeros(n, dtype=torch.float32, device=device)
+        ctx.attach_grad_arena(self.arena.data_ptr(), n)
+        ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        base = self.arena.data_ptr()
+        views = []
+        for which in (0, 1):
+            ptr, numel = ctx.grad_buffer(which)
+            off = (ptr - base) // 4
+            views.append(self.arena.narrow(0, off, numel))
+        self.critic_grads, self.actor_grads = views
+
+    def phase(self, p: int, batch: int, grad_scale: float) -> None:
+        self.ctx.step_phase(batch, p, grad_scale)
+
+
+class DataParallelUpdate:
+    """Callable running one update across the process group."""
+
+    def __init__(self, backend, group=None):
+        self.backend = backend
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def __call__(self, batch: int) -> None:
+        b, scale = self.backend, 1.0 / self.world
+        b.phase(0, batch, scale)
+        dist.all_reduce(b.critic_grads, op=dist.ReduceOp.SUM, group=self.group)
+        b.phase(1, batch, scale)
+        dist.all_reduce(b.actor_grads, op=dist.ReduceOp.SUM, group=self.group)
+        b.phase(2, batch, scale)
+
+
+def run_dp_bench(args, rank: int, world: int, local_rank: int):
+    """bench.py --gpus N under torch.distributed.run (one rank per GPU)."""
+    import bench as B
+    from sacmi import Config, Context
+
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    fill = args.fill // world                       # this rank's replay shard
+    ctx = Context(Config(B.S_DIM, B.A_DIM, B.HIDDEN, max_batch=args.batch, capacity=fill,
+                         seed=1000 + rank), local_rank)
+    B.init_agent(ctx, 0)                            # identical replicas
+    key = np.random.default_rng(77 + rank).integers(0, 2**32, size=624, dtype=np.uint32)
+    ctx.set_mt(0, key, 624)                         # per-shard sampling stream
+    chunk = 100_000
+    for c0 in range(0, fill, chunk):
+        ctx.push(*B.synth(min(chunk, fill - c0), 5000 + rank * 7919 + c0))
+    upd = DataParallelUpdate(GpuBackend(ctx, device))
+    for _ in range(args.warmup):
+        upd(args.batch)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        upd(args.batch)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], device=device)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    # replicas must have stayed identical: compare a parameter checksum across ranks
+    w = torch.from_numpy(ctx.get_net("policy")["fc2.weight"]).to(device).double()
+    chk = torch.stack([w.sum(), (w * w).sum()])
+    allchk = [torch.zeros_like(chk) for _ in range(world)]
+    dist.all_gather(allchk, chk)
+    replicas_equal = all(bool(torch.equal(allchk[0], c)) for c in allchk)
+    if rank == 0:
+        iters = args.steps / dt
+        value = world * iters
+        flops = B.necessary_flops(B.S_DIM, B.A_DIM, B.HIDDEN, args.batch)
+        out = {
+            "metric": "SAC gradient-steps/sec, Humanoid-v5 batch=256 (obs 376, act 17, hidden 512)",
+            "value": round(value, 2), "unit": "grad-steps/s (batch-256 equivalent)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * dt / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "BASELINE configs[3] shape at batch 256/GPU: Humanoid-v5, "
+                                   "hidden=512, per-GPU replay shard + RCCL grad all-reduce",
+                       "state_dim": B.S_DIM, "action_dim": B.A_DIM, "hidden": B.HIDDEN,
+                       "global_batch": args.batch * world, "replay_fill": fill * world,
+                       "parallelism": f"dp{world}"},
+            "iterations_per_s": round(iters, 2),
+            "mfma_util_step": round(flops * value / 1e12 / B.PEAK_FP32_MFMA_TFLOPS / world, 4),
+            "replicas_bitwise_equal": replicas_equal,
+            "roofline": None, "cpu_baseline": None,
+        }
+        print(json.dumps(out))
+    dist.barrier()
+    dist.destroy_process_group()

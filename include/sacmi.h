@@ -159,6 +159,11 @@ int sacmi_fetch_losses(sacmi_ctx* ctx, float* out, int32_t max_steps, int32_t* n
  * Adam kernels. */
 int sacmi_step_phase(sacmi_ctx* ctx, int32_t batch, int32_t phase, float grad_scale);
 int sacmi_grad_buffer(sacmi_ctx* ctx, int which, void** device_ptr, int64_t* numel);
+/* Gradient arena size (floats) and adoption of a caller-allocated device buffer of
+ * that size (e.g. a torch tensor), so collectives run on it in place.  Must be on the
+ * context's device and stay alive for the context's lifetime. */
+int sacmi_grad_arena_numel(sacmi_ctx* ctx, int64_t* numel);
+int sacmi_attach_grad_arena(sacmi_ctx* ctx, void* device_ptr, int64_t numel);
 
 /* ---- prioritized replay ------------------------------------------------------------ */
 /* PrioritizedReplayBuffer.sample(batch) indices + IS weights; u: NULL -> draw from

@@ -265,3 +265,38 @@ def test_graph_and_eager_identical():
     for n in NETS:
         for k in res[0][1][n]:
             assert np.array_equal(res[0][1][n][k], res[1][1][n][k])
+
+
+def test_dp_phase_path_matches_fused_step_world1():
+    """sacmi.dp over a 1-rank RCCL group (phases + in-place all-reduce on the adopted
+    torch gradient arena) == the fused single-graph update, bit for bit."""
+    import socket
+    import torch.distributed as dist
+    from sacmi.dp import DataParallelUpdate, GpuBackend
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        cfg = SacConfig(24, 4, 64)
+        params = init_params(cfg, 71, bias_scale=0.05)
+        rows = synthetic_rows(cfg, 400, 72, state_scale=0.5)
+        key = (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32)
+        ctxs = []
+        for _ in range(2):
+            ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=3)
+            load_params(ctx, params)
+            ctx.push(*rows)
+            ctx.set_mt(0, key, 624)
+            ctxs.append(ctx)
+        upd = DataParallelUpdate(GpuBackend(ctxs[0], torch.device("cuda", 0)))
+        for _ in range(3):
+            upd(64)
+            ctxs[1].step(64)
+        torch.cuda.synchronize()
+        for n in NETS:
+            a, b = ctxs[0].get_net(n), ctxs[1].get_net(n)
+            for k in a:
+                assert np.array_equal(a[k], b[k]), (n, k)
+        assert ctxs[0].get_scalar(0) == ctxs[1].get_scalar(0)
+    finally:
+        dist.destroy_process_group()
