@@ -245,7 +245,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   gemm_core_l<TM, TN, KSPLIT, 3, true, true>(d, m0, 0, red);
   __syncthreads();
   const float alpha_unused = 0.f; (void)alpha_unused;
-  const uint64_t ctr = a.sc->noise_counter;
+  const uint64_t ctr = a.ctr_override ? a.ctr_override : a.sc->noise_counter;
   for (int e = threadIdx.x; e < TM * A; e += 64 * KSPLIT) {
     const int row = e / A, j = e % A;
     const int m = m0 + row;
@@ -256,13 +256,15 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
       const float sd = expf(ls);
       float eps;
-      if (a.gen_eps) {
+      if (a.deterministic) {
+        eps = 0.f;
+      } else if (a.gen_eps) {
         eps = philox_normal(a.seed, ctr, (uint32_t)(m * A + j));
         a.eps[(size_t)m * A + j] = eps;
       } else {
         eps = a.eps[(size_t)m * A + j];
       }
-      const float x = mean + eps * sd;
+      const float x = a.deterministic ? mean : mean + eps * sd;
       const float y = tanhf(x);
       a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
       const float dx = x - mean;
@@ -602,7 +604,7 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
 // stacked policy input [s2|1|.. ; s|1|..]  (replay_buffer.py:15-19 + sac_imp.py:81-85)
 __global__ __launch_bounds__(128) void k_gather(GatherArgs a) {
   const int b = blockIdx.x;
-  const int64_t slot = (a.sc->head + (int64_t)a.idx[b]) % a.capacity;
+  const int64_t slot = a.by_slot ? (int64_t)a.idx[b] : (a.sc->head + (int64_t)a.idx[b]) % a.capacity;
   const float* so = a.obs + slot * a.ldo;
   const float* s2 = a.obs2 + slot * a.ldo;
   const float* ac = a.act + slot * a.lda_;

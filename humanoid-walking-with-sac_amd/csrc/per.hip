@@ -1,10 +1,29 @@
-// Prioritized replay (reference PrioritizedReplayBuffer, replay_buffer.py:25-90).
+// Prioritized replay on the GPU (reference PrioritizedReplayBuffer,
+// replay_buffer.py:25-90; numpy 2.2 RandomState.choice(p=...)).
+//
+//   probs = prio[:len] ** alpha            float32 powf (numpy's SIMD pow is <=1 ulp
+//                                          away: the one non-bit-exact step)
+//   probs /= probs.sum()                   numpy's exact reduction order: 8192-element
+//                                          chunks, each a pairwise tree (leaves of <=128
+//                                          with 8 accumulators), chunk sums added in order
+//   cdf = float64(probs).cumsum()          exact int64 fixed-point prefix in 2^-52 units:
+//                                          bit-identical to the sequential float64 cumsum
+//                                          whenever every nonzero prob >= 2^-29 (all
+//                                          partial sums are then exact doubles); else a
+//                                          sequential float64 fallback
+//   cdf /= cdf[-1]; idx = cdf.searchsorted(u, 'right'), u = MT19937 53-bit doubles
+//   w = (len * probs[idx]) ** -beta; w /= w.max()
 #include "sacmi_internal.h"
 
 #include <cstdio>
 
 namespace sacmi {
 
+constexpr int kChunk = 8192;     // NPY_BUFSIZE
+constexpr int kLeaf = 128;       // PW_BLOCKSIZE
+constexpr int kScanBlock = 1024;
+
+// ---------------------------------------------------------------------------
 // push: every new row gets max(priorities[0:capacity]) (or 1.0 when the buffer was
 // empty) — replay_buffer.py:38,46.  Priorities are >= 0, so the float max is the
 // unsigned max of the bit patterns (order-independent => deterministic).
@@ -36,6 +55,335 @@ void launch_per_push(float* prio, int64_t cap, int64_t pos, int64_t n, int empty
   if (fb > 1024) fb = 1024;
   if (fb < 1) fb = 1;
   hipLaunchKernelGGL(k_prio_fill, dim3((unsigned)fb), dim3(256), 0, s, prio, cap, pos, n, mb, empty);
+}
+
+// ---------------------------------------------------------------------------
+// 1. probs = prio ** alpha
+__global__ void k_per_pow(const float* prio, int64_t len, float alpha, float* probs) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
+       i += (int64_t)gridDim.x * blockDim.x)
+    probs[i] = powf(prio[i], alpha);
+}
+
+// numpy pairwise leaf (loops_utils.h.src, n <= 128)
+__device__ float pw_leaf(const float* a, int n) {
+  if (n < 8) {
+    float res = -0.0f;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += a[i + 0]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+  }
+  float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+// 2. one workgroup per 8192-element chunk: leaves in parallel, tree combined in the
+// recursion order (deterministic, no contraction: plain float adds).
+__global__ __launch_bounds__(128) void k_per_chunk_sum(const float* probs, int64_t len,
+                                                       float* chunk_sum) {
+#pragma clang fp contract(off)
+  __shared__ int leaf_off[kChunk / 64], leaf_len[kChunk / 64];
+  __shared__ float leaf_val[kChunk / 64];
+  __shared__ int nleaf;
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const int n = (int)((len - c0) < kChunk ? (len - c0) : kChunk);
+  const float* a = probs + c0;
+  if (threadIdx.x == 0) {
+    // enumerate leaves in order with an explicit stack of (off, n)
+    int st_off[32], st_n[32], sp = 0, k = 0;
+    st_off[sp] = 0; st_n[sp] = n; ++sp;
+    while (sp) {
+      --sp;
+      const int o = st_off[sp], m = st_n[sp];
+      if (m <= kLeaf) { leaf_off[k] = o; leaf_len[k] = m; ++k; continue; }
+      int m2 = m / 2;
+      m2 -= m2 % 8;
+      st_off[sp] = o + m2; st_n[sp] = m - m2; ++sp;   // right pushed first
+      st_off[sp] = o; st_n[sp] = m2; ++sp;            // left popped first
+    }
+    nleaf = k;
+  }
+  __syncthreads();
+  for (int l = threadIdx.x; l < nleaf; l += blockDim.x) leaf_val[l] = pw_leaf(a + leaf_off[l], leaf_len[l]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // post-order combine: stack of partial sums mirrors the recursion
+    int st_n[32], st_state[32], sp = 0, leaf = 0;
+    float st_left[32];
+    float result = 0.f;
+    st_n[sp] = n; st_state[sp] = 0; ++sp;
+    bool have = false;
+    float val = 0.f;
+    while (sp) {
+      const int top = sp - 1;
+      const int m = st_n[top];
+      if (m <= kLeaf) {
+        val = leaf_val[leaf++];
+        have = true;
+        --sp;
+      } else if (st_state[top] == 0) {
+        int m2 = m / 2;
+        m2 -= m2 % 8;
+        st_state[top] = 1;
+        st_n[sp] = m2; st_state[sp] = 0; ++sp;       // left child
+        continue;
+      } else if (st_state[top] == 1) {
+        st_left[top] = val;
+        int m2 = m / 2;
+        m2 -= m2 % 8;
+        st_state[top] = 2;
+        st_n[sp] = m - m2; st_state[sp] = 0; ++sp;   // right child
+        continue;
+      } else {
+        val = st_left[top] + val;
+        have = true;
+        --sp;
+      }
+      if (sp == 0 && have) result = val;
+    }
+    chunk_sum[blockIdx.x] = (n > 0) ? result : -0.0f;
+  }
+}
+
+// 3. normalise + fixed point + block-local inclusive scan
+__global__ __launch_bounds__(kScanBlock) void k_per_norm_scan(float* probs, int64_t len,
+                                                              const float* chunk_sum, int nchunk,
+                                                              int64_t* q, int64_t* block_sum,
+                                                              int* bad) {
+#pragma clang fp contract(off)
+  __shared__ float s_total;
+  __shared__ int64_t wsum[kScanBlock / 64];
+  if (threadIdx.x == 0) {
+    float t = -0.0f;
+    for (int c = 0; c < nchunk; ++c) t = t + chunk_sum[c];
+    s_total = t;
+  }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kScanBlock + threadIdx.x;
+  int64_t v = 0;
+  if (i < len) {
+    const float p = probs[i] / s_total;
+    probs[i] = p;
+    if (p != 0.f && !(p >= 1.862645149230957e-09f)) atomicOr(bad, 1);   // 2^-29
+    v = (int64_t)((double)p * 4503599627370496.0);                    // exact when p >= 2^-29
+  }
+  // inclusive scan in the block
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int64_t base = 0;
+  for (int k = 0; k < w; ++k) base += wsum[k];
+  x += base;
+  if (i < len) q[i] = x;
+  if (threadIdx.x == kScanBlock - 1) block_sum[blockIdx.x] = x;
+}
+
+// 4. exclusive scan of block sums (one workgroup, sequential in chunks of 1024)
+__global__ __launch_bounds__(1024) void k_per_scan_blocks(int64_t* block_sum, int nblocks) {
+  __shared__ int64_t wsum[16];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < nblocks; b0 += 1024) {
+    const int b = b0 + threadIdx.x;
+    const int64_t v = b < nblocks ? block_sum[b] : 0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int64_t base = carry;
+    for (int k = 0; k < w; ++k) base += wsum[k];
+    if (b < nblocks) block_sum[b] = base + x - v;   // exclusive
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = base + x;
+    __syncthreads();
+  }
+}
+
+// 5. cdf = prefix / prefix[-1]  (or the sequential float64 fallback)
+__global__ void k_per_cdf(const int64_t* q, const int64_t* block_off, const float* probs,
+                          int64_t len, const int* bad, double* cdf) {
+  if (*bad) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      double s = 0.0;
+      for (int64_t i = 0; i < len; ++i) { s = s + (double)probs[i]; cdf[i] = s; }
+      const double last = cdf[len - 1];
+      for (int64_t i = 0; i < len; ++i) cdf[i] = cdf[i] / last;
+    }
+    return;
+  }
+  const int64_t nb = (len + kScanBlock - 1) / kScanBlock;
+  const double last = (double)(q[len - 1] + block_off[nb - 1]);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
+       i += (int64_t)gridDim.x * blockDim.x)
+    cdf[i] = (double)(q[i] + block_off[i / kScanBlock]) / last;
+}
+
+// 6. uniforms (numpy MT stream), searchsorted(side='right'), IS weights
+__device__ __forceinline__ uint32_t mt_temper_p(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9D2C5680u;
+  y ^= (y << 15) & 0xEFC60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+__device__ void mt_twist_serial_p(uint32_t* key) {
+  for (int i = 0; i < 624; ++i) {
+    const uint32_t y = (key[i] & 0x80000000u) | (key[(i + 1) % 624] & 0x7FFFFFFFu);
+    key[i] = key[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908B0DFu : 0u);
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_per_draw(const double* cdf, const float* probs,
+                                                   int64_t len, int k, uint32_t* mt, int gen_u,
+                                                   const double* u_in, double* u_buf,
+                                                   DevScalars* sc, double beta_start,
+                                                   double beta_frames, int32_t* idx32,
+                                                   int64_t* idx64, float* w_out) {
+#pragma clang fp contract(off)
+  __shared__ uint32_t key[624];
+  __shared__ int s_pos;
+  __shared__ float s_wmax[16];
+  __shared__ float s_beta;
+  const int t = threadIdx.x;
+  if (gen_u) {
+    for (int i = t; i < 624; i += blockDim.x) key[i] = mt[i];
+    if (t == 0) s_pos = (int)mt[624];
+    __syncthreads();
+    // 2k words in stream order; a block twist (serial, one lane) whenever exhausted
+    int done = 0;
+    const int need = 2 * k;
+    uint32_t* words = reinterpret_cast<uint32_t*>(u_buf);   // reuse as scratch (<= 2k words)
+    while (done < need) {
+      // every wave reads the position between two barriers, so all take the same
+      // branch below (thread 0 rewrites s_pos only after the second barrier)
+      __syncthreads();
+      int pos = s_pos;
+      __syncthreads();
+      if (pos >= 624) {
+        if (t == 0) { mt_twist_serial_p(key); s_pos = 0; }
+        __syncthreads();
+        pos = 0;
+      }
+      const int take = min(624 - pos, need - done);
+      for (int j = t; j < take; j += blockDim.x) words[done + j] = mt_temper_p(key[pos + j]);
+      __syncthreads();
+      if (t == 0) s_pos = pos + take;
+      done += take;
+    }
+    __syncthreads();
+    for (int i = t; i < 624; i += blockDim.x) mt[i] = key[i];
+    if (t == 0) mt[624] = (uint32_t)s_pos;
+    __syncthreads();
+    // convert pairs to doubles (in place, back to front safe: i-th double uses words
+    // 2i, 2i+1 which are at or after its own byte range)
+    for (int i = 0; i < k; i += blockDim.x) {
+      const int j = i + t;
+      uint32_t w0 = 0, w1 = 0;
+      if (j < k) { w0 = words[2 * j]; w1 = words[2 * j + 1]; }
+      __syncthreads();
+      if (j < k)
+        u_buf[j] = ((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) / 9007199254740992.0;
+      __syncthreads();
+    }
+  } else {
+    for (int j = t; j < k; j += blockDim.x) u_buf[j] = u_in[j];
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double fr = (double)sc->per_frame;
+    double beta = beta_start + fr * (1.0 - beta_start) / beta_frames;
+    if (beta > 1.0) beta = 1.0;
+    s_beta = (float)(-beta);
+    sc->per_frame += 1;
+  }
+  __syncthreads();
+  float wmax = 0.f;
+  for (int j = t; j < k; j += blockDim.x) {
+    const double u = u_buf[j];
+    int64_t lo = 0, hi = len;            // first index with cdf > u
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+    }
+    if (lo > len - 1) lo = len - 1;
+    idx32[j] = (int32_t)lo;
+    idx64[j] = lo;
+    const float pw = powf((float)len * probs[lo], s_beta);
+    w_out[j] = pw;
+    wmax = fmaxf(wmax, pw);
+  }
+  for (int o = 32; o >= 1; o >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o, 64));
+  if ((t & 63) == 0) s_wmax[t >> 6] = wmax;
+  __syncthreads();
+  float m = 0.f;
+  for (int q = 0; q < (int)(blockDim.x >> 6); ++q) m = fmaxf(m, s_wmax[q]);
+  for (int j = t; j < k; j += blockDim.x) w_out[j] = w_out[j] / m;
+}
+
+void launch_per_sample(const PerArgs& a, hipStream_t s) {
+  const int64_t len = a.len;
+  int64_t blocks = (len + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_per_pow, dim3((unsigned)blocks), dim3(256), 0, s, a.prio, len, a.alpha, a.probs);
+  const int nchunk = (int)((len + kChunk - 1) / kChunk);
+  hipLaunchKernelGGL(k_per_chunk_sum, dim3(nchunk), dim3(128), 0, s, a.probs, len, a.chunk_sums);
+  const int nb = (int)((len + kScanBlock - 1) / kScanBlock);
+  (void)hipMemsetAsync(a.bad, 0, 4, s);
+  hipLaunchKernelGGL(k_per_norm_scan, dim3(nb), dim3(kScanBlock), 0, s, a.probs, len,
+                     a.chunk_sums, nchunk, a.q, a.block_sums, a.bad);
+  hipLaunchKernelGGL(k_per_scan_blocks, dim3(1), dim3(1024), 0, s, a.block_sums, nb);
+  hipLaunchKernelGGL(k_per_cdf, dim3((unsigned)blocks), dim3(256), 0, s, a.q, a.block_sums,
+                     a.probs, len, a.bad, a.cdf);
+  hipLaunchKernelGGL(k_per_draw, dim3(1), dim3(1024), 0, s, a.cdf, a.probs, len, a.k, a.mt,
+                     a.gen_u, a.u, a.u_scratch, a.sc, a.beta_start, a.beta_frames, a.idx32,
+                     a.idx_out, a.w_out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fprintf(stderr, "sacmi: PER launch failed: %s\n", hipGetErrorString(e));
+}
+
+// update_priorities (replay_buffer.py:84-87): sequential semantics, last duplicate wins
+__global__ void k_owner_claim(const int64_t* idx, int64_t n, int32_t* owner) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    atomicMax(&owner[idx[i]], (int32_t)i);
+}
+__global__ void k_owner_write(const int64_t* idx, const float* val, int64_t n, int32_t* owner,
+                              float* prio) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (owner[idx[i]] == (int32_t)i) prio[idx[i]] = val[i];
+}
+__global__ void k_owner_reset(const int64_t* idx, int64_t n, int32_t* owner) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    owner[idx[i]] = -1;
+}
+
+void launch_per_update(float* prio, const int64_t* idx, const float* val, int64_t n,
+                       int32_t* owner, hipStream_t s) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_owner_claim, dim3((unsigned)blocks), dim3(256), 0, s, idx, n, owner);
+  hipLaunchKernelGGL(k_owner_write, dim3((unsigned)blocks), dim3(256), 0, s, idx, val, n, owner, prio);
+  hipLaunchKernelGGL(k_owner_reset, dim3((unsigned)blocks), dim3(256), 0, s, idx, n, owner);
 }
 
 }  // namespace sacmi

@@ -70,9 +70,10 @@ struct DevBuf {
 
 struct GraphKey {
   int batch, dev_idx, dev_eps, phase_mask, ring;
+  int64_t per_len;   // PER launch geometry depends on the fill
   bool operator<(const GraphKey& o) const {
-    return std::tie(batch, dev_idx, dev_eps, phase_mask, ring) <
-           std::tie(o.batch, o.dev_idx, o.dev_eps, o.phase_mask, o.ring);
+    return std::tie(batch, dev_idx, dev_eps, phase_mask, ring, per_len) <
+           std::tie(o.batch, o.dev_idx, o.dev_eps, o.phase_mask, o.ring, o.per_len);
   }
 };
 
@@ -110,9 +111,15 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> ax, ah1, ah2, aeps, acache, alogp, aout;
   // staging
   sacmi::DevBuf<float> stage, per_scr;
+  // PER scratch (replay_kind == PER)
+  sacmi::DevBuf<float> per_probs, per_chunk, per_w, per_val;
+  sacmi::DevBuf<int64_t> per_q, per_blk, per_idx;
+  sacmi::DevBuf<double> per_cdf, per_u, per_uin;
+  sacmi::DevBuf<int32_t> per_owner, per_bad;
   std::map<sacmi::GraphKey, hipGraphExec_t> graphs;
   bool use_graphs = true;
-  bool G_external = false;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
+  bool G_external = false;
+  uint64_t act_calls = 0;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
   // profiling (sacmi_profile_step): one event per launch site
   bool prof = false;
   std::vector<std::string> prof_names;
@@ -209,7 +216,21 @@ static void alloc_all(sacmi_ctx* c) {
   c->act.alloc((size_t)cap * c->ldact);
   c->rew.alloc(cap);
   c->done.alloc(cap);
-  if (c->cfg.replay_kind == SACMI_REPLAY_PER) c->prio.alloc(cap);
+  if (c->cfg.replay_kind == SACMI_REPLAY_PER) {
+    c->prio.alloc(cap);
+    c->per_probs.alloc(cap);
+    c->per_q.alloc(cap);
+    c->per_cdf.alloc(cap);
+    c->per_chunk.alloc(cap / 8192 + 2);
+    c->per_blk.alloc(cap / 1024 + 2);
+    c->per_bad.alloc(4);
+    c->per_owner.alloc(cap);
+    CHECK_HIP(hipMemset(c->per_owner.p, 0xFF, (size_t)cap * 4));   // -1: no writer
+    CHECK_HIP(hipDeviceSynchronize());
+    c->per_u.alloc(c->Bm + 2);
+    c->per_uin.alloc(c->Bm + 2);
+    c->per_w.alloc(c->Bm + 2);
+  }
   c->mt.alloc(2 * 625);
   c->per_scr.alloc(16);
   c->idx32.alloc(Bm); c->idx64.alloc(Bm);
@@ -325,6 +346,18 @@ static void mark(sacmi_ctx* c, const char* name, double flops = 0) {
   c->prof_flops.push_back(flops);
 }
 
+static PerArgs per_args(sacmi_ctx* c, int k, int gen_u) {
+  PerArgs a{};
+  a.prio = c->prio.p; a.len = c->len; a.alpha = (float)c->cfg.per_alpha;
+  a.probs = c->per_probs.p; a.chunk_sums = c->per_chunk.p; a.q = c->per_q.p;
+  a.block_sums = c->per_blk.p; a.bad = c->per_bad.p; a.cdf = c->per_cdf.p;
+  a.mt = c->mt.p + 625; a.gen_u = gen_u; a.u = c->per_uin.p; a.u_scratch = c->per_u.p;
+  a.k = k; a.sc = c->sc.p; a.beta_start = c->cfg.per_beta_start;
+  a.beta_frames = c->cfg.per_beta_frames; a.idx32 = c->idx32.p; a.idx_out = c->idx64.p;
+  a.w_out = c->per_w.p;
+  return a;
+}
+
 static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
                            float grad_scale, bool use_ring) {
   hipStream_t s = c->stream;
@@ -339,7 +372,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   const Linear(&q)[2][3] = c->q_fc;
 
   if (phase_mask & 1) {
-    if (dev_idx) {
+    const bool per = c->cfg.replay_kind == SACMI_REPLAY_PER;
+    if (dev_idx && per) {
+      mark(c, "per_sample");
+      launch_per_sample(per_args(c, B, 1), s);
+    } else if (dev_idx) {
       MtSampleArgs m{};
       m.mt = c->mt.p; m.sc = c->sc.p; m.k = B;
       const int k = B;
@@ -354,6 +391,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     g.done = c->done.p; g.ldo = c->ldo; g.lda_ = c->ldact; g.capacity = c->capacity;
     g.sc = c->sc.p; g.S = S; g.A = A; g.B = B; g.xq = c->xq.p; g.x2 = c->x2.p; g.ldx = Kx;
     g.r = c->r.p; g.d = c->d.p;
+    g.by_slot = per ? 1 : 0;
     mark(c, "gather");
     launch_gather(g, s);
 
@@ -520,7 +558,8 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
     CHECK_HIP(hipGetLastError());
     return;
   }
-  GraphKey key{B, dev_idx, dev_eps, phase_mask | (grad_scale != 1.f ? 8 : 0), use_ring ? c->ring_slots : 0};
+  GraphKey key{B, dev_idx, dev_eps, phase_mask | (grad_scale != 1.f ? 8 : 0), use_ring ? c->ring_slots : 0,
+               c->cfg.replay_kind == SACMI_REPLAY_PER ? c->len : 0};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g;
@@ -640,9 +679,12 @@ int sacmi_destroy(sacmi_ctx* c) {
                     &c->cache, &c->logp, &c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1,
                     &c->hqa2, &c->dq, &c->dh2, &c->dh1, &c->dha2, &c->dha1, &c->dhead, &c->dhp2,
                     &c->dhp1, &c->lpart_c, &c->lpart_a, &c->ring, &c->ax, &c->ah1, &c->ah2,
-                    &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr})
+                    &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr, &c->per_probs,
+                    &c->per_chunk, &c->per_w, &c->per_val})
       b->release();
     c->sc.release(); c->mt.release(); c->idx32.release(); c->idx64.release();
+    c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
+    c->per_u.release(); c->per_uin.release(); c->per_owner.release(); c->per_bad.release();
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
   });
@@ -835,6 +877,20 @@ int sacmi_get_rows(sacmi_ctx* c, const int64_t* idx, int64_t n, float* s, float*
   });
 }
 
+int sacmi_get_slots(sacmi_ctx* c, const int64_t* slots, int64_t n, float* s, float* a, float* r,
+                    float* s2, uint8_t* d) {
+  return guard([&] {
+    std::vector<int64_t> pos(n);
+    const int64_t head = c->len < c->capacity ? 0 : c->wpos;
+    for (int64_t i = 0; i < n; ++i) {
+      REQUIRE(slots[i] >= 0 && slots[i] < c->len, SACMI_EVALUE, "slot out of range");
+      pos[i] = (slots[i] - head + c->capacity) % c->capacity;
+    }
+    const int st = sacmi_get_rows(c, pos.data(), n, s, a, r, s2, d);
+    if (st != SACMI_OK) throw Error{st, g_last_error};
+  });
+}
+
 int sacmi_rng_set_mt(sacmi_ctx* c, int stream, const uint32_t* key, int32_t pos) {
   return guard([&] {
     REQUIRE(stream == 0 || stream == 1, SACMI_EVALUE, "stream must be 0 or 1");
@@ -991,21 +1047,96 @@ int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_o
   });
 }
 
-int sacmi_per_sample(sacmi_ctx* c, int32_t, const double*, int64_t*, float*) {
-  return guard([&] { throw Error{SACMI_ESTATE, "PER sampling not built yet"}; });
-}
-int sacmi_per_update(sacmi_ctx* c, const int64_t*, const float*, int64_t) {
-  return guard([&] { throw Error{SACMI_ESTATE, "PER not built yet"}; });
-}
-int sacmi_per_get_priorities(sacmi_ctx* c, float*, int64_t) {
-  return guard([&] { throw Error{SACMI_ESTATE, "PER not built yet"}; });
-}
-int sacmi_per_set_priorities(sacmi_ctx* c, const float*, int64_t) {
-  return guard([&] { throw Error{SACMI_ESTATE, "PER not built yet"}; });
+static void require_per(sacmi_ctx* c) {
+  REQUIRE(c->cfg.replay_kind == SACMI_REPLAY_PER, SACMI_ESTATE, "context was not created with PER replay");
 }
 
-int sacmi_act(sacmi_ctx* c, const float*, int32_t, int32_t, const float*, float*) {
-  return guard([&] { throw Error{SACMI_ESTATE, "act not built yet"}; });
+int sacmi_per_sample(sacmi_ctx* c, int32_t batch, const double* u, int64_t* idx_out,
+                     float* weights_out) {
+  return guard([&] {
+    require_per(c);
+    REQUIRE(c->len > 0, SACMI_EVALUE, "probabilities do not sum to 1");   // empty buffer
+    REQUIRE(batch >= 0 && batch <= c->Bm, SACMI_EVALUE, "batch must be in [0, max_batch]");
+    const int k = (int)std::min<int64_t>(batch, c->len);    // replay_buffer.py:50
+    if (k == 0) return;
+    if (u) CHECK_HIP(hipMemcpyAsync(c->per_uin.p, u, (size_t)k * 8, hipMemcpyHostToDevice, c->stream));
+    launch_per_sample(per_args(c, k, u ? 0 : 1), c->stream);
+    CHECK_HIP(hipGetLastError());
+    if (idx_out) CHECK_HIP(hipMemcpyAsync(idx_out, c->idx64.p, (size_t)k * 8, hipMemcpyDeviceToHost, c->stream));
+    if (weights_out) CHECK_HIP(hipMemcpyAsync(weights_out, c->per_w.p, (size_t)k * 4, hipMemcpyDeviceToHost, c->stream));
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int sacmi_per_update(sacmi_ctx* c, const int64_t* idx, const float* values, int64_t n) {
+  return guard([&] {
+    require_per(c);
+    if (n <= 0) return;
+    for (int64_t i = 0; i < n; ++i)
+      REQUIRE(idx[i] >= 0 && idx[i] < c->capacity, SACMI_EVALUE, "index out of range");
+    if ((int64_t)c->per_idx.n < n) {
+      c->per_idx.release(); c->per_val.release();
+      c->per_idx.alloc(n); c->per_val.alloc(n);
+    }
+    CHECK_HIP(hipMemcpyAsync(c->per_idx.p, idx, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+    CHECK_HIP(hipMemcpyAsync(c->per_val.p, values, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    launch_per_update(c->prio.p, c->per_idx.p, c->per_val.p, n, c->per_owner.p, c->stream);
+    CHECK_HIP(hipGetLastError());
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int sacmi_per_get_priorities(sacmi_ctx* c, float* out, int64_t n) {
+  return guard([&] {
+    require_per(c);
+    REQUIRE(n >= 0 && n <= c->capacity, SACMI_EVALUE, "n > capacity");
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    CHECK_HIP(hipMemcpy(out, c->prio.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  });
+}
+
+int sacmi_per_set_priorities(sacmi_ctx* c, const float* in, int64_t n) {
+  return guard([&] {
+    require_per(c);
+    REQUIRE(n >= 0 && n <= c->capacity, SACMI_EVALUE, "n > capacity");
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    CHECK_HIP(hipMemcpy(c->prio.p, in, (size_t)n * 4, hipMemcpyHostToDevice));
+  });
+}
+
+// select_action (sac_imp.py:54-72): the policy forward on n states through the same
+// kernels as the update (rows of the step's stacked policy input are reused).
+int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministic,
+              const float* eps, float* a_out) {
+  return guard([&] {
+    REQUIRE(states && a_out, SACMI_EVALUE, "null argument");
+    REQUIRE(n > 0 && n <= 2 * c->Bm, SACMI_EVALUE, "n must be in [1, 2*max_batch]");
+    hipStream_t s = c->stream;
+    const int S = c->S, A = c->A, H = c->H, Kx = c->Kx, Hd = c->Hd;
+    CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, states, (size_t)S * 4, (size_t)S * 4, n,
+                               hipMemcpyHostToDevice, s));
+    if (eps && !deterministic)
+      CHECK_HIP(hipMemcpyAsync(c->eps.p, eps, (size_t)n * A * 4, hipMemcpyHostToDevice, s));
+    Level l1, l2;
+    l1.add(gd(c->x2.p, Kx, 1, c->P.p + c->p_fc1.off, c->p_fc1.ld, 1, c->hp1.p, Hd, n, H, S + 1, EPI_RELU));
+    launch_gemm(l1.b, s);
+    l2.add(gd(c->hp1.p, Hd, 1, c->P.p + c->p_fc2.off, Hd, 1, c->hp2.p, Hd, n, H, H + 1, EPI_RELU));
+    launch_gemm(l2.b, s);
+    HeadSampleArgs hs{};
+    hs.h = c->hp2.p; hs.Wh = c->P.p + c->p_head.off; hs.rows = n; hs.A = A; hs.K = H + 1;
+    hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = eps ? 0 : 1; hs.seed = c->cfg.seed;
+    hs.sc = c->sc.p; hs.act = c->x2.p + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
+    hs.cache = c->cache.p;
+    hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
+    hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
+    hs.deterministic = deterministic ? 1 : 0;
+    hs.ctr_override = (1ull << 63) | (++c->act_calls);   // disjoint from update noise
+    launch_heads_sample(hs, s);
+    CHECK_HIP(hipGetLastError());
+    CHECK_HIP(hipMemcpy2DAsync(a_out, (size_t)A * 4, c->x2.p + S + 1, (size_t)Kx * 4, (size_t)A * 4, n,
+                               hipMemcpyDeviceToHost, s));
+    CHECK_HIP(hipStreamSynchronize(s));
+  });
 }
 
 }  // extern "C"

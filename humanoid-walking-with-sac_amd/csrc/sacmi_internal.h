@@ -98,6 +98,8 @@ struct HeadSampleArgs {
   float* logp;           // [rows]
   float* cache;          // [rows, 3A]: mean | log_std(raw) | y
   float scale, bias;
+  int deterministic;     // 1: action = tanh(mean)*scale+bias (select_action(evaluate=True))
+  uint64_t ctr_override; // nonzero: Philox counter to use instead of sc->noise_counter
 };
 
 // Sample-backward epilogue of the dL/da GEMM.
@@ -179,6 +181,7 @@ struct GatherArgs {
   int S, A, B;
   float* xq; float* x2; int ldx;   // xq [B, ldx], x2 [2B, ldx]
   float* r; float* d;
+  int by_slot;            // 1: idx are ring slots (PER), 0: deque positions
 };
 void launch_gather(const GatherArgs& a, hipStream_t s);
 
@@ -197,26 +200,30 @@ void launch_fill(float* p, int64_t n, float v, hipStream_t s);
 void launch_set_column(float* p, int rows, int ld, int col, float v, hipStream_t s);
 void launch_increment_steps(DevScalars* sc, hipStream_t s);
 
-// PER
+// PER (per.hip)
 struct PerArgs {
-  float* prio; int64_t len; int64_t cap;
+  const float* prio; int64_t len;
   float alpha;
-  float* probs;           // [len]
+  float* probs;           // [len] scratch: prio^alpha, then normalised
+  float* chunk_sums;      // [ceil(len/8192)]
+  int64_t* q;             // [len] fixed-point prefix (block-local)
+  int64_t* block_sums;    // [ceil(len/1024)]
+  int* bad;               // 1 -> sequential float64 cumsum fallback
   double* cdf;            // [len]
-  float* chunk_sums;      // scratch
-  int64_t* ichunk;        // scratch
-  const double* u;        // [k] uniforms (device)
-  uint32_t* mt;           // numpy MT state when u is generated on device
-  int gen_u;
+  uint32_t* mt;           // numpy MT19937 stream (625 words)
+  int gen_u;              // 1: draw u from mt; 0: u given in `u`
+  const double* u;        // [k]
+  double* u_scratch;      // [k]
   int k;
-  int64_t* idx_out;
-  float* w_out;
-  DevScalars* sc;
-  float beta_start, beta_frames;
-  double* u_scratch;
+  DevScalars* sc;         // per_frame
+  double beta_start, beta_frames;
+  int32_t* idx32;         // [k] ring slots (feeds the update's gather)
+  int64_t* idx_out;       // [k]
+  float* w_out;           // [k]
 };
 void launch_per_sample(const PerArgs& a, hipStream_t s);
-void launch_per_update(float* prio, const int64_t* idx, const float* val, int64_t n, hipStream_t s);
+void launch_per_update(float* prio, const int64_t* idx, const float* val, int64_t n,
+                       int32_t* owner, hipStream_t s);
 void launch_per_push(float* prio, int64_t cap, int64_t pos, int64_t n, int empty, float* scratch,
                      hipStream_t s);
 

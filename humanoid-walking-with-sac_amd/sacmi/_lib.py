@@ -67,6 +67,7 @@ _PROTOS = {
     "sacmi_push": [c_vp, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p, ctypes.c_int64],
     "sacmi_len": [c_vp, c_i64p],
     "sacmi_get_rows": [c_vp, c_i64p, ctypes.c_int64, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p],
+    "sacmi_get_slots": [c_vp, c_i64p, ctypes.c_int64, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p],
     "sacmi_rng_set_mt": [c_vp, ctypes.c_int, c_u32p, ctypes.c_int32],
     "sacmi_rng_get_mt": [c_vp, ctypes.c_int, c_u32p, c_i32p],
     "sacmi_sample_indices": [c_vp, ctypes.c_int32, c_i64p],

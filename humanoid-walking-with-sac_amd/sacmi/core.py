@@ -164,6 +164,17 @@ class Context:
                L.fptr(s2), L.u8ptr(d))
         return s, a, r, s2, d.astype(bool)
 
+    def get_slots(self, slots):
+        """Rows at ring slots (PER indices)."""
+        idx = np.ascontiguousarray(slots, np.int64)
+        n = idx.size
+        S, A = self.cfg.state_dim, self.cfg.action_dim
+        s = np.empty((n, S), np.float32); s2 = np.empty((n, S), np.float32)
+        a = np.empty((n, A), np.float32); r = np.empty(n, np.float32); d = np.empty(n, np.uint8)
+        L.call("sacmi_get_slots", self._h, L.i64ptr(idx), n, L.fptr(s), L.fptr(a), L.fptr(r),
+               L.fptr(s2), L.u8ptr(d))
+        return s, a, r, s2, d.astype(bool)
+
     # -- rng -----------------------------------------------------------------------
     def set_mt(self, stream: int, key, pos: int) -> None:
         k = np.ascontiguousarray(key, np.uint32)
@@ -227,9 +238,11 @@ class Context:
         L.call("sacmi_per_sample", self._h, int(batch), L.dptr(u_a), L.i64ptr(idx), L.fptr(w))
         return idx, w
 
-    def per_update(self, idx, prio) -> None:
+    def per_update(self, idx, values) -> None:
+        """priorities[idx[i]] = values[i], last duplicate wins (values already hold the
+        reference's float32(float(p) + 1e-6))."""
         idx = np.ascontiguousarray(idx, np.int64)
-        p = np.ascontiguousarray(prio, np.float32).reshape(-1)
+        p = np.ascontiguousarray(values, np.float32).reshape(-1)
         L.call("sacmi_per_update", self._h, L.i64ptr(idx), L.fptr(p), idx.size)
 
     def per_priorities(self, n: int | None = None) -> np.ndarray:

@@ -128,6 +128,11 @@ int sacmi_len(sacmi_ctx* ctx, int64_t* n);
 int sacmi_get_rows(sacmi_ctx* ctx, const int64_t* idx, int64_t n, float* s, float* a,
                    float* r, float* s2, uint8_t* d);
 
+/* Same, addressed by ring slot (PrioritizedReplayBuffer indices are list positions
+ * = ring slots, replay_buffer.py:40-44,73). */
+int sacmi_get_slots(sacmi_ctx* ctx, const int64_t* slots, int64_t n, float* s, float* a,
+                    float* r, float* s2, uint8_t* d);
+
 /* ---- RNG bridges ----------------------------------------------------------------- */
 /* stream 0 = CPython `random` (uniform indices), stream 1 = numpy legacy
  * RandomState (PER).  key: 624 words, pos: index 0..624. */
@@ -139,7 +144,7 @@ int sacmi_sample_indices(sacmi_ctx* ctx, int32_t batch, int64_t* idx_out);
 
 /* ---- the gradient step ----------------------------------------------------------- */
 /* One update_parameters(batch): sample (uniform: device MT stream 0 unless idx is
- * given), gather, target, twin-critic step, actor step, alpha step, Polyak.
+ * given; PER contexts: the device PER sampler on stream 1, ring-slot indices), gather, target, twin-critic step, actor step, alpha step, Polyak.
  * idx:  NULL -> draw on device; else [batch] deque positions.
  * eps1, eps2: NULL -> on-device Philox noise; else [batch, A] standard normals
  *   (eps1 for policy.sample(next_state), eps2 for policy.sample(state)).
@@ -170,7 +175,10 @@ int sacmi_attach_grad_arena(sacmi_ctx* ctx, void* device_ptr, int64_t numel);
  * MT stream 1 on device, else [min(batch,len)] uniforms in [0,1).  Advances frame. */
 int sacmi_per_sample(sacmi_ctx* ctx, int32_t batch, const double* u, int64_t* idx_out,
                      float* weights_out);
-int sacmi_per_update(sacmi_ctx* ctx, const int64_t* idx, const float* prio, int64_t n);
+/* priorities[idx[i]] = values[i] in order i = 0..n-1 (last duplicate wins), where the
+ * caller passes the reference's stored value float32(float(p) + 1e-6)
+ * (replay_buffer.py:87; the +1e-6 is a double add, done host-side). */
+int sacmi_per_update(sacmi_ctx* ctx, const int64_t* idx, const float* values, int64_t n);
 int sacmi_per_get_priorities(sacmi_ctx* ctx, float* out, int64_t n);
 int sacmi_per_set_priorities(sacmi_ctx* ctx, const float* in, int64_t n);
 

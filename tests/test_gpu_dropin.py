@@ -1,0 +1,149 @@
+"""The drop-in modules (sac_imp / replay_buffer / networks_model1 names) on the GPU,
+driven the way the reference's trainer.py drives them (trainer.py:182-209)."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.pyrandom import MT19937, sample_indices
+
+pytestmark = pytest.mark.gpu
+
+S, A, H = 24, 4, 64
+
+
+def _agent(**kw):
+    from sac_imp import SAC
+    torch.manual_seed(0)
+    return SAC(S, A, hidden_dim=H, device="cuda", capacity=5000, max_batch=256, **kw)
+
+
+def _fill(agent, n, seed=0):
+    rng = np.random.default_rng(seed)
+    for _ in range(n):    # the trainer pushes one transition per env step
+        agent.replay_buffer.push(rng.standard_normal(S), rng.uniform(-0.4, 0.4, A).astype(np.float32),
+                                 float(rng.standard_normal()), rng.standard_normal(S),
+                                 bool(rng.random() < 0.02))
+
+
+def test_trainer_loop_contract():
+    agent = _agent()
+    _fill(agent, 300)
+    assert len(agent.replay_buffer) == 300
+    hist = []
+    for _ in range(5):
+        if len(agent.replay_buffer) > 64:               # trainer.py:202 gate (strict)
+            hist.append(agent.update_parameters(64))
+    assert len(hist) == 5
+    for h in hist:
+        assert set(h) == {"q1_loss", "q2_loss", "policy_loss"}
+        assert all(isinstance(v, float) and np.isfinite(v) for v in h.values())
+    # alpha becomes exp(log_alpha) (a tensor) after the first update (sac_imp.py:135)
+    assert torch.is_tensor(agent.alpha)
+    np.testing.assert_allclose(float(agent.alpha), float(agent.log_alpha.exp()), rtol=1e-6)
+
+
+def test_state_dicts_match_reference_layout_and_init():
+    agent = _agent()
+    sd = agent.policy.state_dict()
+    assert list(sd) == ["fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias", "mean.weight",
+                        "mean.bias", "log_std.weight", "log_std.bias"]
+    assert tuple(agent.q1.state_dict()["fc1.weight"].shape) == (H, S + A)
+    # targets start as copies (sac_imp.py:35-36)
+    for k, v in agent.q1.state_dict().items():
+        assert torch.equal(v, agent.q1_target.state_dict()[k])
+    # device holds exactly the mirrors' values
+    live = agent._ctx.get_net("policy")
+    for k, v in sd.items():
+        assert np.array_equal(live[k].reshape(v.shape), v.numpy())
+
+
+def test_select_action_shapes_and_bounds():
+    agent = _agent()
+    a = agent.select_action(np.zeros(S))
+    assert a.shape == (A,) and np.all(np.abs(a) <= 0.4)
+    st = np.random.default_rng(1).standard_normal(S).astype(np.float32)
+    det = agent.select_action(st, evaluate=True)
+    with torch.no_grad():   # evaluate: tanh(mean)*scale+bias on the CPU mirror
+        mean, _ = agent.policy(torch.from_numpy(st).unsqueeze(0))
+        ref = (torch.tanh(mean) * 0.4).numpy()[0]
+    np.testing.assert_allclose(det, ref, rtol=1e-5, atol=1e-6)
+    b = agent.select_action(np.zeros((7, S)))
+    assert b.shape == (7, A)
+
+
+def test_sync_python_random_consumes_like_reference():
+    agent = _agent(sync_python_random=True)
+    _fill(agent, 2000)
+    random.seed(123)
+    pre = random.getstate()
+    agent.update_parameters(256)
+    mt = MT19937.from_pystate(pre)
+    sample_indices(mt, 2000, 256)
+    assert random.getstate() == mt.to_pystate()
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    agent = _agent()
+    _fill(agent, 400)
+    for _ in range(3):
+        agent.update_parameters(64)
+    path = str(tmp_path / "ck.pt")
+    agent.save_checkpoint(path, episode=7, total_steps=123)
+    ck = torch.load(path, weights_only=True)
+    for k in ("policy_state_dict", "q1_state_dict", "q1_optimizer_state_dict", "log_alpha",
+              "alpha_optimizer_state_dict", "replay_buffer"):
+        assert k in ck
+    assert float(ck["q1_optimizer_state_dict"]["state"][0]["step"]) == 3.0
+    other = _agent()
+    ep, ts = other.load_checkpoint(path)
+    assert (ep, ts) == (7, 123)
+    assert len(other.replay_buffer) == 400
+    for n in ("policy", "q1", "q2", "q1_target", "q2_target"):
+        a, b = agent._ctx.get_net(n), other._ctx.get_net(n)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (n, k)
+    for n in ("policy", "q1"):
+        assert np.array_equal(agent._ctx.get_net(n, "m")["fc1.weight"],
+                              other._ctx.get_net(n, "m")["fc1.weight"])
+    # both continue identically from the same state and the same sampling stream
+    key, pos = agent._ctx.get_mt(0)
+    other._ctx.set_mt(0, key, pos)
+    from sacmi import _lib as L
+    other._ctx.set_scalar(L.S_NOISE_COUNTER, agent._ctx.get_scalar(L.S_NOISE_COUNTER))
+    assert agent.update_parameters(64) == other.update_parameters(64)
+
+
+def test_loads_shipped_reference_checkpoint_shape():
+    """best_model.pt of the reference (H=256, S=376) has exactly this layout; build the
+    same layout from a fresh agent and load it back through SAC.load."""
+    from sac_imp import SAC
+    torch.manual_seed(0)
+    a = SAC(376, 17, hidden_dim=256, device="cuda", capacity=1000, max_batch=64)
+    sd = {f"{n}_state_dict": getattr(a, n).state_dict()
+          for n in ("policy", "q1", "q2", "q1_target", "q2_target")}
+    sd["alpha"] = torch.tensor([0.0868], requires_grad=True)
+    p = "/tmp/sacmi_bm.pt"
+    torch.save(sd, p)
+    b = SAC(376, 17, hidden_dim=256, device="cuda", capacity=1000, max_batch=64)
+    b.load(p)
+    assert abs(float(b.alpha) - 0.0868) < 1e-7
+    assert torch.equal(b.policy.state_dict()["fc1.weight"], a.policy.state_dict()["fc1.weight"])
+
+
+def test_standalone_replay_buffer_is_random_sample():
+    from replay_buffer import ReplayBuffer
+    rb = ReplayBuffer(capacity=500)
+    for i in range(700):
+        rb.push(np.array([float(i), 0.5]), np.zeros(2, np.float32), float(i), np.zeros(2), False)
+    assert len(rb) == 500
+    random.seed(5)
+    pre = random.getstate()
+    s, a, r, s2, d = rb.sample(32)
+    mt = MT19937.from_pystate(pre)
+    want = sample_indices(mt, 500, 32) + 200          # deque position -> pushed id
+    assert np.array_equal(s[:, 0], want.astype(np.float64))
+    assert random.getstate() == mt.to_pystate()
+    with pytest.raises(ValueError, match="Sample larger than population"):
+        rb.sample(501)

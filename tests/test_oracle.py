@@ -105,3 +105,21 @@ def test_oracle_fp32_bitexact_humanoid(golden_dir):
             pre = f"step{t}.sample."
             if k.startswith(pre):
                 assert np.array_equal(st[k[len(pre):]].reshape(-1)[::stride], z[k]), k
+
+
+@pytest.mark.parametrize("dims", [(24, 4, 64), (376, 17, 256)])
+def test_dropin_networks_init_equals_reference(golden_dir, dims):
+    """networks_model1 drop-in modules, built in SAC.__init__ order under the same torch
+    seed, reproduce the reference's initial weights bit for bit (init_seed3.npz)."""
+    from networks_model1 import GaussianPolicy, QNetwork
+    z = np.load(os.path.join(golden_dir, "init_seed3.npz"))
+    S, A, H = dims
+    torch.manual_seed(3)
+    mods = {"policy": GaussianPolicy(S, A, H)}
+    for n in ("q1", "q2", "q1_target", "q2_target"):
+        mods[n] = QNetwork(S, A, H)
+    mods["q1_target"].load_state_dict(mods["q1"].state_dict())
+    mods["q2_target"].load_state_dict(mods["q2"].state_dict())
+    for n, m in mods.items():
+        for k, v in m.state_dict().items():
+            assert np.array_equal(v.numpy(), z[f"{S}_{A}_{H}.{n}.{k}"]), (n, k)

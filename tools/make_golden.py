@@ -245,6 +245,21 @@ def make_per(out):
     print("per.npz:", len(cases), "cases")
 
 
+def make_init(out):
+    """The reference's own initialisation (nn.Linear + xavier_uniform_/zero bias in
+    SAC.__init__ construction order) under torch.manual_seed(3)."""
+    sac_imp, _ = _ref_modules()
+    blob = {}
+    for (S, A, H) in ((24, 4, 64), (376, 17, 256)):
+        torch.manual_seed(3)
+        agent = sac_imp.SAC(S, A, hidden_dim=H, device="cpu")
+        for n in NETS:
+            for k, v in getattr(agent, n).state_dict().items():
+                blob[f"{S}_{A}_{H}.{n}.{k}"] = v.numpy().copy()
+    np.savez_compressed(os.path.join(out, "init_seed3.npz"), **blob)
+    print("init_seed3.npz")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
@@ -252,7 +267,9 @@ def main():
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     torch.set_num_threads(8)
-    todo = args.only.split(",") if args.only else ["idx", "per", "small", "humanoid"]
+    todo = args.only.split(",") if args.only else ["idx", "per", "small", "humanoid", "init"]
+    if "init" in todo:
+        make_init(args.out)
     if "idx" in todo:
         make_idx(args.out)
     if "per" in todo:
