@@ -92,8 +92,9 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // dependent L2/MALL round trip (~1-2 us), so a wave issues the loads of G chunks at
 // once (with KSPLIT = 16 waves per workgroup and K <= 528 that is ALL of its chunks:
 // one exposed latency per GEMM) and only then runs their MFMAs.
-template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC>
-__device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red) {
+template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM = false>
+__device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
+                                            float* rsum = nullptr) {
   constexpr int MT = TM / 16, NT = TN / 16;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -102,6 +103,9 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float rs[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) rs[i] = 0.f;
   const float* ra[MT];
   const float* rb[NT];
   row_ptrs<MT, AKC>(d.A, d.lda, m0, d.M, lane, ra);
@@ -121,7 +125,13 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
     }
 #pragma unroll
     for (int g = 0; g < G; ++g)
-      if (j + g < nmine) mfma_chunk<MT, NT>(acc, a[g], b[g]);
+      if (j + g < nmine) {
+        mfma_chunk<MT, NT>(acc, a[g], b[g]);
+        if (ROWSUM) {
+#pragma unroll
+          for (int i = 0; i < MT; ++i) rs[i] += (a[g][i][0] + a[g][i][1]) + (a[g][i][2] + a[g][i][3]);
+        }
+      }
   }
   float* my = red + wave * TM * (TN + 1);
   const int rq = (lane >> 4) * 4, cc = lane & 15;
@@ -131,16 +141,28 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
     for (int jj = 0; jj < NT; ++jj)
 #pragma unroll
       for (int r = 0; r < 4; ++r) my[(i * 16 + rq + r) * (TN + 1) + jj * 16 + cc] = acc[i][jj][r];
+  if (ROWSUM) {
+    // lanes l, l+16, l+32, l+48 hold the same row: fold the 4 lane groups, fixed order
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) rsum[wave * TM + i * 16 + lane] = v;
+    }
+  }
 }
 
 // layout dispatch (wave-uniform, once per workgroup)
 template <int TM, int TN, int KSPLIT, int G>
-__device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red) {
+__device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
+                                          float* rsum, bool rowsum) {
   if (d.a_kc) {
     if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true>(d, m0, n0, red);
     else gemm_core_l<TM, TN, KSPLIT, G, true, false>(d, m0, n0, red);
   } else {
     if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true>(d, m0, n0, red);
+    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true>(d, m0, n0, red, rsum);
     else gemm_core_l<TM, TN, KSPLIT, G, false, false>(d, m0, n0, red);
   }
 }
@@ -154,11 +176,57 @@ __device__ __forceinline__ float reduce_partials(const float* red, int row, int 
 }
 
 // ---------------------------------------------------------------------------
+// Adam / Polyak element helpers (torch.optim.Adam single-tensor semantics)
+struct AdamScalars { float step_size, bc2_sqrt; };
+
+// t*(1-tau) + p*tau as three separately rounded fp32 ops, like the reference's tensor
+// expression (sac_imp.py:149) — no FMA contraction, so the result is bit-exact.
+__device__ __forceinline__ float polyak(float t, float p, float omtau, float tau) {
+#pragma clang fp contract(off)
+  const float a = t * omtau;
+  const float b = p * tau;
+  return a + b;
+}
+
+// bias corrections of torch Adam (bc = 1 - beta^t in double, step_size = lr/bc1),
+// from the running products beta^step kept in DevScalars (no pow on the device)
+__device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, int step_idx) {
+  double p1 = a.sc->beta_pow[step_idx][0], p2 = a.sc->beta_pow[step_idx][1];
+  if (a.step_offset) { p1 *= (double)a.beta1; p2 *= (double)a.beta2; }
+  const double bc1 = 1.0 - p1;
+  const double bc2 = 1.0 - p2;
+  return AdamScalars{(float)((double)a.lr / bc1), (float)sqrt(bc2)};
+}
+
+__device__ __forceinline__ AdamScalars fuse_scalars(const AdamFuse& a, int step_idx, int offset) {
+  double p1 = a.sc->beta_pow[step_idx][0], p2 = a.sc->beta_pow[step_idx][1];
+  if (offset) { p1 *= (double)a.beta1; p2 *= (double)a.beta2; }
+  return AdamScalars{(float)((double)a.lr / (1.0 - p1)), (float)sqrt(1.0 - p2)};
+}
+
+// Every op separately rounded (no FMA contraction): the fused-epilogue Adam and the
+// stand-alone Adam kernel then produce identical bits, and the op order is torch's
+// (exp_avg.lerp_, exp_avg_sq.mul_().addcmul_(), sqrt/bc2 + eps, addcdiv_).
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float om_b1,
+                                          float b2, float om_b2, float eps, AdamScalars k) {
+#pragma clang fp contract(off)
+  m = m + om_b1 * (g - m);
+  v = v * b2;
+  v = v + om_b2 * g * g;
+  const float denom = sqrtf(v) / k.bc2_sqrt + eps;
+  p = p + (-k.step_size * m) / denom;
+}
+
+// ---------------------------------------------------------------------------
 // grouped GEMM: one launch runs every independent GEMM of one dependency level.
 // One workgroup (16 waves, K split 16 ways) per output tile, one workgroup per CU.
+// Block 0 of an Adam-fused level also finalises the losses, takes the scalar
+// log_alpha step (alpha = exp(log_alpha), sac_imp.py:128-135) and fills the loss ring.
 template <int TM, int TN, int KSPLIT, int G>
 __global__ __launch_bounds__(64 * KSPLIT) void k_gemm(GemmBatch batch) {
   __shared__ float red[KSPLIT * TM * (TN + 1)];
+  __shared__ float rsum[KSPLIT * TM];
+  __shared__ AdamScalars s_k;
   const int bid = blockIdx.x;
   int p = 0;
   for (int q = 1; q < batch.count; ++q)
@@ -166,16 +234,77 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm(GemmBatch batch) {
   const GemmDesc d = batch.d[p];
   const int t = bid - d.tile_begin;
   const int m0 = (t / d.tiles_n) * TM, n0 = (t % d.tiles_n) * TN;
-  gemm_core<TM, TN, KSPLIT, G>(d, m0, n0, red);
+  const bool adam = d.epi >= EPI_ADAM;
+  const bool rowsum = d.rs_col >= 0 && n0 == 0;
+  if (adam && threadIdx.x == 0)
+    s_k = fuse_scalars(batch.adam, d.adam_step, batch.adam.step_offset);
+  gemm_core<TM, TN, KSPLIT, G>(d, m0, n0, red, rsum, rowsum);
   __syncthreads();
-  for (int e = threadIdx.x; e < TM * TN; e += 64 * KSPLIT) {
-    const int row = e / TN, col = e % TN;
-    const int m = m0 + row, n = n0 + col;
-    if (m >= d.M || n >= d.N) continue;
-    float v = reduce_partials<TM, TN, KSPLIT>(red, row, col);
+  const AdamFuse& af = batch.adam;
+  const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
+  // tile outputs + (rowsum tiles) one extra column: e in [TM*TN, TM*TN + TM)
+  const int ne = TM * TN + (rowsum ? TM : 0);
+  for (int e = threadIdx.x; e < ne; e += 64 * KSPLIT) {
+    int row, n;
+    float v;
+    if (e < TM * TN) {
+      row = e / TN;
+      const int col = e % TN;
+      n = n0 + col;
+      if (m0 + row >= d.M || n >= d.N) continue;
+      v = reduce_partials<TM, TN, KSPLIT>(red, row, col);
+    } else {
+      row = e - TM * TN;
+      n = d.rs_col;
+      if (m0 + row >= d.M) continue;
+      v = rsum[row];
+#pragma unroll
+      for (int w = 1; w < KSPLIT; ++w) v += rsum[w * TM + row];
+    }
+    const int m = m0 + row;
+    const size_t ci = (size_t)m * d.ldc + n;
+    if (adam) {
+      const size_t ai = (size_t)(d.C - af.P) + ci;
+      af.G[ai] = v;
+      float pp = d.C[ci], mm = af.M[ai], vv = af.V[ai];
+      adam_elem(pp, mm, vv, v, omb1, af.beta2, omb2, af.eps, s_k);
+      d.C[ci] = pp; af.M[ai] = mm; af.V[ai] = vv;
+      if (d.epi == EPI_ADAM_POLYAK) {
+        float* tp = af.T + (ai - af.t_base);
+        *tp = polyak(*tp, pp, omtau, af.tau);
+      }
+      continue;
+    }
+    if (d.bias) v += d.bias[(size_t)n * d.bias_ld];
     if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
     else if (d.epi == EPI_MASK) v = d.aux[(size_t)m * d.ldaux + n] > 0.f ? v : 0.f;
-    d.C[(size_t)m * d.ldc + n] = v;
+    d.C[ci] = v;
+  }
+  if (batch.has_adam && bid == 0) {
+    __syncthreads();
+    if (threadIdx.x < af.n_losses) {
+      float sum = 0.f;
+      for (int w = 0; w < af.n_part; ++w) sum += af.loss_part[w * af.n_losses + threadIdx.x];
+      af.sc->losses[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
+    }
+    if (threadIdx.x == 0 && af.log_alpha_idx >= 0 && af.auto_entropy) {
+      const AdamScalars k = fuse_scalars(af, 3, af.step_offset);
+      const int64_t i = af.log_alpha_idx;
+      float pp = af.P[i], mm = af.M[i], vv = af.V[i];
+      adam_elem(pp, mm, vv, *af.log_alpha_grad, omb1, af.beta2, omb2, af.eps, k);
+      af.P[i] = pp; af.M[i] = mm; af.V[i] = vv;
+      af.sc->alpha = expf(pp);
+      af.sc->alpha_is_tensor = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && af.loss_ring) {
+      const int64_t pos = af.sc->loss_ring_pos;
+      const int64_t q = pos % af.ring;
+      af.loss_ring[q * 3 + 0] = af.sc->losses[0];
+      af.loss_ring[q * 3 + 1] = af.sc->losses[1];
+      af.loss_ring[q * 3 + 2] = af.sc->losses[2];
+      af.sc->loss_ring_pos = pos + 1;
+    }
   }
 }
 
@@ -195,8 +324,15 @@ static int assign_tiles(GemmBatch& b) {
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
-  // widest tile that still gives one workgroup to most CUs
-  if (assign_tiles<32, 64>(b) >= 192) {
+  int maxk = 0;
+  for (int i = 0; i < b.count; ++i) maxk = b.d[i].K > maxk ? b.d[i].K : maxk;
+  const int t64 = assign_tiles<32, 64>(b);
+  if (t64 > 256 && maxk <= 16 * 8 * 2) {
+    // many tiles of short K (weight gradients at batch <= 256): 8 waves per tile, two
+    // workgroups per CU, both of a wave's chunks loaded at once
+    hipLaunchKernelGGL((k_gemm<32, 64, 8, 2>), dim3(b.total_tiles), dim3(512), 0, s, b);
+  } else if (t64 >= 192) {
+    // widest tile that still gives one workgroup to most CUs
     hipLaunchKernelGGL((k_gemm<32, 64, 16, 2>), dim3(b.total_tiles), dim3(1024), 0, s, b);
   } else {
     assign_tiles<32, 32>(b);
@@ -251,8 +387,9 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
     const int m = m0 + row;
     float lpe = 0.f;
     if (m < a.rows) {
-      const float mean = reduce_partials<TM, TN, KSPLIT>(red, row, j);
-      const float ls_raw = reduce_partials<TM, TN, KSPLIT>(red, row, A + j);
+      const float mean = reduce_partials<TM, TN, KSPLIT>(red, row, j) + a.Wh[(size_t)j * a.ldw + a.K];
+      const float ls_raw = reduce_partials<TM, TN, KSPLIT>(red, row, A + j) +
+                           a.Wh[(size_t)(A + j) * a.ldw + a.K];
       const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
       const float sd = expf(ls);
       float eps;
@@ -492,36 +629,6 @@ void launch_actor_rows(const ActorRowsArgs& a, hipStream_t s) {
 // and 16-byte aligned), + optional Polyak target update (sac_imp.py:146-152) + loss
 // finalisation + the scalar log_alpha step and alpha = exp(log_alpha)
 // (sac_imp.py:128-135) + the loss ring slot of this update.
-struct AdamScalars { float step_size, bc2_sqrt; };
-
-// t*(1-tau) + p*tau as three separately rounded fp32 ops, like the reference's tensor
-// expression (sac_imp.py:149) — no FMA contraction, so the result is bit-exact.
-__device__ __forceinline__ float polyak(float t, float p, float omtau, float tau) {
-#pragma clang fp contract(off)
-  const float a = t * omtau;
-  const float b = p * tau;
-  return a + b;
-}
-
-// bias corrections of torch Adam (bc = 1 - beta^t in double, step_size = lr/bc1),
-// from the running products beta^step kept in DevScalars (no pow on the device)
-__device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, int step_idx) {
-  double p1 = a.sc->beta_pow[step_idx][0], p2 = a.sc->beta_pow[step_idx][1];
-  if (a.step_offset) { p1 *= (double)a.beta1; p2 *= (double)a.beta2; }
-  const double bc1 = 1.0 - p1;
-  const double bc2 = 1.0 - p2;
-  return AdamScalars{(float)((double)a.lr / bc1), (float)sqrt(bc2)};
-}
-
-__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float om_b1,
-                                          float b2, float om_b2, float eps, AdamScalars k) {
-  m = m + om_b1 * (g - m);
-  v = v * b2;
-  v = v + om_b2 * g * g;
-  const float denom = sqrtf(v) / k.bc2_sqrt + eps;
-  p = p + (-k.step_size * m) / denom;
-}
-
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
   __shared__ AdamScalars s_k[kMaxAdamSegs];
   __shared__ int64_t s_prefix[kMaxAdamSegs + 1];

@@ -277,11 +277,32 @@ static DevScalars download_scalars(sacmi_ctx* c) {
 // one update, enqueued on c->stream.  phase_mask bit p enables phase p.
 static GemmDesc gd(const float* A, int lda, int a_kc, const float* B, int ldb, int b_kc,
                    float* C, int ldc, int M, int N, int K, int epi = EPI_STORE,
-                   const float* aux = nullptr, int ldaux = 0) {
+                   const float* aux = nullptr, int ldaux = 0, int adam_step = 0) {
   GemmDesc d{};
+  d.adam_step = adam_step;
   d.A = A; d.lda = lda; d.a_kc = a_kc;
   d.B = B; d.ldb = ldb; d.b_kc = b_kc;
   d.C = C; d.ldc = ldc; d.M = M; d.N = N; d.K = K; d.epi = epi; d.aux = aux; d.ldaux = ldaux;
+  d.rs_col = -1;
+  return d;
+}
+
+// forward GEMM of a hidden layer (K = H): the bias column H of W~ is added in the
+// epilogue instead of riding in the K loop (keeps K = 32 chunks, balanced over 16 waves)
+static GemmDesc gd_fwd_h(const float* A, int lda, const float* W, int ldw, float* C, int ldc,
+                         int M, int N, int H) {
+  GemmDesc d = gd(A, lda, 1, W, ldw, 1, C, ldc, M, N, H, EPI_RELU);
+  d.bias = W + H;
+  d.bias_ld = ldw;
+  return d;
+}
+
+// weight gradient of a hidden layer: N = H columns by MFMA, the bias column (H) as the
+// row sum of dY (no ninth 64-wide tile for one column)
+static GemmDesc gd_dw_h(const float* dY, int ldy, const float* X, int ldx, float* C, int ldc,
+                        int M, int H, int B, int epi, int step) {
+  GemmDesc d = gd(dY, ldy, 0, X, ldx, 0, C, ldc, M, H, B, epi, nullptr, 0, step);
+  d.rs_col = H;
   return d;
 }
 
@@ -311,7 +332,8 @@ static void validate(const GemmDesc& d) {
   } else {
     check_span(d.B, (int64_t)(d.K - 1) * d.ldb + d.N - 1, "B");
   }
-  if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + d.N - 1, "C");
+  if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C");
+  if (d.bias) check_span(d.bias, (int64_t)(d.N - 1) * d.bias_ld, "bias");
   if (d.epi == EPI_MASK) check_span(d.aux, (int64_t)(d.M - 1) * d.ldaux + d.N - 1, "aux");
 }
 
@@ -404,14 +426,14 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     launch_gemm(l1.b, s);
     // L2
     Level l2;
-    l2.add(gd(c->hp1.p, Hd, 1, W(c->p_fc2), Hd, 1, c->hp2.p, Hd, 2 * B, H, H + 1, EPI_RELU));
+    l2.add(gd_fwd_h(c->hp1.p, Hd, W(c->p_fc2), Hd, c->hp2.p, Hd, 2 * B, H, H));
     for (int i = 0; i < 2; ++i)
-      l2.add(gd(c->hq1.p + i * Hd, 2 * Hd, 1, W(q[i][1]), Hd, 1, c->hq2.p + i * Hd, 2 * Hd, B, H, H + 1, EPI_RELU));
+      l2.add(gd_fwd_h(c->hq1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hq2.p + i * Hd, 2 * Hd, B, H, H));
     mark(c, "gemm_L2_fc2", level_flops(l2.b));
     launch_gemm(l2.b, s);
     // heads + sample for both stacks
     HeadSampleArgs hs{};
-    hs.h = c->hp2.p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H + 1;
+    hs.h = c->hp2.p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
     hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = dev_eps; hs.seed = c->cfg.seed;
     hs.sc = c->sc.p; hs.act = c->x2.p + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
     hs.cache = c->cache.p;
@@ -426,7 +448,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b));
     launch_gemm(l3.b, s);
     for (int i = 0; i < 2; ++i)
-      l4.add(gd(c->hqt1.p + i * Hd, 2 * Hd, 1, Wt(q[i][1]), Hd, 1, c->hqt2.p + i * Hd, 2 * Hd, B, H, H + 1, EPI_RELU));
+      l4.add(gd_fwd_h(c->hqt1.p + i * Hd, 2 * Hd, Wt(q[i][1]), Hd, c->hqt2.p + i * Hd, 2 * Hd, B, H, H));
     mark(c, "gemm_L4_tgt_fc2", level_flops(l4.b));
     launch_gemm(l4.b, s);
     // target / critic loss rows
@@ -439,25 +461,48 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     cr.loss_part = c->lpart_c.p; cr.alpha_grad = G + c->la_idx;
     mark(c, "critic_rows");
     launch_critic_rows(cr, s);
-    // L5: dh1 (relu-masked), dW2~, dW3~
+    // L5: dh1 = (dh2 W2) * relu'(h1)   [+ dW2~, dW3~ when Adam is not fused]
+    const bool fuse = phase_mask == 7;     // single-GPU update: Adam in the dW epilogues
     Level l5;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 2; ++i)
       l5.add(gd(c->dh2.p + i * H, 2 * H, 1, W(q[i][1]), Hd, 0, c->dh1.p + i * H, 2 * H, B, H, H,
                 EPI_MASK, c->hq1.p + i * Hd, 2 * Hd));
-      l5.add(gd(c->dh2.p + i * H, 2 * H, 0, c->hq1.p + i * Hd, 2 * Hd, 0, dW(q[i][1]), Hd, H, H + 1, B));
-      l5.add(gd(c->dq.p + i * B, 1, 0, c->hq2.p + i * Hd, 2 * Hd, 0, dW(q[i][2]), Hd, 1, H + 1, B));
+    // weight gradients of the critics: into the gradient arena, or (fused) straight into
+    // Adam + Polyak on the parameters.  W2 is read by dh1 above, so every critic dW goes
+    // to L6 — in both modes, so the reduction order (and the bits) are the same.
+    Level lw;
+    auto dst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
+    const int wepi = fuse ? EPI_ADAM_POLYAK : EPI_STORE;
+    for (int i = 0; i < 2; ++i) {
+      lw.add(gd_dw_h(c->dh2.p + i * H, 2 * H, c->hq1.p + i * Hd, 2 * Hd, dst(q[i][1]), Hd, H, H, B,
+                     wepi, 1 + i));
+      lw.add(gd_dw_h(c->dq.p + i * B, 1, c->hq2.p + i * Hd, 2 * Hd, dst(q[i][2]), Hd, 1, H, B,
+                     wepi, 1 + i));
     }
-    mark(c, "gemm_L5_critic_bwd2", level_flops(l5.b));
+    mark(c, "gemm_L5_critic_dh1", level_flops(l5.b));
     launch_gemm(l5.b, s);
-    // L6: dW1~
+    // L6: dW1~ (+ dW2~, dW3~ and Adam/Polyak/q-loss when fused)
     Level l6;
     for (int i = 0; i < 2; ++i)
-      l6.add(gd(c->dh1.p + i * H, 2 * H, 0, c->xq.p, Kx, 0, dW(q[i][0]), Kx, H, S + A + 1, B));
-    mark(c, "gemm_L6_critic_dW1", level_flops(l6.b));
+      l6.add(gd(c->dh1.p + i * H, 2 * H, 0, c->xq.p, Kx, 0, dst(q[i][0]), Kx, H, S + A + 1, B,
+                wepi, nullptr, 0, 1 + i));
+    for (int i = 0; i < lw.b.count; ++i) l6.add(lw.b.d[i]);
+    if (fuse) {
+      AdamFuse& f = l6.b.adam;
+      l6.b.has_adam = 1;
+      f.P = P; f.M = c->M.p; f.V = c->V.p; f.T = c->T.p; f.G = G; f.t_base = c->q_begin;
+      f.lr = (float)c->cfg.lr; f.beta1 = 0.9f; f.beta2 = 0.999f; f.eps = 1e-8f;
+      f.tau = (float)c->cfg.tau; f.step_offset = 1; f.sc = c->sc.p;
+      f.loss_part = c->lpart_c.p; f.n_part = nb; f.loss_slot0 = 0; f.n_losses = 2;
+      f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
+    }
+    mark(c, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1", level_flops(l6.b));
     launch_gemm(l6.b, s);
   }
   const float lr = (float)c->cfg.lr;
   if (phase_mask & 2) {
+   const bool fuse = phase_mask == 7;
+   if (!fuse) {
     // critic Adam (+ Polyak, + q-loss finalisation)
     AdamArgs ad{};
     ad.p = P; ad.g = G; ad.m = c->M.p; ad.v = c->V.p; ad.tgt = c->T.p; ad.tgt_base = c->q_begin;
@@ -479,6 +524,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.loss_div = (float)B; ad.log_alpha_idx = -1; ad.auto_entropy = 0;
     mark(c, "adam_critic_polyak");
     launch_adam(ad, s);
+   }
     // L7/L8: updated critics on [s|1|a~]
     const float* xa = c->x2.p + (size_t)B * Kx;
     Level l7, l8;
@@ -487,7 +533,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     mark(c, "gemm_L7_act_fc1", level_flops(l7.b));
     launch_gemm(l7.b, s);
     for (int i = 0; i < 2; ++i)
-      l8.add(gd(c->hqa1.p + i * Hd, 2 * Hd, 1, W(q[i][1]), Hd, 1, c->hqa2.p + i * Hd, 2 * Hd, B, H, H + 1, EPI_RELU));
+      l8.add(gd_fwd_h(c->hqa1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hqa2.p + i * Hd, 2 * Hd, B, H, H));
     mark(c, "gemm_L8_act_fc2", level_flops(l8.b));
     launch_gemm(l8.b, s);
     ActorRowsArgs ar{};
@@ -512,25 +558,39 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     sb.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     mark(c, "gemm_L10_dlda_sample_bwd", 2.0 * B * A * (2.0 * H));
     launch_gemm_sample_bwd(da, sb, s);
-    // L11: dhp2, dW_head~
+    // L11: dhp2 = (dhead Whead) * relu'(hp2);  L12: dhp1 = (dhp2 W2pi) * relu'(hp1);
+    // L13: every policy dW (+ Adam, alpha step, policy loss, loss ring when fused)
     const float* hp2a = c->hp2.p + (size_t)B * Hd;
     const float* hp1a = c->hp1.p + (size_t)B * Hd;
-    Level l11;
+    auto pdst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
+    const int pepi = fuse ? EPI_ADAM : EPI_STORE;
+    Level l11, l12, l13;
     l11.add(gd(c->dhead.p, c->lddh, 1, W(c->p_head), Hd, 0, c->dhp2.p, H, B, H, 2 * A, EPI_MASK, hp2a, Hd));
-    l11.add(gd(c->dhead.p, c->lddh, 0, hp2a, Hd, 0, dW(c->p_head), Hd, 2 * A, H + 1, B));
-    mark(c, "gemm_L11_pi_head_bwd", level_flops(l11.b));
-    launch_gemm(l11.b, s);
-    Level l12;
+    GemmDesc dwh = gd_dw_h(c->dhead.p, c->lddh, hp2a, Hd, pdst(c->p_head), Hd, 2 * A, H, B, pepi, 0);
     l12.add(gd(c->dhp2.p, H, 1, W(c->p_fc2), Hd, 0, c->dhp1.p, H, B, H, H, EPI_MASK, hp1a, Hd));
-    l12.add(gd(c->dhp2.p, H, 0, hp1a, Hd, 0, dW(c->p_fc2), Hd, H, H + 1, B));
-    mark(c, "gemm_L12_pi_fc2_bwd", level_flops(l12.b));
+    GemmDesc dw2 = gd_dw_h(c->dhp2.p, H, hp1a, Hd, pdst(c->p_fc2), Hd, H, H, B, pepi, 0);
+    l13.add(dwh);      // same level structure fused or not: identical reduction order
+    l13.add(dw2);
+    l13.add(gd(c->dhp1.p, H, 0, xa, Kx, 0, pdst(c->p_fc1), c->p_fc1.ld, H, S + 1, B, pepi));
+    if (fuse) {
+      AdamFuse& f = l13.b.adam;
+      l13.b.has_adam = 1;
+      f.P = P; f.M = c->M.p; f.V = c->V.p; f.T = nullptr; f.G = G; f.t_base = 0;
+      f.lr = (float)c->cfg.lr; f.beta1 = 0.9f; f.beta2 = 0.999f; f.eps = 1e-8f; f.tau = 0.f;
+      f.step_offset = 0; f.sc = c->sc.p;
+      f.loss_part = c->lpart_a.p; f.n_part = nb; f.loss_slot0 = 2; f.n_losses = 1;
+      f.loss_div = (float)B; f.log_alpha_idx = c->la_idx; f.auto_entropy = c->cfg.auto_entropy;
+      f.log_alpha_grad = G + c->la_idx;
+      f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
+    }
+    mark(c, "gemm_L11_pi_dhp2", level_flops(l11.b));
+    launch_gemm(l11.b, s);
+    mark(c, "gemm_L12_pi_dhp1", level_flops(l12.b));
     launch_gemm(l12.b, s);
-    Level l13;
-    l13.add(gd(c->dhp1.p, H, 0, xa, Kx, 0, dW(c->p_fc1), c->p_fc1.ld, H, S + 1, B));
-    mark(c, "gemm_L13_pi_dW1", level_flops(l13.b));
+    mark(c, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1", level_flops(l13.b));
     launch_gemm(l13.b, s);
   }
-  if (phase_mask & 4) {
+  if ((phase_mask & 4) && phase_mask != 7) {
     AdamArgs ad{};
     ad.p = P; ad.g = G; ad.m = c->M.p; ad.v = c->V.p; ad.tgt = nullptr;
     ad.nseg = 0;
@@ -1120,10 +1180,10 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     Level l1, l2;
     l1.add(gd(c->x2.p, Kx, 1, c->P.p + c->p_fc1.off, c->p_fc1.ld, 1, c->hp1.p, Hd, n, H, S + 1, EPI_RELU));
     launch_gemm(l1.b, s);
-    l2.add(gd(c->hp1.p, Hd, 1, c->P.p + c->p_fc2.off, Hd, 1, c->hp2.p, Hd, n, H, H + 1, EPI_RELU));
+    l2.add(gd_fwd_h(c->hp1.p, Hd, c->P.p + c->p_fc2.off, Hd, c->hp2.p, Hd, n, H, H));
     launch_gemm(l2.b, s);
     HeadSampleArgs hs{};
-    hs.h = c->hp2.p; hs.Wh = c->P.p + c->p_head.off; hs.rows = n; hs.A = A; hs.K = H + 1;
+    hs.h = c->hp2.p; hs.Wh = c->P.p + c->p_head.off; hs.rows = n; hs.A = A; hs.K = H;
     hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = eps ? 0 : 1; hs.seed = c->cfg.seed;
     hs.sc = c->sc.p; hs.act = c->x2.p + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
     hs.cache = c->cache.p;

@@ -59,7 +59,9 @@ struct DevScalars {
   int64_t loss_ring_pos;
 };
 
-enum Epi { EPI_STORE = 0, EPI_RELU = 1, EPI_MASK = 2 };
+enum Epi { EPI_STORE = 0, EPI_RELU = 1, EPI_MASK = 2,
+           EPI_ADAM = 3,          // C is a parameter tensor: apply Adam with acc as the gradient
+           EPI_ADAM_POLYAK = 4 }; // ... and Polyak-update its target copy
 
 // One GEMM of a grouped launch: C[m,n] = epi( sum_k A(m,k) B(k,n) ).
 //   A(m,k) = a_kc ? A[m*lda + k] : A[k*lda + m]
@@ -74,6 +76,30 @@ struct GemmDesc {
   int lda, ldb, ldc, ldaux;
   int a_kc, b_kc, epi;
   int tiles_n, tile_begin;
+  int adam_step;       // EPI_ADAM*: optimizer step counter index (0 pi, 1 q1, 2 q2)
+  const float* bias;   // forward epilogue: C += bias[n * bias_ld] (before the ReLU)
+  int bias_ld;
+  int rs_col;          // >= 0 (A row-contiguous only): also produce sum_k A(m,k) — the
+                       // bias gradient — into column rs_col of C (n0 == 0 tiles), with
+                       // the same epilogue (store or Adam) as the tile
+};
+
+// Adam fused into weight-gradient epilogues (single-GPU path): the gradient tile never
+// leaves the workgroup.  P/M/V/T arenas mirror each other, so the Adam state of the
+// parameter at C[i] is M[C - P + i], V[...], and its target T[C - P - t_base + i].
+struct AdamFuse {
+  float* P; float* M; float* V; float* T;
+  float* G;            // gradients are also stored (GRAD-slot export)
+  int64_t t_base;
+  float lr, beta1, beta2, eps, tau;
+  int step_idx;        // which optimizer's step counter drives the bias corrections
+  int step_offset;     // t = step + step_offset
+  DevScalars* sc;
+  // block 0 extras
+  const float* loss_part; int n_part, loss_slot0, n_losses; float loss_div;
+  int64_t log_alpha_idx; int auto_entropy;   // scalar alpha Adam (step idx 3), -1: none
+  const float* log_alpha_grad;               // written by k_critic_rows
+  float* loss_ring; int ring;
 };
 
 constexpr int kMaxGemms = 8;
@@ -81,6 +107,8 @@ struct GemmBatch {
   GemmDesc d[kMaxGemms];
   int count;
   int total_tiles;
+  AdamFuse adam;       // used when any desc has epi >= EPI_ADAM
+  int has_adam;
 };
 
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked
@@ -88,7 +116,7 @@ struct GemmBatch {
 struct HeadSampleArgs {
   const float* h;        // [rows, ldh] policy hidden (h~ incl. ones col)
   const float* Wh;       // [2A, ldw] head weights (mean rows ; log_std rows)
-  int rows, A, K, ldh, ldw;
+  int rows, A, K, ldh, ldw;   // K = H: the bias (column K of Wh) is added in the epilogue
   float* eps;            // [rows, A] standard normals (read, or written when gen)
   int gen_eps;           // 1: Philox noise
   uint64_t seed;
