@@ -84,18 +84,27 @@ def init_agent(ctx, seed):
     ctx.set_net("q2_target", q_sd["q2"])
 
 
-def gemm_roofline(ctx, batch, iters=20):
-    sites = ctx.profile_step(batch, iters)
-    g = [(n, ms, f) for (n, ms, f) in sites if n.startswith("gemm_") or n == "heads_sample"]
-    tot_ms = sum(ms for _, ms, _ in sites)
-    gemm = [(n, ms, f) for (n, ms, f) in sites if n.startswith("gemm_")]
-    gms = sum(ms for _, ms, _ in gemm)
+# launch sites whose kernel is the grouped GEMM `sacmi::k_gemm<TM,TN,KSPLIT,G>` (L10 is
+# k_gemm_sample_bwd, a different kernel)
+def _is_k_gemm(site):
+    return site.startswith("gemm_L") and not site.startswith("gemm_L10")
+
+
+def gemm_roofline(ctx, batch, reps=50):
+    """Dominant kernel = k_gemm.  Every launch site is replayed alone `reps` times in
+    one hipGraph and timed with HIP events on the context stream (the stream every
+    update kernel is launched on): achieved = algorithmic FLOPs per launch / mean
+    launch duration, over the k_gemm sites of one update."""
+    sites = ctx.profile_sites(batch, reps)
+    gemm = [(n, us, f) for (n, us, f) in sites if _is_k_gemm(n)]
+    gus = sum(us for _, us, _ in gemm)
     gfl = sum(f for _, _, f in gemm)
     launches = len(gemm)
-    avg_ms = gms / launches
-    achieved = (gfl / launches) / (avg_ms * 1e-3) / 1e12
-    return dict(sites=sites, step_ms_eager=tot_ms, gemm_ms=gms, gemm_flops=gfl,
-                launches=launches, avg_launch_ms=avg_ms, achieved_tflops=achieved), g
+    avg_us = gus / launches
+    achieved = (gfl / launches) / (avg_us * 1e-6) / 1e12
+    return dict(sites=sites, sites_sum_us=sum(us for _, us, _ in sites), gemm_us=gus,
+                gemm_flops=gfl, launches=launches, avg_launch_us=avg_us,
+                achieved_tflops=achieved)
 
 
 def cpu_baseline(rows, seconds=15.0, warmup=5):
@@ -153,6 +162,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--updates-per-launch", type=int, default=20,
+                    help="updates per device launch (trainer.py updates_per_step loop)")
     ap.add_argument("--profile-only", action="store_true",
                     help="just run warmup+steps (for rocprofv3 runs)")
     args = ap.parse_args()
@@ -179,13 +190,23 @@ def main():
             rows_keep = rows
     t_fill = time.perf_counter() - t_fill
 
-    for _ in range(args.warmup):
-        ctx.step_async(args.batch)
+    upl = max(1, min(args.updates_per_launch, 256))
+
+    def run_updates(n):
+        # the trainer's `for _ in range(updates_per_step)` loop: `upl` updates per launch
+        full, rem = divmod(n, upl)
+        for _ in range(full):
+            ctx.step_many_async(args.batch, upl)
+        if rem:
+            ctx.step_many_async(args.batch, rem)
+
+    run_updates(args.warmup)
+    if args.steps % upl:
+        ctx.step_many_async(args.batch, args.steps % upl)     # build that graph untimed
     ctx.synchronize()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.step_async(args.batch)
+    run_updates(args.steps)
     losses = ctx.fetch_losses(args.steps)      # D2H of every loss, inside the timed region
     ctx.synchronize()
     torch.cuda.synchronize()
@@ -196,7 +217,17 @@ def main():
         return
     sps = args.steps / dt
 
-    # API-faithful mode: losses synced every step (sac_imp.py:140-144 .item())
+    # one update per launch (update_parameters_async), and the API-faithful mode with
+    # the losses synced every update (sac_imp.py:140-144 .item())
+    n_one = max(50, args.steps // 2)
+    ctx.step_async(args.batch)
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(n_one):
+        ctx.step_async(args.batch)
+    ctx.fetch_losses(n_one)
+    ctx.synchronize()
+    one_sps = n_one / (time.perf_counter() - t1)
     n_sync = max(20, args.steps // 4)
     t1 = time.perf_counter()
     for _ in range(n_sync):
@@ -205,16 +236,17 @@ def main():
 
     roof = None
     if not args.no_roofline:
-        info, _ = gemm_roofline(ctx, args.batch)
+        info = gemm_roofline(ctx, args.batch)
         roof = {"bound": "mfma", "achieved": round(info["achieved_tflops"], 3),
                 "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(info["achieved_tflops"] / PEAK_FP32_MFMA_TFLOPS, 4),
-                "traffic": None, "kernel": "k_gemm<32,32,4> (grouped fp32 MFMA GEMM)",
+                "traffic": None,
+                "kernel": "sacmi::k_gemm (grouped fp32 MFMA GEMM, all tile configs)",
                 "launches_per_step": info["launches"],
-                "avg_launch_us": round(info["avg_launch_ms"] * 1e3, 3),
+                "avg_launch_us": round(info["avg_launch_us"], 3),
                 "gemm_flops_per_step": info["gemm_flops"],
-                "eager_step_us": round(info["step_ms_eager"] * 1e3, 2),
-                "sites_us": {n: round(ms * 1e3, 2) for (n, ms, _) in info["sites"]}}
+                "sites_sum_us": round(info["sites_sum_us"], 2),
+                "sites_us": {n: round(us, 2) for (n, us, _) in info["sites"]}}
     flops = necessary_flops(S_DIM, A_DIM, HIDDEN, args.batch)
     cpu = None
     if not args.no_cpu_baseline:
@@ -230,6 +262,8 @@ def main():
                                "uniform replay (HBM ring, device random.sample)",
                    "state_dim": S_DIM, "action_dim": A_DIM, "hidden": HIDDEN,
                    "global_batch": args.batch, "replay_fill": fill, "parallelism": "single GPU"},
+        "updates_per_launch": upl,
+        "one_update_per_launch_steps_per_s": round(one_sps, 2),
         "api_faithful_steps_per_s": round(sync_sps, 2),
         "mfma_util_step": round(flops * sps / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
         "necessary_gflop_per_step": round(flops / 1e9, 4),

@@ -20,6 +20,25 @@
 
 namespace sacmi {
 
+// Diagnostic timestamps (tools/gemm_bench.hip builds with SACMI_DIAG_STAMPS; the library
+// build compiles them away): per workgroup, per wave, 100 MHz real-time counter.
+#ifdef SACMI_DIAG_STAMPS
+__device__ unsigned long long g_stamps[4096][40];
+#define SACMI_STAMP(slot)                                                            \
+  do {                                                                              \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                             \
+      g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();                \
+      if ((slot) == 0)                                                              \
+        g_stamps[blockIdx.x][34] =                                                  \
+            ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |  \
+            __builtin_amdgcn_s_getreg((31 << 11) | 4);                              \
+    }                                                                               \
+  } while (0)
+#else
+#define SACMI_STAMP(slot) do { } while (0)
+#endif
+
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 
@@ -98,6 +117,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   constexpr int MT = TM / 16, NT = TN / 16;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  SACMI_STAMP(wave);
   f4 acc[MT][NT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -133,6 +153,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
         }
       }
   }
+  SACMI_STAMP(16 + wave);
   float* my = red + wave * TM * (TN + 1);
   const int rq = (lane >> 4) * 4, cc = lane & 15;
 #pragma unroll
@@ -223,7 +244,7 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // Block 0 of an Adam-fused level also finalises the losses, takes the scalar
 // log_alpha step (alpha = exp(log_alpha), sac_imp.py:128-135) and fills the loss ring.
 template <int TM, int TN, int KSPLIT, int G>
-__global__ __launch_bounds__(64 * KSPLIT) void k_gemm(GemmBatch batch) {
+__global__ __launch_bounds__(64 * KSPLIT, 4) void k_gemm(GemmBatch batch) {
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   __shared__ float rsum[KSPLIT * TM];
   __shared__ AdamScalars s_k;
@@ -240,46 +261,79 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm(GemmBatch batch) {
     s_k = fuse_scalars(batch.adam, d.adam_step, batch.adam.step_offset);
   gemm_core<TM, TN, KSPLIT, G>(d, m0, n0, red, rsum, rowsum);
   __syncthreads();
+  if (threadIdx.x < 64) SACMI_STAMP(32);
   const AdamFuse& af = batch.adam;
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
-  // tile outputs + (rowsum tiles) one extra column: e in [TM*TN, TM*TN + TM)
-  const int ne = TM * TN + (rowsum ? TM : 0);
-  for (int e = threadIdx.x; e < ne; e += 64 * KSPLIT) {
-    int row, n;
-    float v;
-    if (e < TM * TN) {
+  // Element slots: EPT tile outputs per thread (e = tid + s*NTH) plus one slot for the
+  // rowsum (bias-gradient) column. All global loads of all slots are issued before any
+  // compute or store, so a thread waits for memory once, not once per element.
+  constexpr int NTH = 64 * KSPLIT, EPT = TM * TN / NTH, NS = EPT + 1;
+  static_assert(TM * TN % NTH == 0 && TM <= NTH, "epilogue slot layout");
+  const int tid = threadIdx.x;
+  float v[NS];
+  size_t ci[NS];
+  bool ok[NS];
+  int nn[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int row;
+    if (s < EPT) {
+      const int e = tid + s * NTH;
       row = e / TN;
       const int col = e % TN;
-      n = n0 + col;
-      if (m0 + row >= d.M || n >= d.N) continue;
-      v = reduce_partials<TM, TN, KSPLIT>(red, row, col);
+      nn[s] = n0 + col;
+      ok[s] = m0 + row < d.M && nn[s] < d.N;
+      v[s] = reduce_partials<TM, TN, KSPLIT>(red, row, col);
     } else {
-      row = e - TM * TN;
-      n = d.rs_col;
-      if (m0 + row >= d.M) continue;
-      v = rsum[row];
+      row = tid < TM ? tid : 0;
+      nn[s] = d.rs_col;
+      ok[s] = rowsum && tid < TM && m0 + row < d.M;
+      float r = rsum[row];
 #pragma unroll
-      for (int w = 1; w < KSPLIT; ++w) v += rsum[w * TM + row];
+      for (int w = 1; w < KSPLIT; ++w) r += rsum[w * TM + row];
+      v[s] = r;
     }
-    const int m = m0 + row;
-    const size_t ci = (size_t)m * d.ldc + n;
-    if (adam) {
-      const size_t ai = (size_t)(d.C - af.P) + ci;
-      af.G[ai] = v;
-      float pp = d.C[ci], mm = af.M[ai], vv = af.V[ai];
-      adam_elem(pp, mm, vv, v, omb1, af.beta2, omb2, af.eps, s_k);
-      d.C[ci] = pp; af.M[ai] = mm; af.V[ai] = vv;
-      if (d.epi == EPI_ADAM_POLYAK) {
-        float* tp = af.T + (ai - af.t_base);
-        *tp = polyak(*tp, pp, omtau, af.tau);
-      }
-      continue;
-    }
-    if (d.bias) v += d.bias[(size_t)n * d.bias_ld];
-    if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
-    else if (d.epi == EPI_MASK) v = d.aux[(size_t)m * d.ldaux + n] > 0.f ? v : 0.f;
-    d.C[ci] = v;
+    ci[s] = (size_t)(m0 + row) * d.ldc + nn[s];
   }
+  if (adam) {
+    const bool pol = d.epi == EPI_ADAM_POLYAK;
+    const size_t base = (size_t)(d.C - af.P);
+    float pp[NS], mm[NS], vv[NS], tt[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (!ok[s]) continue;
+      const size_t ai = base + ci[s];
+      pp[s] = d.C[ci[s]]; mm[s] = af.M[ai]; vv[s] = af.V[ai];
+      if (pol) tt[s] = af.T[ai - af.t_base];
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (!ok[s]) continue;
+      const size_t ai = base + ci[s];
+      adam_elem(pp[s], mm[s], vv[s], v[s], omb1, af.beta2, omb2, af.eps, s_k);
+      if (af.G) af.G[ai] = v[s];
+      d.C[ci[s]] = pp[s]; af.M[ai] = mm[s]; af.V[ai] = vv[s];
+      if (pol) af.T[ai - af.t_base] = polyak(tt[s], pp[s], omtau, af.tau);
+    }
+  } else {
+    float bx[NS], ax[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (!ok[s]) continue;
+      if (d.bias) bx[s] = d.bias[(size_t)nn[s] * d.bias_ld];
+      if (d.epi == EPI_MASK) ax[s] = d.aux[(ci[s] / d.ldc) * d.ldaux + nn[s]];
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (!ok[s]) continue;
+      float x = v[s];
+      if (d.bias) x += bx[s];
+      if (d.epi == EPI_RELU) x = x > 0.f ? x : 0.f;
+      else if (d.epi == EPI_MASK) x = ax[s] > 0.f ? x : 0.f;
+      d.C[ci[s]] = x;
+    }
+  }
+  if (threadIdx.x < 64) SACMI_STAMP(33);
   if (batch.has_adam && bid == 0) {
     __syncthreads();
     if (threadIdx.x < af.n_losses) {

@@ -71,9 +71,10 @@ struct DevBuf {
 struct GraphKey {
   int batch, dev_idx, dev_eps, phase_mask, ring;
   int64_t per_len;   // PER launch geometry depends on the fill
+  int reps;          // consecutive updates in one graph
   bool operator<(const GraphKey& o) const {
-    return std::tie(batch, dev_idx, dev_eps, phase_mask, ring, per_len) <
-           std::tie(o.batch, o.dev_idx, o.dev_eps, o.phase_mask, o.ring, o.per_len);
+    return std::tie(batch, dev_idx, dev_eps, phase_mask, ring, per_len, reps) <
+           std::tie(o.batch, o.dev_idx, o.dev_eps, o.phase_mask, o.ring, o.per_len, o.reps);
   }
 };
 
@@ -84,6 +85,7 @@ struct sacmi_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  bool keep_grads = false;             // SACMI_S_KEEP_GRADS
   int S = 0, A = 0, H = 0, Bm = 0;
   int Kx = 0, Hd = 0, Kp1 = 0, lddh = 0;
   // layout
@@ -122,6 +124,9 @@ struct sacmi_ctx {
   uint64_t act_calls = 0;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
   // profiling (sacmi_profile_step): one event per launch site
   bool prof = false;
+  bool prof_collect = false;   // record site names/FLOPs without events
+  int prof_site = -1;          // >= 0: enqueue only this launch site
+  int site_counter = 0;        // launch sites seen by the current enqueue_update
   std::vector<std::string> prof_names;
   std::vector<double> prof_flops;
   std::vector<hipEvent_t> prof_events;
@@ -172,6 +177,7 @@ static void build_layout(sacmi_ctx* c) {
   take(c->q_fc[1][2], 1, H, c->Hd, H, H, true);
   off = round_up64(off, 64);
   c->q_end = off;
+  REQUIRE((c->q_end - c->q_begin) % 4 == 0 && c->q_begin % 4 == 0, SACMI_ESTATE, "critic region not float4-aligned");
   c->pi_begin = off;
   take(c->p_fc1, H, S, c->Kp1, S, S, true);
   take(c->p_fc2, H, H, c->Hd, H, H, true);
@@ -358,14 +364,22 @@ static double level_flops(const GemmBatch& b) {
 }
 
 // profiling mark: records an event BEFORE the launch it names
-static void mark(sacmi_ctx* c, const char* name, double flops = 0) {
-  if (!c->prof) return;
-  hipEvent_t e;
-  CHECK_HIP(hipEventCreate(&e));
-  CHECK_HIP(hipEventRecord(e, c->stream));
-  c->prof_events.push_back(e);
-  c->prof_names.push_back(name);
-  c->prof_flops.push_back(flops);
+// Hook in front of every launch site of the update.  Returns whether the site's
+// kernels are enqueued: always, except in site-isolation mode (prof_site >= 0), where
+// only site number prof_site runs (sacmi_profile_sites).
+static bool mark(sacmi_ctx* c, const char* name, double flops = 0) {
+  const int site = c->site_counter++;
+  if (c->prof || c->prof_collect) {
+    c->prof_names.push_back(name);
+    c->prof_flops.push_back(flops);
+  }
+  if (c->prof) {
+    hipEvent_t e;
+    CHECK_HIP(hipEventCreate(&e));
+    CHECK_HIP(hipEventRecord(e, c->stream));
+    c->prof_events.push_back(e);
+  }
+  return c->prof_site < 0 || site == c->prof_site;
 }
 
 static PerArgs per_args(sacmi_ctx* c, int k, int gen_u) {
@@ -383,6 +397,7 @@ static PerArgs per_args(sacmi_ctx* c, int k, int gen_u) {
 static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
                            float grad_scale, bool use_ring) {
   hipStream_t s = c->stream;
+  c->site_counter = 0;
   const int S = c->S, A = c->A, H = c->H, Kx = c->Kx, Hd = c->Hd;
   float* P = c->P.p;
   float* G = c->G.p;
@@ -396,8 +411,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   if (phase_mask & 1) {
     const bool per = c->cfg.replay_kind == SACMI_REPLAY_PER;
     if (dev_idx && per) {
-      mark(c, "per_sample");
-      launch_per_sample(per_args(c, B, 1), s);
+      if (mark(c, "per_sample")) launch_per_sample(per_args(c, B, 1), s);
     } else if (dev_idx) {
       MtSampleArgs m{};
       m.mt = c->mt.p; m.sc = c->sc.p; m.k = B;
@@ -405,8 +419,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       int setsize = 21;
       if (k > 5) setsize += (int)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
       m.setsize = setsize; m.idx_out = c->idx32.p; m.idx64_out = c->idx64.p;
-      mark(c, "mt_sample");
-      launch_mt_sample(m, s);
+      if (mark(c, "mt_sample")) launch_mt_sample(m, s);
     }
     GatherArgs g{};
     g.idx = c->idx32.p; g.obs = c->obs.p; g.act = c->act.p; g.rew = c->rew.p; g.obs2 = c->obs2.p;
@@ -414,23 +427,20 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     g.sc = c->sc.p; g.S = S; g.A = A; g.B = B; g.xq = c->xq.p; g.x2 = c->x2.p; g.ldx = Kx;
     g.r = c->r.p; g.d = c->d.p;
     g.by_slot = per ? 1 : 0;
-    mark(c, "gather");
-    launch_gather(g, s);
+    if (mark(c, "gather")) launch_gather(g, s);
 
     // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
     Level l1;
     l1.add(gd(c->x2.p, Kx, 1, W(c->p_fc1), c->p_fc1.ld, 1, c->hp1.p, Hd, 2 * B, H, S + 1, EPI_RELU));
     for (int i = 0; i < 2; ++i)
       l1.add(gd(c->xq.p, Kx, 1, W(q[i][0]), Kx, 1, c->hq1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    mark(c, "gemm_L1_fc1", level_flops(l1.b));
-    launch_gemm(l1.b, s);
+    if (mark(c, "gemm_L1_fc1", level_flops(l1.b))) launch_gemm(l1.b, s);
     // L2
     Level l2;
     l2.add(gd_fwd_h(c->hp1.p, Hd, W(c->p_fc2), Hd, c->hp2.p, Hd, 2 * B, H, H));
     for (int i = 0; i < 2; ++i)
       l2.add(gd_fwd_h(c->hq1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hq2.p + i * Hd, 2 * Hd, B, H, H));
-    mark(c, "gemm_L2_fc2", level_flops(l2.b));
-    launch_gemm(l2.b, s);
+    if (mark(c, "gemm_L2_fc2", level_flops(l2.b))) launch_gemm(l2.b, s);
     // heads + sample for both stacks
     HeadSampleArgs hs{};
     hs.h = c->hp2.p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
@@ -439,18 +449,15 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     hs.cache = c->cache.p;
     hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
-    mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * (H + 1));
-    launch_heads_sample(hs, s);
+    if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * (H + 1))) launch_heads_sample(hs, s);
     // L3/L4: target critics on [s2|1|a']
     Level l3, l4;
     for (int i = 0; i < 2; ++i)
       l3.add(gd(c->x2.p, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b));
-    launch_gemm(l3.b, s);
+    if (mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b))) launch_gemm(l3.b, s);
     for (int i = 0; i < 2; ++i)
       l4.add(gd_fwd_h(c->hqt1.p + i * Hd, 2 * Hd, Wt(q[i][1]), Hd, c->hqt2.p + i * Hd, 2 * Hd, B, H, H));
-    mark(c, "gemm_L4_tgt_fc2", level_flops(l4.b));
-    launch_gemm(l4.b, s);
+    if (mark(c, "gemm_L4_tgt_fc2", level_flops(l4.b))) launch_gemm(l4.b, s);
     // target / critic loss rows
     CriticRowsArgs cr{};
     cr.hq2 = c->hq2.p; cr.hqt2 = c->hqt2.p; cr.ldh = Hd; cr.H = H; cr.B = B;
@@ -459,8 +466,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     cr.gamma = (float)c->cfg.gamma; cr.target_entropy = (float)(-A);
     cr.auto_entropy = c->cfg.auto_entropy; cr.sc = c->sc.p; cr.dq = c->dq.p; cr.dh2 = c->dh2.p;
     cr.loss_part = c->lpart_c.p; cr.alpha_grad = G + c->la_idx;
-    mark(c, "critic_rows");
-    launch_critic_rows(cr, s);
+    if (mark(c, "critic_rows")) launch_critic_rows(cr, s);
     // L5: dh1 = (dh2 W2) * relu'(h1)   [+ dW2~, dW3~ when Adam is not fused]
     const bool fuse = phase_mask == 7;     // single-GPU update: Adam in the dW epilogues
     Level l5;
@@ -479,8 +485,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       lw.add(gd_dw_h(c->dq.p + i * B, 1, c->hq2.p + i * Hd, 2 * Hd, dst(q[i][2]), Hd, 1, H, B,
                      wepi, 1 + i));
     }
-    mark(c, "gemm_L5_critic_dh1", level_flops(l5.b));
-    launch_gemm(l5.b, s);
+    if (mark(c, "gemm_L5_critic_dh1", level_flops(l5.b))) launch_gemm(l5.b, s);
     // L6: dW1~ (+ dW2~, dW3~ and Adam/Polyak/q-loss when fused)
     Level l6;
     for (int i = 0; i < 2; ++i)
@@ -490,14 +495,14 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     if (fuse) {
       AdamFuse& f = l6.b.adam;
       l6.b.has_adam = 1;
-      f.P = P; f.M = c->M.p; f.V = c->V.p; f.T = c->T.p; f.G = G; f.t_base = c->q_begin;
+      f.P = P; f.M = c->M.p; f.V = c->V.p; f.T = c->T.p; f.G = c->keep_grads ? G : nullptr;
+      f.t_base = c->q_begin;
       f.lr = (float)c->cfg.lr; f.beta1 = 0.9f; f.beta2 = 0.999f; f.eps = 1e-8f;
       f.tau = (float)c->cfg.tau; f.step_offset = 1; f.sc = c->sc.p;
       f.loss_part = c->lpart_c.p; f.n_part = nb; f.loss_slot0 = 0; f.n_losses = 2;
       f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
     }
-    mark(c, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1", level_flops(l6.b));
-    launch_gemm(l6.b, s);
+    if (mark(c, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1", level_flops(l6.b))) launch_gemm(l6.b, s);
   }
   const float lr = (float)c->cfg.lr;
   if (phase_mask & 2) {
@@ -522,33 +527,28 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.tau = (float)c->cfg.tau; ad.step_offset = 1; ad.sc = c->sc.p;
     ad.loss_part = c->lpart_c.p; ad.n_part = nb; ad.loss_slot0 = 0; ad.n_losses = 2;
     ad.loss_div = (float)B; ad.log_alpha_idx = -1; ad.auto_entropy = 0;
-    mark(c, "adam_critic_polyak");
-    launch_adam(ad, s);
+    if (mark(c, "adam_critic_polyak")) launch_adam(ad, s);
    }
     // L7/L8: updated critics on [s|1|a~]
     const float* xa = c->x2.p + (size_t)B * Kx;
     Level l7, l8;
     for (int i = 0; i < 2; ++i)
       l7.add(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, c->hqa1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    mark(c, "gemm_L7_act_fc1", level_flops(l7.b));
-    launch_gemm(l7.b, s);
+    if (mark(c, "gemm_L7_act_fc1", level_flops(l7.b))) launch_gemm(l7.b, s);
     for (int i = 0; i < 2; ++i)
       l8.add(gd_fwd_h(c->hqa1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hqa2.p + i * Hd, 2 * Hd, B, H, H));
-    mark(c, "gemm_L8_act_fc2", level_flops(l8.b));
-    launch_gemm(l8.b, s);
+    if (mark(c, "gemm_L8_act_fc2", level_flops(l8.b))) launch_gemm(l8.b, s);
     ActorRowsArgs ar{};
     ar.hqa2 = c->hqa2.p; ar.ldh = Hd; ar.H = H; ar.B = B; ar.w3 = W(q[0][2]);
     ar.w3_stride = (int)(q[1][2].off - q[0][2].off); ar.logp_a = c->logp.p + B; ar.sc = c->sc.p;
     ar.dha2 = c->dha2.p; ar.loss_part = c->lpart_a.p;
-    mark(c, "actor_rows");
-    launch_actor_rows(ar, s);
+    if (mark(c, "actor_rows")) launch_actor_rows(ar, s);
     // L9: dha1
     Level l9;
     for (int i = 0; i < 2; ++i)
       l9.add(gd(c->dha2.p + i * H, 2 * H, 1, W(q[i][1]), Hd, 0, c->dha1.p + i * H, 2 * H, B, H, H,
                 EPI_MASK, c->hqa1.p + i * Hd, 2 * Hd));
-    mark(c, "gemm_L9_act_dh1", level_flops(l9.b));
-    launch_gemm(l9.b, s);
+    if (mark(c, "gemm_L9_act_dh1", level_flops(l9.b))) launch_gemm(l9.b, s);
     // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
     GemmDesc da = gd(c->dha1.p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
     validate(da);
@@ -556,8 +556,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     sb.cache = c->cache.p + (size_t)B * 3 * A; sb.eps = c->eps.p + (size_t)B * A;
     sb.dhead = c->dhead.p; sb.lddh = c->lddh; sb.A = A; sb.B = B; sb.sc = c->sc.p;
     sb.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
-    mark(c, "gemm_L10_dlda_sample_bwd", 2.0 * B * A * (2.0 * H));
-    launch_gemm_sample_bwd(da, sb, s);
+    if (mark(c, "gemm_L10_dlda_sample_bwd", 2.0 * B * A * (2.0 * H))) launch_gemm_sample_bwd(da, sb, s);
     // L11: dhp2 = (dhead Whead) * relu'(hp2);  L12: dhp1 = (dhp2 W2pi) * relu'(hp1);
     // L13: every policy dW (+ Adam, alpha step, policy loss, loss ring when fused)
     const float* hp2a = c->hp2.p + (size_t)B * Hd;
@@ -575,7 +574,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     if (fuse) {
       AdamFuse& f = l13.b.adam;
       l13.b.has_adam = 1;
-      f.P = P; f.M = c->M.p; f.V = c->V.p; f.T = nullptr; f.G = G; f.t_base = 0;
+      f.P = P; f.M = c->M.p; f.V = c->V.p; f.T = nullptr; f.G = c->keep_grads ? G : nullptr;
+      f.t_base = 0;
       f.lr = (float)c->cfg.lr; f.beta1 = 0.9f; f.beta2 = 0.999f; f.eps = 1e-8f; f.tau = 0.f;
       f.step_offset = 0; f.sc = c->sc.p;
       f.loss_part = c->lpart_a.p; f.n_part = nb; f.loss_slot0 = 2; f.n_losses = 1;
@@ -583,12 +583,9 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.log_alpha_grad = G + c->la_idx;
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
     }
-    mark(c, "gemm_L11_pi_dhp2", level_flops(l11.b));
-    launch_gemm(l11.b, s);
-    mark(c, "gemm_L12_pi_dhp1", level_flops(l12.b));
-    launch_gemm(l12.b, s);
-    mark(c, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1", level_flops(l13.b));
-    launch_gemm(l13.b, s);
+    if (mark(c, "gemm_L11_pi_dhp2", level_flops(l11.b))) launch_gemm(l11.b, s);
+    if (mark(c, "gemm_L12_pi_dhp1", level_flops(l12.b))) launch_gemm(l12.b, s);
+    if (mark(c, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1", level_flops(l13.b))) launch_gemm(l13.b, s);
   }
   if ((phase_mask & 4) && phase_mask != 7) {
     AdamArgs ad{};
@@ -606,26 +603,28 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.loss_part = c->lpart_a.p; ad.n_part = nb; ad.loss_slot0 = 2; ad.n_losses = 1;
     ad.loss_div = (float)B; ad.log_alpha_idx = c->la_idx; ad.auto_entropy = c->cfg.auto_entropy;
     ad.loss_ring = use_ring ? c->ring.p : nullptr; ad.ring = c->ring_slots;
-    mark(c, "adam_actor_alpha");
-    launch_adam(ad, s);
+    if (mark(c, "adam_actor_alpha")) launch_adam(ad, s);
   }
 }
 
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
-                       float grad_scale, bool use_ring) {
+                       float grad_scale, bool use_ring, int reps = 1) {
   if (!c->use_graphs) {
-    enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring);
+    for (int r = 0; r < reps; ++r)
+      enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring);
     CHECK_HIP(hipGetLastError());
     return;
   }
-  GraphKey key{B, dev_idx, dev_eps, phase_mask | (grad_scale != 1.f ? 8 : 0), use_ring ? c->ring_slots : 0,
-               c->cfg.replay_kind == SACMI_REPLAY_PER ? c->len : 0};
+  GraphKey key{B, dev_idx, dev_eps,
+               phase_mask | (grad_scale != 1.f ? 8 : 0) | (c->keep_grads ? 16 : 0), use_ring ? c->ring_slots : 0,
+               c->cfg.replay_kind == SACMI_REPLAY_PER ? c->len : 0, reps};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g;
     CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     try {
-      enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring);
+      for (int r = 0; r < reps; ++r)
+        enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring);
     } catch (...) {
       (void)hipStreamEndCapture(c->stream, &g);
       throw;
@@ -837,6 +836,14 @@ static void scalar_io(sacmi_ctx* c, int which, const double* in, double* out) {
     case SACMI_S_ADAM_M_LOG_ALPHA: arena_scalar(c, c->M.p, c->la_idx, in, out); return;
     case SACMI_S_ADAM_V_LOG_ALPHA: arena_scalar(c, c->V.p, c->la_idx, in, out); return;
     case SACMI_S_GRAD_LOG_ALPHA: arena_scalar(c, c->G.p, c->la_idx, in, out); return;
+    case SACMI_S_KEEP_GRADS:
+      if (in) {
+        if (c->keep_grads != (*in != 0)) destroy_graphs(c);
+        c->keep_grads = *in != 0;
+      } else {
+        *out = c->keep_grads ? 1.0 : 0.0;
+      }
+      return;
     default: break;
   }
   DevScalars h = download_scalars(c);
@@ -1013,6 +1020,15 @@ int sacmi_step_async(sacmi_ctx* c, int32_t batch) {
   });
 }
 
+int sacmi_step_many_async(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
+  return guard([&] {
+    check_batch(c, batch);
+    REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
+    REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
+    run_update(c, batch, 1, 1, 7, 1.f, true, n_updates);
+  });
+}
+
 int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_out) {
   return guard([&] {
     DevScalars h = download_scalars(c);
@@ -1079,7 +1095,7 @@ int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_o
       c->prof_events.clear(); c->prof_names.clear(); c->prof_flops.clear();
       try {
         enqueue_update(c, batch, 1, 1, 7, 1.f, false);
-        mark(c, "end");
+        (void)mark(c, "end");
       } catch (...) {
         c->prof = false;
         throw;
@@ -1103,6 +1119,64 @@ int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_o
       ms_out[i] = (float)(acc[i] / iters);
       flops_out[i] = fl[i];
     }
+    *n_sites = n;
+  });
+}
+
+int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_out,
+                        float* us_out, double* flops_out, int32_t max_sites, int32_t* n_sites) {
+  return guard([&] {
+    check_batch(c, batch);
+    REQUIRE(reps > 0 && reps <= 1000, SACMI_EVALUE, "reps must be in [1, 1000]");
+    // enumerate the sites of the fused single-GPU update without launching anything
+    c->prof_names.clear(); c->prof_flops.clear();
+    c->prof_collect = true;
+    c->prof_site = 1 << 30;
+    try {
+      enqueue_update(c, batch, 1, 1, 7, 1.f, false);
+    } catch (...) {
+      c->prof_collect = false; c->prof_site = -1;
+      throw;
+    }
+    c->prof_collect = false;
+    const std::vector<std::string> names = c->prof_names;
+    const std::vector<double> fl = c->prof_flops;
+    c->prof_names.clear(); c->prof_flops.clear();
+    const int n = (int)std::min<size_t>(names.size(), (size_t)max_sites);
+    hipEvent_t e0, e1;
+    CHECK_HIP(hipEventCreate(&e0));
+    CHECK_HIP(hipEventCreate(&e1));
+    for (int i = 0; i < n; ++i) {
+      c->prof_site = i;
+      hipGraph_t g;
+      CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      try {
+        for (int r = 0; r < reps; ++r) enqueue_update(c, batch, 1, 1, 7, 1.f, false);
+      } catch (...) {
+        (void)hipStreamEndCapture(c->stream, &g);
+        c->prof_site = -1;
+        throw;
+      }
+      CHECK_HIP(hipStreamEndCapture(c->stream, &g));
+      hipGraphExec_t ex;
+      CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      CHECK_HIP(hipGraphDestroy(g));
+      CHECK_HIP(hipGraphLaunch(ex, c->stream));      // warm
+      CHECK_HIP(hipEventRecord(e0, c->stream));
+      CHECK_HIP(hipGraphLaunch(ex, c->stream));
+      CHECK_HIP(hipEventRecord(e1, c->stream));
+      CHECK_HIP(hipEventSynchronize(e1));
+      float ms = 0;
+      CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
+      CHECK_HIP(hipGraphExecDestroy(ex));
+      std::memset(names_out + 32 * i, 0, 32);
+      std::strncpy(names_out + 32 * i, names[i].c_str(), 31);
+      us_out[i] = ms * 1000.f / reps;
+      flops_out[i] = fl[i];
+    }
+    c->prof_site = -1;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     *n_sites = n;
   });
 }

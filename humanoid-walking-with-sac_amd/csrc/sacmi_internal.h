@@ -89,7 +89,7 @@ struct GemmDesc {
 // parameter at C[i] is M[C - P + i], V[...], and its target T[C - P - t_base + i].
 struct AdamFuse {
   float* P; float* M; float* V; float* T;
-  float* G;            // gradients are also stored (GRAD-slot export)
+  float* G;            // non-null: gradients are also stored (GRAD-slot export)
   int64_t t_base;
   float lr, beta1, beta2, eps, tau;
   int step_idx;        // which optimizer's step counter drives the bias corrections

@@ -34,7 +34,7 @@ POLICY, Q1, Q2, Q1_TARGET, Q2_TARGET = range(5)
 SLOT_PARAM, SLOT_GRAD, SLOT_ADAM_M, SLOT_ADAM_V = range(4)
 (S_LOG_ALPHA, S_ALPHA, S_ALPHA_IS_TENSOR, S_STEP_POLICY, S_STEP_Q1, S_STEP_Q2, S_STEP_ALPHA,
  S_ADAM_M_LOG_ALPHA, S_ADAM_V_LOG_ALPHA, S_GRAD_LOG_ALPHA, S_PER_FRAME,
- S_NOISE_COUNTER) = range(12)
+ S_NOISE_COUNTER, S_KEEP_GRADS) = range(13)
 
 
 class SacmiConfig(ctypes.Structure):
@@ -73,6 +73,7 @@ _PROTOS = {
     "sacmi_sample_indices": [c_vp, ctypes.c_int32, c_i64p],
     "sacmi_step": [c_vp, ctypes.c_int32, c_i64p, c_f32p, c_f32p, c_f32p],
     "sacmi_step_async": [c_vp, ctypes.c_int32],
+    "sacmi_step_many_async": [c_vp, ctypes.c_int32, ctypes.c_int32],
     "sacmi_fetch_losses": [c_vp, c_f32p, ctypes.c_int32, c_i32p],
     "sacmi_step_phase": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float],
     "sacmi_grad_buffer": [c_vp, ctypes.c_int, ctypes.POINTER(c_vp), c_i64p],
@@ -85,6 +86,8 @@ _PROTOS = {
     "sacmi_act": [c_vp, c_f32p, ctypes.c_int32, ctypes.c_int32, c_f32p, c_f32p],
     "sacmi_profile_step": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
                            ctypes.c_int32, c_i32p],
+    "sacmi_profile_sites": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
+                            ctypes.c_int32, c_i32p],
 }
 EXPORTS = tuple(_PROTOS) + ("sacmi_abi_version", "sacmi_last_error")
 

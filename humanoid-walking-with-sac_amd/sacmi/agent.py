@@ -220,6 +220,25 @@ class SAC:
         self._ctx.step_async(batch_size)
         self._stale = True
 
+    def update_parameters_many(self, batch_size=256, n_updates=1):
+        """The trainer's `for _ in range(updates_per_step): update_parameters(batch_size)`
+        (trainer.py:203-204) as one device launch; returns the last update's losses,
+        which is what that loop keeps."""
+        self._flush_device()
+        if len(self.replay_buffer) < batch_size:
+            raise ValueError("Sample larger than population or is negative")
+        rb = self.replay_buffer
+        if rb.sync_python_random:
+            st = random.getstate()
+            self._ctx.set_mt(0, np.array(st[1][:624], np.uint32), st[1][624])
+        self._ctx.step_many_async(batch_size, n_updates)
+        if rb.sync_python_random:
+            key, pos = self._ctx.get_mt(0)
+            random.setstate((3, tuple(int(x) for x in key) + (pos,), st[2]))
+        self._stale = True
+        out = self._ctx.fetch_losses(1)[0]
+        return {"q1_loss": float(out[0]), "q2_loss": float(out[1]), "policy_loss": float(out[2])}
+
     def fetch_losses(self, max_steps=4096):
         rows = self._ctx.fetch_losses(max_steps)
         return [{"q1_loss": float(r[0]), "q2_loss": float(r[1]), "policy_loss": float(r[2])}

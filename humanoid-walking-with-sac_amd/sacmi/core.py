@@ -206,6 +206,10 @@ class Context:
     def step_async(self, batch: int) -> None:
         L.call("sacmi_step_async", self._h, int(batch))
 
+    def step_many_async(self, batch: int, n_updates: int) -> None:
+        """n_updates consecutive updates in one launch (trainer.py:203-204 loop)."""
+        L.call("sacmi_step_many_async", self._h, int(batch), int(n_updates))
+
     def fetch_losses(self, max_steps: int) -> np.ndarray:
         out = np.zeros((max_steps, 3), np.float32)
         n = ctypes.c_int32()
@@ -267,6 +271,20 @@ class Context:
                L.dptr(fl), mx, ctypes.byref(n))
         raw = names.raw
         return [(raw[32 * i:32 * i + 32].split(b"\0")[0].decode(), float(ms[i]), float(fl[i]))
+                for i in range(n.value)]
+
+    def profile_sites(self, batch: int, reps: int = 50):
+        """[(site, mean_us, flops_per_launch)]: each launch site alone, `reps` times in
+        one hipGraph, timed with HIP events on the context stream (advances the state)."""
+        mx = 64
+        names = ctypes.create_string_buffer(32 * mx)
+        us = np.zeros(mx, np.float32)
+        fl = np.zeros(mx, np.float64)
+        n = ctypes.c_int32()
+        L.call("sacmi_profile_sites", self._h, int(batch), int(reps), names, L.fptr(us),
+               L.dptr(fl), mx, ctypes.byref(n))
+        raw = names.raw
+        return [(raw[32 * i:32 * i + 32].split(b"\0")[0].decode(), float(us[i]), float(fl[i]))
                 for i in range(n.value)]
 
     # -- act -------------------------------------------------------------------------

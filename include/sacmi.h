@@ -6,6 +6,7 @@
  *
  *   sac_imp.SAC.__init__            sac_imp.py:9-52        -> sacmi_create
  *   sac_imp.SAC.update_parameters   sac_imp.py:74-144      -> sacmi_step / sacmi_step_async
+ *   trainer updates_per_step loop   trainer.py:203-204     -> sacmi_step_many_async
  *   sac_imp.SAC._soft_update_...    sac_imp.py:146-152     -> (inside sacmi_step)
  *   sac_imp.SAC.select_action       sac_imp.py:54-72       -> sacmi_act
  *   nn.Module.state_dict / load     sac_imp.py:154-233     -> sacmi_get_tensor / sacmi_set_tensor
@@ -94,7 +95,10 @@ enum sacmi_scalar {
   SACMI_S_GRAD_LOG_ALPHA = 9,
   SACMI_S_PER_FRAME = 10,      /* PrioritizedReplayBuffer.frame (replay_buffer.py:31) */
   SACMI_S_NOISE_COUNTER = 11,  /* Philox counter (updates drawn so far)             */
-  SACMI_S_COUNT = 12
+  SACMI_S_KEEP_GRADS = 12,     /* host flag: 1 = single-GPU updates also export the   */
+                               /* gradients to the GRAD slot (param.grad after        */
+                               /* backward); 0 (default) skips those stores           */
+  SACMI_S_COUNT = 13
 };
 
 /* ---- lifecycle ---------------------------------------------------------------- */
@@ -154,6 +158,11 @@ int sacmi_step(sacmi_ctx* ctx, int32_t batch, const int64_t* idx, const float* e
 /* Same work, enqueued only (no host sync, no host writes); losses stay on device
  * in a ring of `ring` slots, fetched by sacmi_fetch_losses. */
 int sacmi_step_async(sacmi_ctx* ctx, int32_t batch);
+/* n_updates consecutive updates (device indices + device noise) as ONE launch: the
+ * `for _ in range(updates_per_step): agent.update_parameters(batch_size)` loop of
+ * trainer.py:203-204.  Identical results to n_updates sacmi_step_async calls; every
+ * update's losses go to the ring.  1 <= n_updates <= 256. */
+int sacmi_step_many_async(sacmi_ctx* ctx, int32_t batch, int32_t n_updates);
 int sacmi_fetch_losses(sacmi_ctx* ctx, float* out, int32_t max_steps, int32_t* n_out);
 
 /* Data-parallel split of the step (one process per GPU).  phase 0: sample, gather,
@@ -195,6 +204,13 @@ int sacmi_act(sacmi_ctx* ctx, const float* s, int32_t n, int32_t deterministic,
  * one launch (GEMM sites; 0 elsewhere).  The model state advances as in sacmi_step. */
 int sacmi_profile_step(sacmi_ctx* ctx, int32_t batch, int32_t iters, char* names_out,
                        float* ms_out, double* flops_out, int32_t max_sites, int32_t* n_sites);
+/* Per launch site of the single-GPU update: that site's kernels alone, `reps` times
+ * back to back inside one hipGraph, timed with HIP events on the context's stream;
+ * us_out = mean microseconds per launch of the site (the duration the kernel has in
+ * the step's graph, boundary included).  Diagnostic: every replay advances the model
+ * state again (Adam sites take `reps` extra steps). */
+int sacmi_profile_sites(sacmi_ctx* ctx, int32_t batch, int32_t reps, char* names_out,
+                        float* us_out, double* flops_out, int32_t max_sites, int32_t* n_sites);
 
 #ifdef __cplusplus
 }

@@ -39,7 +39,10 @@ def make_ctx(cfg: SacConfig, max_batch, capacity, **kw):
     c = Config(cfg.state_dim, cfg.action_dim, cfg.hidden_dim, max_batch=max_batch,
                gamma=cfg.gamma, tau=cfg.tau, lr=cfg.lr, alpha=cfg.alpha,
                automatic_entropy_tuning=cfg.automatic_entropy_tuning, capacity=capacity, **kw)
-    return Context(c, 0)
+    ctx = Context(c, 0)
+    from sacmi import _lib as L
+    ctx.set_scalar(L.S_KEEP_GRADS, 1)     # the tests compare gradients too
+    return ctx
 
 
 def load_params(ctx, params):
@@ -217,8 +220,10 @@ def test_polyak_bitexact_and_determinism():
     params = init_params(cfg, 51, bias_scale=0.05)
     rows = synthetic_rows(cfg, 400, 52, state_scale=0.5)
     outs = []
-    for _ in range(2):
+    from sacmi import _lib as L
+    for keep in (1, 0):          # gradient export on/off: same bits, targets included
         ctx = make_ctx(cfg, max_batch=64, capacity=400)
+        ctx.set_scalar(L.S_KEEP_GRADS, keep)
         load_params(ctx, params)
         ctx.push(*rows)
         ctx.set_mt(0, (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32), 624)
@@ -236,6 +241,32 @@ def test_polyak_bitexact_and_determinism():
     for n in NETS:
         for k in outs[0][n]:
             assert np.array_equal(outs[0][n][k], outs[1][n][k]), (n, k)
+
+
+def test_many_updates_per_launch_identical():
+    """sacmi_step_many_async(n) (trainer.py:203-204 loop in one launch) == n single
+    launches, bit for bit, losses included."""
+    cfg = SacConfig(24, 4, 64)
+    params = init_params(cfg, 61, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 500, 62, state_scale=0.5)
+    res = []
+    for many in (True, False):
+        ctx = make_ctx(cfg, max_batch=64, capacity=500)
+        load_params(ctx, params)
+        ctx.push(*rows)
+        ctx.set_mt(0, (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32), 624)
+        if many:
+            ctx.step_many_async(64, 5)
+            ctx.step_many_async(64, 2)
+        else:
+            for _ in range(7):
+                ctx.step_async(64)
+        res.append((ctx.fetch_losses(7), {n: ctx.get_net(n) for n in NETS}, ctx.get_mt(0)))
+    assert np.array_equal(res[0][0], res[1][0]) and res[0][0].shape == (7, 3)
+    for n in NETS:
+        for k in res[0][1][n]:
+            assert np.array_equal(res[0][1][n][k], res[1][1][n][k]), (n, k)
+    assert np.array_equal(res[0][2][0], res[1][2][0]) and res[0][2][1] == res[1][2][1]
 
 
 def test_batch_larger_than_buffer_raises():

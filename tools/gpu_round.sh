@@ -17,8 +17,9 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- \
-    python3 $GRAFT_REPO_ROOT/bench.py --profile-only --steps 200 --warmup 20 --fill 200000 > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- \
+    python3 $GRAFT_REPO_ROOT/bench.py ${PROF_ARGS:-${BENCH_ARGS:-}} > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1
   rc=$?; echo prof_rc=$rc; [ $rc -ne 0 ] && { tail -20 $GRAFT_REPO_ROOT/$OUT/prof.log; exit $rc; }
-  find $GRAFT_REPO_ROOT/$OUT/prof -name "*stats*"
+  python3 $GRAFT_REPO_ROOT/tools/rocprof_kgemm.py $GRAFT_REPO_ROOT/$OUT/prof/run_kernel_stats.csv > $GRAFT_REPO_ROOT/$OUT/prof_summary.txt
+  tail -3 $GRAFT_REPO_ROOT/$OUT/prof_summary.txt; tail -1 $GRAFT_REPO_ROOT/$OUT/prof.log | cut -c1-400
 fi
