@@ -110,13 +110,20 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // its partial sums to red[wave][TM][TN+1].  At batch 256 every operand read is a
 // dependent L2/MALL round trip (~1-2 us), so a wave issues the loads of G chunks at
 // once (with KSPLIT = 16 waves per workgroup and K <= 528 that is ALL of its chunks:
-// one exposed latency per GEMM) and only then runs their MFMAs.
-template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM = false>
+// one exposed latency per GEMM) and only then runs their MFMAs.  `pre()` runs once,
+// right after the last group's loads are issued: the epilogue's own global loads go
+// out there, younger than every operand load (vmcnt retires in order), so the MFMAs
+// never wait for them and their latency hides under the (last) MFMA phase.
+// With MG > 1 the workgroup covers MG*TM rows: wave group g = wave / KSPLIT takes rows
+// m0 + g*TM .. +TM, and the K split runs inside each group.
+template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1, class Pre>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
-                                            float* rsum = nullptr) {
+                                            float* rsum, Pre&& pre) {
   constexpr int MT = TM / 16, NT = TN / 16;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  const int ks = wave % KSPLIT;
+  m0 += (wave / KSPLIT) * TM;
   SACMI_STAMP(wave);
   f4 acc[MT][NT];
 #pragma unroll
@@ -131,18 +138,20 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   row_ptrs<MT, AKC>(d.A, d.lda, m0, d.M, lane, ra);
   row_ptrs<NT, BKC>(d.B, d.ldb, n0, d.N, lane, rb);
   const int nch = (d.K + 15) >> 4;
-  const int nmine = nch > wave ? (nch - wave + KSPLIT - 1) / KSPLIT : 0;
+  const int nmine = nch > ks ? (nch - ks + KSPLIT - 1) / KSPLIT : 0;
   const int kl = 4 * (lane >> 4);
   float a[G][MT][4], b[G][NT][4];
+  if (nmine == 0) pre();
   for (int j = 0; j < nmine; j += G) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (j + g < nmine) {
-        const int k = (wave + (j + g) * KSPLIT) * 16 + kl;
+        const int k = (ks + (j + g) * KSPLIT) * 16 + kl;
         fetch_op<MT, AKC>(ra, d.lda, k, d.K, a[g]);
         fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
       }
     }
+    if (j + G >= nmine) pre();       // after the LAST operand loads (vmcnt is in order)
 #pragma unroll
     for (int g = 0; g < G; ++g)
       if (j + g < nmine) {
@@ -175,25 +184,45 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
 }
 
 // layout dispatch (wave-uniform, once per workgroup)
-template <int TM, int TN, int KSPLIT, int G>
+template <int TM, int TN, int KSPLIT, int G, int MG, class Pre>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
-                                          float* rsum, bool rowsum) {
+                                          float* rsum, bool rowsum, Pre&& pre) {
   if (d.a_kc) {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true>(d, m0, n0, red);
-    else gemm_core_l<TM, TN, KSPLIT, G, true, false>(d, m0, n0, red);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG>(d, m0, n0, red, rsum, pre);
   } else {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true>(d, m0, n0, red);
-    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true>(d, m0, n0, red, rsum);
-    else gemm_core_l<TM, TN, KSPLIT, G, false, false>(d, m0, n0, red);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG>(d, m0, n0, red, rsum, pre);
+    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG>(d, m0, n0, red, rsum, pre);
   }
 }
 
-template <int TM, int TN, int KSPLIT>
+// Sum of the KSPLIT partials of tile element (row, col); with MG wave groups the
+// tile has MG*TM rows and group g's partials sit at waves g*KSPLIT .. g*KSPLIT+KSPLIT-1.
+template <int TM, int TN, int KSPLIT, int MG = 1>
 __device__ __forceinline__ float reduce_partials(const float* red, int row, int col) {
-  float s = red[row * (TN + 1) + col];
+  const float* base = red + (row / TM) * KSPLIT * TM * (TN + 1) + (row % TM) * (TN + 1) + col;
+  float s = base[0];
 #pragma unroll
-  for (int w = 1; w < KSPLIT; ++w) s += red[w * TM * (TN + 1) + row * (TN + 1) + col];
+  for (int w = 1; w < KSPLIT; ++w) s += base[w * TM * (TN + 1)];
   return s;
+}
+
+// ---------------------------------------------------------------------------
+// Buffer-resource access (raw buffer ops): the base lives in a wave-uniform SGPR
+// descriptor and each lane carries one 32-bit byte offset, shared by every array that
+// is indexed alike (the Adam state) — no per-array 64-bit addresses held in VGPRs.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int kBufDword3 = 0x00020000;   // gfx9-family raw buffer descriptor word 3
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)bytes, kBufDword3);
+}
+__device__ __forceinline__ float buf_ld(rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void buf_st(rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)off, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -243,10 +272,20 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // One workgroup (16 waves, K split 16 ways) per output tile, one workgroup per CU.
 // Block 0 of an Adam-fused level also finalises the losses, takes the scalar
 // log_alpha step (alpha = exp(log_alpha), sac_imp.py:128-135) and fills the loss ring.
-template <int TM, int TN, int KSPLIT, int G>
-__global__ __launch_bounds__(64 * KSPLIT, 4) void k_gemm(GemmBatch batch) {
-  __shared__ float red[KSPLIT * TM * (TN + 1)];
-  __shared__ float rsum[KSPLIT * TM];
+// waves per SIMD the register allocation must allow: 4-wave tiles run one wave per SIMD
+// (full register file), 64x64 8-wave tiles two, the 16-wave tiles four
+// waves per SIMD the register allocation must allow: every wave of the workgroup
+// resident at once, one workgroup per CU
+template <int W>
+constexpr int gemm_min_waves() { return W >= 4 ? W / 4 : 1; }
+
+// TM x TN per wave group, MG wave groups (workgroup tile MG*TM x TN), K split KSPLIT
+// ways inside each group; ADAM: fused optimizer epilogue (every desc EPI_ADAM*)
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM>
+__global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
+  constexpr int TMW = TM * MG;
+  __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
+  __shared__ float rsum[MG * KSPLIT * TM];
   __shared__ AdamScalars s_k;
   const int bid = blockIdx.x;
   int p = 0;
@@ -254,83 +293,92 @@ __global__ __launch_bounds__(64 * KSPLIT, 4) void k_gemm(GemmBatch batch) {
     if (bid >= batch.d[q].tile_begin) p = q;
   const GemmDesc d = batch.d[p];
   const int t = bid - d.tile_begin;
-  const int m0 = (t / d.tiles_n) * TM, n0 = (t % d.tiles_n) * TN;
-  const bool adam = d.epi >= EPI_ADAM;
+  const int m0 = (t / d.tiles_n) * TMW, n0 = (t % d.tiles_n) * TN;
   const bool rowsum = d.rs_col >= 0 && n0 == 0;
-  if (adam && threadIdx.x == 0)
+  if (ADAM && threadIdx.x == 0)
     s_k = fuse_scalars(batch.adam, d.adam_step, batch.adam.step_offset);
-  gemm_core<TM, TN, KSPLIT, G>(d, m0, n0, red, rsum, rowsum);
-  __syncthreads();
-  if (threadIdx.x < 64) SACMI_STAMP(32);
   const AdamFuse& af = batch.adam;
-  const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
   // Element slots: EPT tile outputs per thread (e = tid + s*NTH) plus one slot for the
-  // rowsum (bias-gradient) column. All global loads of all slots are issued before any
-  // compute or store, so a thread waits for memory once, not once per element.
-  constexpr int NTH = 64 * KSPLIT, EPT = TM * TN / NTH, NS = EPT + 1;
-  static_assert(TM * TN % NTH == 0 && TM <= NTH, "epilogue slot layout");
+  // rowsum (bias-gradient) column.  Their epilogue operands (bias, ReLU mask, Adam
+  // state) are loaded by pre() while the MFMAs run.
+  constexpr int NTH = 64 * KSPLIT * MG, EPT = TMW * TN / NTH, NS = EPT + 1;
+  static_assert(TMW * TN % NTH == 0 && TMW <= NTH, "epilogue slot layout");
   const int tid = threadIdx.x;
-  float v[NS];
-  size_t ci[NS];
-  bool ok[NS];
-  int nn[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    int row;
+  // slot s -> (row, col in tile, output column n, valid); recomputed where needed so
+  // that only the prefetched values stay live across the MFMA phase
+  auto slot = [&](int s, int& row, int& col, int& n) -> bool {
     if (s < EPT) {
       const int e = tid + s * NTH;
       row = e / TN;
-      const int col = e % TN;
-      nn[s] = n0 + col;
-      ok[s] = m0 + row < d.M && nn[s] < d.N;
-      v[s] = reduce_partials<TM, TN, KSPLIT>(red, row, col);
+      col = e % TN;
+      n = n0 + col;
+      return m0 + row < d.M && n < d.N;
+    }
+    row = tid < TMW ? tid : 0;
+    col = -1;
+    n = d.rs_col;
+    return rowsum && tid < TMW && m0 + row < d.M;
+  };
+  const bool pol = d.epi == EPI_ADAM_POLYAK;
+  // byte span of this desc's output (tile rows, plus the rowsum column)
+  const uint32_t span = (uint32_t)(((size_t)(d.M - 1) * d.ldc + (d.rs_col >= d.N ? d.rs_col + 1 : d.N)) * 4);
+  const size_t abase = ADAM ? (size_t)(d.C - af.P) : 0;
+  const rsrc_t rC = make_rsrc(d.C, span);
+  // (unused descriptors get a zero-length range: any access through them is dropped)
+  const rsrc_t rM = make_rsrc(ADAM ? af.M + abase : d.C, ADAM ? span : 0);
+  const rsrc_t rV = make_rsrc(ADAM ? af.V + abase : d.C, ADAM ? span : 0);
+  const rsrc_t rT = make_rsrc(ADAM && pol ? af.T + abase - af.t_base : d.C, ADAM && pol ? span : 0);
+  const rsrc_t rG = make_rsrc(ADAM && af.G ? af.G + abase : d.C, ADAM && af.G ? span : 0);
+  const rsrc_t rX = d.bias ? make_rsrc(d.bias, (uint32_t)(((size_t)(d.N - 1) * d.bias_ld + 1) * 4))
+                  : d.epi == EPI_MASK ? make_rsrc(d.aux, (uint32_t)(((size_t)(d.M - 1) * d.ldaux + d.N) * 4))
+                  : make_rsrc(d.C, 0);
+  // Adam: param, exp_avg, exp_avg_sq, target; otherwise x0 = the bias or the ReLU-mask
+  // source (a level has one or the other: validate())
+  float x0[NS], x1[ADAM ? NS : 1], x2[ADAM ? NS : 1], x3[ADAM ? NS : 1];
+  // the epilogue operands (Adam state, or the bias / mask) go out under the MFMAs
+  auto pre = [&]() {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      int row, col, n;
+      if (!slot(s, row, col, n)) continue;
+      if constexpr (ADAM) {
+        const uint32_t o = (uint32_t)((m0 + row) * d.ldc + n) * 4u;
+        x0[s] = buf_ld(rC, o); x1[s] = buf_ld(rM, o); x2[s] = buf_ld(rV, o);
+        if (pol) x3[s] = buf_ld(rT, o);
+      } else {
+        if (d.bias) x0[s] = buf_ld(rX, (uint32_t)(n * d.bias_ld) * 4u);
+        else if (d.epi == EPI_MASK) x0[s] = buf_ld(rX, (uint32_t)((m0 + row) * d.ldaux + n) * 4u);
+      }
+    }
+  };
+  gemm_core<TM, TN, KSPLIT, G, MG>(d, m0, n0, red, rsum, rowsum, pre);
+  __syncthreads();
+  if (threadIdx.x < 64) SACMI_STAMP(32);
+  const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int row, col, n;
+    if (!slot(s, row, col, n)) continue;
+    float v;
+    if (s < EPT) {
+      v = reduce_partials<TM, TN, KSPLIT, MG>(red, row, col);
     } else {
-      row = tid < TM ? tid : 0;
-      nn[s] = d.rs_col;
-      ok[s] = rowsum && tid < TM && m0 + row < d.M;
-      float r = rsum[row];
+      const float* rb = rsum + (row / TM) * KSPLIT * TM + row % TM;
+      v = rb[0];
 #pragma unroll
-      for (int w = 1; w < KSPLIT; ++w) r += rsum[w * TM + row];
-      v[s] = r;
+      for (int w = 1; w < KSPLIT; ++w) v += rb[w * TM];
     }
-    ci[s] = (size_t)(m0 + row) * d.ldc + nn[s];
-  }
-  if (adam) {
-    const bool pol = d.epi == EPI_ADAM_POLYAK;
-    const size_t base = (size_t)(d.C - af.P);
-    float pp[NS], mm[NS], vv[NS], tt[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (!ok[s]) continue;
-      const size_t ai = base + ci[s];
-      pp[s] = d.C[ci[s]]; mm[s] = af.M[ai]; vv[s] = af.V[ai];
-      if (pol) tt[s] = af.T[ai - af.t_base];
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (!ok[s]) continue;
-      const size_t ai = base + ci[s];
-      adam_elem(pp[s], mm[s], vv[s], v[s], omb1, af.beta2, omb2, af.eps, s_k);
-      if (af.G) af.G[ai] = v[s];
-      d.C[ci[s]] = pp[s]; af.M[ai] = mm[s]; af.V[ai] = vv[s];
-      if (pol) af.T[ai - af.t_base] = polyak(tt[s], pp[s], omtau, af.tau);
-    }
-  } else {
-    float bx[NS], ax[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (!ok[s]) continue;
-      if (d.bias) bx[s] = d.bias[(size_t)nn[s] * d.bias_ld];
-      if (d.epi == EPI_MASK) ax[s] = d.aux[(ci[s] / d.ldc) * d.ldaux + nn[s]];
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (!ok[s]) continue;
-      float x = v[s];
-      if (d.bias) x += bx[s];
-      if (d.epi == EPI_RELU) x = x > 0.f ? x : 0.f;
-      else if (d.epi == EPI_MASK) x = ax[s] > 0.f ? x : 0.f;
-      d.C[ci[s]] = x;
+    const uint32_t o = (uint32_t)((m0 + row) * d.ldc + n) * 4u;
+    if constexpr (ADAM) {
+      adam_elem(x0[s], x1[s], x2[s], v, omb1, af.beta2, omb2, af.eps, s_k);
+      if (af.G) buf_st(rG, o, v);
+      buf_st(rC, o, x0[s]); buf_st(rM, o, x1[s]); buf_st(rV, o, x2[s]);
+      if (pol) buf_st(rT, o, polyak(x3[s], x0[s], omtau, af.tau));
+    } else {
+      if (d.bias) v += x0[s];
+      if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
+      else if (d.epi == EPI_MASK) v = x0[s] > 0.f ? v : 0.f;
+      buf_st(rC, o, v);
     }
   }
   if (threadIdx.x < 64) SACMI_STAMP(33);
@@ -378,19 +426,29 @@ static int assign_tiles(GemmBatch& b) {
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
-  int maxk = 0;
-  for (int i = 0; i < b.count; ++i) maxk = b.d[i].K > maxk ? b.d[i].K : maxk;
+  int maxk = 0, n_adam = 0;
+  for (int i = 0; i < b.count; ++i) {
+    maxk = b.d[i].K > maxk ? b.d[i].K : maxk;
+    n_adam += b.d[i].epi >= EPI_ADAM;
+  }
+  // (Level::add guarantees a level is all-Adam or all-plain)
   const int t64 = assign_tiles<32, 64>(b);
-  if (t64 > 256 && maxk <= 16 * 8 * 2) {
-    // many tiles of short K (weight gradients at batch <= 256): 8 waves per tile, two
-    // workgroups per CU, both of a wave's chunks loaded at once
-    hipLaunchKernelGGL((k_gemm<32, 64, 8, 2>), dim3(b.total_tiles), dim3(512), 0, s, b);
+  if (n_adam && t64 <= 256 && maxk <= 16 * 16) {
+    // fused Adam, one 32x64 tile per CU (policy level): 16 waves, one K chunk each
+    hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, true>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+  } else if (n_adam || (t64 > 256 && maxk <= 16 * 8 * 2)) {
+    // weight gradients at batch <= 256 with more 32x64 tiles than CUs (the twin
+    // critic level): 64x64 tiles — exactly 256 of them — as two 32-row wave groups,
+    // each with an 8-way K split; the epilogue state is prefetched under the MFMAs
+    assign_tiles<64, 64>(b);
+    if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, true>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+    else hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false>), dim3(b.total_tiles), dim3(1024), 0, s, b);
   } else if (t64 >= 192) {
     // widest tile that still gives one workgroup to most CUs
-    hipLaunchKernelGGL((k_gemm<32, 64, 16, 2>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+    hipLaunchKernelGGL((k_gemm<32, 64, 16, 2, 1, false>), dim3(b.total_tiles), dim3(1024), 0, s, b);
   } else {
     assign_tiles<32, 32>(b);
-    hipLaunchKernelGGL((k_gemm<32, 32, 16, 4>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+    hipLaunchKernelGGL((k_gemm<32, 32, 16, 4, 1, false>), dim3(b.total_tiles), dim3(1024), 0, s, b);
   }
   HIP_LAUNCH_CHECK();
 }
@@ -432,7 +490,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   d.A = a.h; d.lda = a.ldh; d.a_kc = 1; d.M = a.rows;
   d.B = a.Wh; d.ldb = a.ldw; d.b_kc = 1; d.N = 2 * A; d.K = a.K;
   const int m0 = blockIdx.x * TM;
-  gemm_core_l<TM, TN, KSPLIT, 3, true, true>(d, m0, 0, red);
+  gemm_core_l<TM, TN, KSPLIT, 3, true, true, false>(d, m0, 0, red, nullptr, [] {});
   __syncthreads();
   const float alpha_unused = 0.f; (void)alpha_unused;
   const uint64_t ctr = a.ctr_override ? a.ctr_override : a.sc->noise_counter;
@@ -500,7 +558,7 @@ template <int TM, int TN, int KSPLIT>
 __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, SampleBwdArgs a) {
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   const int m0 = blockIdx.x * TM;
-  gemm_core_l<TM, TN, KSPLIT, 4, true, false>(d, m0, 0, red);
+  gemm_core_l<TM, TN, KSPLIT, 4, true, false, false>(d, m0, 0, red, nullptr, [] {});
   __syncthreads();
   const int A = a.A;
   const float glogp = a.sc->alpha / (float)a.B;

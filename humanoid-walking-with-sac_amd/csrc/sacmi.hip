@@ -340,6 +340,7 @@ static void validate(const GemmDesc& d) {
   }
   if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C");
   if (d.bias) check_span(d.bias, (int64_t)(d.N - 1) * d.bias_ld, "bias");
+  REQUIRE(!(d.bias && d.epi == EPI_MASK), SACMI_ESTATE, "GEMM epilogue: bias and mask are exclusive");
   if (d.epi == EPI_MASK) check_span(d.aux, (int64_t)(d.M - 1) * d.ldaux + d.N - 1, "aux");
 }
 
@@ -348,6 +349,8 @@ struct Level {
   void add(const GemmDesc& d0) {
     validate(d0);
     if (b.count >= kMaxGemms) throw Error{SACMI_ESTATE, "too many GEMMs in one level"};
+    if (b.count && (b.d[0].epi >= EPI_ADAM) != (d0.epi >= EPI_ADAM))
+      throw Error{SACMI_ESTATE, "a GEMM level is either all fused-Adam or all plain"};
     GemmDesc d = d0;
     const int tm = (d.M + 31) / 32, tn = (d.N + 31) / 32;
     d.tiles_n = tn;

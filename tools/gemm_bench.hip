@@ -37,14 +37,14 @@ static GemmDesc mk(const float* A, int lda, int akc, const float* B, int ldb, in
   return d;
 }
 
-template <int TM, int TN, int KS, int G>
+template <int TM, int TN, int KS, int G, int MG, bool AD>
 static float time_cfg(GemmBatch b, int iters, hipStream_t s) {
-  assign_tiles<TM, TN>(b);
+  assign_tiles<TM * MG, TN>(b);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G>), dim3(b.total_tiles), dim3(64 * KS), 0, s, b);
+  for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
   CK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G>), dim3(b.total_tiles), dim3(64 * KS), 0, s, b);
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
   CK(hipEventRecord(e1, s));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -55,24 +55,24 @@ static float time_cfg(GemmBatch b, int iters, hipStream_t s) {
 
 #ifdef SACMI_DIAG_STAMPS
 // one launch after warm-up; per-phase breakdown from the in-kernel stamps (µs)
-template <int TM, int TN, int KS, int G>
+template <int TM, int TN, int KS, int G, int MG, bool AD>
 static void stamp_cfg(GemmBatch b, hipStream_t s) {
-  assign_tiles<TM, TN>(b);
-  for (int i = 0; i < 30; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G>), dim3(b.total_tiles), dim3(64 * KS), 0, s, b);
+  assign_tiles<TM * MG, TN>(b);
+  for (int i = 0; i < 30; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
   CK(hipStreamSynchronize(s));
   static unsigned long long h[4096][40];
   memset(h, 0, sizeof(h));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), h, sizeof(h)));
-  hipLaunchKernelGGL((k_gemm<TM, TN, KS, G>), dim3(b.total_tiles), dim3(64 * KS), 0, s, b);
+  hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
   CK(hipStreamSynchronize(s));
   CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof(h)));
   const int nb = std::min(b.total_tiles, 4096);
   unsigned long long t0 = ~0ull, tend = 0;
-  for (int i = 0; i < nb; ++i) { t0 = std::min(t0, h[i][0]); for (int w = 0; w < KS; ++w) t0 = std::min(t0, h[i][w]); tend = std::max(tend, h[i][33]); }
+  for (int i = 0; i < nb; ++i) { t0 = std::min(t0, h[i][0]); for (int w = 0; w < KS * MG; ++w) t0 = std::min(t0, h[i][w]); tend = std::max(tend, h[i][33]); }
   std::vector<double> start, core_max, core_min, syncw, epi, endt;
   for (int i = 0; i < nb; ++i) {
     unsigned long long e0 = ~0ull, emax = 0, lmax = 0, cmax = 0, cmin = ~0ull;
-    for (int w = 0; w < KS; ++w) {
+    for (int w = 0; w < KS * MG; ++w) {
       e0 = std::min(e0, h[i][w]); emax = std::max(emax, h[i][w]);
       lmax = std::max(lmax, h[i][16 + w]);
       cmax = std::max(cmax, h[i][16 + w] - h[i][w]); cmin = std::min(cmin, h[i][16 + w] - h[i][w]);
@@ -88,7 +88,7 @@ static void stamp_cfg(GemmBatch b, hipStream_t s) {
     const unsigned long long hw = id & 0xffffffffull, xcc = (id >> 32) & 0xf;
     const unsigned long long key = (xcc << 16) | (((hw >> 8) & 0xf) << 0) | (((hw >> 12) & 0x1) << 4) | (((hw >> 13) & 0x7) << 5);
     unsigned long long e0 = ~0ull;
-    for (int w = 0; w < KS; ++w) e0 = std::min(e0, h[i][w]);
+    for (int w = 0; w < KS * MG; ++w) e0 = std::min(e0, h[i][w]);
     per_cu[key].push_back({e0, h[i][33]});
   }
   int maxov = 0;
@@ -148,12 +148,12 @@ static void probe(float* out, hipStream_t s) {
 
 #endif
 
-template <int TM, int TN, int KS, int G>
+template <int TM, int TN, int KS, int G, int MG, bool AD>
 static void occ_cfg(const char* name) {
   int occ = 0;
-  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_gemm<TM, TN, KS, G>, 64 * KS, 0));
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_gemm<TM, TN, KS, G, MG, AD>, 64 * KS, 0));
   hipFuncAttributes fa;
-  CK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_gemm<TM, TN, KS, G>)));
+  CK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_gemm<TM, TN, KS, G, MG, AD>)));
   printf("%-14s occupancy API %d blocks/CU, LDS %zu, regs %d\n", name, occ, fa.sharedSizeBytes, fa.numRegs);
 }
 
@@ -198,9 +198,9 @@ int main(int argc, char** argv) {
   af.sc = sc; af.log_alpha_idx = -1; af.n_losses = 0;
 
   if (argc > 1 && std::string(argv[1]) == "occ") {
-    occ_cfg<32, 64, 8, 2>("<32,64,8,2>"); occ_cfg<32, 64, 16, 2>("<32,64,16,2>");
-    occ_cfg<32, 32, 16, 4>("<32,32,16,4>"); occ_cfg<32, 32, 8, 2>("<32,32,8,2>");
-    occ_cfg<32, 32, 4, 4>("<32,32,4,4>");
+    occ_cfg<32, 64, 8, 2, 1, false>("<32,64,8,2>"); occ_cfg<32, 64, 16, 2, 1, false>("<32,64,16,2>");
+    occ_cfg<32, 32, 16, 4, 1, false>("<32,32,16,4>"); occ_cfg<32, 32, 8, 2, 1, false>("<32,32,8,2>");
+    occ_cfg<32, 32, 4, 4, 1, false>("<32,32,4,4>");
     return 0;
   }
   struct Level { std::string name; std::function<GemmBatch(bool)> make; };
@@ -257,23 +257,35 @@ int main(int argc, char** argv) {
     for (int fused = 0; fused < 2; ++fused) {
       if (fused && L.name[1] != '6' && L.name.substr(0, 3) != "L13") continue;
       GemmBatch b = L.make(fused);
-      int t32 = assign_tiles<32, 32>(b), t64 = assign_tiles<32, 64>(b);
-      printf("%-40s %-6s tiles32=%d tiles64=%d\n", L.name.c_str(), fused ? "adam" : "store", t32, t64);
+      int t32 = assign_tiles<32, 32>(b), t64 = assign_tiles<32, 64>(b), t6464 = assign_tiles<64, 64>(b);
+      printf("%-40s %-6s tiles32x32=%d 32x64=%d 64x64=%d\n", L.name.c_str(), fused ? "adam" : "store", t32, t64, t6464);
 #ifdef SACMI_DIAG_STAMPS
       if (stamps) {
-        printf("   <32,64,8,2>\n"); stamp_cfg<32, 64, 8, 2>(b, s);
-        printf("   <32,64,16,2>\n"); stamp_cfg<32, 64, 16, 2>(b, s);
-        printf("   <32,32,16,4>\n"); stamp_cfg<32, 32, 16, 4>(b, s);
-        printf("   <32,32,8,2>\n"); stamp_cfg<32, 32, 8, 2>(b, s);
+        if (fused) {
+          printf("   <32x2,64,8,1,adam>\n"); stamp_cfg<32, 64, 8, 1, 2, true>(b, s);
+          printf("   <32x2,64,8,2,adam>\n"); stamp_cfg<32, 64, 8, 2, 2, true>(b, s);
+          printf("   <32,64,16,2,adam>\n"); stamp_cfg<32, 64, 16, 2, 1, true>(b, s);
+          continue;
+        }
+        printf("   <64,64,8,2>\n"); stamp_cfg<64, 64, 8, 2, 1, false>(b, s);
+        printf("   <32,64,16,2>\n"); stamp_cfg<32, 64, 16, 2, 1, false>(b, s);
+        printf("   <32,32,16,4>\n"); stamp_cfg<32, 32, 16, 4, 1, false>(b, s);
         continue;
       }
 #endif
-      printf("   <32,64,8,2>  %7.2f us\n", time_cfg<32, 64, 8, 2>(b, iters, s));
-      printf("   <32,64,16,2> %7.2f us\n", time_cfg<32, 64, 16, 2>(b, iters, s));
-      printf("   <32,32,16,4> %7.2f us\n", time_cfg<32, 32, 16, 4>(b, iters, s));
-      printf("   <32,32,8,2>  %7.2f us\n", time_cfg<32, 32, 8, 2>(b, iters, s));
-      printf("   <32,32,4,4>  %7.2f us\n", time_cfg<32, 32, 4, 4>(b, iters, s));
-      printf("   <16,64,8,2>  %7.2f us\n", time_cfg<16, 64, 8, 2>(b, iters, s));
+      if (fused) {
+        printf("   <32x2,64,8,1,adam> %7.2f us\n", time_cfg<32, 64, 8, 1, 2, true>(b, iters, s));
+        printf("   <32x2,64,8,2,adam> %7.2f us\n", time_cfg<32, 64, 8, 2, 2, true>(b, iters, s));
+        printf("   <64,64,8,2,adam>  %7.2f us\n", time_cfg<64, 64, 8, 2, 1, true>(b, iters, s));
+        printf("   <32,64,16,2,adam> %7.2f us\n", time_cfg<32, 64, 16, 2, 1, true>(b, iters, s));
+        continue;
+      }
+      printf("   <32x2,64,8,1> %7.2f us\n", time_cfg<32, 64, 8, 1, 2, false>(b, iters, s));
+      printf("   <64,64,8,2>  %7.2f us\n", time_cfg<64, 64, 8, 2, 1, false>(b, iters, s));
+      printf("   <64,64,4,4>  %7.2f us\n", time_cfg<64, 64, 4, 4, 1, false>(b, iters, s));
+      printf("   <32,64,16,2> %7.2f us\n", time_cfg<32, 64, 16, 2, 1, false>(b, iters, s));
+      printf("   <32,32,16,4> %7.2f us\n", time_cfg<32, 32, 16, 4, 1, false>(b, iters, s));
+      printf("   <32,32,8,2>  %7.2f us\n", time_cfg<32, 32, 8, 2, 1, false>(b, iters, s));
       fflush(stdout);
     }
   }
