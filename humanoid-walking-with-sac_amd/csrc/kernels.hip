@@ -490,18 +490,28 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   d.A = a.h; d.lda = a.ldh; d.a_kc = 1; d.M = a.rows;
   d.B = a.Wh; d.ldb = a.ldw; d.b_kc = 1; d.N = 2 * A; d.K = a.K;
   const int m0 = blockIdx.x * TM;
-  gemm_core_l<TM, TN, KSPLIT, 3, true, true, false>(d, m0, 0, red, nullptr, [] {});
+  static_assert(TM * 64 <= 64 * KSPLIT, "one (row, action) element per thread");
+  // element e = threadIdx.x -> (row, action j); its bias values (and stored noise)
+  // are loaded while the MFMAs run
+  const int e = threadIdx.x;
+  const int row = e / A, j = e % A, m = m0 + row;
+  const bool live = e < TM * A && m < a.rows;
+  float bm = 0.f, bl = 0.f, eps_in = 0.f;
+  auto pre = [&]() {
+    if (live) {
+      bm = a.Wh[(size_t)j * a.ldw + a.K];
+      bl = a.Wh[(size_t)(A + j) * a.ldw + a.K];
+      if (!a.deterministic && !a.gen_eps) eps_in = a.eps[(size_t)m * A + j];
+    }
+  };
+  gemm_core_l<TM, TN, KSPLIT, 3, true, true, false>(d, m0, 0, red, nullptr, pre);
   __syncthreads();
-  const float alpha_unused = 0.f; (void)alpha_unused;
   const uint64_t ctr = a.ctr_override ? a.ctr_override : a.sc->noise_counter;
-  for (int e = threadIdx.x; e < TM * A; e += 64 * KSPLIT) {
-    const int row = e / A, j = e % A;
-    const int m = m0 + row;
+  if (e < TM * A) {
     float lpe = 0.f;
-    if (m < a.rows) {
-      const float mean = reduce_partials<TM, TN, KSPLIT>(red, row, j) + a.Wh[(size_t)j * a.ldw + a.K];
-      const float ls_raw = reduce_partials<TM, TN, KSPLIT>(red, row, A + j) +
-                           a.Wh[(size_t)(A + j) * a.ldw + a.K];
+    if (live) {
+      const float mean = reduce_partials<TM, TN, KSPLIT>(red, row, j) + bm;
+      const float ls_raw = reduce_partials<TM, TN, KSPLIT>(red, row, A + j) + bl;
       const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
       const float sd = expf(ls);
       float eps;
@@ -511,7 +521,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
         eps = philox_normal(a.seed, ctr, (uint32_t)(m * A + j));
         a.eps[(size_t)m * A + j] = eps;
       } else {
-        eps = a.eps[(size_t)m * A + j];
+        eps = eps_in;
       }
       const float x = a.deterministic ? mean : mean + eps * sd;
       const float y = tanhf(x);
@@ -526,11 +536,11 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   }
   __syncthreads();
   if (threadIdx.x < TM) {
-    const int m = m0 + threadIdx.x;
-    if (m < a.rows) {
+    const int mm = m0 + threadIdx.x;
+    if (mm < a.rows) {
       float s = 0.f;
-      for (int j = 0; j < A; ++j) s += lp[threadIdx.x][j];
-      a.logp[m] = s;
+      for (int jj = 0; jj < A; ++jj) s += lp[threadIdx.x][jj];
+      a.logp[mm] = s;
     }
   }
 }
@@ -558,20 +568,29 @@ template <int TM, int TN, int KSPLIT>
 __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, SampleBwdArgs a) {
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   const int m0 = blockIdx.x * TM;
-  gemm_core_l<TM, TN, KSPLIT, 4, true, false, false>(d, m0, 0, red, nullptr, [] {});
-  __syncthreads();
+  static_assert(TM * TN <= 64 * KSPLIT, "one (row, action) element per thread");
+  // element e = threadIdx.x -> (row, action j); the sample cache and noise are loaded
+  // while the MFMAs run
   const int A = a.A;
+  const int e = threadIdx.x;
+  const int row = e / A, j = e % A, m = m0 + row;
+  const bool live = e < TM * A && m < d.M;
+  float ls_raw = 0.f, y = 0.f, eps = 0.f;
+  auto pre = [&]() {
+    if (live) {
+      const float* cr = a.cache + (size_t)m * 3 * A;
+      ls_raw = cr[A + j];
+      y = cr[2 * A + j];
+      eps = a.eps[(size_t)m * A + j];
+    }
+  };
+  gemm_core_l<TM, TN, KSPLIT, 4, true, false, false>(d, m0, 0, red, nullptr, pre);
+  __syncthreads();
   const float glogp = a.sc->alpha / (float)a.B;
-  for (int e = threadIdx.x; e < TM * A; e += 64 * KSPLIT) {
-    const int row = e / A, j = e % A;
-    const int m = m0 + row;
-    if (m >= d.M) continue;
+  if (live) {
     const float ga = reduce_partials<TM, TN, KSPLIT>(red, row, j);
-    const float* cr = a.cache + (size_t)m * 3 * A;
-    const float ls_raw = cr[A + j], y = cr[2 * A + j];
     const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
     const float sd = expf(ls);
-    const float eps = a.eps[(size_t)m * A + j];
     const float omy2 = 1.f - y * y;
     const float u = a.scale * omy2 + 1e-6f;
     const float G = a.scale * ga + glogp * (2.f * a.scale * y / u);
@@ -596,27 +615,49 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// NV simultaneous dots h_v . w_v over K4 float4 chunks, one wave; every load of the
-// row is issued before any reduction (one latency instead of NV).
-template <int NV>
-__device__ __forceinline__ void wave_dots(const float* const (&h)[NV], const float* const (&w)[NV],
-                                          int K4, int lane, float (&out)[NV]) {
-  float s[NV];
+// One wave holds a whole hidden row: lane l keeps float4 chunks q = l + 64 j (j < J)
+// of h (ones column included, so the dot carries the fc3 bias) and of w3, computes
+// the dot, and later writes the row's backward values straight from those registers.
+template <int J>
+struct RowRegs {
+  float4 h[J], w[J];
+};
+
+template <int J>
+__device__ __forceinline__ float row_load_dot(const float* h, const float* w, int K4, int lane,
+                                              RowRegs<J>& r) {
 #pragma unroll
-  for (int v = 0; v < NV; ++v) s[v] = 0.f;
-#pragma unroll 3
-  for (int q = lane; q < K4; q += 64) {
-    float4 x[NV], y[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      x[v] = reinterpret_cast<const float4*>(h[v])[q];
-      y[v] = reinterpret_cast<const float4*>(w[v])[q];
+  for (int j = 0; j < J; ++j) {
+    const int q = lane + 64 * j;
+    if (q < K4) {
+      r.h[j] = reinterpret_cast<const float4*>(h)[q];
+      r.w[j] = reinterpret_cast<const float4*>(w)[q];
+    } else {
+      r.h[j] = float4{0.f, 0.f, 0.f, 0.f};
+      r.w[j] = float4{0.f, 0.f, 0.f, 0.f};
     }
-#pragma unroll
-    for (int v = 0; v < NV; ++v) s[v] += x[v].x * y[v].x + x[v].y * y[v].y + x[v].z * y[v].z + x[v].w * y[v].w;
   }
+  float s = 0.f;
 #pragma unroll
-  for (int v = 0; v < NV; ++v) out[v] = wave_sum(s[v]);
+  for (int j = 0; j < J; ++j)
+    s += r.h[j].x * r.w[j].x + r.h[j].y * r.w[j].y + r.h[j].z * r.w[j].z + r.h[j].w * r.w[j].w;
+  return s;
+}
+
+// out[0:H] = dq * w3 * [h > 0] from the registers (H % 4 == 0: chunks q < H/4)
+template <int J>
+__device__ __forceinline__ void row_store_bwd(float* out, float dq, int H4, int lane,
+                                              const RowRegs<J>& r) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int q = lane + 64 * j;
+    if (q < H4) {
+      const float4 x = r.h[j], y = r.w[j];
+      reinterpret_cast<float4*>(out)[q] =
+          float4{x.x > 0.f ? dq * y.x : 0.f, x.y > 0.f ? dq * y.y : 0.f,
+                 x.z > 0.f ? dq * y.z : 0.f, x.w > 0.f ? dq * y.w : 0.f};
+    }
+  }
 }
 
 // Target + critic loss rows (sac_imp.py:87-105 forward tail, mse backward).
@@ -624,7 +665,7 @@ __device__ __forceinline__ void wave_dots(const float* const (&h)[NV], const flo
 //   q_i = h2_i[b].w3_i ; qt_i = ht2_i[b].w3t_i ;  q^ = r + (1-d)*gamma*(min qt - alpha*logp')
 //   dq_i = 2 (q_i - q^) / B ;  dh2_i[b,:] = dq_i * w3_i * [h2_i > 0]
 constexpr int kRowsPerBlock = 4;
-
+template <int J>
 __global__ __launch_bounds__(256) void k_critic_rows(CriticRowsArgs a) {
   __shared__ float part[kRowsPerBlock][2];
   __shared__ float red[256];
@@ -635,13 +676,15 @@ __global__ __launch_bounds__(256) void k_critic_rows(CriticRowsArgs a) {
   float e1 = 0.f, e2 = 0.f;
   if (b < a.B) {
     const float* h1 = a.hq2 + (size_t)b * 2 * a.ldh;
-    const float* h2 = h1 + a.ldh;
     const float* t1 = a.hqt2 + (size_t)b * 2 * a.ldh;
-    const float* t2 = t1 + a.ldh;
-    const float* const hv[4] = {h1, h2, t1, t2};
-    const float* const wv[4] = {a.w3, a.w3 + a.w3_stride, a.w3t, a.w3t + a.w3_stride};
+    RowRegs<J> r1, r2, rt1, rt2;
     float dv[4];
-    wave_dots<4>(hv, wv, K4, lane, dv);
+    dv[0] = row_load_dot<J>(h1, a.w3, K4, lane, r1);
+    dv[1] = row_load_dot<J>(h1 + a.ldh, a.w3 + a.w3_stride, K4, lane, r2);
+    dv[2] = row_load_dot<J>(t1, a.w3t, K4, lane, rt1);
+    dv[3] = row_load_dot<J>(t1 + a.ldh, a.w3t + a.w3_stride, K4, lane, rt2);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dv[v] = wave_sum(dv[v]);
     const float q1 = dv[0], q2 = dv[1], qt1 = dv[2], qt2 = dv[3];
     const float vt = fminf(qt1, qt2) - alpha * a.logp_t[b];
     const float qhat = a.r[b] + ((1.f - a.d[b]) * a.gamma) * vt;
@@ -650,10 +693,8 @@ __global__ __launch_bounds__(256) void k_critic_rows(CriticRowsArgs a) {
     const float dq1 = 2.f * e1 / (float)a.B, dq2 = 2.f * e2 / (float)a.B;
     if (lane == 0) { a.dq[b] = dq1; a.dq[a.B + b] = dq2; }
     float* o = a.dh2 + (size_t)b * 2 * a.H;
-    for (int h = lane; h < a.H; h += 64) {
-      o[h] = h1[h] > 0.f ? dq1 * a.w3[h] : 0.f;
-      o[a.H + h] = h2[h] > 0.f ? dq2 * a.w3[a.w3_stride + h] : 0.f;
-    }
+    row_store_bwd<J>(o, dq1, a.H / 4, lane, r1);
+    row_store_bwd<J>(o + a.H, dq2, a.H / 4, lane, r2);
   }
   if (lane == 0) { part[w][0] = e1 * e1; part[w][1] = e2 * e2; }
   __syncthreads();
@@ -676,9 +717,17 @@ __global__ __launch_bounds__(256) void k_critic_rows(CriticRowsArgs a) {
   }
 }
 
+// float4 chunks per lane for a hidden row of H (+1 ones column)
+static int row_chunks(int H) { return ((H + 1 + 3) / 4 + 63) / 64; }
+
 void launch_critic_rows(const CriticRowsArgs& a, hipStream_t s) {
   const int grid = (a.B + kRowsPerBlock - 1) / kRowsPerBlock;
-  hipLaunchKernelGGL(k_critic_rows, dim3(grid), dim3(256), 0, s, a);
+  switch (row_chunks(a.H)) {
+    case 1: hipLaunchKernelGGL(k_critic_rows<1>, dim3(grid), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(k_critic_rows<2>, dim3(grid), dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(k_critic_rows<3>, dim3(grid), dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(k_critic_rows<4>, dim3(grid), dim3(256), 0, s, a); break;
+  }
   HIP_LAUNCH_CHECK();
 }
 
@@ -686,6 +735,7 @@ void launch_critic_rows(const CriticRowsArgs& a, hipStream_t s) {
 // L_pi partial = alpha*logp - min(qa1, qa2); min backward splits ties 1/2 : 1/2.
 // Also advances the step counters (the critic Adam ran before this kernel, the
 // actor Adam runs after it).
+template <int J>
 __global__ __launch_bounds__(256) void k_actor_rows(ActorRowsArgs a) {
   __shared__ float part[kRowsPerBlock];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -695,22 +745,17 @@ __global__ __launch_bounds__(256) void k_actor_rows(ActorRowsArgs a) {
   float lpart = 0.f;
   if (b < a.B) {
     const float* h1 = a.hqa2 + (size_t)b * 2 * a.ldh;
-    const float* h2 = h1 + a.ldh;
-    const float* const hv[2] = {h1, h2};
-    const float* const wv[2] = {a.w3, a.w3 + a.w3_stride};
-    float dv[2];
-    wave_dots<2>(hv, wv, K4, lane, dv);
-    const float q1 = dv[0], q2 = dv[1];
+    RowRegs<J> r1, r2;
+    const float q1 = wave_sum(row_load_dot<J>(h1, a.w3, K4, lane, r1));
+    const float q2 = wave_sum(row_load_dot<J>(h1 + a.ldh, a.w3 + a.w3_stride, K4, lane, r2));
     const float qmin = fminf(q1, q2);
     lpart = alpha * a.logp_a[b] - qmin;
     const float g = -1.f / (float)a.B;
     const float w1 = q1 < q2 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
     const float dq1 = g * w1, dq2 = g * (1.f - w1);
     float* o = a.dha2 + (size_t)b * 2 * a.H;
-    for (int h = lane; h < a.H; h += 64) {
-      o[h] = h1[h] > 0.f ? dq1 * a.w3[h] : 0.f;
-      o[a.H + h] = h2[h] > 0.f ? dq2 * a.w3[a.w3_stride + h] : 0.f;
-    }
+    row_store_bwd<J>(o, dq1, a.H / 4, lane, r1);
+    row_store_bwd<J>(o + a.H, dq2, a.H / 4, lane, r2);
   }
   if (lane == 0) part[w] = lpart;
   __syncthreads();
@@ -731,7 +776,12 @@ __global__ __launch_bounds__(256) void k_actor_rows(ActorRowsArgs a) {
 
 void launch_actor_rows(const ActorRowsArgs& a, hipStream_t s) {
   const int grid = (a.B + kRowsPerBlock - 1) / kRowsPerBlock;
-  hipLaunchKernelGGL(k_actor_rows, dim3(grid), dim3(256), 0, s, a);
+  switch (row_chunks(a.H)) {
+    case 1: hipLaunchKernelGGL(k_actor_rows<1>, dim3(grid), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(k_actor_rows<2>, dim3(grid), dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(k_actor_rows<3>, dim3(grid), dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(k_actor_rows<4>, dim3(grid), dim3(256), 0, s, a); break;
+  }
   HIP_LAUNCH_CHECK();
 }
 

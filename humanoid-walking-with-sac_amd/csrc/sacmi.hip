@@ -688,6 +688,7 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
             "dims must be positive");
     REQUIRE(cfg->action_dim <= 32, SACMI_EVALUE, "action_dim > 32 not supported");
     REQUIRE(cfg->hidden_dim % 4 == 0, SACMI_EVALUE, "hidden_dim must be a multiple of 4");
+    REQUIRE(cfg->hidden_dim <= 1020, SACMI_EVALUE, "hidden_dim must be <= 1020 (one wave holds a hidden row)");
     REQUIRE(cfg->max_batch > 0 && cfg->max_batch <= 65536, SACMI_EVALUE, "bad max_batch");
     REQUIRE(cfg->capacity > 0 && cfg->capacity < (int64_t)1 << 31, SACMI_EVALUE, "bad capacity");
     int ndev = 0;
