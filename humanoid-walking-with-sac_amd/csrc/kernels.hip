@@ -13,7 +13,7 @@
 // row-major activations) and 4 coalesced 64-byte row segments otherwise.
 // Workgroups split K across their waves and reduce through LDS in a fixed wave
 // order: no float atomics anywhere, results are bitwise reproducible.
-#include "sacmi_internal.h"
+#include "replay_dev.h"
 
 #include <cmath>
 #include <cstdio>
@@ -288,6 +288,19 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   __shared__ float rsum[MG * KSPLIT * TM];
   __shared__ AdamScalars s_k;
   const int bid = blockIdx.x;
+  if (bid >= batch.total_tiles) {   // ride-along workgroups (next update's replay work)
+    if constexpr (MG * KSPLIT == 16) {   // the host attaches rides to 1024-thread configs
+      const int rb = bid - batch.total_tiles;
+      if (batch.ride.kind == 1) {
+        mt_sample_body(batch.ride.mt, batch.ride.tbl_log2, reinterpret_cast<uint32_t*>(red));
+      } else {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (int b = rb * 16 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 16)
+          gather_row(batch.ride.ga, b, lane, 64);
+      }
+    }
+    return;
+  }
   int p = 0;
   for (int q = 1; q < batch.count; ++q)
     if (bid >= batch.d[q].tile_begin) p = q;
@@ -426,6 +439,7 @@ static int assign_tiles(GemmBatch& b) {
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
+  const int extra = b.ride.kind ? b.ride.nblocks : 0;
   int maxk = 0, n_adam = 0;
   for (int i = 0; i < b.count; ++i) {
     maxk = b.d[i].K > maxk ? b.d[i].K : maxk;
@@ -435,20 +449,20 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   const int t64 = assign_tiles<32, 64>(b);
   if (n_adam && t64 <= 256 && maxk <= 16 * 16) {
     // fused Adam, one 32x64 tile per CU (policy level): 16 waves, one K chunk each
-    hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, true>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+    hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, true>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
   } else if (n_adam || (t64 > 256 && maxk <= 16 * 8 * 2)) {
     // weight gradients at batch <= 256 with more 32x64 tiles than CUs (the twin
     // critic level): 64x64 tiles — exactly 256 of them — as two 32-row wave groups,
     // each with an 8-way K split; the epilogue state is prefetched under the MFMAs
     assign_tiles<64, 64>(b);
-    if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, true>), dim3(b.total_tiles), dim3(1024), 0, s, b);
-    else hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+    if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, true>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
+    else hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
   } else if (t64 >= 192) {
     // widest tile that still gives one workgroup to most CUs
-    hipLaunchKernelGGL((k_gemm<32, 64, 16, 2, 1, false>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+    hipLaunchKernelGGL((k_gemm<32, 64, 16, 2, 1, false>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
   } else {
     assign_tiles<32, 32>(b);
-    hipLaunchKernelGGL((k_gemm<32, 32, 16, 4, 1, false>), dim3(b.total_tiles), dim3(1024), 0, s, b);
+    hipLaunchKernelGGL((k_gemm<32, 32, 16, 4, 1, false>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
   }
   HIP_LAUNCH_CHECK();
 }
@@ -872,32 +886,7 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
 // replay gather: deque positions -> ring slots -> critic input [s|1|a] and the
 // stacked policy input [s2|1|.. ; s|1|..]  (replay_buffer.py:15-19 + sac_imp.py:81-85)
 __global__ __launch_bounds__(128) void k_gather(GatherArgs a) {
-  const int b = blockIdx.x;
-  const int64_t slot = a.by_slot ? (int64_t)a.idx[b] : (a.sc->head + (int64_t)a.idx[b]) % a.capacity;
-  const float* so = a.obs + slot * a.ldo;
-  const float* s2 = a.obs2 + slot * a.ldo;
-  const float* ac = a.act + slot * a.lda_;
-  float* xq = a.xq + (size_t)b * a.ldx;
-  float* xt = a.x2 + (size_t)b * a.ldx;
-  float* xa = a.x2 + (size_t)(a.B + b) * a.ldx;
-  if ((a.S & 3) == 0) {
-    for (int q = threadIdx.x; q < a.S / 4; q += blockDim.x) {
-      const float4 v = reinterpret_cast<const float4*>(so)[q];
-      reinterpret_cast<float4*>(xq)[q] = v;
-      reinterpret_cast<float4*>(xa)[q] = v;
-      reinterpret_cast<float4*>(xt)[q] = reinterpret_cast<const float4*>(s2)[q];
-    }
-  } else {
-    for (int q = threadIdx.x; q < a.S; q += blockDim.x) {
-      const float v = so[q];
-      xq[q] = v; xa[q] = v; xt[q] = s2[q];
-    }
-  }
-  for (int j = threadIdx.x; j < a.A; j += blockDim.x) xq[a.S + 1 + j] = ac[j];
-  if (threadIdx.x == 0) {
-    a.r[b] = a.rew[slot];
-    a.d[b] = a.done[slot];
-  }
+  gather_row(a, blockIdx.x, threadIdx.x, 128);
 }
 
 void launch_gather(const GatherArgs& a, hipStream_t s) {

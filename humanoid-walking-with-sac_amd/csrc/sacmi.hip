@@ -4,7 +4,7 @@
 // sequences the ~20 kernels of one SAC update on one HIP stream, and caches each
 // distinct update configuration as an instantiated hipGraph so a training step is
 // one graph launch (the step is launch-latency bound at batch 256: SURVEY §7).
-#include "sacmi_internal.h"
+#include "replay_dev.h"
 
 #include <cmath>
 #include <cstdio>
@@ -101,9 +101,10 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> obs, act, rew, obs2, done, prio;
   sacmi::DevBuf<uint32_t> mt;      // [2][625]: random / numpy streams
   // scratch
-  sacmi::DevBuf<int32_t> idx32;
-  sacmi::DevBuf<int64_t> idx64;
+  sacmi::DevBuf<int32_t> idx32, idx32b;   // b: second batch set (odd updates of a graph)
+  sacmi::DevBuf<int64_t> idx64, idx64b;
   sacmi::DevBuf<float> xq, x2, r, d, hp1, hp2, eps, cache, logp;
+  sacmi::DevBuf<float> xqb, x2b, rb, db;
   sacmi::DevBuf<float> hq1, hq2, hqt1, hqt2, hqa1, hqa2;
   sacmi::DevBuf<float> dq, dh2, dh1, dha2, dha1, dhead, dhp2, dhp1;
   sacmi::DevBuf<float> lpart_c, lpart_a, ring;
@@ -239,10 +240,10 @@ static void alloc_all(sacmi_ctx* c) {
   }
   c->mt.alloc(2 * 625);
   c->per_scr.alloc(16);
-  c->idx32.alloc(Bm); c->idx64.alloc(Bm);
-  c->xq.alloc((size_t)Bm * c->Kx);
-  c->x2.alloc((size_t)2 * Bm * c->Kx);
-  c->r.alloc(Bm); c->d.alloc(Bm);
+  c->idx32.alloc(Bm); c->idx64.alloc(Bm); c->idx32b.alloc(Bm); c->idx64b.alloc(Bm);
+  c->xq.alloc((size_t)Bm * c->Kx); c->xqb.alloc((size_t)Bm * c->Kx);
+  c->x2.alloc((size_t)2 * Bm * c->Kx); c->x2b.alloc((size_t)2 * Bm * c->Kx);
+  c->r.alloc(Bm); c->d.alloc(Bm); c->rb.alloc(Bm); c->db.alloc(Bm);
   c->hp1.alloc((size_t)2 * Bm * c->Hd); c->hp2.alloc((size_t)2 * Bm * c->Hd);
   c->eps.alloc((size_t)2 * Bm * A);
   c->cache.alloc((size_t)2 * Bm * 3 * A);
@@ -259,6 +260,8 @@ static void alloc_all(sacmi_ctx* c) {
   // constant-1 (bias) columns
   launch_set_column(c->xq.p, Bm, c->Kx, S, 1.f, s);
   launch_set_column(c->x2.p, 2 * Bm, c->Kx, S, 1.f, s);
+  launch_set_column(c->xqb.p, Bm, c->Kx, S, 1.f, s);
+  launch_set_column(c->x2b.p, 2 * Bm, c->Kx, S, 1.f, s);
   launch_set_column(c->hp1.p, 2 * Bm, c->Hd, H, 1.f, s);
   launch_set_column(c->hp2.p, 2 * Bm, c->Hd, H, 1.f, s);
   for (auto* b : {&c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1, &c->hqa2}) {
@@ -397,10 +400,56 @@ static PerArgs per_args(sacmi_ctx* c, int k, int gen_u) {
   return a;
 }
 
+// The minibatch buffers of one update (indices, gathered rows, r, d): set 0 is the one
+// every single update and the host-side APIs use; set 1 serves the odd updates of a
+// multi-update graph, so that the next update's gather can run while this one still
+// reads its rows.
+struct BatchBufs {
+  int32_t* idx32; int64_t* idx64; float* xq; float* x2; float* r; float* d;
+};
+static BatchBufs batch_bufs(sacmi_ctx* c, int parity) {
+  if (parity == 0) return BatchBufs{c->idx32.p, c->idx64.p, c->xq.p, c->x2.p, c->r.p, c->d.p};
+  return BatchBufs{c->idx32b.p, c->idx64b.p, c->xqb.p, c->x2b.p, c->rb.p, c->db.p};
+}
+
+static int sample_setsize(int k) {   // random.py:486-488
+  int setsize = 21;
+  if (k > 5) setsize += (int)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
+  return setsize;
+}
+
+static MtSampleArgs mt_args(sacmi_ctx* c, int B, const BatchBufs& bb) {
+  MtSampleArgs m{};
+  m.mt = c->mt.p; m.sc = c->sc.p; m.k = B;
+  m.setsize = sample_setsize(B); m.idx_out = bb.idx32; m.idx64_out = bb.idx64;
+  return m;
+}
+
+static GatherArgs gather_args(sacmi_ctx* c, int B, const BatchBufs& bb, bool per) {
+  GatherArgs g{};
+  g.idx = bb.idx32; g.obs = c->obs.p; g.act = c->act.p; g.rew = c->rew.p; g.obs2 = c->obs2.p;
+  g.done = c->done.p; g.ldo = c->ldo; g.lda_ = c->ldact; g.capacity = c->capacity;
+  g.sc = c->sc.p; g.S = c->S; g.A = c->A; g.B = B; g.xq = bb.xq; g.x2 = bb.x2; g.ldx = c->Kx;
+  g.r = bb.r; g.d = bb.d;
+  g.by_slot = per ? 1 : 0;
+  return g;
+}
+
+// Can the next update's sampling + gather ride along in this update's launches?
+static bool ride_possible(sacmi_ctx* c, int B) {
+  return c->cfg.replay_kind == SACMI_REPLAY_UNIFORM &&
+         mt_sample_lds_words(mt_sample_tbl_log2(B), sample_setsize(B)) * 4 <= kRideLdsBytes;
+}
+
+// parity: which batch buffer set this update uses; have_batch: its indices and rows
+// were produced by the previous update's ride-along work; ride_next: produce the next
+// update's (into the other set) inside this update's L11 / L13 launches.
 static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
-                           float grad_scale, bool use_ring) {
+                           float grad_scale, bool use_ring, int parity = 0,
+                           bool have_batch = false, bool ride_next = false) {
   hipStream_t s = c->stream;
   c->site_counter = 0;
+  const BatchBufs bb = batch_bufs(c, parity);
   const int S = c->S, A = c->A, H = c->H, Kx = c->Kx, Hd = c->Hd;
   float* P = c->P.p;
   float* G = c->G.p;
@@ -413,30 +462,20 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
 
   if (phase_mask & 1) {
     const bool per = c->cfg.replay_kind == SACMI_REPLAY_PER;
-    if (dev_idx && per) {
+    if (have_batch) {
+      // indices and rows were produced by the previous update (ride-along)
+    } else if (dev_idx && per) {
       if (mark(c, "per_sample")) launch_per_sample(per_args(c, B, 1), s);
     } else if (dev_idx) {
-      MtSampleArgs m{};
-      m.mt = c->mt.p; m.sc = c->sc.p; m.k = B;
-      const int k = B;
-      int setsize = 21;
-      if (k > 5) setsize += (int)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
-      m.setsize = setsize; m.idx_out = c->idx32.p; m.idx64_out = c->idx64.p;
-      if (mark(c, "mt_sample")) launch_mt_sample(m, s);
+      if (mark(c, "mt_sample")) launch_mt_sample(mt_args(c, B, bb), s);
     }
-    GatherArgs g{};
-    g.idx = c->idx32.p; g.obs = c->obs.p; g.act = c->act.p; g.rew = c->rew.p; g.obs2 = c->obs2.p;
-    g.done = c->done.p; g.ldo = c->ldo; g.lda_ = c->ldact; g.capacity = c->capacity;
-    g.sc = c->sc.p; g.S = S; g.A = A; g.B = B; g.xq = c->xq.p; g.x2 = c->x2.p; g.ldx = Kx;
-    g.r = c->r.p; g.d = c->d.p;
-    g.by_slot = per ? 1 : 0;
-    if (mark(c, "gather")) launch_gather(g, s);
+    if (!have_batch && mark(c, "gather")) launch_gather(gather_args(c, B, bb, per), s);
 
     // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
     Level l1;
-    l1.add(gd(c->x2.p, Kx, 1, W(c->p_fc1), c->p_fc1.ld, 1, c->hp1.p, Hd, 2 * B, H, S + 1, EPI_RELU));
+    l1.add(gd(bb.x2, Kx, 1, W(c->p_fc1), c->p_fc1.ld, 1, c->hp1.p, Hd, 2 * B, H, S + 1, EPI_RELU));
     for (int i = 0; i < 2; ++i)
-      l1.add(gd(c->xq.p, Kx, 1, W(q[i][0]), Kx, 1, c->hq1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+      l1.add(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, c->hq1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
     if (mark(c, "gemm_L1_fc1", level_flops(l1.b))) launch_gemm(l1.b, s);
     // L2
     Level l2;
@@ -448,7 +487,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     HeadSampleArgs hs{};
     hs.h = c->hp2.p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
     hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = dev_eps; hs.seed = c->cfg.seed;
-    hs.sc = c->sc.p; hs.act = c->x2.p + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
+    hs.sc = c->sc.p; hs.act = bb.x2 + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
     hs.cache = c->cache.p;
     hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
@@ -456,7 +495,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     // L3/L4: target critics on [s2|1|a']
     Level l3, l4;
     for (int i = 0; i < 2; ++i)
-      l3.add(gd(c->x2.p, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+      l3.add(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
     if (mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b))) launch_gemm(l3.b, s);
     for (int i = 0; i < 2; ++i)
       l4.add(gd_fwd_h(c->hqt1.p + i * Hd, 2 * Hd, Wt(q[i][1]), Hd, c->hqt2.p + i * Hd, 2 * Hd, B, H, H));
@@ -465,7 +504,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     CriticRowsArgs cr{};
     cr.hq2 = c->hq2.p; cr.hqt2 = c->hqt2.p; cr.ldh = Hd; cr.H = H; cr.B = B;
     cr.w3 = W(q[0][2]); cr.w3t = Wt(q[0][2]); cr.w3_stride = (int)(q[1][2].off - q[0][2].off);
-    cr.r = c->r.p; cr.d = c->d.p; cr.logp_t = c->logp.p; cr.logp_a = c->logp.p + B;
+    cr.r = bb.r; cr.d = bb.d; cr.logp_t = c->logp.p; cr.logp_a = c->logp.p + B;
     cr.gamma = (float)c->cfg.gamma; cr.target_entropy = (float)(-A);
     cr.auto_entropy = c->cfg.auto_entropy; cr.sc = c->sc.p; cr.dq = c->dq.p; cr.dh2 = c->dh2.p;
     cr.loss_part = c->lpart_c.p; cr.alpha_grad = G + c->la_idx;
@@ -492,7 +531,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     // L6: dW1~ (+ dW2~, dW3~ and Adam/Polyak/q-loss when fused)
     Level l6;
     for (int i = 0; i < 2; ++i)
-      l6.add(gd(c->dh1.p + i * H, 2 * H, 0, c->xq.p, Kx, 0, dst(q[i][0]), Kx, H, S + A + 1, B,
+      l6.add(gd(c->dh1.p + i * H, 2 * H, 0, bb.xq, Kx, 0, dst(q[i][0]), Kx, H, S + A + 1, B,
                 wepi, nullptr, 0, 1 + i));
     for (int i = 0; i < lw.b.count; ++i) l6.add(lw.b.d[i]);
     if (fuse) {
@@ -533,7 +572,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     if (mark(c, "adam_critic_polyak")) launch_adam(ad, s);
    }
     // L7/L8: updated critics on [s|1|a~]
-    const float* xa = c->x2.p + (size_t)B * Kx;
+    const float* xa = bb.x2 + (size_t)B * Kx;
     Level l7, l8;
     for (int i = 0; i < 2; ++i)
       l7.add(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, c->hqa1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
@@ -586,6 +625,16 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.log_alpha_grad = G + c->la_idx;
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
     }
+    if (ride_next) {
+      // the next update's random.sample rides in L11 (128 tiles: idle CUs)
+      const BatchBufs nb2 = batch_bufs(c, parity ^ 1);
+      l11.b.ride.kind = 1; l11.b.ride.nblocks = 1;
+      l11.b.ride.tbl_log2 = mt_sample_tbl_log2(B);
+      l11.b.ride.mt = mt_args(c, B, nb2);
+      // ... and its gather in L13
+      l13.b.ride.kind = 2; l13.b.ride.nblocks = 16;
+      l13.b.ride.ga = gather_args(c, B, nb2, false);
+    }
     if (mark(c, "gemm_L11_pi_dhp2", level_flops(l11.b))) launch_gemm(l11.b, s);
     if (mark(c, "gemm_L12_pi_dhp1", level_flops(l12.b))) launch_gemm(l12.b, s);
     if (mark(c, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1", level_flops(l13.b))) launch_gemm(l13.b, s);
@@ -612,9 +661,16 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
 
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
                        float grad_scale, bool use_ring, int reps = 1) {
-  if (!c->use_graphs) {
+  // consecutive fused updates hand the next update's sampling + gather to ride-along
+  // workgroups of the current one
+  const bool ride = reps > 1 && phase_mask == 7 && dev_idx && ride_possible(c, B);
+  auto enqueue_all = [&]() {
     for (int r = 0; r < reps; ++r)
-      enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring);
+      enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring, ride ? (r & 1) : 0,
+                     ride && r > 0, ride && r + 1 < reps);
+  };
+  if (!c->use_graphs) {
+    enqueue_all();
     CHECK_HIP(hipGetLastError());
     return;
   }
@@ -626,8 +682,7 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
     hipGraph_t g;
     CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     try {
-      for (int r = 0; r < reps; ++r)
-        enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring);
+      enqueue_all();
     } catch (...) {
       (void)hipStreamEndCapture(c->stream, &g);
       throw;
@@ -738,7 +793,8 @@ int sacmi_destroy(sacmi_ctx* c) {
       c->G.p = nullptr;
     }
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
-                    &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->hp1, &c->hp2, &c->eps,
+                    &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->xqb, &c->x2b, &c->rb,
+                    &c->db, &c->hp1, &c->hp2, &c->eps,
                     &c->cache, &c->logp, &c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1,
                     &c->hqa2, &c->dq, &c->dh2, &c->dh1, &c->dha2, &c->dha1, &c->dhead, &c->dhp2,
                     &c->dhp1, &c->lpart_c, &c->lpart_a, &c->ring, &c->ax, &c->ah1, &c->ah2,
@@ -746,6 +802,7 @@ int sacmi_destroy(sacmi_ctx* c) {
                     &c->per_chunk, &c->per_w, &c->per_val})
       b->release();
     c->sc.release(); c->mt.release(); c->idx32.release(); c->idx64.release();
+    c->idx32b.release(); c->idx64b.release();
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
     c->per_u.release(); c->per_uin.release(); c->per_owner.release(); c->per_bad.release();
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -990,12 +1047,7 @@ int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
     REQUIRE(batch <= c->Bm, SACMI_EVALUE, "batch > max_batch");
     REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
     if (batch == 0) return;
-    MtSampleArgs m{};
-    m.mt = c->mt.p; m.sc = c->sc.p; m.k = batch;
-    int setsize = 21;
-    if (batch > 5) setsize += (int)std::pow(4.0, std::ceil(std::log((double)batch * 3) / std::log(4.0)));
-    m.setsize = setsize; m.idx_out = c->idx32.p; m.idx64_out = c->idx64.p;
-    launch_mt_sample(m, c->stream);
+    launch_mt_sample(mt_args(c, batch, batch_bufs(c, 0)), c->stream);
     CHECK_HIP(hipGetLastError());
     CHECK_HIP(hipMemcpyAsync(idx_out, c->idx64.p, (size_t)batch * 8, hipMemcpyDeviceToHost, c->stream));
     CHECK_HIP(hipStreamSynchronize(c->stream));

@@ -102,6 +102,40 @@ struct AdamFuse {
   float* loss_ring; int ring;
 };
 
+struct GatherArgs {
+  const int32_t* idx;     // deque positions [B]
+  const float* obs; const float* act; const float* rew; const float* obs2; const float* done;
+  int ldo, lda_;          // row strides of obs/obs2 and act in the ring
+  int64_t capacity;
+  const DevScalars* sc;
+  int S, A, B;
+  float* xq; float* x2; int ldx;   // xq [B, ldx], x2 [2B, ldx]
+  float* r; float* d;
+  int by_slot;            // 1: idx are ring slots (PER), 0: deque positions
+};
+struct MtSampleArgs {
+  uint32_t* mt;           // 624 key words + pos
+  const DevScalars* sc;   // len
+  int k;                  // batch
+  int setsize;            // random.sample branch threshold (host-computed, exact)
+  int32_t* idx_out;       // [k]
+  int64_t* idx64_out;     // [k] or null
+  int32_t* pool;          // scratch [max setsize] for the pool branch
+};
+// Work of the NEXT update of a multi-update graph that rides along, as extra
+// workgroups, in a GEMM launch whose tiles leave CUs idle (1024-thread configs):
+// its random.sample (kind 1, one workgroup) or its minibatch gather (kind 2).
+// every k_gemm config launch_gemm picks has 1024 threads and a reduction buffer of at
+// least 16*32*33 floats: the LDS a ride-along random.sample may use
+constexpr size_t kRideLdsBytes = (size_t)16 * 32 * 33 * 4;
+struct RideAlong {
+  int kind;        // 0 none, 1 random.sample, 2 gather
+  int nblocks;
+  int tbl_log2;    // kind 1: hash table size
+  MtSampleArgs mt;
+  GatherArgs ga;
+};
+
 constexpr int kMaxGemms = 8;
 struct GemmBatch {
   GemmDesc d[kMaxGemms];
@@ -109,6 +143,7 @@ struct GemmBatch {
   int total_tiles;
   AdamFuse adam;       // used when any desc has epi >= EPI_ADAM
   int has_adam;
+  RideAlong ride;      // extra workgroups after the tiles
 };
 
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked
@@ -200,28 +235,8 @@ struct AdamArgs {
 };
 void launch_adam(const AdamArgs& a, hipStream_t s);
 
-struct GatherArgs {
-  const int32_t* idx;     // deque positions [B]
-  const float* obs; const float* act; const float* rew; const float* obs2; const float* done;
-  int ldo, lda_;          // row strides of obs/obs2 and act in the ring
-  int64_t capacity;
-  const DevScalars* sc;
-  int S, A, B;
-  float* xq; float* x2; int ldx;   // xq [B, ldx], x2 [2B, ldx]
-  float* r; float* d;
-  int by_slot;            // 1: idx are ring slots (PER), 0: deque positions
-};
 void launch_gather(const GatherArgs& a, hipStream_t s);
 
-struct MtSampleArgs {
-  uint32_t* mt;           // 624 key words + pos
-  const DevScalars* sc;   // len
-  int k;                  // batch
-  int setsize;            // random.sample branch threshold (host-computed, exact)
-  int32_t* idx_out;       // [k]
-  int64_t* idx64_out;     // [k] or null
-  int32_t* pool;          // scratch [max setsize] for the pool branch
-};
 void launch_mt_sample(const MtSampleArgs& a, hipStream_t s);
 
 void launch_fill(float* p, int64_t n, float v, hipStream_t s);
