@@ -96,15 +96,28 @@ def gemm_roofline(ctx, batch, reps=50):
     update kernel is launched on): achieved = algorithmic FLOPs per launch / mean
     launch duration, over the k_gemm sites of one update."""
     sites = ctx.profile_sites(batch, reps)
-    gemm = [(n, us, f) for (n, us, f) in sites if _is_k_gemm(n)]
-    gus = sum(us for _, us, _ in gemm)
-    gfl = sum(f for _, _, f in gemm)
+    gemm = [(n, us, f, b) for (n, us, f, b) in sites if _is_k_gemm(n)]
+    gus = sum(x[1] for x in gemm)
+    gfl = sum(x[2] for x in gemm)
+    gby = sum(x[3] for x in gemm)
     launches = len(gemm)
     avg_us = gus / launches
     achieved = (gfl / launches) / (avg_us * 1e-6) / 1e12
-    return dict(sites=sites, sites_sum_us=sum(us for _, us, _ in sites), gemm_us=gus,
-                gemm_flops=gfl, launches=launches, avg_launch_us=avg_us,
+    return dict(sites=sites, sites_sum_us=sum(x[1] for x in sites), gemm_us=gus,
+                gemm_flops=gfl, gemm_bytes=gby, launches=launches, avg_launch_us=avg_us,
                 achieved_tflops=achieved)
+
+
+def pmc_traffic():
+    """Measured bytes past L2 per k_gemm launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, two
+    separate --pmc passes over this bench command: tools/gpu_pmc.sh + tools/pmc_summary.py),
+    read from the committed summary; None when absent."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        per = json.load(open(path))["per_launch"]
+        return per["traffic_bytes"], os.path.relpath(path, ROOT)
+    except (OSError, KeyError, TypeError, ValueError):
+        return None, None
 
 
 def cpu_baseline(rows, seconds=15.0, warmup=5):
@@ -237,16 +250,20 @@ def main():
     roof = None
     if not args.no_roofline:
         info = gemm_roofline(ctx, args.batch)
+        traffic, traffic_src = pmc_traffic()
         roof = {"bound": "mfma", "achieved": round(info["achieved_tflops"], 3),
                 "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(info["achieved_tflops"] / PEAK_FP32_MFMA_TFLOPS, 4),
-                "traffic": None,
+                "traffic": None if traffic is None else round(traffic),
+                "traffic_unit": "bytes past L2 per k_gemm launch (PMC)",
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": round(info["gemm_bytes"] / info["launches"]),
                 "kernel": "sacmi::k_gemm (grouped fp32 MFMA GEMM, all tile configs)",
                 "launches_per_step": info["launches"],
                 "avg_launch_us": round(info["avg_launch_us"], 3),
                 "gemm_flops_per_step": info["gemm_flops"],
                 "sites_sum_us": round(info["sites_sum_us"], 2),
-                "sites_us": {n: round(us, 2) for (n, us, _) in info["sites"]}}
+                "sites_us": {x[0]: round(x[1], 2) for x in info["sites"]}}
     flops = necessary_flops(S_DIM, A_DIM, HIDDEN, args.batch)
     cpu = None
     if not args.no_cpu_baseline:

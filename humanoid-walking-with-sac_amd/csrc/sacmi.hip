@@ -129,7 +129,7 @@ struct sacmi_ctx {
   int prof_site = -1;          // >= 0: enqueue only this launch site
   int site_counter = 0;        // launch sites seen by the current enqueue_update
   std::vector<std::string> prof_names;
-  std::vector<double> prof_flops;
+  std::vector<double> prof_flops, prof_bytes;
   std::vector<hipEvent_t> prof_events;
 };
 
@@ -369,15 +369,34 @@ static double level_flops(const GemmBatch& b) {
   return f;
 }
 
+// Algorithmic bytes of one level: each operand read once, the output written once, the
+// epilogue's own operands (ReLU-mask source, bias) read once, and for a fused Adam the
+// optimizer state (param, exp_avg, exp_avg_sq [+ target]) read and written once.
+static double level_bytes(const GemmBatch& b) {
+  double n = 0;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    const double out = (double)d.M * (d.N + (d.rs_col >= 0 ? 1 : 0));
+    n += (double)d.M * d.K + (double)d.N * d.K;
+    if (d.epi >= EPI_ADAM) {
+      n += out * (d.epi == EPI_ADAM_POLYAK ? 8 : 6) + (b.adam.G ? out : 0);
+    } else {
+      n += out + (d.epi == EPI_MASK ? out : 0) + (d.bias ? d.N : 0);
+    }
+  }
+  return 4.0 * n;
+}
+
 // profiling mark: records an event BEFORE the launch it names
 // Hook in front of every launch site of the update.  Returns whether the site's
 // kernels are enqueued: always, except in site-isolation mode (prof_site >= 0), where
 // only site number prof_site runs (sacmi_profile_sites).
-static bool mark(sacmi_ctx* c, const char* name, double flops = 0) {
+static bool mark(sacmi_ctx* c, const char* name, double flops = 0, double bytes = 0) {
   const int site = c->site_counter++;
   if (c->prof || c->prof_collect) {
     c->prof_names.push_back(name);
     c->prof_flops.push_back(flops);
+    c->prof_bytes.push_back(bytes);
   }
   if (c->prof) {
     hipEvent_t e;
@@ -476,13 +495,13 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     l1.add(gd(bb.x2, Kx, 1, W(c->p_fc1), c->p_fc1.ld, 1, c->hp1.p, Hd, 2 * B, H, S + 1, EPI_RELU));
     for (int i = 0; i < 2; ++i)
       l1.add(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, c->hq1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    if (mark(c, "gemm_L1_fc1", level_flops(l1.b))) launch_gemm(l1.b, s);
+    if (mark(c, "gemm_L1_fc1", level_flops(l1.b), level_bytes(l1.b))) launch_gemm(l1.b, s);
     // L2
     Level l2;
     l2.add(gd_fwd_h(c->hp1.p, Hd, W(c->p_fc2), Hd, c->hp2.p, Hd, 2 * B, H, H));
     for (int i = 0; i < 2; ++i)
       l2.add(gd_fwd_h(c->hq1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hq2.p + i * Hd, 2 * Hd, B, H, H));
-    if (mark(c, "gemm_L2_fc2", level_flops(l2.b))) launch_gemm(l2.b, s);
+    if (mark(c, "gemm_L2_fc2", level_flops(l2.b), level_bytes(l2.b))) launch_gemm(l2.b, s);
     // heads + sample for both stacks
     HeadSampleArgs hs{};
     hs.h = c->hp2.p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
@@ -496,10 +515,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     Level l3, l4;
     for (int i = 0; i < 2; ++i)
       l3.add(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    if (mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b))) launch_gemm(l3.b, s);
+    if (mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b), level_bytes(l3.b))) launch_gemm(l3.b, s);
     for (int i = 0; i < 2; ++i)
       l4.add(gd_fwd_h(c->hqt1.p + i * Hd, 2 * Hd, Wt(q[i][1]), Hd, c->hqt2.p + i * Hd, 2 * Hd, B, H, H));
-    if (mark(c, "gemm_L4_tgt_fc2", level_flops(l4.b))) launch_gemm(l4.b, s);
+    if (mark(c, "gemm_L4_tgt_fc2", level_flops(l4.b), level_bytes(l4.b))) launch_gemm(l4.b, s);
     // target / critic loss rows
     CriticRowsArgs cr{};
     cr.hq2 = c->hq2.p; cr.hqt2 = c->hqt2.p; cr.ldh = Hd; cr.H = H; cr.B = B;
@@ -527,7 +546,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       lw.add(gd_dw_h(c->dq.p + i * B, 1, c->hq2.p + i * Hd, 2 * Hd, dst(q[i][2]), Hd, 1, H, B,
                      wepi, 1 + i));
     }
-    if (mark(c, "gemm_L5_critic_dh1", level_flops(l5.b))) launch_gemm(l5.b, s);
+    if (mark(c, "gemm_L5_critic_dh1", level_flops(l5.b), level_bytes(l5.b))) launch_gemm(l5.b, s);
     // L6: dW1~ (+ dW2~, dW3~ and Adam/Polyak/q-loss when fused)
     Level l6;
     for (int i = 0; i < 2; ++i)
@@ -544,7 +563,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.loss_part = c->lpart_c.p; f.n_part = nb; f.loss_slot0 = 0; f.n_losses = 2;
       f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
     }
-    if (mark(c, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1", level_flops(l6.b))) launch_gemm(l6.b, s);
+    if (mark(c, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1", level_flops(l6.b), level_bytes(l6.b))) launch_gemm(l6.b, s);
   }
   const float lr = (float)c->cfg.lr;
   if (phase_mask & 2) {
@@ -576,10 +595,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     Level l7, l8;
     for (int i = 0; i < 2; ++i)
       l7.add(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, c->hqa1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    if (mark(c, "gemm_L7_act_fc1", level_flops(l7.b))) launch_gemm(l7.b, s);
+    if (mark(c, "gemm_L7_act_fc1", level_flops(l7.b), level_bytes(l7.b))) launch_gemm(l7.b, s);
     for (int i = 0; i < 2; ++i)
       l8.add(gd_fwd_h(c->hqa1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hqa2.p + i * Hd, 2 * Hd, B, H, H));
-    if (mark(c, "gemm_L8_act_fc2", level_flops(l8.b))) launch_gemm(l8.b, s);
+    if (mark(c, "gemm_L8_act_fc2", level_flops(l8.b), level_bytes(l8.b))) launch_gemm(l8.b, s);
     ActorRowsArgs ar{};
     ar.hqa2 = c->hqa2.p; ar.ldh = Hd; ar.H = H; ar.B = B; ar.w3 = W(q[0][2]);
     ar.w3_stride = (int)(q[1][2].off - q[0][2].off); ar.logp_a = c->logp.p + B; ar.sc = c->sc.p;
@@ -590,7 +609,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     for (int i = 0; i < 2; ++i)
       l9.add(gd(c->dha2.p + i * H, 2 * H, 1, W(q[i][1]), Hd, 0, c->dha1.p + i * H, 2 * H, B, H, H,
                 EPI_MASK, c->hqa1.p + i * Hd, 2 * Hd));
-    if (mark(c, "gemm_L9_act_dh1", level_flops(l9.b))) launch_gemm(l9.b, s);
+    if (mark(c, "gemm_L9_act_dh1", level_flops(l9.b), level_bytes(l9.b))) launch_gemm(l9.b, s);
     // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
     GemmDesc da = gd(c->dha1.p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
     validate(da);
@@ -635,9 +654,9 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l13.b.ride.kind = 2; l13.b.ride.nblocks = 16;
       l13.b.ride.ga = gather_args(c, B, nb2, false);
     }
-    if (mark(c, "gemm_L11_pi_dhp2", level_flops(l11.b))) launch_gemm(l11.b, s);
-    if (mark(c, "gemm_L12_pi_dhp1", level_flops(l12.b))) launch_gemm(l12.b, s);
-    if (mark(c, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1", level_flops(l13.b))) launch_gemm(l13.b, s);
+    if (mark(c, "gemm_L11_pi_dhp2", level_flops(l11.b), level_bytes(l11.b))) launch_gemm(l11.b, s);
+    if (mark(c, "gemm_L12_pi_dhp1", level_flops(l12.b), level_bytes(l12.b))) launch_gemm(l12.b, s);
+    if (mark(c, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1", level_flops(l13.b), level_bytes(l13.b))) launch_gemm(l13.b, s);
   }
   if ((phase_mask & 4) && phase_mask != 7) {
     AdamArgs ad{};
@@ -1148,7 +1167,7 @@ int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_o
     std::vector<double> fl;
     for (int it = 0; it < iters; ++it) {
       c->prof = true;
-      c->prof_events.clear(); c->prof_names.clear(); c->prof_flops.clear();
+      c->prof_events.clear(); c->prof_names.clear(); c->prof_flops.clear(); c->prof_bytes.clear();
       try {
         enqueue_update(c, batch, 1, 1, 7, 1.f, false);
         (void)mark(c, "end");
@@ -1180,12 +1199,13 @@ int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_o
 }
 
 int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_out,
-                        float* us_out, double* flops_out, int32_t max_sites, int32_t* n_sites) {
+                        float* us_out, double* flops_out, double* bytes_out, int32_t max_sites,
+                        int32_t* n_sites) {
   return guard([&] {
     check_batch(c, batch);
     REQUIRE(reps > 0 && reps <= 1000, SACMI_EVALUE, "reps must be in [1, 1000]");
     // enumerate the sites of the fused single-GPU update without launching anything
-    c->prof_names.clear(); c->prof_flops.clear();
+    c->prof_names.clear(); c->prof_flops.clear(); c->prof_bytes.clear();
     c->prof_collect = true;
     c->prof_site = 1 << 30;
     try {
@@ -1196,8 +1216,8 @@ int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_o
     }
     c->prof_collect = false;
     const std::vector<std::string> names = c->prof_names;
-    const std::vector<double> fl = c->prof_flops;
-    c->prof_names.clear(); c->prof_flops.clear();
+    const std::vector<double> fl = c->prof_flops, by = c->prof_bytes;
+    c->prof_names.clear(); c->prof_flops.clear(); c->prof_bytes.clear();
     const int n = (int)std::min<size_t>(names.size(), (size_t)max_sites);
     hipEvent_t e0, e1;
     CHECK_HIP(hipEventCreate(&e0));
@@ -1229,6 +1249,7 @@ int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_o
       std::strncpy(names_out + 32 * i, names[i].c_str(), 31);
       us_out[i] = ms * 1000.f / reps;
       flops_out[i] = fl[i];
+      if (bytes_out) bytes_out[i] = by[i];
     }
     c->prof_site = -1;
     (void)hipEventDestroy(e0);

@@ -87,7 +87,7 @@ _PROTOS = {
     "sacmi_profile_step": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
                            ctypes.c_int32, c_i32p],
     "sacmi_profile_sites": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
-                            ctypes.c_int32, c_i32p],
+                            c_f64p, ctypes.c_int32, c_i32p],
 }
 EXPORTS = tuple(_PROTOS) + ("sacmi_abi_version", "sacmi_last_error")
 

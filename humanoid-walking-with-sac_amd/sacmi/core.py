@@ -274,18 +274,20 @@ class Context:
                 for i in range(n.value)]
 
     def profile_sites(self, batch: int, reps: int = 50):
-        """[(site, mean_us, flops_per_launch)]: each launch site alone, `reps` times in
-        one hipGraph, timed with HIP events on the context stream (advances the state)."""
+        """[(site, mean_us, flops_per_launch, bytes_per_launch)]: each launch site alone,
+        `reps` times in one hipGraph, timed with HIP events on the context stream
+        (advances the state)."""
         mx = 64
         names = ctypes.create_string_buffer(32 * mx)
         us = np.zeros(mx, np.float32)
         fl = np.zeros(mx, np.float64)
+        by = np.zeros(mx, np.float64)
         n = ctypes.c_int32()
         L.call("sacmi_profile_sites", self._h, int(batch), int(reps), names, L.fptr(us),
-               L.dptr(fl), mx, ctypes.byref(n))
+               L.dptr(fl), L.dptr(by), mx, ctypes.byref(n))
         raw = names.raw
-        return [(raw[32 * i:32 * i + 32].split(b"\0")[0].decode(), float(us[i]), float(fl[i]))
-                for i in range(n.value)]
+        return [(raw[32 * i:32 * i + 32].split(b"\0")[0].decode(), float(us[i]), float(fl[i]),
+                 float(by[i])) for i in range(n.value)]
 
     # -- act -------------------------------------------------------------------------
     def act(self, states, deterministic: bool, eps=None) -> np.ndarray:

@@ -207,10 +207,12 @@ int sacmi_profile_step(sacmi_ctx* ctx, int32_t batch, int32_t iters, char* names
 /* Per launch site of the single-GPU update: that site's kernels alone, `reps` times
  * back to back inside one hipGraph, timed with HIP events on the context's stream;
  * us_out = mean microseconds per launch of the site (the duration the kernel has in
- * the step's graph, boundary included).  Diagnostic: every replay advances the model
- * state again (Adam sites take `reps` extra steps). */
+ * the step's graph, boundary included); flops_out / bytes_out (may be NULL) = the
+ * algorithmic FLOPs / bytes of one launch (GEMM sites; 0 elsewhere).  Diagnostic:
+ * every replay advances the model state again (Adam sites take `reps` extra steps). */
 int sacmi_profile_sites(sacmi_ctx* ctx, int32_t batch, int32_t reps, char* names_out,
-                        float* us_out, double* flops_out, int32_t max_sites, int32_t* n_sites);
+                        float* us_out, double* flops_out, double* bytes_out, int32_t max_sites,
+                        int32_t* n_sites);
 
 #ifdef __cplusplus
 }
