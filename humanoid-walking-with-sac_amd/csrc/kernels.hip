@@ -306,7 +306,18 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
     if (bid >= batch.d[q].tile_begin) p = q;
   const GemmDesc d = batch.d[p];
   const int t = bid - d.tile_begin;
-  const int m0 = (t / d.tiles_n) * TMW, n0 = (t % d.tiles_n) * TN;
+  if (t >= d.tiles_m * d.tiles_n) return;   // padding to a multiple of 8 blocks
+  int tr, tc;
+  if (d.xcd_gr) {
+    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
+    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
+    tr = (x / gc) * sr + j / sc;
+    tc = (x % gc) * sc + j % sc;
+  } else {
+    tr = t / d.tiles_n;
+    tc = t % d.tiles_n;
+  }
+  const int m0 = tr * TMW, n0 = tc * TN;
   const bool rowsum = d.rs_col >= 0 && n0 == 0;
   if (ADAM && threadIdx.x == 0)
     s_k = fuse_scalars(batch.adam, d.adam_step, batch.adam.step_offset);
@@ -423,14 +434,31 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   }
 }
 
+// Tile order and XCD placement.  Workgroups are dealt round-robin over the 8 XCDs
+// (block b -> XCD b % 8: observed dispatch behaviour, used for speed only), and each
+// XCD has its own L2.  Row-major tile order puts the 8 column tiles of a row block on
+// 8 different XCDs, so every XCD fetches every A row block: traffic past L2 ~ 8A + B.
+// Each desc starts on a multiple of 8 blocks and, where its tile grid divides, XCD x
+// gets a compact (tm/gr) x (tn/gc) sub-grid of tiles (gr*gc = 8): traffic gc*A + gr*B,
+// gr chosen per desc to minimise it.
 template <int TM, int TN>
 static int assign_tiles(GemmBatch& b) {
   int tot = 0;
   for (int i = 0; i < b.count; ++i) {
     GemmDesc& d = b.d[i];
     d.tiles_n = (d.N + TN - 1) / TN;
+    d.tiles_m = (d.M + TM - 1) / TM;
     d.tile_begin = tot;
-    tot += ((d.M + TM - 1) / TM) * d.tiles_n;
+    const double A = (double)d.M * d.K, B = (double)d.N * d.K;
+    d.xcd_gr = 0;
+    double best = 8 * A + B;      // row-major order
+    for (int gr : {1, 2, 4, 8}) {
+      const int gc = 8 / gr;
+      if (d.tiles_m % gr || d.tiles_n % gc) continue;
+      const double cost = gc * A + gr * B;
+      if (cost < best) { best = cost; d.xcd_gr = gr; }
+    }
+    tot += (d.tiles_m * d.tiles_n + 7) & ~7;
   }
   b.total_tiles = tot;
   return tot;

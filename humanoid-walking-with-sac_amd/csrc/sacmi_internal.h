@@ -76,6 +76,8 @@ struct GemmDesc {
   int lda, ldb, ldc, ldaux;
   int a_kc, b_kc, epi;
   int tiles_n, tile_begin;
+  int tiles_m;         // row blocks
+  int xcd_gr;          // >0: XCD-blocked tile order, gr x (8/gr) XCD grid (launch_gemm)
   int adam_step;       // EPI_ADAM*: optimizer step counter index (0 pi, 1 q1, 2 q2)
   const float* bias;   // forward epilogue: C += bias[n * bias_ld] (before the ReLU)
   int bias_ld;

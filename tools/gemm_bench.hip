@@ -68,9 +68,11 @@ static void stamp_cfg(GemmBatch b, hipStream_t s) {
   CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof(h)));
   const int nb = std::min(b.total_tiles, 4096);
   unsigned long long t0 = ~0ull, tend = 0;
-  for (int i = 0; i < nb; ++i) { t0 = std::min(t0, h[i][0]); for (int w = 0; w < KS * MG; ++w) t0 = std::min(t0, h[i][w]); tend = std::max(tend, h[i][33]); }
+  auto live = [&](int i) { return h[i][33] != 0; };   // padding blocks exit unstamped
+  for (int i = 0; i < nb; ++i) { if (!live(i)) continue; for (int w = 0; w < KS * MG; ++w) t0 = std::min(t0, h[i][w]); tend = std::max(tend, h[i][33]); }
   std::vector<double> start, core_max, core_min, syncw, epi, endt;
   for (int i = 0; i < nb; ++i) {
+    if (!live(i)) continue;
     unsigned long long e0 = ~0ull, emax = 0, lmax = 0, cmax = 0, cmin = ~0ull;
     for (int w = 0; w < KS * MG; ++w) {
       e0 = std::min(e0, h[i][w]); emax = std::max(emax, h[i][w]);
@@ -84,6 +86,7 @@ static void stamp_cfg(GemmBatch b, hipStream_t s) {
   // residency census: CU identity = (xcc, se, sh, cu) from HW_ID; max WGs overlapping on one CU
   std::map<unsigned long long, std::vector<std::pair<unsigned long long, unsigned long long>>> per_cu;
   for (int i = 0; i < nb; ++i) {
+    if (!live(i)) continue;
     const unsigned long long id = h[i][34];
     const unsigned long long hw = id & 0xffffffffull, xcc = (id >> 32) & 0xf;
     const unsigned long long key = (xcc << 16) | (((hw >> 8) & 0xf) << 0) | (((hw >> 12) & 0x1) << 4) | (((hw >> 13) & 0x7) << 5);
