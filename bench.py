@@ -108,11 +108,12 @@ def gemm_roofline(ctx, batch, reps=50):
                 achieved_tflops=achieved)
 
 
-def pmc_traffic():
+def pmc_traffic(config):
     """Measured bytes past L2 per k_gemm launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, two
     separate --pmc passes over this bench command: tools/gpu_pmc.sh + tools/pmc_summary.py),
     read from the committed summary; None when absent."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json" if config == 2 else
+                        f"r01_pmc_traffic_c{config}.json")
     try:
         per = json.load(open(path))["per_launch"]
         return per["traffic_bytes"], os.path.relpath(path, ROOT)
@@ -120,27 +121,33 @@ def pmc_traffic():
         return None, None
 
 
-def cpu_baseline(rows, seconds=15.0, warmup=5):
-    """The reference update on CPU (oracle torch port, fp32) + the reference's deque
-    replay data path, timed on this host's cores for a bounded number of steps."""
+def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False):
+    """The reference update on CPU (oracle torch port, fp32) + the reference's replay
+    data path (deque + random.sample, or the prioritized buffer's numpy sampler), timed
+    on this host's cores for a bounded number of steps."""
     import random
-    from oracle.replay_ref import DequeReplay
+    from oracle.replay_ref import DequeReplay, PerReplayNumpy
     from oracle.sac_step import OracleSAC, SacConfig, init_params
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     cfg = SacConfig(S_DIM, A_DIM, HIDDEN)
     agent = OracleSAC(cfg, init_params(cfg, 0), dtype=torch.float32)
     s, a, r, s2, d = rows
-    buf = DequeReplay(capacity=len(r))
-    for i in range(len(r)):
-        buf.push(s[i], a[i], float(r[i]), s2[i], bool(d[i]))
+    if per:
+        buf = PerReplayNumpy(capacity=len(r))
+        buf.fill(rows)
+    else:
+        buf = DequeReplay(capacity=len(r))
+        for i in range(len(r)):
+            buf.push(s[i], a[i], float(r[i]), s2[i], bool(d[i]))
     random.seed(0)
+    np.random.seed(0)
     gen = torch.Generator().manual_seed(0)
 
     def one():
-        bs, ba, br, bs2, bd = buf.sample(BATCH)
-        e1 = torch.randn(BATCH, A_DIM, generator=gen).numpy()
-        e2 = torch.randn(BATCH, A_DIM, generator=gen).numpy()
+        bs, ba, br, bs2, bd = buf.sample(batch)[:5]
+        e1 = torch.randn(batch, A_DIM, generator=gen).numpy()
+        e2 = torch.randn(batch, A_DIM, generator=gen).numpy()
         agent.step(bs, ba, br, bs2, bd, e1, e2)
 
     for _ in range(warmup):
@@ -159,9 +166,11 @@ def cpu_baseline(rows, seconds=15.0, warmup=5):
                 break
     except OSError:
         pass
+    replay = ("PrioritizedReplayBuffer numpy sampler (np.random.choice over prios**alpha)"
+              if per else "deque/random.sample replay")
     return dict(value=n / dt, unit="grad-steps/s", cores=threads, kind="port",
-                sample=f"{n} updates (after {warmup} warm-up) in {dt:.1f}s; oracle torch-CPU fp32 "
-                       f"port of sac_imp.update_parameters + deque/random.sample replay over "
+                sample=f"{n} updates (after {warmup} warm-up) in {dt:.1f}s at batch {batch}; oracle "
+                       f"torch-CPU fp32 port of sac_imp.update_parameters + {replay} over "
                        f"{len(r)} rows (float32 rows); {threads} threads on {cpu}")
 
 
@@ -170,7 +179,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+                    help="BASELINE.json configs[1] (2: batch 256 uniform) or configs[2] "
+                         "(3: batch 4096, prioritized replay in HBM)")
+    ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--fill", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -190,8 +202,12 @@ def main():
 
     from sacmi import Config, Context
     torch.cuda.init()
+    per = args.config == 3
+    if args.batch is None:
+        args.batch = 4096 if per else BATCH
     fill = args.fill
-    ctx = Context(Config(S_DIM, A_DIM, HIDDEN, max_batch=args.batch, capacity=fill, seed=1), 0)
+    ctx = Context(Config(S_DIM, A_DIM, HIDDEN, max_batch=args.batch, capacity=fill, seed=1,
+                         replay="per" if per else "uniform"), 0)
     init_agent(ctx, 0)
     t_fill = time.perf_counter()
     chunk = 100_000
@@ -250,7 +266,7 @@ def main():
     roof = None
     if not args.no_roofline:
         info = gemm_roofline(ctx, args.batch)
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic(args.config)
         roof = {"bound": "mfma", "achieved": round(info["achieved_tflops"], 3),
                 "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(info["achieved_tflops"] / PEAK_FP32_MFMA_TFLOPS, 4),
@@ -269,14 +285,17 @@ def main():
     if not args.no_cpu_baseline:
         n_cpu = min(fill, 1_000_000)
         cpu_rows = tuple(x[:n_cpu] for x in synth(n_cpu, 7))
-        cpu = cpu_baseline(cpu_rows, seconds=args.cpu_seconds)
+        cpu = cpu_baseline(cpu_rows, seconds=args.cpu_seconds, batch=args.batch, per=per)
+    workload = ("BASELINE configs[2]: Humanoid-v5 shapes, hidden=512, batch=4096, prioritized "
+                "replay resident in HBM (device np.random.choice over prios**alpha)" if per else
+                "BASELINE configs[1]: Humanoid-v5 shapes, hidden=512, batch=256, uniform replay "
+                "(HBM ring, device random.sample)")
     out = {
-        "metric": "SAC gradient-steps/sec, Humanoid-v5 batch=256 (obs 376, act 17, hidden 512)",
+        "metric": f"SAC gradient-steps/sec, Humanoid-v5 batch={args.batch} (obs 376, act 17, hidden 512)",
         "value": round(sps, 2), "unit": "grad-steps/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 / sps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-        "config": {"workload": "BASELINE configs[1]: Humanoid-v5 shapes, hidden=512, batch=256, "
-                               "uniform replay (HBM ring, device random.sample)",
+        "config": {"workload": workload,
                    "state_dim": S_DIM, "action_dim": A_DIM, "hidden": HIDDEN,
                    "global_batch": args.batch, "replay_fill": fill, "parallelism": "single GPU"},
         "updates_per_launch": upl,
