@@ -13,7 +13,7 @@
 //                                          sequential float64 fallback
 //   cdf /= cdf[-1]; idx = cdf.searchsorted(u, 'right'), u = MT19937 53-bit doubles
 //   w = (len * probs[idx]) ** -beta; w /= w.max()
-#include "sacmi_internal.h"
+#include "replay_dev.h"
 
 #include <cstdio>
 
@@ -83,17 +83,39 @@ __device__ float pw_leaf(const float* a, int n) {
   return res;
 }
 
-// 2. one workgroup per 8192-element chunk: leaves in parallel, tree combined in the
-// recursion order (deterministic, no contraction: plain float adds).
-__global__ __launch_bounds__(128) void k_per_chunk_sum(const float* probs, int64_t len,
+// 2. one workgroup per 8192-element chunk (deterministic, no contraction: plain float
+// adds).  A full chunk is a perfect recursion tree — 8192 halves down to 64 leaves of
+// 128 — so it is staged into LDS with float4 loads, its 64 leaves run in parallel and
+// the tree combines level by level (node = left + right, the recursion's order).  The
+// final partial chunk follows the recursion literally (leaves enumerated and combined
+// on one lane).
+__global__ __launch_bounds__(256) void k_per_chunk_sum(const float* probs, int64_t len,
                                                        float* chunk_sum) {
 #pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) float buf[kChunk];
   __shared__ int leaf_off[kChunk / 64], leaf_len[kChunk / 64];
   __shared__ float leaf_val[kChunk / 64];
   __shared__ int nleaf;
   const int64_t c0 = (int64_t)blockIdx.x * kChunk;
   const int n = (int)((len - c0) < kChunk ? (len - c0) : kChunk);
   const float* a = probs + c0;
+  if (n == kChunk) {
+    for (int q = threadIdx.x; q < kChunk / 4; q += blockDim.x)
+      reinterpret_cast<float4*>(buf)[q] = reinterpret_cast<const float4*>(a)[q];
+    __syncthreads();
+    constexpr int kLeaves = kChunk / kLeaf;   // 64
+    if (threadIdx.x < kLeaves) leaf_val[threadIdx.x] = pw_leaf(buf + threadIdx.x * kLeaf, kLeaf);
+    __syncthreads();
+    for (int w = kLeaves / 2; w >= 1; w >>= 1) {
+      float v = 0.f;
+      if (threadIdx.x < w) v = leaf_val[2 * threadIdx.x] + leaf_val[2 * threadIdx.x + 1];
+      __syncthreads();
+      if (threadIdx.x < w) leaf_val[threadIdx.x] = v;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) chunk_sum[blockIdx.x] = leaf_val[0];
+    return;
+  }
   if (threadIdx.x == 0) {
     // enumerate leaves in order with an explicit stack of (off, n)
     int st_off[32], st_n[32], sp = 0, k = 0;
@@ -234,107 +256,94 @@ __global__ void k_per_cdf(const int64_t* q, const int64_t* block_off, const floa
     cdf[i] = (double)(q[i] + block_off[i / kScanBlock]) / last;
 }
 
-// 6. uniforms (numpy MT stream), searchsorted(side='right'), IS weights
-__device__ __forceinline__ uint32_t mt_temper_p(uint32_t y) {
-  y ^= y >> 11;
-  y ^= (y << 7) & 0x9D2C5680u;
-  y ^= (y << 15) & 0xEFC60000u;
-  y ^= y >> 18;
-  return y;
-}
-
-__device__ void mt_twist_serial_p(uint32_t* key) {
-  for (int i = 0; i < 624; ++i) {
-    const uint32_t y = (key[i] & 0x80000000u) | (key[(i + 1) % 624] & 0x7FFFFFFFu);
-    key[i] = key[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908B0DFu : 0u);
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_per_draw(const double* cdf, const float* probs,
-                                                   int64_t len, int k, uint32_t* mt, int gen_u,
-                                                   const double* u_in, double* u_buf,
-                                                   DevScalars* sc, double beta_start,
-                                                   double beta_frames, int32_t* idx32,
-                                                   int64_t* idx64, float* w_out) {
-#pragma clang fp contract(off)
-  __shared__ uint32_t key[624];
-  __shared__ int s_pos;
-  __shared__ float s_wmax[16];
-  __shared__ float s_beta;
+// 6a. k uniforms from numpy's MT19937 (random_sample: 53-bit doubles from word pairs),
+// one workgroup, block-parallel twist (replay_dev.h); the generator state is written
+// back with exactly the words numpy consumes.  Also beta for this draw
+// (replay_buffer.py:54; -beta stored after the k uniforms) and frame += 1.
+__global__ __launch_bounds__(1024) void k_per_uniforms(uint32_t* mt, int gen_u, const double* u_in,
+                                                       double* u_out, int k, DevScalars* sc,
+                                                       double beta_start, double beta_frames) {
+  extern __shared__ uint32_t words[];   // 2k words
+  __shared__ uint32_t key[kMtN];
   const int t = threadIdx.x;
   if (gen_u) {
-    for (int i = t; i < 624; i += blockDim.x) key[i] = mt[i];
-    if (t == 0) s_pos = (int)mt[624];
+    for (int i = t; i < kMtN; i += blockDim.x) key[i] = mt[i];
+    int pos = (int)mt[kMtN];
     __syncthreads();
-    // 2k words in stream order; a block twist (serial, one lane) whenever exhausted
-    int done = 0;
     const int need = 2 * k;
-    uint32_t* words = reinterpret_cast<uint32_t*>(u_buf);   // reuse as scratch (<= 2k words)
-    while (done < need) {
-      // every wave reads the position between two barriers, so all take the same
-      // branch below (thread 0 rewrites s_pos only after the second barrier)
-      __syncthreads();
-      int pos = s_pos;
-      __syncthreads();
-      if (pos >= 624) {
-        if (t == 0) { mt_twist_serial_p(key); s_pos = 0; }
-        __syncthreads();
-        pos = 0;
-      }
-      const int take = min(624 - pos, need - done);
-      for (int j = t; j < take; j += blockDim.x) words[done + j] = mt_temper_p(key[pos + j]);
-      __syncthreads();
-      if (t == 0) s_pos = pos + take;
+    for (int done = 0; done < need;) {     // every thread tracks pos/done identically
+      if (pos >= kMtN) { mt_twist_block(key); pos = 0; }
+      const int take = min(kMtN - pos, need - done);
+      for (int j = t; j < take; j += blockDim.x) words[done + j] = mt_temper(key[pos + j]);
       done += take;
-    }
-    __syncthreads();
-    for (int i = t; i < 624; i += blockDim.x) mt[i] = key[i];
-    if (t == 0) mt[624] = (uint32_t)s_pos;
-    __syncthreads();
-    // convert pairs to doubles (in place, back to front safe: i-th double uses words
-    // 2i, 2i+1 which are at or after its own byte range)
-    for (int i = 0; i < k; i += blockDim.x) {
-      const int j = i + t;
-      uint32_t w0 = 0, w1 = 0;
-      if (j < k) { w0 = words[2 * j]; w1 = words[2 * j + 1]; }
-      __syncthreads();
-      if (j < k)
-        u_buf[j] = ((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) / 9007199254740992.0;
+      pos += take;
       __syncthreads();
     }
+    for (int i = t; i < kMtN; i += blockDim.x) mt[i] = key[i];
+    if (t == 0) mt[kMtN] = (uint32_t)pos;
+    for (int j = t; j < k; j += blockDim.x)
+      u_out[j] = ((double)(words[2 * j] >> 5) * 67108864.0 + (double)(words[2 * j + 1] >> 6)) /
+                 9007199254740992.0;
   } else {
-    for (int j = t; j < k; j += blockDim.x) u_buf[j] = u_in[j];
-    __syncthreads();
+    for (int j = t; j < k; j += blockDim.x) u_out[j] = u_in[j];
   }
   if (t == 0) {
     const double fr = (double)sc->per_frame;
     double beta = beta_start + fr * (1.0 - beta_start) / beta_frames;
     if (beta > 1.0) beta = 1.0;
-    s_beta = (float)(-beta);
+    u_out[k] = -beta;
     sc->per_frame += 1;
   }
+}
+
+// 6b. searchsorted(cdf, u, 'right') per draw: the block containing the answer is found
+// in an LDS copy of every `stride`-th cdf value, then a binary search inside it; IS
+// weight (len*P)^-beta and its maximum (weights > 0: the max of the float bits is
+// order-independent, hence deterministic).
+constexpr int kTopMax = 2048;
+__global__ __launch_bounds__(256) void k_per_search(const double* cdf, const float* probs,
+                                                    int64_t len, int64_t stride, int ntop,
+                                                    const double* u, int k, int32_t* idx32,
+                                                    int64_t* idx64, float* w_out,
+                                                    unsigned int* wmax_bits) {
+#pragma clang fp contract(off)
+  __shared__ double top[kTopMax];
+  for (int i = threadIdx.x; i < ntop; i += blockDim.x) {
+    const int64_t e = (int64_t)(i + 1) * stride - 1;
+    top[i] = cdf[e < len ? e : len - 1];
+  }
   __syncthreads();
-  float wmax = 0.f;
-  for (int j = t; j < k; j += blockDim.x) {
-    const double u = u_buf[j];
-    int64_t lo = 0, hi = len;            // first index with cdf > u
-    while (lo < hi) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  float pw = 0.f;
+  if (j < k) {
+    const double uj = u[j];
+    int tlo = 0, thi = ntop;             // first top entry > u
+    while (tlo < thi) {
+      const int mid = (tlo + thi) >> 1;
+      if (top[mid] > uj) thi = mid; else tlo = mid + 1;
+    }
+    int64_t lo = (int64_t)tlo * stride;
+    int64_t hi = lo + stride < len ? lo + stride : len;
+    if (lo > len) lo = len;
+    while (lo < hi) {                    // first index with cdf > u inside the block
       const int64_t mid = (lo + hi) >> 1;
-      if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+      if (cdf[mid] > uj) hi = mid; else lo = mid + 1;
     }
     if (lo > len - 1) lo = len - 1;
     idx32[j] = (int32_t)lo;
     idx64[j] = lo;
-    const float pw = powf((float)len * probs[lo], s_beta);
+    pw = powf((float)len * probs[lo], (float)u[k]);
     w_out[j] = pw;
-    wmax = fmaxf(wmax, pw);
   }
-  for (int o = 32; o >= 1; o >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o, 64));
-  if ((t & 63) == 0) s_wmax[t >> 6] = wmax;
-  __syncthreads();
-  float m = 0.f;
-  for (int q = 0; q < (int)(blockDim.x >> 6); ++q) m = fmaxf(m, s_wmax[q]);
-  for (int j = t; j < k; j += blockDim.x) w_out[j] = w_out[j] / m;
+  unsigned int m = __float_as_uint(pw);
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(wmax_bits, m);
+}
+
+// 6c. w /= w.max()
+__global__ void k_per_wnorm(float* w, int k, const unsigned int* wmax_bits) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < k) w[j] = w[j] / __uint_as_float(*wmax_bits);
 }
 
 void launch_per_sample(const PerArgs& a, hipStream_t s) {
@@ -345,15 +354,22 @@ void launch_per_sample(const PerArgs& a, hipStream_t s) {
   const int nchunk = (int)((len + kChunk - 1) / kChunk);
   hipLaunchKernelGGL(k_per_chunk_sum, dim3(nchunk), dim3(128), 0, s, a.probs, len, a.chunk_sums);
   const int nb = (int)((len + kScanBlock - 1) / kScanBlock);
-  (void)hipMemsetAsync(a.bad, 0, 4, s);
+  (void)hipMemsetAsync(a.bad, 0, 8, s);     // bad flag, max-weight bits
   hipLaunchKernelGGL(k_per_norm_scan, dim3(nb), dim3(kScanBlock), 0, s, a.probs, len,
                      a.chunk_sums, nchunk, a.q, a.block_sums, a.bad);
   hipLaunchKernelGGL(k_per_scan_blocks, dim3(1), dim3(1024), 0, s, a.block_sums, nb);
   hipLaunchKernelGGL(k_per_cdf, dim3((unsigned)blocks), dim3(256), 0, s, a.q, a.block_sums,
                      a.probs, len, a.bad, a.cdf);
-  hipLaunchKernelGGL(k_per_draw, dim3(1), dim3(1024), 0, s, a.cdf, a.probs, len, a.k, a.mt,
-                     a.gen_u, a.u, a.u_scratch, a.sc, a.beta_start, a.beta_frames, a.idx32,
-                     a.idx_out, a.w_out);
+  hipLaunchKernelGGL(k_per_uniforms, dim3(1), dim3(1024), (size_t)a.k * 8, s, a.mt, a.gen_u,
+                     a.u, a.u_scratch, a.k, a.sc, a.beta_start, a.beta_frames);
+  int64_t stride = 1024;
+  while ((len + stride - 1) / stride > kTopMax) stride *= 2;
+  const int ntop = (int)((len + stride - 1) / stride);
+  const int sg = (a.k + 255) / 256;
+  unsigned int* wmax = reinterpret_cast<unsigned int*>(a.bad + 1);
+  hipLaunchKernelGGL(k_per_search, dim3(sg), dim3(256), 0, s, a.cdf, a.probs, len, stride, ntop,
+                     a.u_scratch, a.k, a.idx32, a.idx_out, a.w_out, wmax);
+  hipLaunchKernelGGL(k_per_wnorm, dim3(sg), dim3(256), 0, s, a.w_out, a.k, wmax);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) fprintf(stderr, "sacmi: PER launch failed: %s\n", hipGetErrorString(e));
 }
