@@ -174,7 +174,7 @@ def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False):
                        f"{len(r)} rows (float32 rows); {threads} threads on {cpu}")
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -189,22 +189,31 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--updates-per-launch", type=int, default=20,
                     help="updates per device launch (trainer.py updates_per_step loop)")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="run the data-parallel path even at world size 1 (overhead check)")
     ap.add_argument("--profile-only", action="store_true",
                     help="just run warmup+steps (for rocprofv3 runs)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.batch is None:                 # both the single-GPU and the DP paths use it
+        args.batch = 4096 if args.config == 3 else BATCH
+    return args
+
+
+def main():
+    args = parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    per = args.config == 3
+    if world > 1 or args.force_dp:
         from sacmi.dp import run_dp_bench
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
         return run_dp_bench(args, rank, world, local_rank)
 
     from sacmi import Config, Context
     torch.cuda.init()
-    per = args.config == 3
-    if args.batch is None:
-        args.batch = 4096 if per else BATCH
     fill = args.fill
     ctx = Context(Config(S_DIM, A_DIM, HIDDEN, max_batch=args.batch, capacity=fill, seed=1,
                          replay="per" if per else "uniform"), 0)

@@ -684,6 +684,11 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
   // workgroups of the current one
   const bool ride = reps > 1 && phase_mask == 7 && dev_idx && ride_possible(c, B);
   auto enqueue_all = [&]() {
+    if (phase_mask == 5) {   // phase 2 of the previous update, then phase 0 of the next
+      enqueue_update(c, B, dev_idx, dev_eps, 4, grad_scale, use_ring);
+      enqueue_update(c, B, dev_idx, dev_eps, 1, grad_scale, use_ring);
+      return;
+    }
     for (int r = 0; r < reps; ++r)
       enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring, ride ? (r & 1) : 0,
                      ride && r > 0, ride && r + 1 < reps);
@@ -1123,9 +1128,9 @@ int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_o
 
 int sacmi_step_phase(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scale) {
   return guard([&] {
-    REQUIRE(phase >= 0 && phase <= 2, SACMI_EVALUE, "phase must be 0, 1 or 2");
-    if (phase == 0) check_batch(c, batch);
-    run_update(c, batch, 1, 1, 1 << phase, grad_scale, false);
+    REQUIRE(phase >= 0 && phase <= 3, SACMI_EVALUE, "phase must be 0, 1, 2 or 3");
+    if (phase == 0 || phase == 3) check_batch(c, batch);
+    run_update(c, batch, 1, 1, phase == 3 ? 5 : 1 << phase, grad_scale, false);
   });
 }
 

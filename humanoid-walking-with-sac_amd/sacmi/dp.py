@@ -12,6 +12,10 @@ the post-Adam critics, sac_imp.py:101-125):
            all_reduce(SUM) [policy grads | dL/dlog_alpha]
   phase 2  actor Adam (x 1/world) + alpha
 
+Phase 2 of one update and phase 0 of the next have no collective between them, so the
+driver defers phase 2 and launches it together with the next phase 0 (library phase 3);
+``flush()`` runs a deferred phase 2 (before reading parameters).
+
 Every rank applies the identical reduced gradient with the identical deterministic
 kernels, so replicas stay bitwise identical.  The collectives run on tensors that
 alias the library's gradient arena (torch allocates it, libsacmi adopts it), ordered
@@ -45,25 +49,39 @@ class GpuBackend:
             views.append(self.arena.narrow(0, off, numel))
         self.critic_grads, self.actor_grads = views
 
+    supports_fused_tail = True     # library phase 3 = phase 2 + next phase 0
+
     def phase(self, p: int, batch: int, grad_scale: float) -> None:
         self.ctx.step_phase(batch, p, grad_scale)
 
 
 class DataParallelUpdate:
-    """Callable running one update across the process group."""
+    """Callable running one update across the process group (its actor Adam is
+    deferred into the next call; ``flush()`` completes it)."""
 
     def __init__(self, backend, group=None):
         self.backend = backend
         self.group = group
         self.world = dist.get_world_size(group)
+        self._pending = None       # batch of an update whose phase 2 has not run
 
     def __call__(self, batch: int) -> None:
         b, scale = self.backend, 1.0 / self.world
-        b.phase(0, batch, scale)
+        if self._pending is not None and getattr(b, "supports_fused_tail", False):
+            b.phase(3, batch, scale)
+        else:
+            self.flush()
+            b.phase(0, batch, scale)
+        self._pending = None
         dist.all_reduce(b.critic_grads, op=dist.ReduceOp.SUM, group=self.group)
         b.phase(1, batch, scale)
         dist.all_reduce(b.actor_grads, op=dist.ReduceOp.SUM, group=self.group)
-        b.phase(2, batch, scale)
+        self._pending = batch
+
+    def flush(self) -> None:
+        if self._pending is not None:
+            self.backend.phase(2, self._pending, 1.0 / self.world)
+            self._pending = None
 
 
 def run_dp_bench(args, rank: int, world: int, local_rank: int):
@@ -86,12 +104,14 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int):
     upd = DataParallelUpdate(GpuBackend(ctx, device))
     for _ in range(args.warmup):
         upd(args.batch)
+    upd.flush()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         upd(args.batch)
+    upd.flush()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()

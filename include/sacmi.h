@@ -167,7 +167,9 @@ int sacmi_fetch_losses(sacmi_ctx* ctx, float* out, int32_t max_steps, int32_t* n
 
 /* Data-parallel split of the step (one process per GPU).  phase 0: sample, gather,
  * forward, critic backward -> critic gradient buffer; phase 1: critic Adam + Polyak,
- * actor forward/backward -> actor gradient buffer; phase 2: actor Adam + alpha.
+ * actor forward/backward -> actor gradient buffer; phase 2: actor Adam + alpha;
+ * phase 3: phase 2 of the previous update then phase 0 of the next, in one launch
+ * (no collective sits between them).
  * Between phases the caller all-reduces (sum) the buffer named by
  * sacmi_grad_buffer(which=0 critic, 1 actor); grad_scale (1/world) is applied by the
  * Adam kernels. */

@@ -109,6 +109,7 @@ def worker(rank, world, port, cfg, params, shards, idx, eps1, eps2, out_dir, ste
         i = idx[t][rank]
         be.set_batch(*[x[i] for x in rows], eps1[t][rank], eps2[t][rank])
         upd(len(i))
+    upd.flush()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **be.state())
     dist.barrier()
     dist.destroy_process_group()

@@ -323,6 +323,7 @@ def test_dp_phase_path_matches_fused_step_world1():
         for _ in range(3):
             upd(64)
             ctxs[1].step(64)
+        upd.flush()
         torch.cuda.synchronize()
         for n in NETS:
             a, b = ctxs[0].get_net(n), ctxs[1].get_net(n)
