@@ -693,7 +693,11 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
       enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring, ride ? (r & 1) : 0,
                      ride && r > 0, ride && r + 1 < reps);
   };
-  if (!c->use_graphs) {
+  // the caller is capturing this stream into its own graph (e.g. torch.cuda.graph around
+  // a data-parallel update and its collectives): enqueue into that capture directly
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  CHECK_HIP(hipStreamIsCapturing(c->stream, &cap));
+  if (!c->use_graphs || cap != hipStreamCaptureStatusNone) {
     enqueue_all();
     CHECK_HIP(hipGetLastError());
     return;

@@ -84,6 +84,52 @@ class DataParallelUpdate:
             self._pending = None
 
 
+class CapturedDataParallelUpdates:
+    """Runs data-parallel updates as replays of torch.cuda.CUDAGraphs, each holding `n`
+    consecutive updates — library launches and RCCL all-reduces — on one dedicated
+    stream (the trainer's updates_per_step loop without per-update host launches).
+    Every rank captures the same sequence, so the collectives pair up across ranks on
+    replay.  Results are bit-identical to the eager driver (tests/test_gpu_parity.py)."""
+
+    def __init__(self, ctx, device: torch.device, batch: int, group=None):
+        self.device, self.batch = device, batch
+        self.stream = torch.cuda.Stream(device)
+        with torch.cuda.stream(self.stream):
+            self.backend = GpuBackend(ctx, device)
+        ctx.set_stream(self.stream.cuda_stream)
+        self.upd = DataParallelUpdate(self.backend, group)
+        self.graphs = {}
+        # one eager update on the capture stream first: the library's phase graphs and
+        # the communicator's buffers exist before any capture begins
+        with torch.cuda.stream(self.stream):
+            self.upd(batch)
+            self.upd.flush()
+        torch.cuda.synchronize(device)
+
+    def _graph(self, n: int):
+        g = self.graphs.get(n)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream):
+                for _ in range(n):
+                    self.upd(self.batch)
+                self.upd.flush()
+            self.graphs[n] = g
+        return g
+
+    def prepare(self, *sizes: int) -> None:
+        for n in sizes:
+            if n > 0:
+                self._graph(n)
+
+    def run(self, updates: int, per_launch: int) -> None:
+        full, rem = divmod(updates, per_launch)
+        for _ in range(full):
+            self._graph(per_launch).replay()
+        if rem:
+            self._graph(rem).replay()
+
+
 def run_dp_bench(args, rank: int, world: int, local_rank: int):
     """bench.py --gpus N under torch.distributed.run (one rank per GPU)."""
     import bench as B
@@ -101,17 +147,34 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int):
     chunk = 100_000
     for c0 in range(0, fill, chunk):
         ctx.push(*B.synth(min(chunk, fill - c0), 5000 + rank * 7919 + c0))
-    upd = DataParallelUpdate(GpuBackend(ctx, device))
-    for _ in range(args.warmup):
-        upd(args.batch)
-    upd.flush()
+    per_launch = max(1, min(args.updates_per_launch, 256))
+    captured = None
+    if os.environ.get("SACMI_DP_GRAPH", "1") == "1":
+        try:
+            captured = CapturedDataParallelUpdates(ctx, device, args.batch)
+            captured.prepare(min(per_launch, args.steps), args.steps % per_launch,
+                             args.warmup % per_launch)
+        except Exception as e:                     # capture unsupported: eager driver
+            if rank == 0:
+                print(f"sacmi.dp: graph capture failed ({e}); eager updates", flush=True)
+            captured = None
+            torch.cuda.synchronize()
+    if captured is None:
+        upd = DataParallelUpdate(GpuBackend(ctx, device))
+
+        def run(k):
+            for _ in range(k):
+                upd(args.batch)
+            upd.flush()
+    else:
+        def run(k):
+            captured.run(k, per_launch)
+    run(args.warmup)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        upd(args.batch)
-    upd.flush()
+    run(args.steps)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -140,6 +203,8 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int):
                        "global_batch": args.batch * world, "replay_fill": fill * world,
                        "parallelism": f"dp{world}"},
             "iterations_per_s": round(iters, 2),
+            "updates_per_launch": per_launch if captured else 1,
+            "dp_graph": captured is not None,
             "mfma_util_step": round(flops * value / 1e12 / B.PEAK_FP32_MFMA_TFLOPS / world, 4),
             "replicas_bitwise_equal": replicas_equal,
             "roofline": None, "cpu_baseline": None,

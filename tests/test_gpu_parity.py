@@ -330,5 +330,26 @@ def test_dp_phase_path_matches_fused_step_world1():
             for k in a:
                 assert np.array_equal(a[k], b[k]), (n, k)
         assert ctxs[0].get_scalar(0) == ctxs[1].get_scalar(0)
+        # the same updates as torch.cuda.CUDAGraph replays (phases + RCCL all-reduce in
+        # one graph), 5 = 2 + 2 + 1 updates: bit-identical to the eager driver
+        from sacmi.dp import CapturedDataParallelUpdates
+        cap = []
+        for _ in range(2):
+            ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=3)
+            load_params(ctx, params)
+            ctx.push(*rows)
+            ctx.set_mt(0, key, 624)
+            cap.append(ctx)
+        eager = DataParallelUpdate(GpuBackend(cap[1], torch.device("cuda", 0)))
+        for _ in range(6):                 # the captured object's warm-up update + 5
+            eager(64)
+        eager.flush()
+        g = CapturedDataParallelUpdates(cap[0], torch.device("cuda", 0), 64)
+        g.run(5, 2)
+        torch.cuda.synchronize()
+        for n in NETS:
+            a, b = cap[0].get_net(n), cap[1].get_net(n)
+            for k in a:
+                assert np.array_equal(a[k], b[k]), ("captured", n, k)
     finally:
         dist.destroy_process_group()
