@@ -116,14 +116,22 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // never wait for them and their latency hides under the (last) MFMA phase.
 // With MG > 1 the workgroup covers MG*TM rows: wave group g = wave / KSPLIT takes rows
 // m0 + g*TM .. +TM, and the K split runs inside each group.
-template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1, class Pre>
+// AXF 1: A-operand transform (GemmDesc::axk) applied to the loaded fragments before the
+// MFMAs: a(b,k) = A>0 ? coef[row]*w[k] : 0 with coef in LDS (coef[tile row]); with
+// store_a the transformed fragments are also written to d.ax_out.
+template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
+          int AXF = 0, class Pre, class Early = void (*)()>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
-                                            float* rsum, Pre&& pre) {
+                                            float* rsum, Pre&& pre, const float* coef = nullptr,
+                                            bool store_a = false, const float* axw = nullptr,
+                                            Early&& early = [] {}) {
   constexpr int MT = TM / 16, NT = TN / 16;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int ks = wave % KSPLIT;
-  m0 += (wave / KSPLIT) * TM;
+  const int mloc = (wave / KSPLIT) * TM;   // this wave group's first row in the tile
+  m0 += mloc;
+
   SACMI_STAMP(wave);
   f4 acc[MT][NT];
 #pragma unroll
@@ -141,6 +149,9 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   const int nmine = nch > ks ? (nch - ks + KSPLIT - 1) / KSPLIT : 0;
   const int kl = 4 * (lane >> 4);
   float a[G][MT][4], b[G][NT][4];
+  // AXF 1: the row prologue's own loads go out FIRST (older than every operand load), so
+  // its exchange barrier waits for them alone while the operands keep streaming in
+  if constexpr (AXF == 1) early();
   if (nmine == 0) pre();
   for (int j = 0; j < nmine; j += G) {
 #pragma unroll
@@ -151,10 +162,29 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
         fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
       }
     }
-    if (j + G >= nmine) pre();       // after the LAST operand loads (vmcnt is in order)
+    // after the LAST operand loads (vmcnt is in order); a row prologue (AXF 1) must
+    // run before the first transform
+    if (AXF == 1 ? j == 0 : j + G >= nmine) pre();
 #pragma unroll
     for (int g = 0; g < G; ++g)
       if (j + g < nmine) {
+        if constexpr (AXF == 1) {
+          const int k = (ks + (j + g) * KSPLIT) * 16 + kl;
+          float xw[4];                     // w[k..k+3] from the LDS copy (K <= 1024)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) xw[s] = axw[k + s < d.K ? k + s : d.K - 1];
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const int r = mloc + i * 16 + (lane & 15);
+            const float cf = coef[r];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) a[g][i][s] = a[g][i][s] > 0.f ? cf * xw[s] : 0.f;
+            // the rows this level's tile-0 workgroups hold in full: dh2 for a later level
+            if (store_a && m0 - mloc + r < d.M && k < d.K)
+              *reinterpret_cast<float4*>(d.ax_out + (size_t)(m0 - mloc + r) * d.ax_ld + k) =
+                  float4{a[g][i][0], a[g][i][1], a[g][i][2], a[g][i][3]};
+          }
+        }
         mfma_chunk<MT, NT>(acc, a[g], b[g]);
         if (ROWSUM) {
 #pragma unroll
@@ -184,9 +214,20 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
 }
 
 // layout dispatch (wave-uniform, once per workgroup)
-template <int TM, int TN, int KSPLIT, int G, int MG, class Pre>
+// AXK: whether this kernel instantiation carries the A-transform path (launch_gemm picks
+// the variant from the level's descs): 1 -> axk 1 descs, 0 -> none.
+template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, class Pre, class Early>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
-                                          float* rsum, bool rowsum, Pre&& pre) {
+                                          float* rsum, bool rowsum, Pre&& pre, const float* coef,
+                                          const float* axw, Early&& early) {
+  if constexpr (AXK == 1) {
+    if (d.axk == 1) {        // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
+      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1>(d, m0, n0, red, rsum, pre, coef,
+                                                               n0 == 0 && d.ax_out != nullptr, axw,
+                                                               early);
+      return;
+    }
+  }
   if (d.a_kc) {
     if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG>(d, m0, n0, red, rsum, pre);
     else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG>(d, m0, n0, red, rsum, pre);
@@ -274,6 +315,113 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // log_alpha step (alpha = exp(log_alpha), sac_imp.py:128-135) and fills the loss ring.
 // waves per SIMD the register allocation must allow: 4-wave tiles run one wave per SIMD
 // (full register file), 64x64 8-wave tiles two, the 16-wave tiles four
+// Row prologue of an axk-1 level (runs inside pre(), i.e. while the operand loads are in
+// flight): four threads per batch row sum the dot partials of its heads, the row's
+// thread loads r, d, logp meanwhile and turns the heads into the per-row coefficients
+// of the backward —
+//   critic (sac_imp.py:87-113): q^ = r + (1-d) gamma (min(qt1,qt2) - alpha logp'),
+//           coef_i = dL/dq_i = 2 (q_i - q^) / B, loss partial sum (q_i - q^)^2
+//   actor (sac_imp.py:116-121): coef_i = dL/dqa_i = -[i is the min]/B (ties 1/2 : 1/2),
+//           loss partial sum (alpha logp - min qa)
+// `writer` (one workgroup per row block) stores the coefficients and the loss partial;
+// the actor's block 0 also advances the step counters and forms dL/dlog_alpha.  Every
+// thread of the workgroup calls it (two barriers).
+// Registers a thread carries from rows_load() (before the operand loads) to
+// rows_finish() (after them).
+struct RowsRegs {
+  float q;                    // thread (row, slot): the head's finished value
+  float r, d, lp, alpha;      // thread row < TMW: the row's own inputs
+};
+
+template <int TMW>
+__device__ __forceinline__ void rows_load(const RowsFuse& rf, int m0, RowsRegs& x) {
+  const int t = threadIdx.x;
+  const int nslot = rf.kind == 1 ? 4 : 2;
+  x.q = 0.f;
+  if (t < TMW * nslot) {
+    const int row = t / nslot, sl = t % nslot, b = m0 + row;
+    if (b < rf.B) {
+      const float* pp = rf.part + ((size_t)sl * rf.B + b) * rf.nparts;
+      float acc = pp[0];
+      for (int i = 1; i < rf.nparts; ++i) acc += pp[i];
+      x.q = acc + *rf.b3[sl];
+    }
+  }
+  x.r = x.d = x.lp = x.alpha = 0.f;
+  const int b = m0 + t;
+  if (t < TMW && b < rf.B) {
+    x.alpha = rf.sc->alpha;
+    x.lp = rf.logp[b];
+    if (rf.kind == 1) { x.r = rf.r[b]; x.d = rf.d[b]; }
+  }
+}
+
+template <int TMW>
+__device__ void rows_finish(const RowsFuse& rf, int m0, bool writer, bool first_block,
+                            const RowsRegs& x, float (*s_q)[4], float (*s_coef)[TMW],
+                            float (*s_l)[2]) {
+  const int t = threadIdx.x;
+  const int nslot = rf.kind == 1 ? 4 : 2;
+  if (t < TMW * nslot) s_q[t / nslot][t % nslot] = x.q;
+  if (first_block && rf.kind == 2) {
+    const int w0 = TMW * nslot;            // first wave past the partial-sum threads
+    if (t >= w0 && t < w0 + 64) {
+      // dL/dlog_alpha = -mean(logp_a + te) (sac_imp.py:128-133) from the heads kernel's
+      // per-workgroup sums: strided per lane, then a fixed butterfly
+      const int lane = t - w0;
+      float acc = 0.f;
+      if (rf.alpha_grad)
+        for (int w = lane; w < rf.n_lp; w += 64) acc += rf.logp_part[2 * w + 1];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (lane == 0) {
+        if (rf.alpha_grad) *rf.alpha_grad = -(acc + (float)rf.B * rf.target_entropy) / (float)rf.B;
+        // step counters: the critic Adam ran before this level, the actor Adam after
+        for (int i = 0; i < 4; ++i) {
+          rf.sc->step[i] += 1.0;
+          rf.sc->beta_pow[i][0] *= 0.9;   // torch Adam default betas (sac_imp.py:39-49)
+          rf.sc->beta_pow[i][1] *= 0.999;
+        }
+        rf.sc->noise_counter += 1;
+      }
+    }
+  }
+  __syncthreads();
+  SACMI_STAMP(36);
+  const int b = m0 + t;
+  if (t < TMW) {
+    float c0 = 0.f, c1 = 0.f, l0 = 0.f, l1 = 0.f;
+    if (b < rf.B) {
+      if (rf.kind == 1) {
+        const float vt = fminf(s_q[t][2], s_q[t][3]) - x.alpha * x.lp;
+        const float qhat = x.r + ((1.f - x.d) * rf.gamma) * vt;
+        const float e1 = s_q[t][0] - qhat, e2 = s_q[t][1] - qhat;
+        c0 = 2.f * e1 / (float)rf.B;
+        c1 = 2.f * e2 / (float)rf.B;
+        l0 = e1 * e1;
+        l1 = e2 * e2;
+      } else {
+        const float q1 = s_q[t][0], q2 = s_q[t][1];
+        l0 = x.alpha * x.lp - fminf(q1, q2);
+        const float g = -1.f / (float)rf.B;
+        const float w1 = q1 < q2 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
+        c0 = g * w1;
+        c1 = g * (1.f - w1);
+      }
+      if (writer && rf.dq) { rf.dq[b] = c0; rf.dq[rf.B + b] = c1; }
+    }
+    s_coef[0][t] = c0; s_coef[1][t] = c1;
+    s_l[t][0] = l0; s_l[t][1] = l1;
+  }
+  __syncthreads();                         // coefficients visible to the transform
+  SACMI_STAMP(35);
+  if (writer && t < (rf.kind == 1 ? 2 : 1)) {
+    float acc = 0.f;
+    for (int r = 0; r < TMW; ++r) acc += s_l[r][t];
+    rf.loss_part[(m0 / TMW) * (rf.kind == 1 ? 2 : 1) + t] = acc;
+  }
+}
+
 // waves per SIMD the register allocation must allow: every wave of the workgroup
 // resident at once, one workgroup per CU
 template <int W>
@@ -281,12 +429,14 @@ constexpr int gemm_min_waves() { return W >= 4 ? W / 4 : 1; }
 
 // TM x TN per wave group, MG wave groups (workgroup tile MG*TM x TN), K split KSPLIT
 // ways inside each group; ADAM: fused optimizer epilogue (every desc EPI_ADAM*)
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM>
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0>
 __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
   constexpr int TMW = TM * MG;
   __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
   __shared__ float rsum[MG * KSPLIT * TM];
   __shared__ AdamScalars s_k;
+  __shared__ float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
+  __shared__ float s_axw[AXK == 1 ? 1024 : 1];   // the transform's w3 row
   const int bid = blockIdx.x;
   if (bid >= batch.total_tiles) {   // ride-along workgroups (next update's replay work)
     if constexpr (MG * KSPLIT == 16) {   // the host attaches rides to 1024-thread configs
@@ -359,8 +509,15 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   // Adam: param, exp_avg, exp_avg_sq, target; otherwise x0 = the bias or the ReLU-mask
   // source (a level has one or the other: validate())
   float x0[NS], x1[ADAM ? NS : 1], x2[ADAM ? NS : 1], x3[ADAM ? NS : 1];
-  // the epilogue operands (Adam state, or the bias / mask) go out under the MFMAs
+  RowsRegs rows_x{};
+  // the epilogue operands (Adam state, or the bias / mask) go out under the MFMAs; the
+  // fc3 dot weights of the tile go to LDS; an axk-1 level runs its row prologue
   auto pre = [&]() {
+    if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? d.dotw[n0 + tid] : 0.f;
+    if constexpr (AXK == 1) {
+      if (d.axk == 1)
+        rows_finish<TMW>(batch.rows, m0, p == 0 && n0 == 0, bid == 0, rows_x, s_q, s_coef, s_l);
+    }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       int row, col, n;
@@ -375,34 +532,54 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
       }
     }
   };
-  gemm_core<TM, TN, KSPLIT, G, MG>(d, m0, n0, red, rsum, rowsum, pre);
+  auto early = [&]() {       // axk 1: the row prologue's loads, ahead of the operand loads
+    if constexpr (AXK == 1) {
+      for (int k = tid; k < d.K; k += NTH) s_axw[k] = d.ax_w[k];   // read after the barriers
+      rows_load<TMW>(batch.rows, m0, rows_x);
+    }
+  };
+  gemm_core<TM, TN, KSPLIT, G, MG, AXK>(d, m0, n0, red, rsum, rowsum, pre, s_coef[d.ax_slot], s_axw,
+                                        early);
   __syncthreads();
   if (threadIdx.x < 64) SACMI_STAMP(32);
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     int row, col, n;
-    if (!slot(s, row, col, n)) continue;
-    float v;
-    if (s < EPT) {
-      v = reduce_partials<TM, TN, KSPLIT, MG>(red, row, col);
-    } else {
-      const float* rb = rsum + (row / TM) * KSPLIT * TM + row % TM;
-      v = rb[0];
+    const bool ok = slot(s, row, col, n);
+    float v = 0.f;
+    if (ok) {
+      if (s < EPT) {
+        v = reduce_partials<TM, TN, KSPLIT, MG>(red, row, col);
+      } else {
+        const float* rb = rsum + (row / TM) * KSPLIT * TM + row % TM;
+        v = rb[0];
 #pragma unroll
-      for (int w = 1; w < KSPLIT; ++w) v += rb[w * TM];
+        for (int w = 1; w < KSPLIT; ++w) v += rb[w * TM];
+      }
+      const uint32_t o = (uint32_t)((m0 + row) * d.ldc + n) * 4u;
+      if constexpr (ADAM) {
+        adam_elem(x0[s], x1[s], x2[s], v, omb1, af.beta2, omb2, af.eps, s_k);
+        if (af.G) buf_st(rG, o, v);
+        buf_st(rC, o, x0[s]); buf_st(rM, o, x1[s]); buf_st(rV, o, x2[s]);
+        if (pol) buf_st(rT, o, polyak(x3[s], x0[s], omtau, af.tau));
+      } else {
+        if (d.bias) v += x0[s];
+        if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
+        else if (d.epi == EPI_MASK) v = x0[s] > 0.f ? v : 0.f;
+        buf_st(rC, o, v);
+      }
     }
-    const uint32_t o = (uint32_t)((m0 + row) * d.ldc + n) * 4u;
-    if constexpr (ADAM) {
-      adam_elem(x0[s], x1[s], x2[s], v, omb1, af.beta2, omb2, af.eps, s_k);
-      if (af.G) buf_st(rG, o, v);
-      buf_st(rC, o, x0[s]); buf_st(rM, o, x1[s]); buf_st(rV, o, x2[s]);
-      if (pol) buf_st(rT, o, polyak(x3[s], x0[s], omtau, af.tau));
-    } else {
-      if (d.bias) v += x0[s];
-      if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
-      else if (d.epi == EPI_MASK) v = x0[s] > 0.f ? v : 0.f;
-      buf_st(rC, o, v);
+    if constexpr (!ADAM) {
+      // fc3 dot partial of this row over its 32-column block: the 32 lanes of a half
+      // wave hold one row's 32 consecutive columns (TN = 32 or 64, row-major slots)
+      if (s < EPT && d.dotp) {
+        float c = ok ? v * s_dotw[col] : 0.f;
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+        if ((tid & 31) == 0 && m0 + row < d.M)
+          d.dotp[(size_t)(m0 + row) * d.dotp_ld + (n0 + col) / 32] = c;
+      }
     }
   }
   if (threadIdx.x < 64) SACMI_STAMP(33);
@@ -474,23 +651,30 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     n_adam += b.d[i].epi >= EPI_ADAM;
   }
   // (Level::add guarantees a level is all-Adam or all-plain)
+  int axk = 0;
+  for (int i = 0; i < b.count; ++i) axk = b.d[i].axk > axk ? b.d[i].axk : axk;
+  const dim3 blk(1024);
   const int t64 = assign_tiles<32, 64>(b);
   if (n_adam && t64 <= 256 && maxk <= 16 * 16) {
     // fused Adam, one 32x64 tile per CU (policy level): 16 waves, one K chunk each
-    hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, true>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
+    hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, true>), dim3(b.total_tiles + extra), blk, 0, s, b);
   } else if (n_adam || (t64 > 256 && maxk <= 16 * 8 * 2)) {
     // weight gradients at batch <= 256 with more 32x64 tiles than CUs (the twin
     // critic level): 64x64 tiles — exactly 256 of them — as two 32-row wave groups,
     // each with an 8-way K split; the epilogue state is prefetched under the MFMAs
-    assign_tiles<64, 64>(b);
-    if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, true>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
-    else hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
+    const int g = assign_tiles<64, 64>(b) + extra;
+    if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, true>), dim3(g), blk, 0, s, b);
+    else hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false>), dim3(g), blk, 0, s, b);
+  } else if (axk == 1) {
+    // dh1 / dha1 with the fc3 backward folded in (row prologue + A transform)
+    const int g = assign_tiles<32, 32>(b) + extra;
+    hipLaunchKernelGGL((k_gemm<32, 32, 16, 2, 1, false, 1>), dim3(g), blk, 0, s, b);
   } else if (t64 >= 192) {
     // widest tile that still gives one workgroup to most CUs
-    hipLaunchKernelGGL((k_gemm<32, 64, 16, 2, 1, false>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
+    hipLaunchKernelGGL((k_gemm<32, 64, 16, 2, 1, false>), dim3(b.total_tiles + extra), blk, 0, s, b);
   } else {
-    assign_tiles<32, 32>(b);
-    hipLaunchKernelGGL((k_gemm<32, 32, 16, 4, 1, false>), dim3(b.total_tiles + extra), dim3(1024), 0, s, b);
+    const int g = assign_tiles<32, 32>(b) + extra;
+    hipLaunchKernelGGL((k_gemm<32, 32, 16, 2, 1, false>), dim3(g), blk, 0, s, b);
   }
   HIP_LAUNCH_CHECK();
 }
@@ -577,12 +761,25 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
     lp[row][j] = lpe;
   }
   __syncthreads();
+  __shared__ float s_lp[TM];
   if (threadIdx.x < TM) {
     const int mm = m0 + threadIdx.x;
+    float s = 0.f;
     if (mm < a.rows) {
-      float s = 0.f;
       for (int jj = 0; jj < A; ++jj) s += lp[threadIdx.x][jj];
       a.logp[mm] = s;
+    }
+    s_lp[threadIdx.x] = s;
+  }
+  if (a.logp_part) {
+    __syncthreads();
+    if (threadIdx.x < 2) {    // rows below / at-or-above split_row, fixed order
+      float s = 0.f;
+      for (int r = 0; r < TM; ++r) {
+        const int mm = m0 + r;
+        if (mm < a.rows && (mm >= a.split_row) == (threadIdx.x == 1)) s += s_lp[r];
+      }
+      a.logp_part[2 * blockIdx.x + threadIdx.x] = s;
     }
   }
 }
@@ -655,176 +852,6 @@ __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
-}
-
-// One wave holds a whole hidden row: lane l keeps float4 chunks q = l + 64 j (j < J)
-// of h (ones column included, so the dot carries the fc3 bias) and of w3, computes
-// the dot, and later writes the row's backward values straight from those registers.
-template <int J>
-struct RowRegs {
-  float4 h[J], w[J];
-};
-
-template <int J>
-__device__ __forceinline__ float row_load_dot(const float* h, const float* w, int K4, int lane,
-                                              RowRegs<J>& r) {
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int q = lane + 64 * j;
-    if (q < K4) {
-      r.h[j] = reinterpret_cast<const float4*>(h)[q];
-      r.w[j] = reinterpret_cast<const float4*>(w)[q];
-    } else {
-      r.h[j] = float4{0.f, 0.f, 0.f, 0.f};
-      r.w[j] = float4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j)
-    s += r.h[j].x * r.w[j].x + r.h[j].y * r.w[j].y + r.h[j].z * r.w[j].z + r.h[j].w * r.w[j].w;
-  return s;
-}
-
-// out[0:H] = dq * w3 * [h > 0] from the registers (H % 4 == 0: chunks q < H/4)
-template <int J>
-__device__ __forceinline__ void row_store_bwd(float* out, float dq, int H4, int lane,
-                                              const RowRegs<J>& r) {
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int q = lane + 64 * j;
-    if (q < H4) {
-      const float4 x = r.h[j], y = r.w[j];
-      reinterpret_cast<float4*>(out)[q] =
-          float4{x.x > 0.f ? dq * y.x : 0.f, x.y > 0.f ? dq * y.y : 0.f,
-                 x.z > 0.f ? dq * y.z : 0.f, x.w > 0.f ? dq * y.w : 0.f};
-    }
-  }
-}
-
-// Target + critic loss rows (sac_imp.py:87-105 forward tail, mse backward).
-// One wave per row b:
-//   q_i = h2_i[b].w3_i ; qt_i = ht2_i[b].w3t_i ;  q^ = r + (1-d)*gamma*(min qt - alpha*logp')
-//   dq_i = 2 (q_i - q^) / B ;  dh2_i[b,:] = dq_i * w3_i * [h2_i > 0]
-constexpr int kRowsPerBlock = 4;
-template <int J>
-__global__ __launch_bounds__(256) void k_critic_rows(CriticRowsArgs a) {
-  __shared__ float part[kRowsPerBlock][2];
-  __shared__ float red[256];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int b = blockIdx.x * kRowsPerBlock + w;
-  const int K4 = (a.H + 1 + 3) / 4;
-  const float alpha = a.sc->alpha;
-  float e1 = 0.f, e2 = 0.f;
-  if (b < a.B) {
-    const float* h1 = a.hq2 + (size_t)b * 2 * a.ldh;
-    const float* t1 = a.hqt2 + (size_t)b * 2 * a.ldh;
-    RowRegs<J> r1, r2, rt1, rt2;
-    float dv[4];
-    dv[0] = row_load_dot<J>(h1, a.w3, K4, lane, r1);
-    dv[1] = row_load_dot<J>(h1 + a.ldh, a.w3 + a.w3_stride, K4, lane, r2);
-    dv[2] = row_load_dot<J>(t1, a.w3t, K4, lane, rt1);
-    dv[3] = row_load_dot<J>(t1 + a.ldh, a.w3t + a.w3_stride, K4, lane, rt2);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) dv[v] = wave_sum(dv[v]);
-    const float q1 = dv[0], q2 = dv[1], qt1 = dv[2], qt2 = dv[3];
-    const float vt = fminf(qt1, qt2) - alpha * a.logp_t[b];
-    const float qhat = a.r[b] + ((1.f - a.d[b]) * a.gamma) * vt;
-    e1 = q1 - qhat;
-    e2 = q2 - qhat;
-    const float dq1 = 2.f * e1 / (float)a.B, dq2 = 2.f * e2 / (float)a.B;
-    if (lane == 0) { a.dq[b] = dq1; a.dq[a.B + b] = dq2; }
-    float* o = a.dh2 + (size_t)b * 2 * a.H;
-    row_store_bwd<J>(o, dq1, a.H / 4, lane, r1);
-    row_store_bwd<J>(o + a.H, dq2, a.H / 4, lane, r2);
-  }
-  if (lane == 0) { part[w][0] = e1 * e1; part[w][1] = e2 * e2; }
-  __syncthreads();
-  if (threadIdx.x < 2) {
-    float s = 0.f;
-    for (int r = 0; r < kRowsPerBlock; ++r) s += part[r][threadIdx.x];
-    a.loss_part[blockIdx.x * 2 + threadIdx.x] = s;
-  }
-  // alpha gradient: d/dlog_alpha of -mean(log_alpha * (logp + te)) = -mean(logp + te)
-  if (blockIdx.x == 0 && a.auto_entropy) {
-    float s = 0.f;
-    for (int i = threadIdx.x; i < a.B; i += 256) s += a.logp_a[i] + a.target_entropy;
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o >= 1; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) *a.alpha_grad = -red[0] / (float)a.B;
-  }
-}
-
-// float4 chunks per lane for a hidden row of H (+1 ones column)
-static int row_chunks(int H) { return ((H + 1 + 3) / 4 + 63) / 64; }
-
-void launch_critic_rows(const CriticRowsArgs& a, hipStream_t s) {
-  const int grid = (a.B + kRowsPerBlock - 1) / kRowsPerBlock;
-  switch (row_chunks(a.H)) {
-    case 1: hipLaunchKernelGGL(k_critic_rows<1>, dim3(grid), dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(k_critic_rows<2>, dim3(grid), dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(k_critic_rows<3>, dim3(grid), dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(k_critic_rows<4>, dim3(grid), dim3(256), 0, s, a); break;
-  }
-  HIP_LAUNCH_CHECK();
-}
-
-// Actor rows (sac_imp.py:116-121): qa_i = ha2_i[b].w3_i with the UPDATED critics,
-// L_pi partial = alpha*logp - min(qa1, qa2); min backward splits ties 1/2 : 1/2.
-// Also advances the step counters (the critic Adam ran before this kernel, the
-// actor Adam runs after it).
-template <int J>
-__global__ __launch_bounds__(256) void k_actor_rows(ActorRowsArgs a) {
-  __shared__ float part[kRowsPerBlock];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int b = blockIdx.x * kRowsPerBlock + w;
-  const int K4 = (a.H + 1 + 3) / 4;
-  const float alpha = a.sc->alpha;
-  float lpart = 0.f;
-  if (b < a.B) {
-    const float* h1 = a.hqa2 + (size_t)b * 2 * a.ldh;
-    RowRegs<J> r1, r2;
-    const float q1 = wave_sum(row_load_dot<J>(h1, a.w3, K4, lane, r1));
-    const float q2 = wave_sum(row_load_dot<J>(h1 + a.ldh, a.w3 + a.w3_stride, K4, lane, r2));
-    const float qmin = fminf(q1, q2);
-    lpart = alpha * a.logp_a[b] - qmin;
-    const float g = -1.f / (float)a.B;
-    const float w1 = q1 < q2 ? 1.f : (q1 == q2 ? 0.5f : 0.f);
-    const float dq1 = g * w1, dq2 = g * (1.f - w1);
-    float* o = a.dha2 + (size_t)b * 2 * a.H;
-    row_store_bwd<J>(o, dq1, a.H / 4, lane, r1);
-    row_store_bwd<J>(o + a.H, dq2, a.H / 4, lane, r2);
-  }
-  if (lane == 0) part[w] = lpart;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int r = 0; r < kRowsPerBlock; ++r) s += part[r];
-    a.loss_part[blockIdx.x] = s;
-    if (blockIdx.x == 0) {
-      for (int i = 0; i < 4; ++i) {
-        a.sc->step[i] += 1.0;
-        a.sc->beta_pow[i][0] *= 0.9;     // torch Adam default betas (sac_imp.py:39-49)
-        a.sc->beta_pow[i][1] *= 0.999;
-      }
-      a.sc->noise_counter += 1;
-    }
-  }
-}
-
-void launch_actor_rows(const ActorRowsArgs& a, hipStream_t s) {
-  const int grid = (a.B + kRowsPerBlock - 1) / kRowsPerBlock;
-  switch (row_chunks(a.H)) {
-    case 1: hipLaunchKernelGGL(k_actor_rows<1>, dim3(grid), dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(k_actor_rows<2>, dim3(grid), dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(k_actor_rows<3>, dim3(grid), dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(k_actor_rows<4>, dim3(grid), dim3(256), 0, s, a); break;
-  }
-  HIP_LAUNCH_CHECK();
 }
 
 // ---------------------------------------------------------------------------

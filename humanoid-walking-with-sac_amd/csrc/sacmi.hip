@@ -106,8 +106,10 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> xq, x2, r, d, hp1, hp2, eps, cache, logp;
   sacmi::DevBuf<float> xqb, x2b, rb, db;
   sacmi::DevBuf<float> hq1, hq2, hqt1, hqt2, hqa1, hqa2;
-  sacmi::DevBuf<float> dq, dh2, dh1, dha2, dha1, dhead, dhp2, dhp1;
-  sacmi::DevBuf<float> lpart_c, lpart_a, ring;
+  sacmi::DevBuf<float> dq, dh2, dh1, dha1, dhead, dhp2, dhp1;
+  sacmi::DevBuf<float> dotp;       // fc3 dot partials [6 slots][B][nparts]
+  int nparts = 0;
+  sacmi::DevBuf<float> lpart_c, lpart_a, ring, lp_part;
   int ring_slots = 0;
   // act scratch
   int act_rows = 0;
@@ -251,11 +253,14 @@ static void alloc_all(sacmi_ctx* c) {
   for (auto* b : {&c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1, &c->hqa2})
     b->alloc((size_t)Bm * 2 * c->Hd);
   c->dq.alloc((size_t)2 * Bm);
-  for (auto* b : {&c->dh2, &c->dh1, &c->dha2, &c->dha1}) b->alloc((size_t)Bm * 2 * H);
+  for (auto* b : {&c->dh2, &c->dh1, &c->dha1}) b->alloc((size_t)Bm * 2 * H);
+  c->nparts = (H + 31) / 32;
+  c->dotp.alloc((size_t)6 * Bm * c->nparts);
   c->dhead.alloc((size_t)Bm * c->lddh);
   c->dhp2.alloc((size_t)Bm * H); c->dhp1.alloc((size_t)Bm * H);
-  const int nb = (Bm + 3) / 4;
-  c->lpart_c.alloc((size_t)nb * 2); c->lpart_a.alloc(nb);
+  const int nrb = (Bm + 31) / 32;    // row blocks of the L5 / L9 tiling (loss partials)
+  c->lpart_c.alloc((size_t)nrb * 2); c->lpart_a.alloc(nrb);
+  c->lp_part.alloc((size_t)2 * ((2 * Bm + 15) / 16) + 2);   // heads: per-workgroup logp sums
   hipStream_t s = c->stream;
   // constant-1 (bias) columns
   launch_set_column(c->xq.p, Bm, c->Kx, S, 1.f, s);
@@ -344,6 +349,18 @@ static void validate(const GemmDesc& d) {
   if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C");
   if (d.bias) check_span(d.bias, (int64_t)(d.N - 1) * d.bias_ld, "bias");
   REQUIRE(!(d.bias && d.epi == EPI_MASK), SACMI_ESTATE, "GEMM epilogue: bias and mask are exclusive");
+  if (d.axk) {
+    REQUIRE(d.a_kc && !d.b_kc && d.ax_w, SACMI_ESTATE, "A transform needs a K-contiguous A and w");
+    check_span(d.ax_w, d.K - 1, "ax_w");
+    if (d.ax_out) {
+      REQUIRE(d.K % 4 == 0 && d.ax_ld % 4 == 0, SACMI_ESTATE, "ax_out rows must be float4-aligned");
+      check_span(d.ax_out, (int64_t)(d.M - 1) * d.ax_ld + d.K - 1, "ax_out");
+    }
+  }
+  if (d.dotp) {
+    check_span(d.dotw, d.N - 1, "dotw");
+    check_span(d.dotp, (int64_t)(d.M - 1) * d.dotp_ld + (d.N - 1) / 32, "dotp");
+  }
   if (d.epi == EPI_MASK) check_span(d.aux, (int64_t)(d.M - 1) * d.ldaux + d.N - 1, "aux");
 }
 
@@ -473,8 +490,14 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   float* P = c->P.p;
   float* G = c->G.p;
   const float* T = c->T.p;
-  const int nb = (B + 3) / 4;
+  const int nb = (B + 31) / 32;     // loss partials: one per 32-row block of L5 / L9
   auto W = [&](const Linear& l) { return P + l.off; };
+  // fc3 dot partials: slot 0/1 q1/q2 (L2), 2/3 target q1/q2 (L4), 4/5 updated q1/q2 (L8)
+  auto dotp = [&](int slot) { return c->dotp.p + (size_t)slot * B * c->nparts; };
+  auto with_dot = [&](GemmDesc g, const float* w3, int slot) {
+    g.dotw = w3; g.dotp = dotp(slot); g.dotp_ld = c->nparts;
+    return g;
+  };
   auto Wt = [&](const Linear& l) { return T + (l.off - c->q_begin); };
   auto dW = [&](const Linear& l) { return G + l.off; };
   const Linear(&q)[2][3] = c->q_fc;
@@ -500,7 +523,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     Level l2;
     l2.add(gd_fwd_h(c->hp1.p, Hd, W(c->p_fc2), Hd, c->hp2.p, Hd, 2 * B, H, H));
     for (int i = 0; i < 2; ++i)
-      l2.add(gd_fwd_h(c->hq1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hq2.p + i * Hd, 2 * Hd, B, H, H));
+      l2.add(with_dot(gd_fwd_h(c->hq1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hq2.p + i * Hd, 2 * Hd, B, H, H),
+                      W(q[i][2]), i));
     if (mark(c, "gemm_L2_fc2", level_flops(l2.b), level_bytes(l2.b))) launch_gemm(l2.b, s);
     // heads + sample for both stacks
     HeadSampleArgs hs{};
@@ -510,30 +534,38 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     hs.cache = c->cache.p;
     hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
-    if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * (H + 1))) launch_heads_sample(hs, s);
+    hs.logp_part = c->lp_part.p; hs.split_row = B;    // sums of log pi(a~|s) for dL/dlog_alpha
+    if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) launch_heads_sample(hs, s);
     // L3/L4: target critics on [s2|1|a']
     Level l3, l4;
     for (int i = 0; i < 2; ++i)
       l3.add(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
     if (mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b), level_bytes(l3.b))) launch_gemm(l3.b, s);
     for (int i = 0; i < 2; ++i)
-      l4.add(gd_fwd_h(c->hqt1.p + i * Hd, 2 * Hd, Wt(q[i][1]), Hd, c->hqt2.p + i * Hd, 2 * Hd, B, H, H));
+      l4.add(with_dot(gd_fwd_h(c->hqt1.p + i * Hd, 2 * Hd, Wt(q[i][1]), Hd, c->hqt2.p + i * Hd, 2 * Hd, B, H, H),
+                      Wt(q[i][2]), 2 + i));
     if (mark(c, "gemm_L4_tgt_fc2", level_flops(l4.b), level_bytes(l4.b))) launch_gemm(l4.b, s);
-    // target / critic loss rows
-    CriticRowsArgs cr{};
-    cr.hq2 = c->hq2.p; cr.hqt2 = c->hqt2.p; cr.ldh = Hd; cr.H = H; cr.B = B;
-    cr.w3 = W(q[0][2]); cr.w3t = Wt(q[0][2]); cr.w3_stride = (int)(q[1][2].off - q[0][2].off);
-    cr.r = bb.r; cr.d = bb.d; cr.logp_t = c->logp.p; cr.logp_a = c->logp.p + B;
-    cr.gamma = (float)c->cfg.gamma; cr.target_entropy = (float)(-A);
-    cr.auto_entropy = c->cfg.auto_entropy; cr.sc = c->sc.p; cr.dq = c->dq.p; cr.dh2 = c->dh2.p;
-    cr.loss_part = c->lpart_c.p; cr.alpha_grad = G + c->la_idx;
-    if (mark(c, "critic_rows")) launch_critic_rows(cr, s);
-    // L5: dh1 = (dh2 W2) * relu'(h1)   [+ dW2~, dW3~ when Adam is not fused]
+    // L5: dh1 = (dh2 W2) * relu'(h1), with the target / critic-loss rows folded in: the
+    // row prologue finishes q1, q2, qt1, qt2 from the dot partials of L2 / L4 and gives
+    // dq_i = 2 (q_i - q^) / B; the A operand dh2 = dq * w3 * [h2 > 0] is formed from h2 on
+    // the fly (and stored once by the column-tile-0 workgroups for L6's dW2)
     const bool fuse = phase_mask == 7;     // single-GPU update: Adam in the dW epilogues
     Level l5;
-    for (int i = 0; i < 2; ++i)
-      l5.add(gd(c->dh2.p + i * H, 2 * H, 1, W(q[i][1]), Hd, 0, c->dh1.p + i * H, 2 * H, B, H, H,
-                EPI_MASK, c->hq1.p + i * Hd, 2 * Hd));
+    for (int i = 0; i < 2; ++i) {
+      GemmDesc g = gd(c->hq2.p + i * Hd, 2 * Hd, 1, W(q[i][1]), Hd, 0, c->dh1.p + i * H, 2 * H, B, H, H,
+                      EPI_MASK, c->hq1.p + i * Hd, 2 * Hd);
+      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][2]); g.ax_out = c->dh2.p + i * H; g.ax_ld = 2 * H;
+      l5.add(g);
+    }
+    {
+      RowsFuse& rf = l5.b.rows;
+      rf.kind = 1; rf.part = dotp(0); rf.nparts = c->nparts; rf.B = B;
+      rf.b3[0] = W(q[0][2]) + H; rf.b3[1] = W(q[1][2]) + H;
+      rf.b3[2] = Wt(q[0][2]) + H; rf.b3[3] = Wt(q[1][2]) + H;
+      rf.r = bb.r; rf.d = bb.d; rf.logp = c->logp.p; rf.logp_a = c->logp.p + B;
+      rf.gamma = (float)c->cfg.gamma;
+      rf.sc = c->sc.p; rf.dq = c->dq.p; rf.loss_part = c->lpart_c.p;
+    }
     // weight gradients of the critics: into the gradient arena, or (fused) straight into
     // Adam + Polyak on the parameters.  W2 is read by dh1 above, so every critic dW goes
     // to L6 — in both modes, so the reduction order (and the bits) are the same.
@@ -597,18 +629,29 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l7.add(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, c->hqa1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
     if (mark(c, "gemm_L7_act_fc1", level_flops(l7.b), level_bytes(l7.b))) launch_gemm(l7.b, s);
     for (int i = 0; i < 2; ++i)
-      l8.add(gd_fwd_h(c->hqa1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hqa2.p + i * Hd, 2 * Hd, B, H, H));
+      l8.add(with_dot(gd_fwd_h(c->hqa1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hqa2.p + i * Hd, 2 * Hd, B, H, H),
+                      W(q[i][2]), 4 + i));
     if (mark(c, "gemm_L8_act_fc2", level_flops(l8.b), level_bytes(l8.b))) launch_gemm(l8.b, s);
-    ActorRowsArgs ar{};
-    ar.hqa2 = c->hqa2.p; ar.ldh = Hd; ar.H = H; ar.B = B; ar.w3 = W(q[0][2]);
-    ar.w3_stride = (int)(q[1][2].off - q[0][2].off); ar.logp_a = c->logp.p + B; ar.sc = c->sc.p;
-    ar.dha2 = c->dha2.p; ar.loss_part = c->lpart_a.p;
-    if (mark(c, "actor_rows")) launch_actor_rows(ar, s);
-    // L9: dha1
+    // L9: dha1 = (dha2 W2) * relu'(ha1), with the actor rows folded in: the prologue
+    // finishes qa1, qa2 (L8's dot partials), min (ties 1/2 : 1/2), policy-loss partials,
+    // step counters; dha2 = dqa * w3 * [ha2 > 0] is formed from ha2 on the fly
     Level l9;
-    for (int i = 0; i < 2; ++i)
-      l9.add(gd(c->dha2.p + i * H, 2 * H, 1, W(q[i][1]), Hd, 0, c->dha1.p + i * H, 2 * H, B, H, H,
-                EPI_MASK, c->hqa1.p + i * Hd, 2 * Hd));
+    for (int i = 0; i < 2; ++i) {
+      GemmDesc g = gd(c->hqa2.p + i * Hd, 2 * Hd, 1, W(q[i][1]), Hd, 0, c->dha1.p + i * H, 2 * H, B, H, H,
+                      EPI_MASK, c->hqa1.p + i * Hd, 2 * Hd);
+      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][2]);
+      l9.add(g);
+    }
+    {
+      RowsFuse& rf = l9.b.rows;
+      rf.kind = 2; rf.part = dotp(4); rf.nparts = c->nparts; rf.B = B;
+      rf.b3[0] = W(q[0][2]) + H; rf.b3[1] = W(q[1][2]) + H;
+      rf.logp = c->logp.p + B; rf.sc = c->sc.p; rf.loss_part = c->lpart_a.p;
+      if (c->cfg.auto_entropy) {
+        rf.alpha_grad = G + c->la_idx; rf.logp_part = c->lp_part.p; rf.n_lp = (2 * B + 15) / 16;
+        rf.target_entropy = (float)(-A);
+      }
+    }
     if (mark(c, "gemm_L9_act_dh1", level_flops(l9.b), level_bytes(l9.b))) launch_gemm(l9.b, s);
     // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
     GemmDesc da = gd(c->dha1.p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
@@ -824,8 +867,8 @@ int sacmi_destroy(sacmi_ctx* c) {
                     &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->xqb, &c->x2b, &c->rb,
                     &c->db, &c->hp1, &c->hp2, &c->eps,
                     &c->cache, &c->logp, &c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1,
-                    &c->hqa2, &c->dq, &c->dh2, &c->dh1, &c->dha2, &c->dha1, &c->dhead, &c->dhp2,
-                    &c->dhp1, &c->lpart_c, &c->lpart_a, &c->ring, &c->ax, &c->ah1, &c->ah2,
+                    &c->hqa2, &c->dq, &c->dh2, &c->dh1, &c->dotp, &c->dha1, &c->dhead, &c->dhp2,
+                    &c->dhp1, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
                     &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr, &c->per_probs,
                     &c->per_chunk, &c->per_w, &c->per_val})
       b->release();

@@ -78,6 +78,21 @@ struct GemmDesc {
   int tiles_n, tile_begin;
   int tiles_m;         // row blocks
   int xcd_gr;          // >0: XCD-blocked tile order, gr x (8/gr) XCD grid (launch_gemm)
+  // fc3 dot partials (forward ReLU levels feeding a scalar head): for every row and
+  // every 32-column block of this GEMM's output, sum_n relu(y[row][n]) * dotw[n] is
+  // written to dotp[row * dotp_ld + n / 32]
+  const float* dotw;
+  float* dotp;
+  int dotp_ld;
+  // A-operand transform (the critic / actor fc3 backward folded into the next GEMM):
+  //   axk 1 (A K-contiguous, rows = batch): a(b,k) = A(b,k) > 0 ? coef[b] * ax_w[k] : 0,
+  //         coef from this workgroup's row prologue (GemmBatch.rows, slot ax_slot);
+  //         the column-tile-0 workgroups also store the transformed rows to ax_out
+  //         (row stride ax_ld) when it is set — the dh2 a later level needs
+  int axk, ax_slot;
+  const float* ax_w;
+  float* ax_out;
+  int ax_ld;
   int adam_step;       // EPI_ADAM*: optimizer step counter index (0 pi, 1 q1, 2 q2)
   const float* bias;   // forward epilogue: C += bias[n * bias_ld] (before the ReLU)
   int bias_ld;
@@ -138,6 +153,29 @@ struct RideAlong {
   GatherArgs ga;
 };
 
+// Row prologue of a level whose A operand is transformed with axk 1: per batch row,
+// the fc3 heads are finished from the dot partials of the previous levels and turned
+// into the coefficients of the backward (sac_imp.py:87-113 critic / 116-121 actor).
+struct RowsFuse {
+  int kind;                  // 0 none, 1 critic (target + MSE), 2 actor (min Q)
+  const float* part;         // [nslot][B][nparts] dot partials (critic: q1 q2 qt1 qt2; actor: qa1 qa2)
+  int nparts, B;
+  const float* b3[4];        // fc3 bias of each slot (device parameters)
+  const float* r; const float* d;
+  const float* logp;         // critic: log pi(a'|s2);  actor: log pi(a~|s)
+  const float* logp_a;       // critic: log pi(a~|s) for the alpha gradient
+  float gamma, target_entropy;
+  int auto_entropy;
+  DevScalars* sc;
+  float* dq;                 // [2][B] out: the per-row head gradients (read by later levels)
+  float* loss_part;          // critic [row blocks][2] squared errors; actor [row blocks]
+  // actor: dL/dlog_alpha = -mean(logp_a + te) (sac_imp.py:128-133) from the heads
+  // kernel's per-workgroup logp sums (slot 1 of each of n_lp workgroups)
+  float* alpha_grad;
+  const float* logp_part;
+  int n_lp;
+};
+
 constexpr int kMaxGemms = 8;
 struct GemmBatch {
   GemmDesc d[kMaxGemms];
@@ -146,6 +184,7 @@ struct GemmBatch {
   AdamFuse adam;       // used when any desc has epi >= EPI_ADAM
   int has_adam;
   RideAlong ride;      // extra workgroups after the tiles
+  RowsFuse rows;       // prologue for axk-1 descs
 };
 
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked
@@ -165,6 +204,8 @@ struct HeadSampleArgs {
   float scale, bias;
   int deterministic;     // 1: action = tanh(mean)*scale+bias (select_action(evaluate=True))
   uint64_t ctr_override; // nonzero: Philox counter to use instead of sc->noise_counter
+  float* logp_part;      // [grid][2] or null: per workgroup, sum of logp over its rows
+  int split_row;         //   < split_row (slot 0) and >= split_row (slot 1)
 };
 
 // Sample-backward epilogue of the dL/da GEMM.
@@ -183,39 +224,6 @@ void launch_gemm(const GemmBatch& batch, hipStream_t s);
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s);
 
-struct CriticRowsArgs {
-  const float* hq2;   // [B, 2*ldh] critic hidden-2 (q1 | q2)
-  const float* hqt2;  // [B, 2*ldh] target hidden-2
-  int ldh, H, B;
-  const float* w3;    // q1.fc3 row (ld = ld3); q2.fc3 at + w3_stride
-  const float* w3t;   // target fc3
-  int w3_stride;
-  const float* r;     // [B]
-  const float* d;     // [B]
-  const float* logp_t;  // [B] next-state log-probs
-  const float* logp_a;  // [B] actor log-probs (for the alpha gradient)
-  float gamma;
-  float target_entropy;
-  int auto_entropy;
-  DevScalars* sc;
-  float* dq;          // [2, B]
-  float* dh2;         // [B, 2H]
-  float* loss_part;   // [nblocks, 2]
-  float* alpha_grad;  // gradient slot of log_alpha
-};
-void launch_critic_rows(const CriticRowsArgs& a, hipStream_t s);
-
-struct ActorRowsArgs {
-  const float* hqa2;  // [B, 2*ldh]
-  int ldh, H, B;
-  const float* w3;
-  int w3_stride;
-  const float* logp_a;
-  DevScalars* sc;
-  float* dha2;        // [B, 2H]
-  float* loss_part;   // [nblocks]
-};
-void launch_actor_rows(const ActorRowsArgs& a, hipStream_t s);
 
 constexpr int kMaxAdamSegs = 8;
 struct AdamSeg { int64_t off, n; int step_idx; };

@@ -37,14 +37,14 @@ static GemmDesc mk(const float* A, int lda, int akc, const float* B, int ldb, in
   return d;
 }
 
-template <int TM, int TN, int KS, int G, int MG, bool AD>
+template <int TM, int TN, int KS, int G, int MG, bool AD, int AX = 0>
 static float time_cfg(GemmBatch b, int iters, hipStream_t s) {
   assign_tiles<TM * MG, TN>(b);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
+  for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD, AX>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
   CK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD, AX>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
   CK(hipEventRecord(e1, s));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -55,15 +55,15 @@ static float time_cfg(GemmBatch b, int iters, hipStream_t s) {
 
 #ifdef SACMI_DIAG_STAMPS
 // one launch after warm-up; per-phase breakdown from the in-kernel stamps (µs)
-template <int TM, int TN, int KS, int G, int MG, bool AD>
+template <int TM, int TN, int KS, int G, int MG, bool AD, int AX = 0>
 static void stamp_cfg(GemmBatch b, hipStream_t s) {
   assign_tiles<TM * MG, TN>(b);
-  for (int i = 0; i < 30; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
+  for (int i = 0; i < 30; ++i) hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD, AX>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
   CK(hipStreamSynchronize(s));
   static unsigned long long h[4096][40];
   memset(h, 0, sizeof(h));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), h, sizeof(h)));
-  hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
+  hipLaunchKernelGGL((k_gemm<TM, TN, KS, G, MG, AD, AX>), dim3(b.total_tiles), dim3(64 * KS * MG), 0, s, b);
   CK(hipStreamSynchronize(s));
   CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamps), sizeof(h)));
   const int nb = std::min(b.total_tiles, 4096);
@@ -106,6 +106,19 @@ static void stamp_cfg(GemmBatch b, hipStream_t s) {
   for (double x : start) early += x < 1.0;
   printf("      CUs used %zu, max WGs co-resident on one CU %d, WGs started < 1us: %d of %d\n", per_cu.size(), maxov, early, nb);
   auto q = [](std::vector<double> v, double f) { std::sort(v.begin(), v.end()); return v[(size_t)(f * (v.size() - 1))]; };
+  {
+    std::vector<double> p1, p2;
+    for (int i = 0; i < nb; ++i) {
+      if (!live(i) || !h[i][35]) continue;
+      p1.push_back((h[i][36] - h[i][0]) * 0.01);
+      p2.push_back((h[i][35] - h[i][0]) * 0.01);
+    }
+    if (!p1.empty()) {
+      std::sort(p1.begin(), p1.end()); std::sort(p2.begin(), p2.end());
+      printf("      prologue (from wave-0 entry): first barrier med %.2f max %.2f | done med %.2f max %.2f\n",
+             p1[p1.size() / 2], p1.back(), p2[p2.size() / 2], p2.back());
+    }
+  }
   printf("      span %.2f | start med %.2f max %.2f | core(max wave) med %.2f max %.2f | core(min wave) med %.2f | "
          "lds+sync med %.2f | epilogue med %.2f max %.2f | end med %.2f\n",
          (tend - t0) * 0.01, q(start, .5), q(start, 1), q(core_max, .5), q(core_max, 1), q(core_min, .5),
@@ -253,6 +266,25 @@ int main(int argc, char** argv) {
       b.d[b.count++] = mk(dh2 + i * H, 2 * H, 1, P + i * qn + q1n, Hd, 0, dh1 + i * H, 2 * H, B, H, H, EPI_MASK);
     b.d[0].aux = hq1; b.d[0].ldaux = 2 * Hd; b.d[1].aux = hq1 + Hd; b.d[1].ldaux = 2 * Hd;
     return b; }});
+  // L5 with the critic rows folded in (row prologue from dot partials + A transform)
+  float* part = dalloc((size_t)4 * B * 16, 0.1f);
+  float* rvec = dalloc(B), *dvec = dalloc(B, 0.f), *lpv = dalloc(2 * B), *dqv = dalloc(2 * B);
+  float* lpart = dalloc(64);
+  float* dh2o = dalloc((size_t)B * 2 * H);
+  levels.push_back({"L5 fused rows (K=512)", [&](bool) {
+    GemmBatch b{};
+    for (int i = 0; i < 2; ++i) {
+      GemmDesc g = mk(hq2 + i * Hd, 2 * Hd, 1, P + i * qn + q1n, Hd, 0, dh1 + i * H, 2 * H, B, H, H, EPI_MASK);
+      g.aux = hq1 + i * Hd; g.ldaux = 2 * Hd;
+      g.axk = 1; g.ax_slot = i; g.ax_w = P + i * qn + q1n + q2n; g.ax_out = dh2o + i * H; g.ax_ld = 2 * H;
+      b.d[b.count++] = g;
+    }
+    RowsFuse& rf = b.rows;
+    rf.kind = 1; rf.part = part; rf.nparts = 16; rf.B = B;
+    for (int i = 0; i < 4; ++i) rf.b3[i] = P + q1n + q2n + H;
+    rf.r = rvec; rf.d = dvec; rf.logp = lpv; rf.gamma = 0.99f; rf.sc = sc; rf.dq = dqv;
+    rf.loss_part = lpart;
+    return b; }});
   (void)scratch; (void)dhp2;
 
   const int iters = 300;
@@ -262,6 +294,13 @@ int main(int argc, char** argv) {
       GemmBatch b = L.make(fused);
       int t32 = assign_tiles<32, 32>(b), t64 = assign_tiles<32, 64>(b), t6464 = assign_tiles<64, 64>(b);
       printf("%-40s %-6s tiles32x32=%d 32x64=%d 64x64=%d\n", L.name.c_str(), fused ? "adam" : "store", t32, t64, t6464);
+      if (L.name.rfind("L5 fused", 0) == 0) {
+#ifdef SACMI_DIAG_STAMPS
+        if (stamps) { printf("   <32,32,16,2,axk1>\n"); stamp_cfg<32, 32, 16, 2, 1, false, 1>(b, s); continue; }
+#endif
+        printf("   <32,32,16,2,axk1> %7.2f us\n", time_cfg<32, 32, 16, 2, 1, false, 1>(b, iters, s));
+        continue;
+      }
 #ifdef SACMI_DIAG_STAMPS
       if (stamps) {
         if (fused) {
@@ -288,7 +327,7 @@ int main(int argc, char** argv) {
       printf("   <64,64,4,4>  %7.2f us\n", time_cfg<64, 64, 4, 4, 1, false>(b, iters, s));
       printf("   <32,64,16,2> %7.2f us\n", time_cfg<32, 64, 16, 2, 1, false>(b, iters, s));
       printf("   <32,32,16,4> %7.2f us\n", time_cfg<32, 32, 16, 4, 1, false>(b, iters, s));
-      printf("   <32,32,8,2>  %7.2f us\n", time_cfg<32, 32, 8, 2, 1, false>(b, iters, s));
+      printf("   <32,32,16,2> %7.2f us\n", time_cfg<32, 32, 16, 2, 1, false>(b, iters, s));
       fflush(stdout);
     }
   }
