@@ -803,9 +803,12 @@ void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {
 //   dmean = G*(1-y^2);  dlog_std = [-20<=ls<=2] * (G*(1-y^2)*eps*std - alpha/B)
 // (the Normal.log_prob quadratic term's gradients w.r.t. mean and std cancel
 // exactly: x - mean = eps*std).
-template <int TM, int TN, int KSPLIT>
+// NST: k-steps (of 4) of the dhp2 tail's K = 2A, a compile-time bound
+template <int TM, int TN, int KSPLIT, int NST>
 __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, SampleBwdArgs a) {
   __shared__ float red[KSPLIT * TM * (TN + 1)];
+  __shared__ float s_dh[TM][64 + 1];     // this workgroup's dhead rows, zero beyond 2A
+  for (int i = threadIdx.x; i < TM * 65; i += 64 * KSPLIT) (&s_dh[0][0])[i] = 0.f;
   const int m0 = blockIdx.x * TM;
   static_assert(TM * TN <= 64 * KSPLIT, "one (row, action) element per thread");
   // element e = threadIdx.x -> (row, action j); the sample cache and noise are loaded
@@ -815,6 +818,33 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
   const int row = e / A, j = e % A, m = m0 + row;
   const bool live = e < TM * A && m < d.M;
   float ls_raw = 0.f, y = 0.f, eps = 0.f;
+  // the dhp2 tail's operands for this wave's first 32-column slab: Whead fragments and
+  // the ReLU-mask source, also loaded under the dL/da MFMAs
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K2 = 2 * A, ksteps = (K2 + 3) / 4;
+  float bw[2][NST], mk[2][4];
+  auto load_mask = [&](int n0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + t * 16 + (lane & 15);
+      const float* hp = a.hp2 + (size_t)(m0 + (lane >> 4) * 4) * a.ldh + (n < a.H ? n : 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        mk[t][r] = (m0 + (lane >> 4) * 4 + r < d.M && n < a.H) ? hp[(size_t)r * a.ldh] : 0.f;
+    }
+  };
+  auto load_w = [&](int n0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = n0 + t * 16 + (lane & 15);
+      const float* wp = a.Wh + (size_t)(lane >> 4) * a.ldw + (n < a.H ? n : 0);
+#pragma unroll
+      for (int st = 0; st < NST; ++st) {
+        const int k = 4 * st + (lane >> 4);
+        bw[t][st] = (st < ksteps && k < K2 && n < a.H) ? wp[(size_t)4 * st * a.ldw] : 0.f;
+      }
+    }
+  };
   auto pre = [&]() {
     if (live) {
       const float* cr = a.cache + (size_t)m * 3 * A;
@@ -822,8 +852,9 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
       y = cr[2 * A + j];
       eps = a.eps[(size_t)m * A + j];
     }
+    load_mask(wave * 32);
   };
-  gemm_core_l<TM, TN, KSPLIT, 4, true, false, false>(d, m0, 0, red, nullptr, pre);
+  gemm_core_l<TM, TN, KSPLIT, 2, true, false, false>(d, m0, 0, red, nullptr, pre);
   __syncthreads();
   const float glogp = a.sc->alpha / (float)a.B;
   if (live) {
@@ -838,12 +869,42 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
     if (!(ls_raw >= -20.f && ls_raw <= 2.f)) dls = 0.f;
     a.dhead[(size_t)m * a.lddh + j] = dx;
     a.dhead[(size_t)m * a.lddh + A + j] = dls;
+    s_dh[row][j] = dx;
+    s_dh[row][A + j] = dls;
+  }
+  __syncthreads();
+  // dhp2[TM rows, H] = (s_dh[TM, 2A] Whead[2A, H]) * [hp2 > 0]: 16x16x4 MFMAs, A from LDS,
+  // each wave a 32-column slab per pass (networks_model1.py:72-76 backward)
+  for (int n0 = wave * 32; n0 < a.H; n0 += KSPLIT * 32) {
+    f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+    if (n0 != wave * 32) load_mask(n0);   // H > 512: later slabs load their mask here
+    load_w(n0);
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      if (st < ksteps) {
+        const float av = s_dh[lane & 15][4 * st + (lane >> 4)];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bw[t][st], acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, n = n0 + t * 16 + (lane & 15);
+        if (m0 + rr < d.M && n < a.H)
+          a.dhp2[(size_t)(m0 + rr) * a.H + n] = mk[t][r] > 0.f ? acc[t][r] : 0.f;
+      }
   }
 }
 
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s) {
   const int grid = (d.M + 15) / 16;
-  hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16>), dim3(grid), dim3(1024), 0, s, d, a);
+  if ((2 * a.A + 3) / 4 <= 10)
+    hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 10>), dim3(grid), dim3(1024), 0, s, d, a);
+  else
+    hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 16>), dim3(grid), dim3(1024), 0, s, d, a);
   HIP_LAUNCH_CHECK();
 }
 

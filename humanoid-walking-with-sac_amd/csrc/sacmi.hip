@@ -656,19 +656,23 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
     GemmDesc da = gd(c->dha1.p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
     validate(da);
+    // ... and, for the same rows, dhp2 = (dhead Whead) * relu'(hp2) (policy heads backward)
+    const float* hp2a = c->hp2.p + (size_t)B * Hd;
+    const float* hp1a = c->hp1.p + (size_t)B * Hd;
     SampleBwdArgs sb{};
     sb.cache = c->cache.p + (size_t)B * 3 * A; sb.eps = c->eps.p + (size_t)B * A;
     sb.dhead = c->dhead.p; sb.lddh = c->lddh; sb.A = A; sb.B = B; sb.sc = c->sc.p;
     sb.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
-    if (mark(c, "gemm_L10_dlda_sample_bwd", 2.0 * B * A * (2.0 * H))) launch_gemm_sample_bwd(da, sb, s);
-    // L11: dhp2 = (dhead Whead) * relu'(hp2);  L12: dhp1 = (dhp2 W2pi) * relu'(hp1);
+    sb.Wh = W(c->p_head); sb.ldw = Hd; sb.H = H; sb.hp2 = hp2a; sb.ldh = Hd; sb.dhp2 = c->dhp2.p;
+    check_span(sb.dhp2, (int64_t)B * H - 1, "dhp2");
+    check_span(sb.Wh, (int64_t)(2 * A - 1) * Hd + H - 1, "Whead");
+    if (mark(c, "gemm_L10_dlda_sample_bwd_dhp2", 2.0 * B * A * (2.0 * H) + 2.0 * B * (2.0 * A) * H))
+      launch_gemm_sample_bwd(da, sb, s);
+    // L12: dhp1 = (dhp2 W2pi) * relu'(hp1);
     // L13: every policy dW (+ Adam, alpha step, policy loss, loss ring when fused)
-    const float* hp2a = c->hp2.p + (size_t)B * Hd;
-    const float* hp1a = c->hp1.p + (size_t)B * Hd;
     auto pdst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
     const int pepi = fuse ? EPI_ADAM : EPI_STORE;
-    Level l11, l12, l13;
-    l11.add(gd(c->dhead.p, c->lddh, 1, W(c->p_head), Hd, 0, c->dhp2.p, H, B, H, 2 * A, EPI_MASK, hp2a, Hd));
+    Level l12, l13;
     GemmDesc dwh = gd_dw_h(c->dhead.p, c->lddh, hp2a, Hd, pdst(c->p_head), Hd, 2 * A, H, B, pepi, 0);
     l12.add(gd(c->dhp2.p, H, 1, W(c->p_fc2), Hd, 0, c->dhp1.p, H, B, H, H, EPI_MASK, hp1a, Hd));
     GemmDesc dw2 = gd_dw_h(c->dhp2.p, H, hp1a, Hd, pdst(c->p_fc2), Hd, H, H, B, pepi, 0);
@@ -688,16 +692,15 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
     }
     if (ride_next) {
-      // the next update's random.sample rides in L11 (128 tiles: idle CUs)
+      // the next update's random.sample rides in L12 (128 tiles: idle CUs)
       const BatchBufs nb2 = batch_bufs(c, parity ^ 1);
-      l11.b.ride.kind = 1; l11.b.ride.nblocks = 1;
-      l11.b.ride.tbl_log2 = mt_sample_tbl_log2(B);
-      l11.b.ride.mt = mt_args(c, B, nb2);
+      l12.b.ride.kind = 1; l12.b.ride.nblocks = 1;
+      l12.b.ride.tbl_log2 = mt_sample_tbl_log2(B);
+      l12.b.ride.mt = mt_args(c, B, nb2);
       // ... and its gather in L13
       l13.b.ride.kind = 2; l13.b.ride.nblocks = 16;
       l13.b.ride.ga = gather_args(c, B, nb2, false);
     }
-    if (mark(c, "gemm_L11_pi_dhp2", level_flops(l11.b), level_bytes(l11.b))) launch_gemm(l11.b, s);
     if (mark(c, "gemm_L12_pi_dhp1", level_flops(l12.b), level_bytes(l12.b))) launch_gemm(l12.b, s);
     if (mark(c, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1", level_flops(l13.b), level_bytes(l13.b))) launch_gemm(l13.b, s);
   }

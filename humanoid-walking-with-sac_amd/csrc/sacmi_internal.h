@@ -216,6 +216,12 @@ struct SampleBwdArgs {
   int lddh, A, B;
   const DevScalars* sc;
   float scale;
+  // dhp2 = (dhead Whead) * [hp2 > 0] for the same rows (the policy heads' backward)
+  const float* Wh;       // [2A, ldw] head weights
+  int ldw, H;
+  const float* hp2;      // actor rows' hidden-2 [B, ldh] (ReLU mask source)
+  int ldh;
+  float* dhp2;           // [B, H]
 };
 
 // ---------------------------------------------------------------------------
