@@ -724,15 +724,29 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   }
 }
 
+// Explicit batch-set control for a phase-split update (the data-parallel driver's
+// captured sequences): parity = this update's minibatch buffer set, have_batch = its
+// indices/rows were produced by the previous update's rides, ride_next = produce the
+// next update's (in the phase-1 launches).
+struct PhaseRide {
+  int parity = 0;
+  bool have_batch = false, ride_next = false;
+};
+
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
-                       float grad_scale, bool use_ring, int reps = 1) {
+                       float grad_scale, bool use_ring, int reps = 1, PhaseRide pr = {}) {
   // consecutive fused updates hand the next update's sampling + gather to ride-along
   // workgroups of the current one
   const bool ride = reps > 1 && phase_mask == 7 && dev_idx && ride_possible(c, B);
   auto enqueue_all = [&]() {
     if (phase_mask == 5) {   // phase 2 of the previous update, then phase 0 of the next
-      enqueue_update(c, B, dev_idx, dev_eps, 4, grad_scale, use_ring);
-      enqueue_update(c, B, dev_idx, dev_eps, 1, grad_scale, use_ring);
+      enqueue_update(c, B, dev_idx, dev_eps, 4, grad_scale, use_ring, pr.parity ^ 1);
+      enqueue_update(c, B, dev_idx, dev_eps, 1, grad_scale, use_ring, pr.parity, pr.have_batch);
+      return;
+    }
+    if (phase_mask != 7) {   // one phase of a split update
+      enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring, pr.parity,
+                     pr.have_batch, pr.ride_next);
       return;
     }
     for (int r = 0; r < reps; ++r)
@@ -749,7 +763,9 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
     return;
   }
   GraphKey key{B, dev_idx, dev_eps,
-               phase_mask | (grad_scale != 1.f ? 8 : 0) | (c->keep_grads ? 16 : 0), use_ring ? c->ring_slots : 0,
+               phase_mask | (grad_scale != 1.f ? 8 : 0) | (c->keep_grads ? 16 : 0) |
+                   (pr.parity ? 32 : 0) | (pr.have_batch ? 64 : 0) | (pr.ride_next ? 128 : 0),
+               use_ring ? c->ring_slots : 0,
                c->cfg.replay_kind == SACMI_REPLAY_PER ? c->len : 0, reps};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
@@ -1182,6 +1198,26 @@ int sacmi_step_phase(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scal
     if (phase == 0 || phase == 3) check_batch(c, batch);
     run_update(c, batch, 1, 1, phase == 3 ? 5 : 1 << phase, grad_scale, false);
   });
+}
+
+int sacmi_step_phase_ex(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scale,
+                        int32_t parity, int32_t have_batch, int32_t ride_next) {
+  return guard([&] {
+    REQUIRE(phase >= 0 && phase <= 3, SACMI_EVALUE, "phase must be 0, 1, 2 or 3");
+    REQUIRE(parity == 0 || parity == 1, SACMI_EVALUE, "parity must be 0 or 1");
+    if (phase == 0 || phase == 3) check_batch(c, batch);
+    PhaseRide pr;
+    pr.parity = parity;
+    pr.have_batch = have_batch && (phase == 0 || phase == 3);
+    pr.ride_next = ride_next && phase == 1 && ride_possible(c, batch);
+    REQUIRE(!pr.have_batch || ride_possible(c, batch), SACMI_EVALUE,
+            "have_batch needs uniform replay with a ride-capable batch size");
+    run_update(c, batch, 1, 1, phase == 3 ? 5 : 1 << phase, grad_scale, false, 1, pr);
+  });
+}
+
+int sacmi_step_ride_possible(sacmi_ctx* c, int32_t batch, int32_t* out) {
+  return guard([&] { *out = ride_possible(c, batch) ? 1 : 0; });
 }
 
 int sacmi_grad_arena_numel(sacmi_ctx* c, int64_t* numel) {

@@ -216,8 +216,18 @@ class Context:
         L.call("sacmi_fetch_losses", self._h, L.fptr(out), int(max_steps), ctypes.byref(n))
         return out[:n.value]
 
-    def step_phase(self, batch: int, phase: int, grad_scale: float = 1.0) -> None:
-        L.call("sacmi_step_phase", self._h, int(batch), int(phase), float(grad_scale))
+    def step_phase(self, batch: int, phase: int, grad_scale: float = 1.0, parity: int = 0,
+                   have_batch: bool = False, ride_next: bool = False) -> None:
+        if parity or have_batch or ride_next:
+            L.call("sacmi_step_phase_ex", self._h, int(batch), int(phase), float(grad_scale),
+                   int(parity), int(bool(have_batch)), int(bool(ride_next)))
+        else:
+            L.call("sacmi_step_phase", self._h, int(batch), int(phase), float(grad_scale))
+
+    def ride_possible(self, batch: int) -> bool:
+        out = ctypes.c_int32()
+        L.call("sacmi_step_ride_possible", self._h, int(batch), ctypes.byref(out))
+        return bool(out.value)
 
     def grad_arena_numel(self) -> int:
         n = ctypes.c_int64()

@@ -51,8 +51,12 @@ class GpuBackend:
 
     supports_fused_tail = True     # library phase 3 = phase 2 + next phase 0
 
-    def phase(self, p: int, batch: int, grad_scale: float) -> None:
-        self.ctx.step_phase(batch, p, grad_scale)
+    def phase(self, p: int, batch: int, grad_scale: float, parity: int = 0,
+              have_batch: bool = False, ride_next: bool = False) -> None:
+        self.ctx.step_phase(batch, p, grad_scale, parity, have_batch, ride_next)
+
+    def ride_possible(self, batch: int) -> bool:
+        return self.ctx.ride_possible(batch)
 
 
 class DataParallelUpdate:
@@ -64,17 +68,40 @@ class DataParallelUpdate:
         self.group = group
         self.world = dist.get_world_size(group)
         self._pending = None       # batch of an update whose phase 2 has not run
+        # ride-along sequence (begin_sequence): the next update's sampling + gather run
+        # inside this update's phase-1 launches, into the other minibatch buffer set
+        self._seq_left = 0
+        self._parity = 0
+        self._have = False
+
+    def begin_sequence(self, n: int, batch: int) -> None:
+        """The next `n` calls form one uninterrupted sequence (nothing touches the replay
+        buffer or the sampling stream in between, e.g. one captured graph): updates
+        1..n-1 get their minibatch from the previous update's ride-along work."""
+        ok = getattr(self.backend, "ride_possible", None)
+        self._seq_left = n if (ok is not None and ok(batch)) else 0
+        self._parity, self._have = 0, False
 
     def __call__(self, batch: int) -> None:
         b, scale = self.backend, 1.0 / self.world
+        ride_next = self._seq_left > 1
+        kw = {}
+        if self._seq_left > 0:
+            kw = dict(parity=self._parity, have_batch=self._have)
         if self._pending is not None and getattr(b, "supports_fused_tail", False):
-            b.phase(3, batch, scale)
+            b.phase(3, batch, scale, **kw)
         else:
             self.flush()
-            b.phase(0, batch, scale)
+            b.phase(0, batch, scale, **kw)
         self._pending = None
         dist.all_reduce(b.critic_grads, op=dist.ReduceOp.SUM, group=self.group)
-        b.phase(1, batch, scale)
+        if self._seq_left > 0:
+            b.phase(1, batch, scale, parity=self._parity, ride_next=ride_next)
+            self._seq_left -= 1
+            self._have = ride_next
+            self._parity = self._parity ^ 1 if ride_next else 0
+        else:
+            b.phase(1, batch, scale)
         dist.all_reduce(b.actor_grads, op=dist.ReduceOp.SUM, group=self.group)
         self._pending = batch
 
@@ -111,6 +138,7 @@ class CapturedDataParallelUpdates:
         if g is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=self.stream):
+                self.upd.begin_sequence(n, self.batch)
                 for _ in range(n):
                     self.upd(self.batch)
                 self.upd.flush()

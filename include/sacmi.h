@@ -174,6 +174,16 @@ int sacmi_fetch_losses(sacmi_ctx* ctx, float* out, int32_t max_steps, int32_t* n
  * sacmi_grad_buffer(which=0 critic, 1 actor); grad_scale (1/world) is applied by the
  * Adam kernels. */
 int sacmi_step_phase(sacmi_ctx* ctx, int32_t batch, int32_t phase, float grad_scale);
+/* The same with the minibatch buffer sets spelled out, for a fixed sequence of split
+ * updates (e.g. one captured into a graph by the caller): parity (0/1) = the buffer set
+ * of the update whose phase 0 (phase 3: the NEXT update) / phase 1 runs; have_batch =
+ * its indices and rows were produced by the previous update (phases 0, 3); ride_next =
+ * the phase-1 launches also sample and gather the next update into set parity^1
+ * (uniform replay only, sacmi_step_ride_possible).  The caller guarantees that nothing
+ * changes the replay buffer or the sampling stream between a ride and its use. */
+int sacmi_step_phase_ex(sacmi_ctx* ctx, int32_t batch, int32_t phase, float grad_scale,
+                        int32_t parity, int32_t have_batch, int32_t ride_next);
+int sacmi_step_ride_possible(sacmi_ctx* ctx, int32_t batch, int32_t* out);
 int sacmi_grad_buffer(sacmi_ctx* ctx, int which, void** device_ptr, int64_t* numel);
 /* Gradient arena size (floats) and adoption of a caller-allocated device buffer of
  * that size (e.g. a torch tensor), so collectives run on it in place.  Must be on the

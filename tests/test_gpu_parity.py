@@ -344,6 +344,8 @@ def test_dp_phase_path_matches_fused_step_world1():
         for _ in range(6):                 # the captured object's warm-up update + 5
             eager(64)
         eager.flush()
+        # uniform replay at B=64: the captured sequences use ride-along sampling/gather
+        assert cap[0].ride_possible(64)
         g = CapturedDataParallelUpdates(cap[0], torch.device("cuda", 0), 64)
         g.run(5, 2)
         torch.cuda.synchronize()
