@@ -57,21 +57,39 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 //   KC  (K-contiguous, element (row,k) at rp + k):     one 16-byte load
 //   !KC (row-contiguous, element (row,k) at rp + k*ld): 4 loads, each a coalesced
 //        64-byte segment across the 16 lanes of a lane group.
-template <int NT, bool KC>
+template <int NT, bool KC, int OP = 0>
 __device__ __forceinline__ void fetch_op(const float* const (&rp)[NT], int ld, int k, int K,
                                          float (&v)[NT][4]) {
+#ifdef SACMI_EXP_NOLOAD
+  // timing experiment only: no operand loads at all (MFMA + epilogue floor)
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) v[t][s] = (float)(k + s + t) * 1e-3f;
+  return;
+#endif
+#ifdef SACMI_EXP_BLOCKED
+  // timing experiment only (numerics meaningless): every fragment load lane-linear 16 B
+  if (SACMI_EXP_BLOCKED & (1 << OP))
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    float4 x = float4{0.f, 0.f, 0.f, 0.f};
+    if (k < K) x = *reinterpret_cast<const float4*>(rp[t] + (KC ? (size_t)(k >> 4) * 256 : (size_t)(k >> 4) * 16 * ld));
+    v[t][0] = x.x; v[t][1] = x.y; v[t][2] = x.z; v[t][3] = x.w;
+  }
+  if (SACMI_EXP_BLOCKED & (1 << OP)) return;
+#endif
+  // Branch-free: a load inside a divergent `if` is waited for inside it (the select that
+  // consumes it sits in the same block), which would serialise every operand load of the
+  // burst.  Out-of-range k reads a clamped in-bounds address and is zeroed by a select.
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (KC) {
-      if (k < K) {
-        const float4 x = *reinterpret_cast<const float4*>(rp[t] + k);
-        v[t][0] = x.x;
-        v[t][1] = (k + 1 < K) ? x.y : 0.f;
-        v[t][2] = (k + 2 < K) ? x.z : 0.f;
-        v[t][3] = (k + 3 < K) ? x.w : 0.f;
-      } else {
-        v[t][0] = v[t][1] = v[t][2] = v[t][3] = 0.f;
-      }
+      const float4 x = *reinterpret_cast<const float4*>(rp[t] + (k < K ? k : 0));
+      v[t][0] = (k < K) ? x.x : 0.f;
+      v[t][1] = (k + 1 < K) ? x.y : 0.f;
+      v[t][2] = (k + 2 < K) ? x.z : 0.f;
+      v[t][3] = (k + 3 < K) ? x.w : 0.f;
     } else {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -83,9 +101,19 @@ __device__ __forceinline__ void fetch_op(const float* const (&rp)[NT], int ld, i
   }
 }
 
-template <int NT, bool KC>
+template <int NT, bool KC, int OP = 0>
 __device__ __forceinline__ void row_ptrs(const float* P, int ld, int row0, int nrows, int lane,
                                          const float* (&rp)[NT]) {
+#ifdef SACMI_EXP_BLOCKED
+  if (SACMI_EXP_BLOCKED & (1 << OP))
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    int rb = (row0 >> 4) + t;
+    rb = rb < (nrows - 1) / 16 ? rb : (nrows - 1) / 16;
+    rp[t] = KC ? P + (size_t)rb * 16 * ld + lane * 4 : P + (size_t)rb * 256 + lane * 4;
+  }
+  if (SACMI_EXP_BLOCKED & (1 << OP)) return;
+#endif
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     int row = row0 + t * 16 + (lane & 15);
@@ -143,8 +171,8 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   for (int i = 0; i < MT; ++i) rs[i] = 0.f;
   const float* ra[MT];
   const float* rb[NT];
-  row_ptrs<MT, AKC>(d.A, d.lda, m0, d.M, lane, ra);
-  row_ptrs<NT, BKC>(d.B, d.ldb, n0, d.N, lane, rb);
+  row_ptrs<MT, AKC, 0>(d.A, d.lda, m0, d.M, lane, ra);
+  row_ptrs<NT, BKC, 1>(d.B, d.ldb, n0, d.N, lane, rb);
   const int nch = (d.K + 15) >> 4;
   const int nmine = nch > ks ? (nch - ks + KSPLIT - 1) / KSPLIT : 0;
   const int kl = 4 * (lane >> 4);
@@ -156,11 +184,13 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   for (int j = 0; j < nmine; j += G) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      if (j + g < nmine) {
-        const int k = (ks + (j + g) * KSPLIT) * 16 + kl;
-        fetch_op<MT, AKC>(ra, d.lda, k, d.K, a[g]);
-        fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
-      }
+      // unconditional (see fetch_op; a guard, even a wave-uniform one, makes the compiler
+      // drain the loads at the end of the guarded block): a group past the wave's last
+      // chunk re-reads that chunk and is skipped below
+      const int jj = j + g < nmine ? j + g : nmine - 1;
+      const int k = (ks + jj * KSPLIT) * 16 + kl;
+      fetch_op<MT, AKC, 0>(ra, d.lda, k, d.K, a[g]);
+      fetch_op<NT, BKC, 1>(rb, d.ldb, k, d.K, b[g]);
     }
     // after the LAST operand loads (vmcnt is in order); a row prologue (AXF 1) must
     // run before the first transform
