@@ -52,13 +52,77 @@ typedef float f4 __attribute__((ext_vector_type(4)));
   } while (0)
 
 // ---------------------------------------------------------------------------
-// operand fetch: NT 16-row subtiles x 4 consecutive k (k = k0 + 4g .. +3).
-// rp[t] is the lane's row pointer of subtile t (row clamped into range):
-//   KC  (K-contiguous, element (row,k) at rp + k):     one 16-byte load
-//   !KC (row-contiguous, element (row,k) at rp + k*ld): 4 loads, each a coalesced
+// Buffer-resource access (raw buffer ops): the base lives in a wave-uniform SGPR
+// descriptor and each lane carries one 32-bit byte offset, shared by every array that
+// is indexed alike (the Adam state) — no per-array 64-bit addresses held in VGPRs.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int kBufDword3 = 0x00020000;   // gfx9-family raw buffer descriptor word 3
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)bytes, kBufDword3);
+}
+__device__ __forceinline__ float buf_ld(rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void buf_st(rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)off, 0, 0);
+}
+
+// 16-byte buffer load.  The LLVM intrinsic is bound directly: on this toolchain (ROCm 7.2
+// hipcc) __builtin_amdgcn_raw_buffer_load_b128 lowers to a single buffer_load_dword.
+__device__ f4 llvm_raw_buffer_load_v4f32(rsrc_t r, int off, int soff, int aux)
+    __asm("llvm.amdgcn.raw.ptr.buffer.load.v4f32");
+__device__ __forceinline__ float4 buf_ld4(rsrc_t r, uint32_t off) {
+  const f4 v = llvm_raw_buffer_load_v4f32(r, (int)off, 0, 0);
+  return float4{v[0], v[1], v[2], v[3]};
+}
+__device__ void llvm_raw_buffer_store_v4f32(f4 v, rsrc_t r, int off, int soff, int aux)
+    __asm("llvm.amdgcn.raw.ptr.buffer.store.v4f32");
+__device__ __forceinline__ void buf_st4(rsrc_t r, uint32_t off, f4 v) {
+  llvm_raw_buffer_store_v4f32(v, r, (int)off, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// operand fetch: NT 16-row subtiles x 4 consecutive k (k = k0 + 4g .. +3), through one
+// buffer descriptor per operand (SGPRs) and a 32-bit byte offset per subtile row:
+//   KC  (K-contiguous, element (row,k) at off + 4k):       one 16-byte load
+//   !KC (row-contiguous, element (row,k) at off + 4k*ld):  4 loads, each a coalesced
 //        64-byte segment across the 16 lanes of a lane group.
-template <int NT, bool KC, int OP = 0>
-__device__ __forceinline__ void fetch_op(const float* const (&rp)[NT], int ld, int k, int K,
+// Branch-free: a load inside a divergent `if` (or any guarded block) is waited for at the
+// end of that block, which would serialise every operand load of the burst.  Rows are
+// clamped into range (row_offs) and out-of-range k reads a clamped address, zeroed by a
+// select.
+template <int NT>
+struct OpFetch {
+  rsrc_t r;
+  const char* p;
+  uint32_t off[NT];
+};
+
+#ifndef SACMI_FETCH_SADDR
+#define SACMI_FETCH_SADDR 0
+#endif
+// global load with a uniform 64-bit base and a 32-bit per-lane byte offset (saddr form)
+template <class T>
+__device__ __forceinline__ T gld_off(const char* base, uint32_t off) {
+  return *reinterpret_cast<const T*>(base + off);
+}
+
+template <int NT, bool KC>
+__device__ __forceinline__ void row_offs(const float* P, int ld, int row0, int nrows, int lane,
+                                         OpFetch<NT>& f) {
+  f.r = make_rsrc(P, 0x7fffffffu);
+  f.p = reinterpret_cast<const char*>(P);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    int row = row0 + t * 16 + (lane & 15);
+    row = row < nrows ? row : nrows - 1;
+    f.off[t] = KC ? (uint32_t)row * (uint32_t)ld * 4u : (uint32_t)row * 4u;
+  }
+}
+
+template <int NT, bool KC>
+__device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, int K,
                                          float (&v)[NT][4]) {
 #ifdef SACMI_EXP_NOLOAD
   // timing experiment only: no operand loads at all (MFMA + epilogue floor)
@@ -68,24 +132,11 @@ __device__ __forceinline__ void fetch_op(const float* const (&rp)[NT], int ld, i
     for (int s = 0; s < 4; ++s) v[t][s] = (float)(k + s + t) * 1e-3f;
   return;
 #endif
-#ifdef SACMI_EXP_BLOCKED
-  // timing experiment only (numerics meaningless): every fragment load lane-linear 16 B
-  if (SACMI_EXP_BLOCKED & (1 << OP))
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    float4 x = float4{0.f, 0.f, 0.f, 0.f};
-    if (k < K) x = *reinterpret_cast<const float4*>(rp[t] + (KC ? (size_t)(k >> 4) * 256 : (size_t)(k >> 4) * 16 * ld));
-    v[t][0] = x.x; v[t][1] = x.y; v[t][2] = x.z; v[t][3] = x.w;
-  }
-  if (SACMI_EXP_BLOCKED & (1 << OP)) return;
-#endif
-  // Branch-free: a load inside a divergent `if` is waited for inside it (the select that
-  // consumes it sits in the same block), which would serialise every operand load of the
-  // burst.  Out-of-range k reads a clamped in-bounds address and is zeroed by a select.
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (KC) {
-      const float4 x = *reinterpret_cast<const float4*>(rp[t] + (k < K ? k : 0));
+      const uint32_t o = f.off[t] + (uint32_t)(k < K ? k : 0) * 4u;
+      const float4 x = (SACMI_FETCH_SADDR & 1) ? gld_off<float4>(f.p, o) : buf_ld4(f.r, o);
       v[t][0] = (k < K) ? x.x : 0.f;
       v[t][1] = (k + 1 < K) ? x.y : 0.f;
       v[t][2] = (k + 2 < K) ? x.z : 0.f;
@@ -94,31 +145,11 @@ __device__ __forceinline__ void fetch_op(const float* const (&rp)[NT], int ld, i
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int kk = (k + s < K) ? (k + s) : (K - 1);
-        const float x = rp[t][(size_t)kk * ld];
+        const uint32_t o = f.off[t] + (uint32_t)kk * (uint32_t)ld * 4u;
+        const float x = (SACMI_FETCH_SADDR & 2) ? gld_off<float>(f.p, o) : buf_ld(f.r, o);
         v[t][s] = (k + s < K) ? x : 0.f;
       }
     }
-  }
-}
-
-template <int NT, bool KC, int OP = 0>
-__device__ __forceinline__ void row_ptrs(const float* P, int ld, int row0, int nrows, int lane,
-                                         const float* (&rp)[NT]) {
-#ifdef SACMI_EXP_BLOCKED
-  if (SACMI_EXP_BLOCKED & (1 << OP))
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    int rb = (row0 >> 4) + t;
-    rb = rb < (nrows - 1) / 16 ? rb : (nrows - 1) / 16;
-    rp[t] = KC ? P + (size_t)rb * 16 * ld + lane * 4 : P + (size_t)rb * 256 + lane * 4;
-  }
-  if (SACMI_EXP_BLOCKED & (1 << OP)) return;
-#endif
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    int row = row0 + t * 16 + (lane & 15);
-    row = row < nrows ? row : nrows - 1;
-    rp[t] = KC ? P + (size_t)row * ld : P + row;
   }
 }
 
@@ -150,8 +181,7 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
           int AXF = 0, class Pre, class Early = void (*)()>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
-                                            float* rsum, Pre&& pre, const float* coef = nullptr,
-                                            bool store_a = false, const float* axw = nullptr,
+                                            float* rsum, Pre&& pre, bool store_a = false,
                                             Early&& early = [] {}) {
   constexpr int MT = TM / 16, NT = TN / 16;
   const int lane = threadIdx.x & 63;
@@ -169,17 +199,27 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   float rs[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) rs[i] = 0.f;
-  const float* ra[MT];
-  const float* rb[NT];
-  row_ptrs<MT, AKC, 0>(d.A, d.lda, m0, d.M, lane, ra);
-  row_ptrs<NT, BKC, 1>(d.B, d.ldb, n0, d.N, lane, rb);
+  OpFetch<MT> ra;
+  OpFetch<NT> rb;
+  row_offs<MT, AKC>(d.A, d.lda, m0, d.M, lane, ra);
+  row_offs<NT, BKC>(d.B, d.ldb, n0, d.N, lane, rb);
   const int nch = (d.K + 15) >> 4;
   const int nmine = nch > ks ? (nch - ks + KSPLIT - 1) / KSPLIT : 0;
   const int kl = 4 * (lane >> 4);
   float a[G][MT][4], b[G][NT][4];
-  // AXF 1: the row prologue's own loads go out FIRST (older than every operand load), so
-  // its exchange barrier waits for them alone while the operands keep streaming in
-  if constexpr (AXF == 1) early();
+  // per-group side operands: AXF 1 the transform weights w[k..k+3]; !AKC the A K-scale
+  // (a zero-length descriptor where a desc has none: no branch around the loads)
+  constexpr bool XW = AXF == 1 || !AKC;
+  float xw[XW ? G : 1][4];
+  const rsrc_t rxw = AXF == 1 ? make_rsrc(d.ax_w, (uint32_t)d.K * 4u)
+                              : make_rsrc(d.a_ksc ? d.a_ksc : d.A, d.a_ksc ? (uint32_t)d.K * 4u : 0u);
+  const bool has_ksc = AXF != 1 && d.a_ksc != nullptr;
+  // AXF 1 side output: unconditional stores, dropped by a zero-length range where this
+  // workgroup stores nothing (a guarded store makes the compiler's vmcnt bookkeeping
+  // fall back to full drains)
+  const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
+                               store_a ? (uint32_t)(((size_t)(d.M - 1) * d.ax_ld + d.K) * 4) : 0u);
+  early();
   if (nmine == 0) pre();
   for (int j = 0; j < nmine; j += G) {
 #pragma unroll
@@ -189,30 +229,48 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       // chunk re-reads that chunk and is skipped below
       const int jj = j + g < nmine ? j + g : nmine - 1;
       const int k = (ks + jj * KSPLIT) * 16 + kl;
-      fetch_op<MT, AKC, 0>(ra, d.lda, k, d.K, a[g]);
-      fetch_op<NT, BKC, 1>(rb, d.ldb, k, d.K, b[g]);
+      fetch_op<MT, AKC>(ra, d.lda, k, d.K, a[g]);
+      fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
+      if constexpr (AXF == 1) {          // w3 rows are float4-aligned (parameter arena)
+        const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
+        xw[g][0] = x.x; xw[g][1] = x.y; xw[g][2] = x.z; xw[g][3] = x.w;
+      } else if constexpr (!AKC) {       // per-batch-row scale: any alignment
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xw[g][s] = buf_ld(rxw, (uint32_t)(k + s < d.K ? k + s : 0) * 4u);
+      }
+      // keep the issue order group by group: the first group's MFMAs then wait for it alone
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // after the LAST operand loads (vmcnt is in order); a row prologue (AXF 1) must
-    // run before the first transform
-    if (AXF == 1 ? j == 0 : j + G >= nmine) pre();
+    // after the LAST operand loads (vmcnt is in order)
+    if (j + G >= nmine) pre();
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int g = 0; g < G; ++g)
       if (j + g < nmine) {
+        // no FMA contraction here: the scaled fragments feed both the MFMAs and the row
+        // sums, and contracting a*f into a sum would make the row-sum bits depend on the
+        // tile configuration's code generation
+#pragma clang fp contract(off)
         if constexpr (AXF == 1) {
           const int k = (ks + (j + g) * KSPLIT) * 16 + kl;
-          float xw[4];                     // w[k..k+3] from the LDS copy (K <= 1024)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) xw[s] = axw[k + s < d.K ? k + s : d.K - 1];
 #pragma unroll
           for (int i = 0; i < MT; ++i) {
             const int r = mloc + i * 16 + (lane & 15);
-            const float cf = coef[r];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) a[g][i][s] = a[g][i][s] > 0.f ? cf * xw[s] : 0.f;
-            // the rows this level's tile-0 workgroups hold in full: dh2 for a later level
-            if (store_a && m0 - mloc + r < d.M && k < d.K)
-              *reinterpret_cast<float4*>(d.ax_out + (size_t)(m0 - mloc + r) * d.ax_ld + k) =
-                  float4{a[g][i][0], a[g][i][1], a[g][i][2], a[g][i][3]};
+            for (int s = 0; s < 4; ++s)
+              a[g][i][s] = (a[g][i][s] > 0.f && k + s < d.K) ? xw[g][s] : 0.f;
+            // the rows this level's tile-0 workgroups hold in full: u for a later level
+            const int rr = m0 - mloc + r;
+            buf_st4(rAx, (rr < d.M && k < d.K) ? (uint32_t)(rr * d.ax_ld + k) * 4u : 0xfffffff0u,
+                    f4{a[g][i][0], a[g][i][1], a[g][i][2], a[g][i][3]});
+          }
+        } else if constexpr (!AKC) {
+          // A K-scale (selected, not branched: 1 where the desc has none)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const float f = has_ksc ? xw[g][s] : 1.f;
+#pragma unroll
+            for (int i = 0; i < MT; ++i) a[g][i][s] *= f;
           }
         }
         mfma_chunk<MT, NT>(acc, a[g], b[g]);
@@ -248,12 +306,11 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
 // the variant from the level's descs): 1 -> axk 1 descs, 0 -> none.
 template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, class Pre, class Early>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
-                                          float* rsum, bool rowsum, Pre&& pre, const float* coef,
-                                          const float* axw, Early&& early) {
+                                          float* rsum, bool rowsum, Pre&& pre, Early&& early) {
   if constexpr (AXK == 1) {
     if (d.axk == 1) {        // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
-      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1>(d, m0, n0, red, rsum, pre, coef,
-                                                               n0 == 0 && d.ax_out != nullptr, axw,
+      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1>(d, m0, n0, red, rsum, pre,
+                                                               n0 == 0 && d.ax_out != nullptr,
                                                                early);
       return;
     }
@@ -277,23 +334,6 @@ __device__ __forceinline__ float reduce_partials(const float* red, int row, int 
 #pragma unroll
   for (int w = 1; w < KSPLIT; ++w) s += base[w * TM * (TN + 1)];
   return s;
-}
-
-// ---------------------------------------------------------------------------
-// Buffer-resource access (raw buffer ops): the base lives in a wave-uniform SGPR
-// descriptor and each lane carries one 32-bit byte offset, shared by every array that
-// is indexed alike (the Adam state) — no per-array 64-bit addresses held in VGPRs.
-using rsrc_t = __amdgpu_buffer_rsrc_t;
-constexpr int kBufDword3 = 0x00020000;   // gfx9-family raw buffer descriptor word 3
-
-__device__ __forceinline__ rsrc_t make_rsrc(const float* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, (int)bytes, kBufDword3);
-}
-__device__ __forceinline__ float buf_ld(rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
-}
-__device__ __forceinline__ void buf_st(rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)off, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -357,42 +397,81 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // the actor's block 0 also advances the step counters and forms dL/dlog_alpha.  Every
 // thread of the workgroup calls it (two barriers).
 // Registers a thread carries from rows_load() (before the operand loads) to
-// rows_finish() (after them).
+// rows_finish() (after them).  Every prologue load is issued in rows_load() and consumed
+// only in rows_finish(): vmcnt retires in order, so a value consumed before the operand
+// burst would hold the burst back, and one loaded after it would wait for all of it.
+constexpr int kRowsPv = 2;     // dot partials per thread (covers H <= 512; more: loaded late)
 struct RowsRegs {
-  float q;                    // thread (row, slot): the head's finished value
+  float pv[kRowsPv];          // dot partials, flat (row, slot, part) index t + q*NTH
   float r, d, lp, alpha;      // thread row < TMW: the row's own inputs
+  float lpa;                  // actor block 0, wave past the row threads: logp_part[lane]
 };
 
-template <int TMW>
-__device__ __forceinline__ void rows_load(const RowsFuse& rf, int m0, RowsRegs& x) {
+template <int TMW, int NTH>
+__device__ __forceinline__ void rows_load(const RowsFuse& rf, const GemmDesc& d, int m0,
+                                          RowsRegs& x) {
   const int t = threadIdx.x;
   const int nslot = rf.kind == 1 ? 4 : 2;
-  x.q = 0.f;
-  if (t < TMW * nslot) {
-    const int row = t / nslot, sl = t % nslot, b = m0 + row;
-    if (b < rf.B) {
-      const float* pp = rf.part + ((size_t)sl * rf.B + b) * rf.nparts;
-      float acc = pp[0];
-      for (int i = 1; i < rf.nparts; ++i) acc += pp[i];
-      x.q = acc + *rf.b3[sl];
-    }
+  const int per_row = nslot * rf.nparts, V = TMW * per_row;
+  // unconditional buffer loads (a guarded load is drained at the end of its guard);
+  // descriptors of zero length where this desc has no prologue (nothing is read)
+  const bool on = d.axk == 1;
+  const uint32_t big = 0x7fffffffu;
+  const rsrc_t rPart = make_rsrc(on ? rf.part : d.C, on ? big : 0u);
+  const rsrc_t rLp = make_rsrc(on ? rf.logp : d.C, on ? big : 0u);
+  const rsrc_t rR = make_rsrc(on ? (rf.kind == 1 ? rf.r : rf.logp) : d.C, on ? big : 0u);
+  const rsrc_t rD = make_rsrc(on ? (rf.kind == 1 ? rf.d : rf.logp) : d.C, on ? big : 0u);
+  const rsrc_t rLpa = make_rsrc(on && rf.logp_part ? rf.logp_part : d.C, on && rf.logp_part ? big : 0u);
+  const rsrc_t rSc = make_rsrc(on ? &rf.sc->alpha : d.C, on ? 4u : 0u);
+#pragma unroll
+  for (int q = 0; q < kRowsPv; ++q) {
+    const int idx = t + q * NTH;
+    const int row = idx / per_row, rem = idx - row * per_row;
+    const int sl = rem / rf.nparts, i = rem - sl * rf.nparts;
+    const bool ok = idx < V && m0 + row < rf.B;
+    x.pv[q] = buf_ld(rPart, ok ? (uint32_t)(((size_t)sl * rf.B + m0 + row) * rf.nparts + i) * 4u : 0u);
   }
-  x.r = x.d = x.lp = x.alpha = 0.f;
   const int b = m0 + t;
-  if (t < TMW && b < rf.B) {
-    x.alpha = rf.sc->alpha;
-    x.lp = rf.logp[b];
-    if (rf.kind == 1) { x.r = rf.r[b]; x.d = rf.d[b]; }
-  }
+  const uint32_t ob = (uint32_t)((t < TMW && b < rf.B) ? b : 0) * 4u;
+  x.alpha = buf_ld(rSc, 0u);
+  x.lp = buf_ld(rLp, ob);
+  x.r = buf_ld(rR, ob);
+  x.d = buf_ld(rD, ob);
+  const int lane = t - TMW * nslot;
+  x.lpa = buf_ld(rLpa, (uint32_t)(2 * (lane >= 0 && lane < rf.n_lp ? lane : 0) + 1) * 4u);
 }
 
-template <int TMW>
-__device__ void rows_finish(const RowsFuse& rf, int m0, bool writer, bool first_block,
-                            const RowsRegs& x, float (*s_q)[4], float (*s_coef)[TMW],
-                            float (*s_l)[2]) {
+template <int TMW, int NTH>
+__device__ void rows_finish(const RowsFuse& rf, const GemmDesc& d, int m0, bool writer,
+                            bool first_block, const RowsRegs& x0, float* s_part,
+                            float (*s_q)[4], float (*s_coef)[TMW], float (*s_l)[2]) {
   const int t = threadIdx.x;
   const int nslot = rf.kind == 1 ? 4 : 2;
-  if (t < TMW * nslot) s_q[t / nslot][t % nslot] = x.q;
+  const int per_row = nslot * rf.nparts, V = TMW * per_row;
+  // pin every prologue value to this point (after the MFMAs): without it the compiler
+  // hoists cheap uses (e.g. 0 + lpa) up to the loads, and their wait then holds the
+  // operand loads back
+  RowsRegs x = x0;
+#pragma unroll
+  for (int q = 0; q < kRowsPv; ++q) asm volatile("" : "+v"(x.pv[q]));
+  asm volatile("" : "+v"(x.r), "+v"(x.d), "+v"(x.lp), "+v"(x.lpa), "+v"(x.alpha));
+#pragma unroll
+  for (int q = 0; q < kRowsPv; ++q)
+    if (t + q * NTH < V) s_part[t + q * NTH] = x.pv[q];
+  for (int idx = t + kRowsPv * NTH; idx < V; idx += NTH) {     // H > 512 only
+    const int row = idx / per_row, rem = idx - row * per_row;
+    const int sl = rem / rf.nparts, i = rem - sl * rf.nparts;
+    s_part[idx] = m0 + row < rf.B ? rf.part[((size_t)sl * rf.B + m0 + row) * rf.nparts + i] : 0.f;
+  }
+  __syncthreads();
+  if (t < TMW * nslot) {
+    // the row's partials summed in column order (block 0's carries the fc3 bias)
+    const int row = t / nslot, sl = t % nslot;
+    const float* pp = s_part + row * per_row + sl * rf.nparts;
+    float acc = pp[0];
+    for (int i = 1; i < rf.nparts; ++i) acc += pp[i];
+    s_q[row][sl] = m0 + row < rf.B ? acc : 0.f;
+  }
   if (first_block && rf.kind == 2) {
     const int w0 = TMW * nslot;            // first wave past the partial-sum threads
     if (t >= w0 && t < w0 + 64) {
@@ -400,8 +479,10 @@ __device__ void rows_finish(const RowsFuse& rf, int m0, bool writer, bool first_
       // per-workgroup sums: strided per lane, then a fixed butterfly
       const int lane = t - w0;
       float acc = 0.f;
-      if (rf.alpha_grad)
-        for (int w = lane; w < rf.n_lp; w += 64) acc += rf.logp_part[2 * w + 1];
+      if (rf.alpha_grad) {
+        if (lane < rf.n_lp) acc += x.lpa;
+        for (int w = lane + 64; w < rf.n_lp; w += 64) acc += rf.logp_part[2 * w + 1];
+      }
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
       if (lane == 0) {
@@ -443,8 +524,16 @@ __device__ void rows_finish(const RowsFuse& rf, int m0, bool writer, bool first_
     s_coef[0][t] = c0; s_coef[1][t] = c1;
     s_l[t][0] = l0; s_l[t][1] = l1;
   }
-  __syncthreads();                         // coefficients visible to the transform
+  __syncthreads();                         // coefficients visible to the epilogue
   SACMI_STAMP(35);
+}
+
+// the row block's loss partial (fixed row order), at the very end of the kernel: a
+// serial LDS chain nobody else waits for
+template <int TMW>
+__device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool writer,
+                                          const float (*s_l)[2]) {
+  const int t = threadIdx.x;
   if (writer && t < (rf.kind == 1 ? 2 : 1)) {
     float acc = 0.f;
     for (int r = 0; r < TMW; ++r) acc += s_l[r][t];
@@ -464,9 +553,9 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   constexpr int TMW = TM * MG;
   __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
   __shared__ float rsum[MG * KSPLIT * TM];
+  __shared__ float s_part[AXK == 1 ? TMW * 4 * 32 : 1];   // row prologue: dot partials
   __shared__ AdamScalars s_k;
   __shared__ float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
-  __shared__ float s_axw[AXK == 1 ? 1024 : 1];   // the transform's w3 row
   const int bid = blockIdx.x;
   if (bid >= batch.total_tiles) {   // ride-along workgroups (next update's replay work)
     if constexpr (MG * KSPLIT == 16) {   // the host attaches rides to 1024-thread configs
@@ -542,34 +631,48 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   RowsRegs rows_x{};
   // the epilogue operands (Adam state, or the bias / mask) go out under the MFMAs; the
   // fc3 dot weights of the tile go to LDS; an axk-1 level runs its row prologue
+  // the fc3 dot weight of this thread's tile column, loaded up front (buffer op with a
+  // zero-length range where the level has none: no branch, so nothing waits for it early)
+  // (loaded in pre(), after the operand burst; staged to LDS after the MFMAs)
+  float dotw_x = 0.f, dotb_x = 0.f;
   auto pre = [&]() {
-    if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? d.dotw[n0 + tid] : 0.f;
-    if constexpr (AXK == 1) {
-      if (d.axk == 1)
-        rows_finish<TMW>(batch.rows, m0, p == 0 && n0 == 0, bid == 0, rows_x, s_q, s_coef, s_l);
+    // axk 1: the row prologue's loads.  Issued here, behind the operand burst, and
+    // consumed after the MFMAs: anything in flight at the k-loop header is waited for by
+    // the back-edge's conservative vmcnt on the first iteration.
+    if constexpr (AXK == 1) rows_load<TMW, NTH>(batch.rows, d, m0, rows_x);   // unconditional
+    {   // buffer ops with a zero-length range where the level has no dots: no branch
+      const rsrc_t rDW = make_rsrc(d.dotp ? d.dotw : d.C, d.dotp ? (uint32_t)(d.N + 1) * 4u : 0u);
+      const int nn = n0 + (tid < TN ? tid : 0);
+      dotw_x = buf_ld(rDW, (uint32_t)(nn < d.N ? nn : 0) * 4u);
+      dotb_x = buf_ld(rDW, (uint32_t)d.N * 4u);   // the head's bias w3~[N]
     }
+    // unconditional: an empty slot reads past its descriptor's range (returns 0, no
+    // access), and the level's unused operands have zero-length descriptors
+    constexpr uint32_t kOob = 0xfffffff0u;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       int row, col, n;
-      if (!slot(s, row, col, n)) continue;
+      const bool ok = slot(s, row, col, n);
       if constexpr (ADAM) {
-        const uint32_t o = (uint32_t)((m0 + row) * d.ldc + n) * 4u;
+        const uint32_t o = ok ? (uint32_t)((m0 + row) * d.ldc + n) * 4u : kOob;
         x0[s] = buf_ld(rC, o); x1[s] = buf_ld(rM, o); x2[s] = buf_ld(rV, o);
-        if (pol) x3[s] = buf_ld(rT, o);
+        x3[s] = buf_ld(rT, o);
       } else {
-        if (d.bias) x0[s] = buf_ld(rX, (uint32_t)(n * d.bias_ld) * 4u);
-        else if (d.epi == EPI_MASK) x0[s] = buf_ld(rX, (uint32_t)((m0 + row) * d.ldaux + n) * 4u);
+        const uint32_t o = !ok ? kOob
+                         : d.bias ? (uint32_t)(n * d.bias_ld) * 4u
+                                  : (uint32_t)((m0 + row) * d.ldaux + n) * 4u;
+        x0[s] = buf_ld(rX, o);
       }
     }
   };
-  auto early = [&]() {       // axk 1: the row prologue's loads, ahead of the operand loads
-    if constexpr (AXK == 1) {
-      for (int k = tid; k < d.K; k += NTH) s_axw[k] = d.ax_w[k];   // read after the barriers
-      rows_load<TMW>(batch.rows, m0, rows_x);
-    }
-  };
-  gemm_core<TM, TN, KSPLIT, G, MG, AXK>(d, m0, n0, red, rsum, rowsum, pre, s_coef[d.ax_slot], s_axw,
-                                        early);
+  gemm_core<TM, TN, KSPLIT, G, MG, AXK>(d, m0, n0, red, rsum, rowsum, pre, [] {});
+  if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
+  if constexpr (AXK == 1) {
+    // the row prologue, after the MFMAs: its loads went out first and have long landed
+    if (d.axk == 1)
+      rows_finish<TMW, NTH>(batch.rows, d, m0, p == 0 && n0 == 0, bid == 0, rows_x, s_part,
+                            s_q, s_coef, s_l);
+  }
   __syncthreads();
   if (threadIdx.x < 64) SACMI_STAMP(32);
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
@@ -588,6 +691,9 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
         for (int w = 1; w < KSPLIT; ++w) v += rb[w * TM];
       }
       const uint32_t o = (uint32_t)((m0 + row) * d.ldc + n) * 4u;
+      if constexpr (AXK == 1) {
+        if (d.axk == 1) v *= s_coef[d.ax_slot][row];   // dh = coef[b] * (u W2)
+      }
       if constexpr (ADAM) {
         adam_elem(x0[s], x1[s], x2[s], v, omb1, af.beta2, omb2, af.eps, s_k);
         if (af.G) buf_st(rG, o, v);
@@ -607,12 +713,15 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
         float c = ok ? v * s_dotw[col] : 0.f;
 #pragma unroll
         for (int off = 16; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
-        if ((tid & 31) == 0 && m0 + row < d.M)
-          d.dotp[(size_t)(m0 + row) * d.dotp_ld + (n0 + col) / 32] = c;
+        if ((tid & 31) == 0 && m0 + row < d.M)   // block 0 adds the bias: q = sum of blocks
+          d.dotp[(size_t)(m0 + row) * d.dotp_ld + (n0 + col) / 32] = n0 + col == 0 ? c + dotb_x : c;
       }
     }
   }
   if (threadIdx.x < 64) SACMI_STAMP(33);
+  if constexpr (AXK == 1) {
+    if (d.axk == 1) rows_loss<TMW>(batch.rows, m0, p == 0 && n0 == 0, s_l);
+  }
   if (batch.has_adam && bid == 0) {
     __syncthreads();
     if (threadIdx.x < af.n_losses) {
@@ -753,14 +862,15 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   const int row = e / A, j = e % A, m = m0 + row;
   const bool live = e < TM * A && m < a.rows;
   float bm = 0.f, bl = 0.f, eps_in = 0.f;
-  auto pre = [&]() {
-    if (live) {
-      bm = a.Wh[(size_t)j * a.ldw + a.K];
-      bl = a.Wh[(size_t)(A + j) * a.ldw + a.K];
-      if (!a.deterministic && !a.gen_eps) eps_in = a.eps[(size_t)m * A + j];
-    }
+  auto pre = [&]() {     // unconditional loads at clamped addresses (no guarded loads)
+    const int jj = live ? j : 0, mm = live ? m : 0;
+    bm = a.Wh[(size_t)jj * a.ldw + a.K];
+    bl = a.Wh[(size_t)(A + jj) * a.ldw + a.K];
+    const bool want = !a.deterministic && !a.gen_eps;
+    eps_in = buf_ld(make_rsrc(want ? a.eps : a.Wh, want ? 0x7fffffffu : 0u),
+                    (uint32_t)((size_t)mm * A + jj) * 4u);
   };
-  gemm_core_l<TM, TN, KSPLIT, 3, true, true, false>(d, m0, 0, red, nullptr, pre);
+  gemm_core_l<TM, TN, KSPLIT, 2, true, true, false>(d, m0, 0, red, nullptr, pre);
   __syncthreads();
   const uint64_t ctr = a.ctr_override ? a.ctr_override : a.sc->noise_counter;
   if (e < TM * A) {
@@ -853,35 +963,40 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int K2 = 2 * A, ksteps = (K2 + 3) / 4;
   float bw[2][NST], mk[2][4];
+  // every load below is unconditional at a clamped address (zeroed by a select): a
+  // guarded load is drained at the end of its guard, serialising the burst it sits in
   auto load_mask = [&](int n0) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = n0 + t * 16 + (lane & 15);
-      const float* hp = a.hp2 + (size_t)(m0 + (lane >> 4) * 4) * a.ldh + (n < a.H ? n : 0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        mk[t][r] = (m0 + (lane >> 4) * 4 + r < d.M && n < a.H) ? hp[(size_t)r * a.ldh] : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        const int mr = m0 + (lane >> 4) * 4 + r;
+        const bool ok = mr < d.M && n < a.H;
+        const float x = a.hp2[ok ? (size_t)mr * a.ldh + n : 0];
+        mk[t][r] = ok ? x : 0.f;
+      }
     }
   };
   auto load_w = [&](int n0) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int n = n0 + t * 16 + (lane & 15);
-      const float* wp = a.Wh + (size_t)(lane >> 4) * a.ldw + (n < a.H ? n : 0);
 #pragma unroll
       for (int st = 0; st < NST; ++st) {
         const int k = 4 * st + (lane >> 4);
-        bw[t][st] = (st < ksteps && k < K2 && n < a.H) ? wp[(size_t)4 * st * a.ldw] : 0.f;
+        const bool ok = st < ksteps && k < K2 && n < a.H;
+        const float x = a.Wh[ok ? (size_t)k * a.ldw + n : 0];
+        bw[t][st] = ok ? x : 0.f;
       }
     }
   };
   auto pre = [&]() {
-    if (live) {
-      const float* cr = a.cache + (size_t)m * 3 * A;
-      ls_raw = cr[A + j];
-      y = cr[2 * A + j];
-      eps = a.eps[(size_t)m * A + j];
-    }
+    const int mm = live ? m : 0, jj = live ? j : 0;
+    const float* cr = a.cache + (size_t)mm * 3 * A;
+    ls_raw = cr[A + jj];
+    y = cr[2 * A + jj];
+    eps = a.eps[(size_t)mm * A + jj];
     load_mask(wave * 32);
   };
   gemm_core_l<TM, TN, KSPLIT, 2, true, false, false>(d, m0, 0, red, nullptr, pre);

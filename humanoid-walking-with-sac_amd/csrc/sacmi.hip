@@ -357,8 +357,12 @@ static void validate(const GemmDesc& d) {
       check_span(d.ax_out, (int64_t)(d.M - 1) * d.ax_ld + d.K - 1, "ax_out");
     }
   }
+  if (d.a_ksc) {
+    REQUIRE(!d.a_kc && !d.axk, SACMI_ESTATE, "a_ksc needs a row-contiguous A operand");
+    check_span(d.a_ksc, d.K - 1, "a_ksc");
+  }
   if (d.dotp) {
-    check_span(d.dotw, d.N - 1, "dotw");
+    check_span(d.dotw, d.N, "dotw");      // w3 and the head bias w3~[N]
     check_span(d.dotp, (int64_t)(d.M - 1) * d.dotp_ld + (d.N - 1) / 32, "dotp");
   }
   if (d.epi == EPI_MASK) check_span(d.aux, (int64_t)(d.M - 1) * d.ldaux + d.N - 1, "aux");
@@ -560,8 +564,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     {
       RowsFuse& rf = l5.b.rows;
       rf.kind = 1; rf.part = dotp(0); rf.nparts = c->nparts; rf.B = B;
-      rf.b3[0] = W(q[0][2]) + H; rf.b3[1] = W(q[1][2]) + H;
-      rf.b3[2] = Wt(q[0][2]) + H; rf.b3[3] = Wt(q[1][2]) + H;
       rf.r = bb.r; rf.d = bb.d; rf.logp = c->logp.p; rf.logp_a = c->logp.p + B;
       rf.gamma = (float)c->cfg.gamma;
       rf.sc = c->sc.p; rf.dq = c->dq.p; rf.loss_part = c->lpart_c.p;
@@ -573,8 +575,12 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     auto dst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
     const int wepi = fuse ? EPI_ADAM_POLYAK : EPI_STORE;
     for (int i = 0; i < 2; ++i) {
-      lw.add(gd_dw_h(c->dh2.p + i * H, 2 * H, c->hq1.p + i * Hd, 2 * Hd, dst(q[i][1]), Hd, H, H, B,
-                     wepi, 1 + i));
+      // L5 stores u = dh2 / coef (the coefficient factored out of its dh1 rows): the
+      // fc2 weight gradient applies coef = dL/dq_i (dq) as a per-batch-row K-scale
+      GemmDesc w2 = gd_dw_h(c->dh2.p + i * H, 2 * H, c->hq1.p + i * Hd, 2 * Hd, dst(q[i][1]), Hd,
+                            H, H, B, wepi, 1 + i);
+      w2.a_ksc = c->dq.p + i * B;
+      lw.add(w2);
       lw.add(gd_dw_h(c->dq.p + i * B, 1, c->hq2.p + i * Hd, 2 * Hd, dst(q[i][2]), Hd, 1, H, B,
                      wepi, 1 + i));
     }
@@ -645,7 +651,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     {
       RowsFuse& rf = l9.b.rows;
       rf.kind = 2; rf.part = dotp(4); rf.nparts = c->nparts; rf.B = B;
-      rf.b3[0] = W(q[0][2]) + H; rf.b3[1] = W(q[1][2]) + H;
       rf.logp = c->logp.p + B; rf.sc = c->sc.p; rf.loss_part = c->lpart_a.p;
       if (c->cfg.auto_entropy) {
         rf.alpha_grad = G + c->la_idx; rf.logp_part = c->lp_part.p; rf.n_lp = (2 * B + 15) / 16;

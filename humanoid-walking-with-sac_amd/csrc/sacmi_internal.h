@@ -84,15 +84,22 @@ struct GemmDesc {
   const float* dotw;
   float* dotp;
   int dotp_ld;
-  // A-operand transform (the critic / actor fc3 backward folded into the next GEMM):
-  //   axk 1 (A K-contiguous, rows = batch): a(b,k) = A(b,k) > 0 ? coef[b] * ax_w[k] : 0,
-  //         coef from this workgroup's row prologue (GemmBatch.rows, slot ax_slot);
-  //         the column-tile-0 workgroups also store the transformed rows to ax_out
-  //         (row stride ax_ld) when it is set — the dh2 a later level needs
+  // A-operand transform (the critic / actor fc3 backward folded into the next GEMM).
+  // The head gradient of row b is dh2(b,k) = coef[b] * ax_w[k] * [A(b,k) > 0], and coef[b]
+  // factors out of the row's dot products, so
+  //   axk 1 (A K-contiguous, rows = batch): a(b,k) = A(b,k) > 0 ? ax_w[k] : 0, and the
+  //         epilogue multiplies output row b by coef[b] (slot ax_slot of this workgroup's
+  //         row prologue, GemmBatch.rows, which runs after the MFMAs: its loads never sit
+  //         on the critical path); the column-tile-0 workgroups also store the unscaled
+  //         rows u(b,k) = a(b,k) to ax_out (row stride ax_ld) — a later level applies
+  //         coef with a_ksc.
   int axk, ax_slot;
   const float* ax_w;
   float* ax_out;
   int ax_ld;
+  // A row-contiguous only: a(m,k) *= a_ksc[k] (per-K scale, e.g. dh2 = coef (x) u for the
+  // critic fc2 weight gradient)
+  const float* a_ksc;
   int adam_step;       // EPI_ADAM*: optimizer step counter index (0 pi, 1 q1, 2 q2)
   const float* bias;   // forward epilogue: C += bias[n * bias_ld] (before the ReLU)
   int bias_ld;
@@ -160,7 +167,6 @@ struct RowsFuse {
   int kind;                  // 0 none, 1 critic (target + MSE), 2 actor (min Q)
   const float* part;         // [nslot][B][nparts] dot partials (critic: q1 q2 qt1 qt2; actor: qa1 qa2)
   int nparts, B;
-  const float* b3[4];        // fc3 bias of each slot (device parameters)
   const float* r; const float* d;
   const float* logp;         // critic: log pi(a'|s2);  actor: log pi(a~|s)
   const float* logp_a;       // critic: log pi(a~|s) for the alpha gradient

@@ -114,9 +114,9 @@ static void stamp_cfg(GemmBatch b, hipStream_t s) {
       p2.push_back((h[i][35] - h[i][0]) * 0.01);
     }
     if (!p1.empty()) {
-      std::sort(p1.begin(), p1.end()); std::sort(p2.begin(), p2.end());
-      printf("      prologue (from wave-0 entry): first barrier med %.2f max %.2f | done med %.2f max %.2f\n",
-             p1[p1.size() / 2], p1.back(), p2[p2.size() / 2], p2.back());
+      auto md = [](std::vector<double>& v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+      printf("      row prologue (after the MFMAs; from wave-0 entry, medians): sum barrier %.2f | "
+             "coef barrier %.2f\n", md(p1), md(p2));
     }
   }
   printf("      span %.2f | start med %.2f max %.2f | core(max wave) med %.2f max %.2f | core(min wave) med %.2f | "
@@ -281,7 +281,6 @@ int main(int argc, char** argv) {
     }
     RowsFuse& rf = b.rows;
     rf.kind = 1; rf.part = part; rf.nparts = 16; rf.B = B;
-    for (int i = 0; i < 4; ++i) rf.b3[i] = P + q1n + q2n + H;
     rf.r = rvec; rf.d = dvec; rf.logp = lpv; rf.gamma = 0.99f; rf.sc = sc; rf.dq = dqv;
     rf.loss_part = lpart;
     return b; }});
