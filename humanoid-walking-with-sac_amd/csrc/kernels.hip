@@ -400,9 +400,9 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // rows_finish() (after them).  Every prologue load is issued in rows_load() and consumed
 // only in rows_finish(): vmcnt retires in order, so a value consumed before the operand
 // burst would hold the burst back, and one loaded after it would wait for all of it.
-constexpr int kRowsPv = 2;     // dot partials per thread (covers H <= 512; more: loaded late)
+constexpr int kRowsPv = 16;    // dot partials held per (row, slot) thread: H <= 512
 struct RowsRegs {
-  float pv[kRowsPv];          // dot partials, flat (row, slot, part) index t + q*NTH
+  float pv[kRowsPv];          // thread (row, slot) < TMW*nslot: the row's dot partials
   float r, d, lp, alpha;      // thread row < TMW: the row's own inputs
   float lpa;                  // actor block 0, wave past the row threads: logp_part[lane]
 };
@@ -412,24 +412,24 @@ __device__ __forceinline__ void rows_load(const RowsFuse& rf, const GemmDesc& d,
                                           RowsRegs& x) {
   const int t = threadIdx.x;
   const int nslot = rf.kind == 1 ? 4 : 2;
-  const int per_row = nslot * rf.nparts, V = TMW * per_row;
   // unconditional buffer loads (a guarded load is drained at the end of its guard);
-  // descriptors of zero length where this desc has no prologue (nothing is read)
+  // descriptors of zero length where this desc has no prologue (nothing is read), and
+  // reads past a range for the threads / parts that have none (they return 0)
   const bool on = d.axk == 1;
-  const uint32_t big = 0x7fffffffu;
+  const uint32_t big = 0x7fffffffu, oob = 0xfffffff0u;
   const rsrc_t rPart = make_rsrc(on ? rf.part : d.C, on ? big : 0u);
   const rsrc_t rLp = make_rsrc(on ? rf.logp : d.C, on ? big : 0u);
   const rsrc_t rR = make_rsrc(on ? (rf.kind == 1 ? rf.r : rf.logp) : d.C, on ? big : 0u);
   const rsrc_t rD = make_rsrc(on ? (rf.kind == 1 ? rf.d : rf.logp) : d.C, on ? big : 0u);
   const rsrc_t rLpa = make_rsrc(on && rf.logp_part ? rf.logp_part : d.C, on && rf.logp_part ? big : 0u);
   const rsrc_t rSc = make_rsrc(on ? &rf.sc->alpha : d.C, on ? 4u : 0u);
+  {
+    const int row = t / nslot, sl = t % nslot;
+    const bool ok = t < TMW * nslot && m0 + row < rf.B;
+    const uint32_t base = (uint32_t)(((size_t)sl * rf.B + m0 + row) * rf.nparts) * 4u;
 #pragma unroll
-  for (int q = 0; q < kRowsPv; ++q) {
-    const int idx = t + q * NTH;
-    const int row = idx / per_row, rem = idx - row * per_row;
-    const int sl = rem / rf.nparts, i = rem - sl * rf.nparts;
-    const bool ok = idx < V && m0 + row < rf.B;
-    x.pv[q] = buf_ld(rPart, ok ? (uint32_t)(((size_t)sl * rf.B + m0 + row) * rf.nparts + i) * 4u : 0u);
+    for (int i = 0; i < kRowsPv; ++i)
+      x.pv[i] = buf_ld(rPart, ok && i < rf.nparts ? base + 4u * i : oob);
   }
   const int b = m0 + t;
   const uint32_t ob = (uint32_t)((t < TMW && b < rf.B) ? b : 0) * 4u;
@@ -443,11 +443,10 @@ __device__ __forceinline__ void rows_load(const RowsFuse& rf, const GemmDesc& d,
 
 template <int TMW, int NTH>
 __device__ void rows_finish(const RowsFuse& rf, const GemmDesc& d, int m0, bool writer,
-                            bool first_block, const RowsRegs& x0, float* s_part,
+                            bool first_block, const RowsRegs& x0,
                             float (*s_q)[4], float (*s_coef)[TMW], float (*s_l)[2]) {
   const int t = threadIdx.x;
   const int nslot = rf.kind == 1 ? 4 : 2;
-  const int per_row = nslot * rf.nparts, V = TMW * per_row;
   // pin every prologue value to this point (after the MFMAs): without it the compiler
   // hoists cheap uses (e.g. 0 + lpa) up to the loads, and their wait then holds the
   // operand loads back
@@ -455,21 +454,15 @@ __device__ void rows_finish(const RowsFuse& rf, const GemmDesc& d, int m0, bool 
 #pragma unroll
   for (int q = 0; q < kRowsPv; ++q) asm volatile("" : "+v"(x.pv[q]));
   asm volatile("" : "+v"(x.r), "+v"(x.d), "+v"(x.lp), "+v"(x.lpa), "+v"(x.alpha));
-#pragma unroll
-  for (int q = 0; q < kRowsPv; ++q)
-    if (t + q * NTH < V) s_part[t + q * NTH] = x.pv[q];
-  for (int idx = t + kRowsPv * NTH; idx < V; idx += NTH) {     // H > 512 only
-    const int row = idx / per_row, rem = idx - row * per_row;
-    const int sl = rem / rf.nparts, i = rem - sl * rf.nparts;
-    s_part[idx] = m0 + row < rf.B ? rf.part[((size_t)sl * rf.B + m0 + row) * rf.nparts + i] : 0.f;
-  }
-  __syncthreads();
   if (t < TMW * nslot) {
     // the row's partials summed in column order (block 0's carries the fc3 bias)
     const int row = t / nslot, sl = t % nslot;
-    const float* pp = s_part + row * per_row + sl * rf.nparts;
-    float acc = pp[0];
-    for (int i = 1; i < rf.nparts; ++i) acc += pp[i];
+    float acc = x.pv[0];
+#pragma unroll
+    for (int i = 1; i < kRowsPv; ++i)
+      if (i < rf.nparts) acc += x.pv[i];
+    for (int i = kRowsPv; i < rf.nparts; ++i)     // H > 512 only
+      acc += rf.part[((size_t)sl * rf.B + m0 + row) * rf.nparts + i];
     s_q[row][sl] = m0 + row < rf.B ? acc : 0.f;
   }
   if (first_block && rf.kind == 2) {
@@ -553,7 +546,6 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   constexpr int TMW = TM * MG;
   __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
   __shared__ float rsum[MG * KSPLIT * TM];
-  __shared__ float s_part[AXK == 1 ? TMW * 4 * 32 : 1];   // row prologue: dot partials
   __shared__ AdamScalars s_k;
   __shared__ float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
   const int bid = blockIdx.x;
@@ -670,7 +662,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   if constexpr (AXK == 1) {
     // the row prologue, after the MFMAs: its loads went out first and have long landed
     if (d.axk == 1)
-      rows_finish<TMW, NTH>(batch.rows, d, m0, p == 0 && n0 == 0, bid == 0, rows_x, s_part,
+      rows_finish<TMW, NTH>(batch.rows, d, m0, p == 0 && n0 == 0, bid == 0, rows_x,
                             s_q, s_coef, s_l);
   }
   __syncthreads();
