@@ -526,11 +526,15 @@ __device__ void rows_finish(const RowsFuse& rf, const GemmDesc& d, int m0, bool 
 template <int TMW>
 __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool writer,
                                           const float (*s_l)[2]) {
+  // one partial per 32-row block whatever the tile height: the host sizes and reduces
+  // them per 32 rows, and the bits do not depend on the tile configuration
   const int t = threadIdx.x;
-  if (writer && t < (rf.kind == 1 ? 2 : 1)) {
+  const int nl = rf.kind == 1 ? 2 : 1;
+  if (writer && t < nl * (TMW / 32)) {
+    const int h = t / nl, l = t % nl;
     float acc = 0.f;
-    for (int r = 0; r < TMW; ++r) acc += s_l[r][t];
-    rf.loss_part[(m0 / TMW) * (rf.kind == 1 ? 2 : 1) + t] = acc;
+    for (int r = 32 * h; r < 32 * h + 32; ++r) acc += s_l[r][l];
+    if (m0 + 32 * h < rf.B) rf.loss_part[(m0 / 32 + h) * nl + l] = acc;
   }
 }
 
@@ -784,20 +788,27 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   // (Level::add guarantees a level is all-Adam or all-plain)
   int axk = 0;
   for (int i = 0; i < b.count; ++i) axk = b.d[i].axk > axk ? b.d[i].axk : axk;
+  // weight-gradient levels (both operands row-contiguous): the Adam-fused and the plain
+  // (data-parallel) form of a level take the same tile geometry, so their bits agree
+  bool dw = true;
+  for (int i = 0; i < b.count; ++i) dw = dw && !b.d[i].a_kc && !b.d[i].b_kc;
   const dim3 blk(1024);
   const int t64 = assign_tiles<32, 64>(b);
-  if (n_adam && t64 <= 256 && maxk <= 16 * 16) {
-    // fused Adam, one 32x64 tile per CU (policy level): 16 waves, one K chunk each
-    hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, true>), dim3(b.total_tiles + extra), blk, 0, s, b);
-  } else if (n_adam || (t64 > 256 && maxk <= 16 * 8 * 2)) {
-    // weight gradients at batch <= 256 with more 32x64 tiles than CUs (the twin
-    // critic level): 64x64 tiles — exactly 256 of them — as two 32-row wave groups,
-    // each with an 8-way K split; the epilogue state is prefetched under the MFMAs
+  if (dw && t64 <= 256) {
+    // one 32x64 tile per CU (policy level): 16 waves, K split 16 ways
+    if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, true>), dim3(b.total_tiles + extra), blk, 0, s, b);
+    else hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, false>), dim3(b.total_tiles + extra), blk, 0, s, b);
+  } else if (dw || n_adam || t64 > 512) {
+    // more 32x64 tiles than CUs (the twin critic weight gradients; every level at large
+    // batch): 64x64 tiles as two 32-row wave groups, each with an 8-way K split — half
+    // the operand bytes per FLOP of a 32x64 tile; the epilogue state is prefetched under
+    // the MFMAs
     const int g = assign_tiles<64, 64>(b) + extra;
     if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, true>), dim3(g), blk, 0, s, b);
+    else if (axk == 1) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false, 1>), dim3(g), blk, 0, s, b);
     else hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false>), dim3(g), blk, 0, s, b);
   } else if (axk == 1) {
-    // dh1 / dha1 with the fc3 backward folded in (row prologue + A transform)
+    // dh1 / dha1 with the fc3 backward folded in (A transform, coefficient in the epilogue)
     const int g = assign_tiles<32, 32>(b) + extra;
     hipLaunchKernelGGL((k_gemm<32, 32, 16, 2, 1, false, 1>), dim3(g), blk, 0, s, b);
   } else if (t64 >= 192) {

@@ -7,6 +7,7 @@
 #include "../humanoid-walking-with-sac_amd/csrc/kernels.hip"
 #include <algorithm>
 #include <cstring>
+#include <cstdlib>
 #include <map>
 
 #include <cstdio>
@@ -175,7 +176,8 @@ static void occ_cfg(const char* name) {
 
 int main(int argc, char** argv) {
   const bool stamps = argc > 1 && std::string(argv[1]) == "stamps";
-  const int S = 376, A = 17, H = 512, B = 256;
+  const int S = 376, A = 17, H = 512;
+  const int B = getenv("SACMI_BENCH_B") ? atoi(getenv("SACMI_BENCH_B")) : 256;
   const int Kx = (S + 1 + A + 3) / 4 * 4, Hd = (H + 1 + 3) / 4 * 4, Kp1 = (S + 1 + 3) / 4 * 4;
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -298,6 +300,7 @@ int main(int argc, char** argv) {
         if (stamps) { printf("   <32,32,16,2,axk1>\n"); stamp_cfg<32, 32, 16, 2, 1, false, 1>(b, s); continue; }
 #endif
         printf("   <32,32,16,2,axk1> %7.2f us\n", time_cfg<32, 32, 16, 2, 1, false, 1>(b, iters, s));
+        printf("   <32x2,64,8,1,axk1> %7.2f us\n", time_cfg<32, 64, 8, 1, 2, false, 1>(b, iters, s));
         continue;
       }
 #ifdef SACMI_DIAG_STAMPS
