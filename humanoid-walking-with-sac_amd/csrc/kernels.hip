@@ -153,16 +153,42 @@ __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, in
   }
 }
 
-template <int MT, int NT>
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// 4 fp32 fragment values -> 4 bf16 (round to nearest even, v_cvt_pk_bf16_f32)
+__device__ __forceinline__ s4 to_bf16x4(const float (&v)[4]) {
+  const bf16x4 x = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  return __builtin_bit_cast(s4, x);
+}
+
+// One 16-deep K chunk.  fp32: 4 x v_mfma_f32_16x16x4_f32 (k-step s takes element s of
+// every lane's 4).  BF16: the same 4 consecutive k per lane are exactly the operand of
+// v_mfma_f32_16x16x16_bf16 (lane l holds A[l&15][4(l>>4) + j], B[4(l>>4) + j][l&15]), so
+// the chunk is ONE bf16 MFMA on the rounded fragments, fp32 accumulation, same C layout.
+template <int MT, int NT, bool BF16 = false>
 __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[MT][4],
                                            const float (&b)[NT][4]) {
+  if constexpr (BF16) {
+    s4 ab[MT], bb[NT];
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+    for (int i = 0; i < MT; ++i) ab[i] = to_bf16x4(a[i]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bb[j] = to_bf16x4(b[j]);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ab[i], bb[j], acc[i][j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+  }
 }
 
 // Each wave accumulates chunks wave, wave+KSPLIT, ... of a TM x TN tile and writes
@@ -179,7 +205,7 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // MFMAs: a(b,k) = A>0 ? coef[row]*w[k] : 0 with coef in LDS (coef[tile row]); with
 // store_a the transformed fragments are also written to d.ax_out.
 template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
-          int AXF = 0, class Pre, class Early = void (*)()>
+          int AXF = 0, bool BF16 = false, class Pre, class Early = void (*)()>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
                                             float* rsum, Pre&& pre, bool store_a = false,
                                             Early&& early = [] {}) {
@@ -273,7 +299,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
             for (int i = 0; i < MT; ++i) a[g][i][s] *= f;
           }
         }
-        mfma_chunk<MT, NT>(acc, a[g], b[g]);
+        mfma_chunk<MT, NT, BF16>(acc, a[g], b[g]);
         if (ROWSUM) {
 #pragma unroll
           for (int i = 0; i < MT; ++i) rs[i] += (a[g][i][0] + a[g][i][1]) + (a[g][i][2] + a[g][i][3]);
@@ -304,24 +330,23 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
 // layout dispatch (wave-uniform, once per workgroup)
 // AXK: whether this kernel instantiation carries the A-transform path (launch_gemm picks
 // the variant from the level's descs): 1 -> axk 1 descs, 0 -> none.
-template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, class Pre, class Early>
+template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, class Pre, class Early>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
                                           float* rsum, bool rowsum, Pre&& pre, Early&& early) {
   if constexpr (AXK == 1) {
     if (d.axk == 1) {        // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
-      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1>(d, m0, n0, red, rsum, pre,
-                                                               n0 == 0 && d.ax_out != nullptr,
-                                                               early);
+      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1, BF16>(
+          d, m0, n0, red, rsum, pre, n0 == 0 && d.ax_out != nullptr, early);
       return;
     }
   }
   if (d.a_kc) {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG>(d, m0, n0, red, rsum, pre);
-    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG>(d, m0, n0, red, rsum, pre);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
   } else {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG>(d, m0, n0, red, rsum, pre);
-    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG>(d, m0, n0, red, rsum, pre);
-    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG>(d, m0, n0, red, rsum, pre);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
+    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
   }
 }
 
@@ -544,8 +569,9 @@ template <int W>
 constexpr int gemm_min_waves() { return W >= 4 ? W / 4 : 1; }
 
 // TM x TN per wave group, MG wave groups (workgroup tile MG*TM x TN), K split KSPLIT
-// ways inside each group; ADAM: fused optimizer epilogue (every desc EPI_ADAM*)
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0>
+// ways inside each group; ADAM: fused optimizer epilogue (every desc EPI_ADAM*); BF16:
+// bf16 MFMA operands (GemmBatch::bf16), everything around them fp32
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false>
 __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
   constexpr int TMW = TM * MG;
   __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
@@ -661,7 +687,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
       }
     }
   };
-  gemm_core<TM, TN, KSPLIT, G, MG, AXK>(d, m0, n0, red, rsum, rowsum, pre, [] {});
+  gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
   if constexpr (AXK == 1) {
     // the row prologue, after the MFMAs: its loads went out first and have long landed
@@ -776,6 +802,13 @@ static int assign_tiles(GemmBatch& b) {
   return tot;
 }
 
+// one configuration, fp32 or bf16 MFMA operands (1024 threads)
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK>
+static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
+  if (b.bf16) hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, true>), dim3(grid), dim3(1024), 0, s, b);
+  else hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, false>), dim3(grid), dim3(1024), 0, s, b);
+}
+
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
@@ -792,31 +825,30 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   // (data-parallel) form of a level take the same tile geometry, so their bits agree
   bool dw = true;
   for (int i = 0; i < b.count; ++i) dw = dw && !b.d[i].a_kc && !b.d[i].b_kc;
-  const dim3 blk(1024);
   const int t64 = assign_tiles<32, 64>(b);
   if (dw && t64 <= 256) {
     // one 32x64 tile per CU (policy level): 16 waves, K split 16 ways
-    if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, true>), dim3(b.total_tiles + extra), blk, 0, s, b);
-    else hipLaunchKernelGGL((k_gemm<32, 64, 16, 1, 1, false>), dim3(b.total_tiles + extra), blk, 0, s, b);
+    if (n_adam) launch_k<32, 64, 16, 1, 1, true, 0>(b, b.total_tiles + extra, s);
+    else launch_k<32, 64, 16, 1, 1, false, 0>(b, b.total_tiles + extra, s);
   } else if (dw || n_adam || t64 > 512) {
     // more 32x64 tiles than CUs (the twin critic weight gradients; every level at large
     // batch): 64x64 tiles as two 32-row wave groups, each with an 8-way K split — half
     // the operand bytes per FLOP of a 32x64 tile; the epilogue state is prefetched under
     // the MFMAs
     const int g = assign_tiles<64, 64>(b) + extra;
-    if (n_adam) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, true>), dim3(g), blk, 0, s, b);
-    else if (axk == 1) hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false, 1>), dim3(g), blk, 0, s, b);
-    else hipLaunchKernelGGL((k_gemm<32, 64, 8, 1, 2, false>), dim3(g), blk, 0, s, b);
+    if (n_adam) launch_k<32, 64, 8, 1, 2, true, 0>(b, g, s);
+    else if (axk == 1) launch_k<32, 64, 8, 1, 2, false, 1>(b, g, s);
+    else launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
   } else if (axk == 1) {
     // dh1 / dha1 with the fc3 backward folded in (A transform, coefficient in the epilogue)
     const int g = assign_tiles<32, 32>(b) + extra;
-    hipLaunchKernelGGL((k_gemm<32, 32, 16, 2, 1, false, 1>), dim3(g), blk, 0, s, b);
+    launch_k<32, 32, 16, 2, 1, false, 1>(b, g, s);
   } else if (t64 >= 192) {
     // widest tile that still gives one workgroup to most CUs
-    hipLaunchKernelGGL((k_gemm<32, 64, 16, 2, 1, false>), dim3(b.total_tiles + extra), blk, 0, s, b);
+    launch_k<32, 64, 16, 2, 1, false, 0>(b, b.total_tiles + extra, s);
   } else {
     const int g = assign_tiles<32, 32>(b) + extra;
-    hipLaunchKernelGGL((k_gemm<32, 32, 16, 2, 1, false>), dim3(g), blk, 0, s, b);
+    launch_k<32, 32, 16, 2, 1, false, 0>(b, g, s);
   }
   HIP_LAUNCH_CHECK();
 }

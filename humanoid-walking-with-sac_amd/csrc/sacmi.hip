@@ -88,9 +88,11 @@ struct sacmi_ctx {
   bool keep_grads = false;             // SACMI_S_KEEP_GRADS
   int S = 0, A = 0, H = 0, Bm = 0;
   int Kx = 0, Hd = 0, Kp1 = 0, lddh = 0;
+  int nh = 2;                      // hidden layers per net (2: networks_model1, 3: model2)
+  bool bf16 = false;               // bf16 MFMA operands for the MLP GEMMs
   // layout
-  sacmi::Linear q_fc[2][3];        // [net][layer]
-  sacmi::Linear p_fc1, p_fc2, p_head;
+  sacmi::Linear q_fc[2][4];        // [net][layer]: layers 0..nh-1 hidden, nh the head
+  sacmi::Linear p_fc[3], p_head;   // policy hidden layers 0..nh-1, [mean | log_std]
   int64_t q_begin = 0, q_end = 0, pi_begin = 0, la_idx = 0, total = 0;
   // arenas
   sacmi::DevBuf<float> P, T, G, M, V;
@@ -103,10 +105,15 @@ struct sacmi_ctx {
   // scratch
   sacmi::DevBuf<int32_t> idx32, idx32b;   // b: second batch set (odd updates of a graph)
   sacmi::DevBuf<int64_t> idx64, idx64b;
-  sacmi::DevBuf<float> xq, x2, r, d, hp1, hp2, eps, cache, logp;
+  sacmi::DevBuf<float> xq, x2, r, d, eps, cache, logp;
   sacmi::DevBuf<float> xqb, x2b, rb, db;
-  sacmi::DevBuf<float> hq1, hq2, hqt1, hqt2, hqa1, hqa2;
-  sacmi::DevBuf<float> dq, dh2, dh1, dha1, dhead, dhp2, dhp1;
+  // hidden activations per layer: policy on [s2 ; s] (2B rows), the twin critics side by
+  // side (B rows x [q1 | q2], each Hd wide with the bias-1 column at H): critic on (s, a),
+  // target critics on (s2, a'), updated critics on (s, a~)
+  sacmi::DevBuf<float> hp[3], hq[3], hqt[3], hqa[3];
+  // backward: critic dh per hidden layer ([nh-1] = the on-the-fly head-layer rows u,
+  // stored for the weight gradient), actor-pass critic dh (layers 0..nh-2), policy dh
+  sacmi::DevBuf<float> dq, dhead, dhc[3], dha[3], dhp[3];
   sacmi::DevBuf<float> dotp;       // fc3 dot partials [6 slots][B][nparts]
   int nparts = 0;
   sacmi::DevBuf<float> lpart_c, lpart_a, ring, lp_part;
@@ -174,16 +181,18 @@ static void build_layout(sacmi_ctx* c) {
   c->q_begin = 0;
   take(c->q_fc[0][0], H, S + A, c->Kx, S, S, true);
   take(c->q_fc[1][0], H, S + A, c->Kx, S, S, false);   // adjacent: one K=2H dL/da GEMM
-  take(c->q_fc[0][1], H, H, c->Hd, H, H, true);
-  take(c->q_fc[1][1], H, H, c->Hd, H, H, true);
-  take(c->q_fc[0][2], 1, H, c->Hd, H, H, true);
-  take(c->q_fc[1][2], 1, H, c->Hd, H, H, true);
+  for (int l = 1; l < c->nh; ++l) {
+    take(c->q_fc[0][l], H, H, c->Hd, H, H, true);
+    take(c->q_fc[1][l], H, H, c->Hd, H, H, true);
+  }
+  take(c->q_fc[0][c->nh], 1, H, c->Hd, H, H, true);
+  take(c->q_fc[1][c->nh], 1, H, c->Hd, H, H, true);
   off = round_up64(off, 64);
   c->q_end = off;
   REQUIRE((c->q_end - c->q_begin) % 4 == 0 && c->q_begin % 4 == 0, SACMI_ESTATE, "critic region not float4-aligned");
   c->pi_begin = off;
-  take(c->p_fc1, H, S, c->Kp1, S, S, true);
-  take(c->p_fc2, H, H, c->Hd, H, H, true);
+  take(c->p_fc[0], H, S, c->Kp1, S, S, true);
+  for (int l = 1; l < c->nh; ++l) take(c->p_fc[l], H, H, c->Hd, H, H, true);
   take(c->p_head, 2 * A, H, c->Hd, H, H, true);
   off = round_up64(off, 64);
   c->la_idx = off;
@@ -199,15 +208,12 @@ static Linear head_part(const sacmi_ctx* c, int which /*0 mean 1 log_std*/) {
 
 static Linear find_linear(const sacmi_ctx* c, int net, int layer) {
   if (net == SACMI_POLICY) {
-    switch (layer) {
-      case 0: return c->p_fc1;
-      case 1: return c->p_fc2;
-      case 2: return head_part(c, 0);
-      case 3: return head_part(c, 1);
-    }
+    if (layer >= 0 && layer < c->nh) return c->p_fc[layer];
+    if (layer == c->nh) return head_part(c, 0);
+    if (layer == c->nh + 1) return head_part(c, 1);
   } else if (net >= SACMI_Q1 && net <= SACMI_Q2_TARGET) {
     const int q = (net == SACMI_Q1 || net == SACMI_Q1_TARGET) ? 0 : 1;
-    if (layer >= 0 && layer < 3) return c->q_fc[q][layer];
+    if (layer >= 0 && layer <= c->nh) return c->q_fc[q][layer];
   }
   throw Error{SACMI_EVALUE, "bad (net, layer)"};
 }
@@ -246,18 +252,21 @@ static void alloc_all(sacmi_ctx* c) {
   c->xq.alloc((size_t)Bm * c->Kx); c->xqb.alloc((size_t)Bm * c->Kx);
   c->x2.alloc((size_t)2 * Bm * c->Kx); c->x2b.alloc((size_t)2 * Bm * c->Kx);
   c->r.alloc(Bm); c->d.alloc(Bm); c->rb.alloc(Bm); c->db.alloc(Bm);
-  c->hp1.alloc((size_t)2 * Bm * c->Hd); c->hp2.alloc((size_t)2 * Bm * c->Hd);
+  const int nh = c->nh;
+  for (int l = 0; l < nh; ++l) {
+    c->hp[l].alloc((size_t)2 * Bm * c->Hd);
+    for (auto* b : {&c->hq[l], &c->hqt[l], &c->hqa[l]}) b->alloc((size_t)Bm * 2 * c->Hd);
+    c->dhc[l].alloc((size_t)Bm * 2 * H);
+    if (l < nh - 1) c->dha[l].alloc((size_t)Bm * 2 * H);
+    c->dhp[l].alloc((size_t)Bm * H);
+  }
   c->eps.alloc((size_t)2 * Bm * A);
   c->cache.alloc((size_t)2 * Bm * 3 * A);
   c->logp.alloc((size_t)2 * Bm);
-  for (auto* b : {&c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1, &c->hqa2})
-    b->alloc((size_t)Bm * 2 * c->Hd);
   c->dq.alloc((size_t)2 * Bm);
-  for (auto* b : {&c->dh2, &c->dh1, &c->dha1}) b->alloc((size_t)Bm * 2 * H);
   c->nparts = (H + 31) / 32;
   c->dotp.alloc((size_t)6 * Bm * c->nparts);
   c->dhead.alloc((size_t)Bm * c->lddh);
-  c->dhp2.alloc((size_t)Bm * H); c->dhp1.alloc((size_t)Bm * H);
   const int nrb = (Bm + 31) / 32;    // row blocks of the L5 / L9 tiling (loss partials)
   c->lpart_c.alloc((size_t)nrb * 2); c->lpart_a.alloc(nrb);
   c->lp_part.alloc((size_t)2 * ((2 * Bm + 15) / 16) + 2);   // heads: per-workgroup logp sums
@@ -267,11 +276,12 @@ static void alloc_all(sacmi_ctx* c) {
   launch_set_column(c->x2.p, 2 * Bm, c->Kx, S, 1.f, s);
   launch_set_column(c->xqb.p, Bm, c->Kx, S, 1.f, s);
   launch_set_column(c->x2b.p, 2 * Bm, c->Kx, S, 1.f, s);
-  launch_set_column(c->hp1.p, 2 * Bm, c->Hd, H, 1.f, s);
-  launch_set_column(c->hp2.p, 2 * Bm, c->Hd, H, 1.f, s);
-  for (auto* b : {&c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1, &c->hqa2}) {
-    launch_set_column(b->p, Bm, 2 * c->Hd, H, 1.f, s);
-    launch_set_column(b->p, Bm, 2 * c->Hd, c->Hd + H, 1.f, s);
+  for (int l = 0; l < nh; ++l) {
+    launch_set_column(c->hp[l].p, 2 * Bm, c->Hd, H, 1.f, s);
+    for (auto* b : {&c->hq[l], &c->hqt[l], &c->hqa[l]}) {
+      launch_set_column(b->p, Bm, 2 * c->Hd, H, 1.f, s);
+      launch_set_column(b->p, Bm, 2 * c->Hd, c->Hd + H, 1.f, s);
+    }
   }
   CHECK_HIP(hipStreamSynchronize(s));
 }
@@ -504,7 +514,12 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   };
   auto Wt = [&](const Linear& l) { return T + (l.off - c->q_begin); };
   auto dW = [&](const Linear& l) { return G + l.off; };
-  const Linear(&q)[2][3] = c->q_fc;
+  const Linear(&q)[2][4] = c->q_fc;
+  const int nh = c->nh, L = nh - 1;   // L: the last hidden layer (its head is layer nh)
+  auto run = [&](Level& lv, const std::string& name) {
+    lv.b.bf16 = c->bf16 ? 1 : 0;
+    if (mark(c, name.c_str(), level_flops(lv.b), level_bytes(lv.b))) launch_gemm(lv.b, s);
+  };
 
   if (phase_mask & 1) {
     const bool per = c->cfg.replay_kind == SACMI_REPLAY_PER;
@@ -519,20 +534,25 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
 
     // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
     Level l1;
-    l1.add(gd(bb.x2, Kx, 1, W(c->p_fc1), c->p_fc1.ld, 1, c->hp1.p, Hd, 2 * B, H, S + 1, EPI_RELU));
+    l1.add(gd(bb.x2, Kx, 1, W(c->p_fc[0]), c->p_fc[0].ld, 1, c->hp[0].p, Hd, 2 * B, H, S + 1, EPI_RELU));
     for (int i = 0; i < 2; ++i)
-      l1.add(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, c->hq1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    if (mark(c, "gemm_L1_fc1", level_flops(l1.b), level_bytes(l1.b))) launch_gemm(l1.b, s);
-    // L2
-    Level l2;
-    l2.add(gd_fwd_h(c->hp1.p, Hd, W(c->p_fc2), Hd, c->hp2.p, Hd, 2 * B, H, H));
-    for (int i = 0; i < 2; ++i)
-      l2.add(with_dot(gd_fwd_h(c->hq1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hq2.p + i * Hd, 2 * Hd, B, H, H),
-                      W(q[i][2]), i));
-    if (mark(c, "gemm_L2_fc2", level_flops(l2.b), level_bytes(l2.b))) launch_gemm(l2.b, s);
+      l1.add(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, c->hq[0].p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+    run(l1, "gemm_L1_fc1");
+    // L2 (.. L2b): the remaining hidden layers (K = H, bias in the epilogue); the last one
+    // also accumulates the critic head (fc3 / fc4) dot partials of q1 / q2 (slots 0 / 1)
+    for (int l = 1; l < nh; ++l) {
+      Level lv;
+      lv.add(gd_fwd_h(c->hp[l - 1].p, Hd, W(c->p_fc[l]), Hd, c->hp[l].p, Hd, 2 * B, H, H));
+      for (int i = 0; i < 2; ++i) {
+        GemmDesc g = gd_fwd_h(c->hq[l - 1].p + i * Hd, 2 * Hd, W(q[i][l]), Hd, c->hq[l].p + i * Hd,
+                              2 * Hd, B, H, H);
+        lv.add(l == L ? with_dot(g, W(q[i][nh]), i) : g);
+      }
+      run(lv, l == 1 ? "gemm_L2_fc2" : "gemm_L2b_fc3");
+    }
     // heads + sample for both stacks
     HeadSampleArgs hs{};
-    hs.h = c->hp2.p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
+    hs.h = c->hp[L].p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
     hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = dev_eps; hs.seed = c->cfg.seed;
     hs.sc = c->sc.p; hs.act = bb.x2 + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
     hs.cache = c->cache.p;
@@ -540,25 +560,33 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
     hs.logp_part = c->lp_part.p; hs.split_row = B;    // sums of log pi(a~|s) for dL/dlog_alpha
     if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) launch_heads_sample(hs, s);
-    // L3/L4: target critics on [s2|1|a']
-    Level l3, l4;
-    for (int i = 0; i < 2; ++i)
-      l3.add(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    if (mark(c, "gemm_L3_tgt_fc1", level_flops(l3.b), level_bytes(l3.b))) launch_gemm(l3.b, s);
-    for (int i = 0; i < 2; ++i)
-      l4.add(with_dot(gd_fwd_h(c->hqt1.p + i * Hd, 2 * Hd, Wt(q[i][1]), Hd, c->hqt2.p + i * Hd, 2 * Hd, B, H, H),
-                      Wt(q[i][2]), 2 + i));
-    if (mark(c, "gemm_L4_tgt_fc2", level_flops(l4.b), level_bytes(l4.b))) launch_gemm(l4.b, s);
-    // L5: dh1 = (dh2 W2) * relu'(h1), with the target / critic-loss rows folded in: the
-    // row prologue finishes q1, q2, qt1, qt2 from the dot partials of L2 / L4 and gives
-    // dq_i = 2 (q_i - q^) / B; the A operand dh2 = dq * w3 * [h2 > 0] is formed from h2 on
-    // the fly (and stored once by the column-tile-0 workgroups for L6's dW2)
+    // L3/L4 (.. L4b): target critics on [s2|1|a'] (head dot partials: slots 2 / 3)
+    {
+      Level l3;
+      for (int i = 0; i < 2; ++i)
+        l3.add(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt[0].p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+      run(l3, "gemm_L3_tgt_fc1");
+    }
+    for (int l = 1; l < nh; ++l) {
+      Level lv;
+      for (int i = 0; i < 2; ++i) {
+        GemmDesc g = gd_fwd_h(c->hqt[l - 1].p + i * Hd, 2 * Hd, Wt(q[i][l]), Hd, c->hqt[l].p + i * Hd,
+                              2 * Hd, B, H, H);
+        lv.add(l == L ? with_dot(g, Wt(q[i][nh]), 2 + i) : g);
+      }
+      run(lv, l == 1 ? "gemm_L4_tgt_fc2" : "gemm_L4b_tgt_fc3");
+    }
+    // L5: dh[L-1] = (dh[L] W[L]) * relu'(h[L-1]), with the target / critic-loss rows folded
+    // in: the row prologue finishes q1, q2, qt1, qt2 from the dot partials and gives
+    // dq_i = 2 (q_i - q^) / B; the A operand dh[L] = dq * w_head * [h[L] > 0] is formed
+    // from h[L] on the fly (its coefficient-free rows u stored once by the column-tile-0
+    // workgroups, for the weight gradient of layer L)
     const bool fuse = phase_mask == 7;     // single-GPU update: Adam in the dW epilogues
     Level l5;
     for (int i = 0; i < 2; ++i) {
-      GemmDesc g = gd(c->hq2.p + i * Hd, 2 * Hd, 1, W(q[i][1]), Hd, 0, c->dh1.p + i * H, 2 * H, B, H, H,
-                      EPI_MASK, c->hq1.p + i * Hd, 2 * Hd);
-      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][2]); g.ax_out = c->dh2.p + i * H; g.ax_ld = 2 * H;
+      GemmDesc g = gd(c->hq[L].p + i * Hd, 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dhc[L - 1].p + i * H, 2 * H,
+                      B, H, H, EPI_MASK, c->hq[L - 1].p + i * Hd, 2 * Hd);
+      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]); g.ax_out = c->dhc[L].p + i * H; g.ax_ld = 2 * H;
       l5.add(g);
     }
     {
@@ -568,29 +596,38 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       rf.gamma = (float)c->cfg.gamma;
       rf.sc = c->sc.p; rf.dq = c->dq.p; rf.loss_part = c->lpart_c.p;
     }
-    // weight gradients of the critics: into the gradient arena, or (fused) straight into
-    // Adam + Polyak on the parameters.  W2 is read by dh1 above, so every critic dW goes
-    // to L6 — in both modes, so the reduction order (and the bits) are the same.
-    Level lw;
+    run(l5, "gemm_L5_critic_dh1");
+    // L5b (3 hidden layers): dh[l-1] = (dh[l] W[l]) * relu'(h[l-1]) down to dh[0]
+    for (int l = L - 1; l >= 1; --l) {
+      Level lv;
+      for (int i = 0; i < 2; ++i)
+        lv.add(gd(c->dhc[l].p + i * H, 2 * H, 1, W(q[i][l]), Hd, 0, c->dhc[l - 1].p + i * H, 2 * H,
+                  B, H, H, EPI_MASK, c->hq[l - 1].p + i * Hd, 2 * Hd));
+      run(lv, "gemm_L5b_critic_dh");
+    }
+    // L6: every critic weight gradient: into the gradient arena, or (fused) straight into
+    // Adam + Polyak on the parameters.  The hidden weights are read by the dh levels
+    // above, so every critic dW runs here — in both modes, so the reduction order (and
+    // the bits) are the same.
     auto dst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
     const int wepi = fuse ? EPI_ADAM_POLYAK : EPI_STORE;
-    for (int i = 0; i < 2; ++i) {
-      // L5 stores u = dh2 / coef (the coefficient factored out of its dh1 rows): the
-      // fc2 weight gradient applies coef = dL/dq_i (dq) as a per-batch-row K-scale
-      GemmDesc w2 = gd_dw_h(c->dh2.p + i * H, 2 * H, c->hq1.p + i * Hd, 2 * Hd, dst(q[i][1]), Hd,
-                            H, H, B, wepi, 1 + i);
-      w2.a_ksc = c->dq.p + i * B;
-      lw.add(w2);
-      lw.add(gd_dw_h(c->dq.p + i * B, 1, c->hq2.p + i * Hd, 2 * Hd, dst(q[i][2]), Hd, 1, H, B,
-                     wepi, 1 + i));
-    }
-    if (mark(c, "gemm_L5_critic_dh1", level_flops(l5.b), level_bytes(l5.b))) launch_gemm(l5.b, s);
-    // L6: dW1~ (+ dW2~, dW3~ and Adam/Polyak/q-loss when fused)
     Level l6;
     for (int i = 0; i < 2; ++i)
-      l6.add(gd(c->dh1.p + i * H, 2 * H, 0, bb.xq, Kx, 0, dst(q[i][0]), Kx, H, S + A + 1, B,
+      l6.add(gd(c->dhc[0].p + i * H, 2 * H, 0, bb.xq, Kx, 0, dst(q[i][0]), Kx, H, S + A + 1, B,
                 wepi, nullptr, 0, 1 + i));
-    for (int i = 0; i < lw.b.count; ++i) l6.add(lw.b.d[i]);
+    for (int i = 0; i < 2; ++i) {
+      for (int l = 1; l < L; ++l)
+        l6.add(gd_dw_h(c->dhc[l].p + i * H, 2 * H, c->hq[l - 1].p + i * Hd, 2 * Hd, dst(q[i][l]), Hd,
+                       H, H, B, wepi, 1 + i));
+      // L5 stored u = dh[L] / coef (the coefficient factored out of its rows): the layer-L
+      // weight gradient applies coef = dL/dq_i (dq) as a per-batch-row K-scale
+      GemmDesc wl = gd_dw_h(c->dhc[L].p + i * H, 2 * H, c->hq[L - 1].p + i * Hd, 2 * Hd, dst(q[i][L]),
+                            Hd, H, H, B, wepi, 1 + i);
+      wl.a_ksc = c->dq.p + i * B;
+      l6.add(wl);
+      l6.add(gd_dw_h(c->dq.p + i * B, 1, c->hq[L].p + i * Hd, 2 * Hd, dst(q[i][nh]), Hd, 1, H, B,
+                     wepi, 1 + i));
+    }
     if (fuse) {
       AdamFuse& f = l6.b.adam;
       l6.b.has_adam = 1;
@@ -601,7 +638,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.loss_part = c->lpart_c.p; f.n_part = nb; f.loss_slot0 = 0; f.n_losses = 2;
       f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
     }
-    if (mark(c, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1", level_flops(l6.b), level_bytes(l6.b))) launch_gemm(l6.b, s);
+    run(l6, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1");
   }
   const float lr = (float)c->cfg.lr;
   if (phase_mask & 2) {
@@ -611,7 +648,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     AdamArgs ad{};
     ad.p = P; ad.g = G; ad.m = c->M.p; ad.v = c->V.p; ad.tgt = c->T.p; ad.tgt_base = c->q_begin;
     ad.nseg = 0;
-    for (int layer = 0; layer < 3; ++layer)
+    for (int layer = 0; layer <= nh; ++layer)
       for (int i = 0; i < 2; ++i) {
         const Linear& l = q[i][layer];
         REQUIRE(ad.nseg < kMaxAdamSegs, SACMI_ESTATE, "too many Adam segments");
@@ -628,24 +665,31 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.loss_div = (float)B; ad.log_alpha_idx = -1; ad.auto_entropy = 0;
     if (mark(c, "adam_critic_polyak")) launch_adam(ad, s);
    }
-    // L7/L8: updated critics on [s|1|a~]
+    // L7/L8 (.. L8b): updated critics on [s|1|a~] (head dot partials: slots 4 / 5)
     const float* xa = bb.x2 + (size_t)B * Kx;
-    Level l7, l8;
-    for (int i = 0; i < 2; ++i)
-      l7.add(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, c->hqa1.p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
-    if (mark(c, "gemm_L7_act_fc1", level_flops(l7.b), level_bytes(l7.b))) launch_gemm(l7.b, s);
-    for (int i = 0; i < 2; ++i)
-      l8.add(with_dot(gd_fwd_h(c->hqa1.p + i * Hd, 2 * Hd, W(q[i][1]), Hd, c->hqa2.p + i * Hd, 2 * Hd, B, H, H),
-                      W(q[i][2]), 4 + i));
-    if (mark(c, "gemm_L8_act_fc2", level_flops(l8.b), level_bytes(l8.b))) launch_gemm(l8.b, s);
-    // L9: dha1 = (dha2 W2) * relu'(ha1), with the actor rows folded in: the prologue
-    // finishes qa1, qa2 (L8's dot partials), min (ties 1/2 : 1/2), policy-loss partials,
-    // step counters; dha2 = dqa * w3 * [ha2 > 0] is formed from ha2 on the fly
+    {
+      Level l7;
+      for (int i = 0; i < 2; ++i)
+        l7.add(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, c->hqa[0].p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+      run(l7, "gemm_L7_act_fc1");
+    }
+    for (int l = 1; l < nh; ++l) {
+      Level lv;
+      for (int i = 0; i < 2; ++i) {
+        GemmDesc g = gd_fwd_h(c->hqa[l - 1].p + i * Hd, 2 * Hd, W(q[i][l]), Hd, c->hqa[l].p + i * Hd,
+                              2 * Hd, B, H, H);
+        lv.add(l == L ? with_dot(g, W(q[i][nh]), 4 + i) : g);
+      }
+      run(lv, l == 1 ? "gemm_L8_act_fc2" : "gemm_L8b_act_fc3");
+    }
+    // L9: dha[L-1] = (dha[L] W[L]) * relu'(ha[L-1]), with the actor rows folded in: the
+    // prologue finishes qa1, qa2 (dot partials), min (ties 1/2 : 1/2), policy-loss
+    // partials, step counters; dha[L] = dqa * w_head * [ha[L] > 0] is formed on the fly
     Level l9;
     for (int i = 0; i < 2; ++i) {
-      GemmDesc g = gd(c->hqa2.p + i * Hd, 2 * Hd, 1, W(q[i][1]), Hd, 0, c->dha1.p + i * H, 2 * H, B, H, H,
-                      EPI_MASK, c->hqa1.p + i * Hd, 2 * Hd);
-      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][2]);
+      GemmDesc g = gd(c->hqa[L].p + i * Hd, 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dha[L - 1].p + i * H, 2 * H,
+                      B, H, H, EPI_MASK, c->hqa[L - 1].p + i * Hd, 2 * Hd);
+      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]);
       l9.add(g);
     }
     {
@@ -657,33 +701,44 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
         rf.target_entropy = (float)(-A);
       }
     }
-    if (mark(c, "gemm_L9_act_dh1", level_flops(l9.b), level_bytes(l9.b))) launch_gemm(l9.b, s);
+    run(l9, "gemm_L9_act_dh1");
+    for (int l = L - 1; l >= 1; --l) {
+      Level lv;
+      for (int i = 0; i < 2; ++i)
+        lv.add(gd(c->dha[l].p + i * H, 2 * H, 1, W(q[i][l]), Hd, 0, c->dha[l - 1].p + i * H, 2 * H,
+                  B, H, H, EPI_MASK, c->hqa[l - 1].p + i * Hd, 2 * Hd));
+      run(lv, "gemm_L9b_act_dh");
+    }
     // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
-    GemmDesc da = gd(c->dha1.p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
+    GemmDesc da = gd(c->dha[0].p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
     validate(da);
-    // ... and, for the same rows, dhp2 = (dhead Whead) * relu'(hp2) (policy heads backward)
-    const float* hp2a = c->hp2.p + (size_t)B * Hd;
-    const float* hp1a = c->hp1.p + (size_t)B * Hd;
+    // ... and, for the same rows, dhp[L] = (dhead Whead) * relu'(hp[L]) (policy heads backward)
+    auto hpa = [&](int l) { return c->hp[l].p + (size_t)B * Hd; };   // actor rows
     SampleBwdArgs sb{};
     sb.cache = c->cache.p + (size_t)B * 3 * A; sb.eps = c->eps.p + (size_t)B * A;
     sb.dhead = c->dhead.p; sb.lddh = c->lddh; sb.A = A; sb.B = B; sb.sc = c->sc.p;
     sb.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
-    sb.Wh = W(c->p_head); sb.ldw = Hd; sb.H = H; sb.hp2 = hp2a; sb.ldh = Hd; sb.dhp2 = c->dhp2.p;
+    sb.Wh = W(c->p_head); sb.ldw = Hd; sb.H = H; sb.hp2 = hpa(L); sb.ldh = Hd; sb.dhp2 = c->dhp[L].p;
     check_span(sb.dhp2, (int64_t)B * H - 1, "dhp2");
     check_span(sb.Wh, (int64_t)(2 * A - 1) * Hd + H - 1, "Whead");
     if (mark(c, "gemm_L10_dlda_sample_bwd_dhp2", 2.0 * B * A * (2.0 * H) + 2.0 * B * (2.0 * A) * H))
       launch_gemm_sample_bwd(da, sb, s);
-    // L12: dhp1 = (dhp2 W2pi) * relu'(hp1);
+    // L11 (3 hidden layers) .. L12: dhp[l-1] = (dhp[l] Wpi[l]) * relu'(hp[l-1]);
     // L13: every policy dW (+ Adam, alpha step, policy loss, loss ring when fused)
     auto pdst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
     const int pepi = fuse ? EPI_ADAM : EPI_STORE;
+    for (int l = L; l >= 2; --l) {
+      Level lv;
+      lv.add(gd(c->dhp[l].p, H, 1, W(c->p_fc[l]), Hd, 0, c->dhp[l - 1].p, H, B, H, H, EPI_MASK, hpa(l - 1), Hd));
+      run(lv, "gemm_L11_pi_dhp");
+    }
     Level l12, l13;
-    GemmDesc dwh = gd_dw_h(c->dhead.p, c->lddh, hp2a, Hd, pdst(c->p_head), Hd, 2 * A, H, B, pepi, 0);
-    l12.add(gd(c->dhp2.p, H, 1, W(c->p_fc2), Hd, 0, c->dhp1.p, H, B, H, H, EPI_MASK, hp1a, Hd));
-    GemmDesc dw2 = gd_dw_h(c->dhp2.p, H, hp1a, Hd, pdst(c->p_fc2), Hd, H, H, B, pepi, 0);
-    l13.add(dwh);      // same level structure fused or not: identical reduction order
-    l13.add(dw2);
-    l13.add(gd(c->dhp1.p, H, 0, xa, Kx, 0, pdst(c->p_fc1), c->p_fc1.ld, H, S + 1, B, pepi));
+    l12.add(gd(c->dhp[1].p, H, 1, W(c->p_fc[1]), Hd, 0, c->dhp[0].p, H, B, H, H, EPI_MASK, hpa(0), Hd));
+    // same level structure fused or not: identical reduction order
+    l13.add(gd_dw_h(c->dhead.p, c->lddh, hpa(L), Hd, pdst(c->p_head), Hd, 2 * A, H, B, pepi, 0));
+    for (int l = L; l >= 1; --l)
+      l13.add(gd_dw_h(c->dhp[l].p, H, hpa(l - 1), Hd, pdst(c->p_fc[l]), Hd, H, H, B, pepi, 0));
+    l13.add(gd(c->dhp[0].p, H, 0, xa, Kx, 0, pdst(c->p_fc[0]), c->p_fc[0].ld, H, S + 1, B, pepi));
     if (fuse) {
       AdamFuse& f = l13.b.adam;
       l13.b.has_adam = 1;
@@ -706,15 +761,17 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l13.b.ride.kind = 2; l13.b.ride.nblocks = 16;
       l13.b.ride.ga = gather_args(c, B, nb2, false);
     }
-    if (mark(c, "gemm_L12_pi_dhp1", level_flops(l12.b), level_bytes(l12.b))) launch_gemm(l12.b, s);
-    if (mark(c, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1", level_flops(l13.b), level_bytes(l13.b))) launch_gemm(l13.b, s);
+    run(l12, "gemm_L12_pi_dhp1");
+    run(l13, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1");
   }
   if ((phase_mask & 4) && phase_mask != 7) {
     AdamArgs ad{};
     ad.p = P; ad.g = G; ad.m = c->M.p; ad.v = c->V.p; ad.tgt = nullptr;
     ad.nseg = 0;
-    for (const Linear* l : {&c->p_fc1, &c->p_fc2, &c->p_head})
-      ad.seg[ad.nseg++] = AdamSeg{l->off, l->numel_padded(), 0};
+    for (int l = 0; l <= nh; ++l) {
+      const Linear& lin = l < nh ? c->p_fc[l] : c->p_head;
+      ad.seg[ad.nseg++] = AdamSeg{lin.off, lin.numel_padded(), 0};
+    }
     ad.total = 0;
     for (int i = 0; i < ad.nseg; ++i) {
       REQUIRE(ad.seg[i].n % 4 == 0 && ad.seg[i].off % 4 == 0, SACMI_ESTATE, "Adam segment not float4-aligned");
@@ -841,6 +898,10 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
     REQUIRE(cfg->hidden_dim <= 1020, SACMI_EVALUE, "hidden_dim must be <= 1020 (one wave holds a hidden row)");
     REQUIRE(cfg->max_batch > 0 && cfg->max_batch <= 65536, SACMI_EVALUE, "bad max_batch");
     REQUIRE(cfg->capacity > 0 && cfg->capacity < (int64_t)1 << 31, SACMI_EVALUE, "bad capacity");
+    REQUIRE(cfg->n_hidden == 0 || cfg->n_hidden == 2 || cfg->n_hidden == 3, SACMI_EVALUE,
+            "n_hidden must be 2 (networks_model1) or 3 (networks_model2)");
+    REQUIRE(cfg->compute_dtype == SACMI_COMPUTE_FP32 || cfg->compute_dtype == SACMI_COMPUTE_BF16,
+            SACMI_EVALUE, "compute_dtype must be SACMI_COMPUTE_FP32 or SACMI_COMPUTE_BF16");
     int ndev = 0;
     CHECK_HIP(hipGetDeviceCount(&ndev));
     REQUIRE(device >= 0 && device < ndev, SACMI_EDEVICE, "no such HIP device");
@@ -849,6 +910,8 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
     c->cfg = *cfg;
     c->device = device;
     c->S = cfg->state_dim; c->A = cfg->action_dim; c->H = cfg->hidden_dim; c->Bm = cfg->max_batch;
+    c->nh = cfg->n_hidden == 0 ? 2 : cfg->n_hidden;
+    c->bf16 = cfg->compute_dtype == SACMI_COMPUTE_BF16;
     c->capacity = cfg->capacity;
     CHECK_HIP(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
@@ -889,13 +952,14 @@ int sacmi_destroy(sacmi_ctx* c) {
     }
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
                     &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->xqb, &c->x2b, &c->rb,
-                    &c->db, &c->hp1, &c->hp2, &c->eps,
-                    &c->cache, &c->logp, &c->hq1, &c->hq2, &c->hqt1, &c->hqt2, &c->hqa1,
-                    &c->hqa2, &c->dq, &c->dh2, &c->dh1, &c->dotp, &c->dha1, &c->dhead, &c->dhp2,
-                    &c->dhp1, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
+                    &c->db, &c->eps,
+                    &c->cache, &c->logp, &c->dq, &c->dotp, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
                     &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr, &c->per_probs,
                     &c->per_chunk, &c->per_w, &c->per_val})
       b->release();
+    for (int l = 0; l < 3; ++l)
+      for (auto* b : {&c->hp[l], &c->hq[l], &c->hqt[l], &c->hqa[l], &c->dhc[l], &c->dha[l], &c->dhp[l]})
+        b->release();
     c->sc.release(); c->mt.release(); c->idx32.release(); c->idx64.release();
     c->idx32b.release(); c->idx64b.release();
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
@@ -1424,13 +1488,18 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
                                hipMemcpyHostToDevice, s));
     if (eps && !deterministic)
       CHECK_HIP(hipMemcpyAsync(c->eps.p, eps, (size_t)n * A * 4, hipMemcpyHostToDevice, s));
-    Level l1, l2;
-    l1.add(gd(c->x2.p, Kx, 1, c->P.p + c->p_fc1.off, c->p_fc1.ld, 1, c->hp1.p, Hd, n, H, S + 1, EPI_RELU));
+    Level l1;
+    l1.add(gd(c->x2.p, Kx, 1, c->P.p + c->p_fc[0].off, c->p_fc[0].ld, 1, c->hp[0].p, Hd, n, H, S + 1, EPI_RELU));
+    l1.b.bf16 = c->bf16;
     launch_gemm(l1.b, s);
-    l2.add(gd_fwd_h(c->hp1.p, Hd, c->P.p + c->p_fc2.off, Hd, c->hp2.p, Hd, n, H, H));
-    launch_gemm(l2.b, s);
+    for (int l = 1; l < c->nh; ++l) {
+      Level lv;
+      lv.add(gd_fwd_h(c->hp[l - 1].p, Hd, c->P.p + c->p_fc[l].off, Hd, c->hp[l].p, Hd, n, H, H));
+      lv.b.bf16 = c->bf16;
+      launch_gemm(lv.b, s);
+    }
     HeadSampleArgs hs{};
-    hs.h = c->hp2.p; hs.Wh = c->P.p + c->p_head.off; hs.rows = n; hs.A = A; hs.K = H;
+    hs.h = c->hp[c->nh - 1].p; hs.Wh = c->P.p + c->p_head.off; hs.rows = n; hs.A = A; hs.K = H;
     hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = eps ? 0 : 1; hs.seed = c->cfg.seed;
     hs.sc = c->sc.p; hs.act = c->x2.p + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
     hs.cache = c->cache.p;

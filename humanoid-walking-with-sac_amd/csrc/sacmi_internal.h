@@ -191,6 +191,7 @@ struct GemmBatch {
   int has_adam;
   RideAlong ride;      // extra workgroups after the tiles
   RowsFuse rows;       // prologue for axk-1 descs
+  int bf16;            // 1: bf16 MFMA operands (fp32 loads rounded to bf16 in registers)
 };
 
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked

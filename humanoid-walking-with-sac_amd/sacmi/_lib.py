@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsacmi.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_f32p = ctypes.POINTER(ctypes.c_float)
 c_f64p = ctypes.POINTER(ctypes.c_double)
@@ -30,6 +30,7 @@ c_vp = ctypes.c_void_p
 
 SACMI_OK, SACMI_EVALUE, SACMI_ESTATE, SACMI_EDEVICE, SACMI_ENAN = range(5)
 REPLAY_UNIFORM, REPLAY_PER = 0, 1
+COMPUTE_FP32, COMPUTE_BF16 = 0, 1
 POLICY, Q1, Q2, Q1_TARGET, Q2_TARGET = range(5)
 SLOT_PARAM, SLOT_GRAD, SLOT_ADAM_M, SLOT_ADAM_V = range(4)
 (S_LOG_ALPHA, S_ALPHA, S_ALPHA_IS_TENSOR, S_STEP_POLICY, S_STEP_Q1, S_STEP_Q2, S_STEP_ALPHA,
@@ -47,6 +48,7 @@ class SacmiConfig(ctypes.Structure):
         ("action_high", ctypes.c_double), ("capacity", ctypes.c_int64),
         ("per_alpha", ctypes.c_double), ("per_beta_start", ctypes.c_double),
         ("per_beta_frames", ctypes.c_double), ("seed", ctypes.c_uint64),
+        ("n_hidden", ctypes.c_int32), ("compute_dtype", ctypes.c_int32),
     ]
 
 

@@ -20,7 +20,7 @@ import torch
 
 from . import _lib as L
 from .core import Config, Context, net_keys
-from .networks import GaussianPolicy, QNetwork
+from .networks import MODELS
 from .replay import ReplayBuffer
 
 _OPT_NETS = ("policy", "q1", "q2")
@@ -67,7 +67,7 @@ class _AdamMirror(torch.optim.Adam):
             return
         m = ctx.get_net(self._net, "m")
         v = ctx.get_net(self._net, "v")
-        for p, (key, _l, _p) in zip(self._tensors(), net_keys(self._net)):
+        for p, (key, _l, _p) in zip(self._tensors(), net_keys(self._net, self._agent._cfg.n_hidden)):
             self.state[p] = {"step": torch.tensor(float(step)),
                              "exp_avg": torch.from_numpy(m[key].reshape(p.shape)).clone(),
                              "exp_avg_sq": torch.from_numpy(v[key].reshape(p.shape)).clone()}
@@ -86,7 +86,7 @@ class _AdamMirror(torch.optim.Adam):
         which = {"policy": L.S_STEP_POLICY, "q1": L.S_STEP_Q1, "q2": L.S_STEP_Q2}[self._net]
         ctx.set_scalar(which, step)
         if st and st[0]:
-            keys = [k for k, _l, _p in net_keys(self._net)]
+            keys = [k for k, _l, _p in net_keys(self._net, self._agent._cfg.n_hidden)]
             ctx.set_net(self._net, {k: s["exp_avg"].numpy() for k, s in zip(keys, st)}, "m")
             ctx.set_net(self._net, {k: s["exp_avg_sq"].numpy() for k, s in zip(keys, st)}, "v")
 
@@ -109,13 +109,22 @@ class SAC:
     def __init__(self, state_dim, action_dim, hidden_dim=256, gamma=0.99, tau=0.005, lr=3e-4,
                  alpha=0.2, automatic_entropy_tuning=True, device=None, *,
                  capacity: int = 1000000, max_batch: int = 4096, action_bounds=None,
-                 seed: int | None = None, sync_python_random: bool = False):
+                 seed: int | None = None, sync_python_random: bool = False,
+                 networks: str = "model1", compute_dtype: str = "fp32"):
+        """``networks``: "model1" (networks_model1, the reference's import at
+        sac_imp.py:4) or "model2" (networks_model2: three hidden layers, orthogonal
+        policy init — the swap the reference makes by editing that import).
+        ``compute_dtype``: "fp32" (the reference's arithmetic) or "bf16" (bf16 MFMA
+        operands with fp32 accumulation, fp32 master weights / Adam / losses)."""
+        if networks not in MODELS:
+            raise ValueError(f"networks must be one of {sorted(MODELS)}")
+        QNetwork, GaussianPolicy = MODELS[networks]
         self.gamma = gamma
         self.tau = tau
         self.device = device if device is not None else "cuda"
         self.automatic_entropy_tuning = automatic_entropy_tuning
         # host mirrors, built exactly in the reference's order (sac_imp.py:28-36)
-        policy = GaussianPolicy(state_dim, action_dim, hidden_dim, action_bounds)
+        policy = GaussianPolicy(state_dim, action_dim, hidden_dim, action_bounds=action_bounds)
         q1 = QNetwork(state_dim, action_dim, hidden_dim)
         q2 = QNetwork(state_dim, action_dim, hidden_dim)
         q1_target = QNetwork(state_dim, action_dim, hidden_dim)
@@ -128,7 +137,8 @@ class SAC:
         self._cfg = Config(state_dim, action_dim, hidden_dim, max_batch=max_batch, gamma=gamma,
                            tau=tau, lr=lr, alpha=float(alpha),
                            automatic_entropy_tuning=automatic_entropy_tuning,
-                           action_low=lo, action_high=hi, capacity=capacity, seed=seed)
+                           action_low=lo, action_high=hi, capacity=capacity, seed=seed,
+                           n_hidden=QNetwork.n_hidden, compute_dtype=compute_dtype)
         self._ctx = Context(self._cfg, _device_index(device))
         self._mods = {"policy": policy, "q1": q1, "q2": q2, "q1_target": q1_target,
                       "q2_target": q2_target}

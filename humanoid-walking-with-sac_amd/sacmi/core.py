@@ -11,15 +11,19 @@ from . import _lib as L
 
 NET_IDS = {"policy": L.POLICY, "q1": L.Q1, "q2": L.Q2, "q1_target": L.Q1_TARGET,
            "q2_target": L.Q2_TARGET}
-# state_dict key -> (layer, part)
-POLICY_LAYERS = {"fc1": 0, "fc2": 1, "mean": 2, "log_std": 3}
-Q_LAYERS = {"fc1": 0, "fc2": 1, "fc3": 2}
 SLOTS = {"param": L.SLOT_PARAM, "grad": L.SLOT_GRAD, "m": L.SLOT_ADAM_M, "v": L.SLOT_ADAM_V}
+COMPUTE_DTYPES = {"fp32": L.COMPUTE_FP32, "bf16": L.COMPUTE_BF16}
 
 
-def net_keys(net: str):
-    layers = POLICY_LAYERS if net == "policy" else Q_LAYERS
-    for name, layer in layers.items():
+def layer_names(net: str, n_hidden: int = 2):
+    """state_dict layer names in layer-index order: networks_model1.py:14-17,46-50
+    (n_hidden=2), networks_model2.py:23-27,57-62 (n_hidden=3)."""
+    hid = [f"fc{i}" for i in range(1, n_hidden + 1)]
+    return hid + (["mean", "log_std"] if net == "policy" else [f"fc{n_hidden + 1}"])
+
+
+def net_keys(net: str, n_hidden: int = 2):
+    for layer, name in enumerate(layer_names(net, n_hidden)):
         yield f"{name}.weight", layer, 0
         yield f"{name}.bias", layer, 1
 
@@ -43,6 +47,8 @@ class Config:
     per_beta_start: float = 0.4
     per_beta_frames: float = 100000
     seed: int = 0
+    n_hidden: int = 2              # 2: networks_model1, 3: networks_model2
+    compute_dtype: str = "fp32"    # "fp32" | "bf16" (MLP GEMM operands; fp32 accumulate)
 
     def to_c(self) -> L.SacmiConfig:
         c = L.SacmiConfig()
@@ -56,6 +62,10 @@ class Config:
         c.per_alpha, c.per_beta_start = self.per_alpha, self.per_beta_start
         c.per_beta_frames = float(self.per_beta_frames)
         c.seed = int(self.seed) & ((1 << 64) - 1)
+        c.n_hidden = int(self.n_hidden)
+        if self.compute_dtype not in COMPUTE_DTYPES:
+            raise ValueError(f"compute_dtype must be one of {sorted(COMPUTE_DTYPES)}")
+        c.compute_dtype = COMPUTE_DTYPES[self.compute_dtype]
         return c
 
 
@@ -120,14 +130,14 @@ class Context:
 
     def get_net(self, net: str, slot: str = "param", shapes: dict | None = None) -> dict:
         out = {}
-        for key, layer, part in net_keys(net):
+        for key, layer, part in net_keys(net, self.cfg.n_hidden):
             n = self.numel(net, layer, part)
             shp = shapes[key] if shapes else (n,)
             out[key] = self.get_tensor(slot, net, layer, part, shp)
         return out
 
     def set_net(self, net: str, sd: dict, slot: str = "param") -> None:
-        for key, layer, part in net_keys(net):
+        for key, layer, part in net_keys(net, self.cfg.n_hidden):
             self.set_tensor(slot, net, layer, part, np.asarray(sd[key]))
 
     def get_scalar(self, which: int) -> float:

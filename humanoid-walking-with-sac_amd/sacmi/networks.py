@@ -1,4 +1,4 @@
-"""Host-side mirrors of the reference's networks (networks_model1.py).
+"""Host-side mirrors of the reference's networks (networks_model1.py, networks_model2.py).
 
 The device owns the live parameters (libsacmi arenas).  These torch modules exist for
 what the reference's users do with ``agent.policy`` / ``agent.q1`` ...:
@@ -26,6 +26,13 @@ def _xavier_zero(m: nn.Module) -> None:
     if isinstance(m, nn.Linear):
         nn.init.xavier_uniform_(m.weight)
         nn.init.constant_(m.bias, 0)
+
+
+def _orthogonal_zero(m: nn.Module) -> None:
+    """networks_model2.py:72-83 (the policy of model2)."""
+    if isinstance(m, nn.Linear):
+        nn.init.orthogonal_(m.weight, gain=1.0)
+        nn.init.constant_(m.bias, 0.0)
 
 
 class _DeviceMirror:
@@ -60,7 +67,18 @@ class _DeviceMirror:
         return out
 
 
-class QNetwork(_DeviceMirror, nn.Module):
+class _HiddenStack:
+    """forward through fc1..fc{n_hidden} with relu."""
+
+    n_hidden = 2
+
+    def _trunk(self, x):
+        for i in range(1, self.n_hidden + 1):
+            x = F.relu(getattr(self, f"fc{i}")(x))
+        return x
+
+
+class QNetwork(_HiddenStack, _DeviceMirror, nn.Module):
     """Q(s, a): cat -> Linear(S+A,H) relu -> Linear(H,H) relu -> Linear(H,1)."""
 
     def __init__(self, state_dim: int, action_dim: int, hidden_dim: int = 256):
@@ -71,11 +89,11 @@ class QNetwork(_DeviceMirror, nn.Module):
         self.apply(_xavier_zero)
 
     def forward(self, state, action):
-        h = F.relu(self.fc1(torch.cat([state, action], dim=-1)))
-        return self.fc3(F.relu(self.fc2(h)))
+        h = self._trunk(torch.cat([state, action], dim=-1))
+        return getattr(self, f"fc{self.n_hidden + 1}")(h)
 
 
-class GaussianPolicy(_DeviceMirror, nn.Module):
+class GaussianPolicy(_HiddenStack, _DeviceMirror, nn.Module):
     """tanh-squashed Gaussian policy with mean / log_std heads."""
 
     def __init__(self, state_dim: int, action_dim: int, hidden_dim: int = 256,
@@ -91,7 +109,7 @@ class GaussianPolicy(_DeviceMirror, nn.Module):
         self.apply(_xavier_zero)
 
     def forward(self, state):
-        h = F.relu(self.fc2(F.relu(self.fc1(state))))
+        h = self._trunk(state)
         return self.mean(h), torch.clamp(self.log_std(h), LOG_STD_MIN, LOG_STD_MAX)
 
     def sample(self, state):
@@ -102,3 +120,44 @@ class GaussianPolicy(_DeviceMirror, nn.Module):
         y = torch.tanh(x)
         logp = dist.log_prob(x) - torch.log(self.action_scale * (1 - y.pow(2)) + 1e-6)
         return y * self.action_scale + self.action_bias, logp.sum(dim=-1, keepdim=True)
+
+
+class QNetwork2(QNetwork):
+    """networks_model2.QNetwork (networks_model2.py:18-48): three hidden layers
+    fc1..fc3 and the head fc4, xavier-uniform weights, zero biases, default H=512."""
+
+    n_hidden = 3
+
+    def __init__(self, state_dim: int, action_dim: int, hidden_dim: int = 512):
+        nn.Module.__init__(self)
+        self.fc1 = nn.Linear(state_dim + action_dim, hidden_dim)
+        self.fc2 = nn.Linear(hidden_dim, hidden_dim)
+        self.fc3 = nn.Linear(hidden_dim, hidden_dim)
+        self.fc4 = nn.Linear(hidden_dim, 1)
+        self.apply(_xavier_zero)
+
+
+class GaussianPolicy2(GaussianPolicy):
+    """networks_model2.GaussianPolicy (networks_model2.py:51-120): fc1..fc3 + mean /
+    log_std heads, orthogonal weights (gain 1), zero biases, default H=512.  ``device``
+    is accepted for signature parity; the mirror stays on the host (the live weights are
+    in HBM)."""
+
+    n_hidden = 3
+
+    def __init__(self, state_dim: int, action_dim: int, hidden_dim: int = 512, device=None,
+                 action_bounds=None):
+        nn.Module.__init__(self)
+        self.device = device
+        self.fc1 = nn.Linear(state_dim, hidden_dim)
+        self.fc2 = nn.Linear(hidden_dim, hidden_dim)
+        self.fc3 = nn.Linear(hidden_dim, hidden_dim)
+        self.mean = nn.Linear(hidden_dim, action_dim)
+        self.log_std = nn.Linear(hidden_dim, action_dim)
+        lo, hi = action_bounds if action_bounds is not None else (-0.4, 0.4)
+        self.action_scale = (hi - lo) / 2
+        self.action_bias = (hi + lo) / 2
+        self.apply(_orthogonal_zero)
+
+
+MODELS = {"model1": (QNetwork, GaussianPolicy), "model2": (QNetwork2, GaussianPolicy2)}

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SACMI_ABI_VERSION 1
+#define SACMI_ABI_VERSION 2
 
 enum sacmi_status {
   SACMI_OK = 0,
@@ -49,6 +49,11 @@ enum sacmi_status {
 };
 
 enum sacmi_replay_kind { SACMI_REPLAY_UNIFORM = 0, SACMI_REPLAY_PER = 1 };
+
+/* arithmetic of the MLP GEMMs: fp32 (exact f32 MFMA, the reference's precision) or bf16
+ * (bf16 MFMA operands, fp32 accumulation; fp32 master weights, Adam, losses and row
+ * algebra) — BASELINE configs[4] */
+enum sacmi_compute_dtype { SACMI_COMPUTE_FP32 = 0, SACMI_COMPUTE_BF16 = 1 };
 
 typedef struct sacmi_config {
   int32_t state_dim;          /* S  (sac_imp.py:11)                               */
@@ -68,6 +73,10 @@ typedef struct sacmi_config {
   double per_beta_start;      /* 0.4                                             */
   double per_beta_frames;     /* 1e5                                             */
   uint64_t seed;              /* Philox seed for the policy noise (perf mode)     */
+  int32_t n_hidden;           /* hidden layers per net: 2 = networks_model1 (the  */
+                              /* reference's SAC, sac_imp.py:4), 3 = networks_model2 */
+                              /* (networks_model2.py:18-99); 0 means 2            */
+  int32_t compute_dtype;      /* sacmi_compute_dtype                              */
 } sacmi_config;
 
 typedef struct sacmi_ctx sacmi_ctx;
@@ -78,8 +87,10 @@ enum sacmi_net { SACMI_POLICY = 0, SACMI_Q1 = 1, SACMI_Q2 = 2, SACMI_Q1_TARGET =
                  SACMI_Q2_TARGET = 4 };
 enum sacmi_slot { SACMI_SLOT_PARAM = 0, SACMI_SLOT_GRAD = 1, SACMI_SLOT_ADAM_M = 2,
                   SACMI_SLOT_ADAM_V = 3 };
-/* layer index inside a net: policy {0: fc1, 1: fc2, 2: mean, 3: log_std};
- * q {0: fc1, 1: fc2, 2: fc3};  part: 0 = weight, 1 = bias. */
+/* layer index inside a net (n_hidden = 2): policy {0: fc1, 1: fc2, 2: mean, 3: log_std};
+ * q {0: fc1, 1: fc2, 2: fc3}.  n_hidden = 3 (networks_model2): policy {0: fc1, 1: fc2,
+ * 2: fc3, 3: mean, 4: log_std}; q {0: fc1, 1: fc2, 2: fc3, 3: fc4}.
+ * part: 0 = weight, 1 = bias. */
 
 /* scalar ids for get/set_scalar */
 enum sacmi_scalar {

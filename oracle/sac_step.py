@@ -10,7 +10,9 @@ high-precision truth the HIP path is graded against.
 Reference map
 -------------
 * QNetwork.forward            networks_model1.py:27-33   (cat -> fc1 relu fc2 relu fc3)
+                              networks_model2.py:37-48   (n_hidden=3: ... fc3 relu fc4)
 * GaussianPolicy.forward      networks_model1.py:65-76   (log_std clamp [-20, 2])
+                              networks_model2.py:86-99   (n_hidden=3: fc1 fc2 fc3, heads)
 * GaussianPolicy.sample       networks_model1.py:78-99   (rsample, tanh squash, log-prob)
 * SAC.update_parameters       sac_imp.py:74-144
 * SAC._soft_update_target...  sac_imp.py:146-152
@@ -34,6 +36,21 @@ import torch.nn.functional as F
 POLICY_KEYS = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias",
                "mean.weight", "mean.bias", "log_std.weight", "log_std.bias")
 Q_KEYS = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias", "fc3.weight", "fc3.bias")
+
+
+def policy_keys(n_hidden: int = 2) -> tuple:
+    """state_dict keys of GaussianPolicy: networks_model1.py:46-50 (2 hidden layers),
+    networks_model2.py:57-62 (3)."""
+    hid = tuple(f"fc{i}.{p}" for i in range(1, n_hidden + 1) for p in ("weight", "bias"))
+    return hid + POLICY_KEYS[4:]
+
+
+def q_keys(n_hidden: int = 2) -> tuple:
+    """state_dict keys of QNetwork: networks_model1.py:14-17 (fc1..fc3), model2 :23-27
+    (fc1..fc4)."""
+    return tuple(f"fc{i}.{p}" for i in range(1, n_hidden + 2) for p in ("weight", "bias"))
+
+
 NETS = ("policy", "q1", "q2", "q1_target", "q2_target")
 
 
@@ -49,6 +66,7 @@ class SacConfig:
     automatic_entropy_tuning: bool = True
     action_low: float = -0.4
     action_high: float = 0.4
+    n_hidden: int = 2          # 2: networks_model1 (the reference's SAC), 3: networks_model2
 
     @property
     def action_scale(self) -> float:   # networks_model1.py:54
@@ -60,18 +78,38 @@ class SacConfig:
 
 
 def param_shapes(cfg: SacConfig) -> dict:
-    S, A, H = cfg.state_dim, cfg.action_dim, cfg.hidden_dim
-    pol = {"fc1.weight": (H, S), "fc1.bias": (H,), "fc2.weight": (H, H), "fc2.bias": (H,),
-           "mean.weight": (A, H), "mean.bias": (A,), "log_std.weight": (A, H),
-           "log_std.bias": (A,)}
-    q = {"fc1.weight": (H, S + A), "fc1.bias": (H,), "fc2.weight": (H, H), "fc2.bias": (H,),
-         "fc3.weight": (1, H), "fc3.bias": (1,)}
+    S, A, H, nh = cfg.state_dim, cfg.action_dim, cfg.hidden_dim, cfg.n_hidden
+    pol = {"fc1.weight": (H, S), "fc1.bias": (H,)}
+    for i in range(2, nh + 1):
+        pol.update({f"fc{i}.weight": (H, H), f"fc{i}.bias": (H,)})
+    pol.update({"mean.weight": (A, H), "mean.bias": (A,), "log_std.weight": (A, H),
+                "log_std.bias": (A,)})
+    q = {"fc1.weight": (H, S + A), "fc1.bias": (H,)}
+    for i in range(2, nh + 1):
+        q.update({f"fc{i}.weight": (H, H), f"fc{i}.bias": (H,)})
+    q.update({f"fc{nh + 1}.weight": (1, H), f"fc{nh + 1}.bias": (1,)})
     return {"policy": pol, "q1": q, "q2": q, "q1_target": q, "q2_target": q}
+
+
+def orthogonal(rng, shape) -> np.ndarray:
+    """Portable stand-in for torch.nn.init.orthogonal_(w, gain=1) (networks_model2.py:82):
+    QR of a Gaussian matrix, sign-corrected by diag(R), rows orthonormal when out <= in
+    (columns otherwise)."""
+    rows, cols = shape
+    flat = rng.standard_normal((rows, cols))
+    if rows < cols:
+        flat = flat.T
+    q, r = np.linalg.qr(flat)
+    q *= np.sign(np.diag(r))
+    if rows < cols:
+        q = q.T
+    return q.astype(np.float32)
 
 
 def init_params(cfg: SacConfig, seed: int, bias_scale: float = 0.0) -> dict:
     """Portable (numpy PCG64) stand-in for the reference's xavier_uniform init
-    (networks_model1.py:22-25,60-63): W ~ U(-b, b), b = sqrt(6/(fan_in+fan_out)).
+    (networks_model1.py:22-25,60-63): W ~ U(-b, b), b = sqrt(6/(fan_in+fan_out));
+    with n_hidden=3 the policy weights are orthogonal (networks_model2.py:72-83).
     Biases are 0 as in the reference unless ``bias_scale`` > 0 (tests use non-zero
     biases so the bias gradients are exercised).  Targets copy q1/q2
     (sac_imp.py:33-36)."""
@@ -81,7 +119,9 @@ def init_params(cfg: SacConfig, seed: int, bias_scale: float = 0.0) -> dict:
     for net in ("policy", "q1", "q2"):
         d = {}
         for k, shp in shapes[net].items():
-            if k.endswith("weight"):
+            if k.endswith("weight") and net == "policy" and cfg.n_hidden == 3:
+                d[k] = orthogonal(rng, shp)
+            elif k.endswith("weight"):
                 b = math.sqrt(6.0 / (shp[0] + shp[1]))
                 d[k] = rng.uniform(-b, b, size=shp).astype(np.float32)
             else:
@@ -107,18 +147,70 @@ def synthetic_rows(cfg: SacConfig, n: int, seed: int, state_scale: float = 1.0):
 
 
 # ----------------------------------------------------------------------------
+def _n_hidden(p) -> int:
+    return sum(1 for k in p if k.startswith("fc") and k.endswith(".weight")) - (
+        0 if "mean.weight" in p else 1)
+
+
+# ----------------------------------------------------------------------------
+# bf16-operand emulation (test infrastructure for compute_dtype=bf16, which has no
+# reference counterpart: BASELINE configs[4]).  Where the HIP path feeds a GEMM's operands
+# to a bf16 MFMA, the emulation rounds them to bf16 (round-to-nearest-even) and multiplies
+# in the oracle's dtype; the GEMMs the HIP path keeps in fp32 (policy heads forward and
+# their dX, the critic head's forward dot and the dL/da product) stay unrounded.  Roles:
+#   in   first hidden layer: x = [input | 1] against [W | b] (bias folded into K, so
+#        rounded; dW's bias column is the sum of rounded dY); dX unrounded (dL/da)
+#   hid  later hidden layers: forward, dX and dW rounded; bias add / bias grad fp32
+#   head critic fc{n+1}: forward and dX unrounded (dot epilogue / row transform), dW
+#        rounded;  phead: policy mean / log_std, the same
+_ROUND = {"on": False}
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _EmuLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, role):
+        ctx.save_for_backward(x, w)
+        ctx.role = role
+        if role == "in":
+            return _bf(x) @ _bf(w).T + _bf(b)
+        if role == "hid":
+            return _bf(x) @ _bf(w).T + b
+        return x @ w.T + b
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        role = ctx.role
+        dx = _bf(g) @ _bf(w) if role == "hid" else g @ w
+        dw = _bf(g).T @ _bf(x)
+        db = _bf(g).sum(0) if role == "in" else g.sum(0)
+        return dx, dw, db, None
+
+
+def _lin(x, w, b, role):
+    if _ROUND["on"]:
+        return _EmuLinear.apply(x, w, b, role)
+    return F.linear(x, w, b)
+
+
 def _q_forward(p, state, action):
     x = torch.cat([state, action], dim=-1)
-    x = F.relu(F.linear(x, p["fc1.weight"], p["fc1.bias"]))
-    x = F.relu(F.linear(x, p["fc2.weight"], p["fc2.bias"]))
-    return F.linear(x, p["fc3.weight"], p["fc3.bias"])
+    nh = _n_hidden(p)
+    for i in range(1, nh + 1):
+        x = F.relu(_lin(x, p[f"fc{i}.weight"], p[f"fc{i}.bias"], "in" if i == 1 else "hid"))
+    return _lin(x, p[f"fc{nh + 1}.weight"], p[f"fc{nh + 1}.bias"], "head")
 
 
 def _policy_forward(p, state):
-    x = F.relu(F.linear(state, p["fc1.weight"], p["fc1.bias"]))
-    x = F.relu(F.linear(x, p["fc2.weight"], p["fc2.bias"]))
-    mean = F.linear(x, p["mean.weight"], p["mean.bias"])
-    log_std = F.linear(x, p["log_std.weight"], p["log_std.bias"])
+    x = state
+    for i in range(1, _n_hidden(p) + 1):
+        x = F.relu(_lin(x, p[f"fc{i}.weight"], p[f"fc{i}.bias"], "in" if i == 1 else "hid"))
+    mean = _lin(x, p["mean.weight"], p["mean.bias"], "head")
+    log_std = _lin(x, p["log_std.weight"], p["log_std.bias"], "head")
     return mean, torch.clamp(log_std, -20, 2)
 
 
@@ -159,7 +251,15 @@ class OracleSAC:
             self.opt["alpha"] = torch.optim.Adam([self.log_alpha], lr=lr)
         self.alpha = self.cfg.alpha                     # python float until 1st update
 
-    def step(self, s, a, r, s2, d, eps1, eps2) -> dict:
+    def step(self, s, a, r, s2, d, eps1, eps2, bf16_operands: bool = False) -> dict:
+        """``bf16_operands``: emulate compute_dtype=bf16 (see _EmuLinear)."""
+        _ROUND["on"] = bool(bf16_operands)
+        try:
+            return self._step(s, a, r, s2, d, eps1, eps2)
+        finally:
+            _ROUND["on"] = False
+
+    def _step(self, s, a, r, s2, d, eps1, eps2) -> dict:
         cfg, dt = self.cfg, self.dtype
         T = lambda x: torch.as_tensor(np.asarray(x, dtype=np.float32)).to(dt)
         state, action, next_state = T(s), T(a), T(s2)
@@ -200,7 +300,7 @@ class OracleSAC:
         with torch.no_grad():
             tau = cfg.tau
             for src, dst in (("q1", "q1_target"), ("q2", "q2_target")):
-                for k in Q_KEYS:
+                for k in q_keys(cfg.n_hidden):
                     t = self.nets[dst][k]
                     t.copy_(t * (1.0 - tau) + self.nets[src][k] * tau)
         self.last_grads = grads

@@ -68,7 +68,7 @@ def test_select_action_shapes_and_bounds():
     with torch.no_grad():   # evaluate: tanh(mean)*scale+bias on the CPU mirror
         mean, _ = agent.policy(torch.from_numpy(st).unsqueeze(0))
         ref = (torch.tanh(mean) * 0.4).numpy()[0]
-    np.testing.assert_allclose(det, ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(det, ref, rtol=1e-5, atol=1e-5)
     b = agent.select_action(np.zeros((7, S)))
     assert b.shape == (7, A)
 
@@ -147,3 +147,34 @@ def test_standalone_replay_buffer_is_random_sample():
     assert random.getstate() == mt.to_pystate()
     with pytest.raises(ValueError, match="Sample larger than population"):
         rb.sample(501)
+
+
+def test_model2_dropin_checkpoint_and_update(tmp_path, golden_dir):
+    """SAC(networks="model2"): the networks_model2 swap (sac_imp.py:4 import edited) —
+    init equals the reference's under the same torch seed, fc1..fc4 / fc1..fc3+heads
+    state dicts round-trip through the device, updates run."""
+    import os
+    from sac_imp import SAC
+    z = np.load(os.path.join(golden_dir, "init_seed3.npz"))
+    torch.manual_seed(3)
+    agent = SAC(24, 4, hidden_dim=64, device="cuda", capacity=5000, max_batch=256,
+                networks="model2")
+    for n in ("policy", "q1", "q2", "q1_target", "q2_target"):
+        live = agent._ctx.get_net(n)
+        for k, v in getattr(agent, n).state_dict().items():
+            # orthogonal_ runs a LAPACK QR: bitwise on the build host, ULP-level elsewhere
+            np.testing.assert_allclose(v.numpy(), z[f"m2_24_4_64.{n}.{k}"], rtol=1e-5, atol=1e-5)
+            assert np.array_equal(live[k].reshape(v.shape), v.numpy()), (n, k)
+    assert list(agent.q1.state_dict())[-2:] == ["fc4.weight", "fc4.bias"]
+    _fill(agent, 300)
+    h = agent.update_parameters(64)
+    assert all(np.isfinite(v) for v in h.values())
+    p = str(tmp_path / "m2.pt")
+    agent.save_checkpoint(p, 1, 300)
+    torch.manual_seed(4)
+    b = SAC(24, 4, hidden_dim=64, device="cuda", capacity=5000, max_batch=256, networks="model2")
+    b.load_checkpoint(p)
+    for n in ("policy", "q1_target"):
+        for k, v in getattr(agent, n).state_dict().items():
+            assert torch.equal(v, getattr(b, n).state_dict()[k]), (n, k)
+    assert np.isfinite(b.update_parameters(64)["q1_loss"])

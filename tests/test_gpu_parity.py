@@ -38,7 +38,8 @@ def make_ctx(cfg: SacConfig, max_batch, capacity, **kw):
     from sacmi import Config, Context
     c = Config(cfg.state_dim, cfg.action_dim, cfg.hidden_dim, max_batch=max_batch,
                gamma=cfg.gamma, tau=cfg.tau, lr=cfg.lr, alpha=cfg.alpha,
-               automatic_entropy_tuning=cfg.automatic_entropy_tuning, capacity=capacity, **kw)
+               automatic_entropy_tuning=cfg.automatic_entropy_tuning, capacity=capacity,
+               n_hidden=cfg.n_hidden, **kw)
     ctx = Context(c, 0)
     from sacmi import _lib as L
     ctx.set_scalar(L.S_KEEP_GRADS, 1)     # the tests compare gradients too
@@ -140,12 +141,14 @@ def test_step_humanoid_vs_oracle():
         assert abs(lg[i] - l64[k]) <= 1e-4 * max(abs(l64[k]), 1e-3), (k, lg[i], l64[k])
 
 
-def test_golden_small_two_steps_device_sampling(golden_dir):
+@pytest.mark.parametrize("fixture", ["step_small.npz", "step_model2.npz"])
+def test_golden_small_two_steps_device_sampling(golden_dir, fixture):
     """Indices drawn ON THE GPU from the reference's MT state reproduce the
-    reference's update (losses vs the reference's own fp32 outputs)."""
-    z = np.load(os.path.join(golden_dir, "step_small.npz"))
-    S, A, H, B, N = (int(x) for x in z["cfg"])
-    cfg = SacConfig(S, A, H)
+    reference's update (losses vs the reference's own fp32 outputs); step_model2.npz is
+    the reference SAC with networks_model2 (3 hidden layers)."""
+    z = np.load(os.path.join(golden_dir, fixture))
+    S, A, H, B, N = (int(x) for x in z["cfg"][:5])
+    cfg = SacConfig(S, A, H, n_hidden=int(z["cfg"][5]) if z["cfg"].size > 5 else 2)
     params = {n: {k: z[f"in.{n}.{k}"] for k in param_shapes(cfg)[n]} for n in NETS}
     ctx = make_ctx(cfg, max_batch=B, capacity=N)
     load_params(ctx, params)
@@ -168,6 +171,24 @@ def test_golden_small_two_steps_device_sampling(golden_dir):
             d = rel(st[f"{n}.{k}"] - params[n][k], ref - params[n][k])
             assert d < 2e-2, (n, k, d)
     assert abs(ctx.get_scalar(1) - float(z["step1.out.alpha"])) < 1e-6
+
+
+def test_step_model2_vs_oracle():
+    """networks_model2 (3 hidden layers, networks_model2.py:18-99): the extra hidden
+    GEMM levels (forward, critic / actor-pass dh, policy dh) against the fp64 oracle."""
+    cfg = SacConfig(24, 4, 64, n_hidden=3)
+    params = init_params(cfg, 51, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 500, 52, state_scale=0.5)
+    _, out = run_case(cfg, params, rows, B=32, steps=1, seed=53)
+    check_step(out[0], flat_params(params), "model2 small step 0")
+
+
+def test_step_model2_humanoid_vs_oracle():
+    cfg = SacConfig(376, 17, 512, n_hidden=3)
+    params = init_params(cfg, 61, bias_scale=0.02)
+    rows = synthetic_rows(cfg, 2000, 62, state_scale=0.1)
+    _, out = run_case(cfg, params, rows, B=256, steps=1, seed=63)
+    check_step(out[0], flat_params(params), "model2 humanoid step 0")
 
 
 def test_golden_humanoid_losses(golden_dir):
@@ -355,3 +376,58 @@ def test_dp_phase_path_matches_fused_step_world1():
                 assert np.array_equal(a[k], b[k]), ("captured", n, k)
     finally:
         dist.destroy_process_group()
+
+
+BF16_EMU_LOSS_TOL = 1e-4   # relative, vs the oracle emulating the bf16 operands
+BF16_EMU_GRAD_TOL = 2e-2   # per-tensor normwise, vs that emulation (rounding flips of
+                           # fp32-order-dependent operands, amplified by batch cancellation)
+BF16_TRUTH_GRAD_TOL = 0.15  # vs the exact fp64 oracle (cosine >= ~0.99)
+
+
+@pytest.mark.parametrize("n_hidden", [2, 3])
+def test_bf16_compute_vs_emulation(n_hidden):
+    """compute_dtype bf16 (BASELINE configs[4]): bf16 MFMA operands, fp32 accumulation,
+    fp32 master weights / Adam / losses.  No reference counterpart: checked against the
+    fp64 oracle with the same operands rounded to bf16 where the HIP path rounds them
+    (oracle/sac_step.py _EmuLinear) — the deviation from exact arithmetic is bf16's own
+    (fc1 dW ~7 %: strong cancellation over the batch), the kernel's extra error is
+    accumulation-order level."""
+    cfg = SacConfig(376, 17, 512, n_hidden=n_hidden)
+    params = init_params(cfg, 71, bias_scale=0.02)
+    rows = synthetic_rows(cfg, 2000, 72, state_scale=0.1)
+    B = 256
+    rng = np.random.default_rng(73)
+    idx = rng.choice(len(rows[2]), B, replace=False)
+    e1 = rng.standard_normal((B, cfg.action_dim)).astype(np.float32)
+    e2 = rng.standard_normal((B, cfg.action_dim)).astype(np.float32)
+    res = {}
+    for dt in ("fp32", "bf16"):
+        ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]), compute_dtype=dt)
+        load_params(ctx, params)
+        ctx.push(*rows)
+        lg = ctx.step(B, idx=idx, eps1=e1, eps2=e2)
+        res[dt] = (lg, ctx_grads(ctx, cfg))
+        ctx.close()
+    batch = [x[idx] for x in rows]
+    emu = OracleSAC(cfg, params, torch.float64)
+    l_emu = emu.step(*batch, e1, e2, bf16_operands=True)
+    g_emu = emu.grads_flat()
+    exact = OracleSAC(cfg, params, torch.float64)
+    exact.step(*batch, e1, e2)
+    g64 = exact.grads_flat()
+    lb, gb = res["bf16"]
+    for i, k in enumerate(("q1_loss", "q2_loss", "policy_loss")):
+        assert abs(lb[i] - l_emu[k]) <= BF16_EMU_LOSS_TOL * max(abs(l_emu[k]), 1e-2), (k, lb[i], l_emu[k])
+    keys = [k for k in g64 if k != "log_alpha"]
+    e_emu = {k: rel(gb[k], g_emu[k]) for k in keys}
+    e_true = {k: rel(gb[k], g64[k]) for k in keys}
+    print("bf16 grad error vs emulation", {k: f"{e:.2e}" for k, e in e_emu.items()})
+    print("bf16 grad error vs exact", {k: f"{e:.2e}" for k, e in e_true.items()})
+    assert max(e_emu.values()) <= BF16_EMU_GRAD_TOL, e_emu
+    # where bf16 moves a gradient most, the emulation accounts for most of the move
+    worst = max(keys, key=lambda k: e_true[k])
+    assert e_emu[worst] <= 0.25 * e_true[worst], (worst, e_emu[worst], e_true[worst])
+    assert max(e_true.values()) <= BF16_TRUTH_GRAD_TOL, e_true
+    # the bf16 operands really were used: the fp32 path is ~1e-6 from the truth
+    assert max(e_true.values()) > 1e-3, e_true
+    assert not np.array_equal(res["fp32"][0], lb)

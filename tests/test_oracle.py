@@ -69,10 +69,12 @@ def _golden_params(z, cfg):
     return {n: {k: z[f"in.{n}.{k}"] for k in param_shapes(cfg)[n]} for n in NETS}
 
 
-def test_oracle_fp32_bitexact_small(golden_dir):
-    z = _z(golden_dir, "step_small.npz")
-    S, A, H, B, N = (int(x) for x in z["cfg"])
-    cfg = SacConfig(S, A, H)
+@pytest.mark.parametrize("fixture", ["step_small.npz", "step_model2.npz"])
+def test_oracle_fp32_bitexact_small(golden_dir, fixture):
+    """step_model2.npz: networks_model2 (3 hidden layers) swapped into the reference SAC."""
+    z = _z(golden_dir, fixture)
+    S, A, H, B, N = (int(x) for x in z["cfg"][:5])
+    cfg = SacConfig(S, A, H, n_hidden=int(z["cfg"][5]) if z["cfg"].size > 5 else 2)
     orc = OracleSAC(cfg, _golden_params(z, cfg), dtype=torch.float32)
     rows = [z[f"rows.{k}"] for k in ("s", "a", "r", "s2", "d")]
     for t in range(2):
@@ -123,3 +125,31 @@ def test_dropin_networks_init_equals_reference(golden_dir, dims):
     for n, m in mods.items():
         for k, v in m.state_dict().items():
             assert np.array_equal(v.numpy(), z[f"{S}_{A}_{H}.{n}.{k}"]), (n, k)
+
+
+def test_dropin_networks_model2_init_equals_reference(golden_dir):
+    """networks_model2 drop-in (orthogonal policy init, 3 hidden layers) reproduces the
+    reference's initial weights under the same torch seed (init_seed3.npz, m2_ keys)."""
+    from networks_model2 import GaussianPolicy, QNetwork
+    z = np.load(os.path.join(golden_dir, "init_seed3.npz"))
+    S, A, H = 24, 4, 64
+    torch.manual_seed(3)
+    mods = {"policy": GaussianPolicy(S, A, H)}
+    for n in ("q1", "q2", "q1_target", "q2_target"):
+        mods[n] = QNetwork(S, A, H)
+    mods["q1_target"].load_state_dict(mods["q1"].state_dict())
+    mods["q2_target"].load_state_dict(mods["q2"].state_dict())
+    for n, m in mods.items():
+        for k, v in m.state_dict().items():
+            assert np.array_equal(v.numpy(), z[f"m2_{S}_{A}_{H}.{n}.{k}"]), (n, k)
+
+
+def test_model2_key_layout():
+    from sacmi.core import net_keys
+    from oracle.sac_step import param_shapes
+    cfg = SacConfig(24, 4, 64, n_hidden=3)
+    for net in ("policy", "q1"):
+        assert [k for k, _l, _p in net_keys(net, 3)] == list(param_shapes(cfg)[net])
+    cfg2 = SacConfig(24, 4, 64)
+    for net in ("policy", "q1"):
+        assert [k for k, _l, _p in net_keys(net, 2)] == list(param_shapes(cfg2)[net])

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-  timeout -k 10 500 python -m pytest tests -q -m gpu > $OUT/pytest_gpu.log 2>&1
+  eval "timeout -k 10 500 python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}" > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest_rc=$rc" >> $OUT/pytest_gpu.log; tail -3 $OUT/pytest_gpu.log
   [ $rc -ne 0 ] && exit $rc
 fi

@@ -12,6 +12,9 @@ Fixtures
 step_small.npz     S=24 A=4 H=64 B=32, 300 rows, two consecutive updates: every
                    input (params, rows, MT state, the two eps draws) and every output
                    (losses, all params, Adam m/v/step, log_alpha, alpha).
+step_model2.npz    as step_small with networks_model2 (3 hidden layers) swapped into the
+                   reference SAC.
+init_seed3.npz     the reference's own init under torch.manual_seed(3) (model1; model2).
 step_humanoid.npz  S=376 A=17 H=512 B=256, 2000 rows (state scale 0.1), two updates:
                    inputs regenerable from PCG64 seeds; outputs = losses, per-tensor
                    norms of the parameter deltas and strided element samples.
@@ -45,6 +48,29 @@ def _ref_modules():
     import sac_imp            # noqa: F401  (reference)
     import replay_buffer      # noqa: F401  (reference)
     return sys.modules["sac_imp"], sys.modules["replay_buffer"]
+
+
+class _model2_swap:
+    """The reference's SAC with networks_model2 in place of networks_model1 — the swap its
+    author makes by editing sac_imp.py:4 (the import line).  networks_model2's policy
+    defaults to device="cuda" (networks_model2.py:52); the build container has none, so
+    the class is wrapped to pass device="cpu" (nothing else changes)."""
+
+    def __enter__(self):
+        sac_imp, _ = _ref_modules()
+        import networks_model2 as m2   # noqa: F401  (reference)
+        self.saved = (sac_imp.QNetwork, sac_imp.GaussianPolicy)
+
+        class _Policy(m2.GaussianPolicy):
+            def __init__(self, s, a, h=512, device="cpu", action_bounds=None):
+                super().__init__(s, a, h, device="cpu", action_bounds=action_bounds)
+
+        sac_imp.QNetwork, sac_imp.GaussianPolicy = m2.QNetwork, _Policy
+        return self
+
+    def __exit__(self, *exc):
+        sac_imp, _ = _ref_modules()
+        sac_imp.QNetwork, sac_imp.GaussianPolicy = self.saved
 
 
 def _load_into_ref(agent, params):
@@ -152,6 +178,29 @@ def make_step_small(out):
     print("step_small.npz: oracle fp32 == reference bit-exact over 2 updates")
 
 
+def make_step_model2(out):
+    """networks_model2 (3 hidden layers, orthogonal policy init) in the reference SAC."""
+    cfg = SacConfig(24, 4, 64, n_hidden=3)
+    params = init_params(cfg, seed=31, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 300, seed=32, state_scale=0.5)
+    with _model2_swap():
+        rec = run_reference(cfg, params, rows, batch=32, steps=2, py_seed=33, torch_seed=34)
+    check_oracle_bitexact(cfg, params, rows, rec)
+    blob = {"cfg": np.array([24, 4, 64, 32, 300, 3])}
+    for n in NETS:
+        for k, v in params[n].items():
+            blob[f"in.{n}.{k}"] = v
+    for name, arr in zip(("s", "a", "r", "s2", "d"), rows):
+        blob[f"rows.{name}"] = arr
+    for t, st in enumerate(rec):
+        for k in ("mt_key", "mt_pos", "idx", "eps1", "eps2", "losses"):
+            blob[f"step{t}.{k}"] = np.asarray(st[k])
+        for k, v in st["state"].items():
+            blob[f"step{t}.out.{k}"] = np.asarray(v)
+    np.savez_compressed(os.path.join(out, "step_model2.npz"), **blob)
+    print("step_model2.npz: oracle fp32 == reference (networks_model2) bit-exact over 2 updates")
+
+
 def make_step_humanoid(out):
     cfg = SacConfig(376, 17, 512)
     P_SEED, R_SEED = 21, 22
@@ -256,6 +305,13 @@ def make_init(out):
         for n in NETS:
             for k, v in getattr(agent, n).state_dict().items():
                 blob[f"{S}_{A}_{H}.{n}.{k}"] = v.numpy().copy()
+    with _model2_swap():     # networks_model2: orthogonal policy init (networks_model2.py:82)
+        S, A, H = 24, 4, 64
+        torch.manual_seed(3)
+        agent = sac_imp.SAC(S, A, hidden_dim=H, device="cpu")
+        for n in NETS:
+            for k, v in getattr(agent, n).state_dict().items():
+                blob[f"m2_{S}_{A}_{H}.{n}.{k}"] = v.numpy().copy()
     np.savez_compressed(os.path.join(out, "init_seed3.npz"), **blob)
     print("init_seed3.npz")
 
@@ -267,7 +323,7 @@ def main():
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     torch.set_num_threads(8)
-    todo = args.only.split(",") if args.only else ["idx", "per", "small", "humanoid", "init"]
+    todo = args.only.split(",") if args.only else ["idx", "per", "small", "humanoid", "init", "model2"]
     if "init" in todo:
         make_init(args.out)
     if "idx" in todo:
@@ -278,6 +334,8 @@ def main():
         make_step_small(args.out)
     if "humanoid" in todo:
         make_step_humanoid(args.out)
+    if "model2" in todo:
+        make_step_model2(args.out)
 
 
 if __name__ == "__main__":
