@@ -36,41 +36,72 @@ import torch  # noqa: E402
 
 S_DIM, A_DIM, HIDDEN, BATCH = 376, 17, 512, 256
 PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_BF16_MFMA_TFLOPS = 2500.0    # MI355X_MICROARCH.md: Peak BF16 MFMA, dense (no sparsity)
 PEAK_HBM_GBS = 8000.0
 
+# BASELINE.json configs (index + 1) that run on one GPU / per rank: the shape of the
+# networks, the per-GPU batch, the replay kind and the GEMM arithmetic
+CONFIGS = {
+    2: dict(S=376, A=17, H=512, batch=256, replay="uniform", dtype="fp32",
+            workload="BASELINE configs[1]: Humanoid-v5 shapes, hidden=512, batch=256, uniform "
+                     "replay (HBM ring, device random.sample)"),
+    3: dict(S=376, A=17, H=512, batch=4096, replay="per", dtype="fp32",
+            workload="BASELINE configs[2]: Humanoid-v5 shapes, hidden=512, batch=4096, prioritized "
+                     "replay resident in HBM (device np.random.choice over prios**alpha)"),
+    5: dict(S=661, A=23, H=512, batch=4096, replay="uniform", dtype="bf16",
+            workload="BASELINE configs[4] per GPU: NAO-walk shapes (obs 661, act 23), hidden=512, "
+                     "batch=4096, uniform replay, auto-entropy on, bf16 MFMA operands (fp32 "
+                     "accumulation, fp32 master weights / Adam)"),
+}
 
-def necessary_flops(S, A, H, B):
+
+def workload(args) -> dict:
+    w = dict(CONFIGS[args.config])
+    w["batch"] = args.batch
+    if args.dtype:
+        w["dtype"] = args.dtype
+    w["n_hidden"] = 3 if args.networks == "model2" else 2
+    w["networks"] = args.networks
+    return w
+
+
+def necessary_flops(S, A, H, B, n_hidden=2):
     """GEMM FLOPs the update needs (excludes the reference's wasted
-    actor-pass Q dW and state columns of Q-fc1 dX)."""
-    Qf = (S + A) * H + H * H + H
-    Pf = S * H + H * H + 2 * H * A
-    Qdx = H + H * H + H * A
-    Pbw = Pf + H * H + 2 * H * A
-    return 2 * B * ((Pf + 2 * Qf) + 2 * (2 * Qf + H + H * H) + (Pf + 2 * Qf + 2 * Qdx + Pbw))
+    actor-pass Q dW and state columns of Q-fc1 dX); n_hidden-1 H x H layers per net."""
+    HH = (n_hidden - 1) * H * H
+    Qf = (S + A) * H + HH + H
+    Pf = S * H + HH + 2 * H * A
+    Qdx = H + HH + H * A
+    Pbw = Pf + HH + 2 * H * A
+    return 2 * B * ((Pf + 2 * Qf) + 2 * (2 * Qf + H + HH) + (Pf + 2 * Qf + 2 * Qdx + Pbw))
 
 
-def synth(n, seed):
+def synth(n, seed, S=S_DIM, A=A_DIM):
     rng = np.random.default_rng(seed)
-    s = rng.standard_normal((n, S_DIM), dtype=np.float32)
-    s2 = rng.standard_normal((n, S_DIM), dtype=np.float32)
-    a = rng.uniform(-0.4, 0.4, size=(n, A_DIM)).astype(np.float32)
+    s = rng.standard_normal((n, S), dtype=np.float32)
+    s2 = rng.standard_normal((n, S), dtype=np.float32)
+    a = rng.uniform(-0.4, 0.4, size=(n, A)).astype(np.float32)
     r = rng.standard_normal(n, dtype=np.float32)
     d = (rng.random(n) < 0.02).astype(np.uint8)
     return s, a, r, s2, d
 
 
 def init_agent(ctx, seed):
-    """Xavier-uniform weights, zero biases (networks_model1.py:22-25,60-63)."""
+    """Xavier-uniform weights, zero biases (networks_model1.py:22-25,60-63; the same for
+    networks_model2's critics — its orthogonal policy init changes nothing measured)."""
     rng = np.random.default_rng(seed)
     from sacmi.core import net_keys
-    shapes = {"policy": {"fc1": (HIDDEN, S_DIM), "fc2": (HIDDEN, HIDDEN), "mean": (A_DIM, HIDDEN),
-                         "log_std": (A_DIM, HIDDEN)},
-              "q": {"fc1": (HIDDEN, S_DIM + A_DIM), "fc2": (HIDDEN, HIDDEN), "fc3": (1, HIDDEN)}}
+    cfg = ctx.cfg
+    S, A, H, nh = cfg.state_dim, cfg.action_dim, cfg.hidden_dim, cfg.n_hidden
+    shapes = {"policy": {"fc1": (H, S), "mean": (A, H), "log_std": (A, H)},
+              "q": {"fc1": (H, S + A), f"fc{nh + 1}": (1, H)}}
+    for i in range(2, nh + 1):
+        shapes["policy"][f"fc{i}"] = shapes["q"][f"fc{i}"] = (H, H)
     q_sd = {}
     for net in ("policy", "q1", "q2"):
         shp = shapes["policy" if net == "policy" else "q"]
         sd = {}
-        for key, _layer, part in net_keys(net):
+        for key, _layer, part in net_keys(net, nh):
             lname = key.split(".")[0]
             o, i = shp[lname]
             if part == 0:
@@ -121,7 +152,7 @@ def pmc_traffic(config):
         return None, None
 
 
-def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False):
+def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False, n_hidden=2):
     """The reference update on CPU (oracle torch port, fp32) + the reference's replay
     data path (deque + random.sample, or the prioritized buffer's numpy sampler), timed
     on this host's cores for a bounded number of steps."""
@@ -130,9 +161,10 @@ def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False):
     from oracle.sac_step import OracleSAC, SacConfig, init_params
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    cfg = SacConfig(S_DIM, A_DIM, HIDDEN)
-    agent = OracleSAC(cfg, init_params(cfg, 0), dtype=torch.float32)
     s, a, r, s2, d = rows
+    S, A = s.shape[1], a.shape[1]
+    cfg = SacConfig(S, A, HIDDEN, n_hidden=n_hidden)
+    agent = OracleSAC(cfg, init_params(cfg, 0), dtype=torch.float32)
     if per:
         buf = PerReplayNumpy(capacity=len(r))
         buf.fill(rows)
@@ -146,8 +178,8 @@ def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False):
 
     def one():
         bs, ba, br, bs2, bd = buf.sample(batch)[:5]
-        e1 = torch.randn(batch, A_DIM, generator=gen).numpy()
-        e2 = torch.randn(batch, A_DIM, generator=gen).numpy()
+        e1 = torch.randn(batch, A, generator=gen).numpy()
+        e2 = torch.randn(batch, A, generator=gen).numpy()
         agent.step(bs, ba, br, bs2, bd, e1, e2)
 
     for _ in range(warmup):
@@ -179,9 +211,14 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
-                    help="BASELINE.json configs[1] (2: batch 256 uniform) or configs[2] "
-                         "(3: batch 4096, prioritized replay in HBM)")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[1] (2: batch 256 uniform), configs[2] "
+                         "(3: batch 4096, prioritized replay in HBM) or configs[4] per GPU "
+                         "(5: NAO shapes, batch 4096, bf16 MFMA)")
+    ap.add_argument("--networks", default="model1", choices=("model1", "model2"),
+                    help="networks_model1 (2 hidden layers) or networks_model2 (3)")
+    ap.add_argument("--dtype", default=None, choices=("fp32", "bf16"),
+                    help="GEMM operand arithmetic (default: the config's)")
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--fill", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -195,7 +232,7 @@ def parse_args(argv=None):
                     help="just run warmup+steps (for rocprofv3 runs)")
     args = ap.parse_args(argv)
     if args.batch is None:                 # both the single-GPU and the DP paths use it
-        args.batch = 4096 if args.config == 3 else BATCH
+        args.batch = CONFIGS[args.config]["batch"]
     return args
 
 
@@ -205,7 +242,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    per = args.config == 3
+    wl = workload(args)
+    per = wl["replay"] == "per"
+    S, A, H = wl["S"], wl["A"], wl["H"]
     if world > 1 or args.force_dp:
         from sacmi.dp import run_dp_bench
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -215,14 +254,15 @@ def main():
     from sacmi import Config, Context
     torch.cuda.init()
     fill = args.fill
-    ctx = Context(Config(S_DIM, A_DIM, HIDDEN, max_batch=args.batch, capacity=fill, seed=1,
-                         replay="per" if per else "uniform"), 0)
+    ctx = Context(Config(S, A, H, max_batch=args.batch, capacity=fill, seed=1,
+                         replay=wl["replay"], n_hidden=wl["n_hidden"],
+                         compute_dtype=wl["dtype"]), 0)
     init_agent(ctx, 0)
     t_fill = time.perf_counter()
     chunk = 100_000
     rows_keep = None
     for c0 in range(0, fill, chunk):
-        rows = synth(min(chunk, fill - c0), 1000 + c0)
+        rows = synth(min(chunk, fill - c0), 1000 + c0, S, A)
         ctx.push(*rows)
         if rows_keep is None:
             rows_keep = rows
@@ -273,44 +313,44 @@ def main():
     sync_sps = n_sync / (time.perf_counter() - t1)
 
     roof = None
+    peak = PEAK_BF16_MFMA_TFLOPS if wl["dtype"] == "bf16" else PEAK_FP32_MFMA_TFLOPS
     if not args.no_roofline:
         info = gemm_roofline(ctx, args.batch)
         traffic, traffic_src = pmc_traffic(args.config)
         roof = {"bound": "mfma", "achieved": round(info["achieved_tflops"], 3),
-                "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(info["achieved_tflops"] / PEAK_FP32_MFMA_TFLOPS, 4),
+                "peak": peak, "unit": "TFLOP/s",
+                "frac": round(info["achieved_tflops"] / peak, 4),
                 "traffic": None if traffic is None else round(traffic),
                 "traffic_unit": "bytes past L2 per k_gemm launch (PMC)",
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": round(info["gemm_bytes"] / info["launches"]),
-                "kernel": "sacmi::k_gemm (grouped fp32 MFMA GEMM, all tile configs)",
+                "kernel": f"sacmi::k_gemm (grouped {wl['dtype']} MFMA GEMM, all tile configs)",
                 "launches_per_step": info["launches"],
                 "avg_launch_us": round(info["avg_launch_us"], 3),
                 "gemm_flops_per_step": info["gemm_flops"],
                 "sites_sum_us": round(info["sites_sum_us"], 2),
                 "sites_us": {x[0]: round(x[1], 2) for x in info["sites"]}}
-    flops = necessary_flops(S_DIM, A_DIM, HIDDEN, args.batch)
+    flops = necessary_flops(S, A, H, args.batch, wl["n_hidden"])
     cpu = None
     if not args.no_cpu_baseline:
         n_cpu = min(fill, 1_000_000)
-        cpu_rows = tuple(x[:n_cpu] for x in synth(n_cpu, 7))
-        cpu = cpu_baseline(cpu_rows, seconds=args.cpu_seconds, batch=args.batch, per=per)
-    workload = ("BASELINE configs[2]: Humanoid-v5 shapes, hidden=512, batch=4096, prioritized "
-                "replay resident in HBM (device np.random.choice over prios**alpha)" if per else
-                "BASELINE configs[1]: Humanoid-v5 shapes, hidden=512, batch=256, uniform replay "
-                "(HBM ring, device random.sample)")
+        cpu_rows = tuple(x[:n_cpu] for x in synth(n_cpu, 7, S, A))
+        cpu = cpu_baseline(cpu_rows, seconds=args.cpu_seconds, batch=args.batch, per=per,
+                           n_hidden=wl["n_hidden"])
+    env = "Humanoid-v5" if args.config != 5 else "NAO-walk"
     out = {
-        "metric": f"SAC gradient-steps/sec, Humanoid-v5 batch={args.batch} (obs 376, act 17, hidden 512)",
+        "metric": f"SAC gradient-steps/sec, {env} batch={args.batch} (obs {S}, act {A}, hidden {H})",
         "value": round(sps, 2), "unit": "grad-steps/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 / sps, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-        "config": {"workload": workload,
-                   "state_dim": S_DIM, "action_dim": A_DIM, "hidden": HIDDEN,
+        "scaling": "weak", "vs_baseline": None, "dtype": wl["dtype"], "data": "synthetic",
+        "config": {"workload": wl["workload"] + (" [networks_model2: 3 hidden layers]"
+                                                 if wl["n_hidden"] == 3 else ""),
+                   "state_dim": S, "action_dim": A, "hidden": H, "n_hidden": wl["n_hidden"],
                    "global_batch": args.batch, "replay_fill": fill, "parallelism": "single GPU"},
         "updates_per_launch": upl,
         "one_update_per_launch_steps_per_s": round(one_sps, 2),
         "api_faithful_steps_per_s": round(sync_sps, 2),
-        "mfma_util_step": round(flops * sps / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
+        "mfma_util_step": round(flops * sps / 1e12 / peak, 4),
         "necessary_gflop_per_step": round(flops / 1e9, 4),
         "roofline": roof, "cpu_baseline": cpu,
         "fill_seconds": round(t_fill, 2),

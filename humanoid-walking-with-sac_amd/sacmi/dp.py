@@ -166,15 +166,17 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int):
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+    wl = B.workload(args)
+    S, A, H = wl["S"], wl["A"], wl["H"]
     fill = args.fill // world                       # this rank's replay shard
-    ctx = Context(Config(B.S_DIM, B.A_DIM, B.HIDDEN, max_batch=args.batch, capacity=fill,
-                         seed=1000 + rank), local_rank)
+    ctx = Context(Config(S, A, H, max_batch=args.batch, capacity=fill, seed=1000 + rank,
+                         n_hidden=wl["n_hidden"], compute_dtype=wl["dtype"]), local_rank)
     B.init_agent(ctx, 0)                            # identical replicas
     key = np.random.default_rng(77 + rank).integers(0, 2**32, size=624, dtype=np.uint32)
     ctx.set_mt(0, key, 624)                         # per-shard sampling stream
     chunk = 100_000
     for c0 in range(0, fill, chunk):
-        ctx.push(*B.synth(min(chunk, fill - c0), 5000 + rank * 7919 + c0))
+        ctx.push(*B.synth(min(chunk, fill - c0), 5000 + rank * 7919 + c0, S, A))
     per_launch = max(1, min(args.updates_per_launch, 256))
     captured = None
     if os.environ.get("SACMI_DP_GRAPH", "1") == "1":
@@ -218,22 +220,24 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int):
     if rank == 0:
         iters = args.steps / dt
         value = world * iters
-        flops = B.necessary_flops(B.S_DIM, B.A_DIM, B.HIDDEN, args.batch)
+        flops = B.necessary_flops(S, A, H, args.batch, wl["n_hidden"])
+        peak = B.PEAK_BF16_MFMA_TFLOPS if wl["dtype"] == "bf16" else B.PEAK_FP32_MFMA_TFLOPS
+        env = "Humanoid-v5" if args.config != 5 else "NAO-walk"
         out = {
-            "metric": "SAC gradient-steps/sec, Humanoid-v5 batch=256 (obs 376, act 17, hidden 512)",
-            "value": round(value, 2), "unit": "grad-steps/s (batch-256 equivalent)",
+            "metric": f"SAC gradient-steps/sec, {env} batch={args.batch} (obs {S}, act {A}, hidden {H})",
+            "value": round(value, 2), "unit": f"grad-steps/s (batch-{args.batch} per GPU)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": "BASELINE configs[3] shape at batch 256/GPU: Humanoid-v5, "
-                                   "hidden=512, per-GPU replay shard + RCCL grad all-reduce",
-                       "state_dim": B.S_DIM, "action_dim": B.A_DIM, "hidden": B.HIDDEN,
+            "scaling": "weak", "vs_baseline": None, "dtype": wl["dtype"], "data": "synthetic",
+            "config": {"workload": wl["workload"] + f"; {world} ranks: per-GPU replay shard + "
+                                   "RCCL gradient all-reduce over xGMI (uniform replay per shard)",
+                       "state_dim": S, "action_dim": A, "hidden": H, "n_hidden": wl["n_hidden"],
                        "global_batch": args.batch * world, "replay_fill": fill * world,
                        "parallelism": f"dp{world}"},
             "iterations_per_s": round(iters, 2),
             "updates_per_launch": per_launch if captured else 1,
             "dp_graph": captured is not None,
-            "mfma_util_step": round(flops * value / 1e12 / B.PEAK_FP32_MFMA_TFLOPS / world, 4),
+            "mfma_util_step": round(flops * value / 1e12 / peak / world, 4),
             "replicas_bitwise_equal": replicas_equal,
             "roofline": None, "cpu_baseline": None,
         }
