@@ -206,6 +206,49 @@ def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False, n_hidden=
                        f"{len(r)} rows (float32 rows); {threads} threads on {cpu}")
 
 
+def trainer_loop(wl, steps=300, warmup=30, fill=20_000):
+    """The reference trainer's inner loop without the environment (trainer.py:182-205):
+    per env step select_action(state) -> replay_buffer.push(transition) ->
+    update_parameters(batch) (losses synced, as .item() in sac_imp.py:140-144), through
+    the drop-in SAC (sac_imp module name).  Returns env-steps/s and the split."""
+    from sac_imp import SAC
+    S, A, H, B = wl["S"], wl["A"], wl["H"], wl["batch"]
+    torch.manual_seed(0)
+    agent = SAC(S, A, hidden_dim=H, device="cuda", capacity=max(fill * 2, 100_000),
+                max_batch=B, seed=3, networks=wl["networks"], compute_dtype=wl["dtype"])
+    agent._ctx.push(*synth(fill, 11, S, A))
+    rng = np.random.default_rng(12)
+    states = rng.standard_normal((steps + warmup + 1, S)).astype(np.float32)
+
+    def one(i, t):
+        a = agent.select_action(states[i])
+        t1 = time.perf_counter()
+        agent.replay_buffer.push(states[i], a, float(i % 7) * 0.1, states[i + 1], (i % 50) == 49)
+        t2 = time.perf_counter()
+        agent.update_parameters(B)
+        t3 = time.perf_counter()
+        t[0] += t1 - t0_[0]; t[1] += t2 - t1; t[2] += t3 - t2
+        t0_[0] = t3
+
+    t0_ = [time.perf_counter()]
+    tw = [0.0, 0.0, 0.0]
+    for i in range(warmup):
+        one(i, tw)
+    torch.cuda.synchronize()
+    tt = [0.0, 0.0, 0.0]
+    t0 = time.perf_counter()
+    t0_[0] = t0
+    for i in range(warmup, warmup + steps):
+        one(i, tt)
+    dt = time.perf_counter() - t0
+    return {"env_steps_per_s": round(steps / dt, 2),
+            "us_select_action": round(1e6 * tt[0] / steps, 1),
+            "us_push": round(1e6 * tt[1] / steps, 1),
+            "us_update_parameters": round(1e6 * tt[2] / steps, 1),
+            "note": "trainer.py:182-205 loop minus env.step: select_action + push + "
+                    f"update_parameters({B}) per env step, drop-in SAC, {fill}-row replay"}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +271,9 @@ def parse_args(argv=None):
                     help="updates per device launch (trainer.py updates_per_step loop)")
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel path even at world size 1 (overhead check)")
+    ap.add_argument("--no-trainer-loop", action="store_true",
+                    help="skip the env-free trainer-loop measurement (select_action + push + "
+                         "update_parameters per env step)")
     ap.add_argument("--profile-only", action="store_true",
                     help="just run warmup+steps (for rocprofv3 runs)")
     args = ap.parse_args(argv)
@@ -331,6 +377,7 @@ def main():
                 "sites_sum_us": round(info["sites_sum_us"], 2),
                 "sites_us": {x[0]: round(x[1], 2) for x in info["sites"]}}
     flops = necessary_flops(S, A, H, args.batch, wl["n_hidden"])
+    loop = None if args.no_trainer_loop else trainer_loop(wl)
     cpu = None
     if not args.no_cpu_baseline:
         n_cpu = min(fill, 1_000_000)
@@ -352,6 +399,7 @@ def main():
         "api_faithful_steps_per_s": round(sync_sps, 2),
         "mfma_util_step": round(flops * sps / 1e12 / peak, 4),
         "necessary_gflop_per_step": round(flops / 1e9, 4),
+        "trainer_loop": loop,
         "roofline": roof, "cpu_baseline": cpu,
         "fill_seconds": round(t_fill, 2),
     }

@@ -44,4 +44,39 @@ void launch_mt_sample(const MtSampleArgs& a, hipStream_t s) {
   if (e != hipSuccess) fprintf(stderr, "sacmi: k_mt_sample launch failed: %s\n", hipGetErrorString(e));
 }
 
+// one wave per ring row (grid-stride), lanes over the row's columns; coalesced both ways
+__global__ __launch_bounds__(256) void k_push_rows(PushArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const float* s = a.stage;
+  const float* ac = s + a.n * a.S;
+  const float* r = ac + a.n * a.A;
+  const float* s2 = r + a.n;
+  const float* d = s2 + a.n * a.S;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < a.n; i += nw) {
+    const int64_t w = (a.pos0 + i) % a.cap;
+    for (int k = lane; k < a.S; k += 64) {
+      a.obs[w * a.ldo + k] = s[i * a.S + k];
+      a.obs2[w * a.ldo + k] = s2[i * a.S + k];
+    }
+    for (int k = lane; k < a.A; k += 64) a.act[w * a.ldact + k] = ac[i * a.A + k];
+    if (lane == 0) {
+      a.rew[w] = r[i];
+      a.done[w] = d[i];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.sc->len = a.len;
+    a.sc->head = a.head;
+  }
+}
+
+void launch_push_rows(const PushArgs& a, hipStream_t s) {
+  const int64_t blocks = (a.n + 3) / 4;
+  const int grid = (int)(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024);
+  hipLaunchKernelGGL(k_push_rows, dim3(grid), dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fprintf(stderr, "sacmi: k_push_rows launch failed: %s\n", hipGetErrorString(e));
+}
+
 }  // namespace sacmi

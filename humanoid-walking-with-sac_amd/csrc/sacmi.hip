@@ -123,6 +123,15 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> ax, ah1, ah2, aeps, acache, alogp, aout;
   // staging
   sacmi::DevBuf<float> stage, per_scr;
+  // pinned host staging (hipHostMalloc): transition ingest slots (one in-flight H2D copy
+  // each, guarded by an event), act in/out, the scalar block readback
+  static constexpr int kPushSlots = 2;
+  int push_rows = 0;                        // rows per ingest chunk
+  float* push_host[kPushSlots] = {};
+  hipEvent_t push_ev[kPushSlots] = {};
+  int push_slot = 0;
+  float* act_host = nullptr;                // [kActPinned][S] states, then [..][A] eps / out
+  sacmi::DevScalars* sc_host = nullptr;
   // PER scratch (replay_kind == PER)
   sacmi::DevBuf<float> per_probs, per_chunk, per_w, per_val;
   sacmi::DevBuf<int64_t> per_q, per_blk, per_idx;
@@ -287,14 +296,45 @@ static void alloc_all(sacmi_ctx* c) {
 }
 
 static void upload_scalars(sacmi_ctx* c, const DevScalars& h) {
-  CHECK_HIP(hipMemcpyAsync(c->sc.p, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+  *c->sc_host = h;
+  CHECK_HIP(hipMemcpyAsync(c->sc.p, c->sc_host, sizeof(h), hipMemcpyHostToDevice, c->stream));
   CHECK_HIP(hipStreamSynchronize(c->stream));
 }
 static DevScalars download_scalars(sacmi_ctx* c) {
-  DevScalars h;
-  CHECK_HIP(hipMemcpyAsync(&h, c->sc.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  CHECK_HIP(hipMemcpyAsync(c->sc_host, c->sc.p, sizeof(DevScalars), hipMemcpyDeviceToHost, c->stream));
   CHECK_HIP(hipStreamSynchronize(c->stream));
-  return h;
+  return *c->sc_host;
+}
+
+constexpr int kActPinned = 64;   // select_action rows served from pinned staging
+
+static void alloc_pinned(sacmi_ctx* c) {
+  const int S = c->S, A = c->A;
+  c->push_rows = 1024;
+  const size_t row = (size_t)2 * S + A + 2;
+  for (int i = 0; i < sacmi_ctx::kPushSlots; ++i) {
+    CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->push_host[i]), row * c->push_rows * 4,
+                            hipHostMallocDefault));
+    CHECK_HIP(hipEventCreateWithFlags(&c->push_ev[i], hipEventDisableTiming));
+  }
+  c->stage.alloc(row * c->push_rows);
+  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->act_host),
+                          (size_t)kActPinned * (S + 2 * A) * 4, hipHostMallocDefault));
+  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->sc_host), sizeof(DevScalars),
+                          hipHostMallocDefault));
+}
+
+static void free_pinned(sacmi_ctx* c) {
+  for (int i = 0; i < sacmi_ctx::kPushSlots; ++i) {
+    if (c->push_ev[i]) (void)hipEventDestroy(c->push_ev[i]);
+    if (c->push_host[i]) (void)hipHostFree(c->push_host[i]);
+    c->push_ev[i] = nullptr;
+    c->push_host[i] = nullptr;
+  }
+  if (c->act_host) (void)hipHostFree(c->act_host);
+  if (c->sc_host) (void)hipHostFree(c->sc_host);
+  c->act_host = nullptr;
+  c->sc_host = nullptr;
 }
 
 // ---------------------------------------------------------------------------
@@ -919,7 +959,7 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
     alloc_all(c.get());
     c->ring_slots = 4096;
     c->ring.alloc((size_t)c->ring_slots * 3);
-    c->stage.alloc(0);
+    alloc_pinned(c.get());
     DevScalars h{};
     h.alpha = (float)cfg->alpha;
     for (int i = 0; i < 4; ++i) { h.beta_pow[i][0] = 1.0; h.beta_pow[i][1] = 1.0; }
@@ -944,6 +984,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     destroy_graphs(c);
+    free_pinned(c);
     if (c->G_external) {
       auto& reg = alloc_registry();
       for (size_t i = 0; i < reg.size(); ++i)
@@ -1102,29 +1143,41 @@ int sacmi_push(sacmi_ctx* c, const float* s, const float* a, const float* r, con
     if (n == 0) return;
     REQUIRE(s && a && r && s2 && d, SACMI_EVALUE, "null transition array");
     // only the last `capacity` rows of a huge batch survive (deque(maxlen))
-    int64_t skip = n > c->capacity ? n - c->capacity : 0;
+    const int64_t skip = n > c->capacity ? n - c->capacity : 0;
     const int S = c->S, A = c->A;
-    std::vector<float> dn;
     const bool was_empty = c->len == 0;
     const int64_t cap = c->capacity;
-    int64_t w = (c->wpos + skip) % cap;   // ring slot of row `skip`
-    const int64_t pos0 = w;
-    int64_t i = skip;
-    while (i < n) {
-      const int64_t run = std::min<int64_t>(n - i, cap - w);
-      CHECK_HIP(hipMemcpy2DAsync(c->obs.p + w * c->ldo, c->ldo * 4, s + i * S, S * 4, S * 4, run,
-                                 hipMemcpyHostToDevice, c->stream));
-      CHECK_HIP(hipMemcpy2DAsync(c->obs2.p + w * c->ldo, c->ldo * 4, s2 + i * S, S * 4, S * 4, run,
-                                 hipMemcpyHostToDevice, c->stream));
-      CHECK_HIP(hipMemcpy2DAsync(c->act.p + w * c->ldact, c->ldact * 4, a + i * A, A * 4, A * 4, run,
-                                 hipMemcpyHostToDevice, c->stream));
-      CHECK_HIP(hipMemcpyAsync(c->rew.p + w, r + i, run * 4, hipMemcpyHostToDevice, c->stream));
-      dn.resize(run);
-      for (int64_t j = 0; j < run; ++j) dn[j] = d[i + j] ? 1.f : 0.f;
-      CHECK_HIP(hipMemcpyAsync(c->done.p + w, dn.data(), run * 4, hipMemcpyHostToDevice, c->stream));
-      CHECK_HIP(hipStreamSynchronize(c->stream));
-      i += run;
-      w = (w + run) % cap;
+    const int64_t pos0 = (c->wpos + skip) % cap;   // ring slot of row `skip`
+    // chunks of push_rows rows: pack into a pinned slot (SoA), one async H2D copy, one
+    // scatter kernel; the slot is reused once its copy has completed (event)
+    for (int64_t i = skip; i < n; i += c->push_rows) {
+      const int64_t m = std::min<int64_t>(c->push_rows, n - i);
+      const int k = c->push_slot;
+      c->push_slot = (k + 1) % sacmi_ctx::kPushSlots;
+      CHECK_HIP(hipEventSynchronize(c->push_ev[k]));
+      float* h = c->push_host[k];
+      std::memcpy(h, s + i * S, (size_t)m * S * 4);
+      std::memcpy(h + m * S, a + i * A, (size_t)m * A * 4);
+      std::memcpy(h + m * (S + A), r + i, (size_t)m * 4);
+      std::memcpy(h + m * (S + A + 1), s2 + i * S, (size_t)m * S * 4);
+      float* hd = h + m * (2 * S + A + 1);
+      for (int64_t j = 0; j < m; ++j) hd[j] = d[i + j] ? 1.f : 0.f;
+      CHECK_HIP(hipMemcpyAsync(c->stage.p, h, (size_t)m * (2 * S + A + 2) * 4, hipMemcpyHostToDevice,
+                               c->stream));
+      CHECK_HIP(hipEventRecord(c->push_ev[k], c->stream));
+      const int64_t done_rows = i + m - skip;
+      PushArgs pa{};
+      pa.stage = c->stage.p;
+      pa.obs = c->obs.p; pa.obs2 = c->obs2.p; pa.act = c->act.p; pa.rew = c->rew.p; pa.done = c->done.p;
+      pa.S = S; pa.A = A; pa.ldo = c->ldo; pa.ldact = c->ldact;
+      pa.n = m; pa.pos0 = (pos0 + (i - skip)) % cap; pa.cap = cap;
+      pa.sc = c->sc.p;
+      const int64_t len = std::min<int64_t>(cap, c->len + skip + done_rows);
+      const int64_t wpos = (c->wpos + skip + done_rows) % cap;
+      pa.len = len;
+      pa.head = len < cap ? 0 : wpos;
+      launch_push_rows(pa, c->stream);
+      CHECK_HIP(hipGetLastError());
     }
     const int64_t added = n - skip;
     if (c->cfg.replay_kind == SACMI_REPLAY_PER) {
@@ -1132,10 +1185,6 @@ int sacmi_push(sacmi_ctx* c, const float* s, const float* a, const float* r, con
     }
     c->wpos = (c->wpos + n) % c->capacity;
     c->len = std::min<int64_t>(c->capacity, c->len + n);
-    DevScalars h = download_scalars(c);
-    h.len = c->len;
-    h.head = c->len < c->capacity ? 0 : c->wpos;
-    upload_scalars(c, h);
   });
 }
 
@@ -1484,10 +1533,25 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     REQUIRE(n > 0 && n <= 2 * c->Bm, SACMI_EVALUE, "n must be in [1, 2*max_batch]");
     hipStream_t s = c->stream;
     const int S = c->S, A = c->A, H = c->H, Kx = c->Kx, Hd = c->Hd;
-    CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, states, (size_t)S * 4, (size_t)S * 4, n,
+    // env-rate calls (n <= kActPinned) go through pinned staging: no pageable-copy syncs
+    const bool pinned = n <= kActPinned;
+    float* h_in = c->act_host;
+    float* h_eps = c->act_host + (size_t)kActPinned * S;
+    float* h_out = h_eps + (size_t)kActPinned * A;
+    const float* src = states;
+    const float* esrc = eps;
+    if (pinned) {
+      std::memcpy(h_in, states, (size_t)n * S * 4);
+      src = h_in;
+      if (eps && !deterministic) {
+        std::memcpy(h_eps, eps, (size_t)n * A * 4);
+        esrc = h_eps;
+      }
+    }
+    CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, src, (size_t)S * 4, (size_t)S * 4, n,
                                hipMemcpyHostToDevice, s));
     if (eps && !deterministic)
-      CHECK_HIP(hipMemcpyAsync(c->eps.p, eps, (size_t)n * A * 4, hipMemcpyHostToDevice, s));
+      CHECK_HIP(hipMemcpyAsync(c->eps.p, esrc, (size_t)n * A * 4, hipMemcpyHostToDevice, s));
     Level l1;
     l1.add(gd(c->x2.p, Kx, 1, c->P.p + c->p_fc[0].off, c->p_fc[0].ld, 1, c->hp[0].p, Hd, n, H, S + 1, EPI_RELU));
     l1.b.bf16 = c->bf16;
@@ -1509,9 +1573,10 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     hs.ctr_override = (1ull << 63) | (++c->act_calls);   // disjoint from update noise
     launch_heads_sample(hs, s);
     CHECK_HIP(hipGetLastError());
-    CHECK_HIP(hipMemcpy2DAsync(a_out, (size_t)A * 4, c->x2.p + S + 1, (size_t)Kx * 4, (size_t)A * 4, n,
-                               hipMemcpyDeviceToHost, s));
+    CHECK_HIP(hipMemcpy2DAsync(pinned ? h_out : a_out, (size_t)A * 4, c->x2.p + S + 1, (size_t)Kx * 4,
+                               (size_t)A * 4, n, hipMemcpyDeviceToHost, s));
     CHECK_HIP(hipStreamSynchronize(s));
+    if (pinned) std::memcpy(a_out, h_out, (size_t)n * A * 4);
   });
 }
 

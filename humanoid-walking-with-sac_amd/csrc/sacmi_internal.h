@@ -262,6 +262,20 @@ void launch_gather(const GatherArgs& a, hipStream_t s);
 
 void launch_mt_sample(const MtSampleArgs& a, hipStream_t s);
 
+// Transition ingest (replay_buffer.py:10-11 push, batched): one host->device copy of n
+// packed rows [s n*S | a n*A | r n | s2 n*S | d n] (from a pinned staging slot), scattered
+// into the SoA ring at slots (pos0 + i) % cap; block 0 also publishes the fill / head
+// the host computed (DevScalars len, head) — no host round trip.
+struct PushArgs {
+  const float* stage;
+  float *obs, *obs2, *act, *rew, *done;
+  int S, A, ldo, ldact;
+  int64_t n, pos0, cap;
+  DevScalars* sc;
+  int64_t len, head;
+};
+void launch_push_rows(const PushArgs& a, hipStream_t s);
+
 void launch_fill(float* p, int64_t n, float v, hipStream_t s);
 void launch_set_column(float* p, int rows, int ld, int col, float v, hipStream_t s);
 void launch_increment_steps(DevScalars* sc, hipStream_t s);
