@@ -204,8 +204,11 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // AXF 1: A-operand transform (GemmDesc::axk) applied to the loaded fragments before the
 // MFMAs: a(b,k) = A>0 ? coef[row]*w[k] : 0 with coef in LDS (coef[tile row]); with
 // store_a the transformed fragments are also written to d.ax_out.
+// PIPE (G == 1, AXF == 0): software-pipelined K loop — chunk j+1's loads are in flight
+// while chunk j's MFMAs run (two register buffers), and the epilogue operands (pre) go
+// out right behind chunk 0's loads.  Same chunk order per wave: bitwise identical sums.
 template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
-          int AXF = 0, bool BF16 = false, class Pre, class Early = void (*)()>
+          int AXF = 0, bool BF16 = false, bool PIPE = false, class Pre, class Early = void (*)()>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
                                             float* rsum, Pre&& pre, bool store_a = false,
                                             Early&& early = [] {}) {
@@ -246,6 +249,54 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
                                store_a ? (uint32_t)(((size_t)(d.M - 1) * d.ax_ld + d.K) * 4) : 0u);
   early();
+  if constexpr (PIPE) {
+    static_assert(G == 1 && AXF == 0, "pipelined K loop: one chunk per stage, no A transform");
+    float a1[MT][4], b1[NT][4], xw1[4];
+    auto issue = [&](int jj, float (&av)[MT][4], float (&bv)[NT][4], float (&xv)[4]) {
+      jj = jj < nmine ? jj : nmine - 1;   // unconditional: past the end re-reads the last chunk
+      const int k = (ks + jj * KSPLIT) * 16 + kl;
+      fetch_op<MT, AKC>(ra, d.lda, k, d.K, av);
+      fetch_op<NT, BKC>(rb, d.ldb, k, d.K, bv);
+      if constexpr (!AKC) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xv[s] = buf_ld(rxw, (uint32_t)(k + s < d.K ? k + s : 0) * 4u);
+      }
+    };
+    auto consume = [&](float (&av)[MT][4], const float (&bv)[NT][4], const float (&xv)[4]) {
+#pragma clang fp contract(off)
+      if constexpr (!AKC) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float f = has_ksc ? xv[s] : 1.f;
+#pragma unroll
+          for (int i = 0; i < MT; ++i) av[i][s] *= f;
+        }
+      }
+      mfma_chunk<MT, NT, BF16>(acc, av, bv);
+      if (ROWSUM) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) rs[i] += (av[i][0] + av[i][1]) + (av[i][2] + av[i][3]);
+      }
+    };
+    if (nmine == 0) {
+      pre();
+    } else {
+      issue(0, a[0], b[0], xw[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
+      for (int j = 0; j < nmine; j += 2) {
+        issue(j + 1, a1, b1, xw1);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(a[0], b[0], xw[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(j + 2, a[0], b[0], xw[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (j + 1 < nmine) consume(a1, b1, xw1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else {
   if (nmine == 0) pre();
   for (int j = 0; j < nmine; j += G) {
 #pragma unroll
@@ -306,6 +357,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
         }
       }
   }
+  }   // !PIPE
   SACMI_STAMP(16 + wave);
   float* my = red + wave * TM * (TN + 1);
   const int rq = (lane >> 4) * 4, cc = lane & 15;
@@ -330,7 +382,8 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
 // layout dispatch (wave-uniform, once per workgroup)
 // AXK: whether this kernel instantiation carries the A-transform path (launch_gemm picks
 // the variant from the level's descs): 1 -> axk 1 descs, 0 -> none.
-template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, class Pre, class Early>
+template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, bool PIPE, class Pre,
+          class Early>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
                                           float* rsum, bool rowsum, Pre&& pre, Early&& early) {
   if constexpr (AXK == 1) {
@@ -341,12 +394,12 @@ __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, flo
     }
   }
   if (d.a_kc) {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
-    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
   } else {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
-    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
-    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
+    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
   }
 }
 
@@ -408,8 +461,6 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // One workgroup (16 waves, K split 16 ways) per output tile, one workgroup per CU.
 // Block 0 of an Adam-fused level also finalises the losses, takes the scalar
 // log_alpha step (alpha = exp(log_alpha), sac_imp.py:128-135) and fills the loss ring.
-// waves per SIMD the register allocation must allow: 4-wave tiles run one wave per SIMD
-// (full register file), 64x64 8-wave tiles two, the 16-wave tiles four
 // Row prologue of an axk-1 level (runs inside pre(), i.e. while the operand loads are in
 // flight): four threads per batch row sum the dot partials of its heads, the row's
 // thread loads r, d, logp meanwhile and turns the heads into the per-row coefficients
@@ -563,10 +614,24 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
   }
 }
 
+// K split per wave group of the batch-4096-class tile configurations (tuning knobs)
+#ifndef SACMI_FWD_KS
+#define SACMI_FWD_KS 4
+#endif
+#ifndef SACMI_AXK_KS
+#define SACMI_AXK_KS 8
+#endif
+#ifndef SACMI_DW_KS
+#define SACMI_DW_KS 8
+#endif
+#ifndef SACMI_PIPE
+#define SACMI_PIPE 0
+#endif
+
 // waves per SIMD the register allocation must allow: every wave of the workgroup
 // resident at once, one workgroup per CU
 template <int W>
-constexpr int gemm_min_waves() { return W >= 4 ? W / 4 : 1; }
+constexpr int gemm_min_waves() { return 4; }   // 16 waves per CU: one 1024- or two 512-thread WGs
 
 // TM x TN per wave group, MG wave groups (workgroup tile MG*TM x TN), K split KSPLIT
 // ways inside each group; ADAM: fused optimizer epilogue (every desc EPI_ADAM*); BF16:
@@ -687,7 +752,10 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
       }
     }
   };
-  gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16>(d, m0, n0, red, rsum, rowsum, pre, [] {});
+  // the plain (no Adam, no A transform) one-chunk-per-stage configurations pipeline their
+  // K loop (register budget: the Adam and transform variants already sit near 128 VGPRs)
+  constexpr bool PIPE = SACMI_PIPE && G == 1 && !ADAM && AXK == 0;
+  gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
   if constexpr (AXK == 1) {
     // the row prologue, after the MFMAs: its loads went out first and have long landed
@@ -805,8 +873,9 @@ static int assign_tiles(GemmBatch& b) {
 // one configuration, fp32 or bf16 MFMA operands (1024 threads)
 template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK>
 static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
-  if (b.bf16) hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, true>), dim3(grid), dim3(1024), 0, s, b);
-  else hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, false>), dim3(grid), dim3(1024), 0, s, b);
+  const dim3 blk(64 * KSPLIT * MG);
+  if (b.bf16) hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, true>), dim3(grid), blk, 0, s, b);
+  else hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, false>), dim3(grid), blk, 0, s, b);
 }
 
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
@@ -835,10 +904,27 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     // batch): 64x64 tiles as two 32-row wave groups, each with an 8-way K split — half
     // the operand bytes per FLOP of a 32x64 tile; the epilogue state is prefetched under
     // the MFMAs
+    // 16 waves per CU either as one 1024-thread workgroup (8-way K split per wave group)
+    // or as several smaller ones (4- / 2-way): then one workgroup's LDS reduction and
+    // epilogue overlap another's operand loads and MFMAs.  Rides attach to 1024 threads.
     const int g = assign_tiles<64, 64>(b) + extra;
-    if (n_adam) launch_k<32, 64, 8, 1, 2, true, 0>(b, g, s);
-    else if (axk == 1) launch_k<32, 64, 8, 1, 2, false, 1>(b, g, s);
-    else launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
+    if (n_adam) {
+      if (SACMI_DW_KS == 4 && !extra) launch_k<32, 64, 4, 1, 2, true, 0>(b, g, s);
+      else launch_k<32, 64, 8, 1, 2, true, 0>(b, g, s);
+    } else if (axk == 1) {
+      if (SACMI_AXK_KS == 4 && !extra) launch_k<32, 64, 4, 1, 2, false, 1>(b, g, s);
+      else launch_k<32, 64, 8, 1, 2, false, 1>(b, g, s);
+    } else if (dw) {
+      // the plain (data-parallel) form of a weight-gradient level: the fused form's geometry
+      if (SACMI_DW_KS == 4 && !extra) launch_k<32, 64, 4, 1, 2, false, 0>(b, g, s);
+      else launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
+    } else if (!extra && SACMI_FWD_KS == 2) {
+      launch_k<32, 64, 2, 1, 2, false, 0>(b, g, s);
+    } else if (!extra && SACMI_FWD_KS == 4) {
+      launch_k<32, 64, 4, 1, 2, false, 0>(b, g, s);
+    } else {
+      launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
+    }
   } else if (axk == 1) {
     // dh1 / dha1 with the fc3 backward folded in (A transform, coefficient in the epilogue)
     const int g = assign_tiles<32, 32>(b) + extra;

@@ -346,8 +346,308 @@ __global__ void k_per_wnorm(float* w, int k, const unsigned int* wmax_bits) {
   if (j < k) w[j] = w[j] / __uint_as_float(*wmax_bits);
 }
 
+// ---------------------------------------------------------------------------
+// Fused PER sampling: the same arithmetic as the kernels above (bit for bit) in three
+// (+1 fallback check) launches instead of nine (plus a memset):
+//   F1  pow + 8192-chunk pairwise sums (one workgroup per chunk, staged in LDS) and, in
+//       one extra workgroup, the numpy-MT uniforms; block 0 resets the flags/tickets
+//   F2  normalise + fixed-point block scan (k_per_norm_scan's body); F2b the sequential
+//       float64 cumsum fallback when a prob < 2^-29 was seen (one lane; else a no-op)
+//   F3  searchsorted with the cdf formed on the fly from the block-local fixed-point
+//       prefix and an LDS exclusive scan of the block totals (no cdf array), IS weights;
+//       the last workgroup divides by max(w)
+// Flags (PerArgs::bad): [0] fallback needed, [1] max-weight bits, [2] F2 ticket, [3] F3 ticket.
+constexpr int kFusedBlocksMax = 16384;   // fixed-point blocks F3 scans in LDS (16.7 M rows)
+
+__device__ void per_chunk_tree(float* buf, int n, float* chunk_out) {
+#pragma clang fp contract(off)
+  __shared__ int leaf_off[kChunk / 64], leaf_len[kChunk / 64];
+  __shared__ float leaf_val[kChunk / 64];
+  __shared__ int nleaf;
+  if (n == kChunk) {
+    constexpr int kLeaves = kChunk / kLeaf;   // 64
+    if (threadIdx.x < kLeaves) leaf_val[threadIdx.x] = pw_leaf(buf + threadIdx.x * kLeaf, kLeaf);
+    __syncthreads();
+    for (int w = kLeaves / 2; w >= 1; w >>= 1) {
+      float v = 0.f;
+      if (threadIdx.x < w) v = leaf_val[2 * threadIdx.x] + leaf_val[2 * threadIdx.x + 1];
+      __syncthreads();
+      if (threadIdx.x < w) leaf_val[threadIdx.x] = v;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *chunk_out = leaf_val[0];
+    return;
+  }
+  if (threadIdx.x == 0) {
+    int st_off[32], st_n[32], sp = 0, k = 0;
+    st_off[sp] = 0; st_n[sp] = n; ++sp;
+    while (sp) {
+      --sp;
+      const int o = st_off[sp], m = st_n[sp];
+      if (m <= kLeaf) { leaf_off[k] = o; leaf_len[k] = m; ++k; continue; }
+      int m2 = m / 2;
+      m2 -= m2 % 8;
+      st_off[sp] = o + m2; st_n[sp] = m - m2; ++sp;
+      st_off[sp] = o; st_n[sp] = m2; ++sp;
+    }
+    nleaf = k;
+  }
+  __syncthreads();
+  for (int l = threadIdx.x; l < nleaf; l += blockDim.x) leaf_val[l] = pw_leaf(buf + leaf_off[l], leaf_len[l]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int st_n[32], st_state[32], sp = 0, leaf = 0;
+    float st_left[32];
+    float result = 0.f;
+    st_n[sp] = n; st_state[sp] = 0; ++sp;
+    bool have = false;
+    float val = 0.f;
+    while (sp) {
+      const int top = sp - 1;
+      const int m = st_n[top];
+      if (m <= kLeaf) {
+        val = leaf_val[leaf++];
+        have = true;
+        --sp;
+      } else if (st_state[top] == 0) {
+        int m2 = m / 2;
+        m2 -= m2 % 8;
+        st_state[top] = 1;
+        st_n[sp] = m2; st_state[sp] = 0; ++sp;
+        continue;
+      } else if (st_state[top] == 1) {
+        st_left[top] = val;
+        int m2 = m / 2;
+        m2 -= m2 % 8;
+        st_state[top] = 2;
+        st_n[sp] = m - m2; st_state[sp] = 0; ++sp;
+        continue;
+      } else {
+        val = st_left[top] + val;
+        have = true;
+        --sp;
+      }
+      if (sp == 0 && have) result = val;
+    }
+    *chunk_out = (n > 0) ? result : -0.0f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
+  extern __shared__ __attribute__((aligned(16))) float dyn[];   // max(8192 floats, 2k words)
+  if ((int)blockIdx.x == nchunk) {    // the uniforms workgroup (k_per_uniforms' body)
+    __shared__ uint32_t key[kMtN];
+    uint32_t* words = reinterpret_cast<uint32_t*>(dyn);
+    const int t = threadIdx.x;
+    if (a.gen_u) {
+      for (int i = t; i < kMtN; i += blockDim.x) key[i] = a.mt[i];
+      int pos = (int)a.mt[kMtN];
+      __syncthreads();
+      const int need = 2 * a.k;
+      for (int done = 0; done < need;) {
+        if (pos >= kMtN) { mt_twist_block(key); pos = 0; }
+        const int take = min(kMtN - pos, need - done);
+        for (int j = t; j < take; j += blockDim.x) words[done + j] = mt_temper(key[pos + j]);
+        done += take;
+        pos += take;
+        __syncthreads();
+      }
+      for (int i = t; i < kMtN; i += blockDim.x) a.mt[i] = key[i];
+      if (t == 0) a.mt[kMtN] = (uint32_t)pos;
+      for (int j = t; j < a.k; j += blockDim.x)
+        a.u_scratch[j] = ((double)(words[2 * j] >> 5) * 67108864.0 + (double)(words[2 * j + 1] >> 6)) /
+                         9007199254740992.0;
+    } else {
+      for (int j = t; j < a.k; j += blockDim.x) a.u_scratch[j] = a.u[j];
+    }
+    if (t == 0) {
+      const double fr = (double)a.sc->per_frame;
+      double beta = a.beta_start + fr * (1.0 - a.beta_start) / a.beta_frames;
+      if (beta > 1.0) beta = 1.0;
+      a.u_scratch[a.k] = -beta;
+      a.sc->per_frame += 1;
+    }
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 4) a.bad[threadIdx.x] = 0;
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const int n = (int)((a.len - c0) < kChunk ? (a.len - c0) : kChunk);
+  float* buf = dyn;
+  if (n == kChunk) {
+    for (int q = threadIdx.x; q < kChunk / 4; q += blockDim.x) {
+      const float4 x = reinterpret_cast<const float4*>(a.prio + c0)[q];
+      const float4 y = make_float4(powf(x.x, a.alpha), powf(x.y, a.alpha), powf(x.z, a.alpha),
+                                   powf(x.w, a.alpha));
+      reinterpret_cast<float4*>(a.probs + c0)[q] = y;
+      reinterpret_cast<float4*>(buf)[q] = y;
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const float y = powf(a.prio[c0 + i], a.alpha);
+      a.probs[c0 + i] = y;
+      buf[i] = y;
+    }
+  }
+  __syncthreads();
+  per_chunk_tree(buf, n, a.chunk_sums + blockIdx.x);
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_per_f2(PerArgs a, int nchunk, int nb) {
+#pragma clang fp contract(off)
+  __shared__ float s_total;
+  __shared__ int64_t wsum[kScanBlock / 64];
+  if (threadIdx.x < 64) {
+    // the chunk sums added in chunk order (numpy): wave 0 loads 64 at a time in one
+    // coalesced burst, lane 0's running sum takes them one by one through shuffles
+    float t = -0.0f;
+    for (int c0 = 0; c0 < nchunk; c0 += 64) {
+      const int c = c0 + threadIdx.x;
+      const float v = c < nchunk ? a.chunk_sums[c] : 0.f;
+      const int m = nchunk - c0 < 64 ? nchunk - c0 : 64;
+      for (int l = 0; l < m; ++l) t = t + __shfl(v, l, 64);
+    }
+    if (threadIdx.x == 0) s_total = t;
+  }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kScanBlock + threadIdx.x;
+  int64_t v = 0;
+  if (i < a.len) {
+    const float p = a.probs[i] / s_total;
+    a.probs[i] = p;
+    if (p != 0.f && !(p >= 1.862645149230957e-09f)) atomicOr(a.bad, 1);   // 2^-29
+    v = (int64_t)((double)p * 4503599627370496.0);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int64_t base = 0;
+  for (int k = 0; k < w; ++k) base += wsum[k];
+  x += base;
+  if (i < a.len) a.q[i] = x;
+  if (threadIdx.x == kScanBlock - 1) a.block_sums[blockIdx.x] = x;
+}
+
+// F2b: the sequential float64 cumsum when the fixed point is not exact (a prob < 2^-29
+// was seen); a no-op otherwise.  Its own launch: a last-workgroup hand-off inside F2
+// would need a device-scope release per workgroup (an L2 writeback each, ~1000 of them).
+__global__ void k_per_f2b(PerArgs a) {
+  if (!*a.bad) return;
+  double sum = 0.0;
+  for (int64_t j = 0; j < a.len; ++j) { sum = sum + (double)a.probs[j]; a.cdf[j] = sum; }
+  const double last = a.cdf[a.len - 1];
+  for (int64_t j = 0; j < a.len; ++j) a.cdf[j] = a.cdf[j] / last;
+}
+
+__global__ __launch_bounds__(256) void k_per_f3(PerArgs a, int nb, int64_t stride, int ntop) {
+#pragma clang fp contract(off)
+  extern __shared__ int64_t off[];       // [nb] exclusive prefix of the block totals
+  __shared__ double top[kTopMax];
+  __shared__ int64_t wtot[4];
+  __shared__ int s_last;
+  const bool bad = __atomic_load_n(a.bad, __ATOMIC_RELAXED) != 0;
+  // exclusive scan of block_sums[0..nb) in chunks of 256 (k_per_scan_blocks' sums)
+  int64_t carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += 256) {
+    const int b = b0 + threadIdx.x;
+    const int64_t v = b < nb ? a.block_sums[b] : 0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[w] = x;
+    __syncthreads();
+    int64_t base = carry;
+    for (int k = 0; k < w; ++k) base += wtot[k];
+    if (b < nb) off[b] = base + x - v;
+    carry += wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    __syncthreads();
+  }
+  const int64_t len = a.len;
+  const double last = (double)(a.q[len - 1] + off[nb - 1]);
+  auto cdf_at = [&](int64_t e) -> double {
+    return bad ? a.cdf[e] : (double)(a.q[e] + off[e / kScanBlock]) / last;
+  };
+  for (int i = threadIdx.x; i < ntop; i += blockDim.x) {
+    const int64_t e = (int64_t)(i + 1) * stride - 1;
+    top[i] = cdf_at(e < len ? e : len - 1);
+  }
+  __syncthreads();
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  float pw = 0.f;
+  if (j < a.k) {
+    const double uj = a.u_scratch[j];
+    int tlo = 0, thi = ntop;
+    while (tlo < thi) {
+      const int mid = (tlo + thi) >> 1;
+      if (top[mid] > uj) thi = mid; else tlo = mid + 1;
+    }
+    int64_t lo = (int64_t)tlo * stride;
+    int64_t hi = lo + stride < len ? lo + stride : len;
+    if (lo > len) lo = len;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (cdf_at(mid) > uj) hi = mid; else lo = mid + 1;
+    }
+    if (lo > len - 1) lo = len - 1;
+    a.idx32[j] = (int32_t)lo;
+    a.idx_out[j] = lo;
+    pw = powf((float)len * a.probs[lo], (float)a.u_scratch[a.k]);
+    a.w_out[j] = pw;
+  }
+  unsigned int m = __float_as_uint(pw);
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+  unsigned int* wmax = reinterpret_cast<unsigned int*>(a.bad + 1);
+  if ((threadIdx.x & 63) == 0) atomicMax(wmax, m);
+  // last workgroup: w /= max(w)
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(a.bad + 3, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const float mx = __uint_as_float(__atomic_load_n(wmax, __ATOMIC_RELAXED));
+  for (int i = threadIdx.x; i < a.k; i += blockDim.x)
+    a.w_out[i] = __builtin_nontemporal_load(a.w_out + i) / mx;
+}
+
 void launch_per_sample(const PerArgs& a, hipStream_t s) {
   const int64_t len = a.len;
+  const int nb0 = (int)((len + kScanBlock - 1) / kScanBlock);
+  if (nb0 <= kFusedBlocksMax) {
+    const int nchunk = (int)((len + kChunk - 1) / kChunk);
+    size_t lds1 = (size_t)kChunk * 4;
+    if ((size_t)a.k * 8 > lds1) lds1 = (size_t)a.k * 8;
+    static size_t attr1 = 0, attr3 = 0;
+    if (lds1 > attr1) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_per_f1),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
+      attr1 = lds1;
+    }
+    hipLaunchKernelGGL(k_per_f1, dim3(nchunk + 1), dim3(256), lds1, s, a, nchunk);
+    hipLaunchKernelGGL(k_per_f2, dim3(nb0), dim3(kScanBlock), 0, s, a, nchunk, nb0);
+    hipLaunchKernelGGL(k_per_f2b, dim3(1), dim3(64), 0, s, a);
+    int64_t stride = 1024;
+    while ((len + stride - 1) / stride > kTopMax) stride *= 2;
+    const int ntop = (int)((len + stride - 1) / stride);
+    const size_t lds3 = (size_t)nb0 * 8;
+    if (lds3 > attr3) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_per_f3),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds3);
+      attr3 = lds3;
+    }
+    hipLaunchKernelGGL(k_per_f3, dim3((a.k + 255) / 256), dim3(256), lds3, s, a, nb0, stride, ntop);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) fprintf(stderr, "sacmi: PER launch failed: %s\n", hipGetErrorString(e));
+    return;
+  }
+  // very large rings: the unfused sequence
   int64_t blocks = (len + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(k_per_pow, dim3((unsigned)blocks), dim3(256), 0, s, a.prio, len, a.alpha, a.probs);

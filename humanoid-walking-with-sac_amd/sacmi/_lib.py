@@ -17,7 +17,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsacmi.so")
+LIB_PATH = os.environ.get("SACMI_LIB_PATH") or os.path.join(_HERE, "libsacmi.so")   # override: tuning builds
 ABI_VERSION = 2
 
 c_f32p = ctypes.POINTER(ctypes.c_float)

@@ -236,6 +236,39 @@ def test_device_random_sample_after_wraparound():
     assert np.array_equal(rows_s[:, 0], np.arange(n - cap, n, dtype=np.float32))
 
 
+@pytest.mark.parametrize("replay", ["uniform", "per"])
+def test_push_chunks_and_wrap_exact(replay):
+    """Ingest through the pinned staging slots (1024-row chunks, two slots in flight):
+    pushes of 1, 1023, 1500 and 3000 rows into a 2500-row ring — chunk edges, ring wrap
+    inside a chunk, a push larger than the ring (deque(maxlen) keeps the last rows) —
+    land bit for bit in deque order; the device fill the sampler reads matches len."""
+    S, A = 37, 5
+    cfg = SacConfig(S, A, 16)
+    cap = 2500
+    ctx = make_ctx(cfg, max_batch=64, capacity=cap, replay=replay)
+    rng = np.random.default_rng(5)
+    hist = []
+    for n in (1, 1023, 1500, 3000, 7):
+        rows = (rng.standard_normal((n, S)).astype(np.float32),
+                rng.standard_normal((n, A)).astype(np.float32),
+                rng.standard_normal(n).astype(np.float32),
+                rng.standard_normal((n, S)).astype(np.float32),
+                rng.random(n) < 0.3)
+        ctx.push(*rows)
+        hist.append(rows)
+        want = [np.concatenate([h[j] for h in hist])[-cap:] for j in range(5)]
+        L = min(cap, len(want[2]))
+        assert len(ctx) == L
+        got = ctx.get_rows(np.arange(L))
+        for j in range(5):
+            assert np.array_equal(got[j], want[j]), (n, j)
+    if replay == "uniform":
+        idx = ctx.sample_indices(64)
+        assert idx.min() >= 0 and idx.max() < cap and len(set(idx.tolist())) == 64
+    else:
+        assert ctx.per_priorities(cap).max() == 1.0
+
+
 def test_polyak_bitexact_and_determinism():
     cfg = SacConfig(24, 4, 64)
     params = init_params(cfg, 51, bias_scale=0.05)

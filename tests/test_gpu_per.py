@@ -113,3 +113,26 @@ def test_per_driven_update_runs_and_uses_slots():
     lg = c.step(64, eps1=np.zeros((64, 4), np.float32), eps2=np.zeros((64, 4), np.float32))
     want = np.array([L["q1_loss"], L["q2_loss"], L["policy_loss"]])
     np.testing.assert_allclose(lg, want, rtol=1e-5)
+
+
+@pytest.mark.parametrize("n,batch,bad", [(300_001, 4096, False), (70_000, 1000, True)])
+def test_per_many_blocks_vs_oracle(n, batch, bad):
+    """The fused 3-launch PER path over many 8192-row chunks and 1024-row scan blocks
+    (block-total scan in LDS over >256 blocks, ragged last chunk and block): indices
+    bit-exact vs the numpy-semantics oracle; the sequential-cumsum fallback too."""
+    ctx = _ctx(n + 5, batch)
+    _push(ctx, n)
+    rng = np.random.default_rng(11)
+    prio = rng.uniform(0.01, 2.0, n + 5).astype(np.float32)
+    if bad:
+        prio[::13] = np.float32(1e-25)
+    ctx.per_set_priorities(prio)
+    np.random.seed(5)
+    st = np.random.get_state()
+    ctx.set_mt(1, st[1], st[2])
+    idx, w = ctx.per_sample(batch)
+    probs = P.probs_from(prio, n)
+    ridx, rw = P.sample_from_probs(probs, batch, MT19937.from_npstate(st), P.beta_at(1))
+    assert np.array_equal(idx, ridx)
+    ulp = np.spacing(np.maximum(np.abs(rw), np.float32(1e-30)))
+    assert np.all(np.abs(w - rw) <= 4 * ulp)

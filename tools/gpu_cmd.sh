@@ -1,5 +1,5 @@
 set -e
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-bash tools/gpu_round.sh test
-timeout -k 10 300 python bench.py --no-cpu-baseline --no-roofline --steps 100 > $O/tl.json 2> $O/tl.err
+export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O/perprof -o run -- python3 tools/per_probe.py > $O/perprof.log 2>&1
