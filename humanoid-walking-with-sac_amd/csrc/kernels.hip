@@ -205,10 +205,12 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // MFMAs: a(b,k) = A>0 ? coef[row]*w[k] : 0 with coef in LDS (coef[tile row]); with
 // store_a the transformed fragments are also written to d.ax_out.
 // PIPE (G == 1, AXF == 0): software-pipelined K loop — chunk j+1's loads are in flight
-// while chunk j's MFMAs run (two register buffers), and the epilogue operands (pre) go
-// out right behind chunk 0's loads.  Same chunk order per wave: bitwise identical sums.
+// while chunk j's MFMAs run (two register buffers); the epilogue operands (pre) go out
+// right behind chunk 0's loads (PIPE 1) or after the loop (PIPE 2: deep-K levels, whose
+// registers then hold the second buffer instead).  Same chunk order per wave: bitwise
+// identical sums.
 template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
-          int AXF = 0, bool BF16 = false, bool PIPE = false, class Pre, class Early = void (*)()>
+          int AXF = 0, bool BF16 = false, int PIPE = 0, class Pre, class Early = void (*)()>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
                                             float* rsum, Pre&& pre, bool store_a = false,
                                             Early&& early = [] {}) {
@@ -249,7 +251,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
                                store_a ? (uint32_t)(((size_t)(d.M - 1) * d.ax_ld + d.K) * 4) : 0u);
   early();
-  if constexpr (PIPE) {
+  if constexpr (PIPE != 0) {
     static_assert(G == 1 && AXF == 0, "pipelined K loop: one chunk per stage, no A transform");
     float a1[MT][4], b1[NT][4], xw1[4];
     auto issue = [&](int jj, float (&av)[MT][4], float (&bv)[NT][4], float (&xv)[4]) {
@@ -283,7 +285,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
     } else {
       issue(0, a[0], b[0], xw[0]);
       __builtin_amdgcn_sched_barrier(0);
-      pre();
+      if constexpr (PIPE == 1) pre();
       __builtin_amdgcn_sched_barrier(0);
       for (int j = 0; j < nmine; j += 2) {
         issue(j + 1, a1, b1, xw1);
@@ -295,6 +297,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
         if (j + 1 < nmine) consume(a1, b1, xw1);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr (PIPE == 2) pre();
     }
   } else {
   if (nmine == 0) pre();
@@ -382,7 +385,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
 // layout dispatch (wave-uniform, once per workgroup)
 // AXK: whether this kernel instantiation carries the A-transform path (launch_gemm picks
 // the variant from the level's descs): 1 -> axk 1 descs, 0 -> none.
-template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, bool PIPE, class Pre,
+template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, int PIPE, class Pre,
           class Early>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
                                           float* rsum, bool rowsum, Pre&& pre, Early&& early) {
@@ -619,13 +622,16 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
 #define SACMI_FWD_KS 4
 #endif
 #ifndef SACMI_AXK_KS
-#define SACMI_AXK_KS 8
+#define SACMI_AXK_KS 4
 #endif
 #ifndef SACMI_DW_KS
 #define SACMI_DW_KS 8
 #endif
 #ifndef SACMI_PIPE
 #define SACMI_PIPE 0
+#endif
+#ifndef SACMI_PIPE_DW
+#define SACMI_PIPE_DW 0
 #endif
 
 // waves per SIMD the register allocation must allow: every wave of the workgroup
@@ -754,7 +760,8 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   };
   // the plain (no Adam, no A transform) one-chunk-per-stage configurations pipeline their
   // K loop (register budget: the Adam and transform variants already sit near 128 VGPRs)
-  constexpr bool PIPE = SACMI_PIPE && G == 1 && !ADAM && AXK == 0;
+  constexpr int PIPE = (SACMI_PIPE && G == 1 && !ADAM && AXK == 0) ? 1
+                     : (SACMI_PIPE_DW && G == 1 && ADAM && MG == 2) ? 2 : 0;
   gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
   if constexpr (AXK == 1) {

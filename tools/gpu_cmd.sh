@@ -1,5 +1,8 @@
 set -e
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O/perprof -o run -- python3 tools/per_probe.py > $O/perprof.log 2>&1
+for v in base pdw; do
+  if [ $v = base ]; then L=""; else L=$PWD/humanoid-walking-with-sac_amd/sacmi/libsacmi_$v.so; fi
+  SACMI_LIB_PATH=$L timeout -k 10 300 python bench.py --config 3 --no-cpu-baseline --no-trainer-loop --steps 100 > $O/c3_$v.json 2> $O/c3_$v.err
+  SACMI_LIB_PATH=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-trainer-loop --steps 200 > $O/c2_$v.json 2> $O/c2_$v.err
+done
