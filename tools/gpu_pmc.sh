@@ -5,7 +5,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out
-ARGS=${PMC_ARGS:---steps 100 --warmup 20 --fill 200000 --no-cpu-baseline --no-roofline}
+ARGS=${PMC_ARGS:---steps 100 --warmup 20 --fill 200000 --no-cpu-baseline --no-roofline --no-trainer-loop}
 cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   rm -rf $OUT/pmc_$C
