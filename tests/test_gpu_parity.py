@@ -129,6 +129,15 @@ def test_step_small_vs_oracle():
         break
 
 
+def test_step_bipedal_config1_vs_oracle():
+    """BASELINE configs[0] shapes (BipedalWalker-v3: obs 24, act 4, hidden 256, batch 256)."""
+    cfg = SacConfig(24, 4, 256)
+    params = init_params(cfg, 81, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 2000, 82, state_scale=0.5)
+    _, out = run_case(cfg, params, rows, B=256, steps=1, seed=83)
+    check_step(out[0], flat_params(params), "bipedal config 1 step 0")
+
+
 def test_step_humanoid_vs_oracle():
     cfg = SacConfig(376, 17, 512)
     params = init_params(cfg, 41, bias_scale=0.02)
@@ -352,9 +361,11 @@ def test_graph_and_eager_identical():
             assert np.array_equal(res[0][1][n][k], res[1][1][n][k])
 
 
-def test_dp_phase_path_matches_fused_step_world1():
+@pytest.mark.parametrize("n_hidden,dtype", [(2, "fp32"), (3, "fp32"), (2, "bf16")])
+def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype):
     """sacmi.dp over a 1-rank RCCL group (phases + in-place all-reduce on the adopted
-    torch gradient arena) == the fused single-graph update, bit for bit."""
+    torch gradient arena) == the fused single-graph update, bit for bit (also for
+    networks_model2 and the bf16 compute dtype)."""
     import socket
     import torch.distributed as dist
     from sacmi.dp import DataParallelUpdate, GpuBackend
@@ -362,13 +373,13 @@ def test_dp_phase_path_matches_fused_step_world1():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        cfg = SacConfig(24, 4, 64)
+        cfg = SacConfig(24, 4, 64, n_hidden=n_hidden)
         params = init_params(cfg, 71, bias_scale=0.05)
         rows = synthetic_rows(cfg, 400, 72, state_scale=0.5)
         key = (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32)
         ctxs = []
         for _ in range(2):
-            ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=3)
+            ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=3, compute_dtype=dtype)
             load_params(ctx, params)
             ctx.push(*rows)
             ctx.set_mt(0, key, 624)
@@ -389,7 +400,7 @@ def test_dp_phase_path_matches_fused_step_world1():
         from sacmi.dp import CapturedDataParallelUpdates
         cap = []
         for _ in range(2):
-            ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=3)
+            ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=3, compute_dtype=dtype)
             load_params(ctx, params)
             ctx.push(*rows)
             ctx.set_mt(0, key, 624)

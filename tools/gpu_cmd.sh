@@ -1,7 +1,7 @@
 set -e
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-bash tools/gpu_pmc.sh
-python3 tools/pmc_summary.py $O $O/pmc_c2.json > $O/pmc_c2.txt
-PMC_ARGS="--config 3 --steps 40 --warmup 10 --fill 200000 --no-cpu-baseline --no-roofline --no-trainer-loop" bash tools/gpu_pmc.sh
-python3 tools/pmc_summary.py $O $O/pmc_c3.json > $O/pmc_c3.txt
+for v in base t64 t65 t66; do
+  if [ $v = base ]; then L=""; else L=$PWD/humanoid-walking-with-sac_amd/sacmi/libsacmi_$v.so; fi
+  SACMI_LIB_PATH=$L timeout -k 10 300 python bench.py --config 3 --no-cpu-baseline --no-trainer-loop --steps 100 > $O/c3_$v.json 2> $O/c3_$v.err
+done
