@@ -178,3 +178,24 @@ def test_model2_dropin_checkpoint_and_update(tmp_path, golden_dir):
         for k, v in getattr(agent, n).state_dict().items():
             assert torch.equal(v, getattr(b, n).state_dict()[k]), (n, k)
     assert np.isfinite(b.update_parameters(64)["q1_loss"])
+
+
+def test_select_action_graph_replays_track_state():
+    """select_action replays one captured graph per (rows, evaluate): every call draws
+    fresh noise (device-side counter), and the replay reads the live weights (after an
+    update the deterministic action follows the new policy, == the CPU mirror)."""
+    agent = _agent()
+    _fill(agent, 300)
+    st = np.random.default_rng(2).standard_normal(S).astype(np.float32)
+    a1, a2 = agent.select_action(st), agent.select_action(st)
+    assert not np.array_equal(a1, a2)
+    d1 = agent.select_action(st, evaluate=True)
+    assert np.array_equal(d1, agent.select_action(st, evaluate=True))
+    for _ in range(3):
+        agent.update_parameters(64)
+    d2 = agent.select_action(st, evaluate=True)
+    assert not np.array_equal(d1, d2)
+    with torch.no_grad():
+        mean, _ = agent.policy(torch.from_numpy(st).unsqueeze(0))
+        ref = (torch.tanh(mean) * 0.4).numpy()[0]
+    np.testing.assert_allclose(d2, ref, rtol=1e-5, atol=1e-5)

@@ -1,7 +1,6 @@
 set -e
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-for v in base t64 t65 t66; do
-  if [ $v = base ]; then L=""; else L=$PWD/humanoid-walking-with-sac_amd/sacmi/libsacmi_$v.so; fi
-  SACMI_LIB_PATH=$L timeout -k 10 300 python bench.py --config 3 --no-cpu-baseline --no-trainer-loop --steps 100 > $O/c3_$v.json 2> $O/c3_$v.err
-done
+PYTEST_ARGS='-x -k "dropin or select or act"' bash tools/gpu_round.sh test
+timeout -k 10 200 python tools/act_probe.py > $O/act.log 2>&1
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-roofline > $O/tl.json 2> $O/tl.err
