@@ -271,6 +271,9 @@ def parse_args(argv=None):
                     help="updates per device launch (trainer.py updates_per_step loop)")
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel path even at world size 1 (overhead check)")
+    ap.add_argument("--dp-native", action="store_true",
+                    help="data parallel through sacmi_step_dp (the library issues the RCCL "
+                         "all-reduces) instead of torch.distributed around the phases")
     ap.add_argument("--no-trainer-loop", action="store_true",
                     help="skip the env-free trainer-loop measurement (select_action + push + "
                          "update_parameters per env step)")
@@ -282,8 +285,31 @@ def parse_args(argv=None):
     return args
 
 
+_RESULT_FD = None   # the process's original stdout while fd 1 is routed to stderr
+
+
+def quiet_stdout() -> None:
+    """Route fd 1 to stderr for the rest of the run (RCCL prints a version banner on
+    stdout at communicator creation, on every rank): the one JSON result line goes to
+    the original stdout through emit()."""
+    global _RESULT_FD
+    if _RESULT_FD is None:
+        sys.stdout.flush()
+        _RESULT_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(line: str) -> None:
+    sys.stdout.flush()
+    if _RESULT_FD is None:
+        print(line, flush=True)
+    else:
+        os.write(_RESULT_FD, (line + "\n").encode())
+
+
 def main():
     args = parse_args()
+    quiet_stdout()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -295,7 +321,7 @@ def main():
         from sacmi.dp import run_dp_bench
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        return run_dp_bench(args, rank, world, local_rank)
+        return run_dp_bench(args, rank, world, local_rank, emit)
 
     from sacmi import Config, Context
     torch.cuda.init()
@@ -337,7 +363,7 @@ def main():
     dt = time.perf_counter() - t0
     assert losses.shape == (args.steps, 3) and np.all(np.isfinite(losses)), losses[-3:]
     if args.profile_only:
-        print(json.dumps({"steps": args.steps, "ms_per_step": 1e3 * dt / args.steps}))
+        emit(json.dumps({"steps": args.steps, "ms_per_step": 1e3 * dt / args.steps}))
         return
     sps = args.steps / dt
 
@@ -403,7 +429,7 @@ def main():
         "roofline": roof, "cpu_baseline": cpu,
         "fill_seconds": round(t_fill, 2),
     }
-    print(json.dumps(out))
+    emit(json.dumps(out))
 
 
 if __name__ == "__main__":

@@ -6,6 +6,9 @@
 // one graph launch (the step is launch-latency bound at batch 256: SURVEY §7).
 #include "replay_dev.h"
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -140,6 +143,10 @@ struct sacmi_ctx {
   std::map<sacmi::GraphKey, hipGraphExec_t> graphs;
   bool use_graphs = true;
   bool G_external = false;
+  // native data parallel (sacmi_allreduce_init / sacmi_step_dp)
+  ncclComm_t comm = nullptr;
+  int dp_world = 0;
+  std::map<std::tuple<int, int, int64_t>, hipGraphExec_t> dp_graphs;   // (batch, n, PER fill)
   uint64_t act_calls = 0;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
   // profiling (sacmi_profile_step): one event per launch site
   bool prof = false;
@@ -172,6 +179,8 @@ static int guard(F&& f) {
 static void destroy_graphs(sacmi_ctx* c) {
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   c->graphs.clear();
+  for (auto& kv : c->dp_graphs) (void)hipGraphExecDestroy(kv.second);
+  c->dp_graphs.clear();
 }
 
 // ---------------------------------------------------------------------------
@@ -914,6 +923,79 @@ static void stage_inputs(sacmi_ctx* c, int B, const int64_t* idx, const float* e
   }
 }
 
+// ---------------------------------------------------------------------------
+// RCCL, loaded at run time: a process that already holds a librccl (e.g. torch's) shares
+// it — two copies of the collective runtime in one process would each own a transport —
+// else $SACMI_RCCL_PATH, else the dynamic loader's librccl.so.1.
+struct RcclApi {
+  void* h = nullptr;
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGetErrorString) err = nullptr;
+};
+
+static RcclApi& rccl() {
+  static RcclApi r;
+  if (r.h) return r;
+  void* h = nullptr;
+  for (const char* n : {"librccl.so", "librccl.so.1"}) {
+    if (!h) h = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
+  }
+  if (!h) {
+    if (const char* p = std::getenv("SACMI_RCCL_PATH")) h = dlopen(p, RTLD_NOW | RTLD_LOCAL);
+  }
+  for (const char* n : {"librccl.so.1", "librccl.so"}) {
+    if (!h) h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+  }
+  REQUIRE(h, SACMI_EDEVICE, std::string("RCCL not found (set SACMI_RCCL_PATH): ") + dlerror());
+  auto sym = [&](const char* name) {
+    void* f = dlsym(h, name);
+    REQUIRE(f, SACMI_EDEVICE, std::string("RCCL symbol missing: ") + name);
+    return f;
+  };
+  r.get_id = reinterpret_cast<decltype(r.get_id)>(sym("ncclGetUniqueId"));
+  r.init_rank = reinterpret_cast<decltype(r.init_rank)>(sym("ncclCommInitRank"));
+  r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(sym("ncclAllReduce"));
+  r.destroy = reinterpret_cast<decltype(r.destroy)>(sym("ncclCommDestroy"));
+  r.err = reinterpret_cast<decltype(r.err)>(sym("ncclGetErrorString"));
+  r.h = h;
+  return r;
+}
+
+#define CHECK_RCCL(x)                                                                \
+  do {                                                                               \
+    ncclResult_t r_ = (x);                                                           \
+    if (r_ != ncclSuccess) throw Error{SACMI_EDEVICE, std::string("RCCL: ") + rccl().err(r_)}; \
+  } while (0)
+
+// n data-parallel updates, enqueued on the context stream: the host-side driver of
+// sacmi/dp.py (DataParallelUpdate over one uninterrupted sequence) with the two
+// all-reduces per update issued here — sum in place on the gradient arena, 1/world
+// applied by the Adam kernels.
+static void enqueue_dp(sacmi_ctx* c, int B, int n) {
+  const float scale = 1.f / (float)c->dp_world;
+  const bool ride = n > 1 && ride_possible(c, B);
+  auto allreduce = [&](int64_t begin, int64_t end) {
+    float* g = c->G.p + begin;
+    CHECK_RCCL(rccl().all_reduce(g, g, (size_t)(end - begin), ncclFloat32, ncclSum, c->comm, c->stream));
+  };
+  int parity = 0;
+  bool have = false;
+  for (int r = 0; r < n; ++r) {
+    if (r > 0) enqueue_update(c, B, 1, 1, 4, scale, true, parity ^ 1);   // previous phase 2
+    enqueue_update(c, B, 1, 1, 1, scale, true, parity, have);            // phase 0
+    allreduce(c->q_begin, c->q_end);
+    const bool rn = ride && r + 1 < n;
+    enqueue_update(c, B, 1, 1, 2, scale, true, parity, false, rn);        // phase 1
+    allreduce(c->pi_begin, c->total);
+    have = rn;
+    parity = rn ? parity ^ 1 : 0;
+  }
+  enqueue_update(c, B, 1, 1, 4, scale, true, parity);                   // last phase 2
+}
+
 }  // namespace sacmi
 
 using namespace sacmi;
@@ -985,6 +1067,8 @@ int sacmi_destroy(sacmi_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     destroy_graphs(c);
     free_pinned(c);
+    if (c->comm) (void)rccl().destroy(c->comm);
+    c->comm = nullptr;
     if (c->G_external) {
       auto& reg = alloc_registry();
       for (size_t i = 0; i < reg.size(); ++i)
@@ -1331,6 +1415,66 @@ int sacmi_step_phase_ex(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_s
     REQUIRE(!pr.have_batch || ride_possible(c, batch), SACMI_EVALUE,
             "have_batch needs uniform replay with a ride-capable batch size");
     run_update(c, batch, 1, 1, phase == 3 ? 5 : 1 << phase, grad_scale, false, 1, pr);
+  });
+}
+
+int sacmi_allreduce_unique_id(void* id_out, int32_t nbytes) {
+  return guard([&] {
+    REQUIRE(id_out && nbytes >= (int32_t)sizeof(ncclUniqueId), SACMI_EVALUE,
+            "id buffer must hold SACMI_RCCL_ID_BYTES bytes");
+    static_assert(sizeof(ncclUniqueId) == SACMI_RCCL_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    CHECK_RCCL(rccl().get_id(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+  });
+}
+
+int sacmi_allreduce_init(sacmi_ctx* c, const void* id, int32_t nbytes, int32_t rank, int32_t world) {
+  return guard([&] {
+    REQUIRE(id && nbytes == (int32_t)sizeof(ncclUniqueId), SACMI_EVALUE, "bad RCCL unique id");
+    REQUIRE(world >= 1 && rank >= 0 && rank < world, SACMI_EVALUE, "bad rank / world");
+    REQUIRE(!c->comm, SACMI_ESTATE, "communicator already initialised");
+    CHECK_HIP(hipSetDevice(c->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm;
+    CHECK_RCCL(rccl().init_rank(&comm, world, uid, rank));
+    c->comm = comm;
+    c->dp_world = world;
+  });
+}
+
+int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
+  return guard([&] {
+    REQUIRE(c->comm, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
+    check_batch(c, batch);
+    REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    CHECK_HIP(hipStreamIsCapturing(c->stream, &cap));
+    if (!c->use_graphs || cap != hipStreamCaptureStatusNone) {
+      enqueue_dp(c, batch, n_updates);
+      CHECK_HIP(hipGetLastError());
+      return;
+    }
+    const auto key = std::make_tuple((int)batch, (int)n_updates,
+                                     c->cfg.replay_kind == SACMI_REPLAY_PER ? c->len : (int64_t)0);
+    auto it = c->dp_graphs.find(key);
+    if (it == c->dp_graphs.end()) {
+      hipGraph_t g;
+      CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      try {
+        enqueue_dp(c, batch, n_updates);
+      } catch (...) {
+        (void)hipStreamEndCapture(c->stream, &g);
+        throw;
+      }
+      CHECK_HIP(hipStreamEndCapture(c->stream, &g));
+      hipGraphExec_t ex;
+      CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      CHECK_HIP(hipGraphDestroy(g));
+      it = c->dp_graphs.emplace(key, ex).first;
+    }
+    CHECK_HIP(hipGraphLaunch(it->second, c->stream));
   });
 }
 

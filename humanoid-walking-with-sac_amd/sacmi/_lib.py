@@ -31,6 +31,7 @@ c_vp = ctypes.c_void_p
 SACMI_OK, SACMI_EVALUE, SACMI_ESTATE, SACMI_EDEVICE, SACMI_ENAN = range(5)
 REPLAY_UNIFORM, REPLAY_PER = 0, 1
 COMPUTE_FP32, COMPUTE_BF16 = 0, 1
+RCCL_ID_BYTES = 128          # SACMI_RCCL_ID_BYTES
 POLICY, Q1, Q2, Q1_TARGET, Q2_TARGET = range(5)
 SLOT_PARAM, SLOT_GRAD, SLOT_ADAM_M, SLOT_ADAM_V = range(4)
 (S_LOG_ALPHA, S_ALPHA, S_ALPHA_IS_TENSOR, S_STEP_POLICY, S_STEP_Q1, S_STEP_Q2, S_STEP_ALPHA,
@@ -89,6 +90,9 @@ _PROTOS = {
     "sacmi_per_get_priorities": [c_vp, c_f32p, ctypes.c_int64],
     "sacmi_per_set_priorities": [c_vp, c_f32p, ctypes.c_int64],
     "sacmi_act": [c_vp, c_f32p, ctypes.c_int32, ctypes.c_int32, c_f32p, c_f32p],
+    "sacmi_allreduce_unique_id": [ctypes.c_char_p, ctypes.c_int32],
+    "sacmi_allreduce_init": [c_vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32],
+    "sacmi_step_dp": [c_vp, ctypes.c_int32, ctypes.c_int32],
     "sacmi_profile_step": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
                            ctypes.c_int32, c_i32p],
     "sacmi_profile_sites": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,

@@ -234,6 +234,21 @@ class Context:
         else:
             L.call("sacmi_step_phase", self._h, int(batch), int(phase), float(grad_scale))
 
+    # -- native data parallel (RCCL issued by the library) ----------------------------
+    @staticmethod
+    def allreduce_unique_id() -> bytes:
+        """rank 0: a fresh RCCL unique id (SACMI_RCCL_ID_BYTES bytes) to hand to every rank."""
+        buf = ctypes.create_string_buffer(L.RCCL_ID_BYTES)
+        L.call("sacmi_allreduce_unique_id", buf, L.RCCL_ID_BYTES)
+        return buf.raw
+
+    def allreduce_init(self, unique_id: bytes, rank: int, world: int) -> None:
+        L.call("sacmi_allreduce_init", self._h, unique_id, len(unique_id), int(rank), int(world))
+
+    def step_dp(self, batch: int, n_updates: int = 1) -> None:
+        """n complete data-parallel updates (phases + library-issued RCCL all-reduces)."""
+        L.call("sacmi_step_dp", self._h, int(batch), int(n_updates))
+
     def ride_possible(self, batch: int) -> bool:
         out = ctypes.c_int32()
         L.call("sacmi_step_ride_possible", self._h, int(batch), ctypes.byref(out))

@@ -158,7 +158,7 @@ class CapturedDataParallelUpdates:
             self._graph(rem).replay()
 
 
-def run_dp_bench(args, rank: int, world: int, local_rank: int):
+def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     """bench.py --gpus N under torch.distributed.run (one rank per GPU)."""
     import bench as B
     from sacmi import Config, Context
@@ -179,7 +179,27 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int):
         ctx.push(*B.synth(min(chunk, fill - c0), 5000 + rank * 7919 + c0, S, A))
     per_launch = max(1, min(args.updates_per_launch, 256))
     captured = None
-    if os.environ.get("SACMI_DP_GRAPH", "1") == "1":
+    native = getattr(args, "dp_native", False)
+    if native:
+        # the library issues the all-reduces itself (sacmi_step_dp): RCCL unique id from
+        # rank 0, broadcast over the process group
+        uid = torch.zeros(128, dtype=torch.uint8, device=device)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(Context.allreduce_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        ctx.allreduce_init(bytes(uid.cpu().numpy().tobytes()), rank, world)
+        for n in {min(per_launch, args.steps), args.steps % per_launch, args.warmup % per_launch}:
+            if n > 0:
+                ctx.step_dp(args.batch, n)        # build the graphs (the updates are warm-up)
+        ctx.synchronize()
+
+        def run(k):
+            full, rem = divmod(k, per_launch)
+            for _ in range(full):
+                ctx.step_dp(args.batch, per_launch)
+            if rem:
+                ctx.step_dp(args.batch, rem)
+    elif os.environ.get("SACMI_DP_GRAPH", "1") == "1":
         try:
             captured = CapturedDataParallelUpdates(ctx, device, args.batch)
             captured.prepare(min(per_launch, args.steps), args.steps % per_launch,
@@ -189,14 +209,16 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int):
                 print(f"sacmi.dp: graph capture failed ({e}); eager updates", flush=True)
             captured = None
             torch.cuda.synchronize()
-    if captured is None:
+    if native:
+        pass
+    elif captured is None:
         upd = DataParallelUpdate(GpuBackend(ctx, device))
 
         def run(k):
             for _ in range(k):
                 upd(args.batch)
             upd.flush()
-    else:
+    elif captured is not None:
         def run(k):
             captured.run(k, per_launch)
     run(args.warmup)
@@ -235,12 +257,14 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int):
                        "global_batch": args.batch * world, "replay_fill": fill * world,
                        "parallelism": f"dp{world}"},
             "iterations_per_s": round(iters, 2),
-            "updates_per_launch": per_launch if captured else 1,
-            "dp_graph": captured is not None,
+            "updates_per_launch": per_launch if (captured or native) else 1,
+            "dp_graph": captured is not None or native,
+            "dp_driver": "library (sacmi_step_dp: RCCL issued by libsacmi)" if native
+                         else "torch.distributed (RCCL) around sacmi phases",
             "mfma_util_step": round(flops * value / 1e12 / peak / world, 4),
             "replicas_bitwise_equal": replicas_equal,
             "roofline": None, "cpu_baseline": None,
         }
-        print(json.dumps(out))
+        emit(json.dumps(out))
     dist.barrier()
     dist.destroy_process_group()

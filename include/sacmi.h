@@ -202,6 +202,26 @@ int sacmi_grad_buffer(sacmi_ctx* ctx, int which, void** device_ptr, int64_t* num
 int sacmi_grad_arena_numel(sacmi_ctx* ctx, int64_t* numel);
 int sacmi_attach_grad_arena(sacmi_ctx* ctx, void* device_ptr, int64_t numel);
 
+/* ---- native data parallel (RCCL over xGMI, no host framework) ------------------------ */
+/* The same split update with the two gradient all-reduces issued by the library itself
+ * (SURVEY §8(b) sacmi_allreduce_init; sac_imp.py:101-125 is the single-process update it
+ * distributes).  One process per GPU: rank 0 creates the RCCL unique id
+ * (sacmi_allreduce_unique_id, SACMI_RCCL_ID_BYTES bytes) and hands it to every rank by any
+ * host channel; each rank then calls sacmi_allreduce_init on its context.  RCCL is loaded
+ * at run time (dlopen: the process's already-loaded librccl if any, else
+ * $SACMI_RCCL_PATH, else librccl.so.1): libsacmi itself has no link dependency on it. */
+#define SACMI_RCCL_ID_BYTES 128
+int sacmi_allreduce_unique_id(void* id_out, int32_t nbytes);
+int sacmi_allreduce_init(sacmi_ctx* ctx, const void* id, int32_t nbytes, int32_t rank,
+                         int32_t world);
+/* n_updates complete data-parallel updates (every rank the same n): per update phase 0
+ * (phase 3 after the first), all-reduce(sum) of the critic gradients, phase 1,
+ * all-reduce of [actor gradients | dL/dlog_alpha], the last phase 2 at the end; updates
+ * 2..n take their minibatch from the previous update's ride-along sampling/gather when
+ * the replay allows it.  Captured into one hipGraph per (batch, n_updates); losses land in
+ * the loss ring (sacmi_fetch_losses).  Each rank samples its own replay shard. */
+int sacmi_step_dp(sacmi_ctx* ctx, int32_t batch, int32_t n_updates);
+
 /* ---- prioritized replay ------------------------------------------------------------ */
 /* PrioritizedReplayBuffer.sample(batch) indices + IS weights; u: NULL -> draw from
  * MT stream 1 on device, else [min(batch,len)] uniforms in [0,1).  Advances frame. */

@@ -475,3 +475,40 @@ def test_bf16_compute_vs_emulation(n_hidden):
     # the bf16 operands really were used: the fp32 path is ~1e-6 from the truth
     assert max(e_true.values()) > 1e-3, e_true
     assert not np.array_equal(res["fp32"][0], lb)
+
+
+@pytest.mark.parametrize("n_hidden", [2, 3])
+def test_native_dp_world1_matches_fused(n_hidden):
+    """sacmi_step_dp: the library's own RCCL data-parallel sequence (phases + in-place
+    all-reduces, one captured graph per (batch, n), ride-along sampling) over a 1-rank
+    communicator == the same number of fused single-GPU updates, bit for bit."""
+    from sacmi import Context
+    cfg = SacConfig(24, 4, 64, n_hidden=n_hidden)
+    params = init_params(cfg, 91, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 400, 92, state_scale=0.5)
+    key = (np.arange(624, dtype=np.uint64) * 69069 % (2**32)).astype(np.uint32)
+    ctxs = []
+    for _ in range(2):
+        ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=5)
+        load_params(ctx, params)
+        ctx.push(*rows)
+        ctx.set_mt(0, key, 624)
+        ctxs.append(ctx)
+    uid = Context.allreduce_unique_id()
+    assert len(uid) == 128
+    ctxs[0].allreduce_init(uid, 0, 1)
+    ctxs[0].step_dp(64, 5)
+    ctxs[0].step_dp(64, 1)
+    for _ in range(6):
+        ctxs[1].step(64)
+    ctxs[0].synchronize()
+    for n in NETS:
+        a, b = ctxs[0].get_net(n), ctxs[1].get_net(n)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (n, k)
+    from sacmi import _lib as L
+    assert ctxs[0].get_scalar(L.S_LOG_ALPHA) == ctxs[1].get_scalar(L.S_LOG_ALPHA)
+    hist = ctxs[0].fetch_losses(6)
+    assert hist.shape == (6, 3) and np.all(np.isfinite(hist))
+    with pytest.raises(Exception):
+        ctxs[1].step_dp(64, 1)            # no communicator on this context
