@@ -17,6 +17,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 
 namespace sacmi {
 
@@ -617,6 +618,13 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
   }
 }
 
+// LDS-staged 128x128 forward kernel for large-M levels (k_fwd) and its tile threshold
+#ifndef SACMI_FWD_BIG
+#define SACMI_FWD_BIG 1
+#endif
+#ifndef SACMI_FWD_BIG_MIN
+#define SACMI_FWD_BIG_MIN 1      // x 256 tiles of 128x128
+#endif
 // K split per wave group of the batch-4096-class tile configurations (tuning knobs)
 #ifndef SACMI_FWD_KS
 #define SACMI_FWD_KS 4
@@ -877,6 +885,166 @@ static int assign_tiles(GemmBatch& b) {
   return tot;
 }
 
+// ---------------------------------------------------------------------------
+// Large-M forward levels (batch-4096 class) in bf16 mode: LDS-staged 128x128 tiles.
+// C = relu(A . W^T [+ b]) with both operands K-contiguous (activations [rows][K],
+// nn.Linear weights [out][K]); [+ per-32-column fc3 dot partials].  Four waves (2x2),
+// each a 64x64 sub-tile over the FULL K (no K split, no partial-tile reduction): the
+// workgroup stages a 32-deep K slab of its 128 A rows and 128 W rows through LDS (double
+// buffered: the next slab's global loads are in flight while this slab's MFMAs run) and
+// every wave reads its fragments from LDS — each operand byte crosses L2->CU once per
+// workgroup instead of once per wave.  Two workgroups per CU.
+constexpr int kFBM = 128, kFBN = 128, kFBK = 32, kFPad = 4;
+
+template <bool BF16>
+__global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) float sA[2][kFBM][kFBK + kFPad];
+  __shared__ __attribute__((aligned(16))) float sB[2][kFBN][kFBK + kFPad];
+  const int bid = blockIdx.x;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  int tr, tc;
+  if (d.xcd_gr) {
+    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
+    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
+    tr = (x / gc) * sr + j / sc;
+    tc = (x % gc) * sc + j % sc;
+  } else {
+    tr = t / d.tiles_n;
+    tc = t % d.tiles_n;
+  }
+  const int m0 = tr * kFBM, n0 = tc * kFBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int M = d.M, N = d.N, K = d.K;
+  // staging: thread t moves rows (t >> 3) + 32 i (i < 4) at k = 4 (t & 7) of both slabs
+  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
+  uint32_t offA[4], offB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ra = min(m0 + (tid >> 3) + 32 * i, M - 1), rb = min(n0 + (tid >> 3) + 32 * i, N - 1);
+    offA[i] = (uint32_t)ra * (uint32_t)d.lda * 4u;
+    offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
+  }
+  const int kq = 4 * (tid & 7);
+  float4 ga[4], gb[4];
+  auto gload = [&](int k0) {
+    const int k = k0 + kq;
+    const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float4 x = buf_ld4(rA, offA[i] + ko), y = buf_ld4(rB, offB[i] + ko);
+      // elements past K read the row's next columns (or pads): zeroed
+      x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
+      y.x = k < K ? y.x : 0.f; y.y = k + 1 < K ? y.y : 0.f; y.z = k + 2 < K ? y.z : 0.f; y.w = k + 3 < K ? y.w : 0.f;
+      ga[i] = x; gb[i] = y;
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<float4*>(&sA[buf][(tid >> 3) + 32 * i][kq]) = ga[i];
+      *reinterpret_cast<float4*>(&sB[buf][(tid >> 3) + 32 * i][kq]) = gb[i];
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // epilogue operands (bias, dot weights) issued up front: they land under the K loop
+  float bias_x[4], dotw_x[4];
+  const bool has_bias = d.bias != nullptr, has_dot = d.dotp != nullptr;
+  const rsrc_t rX = make_rsrc(has_bias ? d.bias : d.C, has_bias ? 0x7fffffffu : 0u);
+  const rsrc_t rW = make_rsrc(has_dot ? d.dotw : d.C, has_dot ? (uint32_t)(N + 1) * 4u : 0u);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn + j * 16 + (lane & 15);
+    const int cc = col < N ? col : 0;
+    bias_x[j] = buf_ld(rX, (uint32_t)(cc * d.bias_ld) * 4u);
+    dotw_x[j] = col < N ? buf_ld(rW, (uint32_t)cc * 4u) : 0.f;
+  }
+  const float dotb = buf_ld(rW, (uint32_t)N * 4u);
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int nslab = (K + kFBK - 1) / kFBK;
+  for (int sl = 0; sl < nslab; ++sl) {
+    const int cur = sl & 1;
+    gload((sl + 1 < nslab ? sl + 1 : sl) * kFBK);   // unconditional: the last re-reads its slab
+#pragma unroll
+    for (int kk = 0; kk < kFBK / 16; ++kk) {
+      float a[4][4], b[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 x = *reinterpret_cast<const float4*>(&sA[cur][wm + i * 16 + (lane & 15)][kk * 16 + 4 * (lane >> 4)]);
+        a[i][0] = x.x; a[i][1] = x.y; a[i][2] = x.z; a[i][3] = x.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 y = *reinterpret_cast<const float4*>(&sB[cur][wn + j * 16 + (lane & 15)][kk * 16 + 4 * (lane >> 4)]);
+        b[j][0] = y.x; b[j][1] = y.y; b[j][2] = y.z; b[j][3] = y.w;
+      }
+      mfma_chunk<4, 4, BF16>(acc, a, b);
+    }
+    swrite(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue: lane holds D[row = (lane >> 4) * 4 + r][col = lane & 15] of each 16x16 tile
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+      float dsum[2] = {0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn + j * 16 + (lane & 15);
+        float v = acc[i][j][r];
+        if (has_bias) v += bias_x[j];
+        if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
+        if (row < M && col < N) d.C[(size_t)row * d.ldc + col] = v;
+        if (has_dot) {
+          // fc3 dot partial over the 32-column block (tiles j, j+1): 16 lanes per tile
+          float c = (row < M && col < N) ? v * dotw_x[j] : 0.f;
+#pragma unroll
+          for (int o = 8; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+          dsum[j >> 1] += c;
+        }
+      }
+      if (has_dot && (lane & 15) == 0 && row < M) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int blk = (n0 + wn) / 32 + h;
+          if (blk * 32 < N)
+            d.dotp[(size_t)row * d.dotp_ld + blk] = blk == 0 ? dsum[h] + dotb : dsum[h];
+        }
+      }
+    }
+  }
+}
+
+// whether launch_gemm may run a level on k_fwd: plain forward GEMMs (both operands
+// K-contiguous, store / ReLU epilogue, optional bias and dot partials), no prologue,
+// no rides, and enough 128x128 tiles to fill the chip
+static bool fwd_big_ok(GemmBatch& b) {
+  // bf16 only: with fp32 operands the 512-thread K-split tiles measured faster (config 3:
+  // 1,351 vs 1,229 updates/s); with bf16 MFMAs the levels are operand-traffic bound and
+  // the LDS sharing wins (config 5: 1,381 -> 1,458)
+  if (b.ride.kind || !b.bf16) return false;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    if (!d.a_kc || !d.b_kc || d.axk || d.a_ksc || d.rs_col >= 0) return false;
+    if (d.epi != EPI_RELU && d.epi != EPI_STORE) return false;
+    if (d.dotp && (d.N % 32)) return false;
+  }
+  return assign_tiles<kFBM, kFBN>(b) >= 256 * SACMI_FWD_BIG_MIN;
+}
+
 // one configuration, fp32 or bf16 MFMA operands (1024 threads)
 template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK>
 static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
@@ -888,6 +1056,14 @@ static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
+  static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
+  if (fwd_big && fwd_big_ok(b)) {
+    if (b.bf16) hipLaunchKernelGGL(k_fwd<true>, dim3(b.total_tiles), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL(k_fwd<false>, dim3(b.total_tiles), dim3(256), 0, s, b);
+    HIP_LAUNCH_CHECK();
+    return;
+  }
+  b = b0;
   const int extra = b.ride.kind ? b.ride.nblocks : 0;
   int maxk = 0, n_adam = 0;
   for (int i = 0; i < b.count; ++i) {
@@ -970,6 +1146,17 @@ __device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t counter, 
 
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;   // math.log(math.sqrt(2*pi))
 
+// 1 - tanh(x)^2 = sech(x)^2 = 4t / (1+t)^2 with t = exp(-2|x|): the reference's
+// `1 - y.pow(2)` (networks_model1.py:93) without its cancellation — for |x| ~ 4 the fp32
+// difference keeps only ~12 good bits, and those few saturated elements dominate the
+// policy gradient through 2y / (1 - y^2) (batch-4096 runs: 1e-4 normwise scatter between
+// fp32 evaluations otherwise; this form tracks the fp64 truth)
+__device__ __forceinline__ float one_minus_tanh2(float x) {
+  const float t = expf(-2.f * fabsf(x));
+  const float u = 1.f + t;
+  return 4.f * t / (u * u);
+}
+
 // ---------------------------------------------------------------------------
 // policy heads (mean | log_std) GEMM + GaussianPolicy.sample epilogue
 // (networks_model1.py:65-99, torch distributions/normal.py:83-103)
@@ -1022,9 +1209,10 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
       const float dx = x - mean;
       lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
-      lpe -= logf(a.scale * (1.f - y * y) + 1e-6f);
+      const float omy2 = one_minus_tanh2(x);
+      lpe -= logf(a.scale * omy2 + 1e-6f);
       float* cr = a.cache + (size_t)m * 3 * A;
-      cr[j] = mean; cr[A + j] = ls_raw; cr[2 * A + j] = y;
+      cr[j] = omy2; cr[A + j] = ls_raw; cr[2 * A + j] = y;
     }
     lp[row][j] = lpe;
   }
@@ -1085,7 +1273,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
   const int e = threadIdx.x;
   const int row = e / A, j = e % A, m = m0 + row;
   const bool live = e < TM * A && m < d.M;
-  float ls_raw = 0.f, y = 0.f, eps = 0.f;
+  float ls_raw = 0.f, y = 0.f, eps = 0.f, omy2 = 0.f;
   // the dhp2 tail's operands for this wave's first 32-column slab: Whead fragments and
   // the ReLU-mask source, also loaded under the dL/da MFMAs
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1122,6 +1310,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
   auto pre = [&]() {
     const int mm = live ? m : 0, jj = live ? j : 0;
     const float* cr = a.cache + (size_t)mm * 3 * A;
+    omy2 = cr[jj];
     ls_raw = cr[A + jj];
     y = cr[2 * A + jj];
     eps = a.eps[(size_t)mm * A + jj];
@@ -1134,7 +1323,6 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
     const float ga = reduce_partials<TM, TN, KSPLIT>(red, row, j);
     const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
     const float sd = expf(ls);
-    const float omy2 = 1.f - y * y;
     const float u = a.scale * omy2 + 1e-6f;
     const float G = a.scale * ga + glogp * (2.f * a.scale * y / u);
     const float dx = G * omy2;

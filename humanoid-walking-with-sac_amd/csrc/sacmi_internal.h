@@ -207,7 +207,7 @@ struct HeadSampleArgs {
   float* act;            // actions written to act[row*ldact + j]
   int ldact;
   float* logp;           // [rows]
-  float* cache;          // [rows, 3A]: mean | log_std(raw) | y
+  float* cache;          // [rows, 3A]: 1 - y^2 (as sech^2 x) | log_std(raw) | y
   float scale, bias;
   int deterministic;     // 1: action = tanh(mean)*scale+bias (select_action(evaluate=True))
   uint64_t ctr_override; // nonzero: Philox counter to use instead of sc->noise_counter
