@@ -622,6 +622,15 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
 #ifndef SACMI_FWD_BIG
 #define SACMI_FWD_BIG 1
 #endif
+#ifndef SACMI_FWD_BF16_N64
+#define SACMI_FWD_BF16_N64 1
+#endif
+#ifndef SACMI_FWD_BF16_ALL64
+#define SACMI_FWD_BF16_ALL64 0
+#endif
+#ifndef SACMI_FWD_BIG_FP32
+#define SACMI_FWD_BIG_FP32 0
+#endif
 #ifndef SACMI_FWD_BIG_MIN
 #define SACMI_FWD_BIG_MIN 1      // x 256 tiles of 128x128
 #endif
@@ -894,10 +903,11 @@ static int assign_tiles(GemmBatch& b) {
 // buffered: the next slab's global loads are in flight while this slab's MFMAs run) and
 // every wave reads its fragments from LDS — each operand byte crosses L2->CU once per
 // workgroup instead of once per wave.  Two workgroups per CU.
-constexpr int kFBM = 128, kFBN = 128, kFBK = 32, kFPad = 4;
+constexpr int kFBM = 128, kFBK = 32, kFPad = 4, kFBN128 = 128;
 
-template <bool BF16>
+template <bool BF16, int kFBN = 128>
 __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
+  constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
   __shared__ __attribute__((aligned(16))) float sA[2][kFBM][kFBK + kFPad];
   __shared__ __attribute__((aligned(16))) float sB[2][kFBN][kFBK + kFPad];
   const int bid = blockIdx.x;
@@ -919,50 +929,54 @@ __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
   }
   const int m0 = tr * kFBM, n0 = tc * kFBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (kFBN / 2);
   const int M = d.M, N = d.N, K = d.K;
+  constexpr int NB = kFBN / 32;          // B rows staged per thread (32 rows per pass)
   // staging: thread t moves rows (t >> 3) + 32 i (i < 4) at k = 4 (t & 7) of both slabs
   const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
-  uint32_t offA[4], offB[4];
+  uint32_t offA[4], offB[NB];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int ra = min(m0 + (tid >> 3) + 32 * i, M - 1), rb = min(n0 + (tid >> 3) + 32 * i, N - 1);
+    const int ra = min(m0 + (tid >> 3) + 32 * i, M - 1);
     offA[i] = (uint32_t)ra * (uint32_t)d.lda * 4u;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int rb = min(n0 + (tid >> 3) + 32 * i, N - 1);
     offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
   }
   const int kq = 4 * (tid & 7);
-  float4 ga[4], gb[4];
+  float4 ga[4], gb[NB];
+  auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
+    x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
+    return x;
+  };
   auto gload = [&](int k0) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float4 x = buf_ld4(rA, offA[i] + ko), y = buf_ld4(rB, offB[i] + ko);
-      // elements past K read the row's next columns (or pads): zeroed
-      x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
-      y.x = k < K ? y.x : 0.f; y.y = k + 1 < K ? y.y : 0.f; y.z = k + 2 < K ? y.z : 0.f; y.w = k + 3 < K ? y.w : 0.f;
-      ga[i] = x; gb[i] = y;
-    }
+    for (int i = 0; i < 4; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) gb[i] = zk(buf_ld4(rB, offB[i] + ko), k);
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<float4*>(&sA[buf][(tid >> 3) + 32 * i][kq]) = ga[i];
-      *reinterpret_cast<float4*>(&sB[buf][(tid >> 3) + 32 * i][kq]) = gb[i];
-    }
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&sA[buf][(tid >> 3) + 32 * i][kq]) = ga[i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) *reinterpret_cast<float4*>(&sB[buf][(tid >> 3) + 32 * i][kq]) = gb[i];
   };
-  f4 acc[4][4];
+  f4 acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   // epilogue operands (bias, dot weights) issued up front: they land under the K loop
-  float bias_x[4], dotw_x[4];
+  float bias_x[NT], dotw_x[NT];
   const bool has_bias = d.bias != nullptr, has_dot = d.dotp != nullptr;
   const rsrc_t rX = make_rsrc(has_bias ? d.bias : d.C, has_bias ? 0x7fffffffu : 0u);
   const rsrc_t rW = make_rsrc(has_dot ? d.dotw : d.C, has_dot ? (uint32_t)(N + 1) * 4u : 0u);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NT; ++j) {
     const int col = n0 + wn + j * 16 + (lane & 15);
     const int cc = col < N ? col : 0;
     bias_x[j] = buf_ld(rX, (uint32_t)(cc * d.bias_ld) * 4u);
@@ -978,18 +992,18 @@ __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
     gload((sl + 1 < nslab ? sl + 1 : sl) * kFBK);   // unconditional: the last re-reads its slab
 #pragma unroll
     for (int kk = 0; kk < kFBK / 16; ++kk) {
-      float a[4][4], b[4][4];
+      float a[4][4], b[NT][4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float4 x = *reinterpret_cast<const float4*>(&sA[cur][wm + i * 16 + (lane & 15)][kk * 16 + 4 * (lane >> 4)]);
         a[i][0] = x.x; a[i][1] = x.y; a[i][2] = x.z; a[i][3] = x.w;
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NT; ++j) {
         const float4 y = *reinterpret_cast<const float4*>(&sB[cur][wn + j * 16 + (lane & 15)][kk * 16 + 4 * (lane >> 4)]);
         b[j][0] = y.x; b[j][1] = y.y; b[j][2] = y.z; b[j][3] = y.w;
       }
-      mfma_chunk<4, 4, BF16>(acc, a, b);
+      mfma_chunk<4, NT, BF16>(acc, a, b);
     }
     swrite(cur ^ 1);
     __syncthreads();
@@ -1002,7 +1016,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
       const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
       float dsum[2] = {0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NT; ++j) {
         const int col = n0 + wn + j * 16 + (lane & 15);
         float v = acc[i][j][r];
         if (has_bias) v += bias_x[j];
@@ -1018,7 +1032,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
       }
       if (has_dot && (lane & 15) == 0 && row < M) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < NT / 2; ++h) {
           const int blk = (n0 + wn) / 32 + h;
           if (blk * 32 < N)
             d.dotp[(size_t)row * d.dotp_ld + blk] = blk == 0 ? dsum[h] + dotb : dsum[h];
@@ -1035,14 +1049,17 @@ static bool fwd_big_ok(GemmBatch& b) {
   // bf16 only: with fp32 operands the 512-thread K-split tiles measured faster (config 3:
   // 1,351 vs 1,229 updates/s); with bf16 MFMAs the levels are operand-traffic bound and
   // the LDS sharing wins (config 5: 1,381 -> 1,458)
-  if (b.ride.kind || !b.bf16) return false;
+  if (b.ride.kind || (!b.bf16 && !SACMI_FWD_BIG_FP32)) return false;
   for (int i = 0; i < b.count; ++i) {
     const GemmDesc& d = b.d[i];
     if (!d.a_kc || !d.b_kc || d.axk || d.a_ksc || d.rs_col >= 0) return false;
     if (d.epi != EPI_RELU && d.epi != EPI_STORE) return false;
     if (d.dotp && (d.N % 32)) return false;
   }
-  return assign_tiles<kFBM, kFBN>(b) >= 256 * SACMI_FWD_BIG_MIN;
+  // 128-column tiles when they give two workgroups per CU, else 64-column ones
+  if (b.bf16 && (!SACMI_FWD_BF16_N64 || (assign_tiles<kFBM, 128>(b) >= 512 && !SACMI_FWD_BF16_ALL64)))
+    return assign_tiles<kFBM, 128>(b) >= 256 * SACMI_FWD_BIG_MIN;
+  return assign_tiles<kFBM, 64>(b) >= 512 * SACMI_FWD_BIG_MIN;
 }
 
 // one configuration, fp32 or bf16 MFMA operands (1024 threads)
@@ -1058,8 +1075,10 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   GemmBatch b = b0;
   static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
   if (fwd_big && fwd_big_ok(b)) {
-    if (b.bf16) hipLaunchKernelGGL(k_fwd<true>, dim3(b.total_tiles), dim3(256), 0, s, b);
-    else hipLaunchKernelGGL(k_fwd<false>, dim3(b.total_tiles), dim3(256), 0, s, b);
+    const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
+    if (b.bf16 && n128) hipLaunchKernelGGL((k_fwd<true, 128>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    else if (b.bf16) hipLaunchKernelGGL((k_fwd<true, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((k_fwd<false, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
     HIP_LAUNCH_CHECK();
     return;
   }

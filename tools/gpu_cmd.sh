@@ -1,5 +1,6 @@
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-PYTEST_ARGS='-k "b4096 or bf16"' bash tools/gpu_round.sh test
-timeout -k 10 300 python bench.py --config 3 --no-cpu-baseline --no-trainer-loop --steps 100 > $O/c3.json 2> $O/c3.err
+L=$PWD/humanoid-walking-with-sac_amd/sacmi
+timeout -k 10 300 python bench.py --config 5 --no-cpu-baseline --no-trainer-loop --steps 100 > $O/c5_base.json 2> $O/c5.err
+SACMI_LIB_PATH=$L/libsacmi_all64.so timeout -k 10 300 python bench.py --config 5 --no-cpu-baseline --no-trainer-loop --steps 100 > $O/c5_all64.json 2> $O/c5b.err
 true
