@@ -396,7 +396,9 @@ def main():
                 "traffic_unit": "bytes past L2 per k_gemm launch (PMC)",
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": round(info["gemm_bytes"] / info["launches"]),
-                "kernel": f"sacmi::k_gemm (grouped {wl['dtype']} MFMA GEMM, all tile configs)",
+                "kernel": f"sacmi::k_gemm (grouped {wl['dtype']} MFMA GEMM, all tile configs)"
+                          + (" + sacmi::k_fwd (LDS-staged large-M forward levels)"
+                             if wl["dtype"] == "bf16" and args.batch >= 2048 else ""),
                 "launches_per_step": info["launches"],
                 "avg_launch_us": round(info["avg_launch_us"], 3),
                 "gemm_flops_per_step": info["gemm_flops"],
