@@ -492,10 +492,14 @@ __global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
   per_chunk_tree(buf, n, a.chunk_sums + blockIdx.x);
 }
 
-__global__ __launch_bounds__(kScanBlock) void k_per_f2(PerArgs a, int nchunk, int nb) {
+// 256 threads per 1024-row scan block, 4 consecutive rows per thread: every block's
+// workgroup is resident at once (the integer prefix is exact, so the grouping does not
+// change a bit of q)
+constexpr int kF2Threads = 256;
+__global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a, int nchunk, int nb) {
 #pragma clang fp contract(off)
   __shared__ float s_total;
-  __shared__ int64_t wsum[kScanBlock / 64];
+  __shared__ int64_t wsum[kF2Threads / 64];
   if (threadIdx.x < 64) {
     // the chunk sums added in chunk order (numpy): wave 0 loads 64 at a time in one
     // coalesced burst, lane 0's running sum takes them one by one through shuffles
@@ -508,28 +512,41 @@ __global__ __launch_bounds__(kScanBlock) void k_per_f2(PerArgs a, int nchunk, in
     }
     if (threadIdx.x == 0) s_total = t;
   }
+  const int64_t i0 = (int64_t)blockIdx.x * kScanBlock + 4 * threadIdx.x;
+  float pin[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) pin[e] = i0 + e < a.len ? a.probs[i0 + e] : 0.f;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * kScanBlock + threadIdx.x;
-  int64_t v = 0;
-  if (i < a.len) {
-    const float p = a.probs[i] / s_total;
-    a.probs[i] = p;
-    if (p != 0.f && !(p >= 1.862645149230957e-09f)) atomicOr(a.bad, 1);   // 2^-29
-    v = (int64_t)((double)p * 4503599627370496.0);
+  int64_t v[4];
+  int64_t run = 0;
+  bool badp = false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = 0;
+    if (i0 + e < a.len) {
+      const float p = pin[e] / s_total;
+      a.probs[i0 + e] = p;
+      badp = badp || (p != 0.f && !(p >= 1.862645149230957e-09f));   // 2^-29
+      v[e] = (int64_t)((double)p * 4503599627370496.0);
+    }
+    run += v[e];
+    v[e] = run;                        // thread-local inclusive prefix
   }
+  if (badp) atomicOr(a.bad, 1);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int64_t x = v;
+  int64_t x = run;
   for (int o = 1; o < 64; o <<= 1) {
     const int64_t y = __shfl_up(x, o, 64);
     if (lane >= o) x += y;
   }
   if (lane == 63) wsum[w] = x;
   __syncthreads();
-  int64_t base = 0;
+  int64_t base = x - run;              // exclusive prefix of this thread inside its wave
   for (int k = 0; k < w; ++k) base += wsum[k];
-  x += base;
-  if (i < a.len) a.q[i] = x;
-  if (threadIdx.x == kScanBlock - 1) a.block_sums[blockIdx.x] = x;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (i0 + e < a.len) a.q[i0 + e] = base + v[e];
+  if (threadIdx.x == kF2Threads - 1) a.block_sums[blockIdx.x] = base + v[3];
 }
 
 // F2b: the sequential float64 cumsum when the fixed point is not exact (a prob < 2^-29
@@ -631,7 +648,7 @@ void launch_per_sample(const PerArgs& a, hipStream_t s) {
       attr1 = lds1;
     }
     hipLaunchKernelGGL(k_per_f1, dim3(nchunk + 1), dim3(256), lds1, s, a, nchunk);
-    hipLaunchKernelGGL(k_per_f2, dim3(nb0), dim3(kScanBlock), 0, s, a, nchunk, nb0);
+    hipLaunchKernelGGL(k_per_f2, dim3(nb0), dim3(kF2Threads), 0, s, a, nchunk, nb0);
     hipLaunchKernelGGL(k_per_f2b, dim3(1), dim3(64), 0, s, a);
     int64_t stride = 1024;
     while ((len + stride - 1) / stride > kTopMax) stride *= 2;
