@@ -622,6 +622,9 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
 #ifndef SACMI_FWD_BIG
 #define SACMI_FWD_BIG 1
 #endif
+#ifndef SACMI_DW_SPLIT
+#define SACMI_DW_SPLIT 1
+#endif
 #ifndef SACMI_FWD_BF16_N64
 #define SACMI_FWD_BF16_N64 1
 #endif
@@ -904,6 +907,68 @@ static int assign_tiles(GemmBatch& b) {
 // every wave reads its fragments from LDS — each operand byte crosses L2->CU once per
 // workgroup instead of once per wave.  Two workgroups per CU.
 constexpr int kFBM = 128, kFBK = 32, kFPad = 4, kFBN128 = 128;
+#ifndef SACMI_FWD_LDS16
+#define SACMI_FWD_LDS16 0       // bf16 mode: k_fwd16 (bf16 LDS slabs, 16x16x32 MFMA)
+#endif
+
+// k_fwd / k_fwd16 epilogue: bias, ReLU, store, per-32-column fc3 dot partials.  A wave
+// owns a 64 x (16 NT) sub-tile at (r0, c0); lane holds D[row = (lane >> 4) * 4 + r]
+// [col = lane & 15] of each 16x16 tile.  The operands are loaded before the K loop.
+template <int NT>
+struct FwdEpi {
+  float bias_x[NT], dotw_x[NT], dotb;
+  __device__ __forceinline__ void load(const GemmDesc& d, int c0, int lane) {
+    const int N = d.N;
+    const bool has_bias = d.bias != nullptr, has_dot = d.dotp != nullptr;
+    const rsrc_t rX = make_rsrc(has_bias ? d.bias : d.C, has_bias ? 0x7fffffffu : 0u);
+    const rsrc_t rW = make_rsrc(has_dot ? d.dotw : d.C, has_dot ? (uint32_t)(N + 1) * 4u : 0u);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = c0 + j * 16 + (lane & 15);
+      const int cc = col < N ? col : 0;
+      bias_x[j] = buf_ld(rX, (uint32_t)(cc * d.bias_ld) * 4u);
+      dotw_x[j] = col < N ? buf_ld(rW, (uint32_t)cc * 4u) : 0.f;
+    }
+    dotb = buf_ld(rW, (uint32_t)N * 4u);
+  }
+  __device__ __forceinline__ void store(const GemmDesc& d, const f4 (&acc)[4][NT], int r0, int c0,
+                                        int lane) const {
+    const int M = d.M, N = d.N;
+    const bool has_bias = d.bias != nullptr, has_dot = d.dotp != nullptr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + i * 16 + (lane >> 4) * 4 + r;
+        float dsum[NT / 2 > 0 ? NT / 2 : 1] = {};
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int col = c0 + j * 16 + (lane & 15);
+          float v = acc[i][j][r];
+          if (has_bias) v += bias_x[j];
+          if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
+          if (row < M && col < N) d.C[(size_t)row * d.ldc + col] = v;
+          if (has_dot) {
+            // fc3 dot partial over the 32-column block (tiles j, j+1): 16 lanes per tile
+            float c = (row < M && col < N) ? v * dotw_x[j] : 0.f;
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+            dsum[j >> 1] += c;
+          }
+        }
+        if (has_dot && (lane & 15) == 0 && row < M) {
+#pragma unroll
+          for (int h = 0; h < NT / 2; ++h) {
+            const int blk = c0 / 32 + h;
+            if (blk * 32 < N)
+              d.dotp[(size_t)row * d.dotp_ld + blk] = blk == 0 ? dsum[h] + dotb : dsum[h];
+          }
+        }
+      }
+    }
+  }
+};
+
 
 template <bool BF16, int kFBN = 128>
 __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
@@ -971,18 +1036,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   // epilogue operands (bias, dot weights) issued up front: they land under the K loop
-  float bias_x[NT], dotw_x[NT];
-  const bool has_bias = d.bias != nullptr, has_dot = d.dotp != nullptr;
-  const rsrc_t rX = make_rsrc(has_bias ? d.bias : d.C, has_bias ? 0x7fffffffu : 0u);
-  const rsrc_t rW = make_rsrc(has_dot ? d.dotw : d.C, has_dot ? (uint32_t)(N + 1) * 4u : 0u);
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int col = n0 + wn + j * 16 + (lane & 15);
-    const int cc = col < N ? col : 0;
-    bias_x[j] = buf_ld(rX, (uint32_t)(cc * d.bias_ld) * 4u);
-    dotw_x[j] = col < N ? buf_ld(rW, (uint32_t)cc * 4u) : 0.f;
-  }
-  const float dotb = buf_ld(rW, (uint32_t)N * 4u);
+  FwdEpi<NT> ep;
+  ep.load(d, n0 + wn, lane);
   gload(0);
   swrite(0);
   __syncthreads();
@@ -1008,38 +1063,343 @@ __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
     swrite(cur ^ 1);
     __syncthreads();
   }
-  // epilogue: lane holds D[row = (lane >> 4) * 4 + r][col = lane & 15] of each 16x16 tile
+  ep.store(d, acc, m0 + wm, n0 + wn, lane);
+}
+
+// bf16 mode, bf16 in LDS: the staging rounds every fp32 operand ONCE per workgroup
+// (v_cvt_pk_bf16_f32) and stores [row][k] bf16 slabs 64 deep; a lane's 8 consecutive k
+// of one row are one ds_read_b128 and exactly its v_mfma_f32_16x16x32_bf16 operand
+// (lane l: A[l&15][8(l>>4) + j], B[8(l>>4) + j][l&15]).  Against k_fwd<true>: half the
+// LDS bytes per MFMA, one conversion per element per workgroup instead of per wave, half
+// the MFMA issues, and half the barriers / load round trips per K.  Same tiles, XCD
+// order and epilogue as k_fwd.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+constexpr int kHBK = 64, kHPad = 8;
+
+__device__ __forceinline__ u2v pack_bf16x4(float4 v) {
+  const bf16x4 x = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+  return __builtin_bit_cast(u2v, x);
+}
+
+template <int kFBN>
+__global__ __launch_bounds__(256, 2) void k_fwd16(GemmBatch batch) {
+  constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
+  constexpr int LDR = kHBK + kHPad;      // bf16 per LDS row: 144 B
+  constexpr int NB = kFBN / 16;          // B rows staged per thread (16 rows per pass)
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][kFBM][LDR];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][kFBN][LDR];
+  const int bid = blockIdx.x;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  int tr, tc;
+  if (d.xcd_gr) {
+    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
+    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
+    tr = (x / gc) * sr + j / sc;
+    tc = (x % gc) * sc + j % sc;
+  } else {
+    tr = t / d.tiles_n;
+    tc = t % d.tiles_n;
+  }
+  const int m0 = tr * kFBM, n0 = tc * kFBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (kFBN / 2);
+  const int M = d.M, N = d.N, K = d.K;
+  // staging: thread t moves rows (t >> 4) + 16 i at k = 4 (t & 15) of both slabs
+  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
+  uint32_t offA[8], offB[NB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 8; ++i) {
+    const int ra = min(m0 + (tid >> 4) + 16 * i, M - 1);
+    offA[i] = (uint32_t)ra * (uint32_t)d.lda * 4u;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int rb = min(n0 + (tid >> 4) + 16 * i, N - 1);
+    offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
+  }
+  const int kq = 4 * (tid & 15);
+  float4 ga[8], gb[NB];
+  auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
+    x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
+    return x;
+  };
+  auto gload = [&](int k0) {
+    const int k = k0 + kq;
+    const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) gb[i] = zk(buf_ld4(rB, offB[i] + ko), k);
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<u2v*>(&sA[buf][(tid >> 4) + 16 * i][kq]) = pack_bf16x4(ga[i]);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) *reinterpret_cast<u2v*>(&sB[buf][(tid >> 4) + 16 * i][kq]) = pack_bf16x4(gb[i]);
+  };
+  f4 acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  FwdEpi<NT> ep;
+  ep.load(d, n0 + wn, lane);
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int nslab = (K + kHBK - 1) / kHBK;
+  for (int sl = 0; sl < nslab; ++sl) {
+    const int cur = sl & 1;
+    gload((sl + 1 < nslab ? sl + 1 : sl) * kHBK);   // unconditional: the last re-reads its slab
+#pragma unroll
+    for (int kk = 0; kk < kHBK / 32; ++kk) {
+      const int kc = kk * 32 + 8 * (lane >> 4);
+      bf16x8 a[4], b[NT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][wm + i * 16 + (lane & 15)][kc]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][wn + j * 16 + (lane & 15)][kc]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    swrite(cur ^ 1);
+    __syncthreads();
+  }
+  ep.store(d, acc, m0 + wm, n0 + wn, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Deep-K weight-gradient levels in bf16 mode (batch 4096 class): dW = dY^T X with both
+// operands row-contiguous.  k_dw_part: 128x128 output tiles, K split NS ways across
+// workgroups; each workgroup stages 32-row slabs of dY (128 columns) and X (128 columns)
+// through LDS (double buffered) and writes its partial tile (+ the bias-gradient row-sum
+// partial) to a workspace.  k_dw_fin: one thread per output element sums the NS partials
+// in fixed order and runs the epilogue (store, or Adam [+ Polyak] with the gradient export
+// and block 0's loss / alpha extras) — both forms of a level take this path, so the
+// fused and the data-parallel updates keep identical bits.
+constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
+#ifndef SACMI_DW_TARGET
+#define SACMI_DW_TARGET 512     // k_dw_part workgroup slots (256 CUs x 2)
+#endif
+constexpr int kDwMaxSplit = 16;
+
+// workspace layout: partial s of desc p at ws + s * ws_stride + desc_off[p], row-major
+// [M][ncols] with ncols = N (+1 for the row-sum column)
+__device__ __forceinline__ int dw_ncols(const GemmDesc& d) { return d.rs_col >= 0 ? d.N + 1 : d.N; }
+
+template <bool BF16>
+__global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int64_t ws_stride) {
+  __shared__ __attribute__((aligned(16))) float sA[2][kDBK][kDBM + kDPad];
+  __shared__ __attribute__((aligned(16))) float sB[2][kDBK][kDBN + kDPad];
+  const int tiles_tot = batch.total_tiles;
+  if ((int)blockIdx.x >= tiles_tot * ns) {   // ride-along: the next update's gather
+    const int rb = blockIdx.x - tiles_tot * ns, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int b = rb * 4 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 4)
+      gather_row(batch.ride.ga, b, lane, 64);
+    return;
+  }
+  const int split = blockIdx.x / tiles_tot, bid = blockIdx.x % tiles_tot;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  const int m0 = (t / d.tiles_n) * kDBM, n0 = (t % d.tiles_n) * kDBN;
+  const int M = d.M, N = d.N, K = d.K;
+  const int kc = ((K + ns - 1) / ns + kDBK - 1) / kDBK * kDBK;
+  const int kb = split * kc, ke = min(K, kb + kc);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  // staging: thread t moves k rows (t >> 5) + 8 i (i < 4), columns 4 (t & 31) .. +3
+  const int c4 = 4 * (tid & 31);
+  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
+  const rsrc_t rS = make_rsrc(d.a_ksc ? d.a_ksc : d.A, d.a_ksc ? (uint32_t)K * 4u : 0u);
+  const bool has_ksc = d.a_ksc != nullptr;
+  const int ma = min(m0 + c4, M - 1), nb = min(n0 + c4, N - 1);
+  float4 ga[4], gb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = k0 + (tid >> 5) + 8 * i;
+      const bool kin = k < ke;
+      const uint32_t kk = (uint32_t)(kin ? k : kb);
+      float4 x = buf_ld4(rA, (kk * (uint32_t)d.lda + (uint32_t)ma) * 4u);
+      float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
+      const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
+      // columns past M / N (and rows past this split's K range) contribute zero
+      x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
+      x.z = kin && m0 + c4 + 2 < M ? x.z * f : 0.f; x.w = kin && m0 + c4 + 3 < M ? x.w * f : 0.f;
+      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+      ga[i] = x; gb[i] = y;
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<float4*>(&sA[buf][(tid >> 5) + 8 * i][c4]) = ga[i];
+      *reinterpret_cast<float4*>(&sB[buf][(tid >> 5) + 8 * i][c4]) = gb[i];
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float rs = 0.f;                       // row sum of A row m0 + tid (tid < 128), this split
+  const bool want_rs = d.rs_col >= 0 && n0 == 0;
+  const int nslab = (ke - kb + kDBK - 1) / kDBK;
+  gload(kb);
+  swrite(0);
+  __syncthreads();
+  for (int sl = 0; sl < nslab; ++sl) {
+    const int cur = sl & 1;
+    gload(kb + (sl + 1 < nslab ? sl + 1 : sl) * kDBK);
+#pragma unroll
+    for (int kk = 0; kk < kDBK / 16; ++kk) {
+      float a[4][4], b[4][4];
+      const int kr = kk * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i][s2] = sA[cur][kr + s2][wm + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j][s2] = sB[cur][kr + s2][wn + j * 16 + (lane & 15)];
+      }
+      mfma_chunk<4, 4, BF16>(acc, a, b);
+    }
+    if (want_rs && tid < kDBM) {
+#pragma clang fp contract(off)
+      for (int r = 0; r < kDBK; ++r) rs += sA[cur][r][tid];
+    }
+    swrite(cur ^ 1);
+    __syncthreads();
+  }
+  // partial tile (+ row-sum partial) to the workspace
+  int64_t off = 0;
+  for (int q = 0; q < p; ++q) off += (int64_t)batch.d[q].M * dw_ncols(batch.d[q]);
+  float* w = batch.ws + (int64_t)split * ws_stride + off;
+  const int nc = dw_ncols(d);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
-      float dsum[2] = {0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
+      for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn + j * 16 + (lane & 15);
-        float v = acc[i][j][r];
-        if (has_bias) v += bias_x[j];
-        if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
-        if (row < M && col < N) d.C[(size_t)row * d.ldc + col] = v;
-        if (has_dot) {
-          // fc3 dot partial over the 32-column block (tiles j, j+1): 16 lanes per tile
-          float c = (row < M && col < N) ? v * dotw_x[j] : 0.f;
-#pragma unroll
-          for (int o = 8; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-          dsum[j >> 1] += c;
-        }
-      }
-      if (has_dot && (lane & 15) == 0 && row < M) {
-#pragma unroll
-        for (int h = 0; h < NT / 2; ++h) {
-          const int blk = (n0 + wn) / 32 + h;
-          if (blk * 32 < N)
-            d.dotp[(size_t)row * d.dotp_ld + blk] = blk == 0 ? dsum[h] + dotb : dsum[h];
-        }
+        if (row < M && col < N) w[(int64_t)row * nc + col] = acc[i][j][r];
       }
     }
+  if (want_rs && tid < kDBM && m0 + tid < M) w[(int64_t)(m0 + tid) * nc + N] = rs;
+}
+
+__global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t ws_stride) {
+  __shared__ AdamScalars s_k[3];
+  const AdamFuse& af = batch.adam;
+  const bool adam = batch.has_adam != 0;
+  if (adam && threadIdx.x < 3) s_k[threadIdx.x] = fuse_scalars(af, threadIdx.x, af.step_offset);
+  __syncthreads();
+  const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
+  int64_t off = 0;
+  for (int q = 0; q < batch.count; ++q) {
+    const GemmDesc& d = batch.d[q];
+    const int nc = dw_ncols(d);
+    const int n_el = d.M * nc;                  // < 2^31 (checked by dw_split_plan)
+    const bool pol = d.epi == EPI_ADAM_POLYAK;
+    const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
+    const float* wsd = batch.ws + off;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n_el; e += gridDim.x * blockDim.x) {
+      const int row = e / nc, col = e - row * nc;
+      const int n = col < d.N ? col : d.rs_col;
+      // all NS partial loads in flight at once (a runtime-trip loop waited on each), then
+      // the fixed-order sum
+      float t[kDwMaxSplit];
+#pragma unroll
+      for (int s = 0; s < kDwMaxSplit; ++s) t[s] = s < ns ? wsd[(int64_t)s * ws_stride + e] : 0.f;
+      float v = t[0];
+#pragma unroll
+      for (int s = 1; s < kDwMaxSplit; ++s)
+        if (s < ns) v += t[s];
+      const int64_t o = (int64_t)row * d.ldc + n;
+      if (adam) {
+        float pp = d.C[o], mm = af.M[abase + o], vv = af.V[abase + o];
+        adam_elem(pp, mm, vv, v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
+        if (af.G) af.G[abase + o] = v;
+        d.C[o] = pp; af.M[abase + o] = mm; af.V[abase + o] = vv;
+        if (pol) {
+          float* tp = af.T + abase - af.t_base + o;
+          *tp = polyak(*tp, pp, omtau, af.tau);
+        }
+      } else {
+        d.C[o] = v;
+      }
+    }
+    off += n_el;
   }
+  if (adam && blockIdx.x == 0) {
+    __syncthreads();
+    if (threadIdx.x < af.n_losses) {
+      float sum = 0.f;
+      for (int w = 0; w < af.n_part; ++w) sum += af.loss_part[w * af.n_losses + threadIdx.x];
+      af.sc->losses[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
+    }
+    if (threadIdx.x == 0 && af.log_alpha_idx >= 0 && af.auto_entropy) {
+      const AdamScalars k = fuse_scalars(af, 3, af.step_offset);
+      const int64_t i = af.log_alpha_idx;
+      float pp = af.P[i], mm = af.M[i], vv = af.V[i];
+      adam_elem(pp, mm, vv, *af.log_alpha_grad, omb1, af.beta2, omb2, af.eps, k);
+      af.P[i] = pp; af.M[i] = mm; af.V[i] = vv;
+      af.sc->alpha = expf(pp);
+      af.sc->alpha_is_tensor = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && af.loss_ring) {
+      const int64_t pos = af.sc->loss_ring_pos;
+      const int64_t q = pos % af.ring;
+      af.loss_ring[q * 3 + 0] = af.sc->losses[0];
+      af.loss_ring[q * 3 + 1] = af.sc->losses[1];
+      af.loss_ring[q * 3 + 2] = af.sc->losses[2];
+      af.sc->loss_ring_pos = pos + 1;
+    }
+  }
+}
+
+// bf16 deep-K weight-gradient levels: split count and workspace need, or 0 (old path)
+static int dw_split_plan(GemmBatch& b, int64_t* stride) {
+  if (!b.bf16 || !b.ws || (b.ride.kind && b.ride.kind != 2)) return 0;
+  int64_t el = 0;
+  int tiles = 0;
+  for (int i = 0; i < b.count; ++i) {
+    GemmDesc& d = b.d[i];
+    if (d.a_kc || d.b_kc || d.axk || d.K < 2048) return 0;
+    if (d.epi != EPI_STORE && d.epi < EPI_ADAM) return 0;
+    d.tiles_m = (d.M + kDBM - 1) / kDBM;
+    d.tiles_n = (d.N + kDBN - 1) / kDBN;
+    d.tile_begin = tiles;
+    tiles += d.tiles_m * d.tiles_n;
+    el += (int64_t)d.M * (d.rs_col >= 0 ? d.N + 1 : d.N);
+  }
+  b.total_tiles = tiles;
+  if (el >= (1LL << 31)) return 0;
+  // as many K splits as fit in one pass over the chip's workgroup slots (2 per CU at
+  // 67 KB of LDS each): a partial second pass costs a whole slab loop (config 5: a
+  // 528-workgroup L6 took 96 us, 440 workgroups 82 us)
+  int ns = SACMI_DW_TARGET / tiles;
+  ns = ns < 1 ? 1 : ns > kDwMaxSplit ? kDwMaxSplit : ns;
+  if ((int64_t)ns * el > b.ws_floats) return 0;
+  *stride = el;
+  return ns;
 }
 
 // whether launch_gemm may run a level on k_fwd: plain forward GEMMs (both operands
@@ -1073,10 +1433,27 @@ static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
+  {
+    int64_t stride = 0;
+    const int ns = SACMI_DW_SPLIT ? dw_split_plan(b, &stride) : 0;
+    if (ns > 0) {
+      const int ride = b.ride.kind == 2 ? b.ride.nblocks : 0;
+      if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
+      else hipLaunchKernelGGL(k_dw_part<false>, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
+      HIP_LAUNCH_CHECK();
+      const int fin_grid = (int)std::min<int64_t>((stride + 255) / 256, 4096);
+      hipLaunchKernelGGL(k_dw_fin, dim3(fin_grid), dim3(256), 0, s, b, ns, stride);
+      HIP_LAUNCH_CHECK();
+      return;
+    }
+    b = b0;
+  }
   static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
   if (fwd_big && fwd_big_ok(b)) {
     const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
-    if (b.bf16 && n128) hipLaunchKernelGGL((k_fwd<true, 128>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    else if (b.bf16 && SACMI_FWD_LDS16) hipLaunchKernelGGL((k_fwd16<64>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    else if (b.bf16 && n128) hipLaunchKernelGGL((k_fwd<true, 128>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16) hipLaunchKernelGGL((k_fwd<true, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else hipLaunchKernelGGL((k_fwd<false, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
     HIP_LAUNCH_CHECK();

@@ -118,6 +118,7 @@ struct sacmi_ctx {
   // stored for the weight gradient), actor-pass critic dh (layers 0..nh-2), policy dh
   sacmi::DevBuf<float> dq, dhead, dhc[3], dha[3], dhp[3];
   sacmi::DevBuf<float> dotp;       // fc3 dot partials [6 slots][B][nparts]
+  sacmi::DevBuf<float> dw_ws;      // bf16 deep-K weight-gradient split-K partials
   int nparts = 0;
   sacmi::DevBuf<float> lpart_c, lpart_a, ring, lp_part;
   int ring_slots = 0;
@@ -283,6 +284,7 @@ static void alloc_all(sacmi_ctx* c) {
   c->logp.alloc((size_t)2 * Bm);
   c->dq.alloc((size_t)2 * Bm);
   c->nparts = (H + 31) / 32;
+  if (c->bf16 && Bm >= 2048) c->dw_ws.alloc((size_t)16 * c->total);
   c->dotp.alloc((size_t)6 * Bm * c->nparts);
   c->dhead.alloc((size_t)Bm * c->lddh);
   const int nrb = (Bm + 31) / 32;    // row blocks of the L5 / L9 tiling (loss partials)
@@ -567,6 +569,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   const int nh = c->nh, L = nh - 1;   // L: the last hidden layer (its head is layer nh)
   auto run = [&](Level& lv, const std::string& name) {
     lv.b.bf16 = c->bf16 ? 1 : 0;
+    lv.b.ws = c->dw_ws.p;
+    lv.b.ws_floats = (int64_t)c->dw_ws.n;
     if (mark(c, name.c_str(), level_flops(lv.b), level_bytes(lv.b))) launch_gemm(lv.b, s);
   };
 
@@ -1078,7 +1082,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
                     &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->xqb, &c->x2b, &c->rb,
                     &c->db, &c->eps,
-                    &c->cache, &c->logp, &c->dq, &c->dotp, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
+                    &c->cache, &c->logp, &c->dq, &c->dotp, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
                     &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr, &c->per_probs,
                     &c->per_chunk, &c->per_w, &c->per_val})
       b->release();

@@ -192,6 +192,8 @@ struct GemmBatch {
   RideAlong ride;      // extra workgroups after the tiles
   RowsFuse rows;       // prologue for axk-1 descs
   int bf16;            // 1: bf16 MFMA operands (fp32 loads rounded to bf16 in registers)
+  float* ws;           // bf16 deep-K weight-gradient levels: split-K partial workspace
+  int64_t ws_floats;   //   (capacity; launch_gemm falls back when a level needs more)
 };
 
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked

@@ -420,8 +420,9 @@ def test_graph_and_eager_identical():
             assert np.array_equal(res[0][1][n][k], res[1][1][n][k])
 
 
-@pytest.mark.parametrize("n_hidden,dtype", [(2, "fp32"), (3, "fp32"), (2, "bf16")])
-def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype):
+@pytest.mark.parametrize("n_hidden,dtype,B", [(2, "fp32", 64), (3, "fp32", 64), (2, "bf16", 64),
+                                              (2, "bf16", 2048)])
+def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype, B):
     """sacmi.dp over a 1-rank RCCL group (phases + in-place all-reduce on the adopted
     torch gradient arena) == the fused single-graph update, bit for bit (also for
     networks_model2 and the bf16 compute dtype)."""
@@ -434,19 +435,19 @@ def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype):
     try:
         cfg = SacConfig(24, 4, 64, n_hidden=n_hidden)
         params = init_params(cfg, 71, bias_scale=0.05)
-        rows = synthetic_rows(cfg, 400, 72, state_scale=0.5)
+        rows = synthetic_rows(cfg, max(400, B + 300), 72, state_scale=0.5)
         key = (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32)
         ctxs = []
         for _ in range(2):
-            ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=3, compute_dtype=dtype)
+            ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]), seed=3, compute_dtype=dtype)
             load_params(ctx, params)
             ctx.push(*rows)
             ctx.set_mt(0, key, 624)
             ctxs.append(ctx)
         upd = DataParallelUpdate(GpuBackend(ctxs[0], torch.device("cuda", 0)))
         for _ in range(3):
-            upd(64)
-            ctxs[1].step(64)
+            upd(B)
+            ctxs[1].step(B)
         upd.flush()
         torch.cuda.synchronize()
         for n in NETS:
@@ -459,18 +460,18 @@ def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype):
         from sacmi.dp import CapturedDataParallelUpdates
         cap = []
         for _ in range(2):
-            ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=3, compute_dtype=dtype)
+            ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]), seed=3, compute_dtype=dtype)
             load_params(ctx, params)
             ctx.push(*rows)
             ctx.set_mt(0, key, 624)
             cap.append(ctx)
         eager = DataParallelUpdate(GpuBackend(cap[1], torch.device("cuda", 0)))
         for _ in range(6):                 # the captured object's warm-up update + 5
-            eager(64)
+            eager(B)
         eager.flush()
         # uniform replay at B=64: the captured sequences use ride-along sampling/gather
-        assert cap[0].ride_possible(64)
-        g = CapturedDataParallelUpdates(cap[0], torch.device("cuda", 0), 64)
+        assert B > 1024 or cap[0].ride_possible(B)
+        g = CapturedDataParallelUpdates(cap[0], torch.device("cuda", 0), B)
         g.run(5, 2)
         torch.cuda.synchronize()
         for n in NETS:
