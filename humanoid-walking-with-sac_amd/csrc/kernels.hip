@@ -908,7 +908,7 @@ static int assign_tiles(GemmBatch& b) {
 // workgroup instead of once per wave.  Two workgroups per CU.
 constexpr int kFBM = 128, kFBK = 32, kFPad = 4, kFBN128 = 128;
 #ifndef SACMI_FWD_LDS16
-#define SACMI_FWD_LDS16 0       // bf16 mode: k_fwd16 (bf16 LDS slabs, 16x16x32 MFMA)
+#define SACMI_FWD_LDS16 1       // bf16 mode: k_fwd16 (bf16 LDS slabs, 16x16x32 MFMA)
 #endif
 
 // k_fwd / k_fwd16 epilogue: bias, ReLU, store, per-32-column fc3 dot partials.  A wave
@@ -1191,6 +1191,9 @@ constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
 #define SACMI_DW_TARGET 512     // k_dw_part workgroup slots (256 CUs x 2)
 #endif
 constexpr int kDwMaxSplit = 16;
+#ifndef SACMI_DW_LDS16
+#define SACMI_DW_LDS16 1        // bf16 mode: k_dw_part16 (bf16 k-major LDS, transposed reads)
+#endif
 
 // workspace layout: partial s of desc p at ws + s * ws_stride + desc_off[p], row-major
 // [M][ncols] with ncols = N (+1 for the row-sum column)
@@ -1232,7 +1235,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int
     for (int i = 0; i < 4; ++i) {
       const int k = k0 + (tid >> 5) + 8 * i;
       const bool kin = k < ke;
-      const uint32_t kk = (uint32_t)(kin ? k : kb);
+      const uint32_t kk = (uint32_t)(kin ? k : 0);   // row 0 always exists (a split may start past K)
       float4 x = buf_ld4(rA, (kk * (uint32_t)d.lda + (uint32_t)ma) * 4u);
       float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
       const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
@@ -1302,6 +1305,159 @@ __global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int
       }
     }
   if (want_rs && tid < kDBM && m0 + tid < M) w[(int64_t)(m0 + tid) * nc + N] = rs;
+}
+
+// bf16 mode, bf16 in LDS: k_dw_part with the operands rounded once at staging and kept
+// k-major ([k][128 columns] bf16, 64-deep slabs, rows padded to 272 B).  The 16x16x32
+// operand (lane l: A[l&15][k = 8(l>>4) + j]) is read with two ds_read_b64_tr_b16 per
+// fragment — the hardware transpose delivers 4 k of one column per lane, lane 4q+p of a
+// 16-lane group addressing k row q, columns 4p..4p+3 of the block — conflict-free with
+// the 68-dword row stride.  Bias-gradient row sums come from the unrounded fp32 staging
+// registers: per thread over its k rows, then over the 8 threads sharing a column group
+// in fixed order.
+typedef short s4t __attribute__((ext_vector_type(4)));
+typedef short s8t __attribute__((ext_vector_type(8)));
+constexpr int kD16K = 64, kD16Pad = 8;
+
+__device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4t*)(p));
+}
+
+__global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
+  constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][kD16K][LDR];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][kD16K][LDR];
+  __shared__ float s_rs[8][kDBM];
+  const int tiles_tot = batch.total_tiles;
+  if ((int)blockIdx.x >= tiles_tot * ns) {   // ride-along: the next update's gather
+    const int rb = blockIdx.x - tiles_tot * ns, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int b = rb * 4 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 4)
+      gather_row(batch.ride.ga, b, lane, 64);
+    return;
+  }
+  const int split = blockIdx.x / tiles_tot, bid = blockIdx.x % tiles_tot;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  const int m0 = (t / d.tiles_n) * kDBM, n0 = (t % d.tiles_n) * kDBN;
+  const int M = d.M, N = d.N, K = d.K;
+  const int kc = ((K + ns - 1) / ns + kD16K - 1) / kD16K * kD16K;
+  const int kb = split * kc, ke = min(K, kb + kc);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  // staging: thread t moves k rows (t >> 5) + 8 i (i < 8), columns 4 (t & 31) .. +3
+  const int c4 = 4 * (tid & 31), kr0 = tid >> 5;
+  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
+  const rsrc_t rS = make_rsrc(d.a_ksc ? d.a_ksc : d.A, d.a_ksc ? (uint32_t)K * 4u : 0u);
+  const bool has_ksc = d.a_ksc != nullptr;
+  const int ma = min(m0 + c4, M - 1), nb = min(n0 + c4, N - 1);
+  const bool want_rs = d.rs_col >= 0 && n0 == 0;
+  float4 ga[8], gb[8];
+  float rs4[4] = {0.f, 0.f, 0.f, 0.f};
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = k0 + kr0 + 8 * i;
+      const bool kin = k < ke;
+      const uint32_t kk = (uint32_t)(kin ? k : 0);   // row 0 always exists (a split may start past K)
+      float4 x = buf_ld4(rA, (kk * (uint32_t)d.lda + (uint32_t)ma) * 4u);
+      float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
+      const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
+      // columns past M / N (and rows past this split's K range) contribute zero
+      x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
+      x.z = kin && m0 + c4 + 2 < M ? x.z * f : 0.f; x.w = kin && m0 + c4 + 3 < M ? x.w * f : 0.f;
+      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+      ga[i] = x; gb[i] = y;
+    }
+  };
+  auto swrite = [&](int buf, bool fresh) {   // fresh: a slab not staged before
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      *reinterpret_cast<u2v*>(&sA[buf][kr0 + 8 * i][c4]) = pack_bf16x4(ga[i]);
+      *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+    }
+    if (want_rs && fresh) {
+#pragma clang fp contract(off)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        rs4[0] += ga[i].x; rs4[1] += ga[i].y; rs4[2] += ga[i].z; rs4[3] += ga[i].w;
+      }
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int nslab = (ke - kb + kD16K - 1) / kD16K;
+  // transposed-read lane roles: group g = lane >> 4 takes k 8g..8g+7; lane 4q+p of the
+  // group addresses k row q (+4 for the second half), columns 4p..4p+3 of a 16-column block
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = lane >> 4;
+  gload(kb);
+  swrite(0, true);
+  __syncthreads();
+  for (int sl = 0; sl < nslab; ++sl) {
+    const int cur = sl & 1;
+    gload(kb + (sl + 1 < nslab ? sl + 1 : sl) * kD16K);
+#pragma unroll
+    for (int kk = 0; kk < kD16K / 32; ++kk) {
+      const int kr = kk * 32 + 8 * tg + tq;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const s4t lo = lds_tr16(&sA[cur][kr][wm + i * 16 + 4 * tp]);
+        const s4t hi = lds_tr16(&sA[cur][kr + 4][wm + i * 16 + 4 * tp]);
+        const s8t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        a[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s4t lo = lds_tr16(&sB[cur][kr][wn + j * 16 + 4 * tp]);
+        const s4t hi = lds_tr16(&sB[cur][kr + 4][wn + j * 16 + 4 * tp]);
+        const s8t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        b[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    swrite(cur ^ 1, sl + 1 < nslab);
+    __syncthreads();
+  }
+  // partial tile (+ row-sum partial) to the workspace
+  int64_t off = 0;
+  for (int q = 0; q < p; ++q) off += (int64_t)batch.d[q].M * dw_ncols(batch.d[q]);
+  float* w = batch.ws + (int64_t)split * ws_stride + off;
+  const int nc = dw_ncols(d);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn + j * 16 + (lane & 15);
+        if (row < M && col < N) w[(int64_t)row * nc + col] = acc[i][j][r];
+      }
+    }
+  if (want_rs) {
+    s_rs[kr0][c4] = rs4[0]; s_rs[kr0][c4 + 1] = rs4[1];
+    s_rs[kr0][c4 + 2] = rs4[2]; s_rs[kr0][c4 + 3] = rs4[3];
+    __syncthreads();
+    if (tid < kDBM && m0 + tid < M) {
+#pragma clang fp contract(off)
+      float v = s_rs[0][tid];
+      for (int g = 1; g < 8; ++g) v += s_rs[g][tid];
+      w[(int64_t)(m0 + tid) * nc + N] = v;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t ws_stride) {
@@ -1438,7 +1594,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     const int ns = SACMI_DW_SPLIT ? dw_split_plan(b, &stride) : 0;
     if (ns > 0) {
       const int ride = b.ride.kind == 2 ? b.ride.nblocks : 0;
-      if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
+      if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
+      else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
       const int fin_grid = (int)std::min<int64_t>((stride + 255) / 256, 4096);
