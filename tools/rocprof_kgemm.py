@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --stats kernel CSV: per-kernel mean duration, and the mean
-over every sacmi::k_gemm instantiation (the bench's roofline kernel), for the
-agreement check against bench.py's `roofline.avg_launch_us`."""
+per GEMM level over every kernel that runs a grouped-GEMM level (the bench's roofline
+kernel family: every sacmi::k_gemm instantiation, k_fwd / k_fwd16 for the large-M bf16
+forward levels, k_dw_part / k_dw_part16 + k_dw_fin for the split-K bf16 weight-gradient
+levels — one level = one part launch + one fin launch), for the agreement check against
+bench.py's `roofline.avg_launch_us`."""
 import csv
 import sys
 
@@ -9,14 +12,18 @@ import sys
 def main(path):
     rows = list(csv.DictReader(open(path)))
     tot_ns = calls = 0
+    level = ("sacmi::k_gemm<", "sacmi::k_fwd<", "sacmi::k_fwd16<", "sacmi::k_dw_part")
     for r in rows:
         name, n, avg = r["Name"], int(r["Calls"]), float(r["AverageNs"])
         print(f"{name[:72]:72s} {n:7d} {avg / 1e3:9.2f} us  {float(r['Percentage']):6.2f}%")
-        if "sacmi::k_gemm<" in name:
+        if any(k in name for k in level):
             tot_ns += avg * n
             calls += n
+        elif "sacmi::k_dw_fin" in name:
+            tot_ns += avg * n                   # second kernel of a split-K level
     if calls:
-        print(f"\nsacmi::k_gemm (all tile configs): {calls} launches, mean {tot_ns / calls / 1e3:.3f} us")
+        print(f"\nGEMM levels (k_gemm all tile configs + k_fwd* + k_dw_part*/k_dw_fin): "
+              f"{calls} levels, mean {tot_ns / calls / 1e3:.3f} us")
 
 
 if __name__ == "__main__":
