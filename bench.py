@@ -139,12 +139,13 @@ def gemm_roofline(ctx, batch, reps=50):
                 achieved_tflops=achieved)
 
 
-def pmc_traffic(config):
+def pmc_traffic(config, networks="model1"):
     """Measured bytes past L2 per k_gemm launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, two
     separate --pmc passes over this bench command: tools/gpu_pmc.sh + tools/pmc_summary.py),
     read from the committed summary; None when absent."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json" if config == 2 else
-                        f"r01_pmc_traffic_c{config}.json")
+    suffix = "" if networks == "model1" else f"_{networks}"     # counters are per workload
+    path = os.path.join(ROOT, "profiles", (f"r01_pmc_traffic{suffix}.json" if config == 2 else
+                                           f"r01_pmc_traffic_c{config}{suffix}.json"))
     try:
         per = json.load(open(path))["per_launch"]
         return per["traffic_bytes"], os.path.relpath(path, ROOT)
@@ -388,7 +389,7 @@ def main():
     peak = PEAK_BF16_MFMA_TFLOPS if wl["dtype"] == "bf16" else PEAK_FP32_MFMA_TFLOPS
     if not args.no_roofline:
         info = gemm_roofline(ctx, args.batch)
-        traffic, traffic_src = pmc_traffic(args.config)
+        traffic, traffic_src = pmc_traffic(args.config, args.networks)
         roof = {"bound": "mfma", "achieved": round(info["achieved_tflops"], 3),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(info["achieved_tflops"] / peak, 4),
