@@ -1337,6 +1337,17 @@ int sacmi_rng_get_mt(sacmi_ctx* c, int stream, uint32_t* key, int32_t* pos) {
   });
 }
 
+int sacmi_rng_seed_device(sacmi_ctx* c, uint64_t seed, uint64_t offset) {
+  return guard([&] {
+    CHECK_HIP(hipStreamSynchronize(c->stream));   // no graph holding the old key in flight
+    destroy_graphs(c);                             // the key is a captured kernel argument
+    c->cfg.seed = seed;
+    double v = (double)offset;
+    REQUIRE((uint64_t)v == offset, SACMI_EVALUE, "offset must be below 2^53");
+    scalar_io(c, SACMI_S_NOISE_COUNTER, &v, nullptr);
+  });
+}
+
 int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
   return guard([&] {
     REQUIRE(batch >= 0 && batch <= c->len, SACMI_EVALUE, "Sample larger than population or is negative");

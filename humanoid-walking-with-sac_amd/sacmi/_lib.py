@@ -73,6 +73,7 @@ _PROTOS = {
     "sacmi_get_slots": [c_vp, c_i64p, ctypes.c_int64, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p],
     "sacmi_rng_set_mt": [c_vp, ctypes.c_int, c_u32p, ctypes.c_int32],
     "sacmi_rng_get_mt": [c_vp, ctypes.c_int, c_u32p, c_i32p],
+    "sacmi_rng_seed_device": [c_vp, ctypes.c_uint64, ctypes.c_uint64],
     "sacmi_sample_indices": [c_vp, ctypes.c_int32, c_i64p],
     "sacmi_step": [c_vp, ctypes.c_int32, c_i64p, c_f32p, c_f32p, c_f32p],
     "sacmi_step_async": [c_vp, ctypes.c_int32],

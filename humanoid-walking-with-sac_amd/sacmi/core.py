@@ -148,6 +148,10 @@ class Context:
     def set_scalar(self, which: int, value: float) -> None:
         L.call("sacmi_set_scalar", self._h, which, float(value))
 
+    def rng_seed_device(self, seed: int, offset: int = 0) -> None:
+        """Re-key the perf-mode policy noise (Philox seed, per-update counter start)."""
+        L.call("sacmi_rng_seed_device", self._h, int(seed), int(offset))
+
     # -- replay --------------------------------------------------------------------
     def push(self, s, a, r, s2, d) -> None:
         S, A = self.cfg.state_dim, self.cfg.action_dim

@@ -154,6 +154,12 @@ int sacmi_get_slots(sacmi_ctx* ctx, const int64_t* slots, int64_t n, float* s, f
 int sacmi_rng_set_mt(sacmi_ctx* ctx, int stream, const uint32_t* key, int32_t pos);
 int sacmi_rng_get_mt(sacmi_ctx* ctx, int stream, uint32_t* key, int32_t* pos);
 
+/* Perf-mode policy noise (eps of GaussianPolicy.sample, networks_model1.py:87-90 — the
+ * reference draws it from torch's generator): Philox4x32-10 keyed by `seed`, counter
+ * `offset` + one per update.  Replaces the seed given at create time; the next update
+ * re-captures its graphs. */
+int sacmi_rng_seed_device(sacmi_ctx* ctx, uint64_t seed, uint64_t offset);
+
 /* random.sample(buffer, batch) positions, drawn on the GPU from stream 0 (advances it). */
 int sacmi_sample_indices(sacmi_ctx* ctx, int32_t batch, int64_t* idx_out);
 

@@ -420,6 +420,40 @@ def test_graph_and_eager_identical():
             assert np.array_equal(res[0][1][n][k], res[1][1][n][k])
 
 
+def test_rng_seed_device_rekeys_noise():
+    """sacmi_rng_seed_device: a context re-keyed to (seed, 0) updates exactly like one
+    created with that seed; re-keying after the update graphs were captured takes effect
+    (a new key changes the next update, the same key and counter change nothing)."""
+    from sacmi import _lib as L
+    cfg = SacConfig(24, 4, 64)
+    params = init_params(cfg, 71, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 400, 72, state_scale=0.5)
+
+    def fresh(seed):
+        ctx = make_ctx(cfg, max_batch=64, capacity=400, seed=seed)
+        load_params(ctx, params)
+        ctx.push(*rows)
+        return ctx
+
+    a, f = fresh(11), fresh(99)
+    f.rng_seed_device(11, 0)
+    for _ in range(2):
+        assert np.array_equal(a.step(64), f.step(64))
+    for n in NETS:
+        pa, pf = a.get_net(n), f.get_net(n)
+        for k in pa:
+            assert np.array_equal(pa[k], pf[k])
+    b, c, d = fresh(99), fresh(99), fresh(99)
+    l1 = [x.step(64) for x in (b, c, d)]               # graphs captured under key 99
+    assert np.array_equal(l1[0], l1[1]) and np.array_equal(l1[0], l1[2])
+    b.rng_seed_device(11, 1)
+    c.rng_seed_device(99, 1)
+    assert b.get_scalar(L.S_NOISE_COUNTER) == 1
+    lb, lc, ld = b.step(64), c.step(64), d.step(64)
+    assert np.array_equal(lc, ld)
+    assert not np.array_equal(lb, ld)
+
+
 @pytest.mark.parametrize("n_hidden,dtype,B", [(2, "fp32", 64), (3, "fp32", 64), (2, "bf16", 64),
                                               (2, "bf16", 2048)])
 def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype, B):
