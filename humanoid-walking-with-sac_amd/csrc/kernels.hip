@@ -1191,6 +1191,9 @@ constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
 #define SACMI_DW_TARGET 512     // k_dw_part workgroup slots (256 CUs x 2)
 #endif
 constexpr int kDwMaxSplit = 16;
+#ifndef SACMI_AXK_LDS16
+#define SACMI_AXK_LDS16 1       // bf16 mode: k_axk16 for the batch-4096-class dh levels
+#endif
 #ifndef SACMI_DW_LDS16
 #define SACMI_DW_LDS16 1        // bf16 mode: k_dw_part16 (bf16 k-major LDS, transposed reads)
 #endif
@@ -1228,7 +1231,12 @@ __global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int
   const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
   const rsrc_t rS = make_rsrc(d.a_ksc ? d.a_ksc : d.A, d.a_ksc ? (uint32_t)K * 4u : 0u);
   const bool has_ksc = d.a_ksc != nullptr;
-  const int ma = min(m0 + c4, M - 1), nb = min(n0 + c4, N - 1);
+  // 4-wide operand reads start at a 4-aligned column <= the last one, so they stay inside
+  // a row padded to a multiple of 4; an operand narrower than 4 columns (the fc3 gradient
+  // dq, lda = 1) reads up to 3 floats past its last row: dw_split_plan's caller keeps
+  // that slack allocated (sacmi.hip: dq).  (A per-load scalar fallback under a branch
+  // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
+  const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
   float4 ga[4], gb[4];
   auto gload = [&](int k0) {
 #pragma unroll
@@ -1354,7 +1362,12 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
   const rsrc_t rS = make_rsrc(d.a_ksc ? d.a_ksc : d.A, d.a_ksc ? (uint32_t)K * 4u : 0u);
   const bool has_ksc = d.a_ksc != nullptr;
-  const int ma = min(m0 + c4, M - 1), nb = min(n0 + c4, N - 1);
+  // 4-wide operand reads start at a 4-aligned column <= the last one, so they stay inside
+  // a row padded to a multiple of 4; an operand narrower than 4 columns (the fc3 gradient
+  // dq, lda = 1) reads up to 3 floats past its last row: dw_split_plan's caller keeps
+  // that slack allocated (sacmi.hip: dq).  (A per-load scalar fallback under a branch
+  // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
+  const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
   const bool want_rs = d.rs_col >= 0 && n0 == 0;
   float4 ga[8], gb[8];
   float rs4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1458,6 +1471,192 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
       w[(int64_t)(m0 + tid) * nc + N] = v;
     }
   }
+}
+
+// bf16 mode, batch-4096 class: the row-prologue dh levels (L5 / L9 and their model2
+// form) on LDS-staged 64x128 tiles.  dh[b][n] = coef[b] * sum_k u[b][k] W[k][n] * [h[b][n] > 0]
+// with u[b][k] = h2[b][k] > 0 ? w3[k] : 0 formed at staging (the coefficient-free rows u
+// also stored, by the column-tile-0 workgroups, for the later weight gradient) and the
+// per-row coefficients from the same row prologue as k_gemm's (rows_load before the K
+// loop, rows_finish after it: identical values, so the losses and dq bits do not depend
+// on the kernel).  A = u in [row][k] bf16 slabs (one ds_read_b128 per 16x16x32 fragment),
+// B = W k-major (two ds_read_b64_tr_b16 per fragment); 2x2 waves of 32x64.
+// AX = false: the same kernel for the plain dh levels (dh = (dY W) * [h > 0]: L12 and the
+// model2 L5b / L9b / L11), no transform, no prologue.
+constexpr int kXBM = 64, kXBN = 128, kXBK = 64;
+
+template <bool AX>
+__global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
+  constexpr int LDA_ = kXBK + 8;        // [row][k] bf16, 144-B rows
+  constexpr int LDB_ = kXBN + 8;        // [k][n] bf16, 272-B rows
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][kXBM][LDA_];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][kXBK][LDB_];
+  __shared__ float s_q[kXBM][4], s_coef[2][kXBM], s_l[kXBM][2];
+  const int bid = blockIdx.x;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  int tr, tc;
+  if (d.xcd_gr) {
+    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
+    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
+    tr = (x / gc) * sr + j / sc;
+    tc = (x % gc) * sc + j % sc;
+  } else {
+    tr = t / d.tiles_n;
+    tc = t % d.tiles_n;
+  }
+  const int m0 = tr * kXBM, n0 = tc * kXBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 64;
+  const int M = d.M, N = d.N, K = d.K;
+  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
+  const rsrc_t rW = make_rsrc(AX ? d.ax_w : d.A, AX ? (uint32_t)K * 4u : 0u);
+  const bool store_a = AX && n0 == 0 && d.ax_out != nullptr;
+  const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
+                               store_a ? (uint32_t)(((size_t)(M - 1) * d.ax_ld + K) * 4) : 0u);
+  // A staging: rows (t >> 4) + 16 i (i < 4) at k = 4 (t & 15); B staging: k rows
+  // (t >> 5) + 8 i (i < 8) at columns 4 (t & 31)
+  const int kq = 4 * (tid & 15), c4 = 4 * (tid & 31), kr0 = tid >> 5;
+  uint32_t offA[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    offA[i] = (uint32_t)min(m0 + (tid >> 4) + 16 * i, M - 1) * (uint32_t)d.lda * 4u;
+  const int nb = min(n0 + c4, N - 1);
+  float4 ga[4], gb[8], gw;
+  auto gload = [&](int k0) {
+    const int k = k0 + kq;
+    const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ga[i] = buf_ld4(rA, offA[i] + ko);
+    gw = buf_ld4(rW, ko);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int kb = k0 + kr0 + 8 * i;
+      const bool kin = kb < K;
+      float4 y = buf_ld4(rB, ((uint32_t)(kin ? kb : 0) * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
+      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+      gb[i] = y;
+    }
+  };
+  auto swrite = [&](int buf, int k0, bool fresh) {
+    const int k = k0 + kq;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // u = [h2 > 0] w3 (exact fp32 values: w3 or 0), rounded to bf16 for the MFMAs
+      const float4 a = ga[i];
+      const float4 u = AX ? make_float4(a.x > 0.f && k < K ? gw.x : 0.f, a.y > 0.f && k + 1 < K ? gw.y : 0.f,
+                                        a.z > 0.f && k + 2 < K ? gw.z : 0.f, a.w > 0.f && k + 3 < K ? gw.w : 0.f)
+                          : make_float4(k < K ? a.x : 0.f, k + 1 < K ? a.y : 0.f,
+                                        k + 2 < K ? a.z : 0.f, k + 3 < K ? a.w : 0.f);
+      const int r = (tid >> 4) + 16 * i;
+      *reinterpret_cast<u2v*>(&sA[buf][r][kq]) = pack_bf16x4(u);
+      if (fresh) {
+        const int rr = m0 + r;
+        buf_st4(rAx, (rr < M && k < K) ? (uint32_t)(rr * d.ax_ld + k) * 4u : 0xfffffff0u,
+                f4{u.x, u.y, u.z, u.w});
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+  };
+  f4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  // the row prologue's loads and the ReLU-mask source, behind the first slab's loads
+  RowsRegs rows_x{};
+  if constexpr (AX) rows_load<kXBM, 256>(batch.rows, d, m0, rows_x);
+  float hm[2][4][4];
+  {
+    const rsrc_t rX = make_rsrc(d.aux, (uint32_t)(((size_t)(M - 1) * d.ldaux + N) * 4));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = n0 + wn + j * 16 + (lane & 15);
+          hm[i][j][r] = buf_ld(rX, row < M && col < N ? (uint32_t)(row * d.ldaux + col) * 4u : 0xfffffff0u);
+        }
+      }
+  }
+  swrite(0, 0, store_a);
+  __syncthreads();
+  const int nslab = (K + kXBK - 1) / kXBK;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = lane >> 4;
+  for (int sl = 0; sl < nslab; ++sl) {
+    const int cur = sl & 1;
+    const int knext = (sl + 1 < nslab ? sl + 1 : sl) * kXBK;
+    gload(knext);   // unconditional: the last re-reads its slab
+#pragma unroll
+    for (int kk = 0; kk < kXBK / 32; ++kk) {
+      const int kc = kk * 32 + 8 * tg;
+      bf16x8 a[2], b[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][wm + i * 16 + (lane & 15)][kc]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const s4t lo = lds_tr16(&sB[cur][kc + tq][wn + j * 16 + 4 * tp]);
+        const s4t hi = lds_tr16(&sB[cur][kc + tq + 4][wn + j * 16 + 4 * tp]);
+        const s8t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        b[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    swrite(cur ^ 1, knext, store_a && sl + 1 < nslab);
+    __syncthreads();
+  }
+  const bool writer = p == 0 && n0 == 0;
+  if constexpr (AX) rows_finish<kXBM, 256>(batch.rows, d, m0, writer, bid == 0, rows_x, s_q, s_coef, s_l);
+  // epilogue: coefficient, ReLU-backward mask, store (k_gemm's op order)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int lr = wm + i * 16 + (lane >> 4) * 4 + r, row = m0 + lr;
+      const float cf = AX ? s_coef[d.ax_slot][lr] : 1.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn + j * 16 + (lane & 15);
+        float v = acc[i][j][r];
+        if (AX) v *= cf;
+        v = hm[i][j][r] > 0.f ? v : 0.f;
+        if (row < M && col < N) d.C[(size_t)row * d.ldc + col] = v;
+      }
+    }
+  if constexpr (AX) rows_loss<kXBM>(batch.rows, m0, writer, s_l);
+}
+
+// whether launch_gemm may run a level on k_axk16: bf16, every desc a row-prologue dh GEMM
+// (A transform, K-contiguous A, MN-contiguous 16-B aligned B, mask epilogue), no rides,
+// and at least one 64x128 tile per CU
+// (-1: no; 1: the row-prologue form; 0: the plain dh form)
+static int axk16_ok(GemmBatch& b) {
+  if (!b.bf16 || b.ride.kind) return -1;
+  const int ax = b.d[0].axk == 1 ? 1 : 0;
+  if (ax != (b.rows.kind != 0 ? 1 : 0)) return -1;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    if (d.axk != ax || !d.a_kc || d.b_kc || d.epi != EPI_MASK || d.bias || d.dotp || d.a_ksc ||
+        d.rs_col >= 0)
+      return -1;
+    if (((uintptr_t)d.A & 15) || (d.lda & 3) || ((uintptr_t)d.B & 15) || (d.ldb & 3) ||
+        (ax && ((uintptr_t)d.ax_w & 15)) || (d.N & 3))
+      return -1;
+  }
+  return assign_tiles<kXBM, kXBN>(b) >= 256 ? ax : -1;
 }
 
 __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t ws_stride) {
@@ -1569,6 +1768,7 @@ static bool fwd_big_ok(GemmBatch& b) {
   for (int i = 0; i < b.count; ++i) {
     const GemmDesc& d = b.d[i];
     if (!d.a_kc || !d.b_kc || d.axk || d.a_ksc || d.rs_col >= 0) return false;
+    if (((uintptr_t)d.A & 15) || (d.lda & 3) || ((uintptr_t)d.B & 15) || (d.ldb & 3)) return false;
     if (d.epi != EPI_RELU && d.epi != EPI_STORE) return false;
     if (d.dotp && (d.N % 32)) return false;
   }
@@ -1605,6 +1805,16 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     }
     b = b0;
   }
+  if (SACMI_AXK_LDS16) {
+    const int ax = axk16_ok(b);
+    if (ax >= 0) {
+      if (ax) hipLaunchKernelGGL(k_axk16<true>, dim3(b.total_tiles), dim3(256), 0, s, b);
+      else hipLaunchKernelGGL(k_axk16<false>, dim3(b.total_tiles), dim3(256), 0, s, b);
+      HIP_LAUNCH_CHECK();
+      return;
+    }
+  }
+  b = b0;
   static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
   if (fwd_big && fwd_big_ok(b)) {
     const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;

@@ -282,7 +282,7 @@ static void alloc_all(sacmi_ctx* c) {
   c->eps.alloc((size_t)2 * Bm * A);
   c->cache.alloc((size_t)2 * Bm * 3 * A);
   c->logp.alloc((size_t)2 * Bm);
-  c->dq.alloc((size_t)2 * Bm);
+  c->dq.alloc((size_t)2 * Bm + 16);   // + slack: the split-K dW kernels read 4 wide (kernels.hip)
   c->nparts = (H + 31) / 32;
   if (c->bf16 && Bm >= 2048) c->dw_ws.alloc((size_t)16 * c->total);
   c->dotp.alloc((size_t)6 * Bm * c->nparts);
@@ -399,13 +399,15 @@ static void validate(const GemmDesc& d) {
     if (((uintptr_t)d.A & 15) || (d.lda & 3)) throw Error{SACMI_ESTATE, "A misaligned"};
     check_span(d.A, (int64_t)(d.M - 1) * d.lda + klast, "A");
   } else {
-    check_span(d.A, (int64_t)(d.K - 1) * d.lda + d.M - 1, "A");
+    // MN-contiguous operands are read 4 columns wide from a 4-aligned start (the split-K
+    // dW kernels): the span covers the last such group
+    check_span(d.A, (int64_t)(d.K - 1) * d.lda + ((d.M - 1) & ~3) + 3, "A");
   }
   if (d.b_kc) {
     if (((uintptr_t)d.B & 15) || (d.ldb & 3)) throw Error{SACMI_ESTATE, "B misaligned"};
     check_span(d.B, (int64_t)(d.N - 1) * d.ldb + klast, "B");
   } else {
-    check_span(d.B, (int64_t)(d.K - 1) * d.ldb + d.N - 1, "B");
+    check_span(d.B, (int64_t)(d.K - 1) * d.ldb + ((d.N - 1) & ~3) + 3, "B");
   }
   if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C");
   if (d.bias) check_span(d.bias, (int64_t)(d.N - 1) * d.bias_ld, "bias");

@@ -455,7 +455,7 @@ def test_rng_seed_device_rekeys_noise():
 
 
 @pytest.mark.parametrize("n_hidden,dtype,B", [(2, "fp32", 64), (3, "fp32", 64), (2, "bf16", 64),
-                                              (2, "bf16", 2048)])
+                                              (2, "bf16", 2048), (3, "bf16", 2048)])
 def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype, B):
     """sacmi.dp over a 1-rank RCCL group (phases + in-place all-reduce on the adopted
     torch gradient arena) == the fused single-graph update, bit for bit (also for
@@ -522,7 +522,7 @@ BF16_EMU_GRAD_TOL = 2e-2   # per-tensor normwise, vs that emulation (rounding fl
 BF16_TRUTH_GRAD_TOL = 0.15  # vs the exact fp64 oracle (cosine >= ~0.99)
 
 
-@pytest.mark.parametrize("n_hidden,B", [(2, 256), (3, 256), (2, 4096)])
+@pytest.mark.parametrize("n_hidden,B", [(2, 256), (3, 256), (2, 4096), (3, 4096)])
 def test_bf16_compute_vs_emulation(n_hidden, B):
     """compute_dtype bf16 (BASELINE configs[4]): bf16 MFMA operands, fp32 accumulation,
     fp32 master weights / Adam / losses.  No reference counterpart: checked against the

@@ -1,2 +1,5 @@
 cd $GRAFT_REPO_ROOT
-PYTEST_ARGS='-k "rng_seed or graph_and_eager"' bash tools/gpu_round.sh test
+O=gpurun_out
+PYTEST_ARGS='-x' bash tools/gpu_round.sh test || exit 1
+timeout -k 10 200 python3 bench.py --config 5 --steps 200 --no-cpu-baseline --no-trainer-loop > $O/v_main.json 2>$O/v_main.err || exit 1
+timeout -k 10 200 python3 bench.py --config 5 --networks model2 --steps 200 --no-cpu-baseline --no-trainer-loop > $O/v_m2.json 2>$O/v_m2.err || exit 1
