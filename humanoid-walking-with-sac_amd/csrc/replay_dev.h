@@ -26,30 +26,33 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t 
   return far ^ (y >> 1) ^ ((y & 1u) ? kMatrixA : 0u);
 }
 
-// In-place twist of key[624] by the whole block (4 dependency phases).
+// In-place twist of key[624] by the whole block (needs >= 227 threads), two barriers.
+// Word i takes key[i+1] (still old for i < 623) and key[(i+397) % 624], which is old for
+// i < 227 and the NEW word i-227 after that: thread t < 227 runs the chain i = t, t+227,
+// t+454 in registers from old words only; thread 0 also recomputes new[169] -> new[396]
+// for word 623 (which takes new[0] and new[396]).  All reads precede the barrier, all
+// writes follow it.  (Was 4 read/write phases, 7 barriers.)
 __device__ void mt_twist_block(uint32_t* key) {
+  constexpr int D = kMtN - kMtM;   // 227
   const int t = threadIdx.x;
-  uint32_t v = 0;
-  // phase A: i in [0,227): all inputs old
-  if (t < kMtN - kMtM) v = mt_mix(key[t], key[t + 1], key[t + kMtM]);
+  uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+  if (t < D) {
+    v0 = mt_mix(key[t], key[t + 1], key[t + kMtM]);
+    v1 = mt_mix(key[t + D], key[t + D + 1], v0);
+    if (t + 2 * D < kMtN - 1) v2 = mt_mix(key[t + 2 * D], key[t + 2 * D + 1], v1);
+    if (t == 0) {
+      const uint32_t a = mt_mix(key[169], key[170], key[169 + kMtM]);   // new[169]
+      const uint32_t b = mt_mix(key[169 + D], key[170 + D], a);         // new[396]
+      v3 = mt_mix(key[kMtN - 1], v0, b);                                // new[623]
+    }
+  }
   __syncthreads();
-  if (t < kMtN - kMtM) key[t] = v;
-  __syncthreads();
-  // phase B: i in [227,454): far = new key[i-227]
-  int i = t + (kMtN - kMtM);
-  if (t < kMtN - kMtM) v = mt_mix(key[i], key[i + 1], key[i - (kMtN - kMtM)]);
-  __syncthreads();
-  if (t < kMtN - kMtM) key[i] = v;
-  __syncthreads();
-  // phase C: i in [454,623)
-  i = t + 2 * (kMtN - kMtM);
-  const bool c = i < kMtN - 1;
-  if (c) v = mt_mix(key[i], key[i + 1], key[i - (kMtN - kMtM)]);
-  __syncthreads();
-  if (c) key[i] = v;
-  __syncthreads();
-  // phase D: i = 623
-  if (t == 0) key[kMtN - 1] = mt_mix(key[kMtN - 1], key[0], key[kMtM - 1]);
+  if (t < D) {
+    key[t] = v0;
+    key[t + D] = v1;
+    if (t + 2 * D < kMtN - 1) key[t + 2 * D] = v2;
+    if (t == 0) key[kMtN - 1] = v3;
+  }
   __syncthreads();
 }
 
