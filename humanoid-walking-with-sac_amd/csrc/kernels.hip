@@ -914,6 +914,23 @@ constexpr int kFBM = 128, kFBK = 32, kFPad = 4, kFBN128 = 128;
 // k_fwd / k_fwd16 epilogue: bias, ReLU, store, per-32-column fc3 dot partials.  A wave
 // owns a 64 x (16 NT) sub-tile at (r0, c0); lane holds D[row = (lane >> 4) * 4 + r]
 // [col = lane & 15] of each 16x16 tile.  The operands are loaded before the K loop.
+// DPP row rotation (within each 16-lane row) of a float
+template <int CTRL>
+__device__ __forceinline__ float dpp_row(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
+                                                               0xF, 0xF, false));
+}
+// sum over a 16-lane row, the total in every lane of the row: row_ror 8, 4, 2, 1 (each
+// step adds two equal-shaped partial sums; a + b == b + a, so every lane holds the same bits)
+__device__ __forceinline__ float row16_sum(float x) {
+#pragma clang fp contract(off)
+  x += dpp_row<0x128>(x);
+  x += dpp_row<0x124>(x);
+  x += dpp_row<0x122>(x);
+  x += dpp_row<0x121>(x);
+  return x;
+}
+
 template <int NT>
 struct FwdEpi {
   float bias_x[NT], dotw_x[NT], dotb;
@@ -949,10 +966,11 @@ struct FwdEpi {
           if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
           if (row < M && col < N) d.C[(size_t)row * d.ldc + col] = v;
           if (has_dot) {
-            // fc3 dot partial over the 32-column block (tiles j, j+1): 16 lanes per tile
+            // fc3 dot partial over the 32-column block (tiles j, j+1): 16 lanes per tile,
+            // summed by DPP row rotations (VALU; the ds_bpermute butterfly it replaces
+            // put 256 LDS-crossbar ops per lane in this epilogue)
             float c = (row < M && col < N) ? v * dotw_x[j] : 0.f;
-#pragma unroll
-            for (int o = 8; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+            c = row16_sum(c);
             dsum[j >> 1] += c;
           }
         }
