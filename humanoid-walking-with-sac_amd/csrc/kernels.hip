@@ -407,6 +407,23 @@ __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, flo
   }
 }
 
+// DPP row rotation (within each 16-lane row) of a float
+template <int CTRL>
+__device__ __forceinline__ float dpp_row(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
+                                                               0xF, 0xF, false));
+}
+// sum over a 16-lane row, the total in every lane of the row: row_ror 8, 4, 2, 1 (each
+// step adds two equal-shaped partial sums; a + b == b + a, so every lane holds the same bits)
+__device__ __forceinline__ float row16_sum(float x) {
+#pragma clang fp contract(off)
+  x += dpp_row<0x128>(x);
+  x += dpp_row<0x124>(x);
+  x += dpp_row<0x122>(x);
+  x += dpp_row<0x121>(x);
+  return x;
+}
+
 // Sum of the KSPLIT partials of tile element (row, col); with MG wave groups the
 // tile has MG*TM rows and group g's partials sit at waves g*KSPLIT .. g*KSPLIT+KSPLIT-1.
 template <int TM, int TN, int KSPLIT, int MG = 1>
@@ -828,8 +845,8 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
       // wave hold one row's 32 consecutive columns (TN = 32 or 64, row-major slots)
       if (s < EPT && d.dotp) {
         float c = ok ? v * s_dotw[col] : 0.f;
-#pragma unroll
-        for (int off = 16; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+        c = row16_sum(c);                 // DPP within each 16-lane row
+        c += __shfl_xor(c, 16, 64);       // the two rows of the half wave
         if ((tid & 31) == 0 && m0 + row < d.M)   // block 0 adds the bias: q = sum of blocks
           d.dotp[(size_t)(m0 + row) * d.dotp_ld + (n0 + col) / 32] = n0 + col == 0 ? c + dotb_x : c;
       }
@@ -914,23 +931,6 @@ constexpr int kFBM = 128, kFBK = 32, kFPad = 4, kFBN128 = 128;
 // k_fwd / k_fwd16 epilogue: bias, ReLU, store, per-32-column fc3 dot partials.  A wave
 // owns a 64 x (16 NT) sub-tile at (r0, c0); lane holds D[row = (lane >> 4) * 4 + r]
 // [col = lane & 15] of each 16x16 tile.  The operands are loaded before the K loop.
-// DPP row rotation (within each 16-lane row) of a float
-template <int CTRL>
-__device__ __forceinline__ float dpp_row(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
-                                                               0xF, 0xF, false));
-}
-// sum over a 16-lane row, the total in every lane of the row: row_ror 8, 4, 2, 1 (each
-// step adds two equal-shaped partial sums; a + b == b + a, so every lane holds the same bits)
-__device__ __forceinline__ float row16_sum(float x) {
-#pragma clang fp contract(off)
-  x += dpp_row<0x128>(x);
-  x += dpp_row<0x124>(x);
-  x += dpp_row<0x122>(x);
-  x += dpp_row<0x121>(x);
-  return x;
-}
-
 template <int NT>
 struct FwdEpi {
   float bias_x[NT], dotw_x[NT], dotb;
