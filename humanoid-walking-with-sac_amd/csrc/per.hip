@@ -502,13 +502,15 @@ __global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a, int nchunk, in
   __shared__ int64_t wsum[kF2Threads / 64];
   if (threadIdx.x < 64) {
     // the chunk sums added in chunk order (numpy): wave 0 loads 64 at a time in one
-    // coalesced burst, lane 0's running sum takes them one by one through shuffles
+    // coalesced burst, the running sum takes them one by one with v_readlane (a scalar
+    // read of lane l: no LDS round trip per element, unlike a shuffle)
     float t = -0.0f;
     for (int c0 = 0; c0 < nchunk; c0 += 64) {
       const int c = c0 + threadIdx.x;
       const float v = c < nchunk ? a.chunk_sums[c] : 0.f;
       const int m = nchunk - c0 < 64 ? nchunk - c0 : 64;
-      for (int l = 0; l < m; ++l) t = t + __shfl(v, l, 64);
+      for (int l = 0; l < m; ++l)
+        t = t + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
     }
     if (threadIdx.x == 0) s_total = t;
   }
