@@ -399,6 +399,7 @@ def main():
                 "algorithmic_bytes_per_launch": round(info["gemm_bytes"] / info["launches"]),
                 "kernel": f"sacmi::k_gemm (grouped {wl['dtype']} MFMA GEMM, all tile configs)"
                           + (" + sacmi::k_fwd16 (bf16-LDS large-M forward levels) + "
+                             "sacmi::k_axk16 (dh levels) + "
                              "sacmi::k_dw_part16/k_dw_fin (split-K weight-gradient levels)"
                              if wl["dtype"] == "bf16" and args.batch >= 2048 else ""),
                 "launches_per_step": info["launches"],
