@@ -1093,7 +1093,13 @@ __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
 // order and epilogue as k_fwd.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u2v __attribute__((ext_vector_type(2)));
-constexpr int kHBK = 64, kHPad = 8;
+#ifndef SACMI_FWD16_BK
+#define SACMI_FWD16_BK 64       // k_fwd16 slab depth (64 or 32)
+#endif
+#ifndef SACMI_FWD16_OCC
+#define SACMI_FWD16_OCC 2       // k_fwd16 workgroups per CU the launch bounds ask for
+#endif
+constexpr int kHBK = SACMI_FWD16_BK, kHPad = 8;
 
 __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
   const bf16x4 x = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
@@ -1101,10 +1107,13 @@ __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
 }
 
 template <int kFBN>
-__global__ __launch_bounds__(256, 2) void k_fwd16(GemmBatch batch) {
+__global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
   constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
-  constexpr int LDR = kHBK + kHPad;      // bf16 per LDS row: 144 B
-  constexpr int NB = kFBN / 16;          // B rows staged per thread (16 rows per pass)
+  constexpr int LDR = kHBK + kHPad;      // bf16 per LDS row: 144 B at 64 deep
+  constexpr int TPR = kHBK / 4;          // staging threads per row (4 k each)
+  constexpr int RPP = 256 / TPR;         // rows per staging pass
+  constexpr int NA = kFBM / RPP;         // A rows staged per thread
+  constexpr int NB = kFBN / RPP;         // B rows staged per thread
   __shared__ __attribute__((aligned(16))) __bf16 sA[2][kFBM][LDR];
   __shared__ __attribute__((aligned(16))) __bf16 sB[2][kFBN][LDR];
   const int bid = blockIdx.x;
@@ -1128,21 +1137,21 @@ __global__ __launch_bounds__(256, 2) void k_fwd16(GemmBatch batch) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * (kFBN / 2);
   const int M = d.M, N = d.N, K = d.K;
-  // staging: thread t moves rows (t >> 4) + 16 i at k = 4 (t & 15) of both slabs
+  // staging: thread t moves rows t / TPR + RPP i at k = 4 (t % TPR) of both slabs
   const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
-  uint32_t offA[8], offB[NB];
+  uint32_t offA[NA], offB[NB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int ra = min(m0 + (tid >> 4) + 16 * i, M - 1);
+  for (int i = 0; i < NA; ++i) {
+    const int ra = min(m0 + tid / TPR + RPP * i, M - 1);
     offA[i] = (uint32_t)ra * (uint32_t)d.lda * 4u;
   }
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const int rb = min(n0 + (tid >> 4) + 16 * i, N - 1);
+    const int rb = min(n0 + tid / TPR + RPP * i, N - 1);
     offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
   }
-  const int kq = 4 * (tid & 15);
-  float4 ga[8], gb[NB];
+  const int kq = 4 * (tid % TPR);
+  float4 ga[NA], gb[NB];
   auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
     x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
     return x;
@@ -1151,15 +1160,15 @@ __global__ __launch_bounds__(256, 2) void k_fwd16(GemmBatch batch) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+    for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
 #pragma unroll
     for (int i = 0; i < NB; ++i) gb[i] = zk(buf_ld4(rB, offB[i] + ko), k);
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) *reinterpret_cast<u2v*>(&sA[buf][(tid >> 4) + 16 * i][kq]) = pack_bf16x4(ga[i]);
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(ga[i]);
 #pragma unroll
-    for (int i = 0; i < NB; ++i) *reinterpret_cast<u2v*>(&sB[buf][(tid >> 4) + 16 * i][kq]) = pack_bf16x4(gb[i]);
+    for (int i = 0; i < NB; ++i) *reinterpret_cast<u2v*>(&sB[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(gb[i]);
   };
   f4 acc[4][NT];
 #pragma unroll
@@ -1988,6 +1997,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       const float x = a.deterministic ? mean : mean + eps * sd;
       const float y = tanhf(x);
       a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
+      if (a.act_host) a.act_host[(size_t)m * A + j] = y * a.scale + a.bias;
       const float dx = x - mean;
       lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
       const float omy2 = one_minus_tanh2(x);
@@ -2019,6 +2029,17 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       a.logp_part[2 * blockIdx.x + threadIdx.x] = s;
     }
   }
+}
+
+__global__ void k_rows_in(float* dst, int ldd, const float* src, int lds, int cols) {
+  const float* s = src + (size_t)blockIdx.x * lds;
+  float* d = dst + (size_t)blockIdx.x * ldd;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) d[c] = s[c];
+}
+
+void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int cols, hipStream_t s) {
+  hipLaunchKernelGGL(k_rows_in, dim3(n), dim3(256), 0, s, dst, ldd, src, lds, cols);
+  HIP_LAUNCH_CHECK();
 }
 
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {

@@ -135,6 +135,7 @@ struct sacmi_ctx {
   hipEvent_t push_ev[kPushSlots] = {};
   int push_slot = 0;
   float* act_host = nullptr;                // [kActPinned][S] states, then [..][A] eps / out
+  float* act_host_dev = nullptr;            // the same memory, device-mapped
   sacmi::DevScalars* sc_host = nullptr;
   // PER scratch (replay_kind == PER)
   sacmi::DevBuf<float> per_probs, per_chunk, per_w, per_val;
@@ -329,8 +330,12 @@ static void alloc_pinned(sacmi_ctx* c) {
     CHECK_HIP(hipEventCreateWithFlags(&c->push_ev[i], hipEventDisableTiming));
   }
   c->stage.alloc(row * c->push_rows);
+  // select_action staging: fine-grained (coherent) and mapped, so the kernels read the
+  // states and write the actions in place (no copy commands on the env-rate path)
   CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->act_host),
-                          (size_t)kActPinned * (S + 2 * A) * 4, hipHostMallocDefault));
+                          (size_t)kActPinned * (S + 2 * A) * 4,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->act_host_dev), c->act_host, 0));
   CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->sc_host), sizeof(DevScalars),
                           hipHostMallocDefault));
 }
@@ -345,6 +350,7 @@ static void free_pinned(sacmi_ctx* c) {
   if (c->act_host) (void)hipHostFree(c->act_host);
   if (c->sc_host) (void)hipHostFree(c->sc_host);
   c->act_host = nullptr;
+  c->act_host_dev = nullptr;
   c->sc_host = nullptr;
 }
 
@@ -1709,8 +1715,16 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
         esrc = h_eps;
       }
     }
-    CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, src, (size_t)S * 4, (size_t)S * 4, n,
-                               hipMemcpyHostToDevice, s));
+    // zero-copy (default for env-rate calls): the first kernel reads the states from the
+    // mapped staging and the heads kernel writes the actions back into it
+    static const bool zc_env = std::getenv("SACMI_ACT_ZEROCOPY") == nullptr ||
+                               std::getenv("SACMI_ACT_ZEROCOPY")[0] != '0';
+    const bool zc = pinned && zc_env && c->act_host_dev;
+    if (zc)
+      launch_rows_in(c->x2.p, Kx, c->act_host_dev, S, n, S, s);
+    else
+      CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, src, (size_t)S * 4, (size_t)S * 4, n,
+                                 hipMemcpyHostToDevice, s));
     if (eps && !deterministic)
       CHECK_HIP(hipMemcpyAsync(c->eps.p, esrc, (size_t)n * A * 4, hipMemcpyHostToDevice, s));
     Level l1;
@@ -1732,10 +1746,12 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
     hs.deterministic = deterministic ? 1 : 0;
     hs.ctr_override = (1ull << 63) | (++c->act_calls);   // disjoint from update noise
+    if (zc) hs.act_host = c->act_host_dev + (h_out - c->act_host);
     launch_heads_sample(hs, s);
     CHECK_HIP(hipGetLastError());
-    CHECK_HIP(hipMemcpy2DAsync(pinned ? h_out : a_out, (size_t)A * 4, c->x2.p + S + 1, (size_t)Kx * 4,
-                               (size_t)A * 4, n, hipMemcpyDeviceToHost, s));
+    if (!zc)
+      CHECK_HIP(hipMemcpy2DAsync(pinned ? h_out : a_out, (size_t)A * 4, c->x2.p + S + 1, (size_t)Kx * 4,
+                                 (size_t)A * 4, n, hipMemcpyDeviceToHost, s));
     CHECK_HIP(hipStreamSynchronize(s));
     if (pinned) std::memcpy(a_out, h_out, (size_t)n * A * 4);
   });

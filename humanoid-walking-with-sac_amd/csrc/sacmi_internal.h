@@ -215,6 +215,7 @@ struct HeadSampleArgs {
   uint64_t ctr_override; // nonzero: Philox counter to use instead of sc->noise_counter
   float* logp_part;      // [grid][2] or null: per workgroup, sum of logp over its rows
   int split_row;         //   < split_row (slot 0) and >= split_row (slot 1)
+  float* act_host;       // or null: the actions also stored [row][A] to host-mapped memory
 };
 
 // Sample-backward epilogue of the dL/da GEMM.
@@ -237,6 +238,8 @@ struct SampleBwdArgs {
 // launchers (kernels.hip)
 void launch_gemm(const GemmBatch& batch, hipStream_t s);
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
+// rows [n][cols] from host-mapped memory (select_action's states) into a device matrix
+void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int cols, hipStream_t s);
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s);
 
 
