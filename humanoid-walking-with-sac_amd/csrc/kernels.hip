@@ -862,6 +862,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
       float sum = 0.f;
       for (int w = 0; w < af.n_part; ++w) sum += af.loss_part[w * af.n_losses + threadIdx.x];
       af.sc->losses[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
+      if (af.loss_host) af.loss_host[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
     }
     if (threadIdx.x == 0 && af.log_alpha_idx >= 0 && af.auto_entropy) {
       const AdamScalars k = fuse_scalars(af, 3, af.step_offset);
@@ -1735,6 +1736,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
       float sum = 0.f;
       for (int w = 0; w < af.n_part; ++w) sum += af.loss_part[w * af.n_losses + threadIdx.x];
       af.sc->losses[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
+      if (af.loss_host) af.loss_host[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
     }
     if (threadIdx.x == 0 && af.log_alpha_idx >= 0 && af.auto_entropy) {
       const AdamScalars k = fuse_scalars(af, 3, af.step_offset);

@@ -136,6 +136,8 @@ struct sacmi_ctx {
   int push_slot = 0;
   float* act_host = nullptr;                // [kActPinned][S] states, then [..][A] eps / out
   float* act_host_dev = nullptr;            // the same memory, device-mapped
+  float* loss_host = nullptr;               // [4] losses of the last fused update (mapped)
+  float* loss_host_dev = nullptr;
   sacmi::DevScalars* sc_host = nullptr;
   // PER scratch (replay_kind == PER)
   sacmi::DevBuf<float> per_probs, per_chunk, per_w, per_val;
@@ -336,6 +338,11 @@ static void alloc_pinned(sacmi_ctx* c) {
                           (size_t)kActPinned * (S + 2 * A) * 4,
                           hipHostMallocMapped | hipHostMallocCoherent));
   CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->act_host_dev), c->act_host, 0));
+  // update_parameters' three losses, stored here by the fused Adam levels' block 0: the
+  // synchronous step reads them after the stream sync, no copy command
+  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->loss_host), 16,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->loss_host_dev), c->loss_host, 0));
   CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->sc_host), sizeof(DevScalars),
                           hipHostMallocDefault));
 }
@@ -351,6 +358,9 @@ static void free_pinned(sacmi_ctx* c) {
   if (c->sc_host) (void)hipHostFree(c->sc_host);
   c->act_host = nullptr;
   c->act_host_dev = nullptr;
+  if (c->loss_host) (void)hipHostFree(c->loss_host);
+  c->loss_host = nullptr;
+  c->loss_host_dev = nullptr;
   c->sc_host = nullptr;
 }
 
@@ -697,6 +707,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.lr = (float)c->cfg.lr; f.beta1 = 0.9f; f.beta2 = 0.999f; f.eps = 1e-8f;
       f.tau = (float)c->cfg.tau; f.step_offset = 1; f.sc = c->sc.p;
       f.loss_part = c->lpart_c.p; f.n_part = nb; f.loss_slot0 = 0; f.n_losses = 2;
+      f.loss_host = c->loss_host_dev;
       f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
     }
     run(l6, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1");
@@ -808,6 +819,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.lr = (float)c->cfg.lr; f.beta1 = 0.9f; f.beta2 = 0.999f; f.eps = 1e-8f; f.tau = 0.f;
       f.step_offset = 0; f.sc = c->sc.p;
       f.loss_part = c->lpart_a.p; f.n_part = nb; f.loss_slot0 = 2; f.n_losses = 1;
+      f.loss_host = c->loss_host_dev;
       f.loss_div = (float)B; f.log_alpha_idx = c->la_idx; f.auto_entropy = c->cfg.auto_entropy;
       f.log_alpha_grad = G + c->la_idx;
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
@@ -1377,8 +1389,8 @@ int sacmi_step(sacmi_ctx* c, int32_t batch, const int64_t* idx, const float* eps
     stage_inputs(c, batch, idx, eps1, eps2);
     run_update(c, batch, idx ? 0 : 1, (eps1 || eps2) ? 0 : 1, 7, 1.f, false);
     if (losses_out) {
-      DevScalars h = download_scalars(c);
-      std::memcpy(losses_out, h.losses, 12);
+      CHECK_HIP(hipStreamSynchronize(c->stream));
+      std::memcpy(losses_out, c->loss_host, 12);    // stored by the update's last kernels
     }
   });
 }

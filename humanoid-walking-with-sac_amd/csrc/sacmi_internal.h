@@ -124,6 +124,7 @@ struct AdamFuse {
   int64_t log_alpha_idx; int auto_entropy;   // scalar alpha Adam (step idx 3), -1: none
   const float* log_alpha_grad;               // written by k_critic_rows
   float* loss_ring; int ring;
+  float* loss_host;      // or null: the losses also stored to host-mapped memory (sync step)
 };
 
 struct GatherArgs {
