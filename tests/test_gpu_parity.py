@@ -544,6 +544,13 @@ def test_bf16_compute_vs_emulation(n_hidden, B):
         ctx.push(*rows)
         lg = ctx.step(B, idx=idx, eps1=e1, eps2=e2)
         res[dt] = (lg, ctx_grads(ctx, cfg))
+        # one update = one step of each optimizer (the actor-pass row prologue advances
+        # them exactly once, whichever kernel runs it) and alpha = exp(log_alpha)
+        from sacmi import _lib as L
+        for which in (L.S_STEP_POLICY, L.S_STEP_Q1, L.S_STEP_Q2, L.S_STEP_ALPHA):
+            assert ctx.get_scalar(which) == 1.0, (dt, which)
+        la = ctx.get_scalar(L.S_LOG_ALPHA)
+        assert abs(ctx.get_scalar(L.S_ALPHA) - np.exp(np.float32(la))) <= 1e-6
         ctx.close()
     batch = [x[idx] for x in rows]
     emu = OracleSAC(cfg, params, torch.float64)

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""HBM-side traffic per sacmi::k_gemm launch from two rocprofv3 --pmc passes
-(tools/gpu_pmc.sh): FETCH_SIZE and WRITE_SIZE, both in KB per dispatch.
+"""HBM-side traffic per GEMM level from two rocprofv3 --pmc passes (tools/gpu_pmc.sh):
+FETCH_SIZE and WRITE_SIZE, both in KB per dispatch.  A level is one sacmi::k_gemm,
+k_fwd / k_fwd16 or k_axk16 launch, or one split-K k_dw_part* launch plus its k_dw_fin
+(bench.py's roofline counts launches the same way).
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports exactly half
 of the bytes of a wide coalesced streaming read -> doubled here.  WRITE_SIZE is exact for
@@ -23,7 +25,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        key = "sacmi::k_gemm" if name.startswith("void sacmi::k_gemm<") else name
+        key = "sacmi::k_gemm" if name.startswith("void sacmi::k_gemm<") else name.split("(")[0]
         acc[key][0] += float(r["Counter_Value"])
         acc[key][1] += 1
     return {k: (v[0] / v[1], v[1]) for k, v in acc.items()}
@@ -43,7 +45,18 @@ def main(root, out=None):
     for k, v in rows.items():
         print(f"{k[:60]:60s} {v['launches']:6d}  fetch {v['fetch_bytes'] / 1e6:8.3f} MB  "
               f"write {v['write_bytes'] / 1e6:8.3f} MB")
-    res = {"kernel": "sacmi::k_gemm", "per_launch": rows.get("sacmi::k_gemm"),
+    # the GEMM-level family: per level = all their bytes / the number of levels
+    lv = [k for k in rows if k.startswith(("sacmi::k_gemm", "void sacmi::k_fwd", "void sacmi::k_axk16",
+                                           "sacmi::k_dw_part", "void sacmi::k_dw_part"))]
+    fin = [k for k in rows if "k_dw_fin" in k]
+    n_lv = sum(rows[k]["launches"] for k in lv)
+    per_level = None
+    if n_lv:
+        tot = lambda f: sum(rows[k][f] * rows[k]["launches"] for k in lv + fin)
+        per_level = {"launches": n_lv, "fetch_bytes": tot("fetch_bytes") / n_lv,
+                     "write_bytes": tot("write_bytes") / n_lv, "traffic_bytes": tot("traffic_bytes") / n_lv}
+    res = {"kernel": "GEMM levels (k_gemm, k_fwd*, k_axk16, k_dw_part* + k_dw_fin)",
+           "per_launch": per_level,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read half count); KB -> bytes x1024",
            "all": rows}
     if out:
