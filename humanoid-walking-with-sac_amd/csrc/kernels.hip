@@ -1702,14 +1702,17 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
     const bool pol = d.epi == EPI_ADAM_POLYAK;
     const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
     const float* wsd = batch.ws + off;
+    const rsrc_t rWs = make_rsrc(wsd, (uint32_t)(((int64_t)(ns - 1) * ws_stride + n_el) * 4));
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n_el; e += gridDim.x * blockDim.x) {
       const int row = e / nc, col = e - row * nc;
       const int n = col < d.N ? col : d.rs_col;
-      // all NS partial loads in flight at once (a runtime-trip loop waited on each), then
-      // the fixed-order sum
+      // all NS partial loads in flight at once, then the fixed-order sum.  Buffer loads
+      // with an out-of-range offset past NS (return 0, no access): no guard, so nothing
+      // drains the load queue between them (a guarded load waits at its guard's end)
       float t[kDwMaxSplit];
 #pragma unroll
-      for (int s = 0; s < kDwMaxSplit; ++s) t[s] = s < ns ? wsd[(int64_t)s * ws_stride + e] : 0.f;
+      for (int s = 0; s < kDwMaxSplit; ++s)
+        t[s] = buf_ld(rWs, s < ns ? (uint32_t)((int64_t)s * ws_stride + e) * 4u : 0xfffffff0u);
       float v = t[0];
 #pragma unroll
       for (int s = 1; s < kDwMaxSplit; ++s)

@@ -1,7 +1,8 @@
 cd $GRAFT_REPO_ROOT
-O=$GRAFT_REPO_ROOT/gpurun_out
-PYTEST_ARGS='-k "bf16"' bash tools/gpu_round.sh test || exit 1
-for c in 2 3 5; do
-  PMC_ARGS="--config $c --steps 100 --warmup 20 --fill 200000 --no-cpu-baseline --no-roofline --no-trainer-loop" bash tools/gpu_pmc.sh > $O/pmc_run_c$c.log 2>&1 || exit 1
-  python3 tools/pmc_summary.py $O $O/pmc_c$c.json > $O/pmc_c$c.txt || exit 1
+O=gpurun_out
+V=$GRAFT_REPO_ROOT/humanoid-walking-with-sac_amd/sacmi
+PYTEST_ARGS='-k "bf16 or b4096"' bash tools/gpu_round.sh test || exit 1
+for v in main f0; do
+  if [ $v = main ]; then L=""; else L=$V/libsacmi_$v.so; fi
+  SACMI_LIB_PATH=$L timeout -k 10 200 python3 bench.py --config 5 --steps 200 --no-cpu-baseline --no-trainer-loop > $O/v_$v.json 2>$O/v_$v.err || exit 1
 done
