@@ -562,6 +562,9 @@ __global__ void k_per_f2b(PerArgs a) {
   for (int64_t j = 0; j < a.len; ++j) a.cdf[j] = a.cdf[j] / last;
 }
 
+#ifndef SACMI_PER_F4
+#define SACMI_PER_F4 1          // w /= max(w) in its own kernel (0: F3 last workgroup, fence + counter: 5 us slower)
+#endif
 __global__ __launch_bounds__(256) void k_per_f3(PerArgs a, int nb, int64_t stride, int ntop) {
 #pragma clang fp contract(off)
   extern __shared__ int64_t off[];       // [nb] exclusive prefix of the block totals
@@ -624,6 +627,9 @@ __global__ __launch_bounds__(256) void k_per_f3(PerArgs a, int nb, int64_t strid
   for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
   unsigned int* wmax = reinterpret_cast<unsigned int*>(a.bad + 1);
   if ((threadIdx.x & 63) == 0) atomicMax(wmax, m);
+#if SACMI_PER_F4
+  return;            // w /= max(w) in k_per_f4 (the kernel boundary orders the atomics)
+#endif
   // last workgroup: w /= max(w)
   __threadfence();
   __syncthreads();
@@ -634,6 +640,13 @@ __global__ __launch_bounds__(256) void k_per_f3(PerArgs a, int nb, int64_t strid
   const float mx = __uint_as_float(__atomic_load_n(wmax, __ATOMIC_RELAXED));
   for (int i = threadIdx.x; i < a.k; i += blockDim.x)
     a.w_out[i] = __builtin_nontemporal_load(a.w_out + i) / mx;
+}
+
+__global__ void k_per_f4(PerArgs a) {
+  const unsigned int* wmax = reinterpret_cast<const unsigned int*>(a.bad + 1);
+  const float mx = __uint_as_float(*wmax);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.k) a.w_out[i] = a.w_out[i] / mx;
 }
 
 void launch_per_sample(const PerArgs& a, hipStream_t s) {
@@ -662,6 +675,7 @@ void launch_per_sample(const PerArgs& a, hipStream_t s) {
       attr3 = lds3;
     }
     hipLaunchKernelGGL(k_per_f3, dim3((a.k + 255) / 256), dim3(256), lds3, s, a, nb0, stride, ntop);
+    if (SACMI_PER_F4) hipLaunchKernelGGL(k_per_f4, dim3((a.k + 255) / 256), dim3(256), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) fprintf(stderr, "sacmi: PER launch failed: %s\n", hipGetErrorString(e));
     return;

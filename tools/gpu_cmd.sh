@@ -1,8 +1,8 @@
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
 V=$GRAFT_REPO_ROOT/humanoid-walking-with-sac_amd/sacmi
-PYTEST_ARGS='-k "bf16 or b4096"' bash tools/gpu_round.sh test || exit 1
-for v in main f0; do
+SACMI_LIB_PATH=$V/libsacmi_f4.so PYTEST_ARGS='-k "per"' bash tools/gpu_round.sh test || exit 1
+for v in main f4; do
   if [ $v = main ]; then L=""; else L=$V/libsacmi_$v.so; fi
-  SACMI_LIB_PATH=$L timeout -k 10 200 python3 bench.py --config 5 --steps 200 --no-cpu-baseline --no-trainer-loop > $O/v_$v.json 2>$O/v_$v.err || exit 1
+  SACMI_LIB_PATH=$L timeout -k 10 200 python3 bench.py --config 3 --steps 100 --no-cpu-baseline --no-trainer-loop > $O/v_$v.json 2>$O/v_$v.err || exit 1
 done
