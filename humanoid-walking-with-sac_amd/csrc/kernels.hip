@@ -1230,18 +1230,38 @@ constexpr int kDwMaxSplit = 16;
 // [M][ncols] with ncols = N (+1 for the row-sum column)
 __device__ __forceinline__ int dw_ncols(const GemmDesc& d) { return d.rs_col >= 0 ? d.N + 1 : d.N; }
 
+// XCD placement of the split-K work (workgroup b runs on XCD b % 8): the split-major work
+// list w = split * tiles + tile is dealt to the XCDs in contiguous eighths, so each XCD's
+// L2 streams the rows of one or two K ranges instead of every range (SACMI_DW_XCD 0: the
+// plain order).  The tile grid is padded to a multiple of 8 workgroups.
+#ifndef SACMI_DW_XCD
+#define SACMI_DW_XCD 1
+#endif
+__host__ __device__ __forceinline__ int dw_grid_tiles(int tiles, int ns) {
+  return SACMI_DW_XCD ? (tiles * ns + 7) / 8 * 8 : tiles * ns;
+}
+__device__ __forceinline__ int dw_work_index(int b, int tiles, int ns) {
+  if (!SACMI_DW_XCD) return b;
+  const int W = tiles * ns, per = (W + 7) / 8;
+  const int w = (b % 8) * per + b / 8;
+  return w < W ? w : -1;
+}
+
 template <bool BF16>
 __global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int64_t ws_stride) {
   __shared__ __attribute__((aligned(16))) float sA[2][kDBK][kDBM + kDPad];
   __shared__ __attribute__((aligned(16))) float sB[2][kDBK][kDBN + kDPad];
   const int tiles_tot = batch.total_tiles;
-  if ((int)blockIdx.x >= tiles_tot * ns) {   // ride-along: the next update's gather
-    const int rb = blockIdx.x - tiles_tot * ns, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nwg = dw_grid_tiles(tiles_tot, ns);
+  if ((int)blockIdx.x >= nwg) {   // ride-along: the next update's gather
+    const int rb = blockIdx.x - nwg, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int b = rb * 4 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 4)
       gather_row(batch.ride.ga, b, lane, 64);
     return;
   }
-  const int split = blockIdx.x / tiles_tot, bid = blockIdx.x % tiles_tot;
+  const int wk = dw_work_index(blockIdx.x, tiles_tot, ns);
+  if (wk < 0) return;
+  const int split = wk / tiles_tot, bid = wk % tiles_tot;
   int p = 0;
   for (int q = 1; q < batch.count; ++q)
     if (bid >= batch.d[q].tile_begin) p = q;
@@ -1366,13 +1386,16 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   __shared__ __attribute__((aligned(16))) __bf16 sB[2][kD16K][LDR];
   __shared__ float s_rs[8][kDBM];
   const int tiles_tot = batch.total_tiles;
-  if ((int)blockIdx.x >= tiles_tot * ns) {   // ride-along: the next update's gather
-    const int rb = blockIdx.x - tiles_tot * ns, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nwg = dw_grid_tiles(tiles_tot, ns);
+  if ((int)blockIdx.x >= nwg) {   // ride-along: the next update's gather
+    const int rb = blockIdx.x - nwg, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int b = rb * 4 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 4)
       gather_row(batch.ride.ga, b, lane, 64);
     return;
   }
-  const int split = blockIdx.x / tiles_tot, bid = blockIdx.x % tiles_tot;
+  const int wk = dw_work_index(blockIdx.x, tiles_tot, ns);
+  if (wk < 0) return;
+  const int split = wk / tiles_tot, bid = wk % tiles_tot;
   int p = 0;
   for (int q = 1; q < batch.count; ++q)
     if (bid >= batch.d[q].tile_begin) p = q;
@@ -1826,9 +1849,10 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     const int ns = SACMI_DW_SPLIT ? dw_split_plan(b, &stride) : 0;
     if (ns > 0) {
       const int ride = b.ride.kind == 2 ? b.ride.nblocks : 0;
-      if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
-      else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
-      else hipLaunchKernelGGL(k_dw_part<false>, dim3(b.total_tiles * ns + ride), dim3(256), 0, s, b, ns, stride);
+      const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
+      if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16, dim3(grid), dim3(256), 0, s, b, ns, stride);
+      else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
+      else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
       const int fin_grid = (int)std::min<int64_t>((stride + 255) / 256, 4096);
       hipLaunchKernelGGL(k_dw_fin, dim3(fin_grid), dim3(256), 0, s, b, ns, stride);
