@@ -1219,6 +1219,9 @@ constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
 #define SACMI_DW_TARGET 512     // k_dw_part workgroup slots (256 CUs x 2)
 #endif
 constexpr int kDwMaxSplit = 16;
+#ifndef SACMI_DW_SPLIT_FP32
+#define SACMI_DW_SPLIT_FP32 0   // the split-K dW path for fp32 levels too (k_dw_part<false>)
+#endif
 #ifndef SACMI_AXK_LDS16
 #define SACMI_AXK_LDS16 1       // bf16 mode: k_axk16 for the batch-4096-class dh levels
 #endif
@@ -1787,7 +1790,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
 
 // bf16 deep-K weight-gradient levels: split count and workspace need, or 0 (old path)
 static int dw_split_plan(GemmBatch& b, int64_t* stride) {
-  if (!b.bf16 || !b.ws || (b.ride.kind && b.ride.kind != 2)) return 0;
+  if ((!b.bf16 && !SACMI_DW_SPLIT_FP32) || !b.ws || (b.ride.kind && b.ride.kind != 2)) return 0;
   int64_t el = 0;
   int tiles = 0;
   for (int i = 0; i < b.count; ++i) {

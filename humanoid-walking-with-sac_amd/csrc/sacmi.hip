@@ -287,6 +287,7 @@ static void alloc_all(sacmi_ctx* c) {
   c->logp.alloc((size_t)2 * Bm);
   c->dq.alloc((size_t)2 * Bm + 16);   // + slack: the split-K dW kernels read 4 wide (kernels.hip)
   c->nparts = (H + 31) / 32;
+  // split-K dW partials (kernels.hip; bf16 only: the fp32 levels measured slower split)
   if (c->bf16 && Bm >= 2048) c->dw_ws.alloc((size_t)16 * c->total);
   c->dotp.alloc((size_t)6 * Bm * c->nparts);
   c->dhead.alloc((size_t)Bm * c->lddh);

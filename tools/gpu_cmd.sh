@@ -1,3 +1,8 @@
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-timeout -k 10 400 python3 bench.py --config 5 > $O/b_c5.json 2> $O/b_c5.err || exit 1
+V=$GRAFT_REPO_ROOT/humanoid-walking-with-sac_amd/sacmi
+SACMI_LIB_PATH=$V/libsacmi_s32.so PYTEST_ARGS='-k "b4096"' bash tools/gpu_round.sh test || exit 1
+for v in main s32; do
+  if [ $v = main ]; then L=""; else L=$V/libsacmi_$v.so; fi
+  SACMI_LIB_PATH=$L timeout -k 10 200 python3 bench.py --config 3 --steps 100 --no-cpu-baseline --no-trainer-loop > $O/v_$v.json 2>$O/v_$v.err || exit 1
+done
