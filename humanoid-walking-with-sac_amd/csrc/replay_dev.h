@@ -159,9 +159,9 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
         r = mt_temper(key[pos + t]) >> (32 - kb);
         acc = r < n;
       }
-      int ncand;
-      const int crank = block_scan_flag(acc, wave_tot, &ncand);
-      const int seq = seqbase + crank;
+      // a candidate's order key is its word's position in the stream (monotone in draw
+      // order, so the smallest key per value is its first occurrence): no scan needed
+      const int seq = seqbase + t;
       uint32_t slot = 0;
       if (acc) {
         slot = hash_slot(r, mask);
@@ -183,9 +183,10 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
       __syncthreads();
       if (count + nfirst >= k) { pos = pos + s_last + 1; break; }
       count += nfirst;
-      seqbase += ncand;
+      seqbase += avail;
       pos = kMtN;
-      __syncthreads();
+      // (no barrier here: the next twist reads key only after this iteration's last
+      // barrier, and the scans' own barriers order every wave_tot reuse)
     }
   }
   __syncthreads();
