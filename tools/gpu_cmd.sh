@@ -1,4 +1,8 @@
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-PYTEST_ARGS='-k "sample or many_updates or ride or dp or golden"' bash tools/gpu_round.sh test || exit 1
-timeout -k 10 200 python3 bench.py --config 5 --steps 200 --no-cpu-baseline --no-trainer-loop > $O/v_main.json 2>$O/v_main.err || exit 1
+V=$GRAFT_REPO_ROOT/humanoid-walking-with-sac_amd/sacmi
+SACMI_LIB_PATH=$V/libsacmi_b256.so PYTEST_ARGS='-k "bf16"' bash tools/gpu_round.sh test || exit 1
+for v in main b256; do
+  if [ $v = main ]; then L=""; else L=$V/libsacmi_$v.so; fi
+  SACMI_LIB_PATH=$L timeout -k 10 200 python3 bench.py --config 5 --steps 200 --no-cpu-baseline --no-trainer-loop > $O/v_$v.json 2>$O/v_$v.err || exit 1
+done
