@@ -365,24 +365,30 @@ def test_polyak_bitexact_and_determinism():
             assert np.array_equal(outs[0][n][k], outs[1][n][k]), (n, k)
 
 
-def test_many_updates_per_launch_identical():
+@pytest.mark.parametrize("shape", ["small", "nao_b4096_bf16"])
+def test_many_updates_per_launch_identical(shape):
     """sacmi_step_many_async(n) (trainer.py:203-204 loop in one launch) == n single
-    launches, bit for bit, losses included."""
-    cfg = SacConfig(24, 4, 64)
+    launches, bit for bit, losses included — also at the config-5 shapes (batch 4096,
+    bf16: the LDS-staged level kernels, split-K dW with its XCD placement, device
+    sampling of 4096 rows)."""
+    if shape == "small":
+        cfg, B, nrows, dt = SacConfig(24, 4, 64), 64, 500, "fp32"
+    else:
+        cfg, B, nrows, dt = SacConfig(661, 23, 512), 4096, 6000, "bf16"
     params = init_params(cfg, 61, bias_scale=0.05)
-    rows = synthetic_rows(cfg, 500, 62, state_scale=0.5)
+    rows = synthetic_rows(cfg, nrows, 62, state_scale=0.5)
     res = []
     for many in (True, False):
-        ctx = make_ctx(cfg, max_batch=64, capacity=500)
+        ctx = make_ctx(cfg, max_batch=B, capacity=nrows, compute_dtype=dt)
         load_params(ctx, params)
         ctx.push(*rows)
         ctx.set_mt(0, (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32), 624)
         if many:
-            ctx.step_many_async(64, 5)
-            ctx.step_many_async(64, 2)
+            ctx.step_many_async(B, 5)
+            ctx.step_many_async(B, 2)
         else:
             for _ in range(7):
-                ctx.step_async(64)
+                ctx.step_async(B)
         res.append((ctx.fetch_losses(7), {n: ctx.get_net(n) for n in NETS}, ctx.get_mt(0)))
     assert np.array_equal(res[0][0], res[1][0]) and res[0][0].shape == (7, 3)
     for n in NETS:
