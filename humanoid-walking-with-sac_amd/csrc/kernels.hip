@@ -73,6 +73,14 @@ __device__ __forceinline__ void buf_st(rsrc_t r, uint32_t off, float v) {
 // hipcc) __builtin_amdgcn_raw_buffer_load_b128 lowers to a single buffer_load_dword.
 __device__ f4 llvm_raw_buffer_load_v4f32(rsrc_t r, int off, int soff, int aux)
     __asm("llvm.amdgcn.raw.ptr.buffer.load.v4f32");
+__device__ __forceinline__ uint2 buf_ld2(rsrc_t r, uint32_t off) {
+  typedef unsigned int u2_t __attribute__((ext_vector_type(2)));
+  const u2_t v = __builtin_bit_cast(u2_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ unsigned short bf16_bits(float x) {
+  return __builtin_bit_cast(unsigned short, (__bf16)x);
+}
 __device__ __forceinline__ float4 buf_ld4(rsrc_t r, uint32_t off) {
   const f4 v = llvm_raw_buffer_load_v4f32(r, (int)off, 0, 0);
   return float4{v[0], v[1], v[2], v[3]};
@@ -832,7 +840,12 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
         adam_elem(x0[s], x1[s], x2[s], v, omb1, af.beta2, omb2, af.eps, s_k);
         if (af.G) buf_st(rG, o, v);
         buf_st(rC, o, x0[s]); buf_st(rM, o, x1[s]); buf_st(rV, o, x2[s]);
-        if (pol) buf_st(rT, o, polyak(x3[s], x0[s], omtau, af.tau));
+        if (af.Ph) af.Ph[abase + (o >> 2)] = bf16_bits(x0[s]);
+        if (pol) {
+          const float tn = polyak(x3[s], x0[s], omtau, af.tau);
+          buf_st(rT, o, tn);
+          if (af.Th) af.Th[abase - af.t_base + (o >> 2)] = bf16_bits(tn);
+        }
       } else {
         if (d.bias) v += x0[s];
         if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
@@ -1107,7 +1120,7 @@ __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
   return __builtin_bit_cast(u2v, x);
 }
 
-template <int kFBN>
+template <int kFBN, bool BH = false>
 __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
   constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
   constexpr int LDR = kHBK + kHPad;      // bf16 per LDS row: 144 B at 64 deep
@@ -1152,9 +1165,16 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
     offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
   }
   const int kq = 4 * (tid % TPR);
-  float4 ga[NA], gb[NB];
+  float4 ga[NA], gb[BH ? 1 : NB];
+  uint2 gh[BH ? NB : 1];              // BH: B from its bf16 shadow, 4 k per 8 bytes
+  const rsrc_t rBh = make_rsrc(BH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
   auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
     x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
+    return x;
+  };
+  auto zkh = [&](uint2 x, int k) {
+    x.x = (k < K ? x.x & 0xffffu : 0u) | (k + 1 < K ? x.x & 0xffff0000u : 0u);
+    x.y = (k + 2 < K ? x.y & 0xffffu : 0u) | (k + 3 < K ? x.y & 0xffff0000u : 0u);
     return x;
   };
   auto gload = [&](int k0) {
@@ -1162,14 +1182,22 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
 #pragma unroll
     for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+    if constexpr (BH) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i) gb[i] = zk(buf_ld4(rB, offB[i] + ko), k);
+      for (int i = 0; i < NB; ++i) gh[i] = zkh(buf_ld2(rBh, offB[i] / 2u + ko / 2u), k);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) gb[i] = zk(buf_ld4(rB, offB[i] + ko), k);
+    }
   };
   auto swrite = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(ga[i]);
 #pragma unroll
-    for (int i = 0; i < NB; ++i) *reinterpret_cast<u2v*>(&sB[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(gb[i]);
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (BH) *reinterpret_cast<u2v*>(&sB[buf][tid / TPR + RPP * i][kq]) = u2v{gh[i].x, gh[i].y};
+      else *reinterpret_cast<u2v*>(&sB[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(gb[i]);
+    }
   };
   f4 acc[4][NT];
 #pragma unroll
@@ -1539,7 +1567,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
 // model2 L5b / L9b / L11), no transform, no prologue.
 constexpr int kXBM = 64, kXBN = 128, kXBK = 64;
 
-template <bool AX>
+template <bool AX, bool BH = false>
 __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
   constexpr int LDA_ = kXBK + 8;        // [row][k] bf16, 144-B rows
   constexpr int LDB_ = kXBN + 8;        // [k][n] bf16, 272-B rows
@@ -1580,7 +1608,9 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
   for (int i = 0; i < 4; ++i)
     offA[i] = (uint32_t)min(m0 + (tid >> 4) + 16 * i, M - 1) * (uint32_t)d.lda * 4u;
   const int nb = min(n0 + c4, N - 1);
-  float4 ga[4], gb[8], gw;
+  float4 ga[4], gb[BH ? 1 : 8], gw;
+  uint2 gh[BH ? 8 : 1];               // BH: W from its bf16 shadow
+  const rsrc_t rBh = make_rsrc(BH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
   auto gload = [&](int k0) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
@@ -1591,10 +1621,18 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
     for (int i = 0; i < 8; ++i) {
       const int kb = k0 + kr0 + 8 * i;
       const bool kin = kb < K;
-      float4 y = buf_ld4(rB, ((uint32_t)(kin ? kb : 0) * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
-      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
-      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
-      gb[i] = y;
+      const uint32_t e = (uint32_t)(kin ? kb : 0) * (uint32_t)d.ldb + (uint32_t)nb;
+      if constexpr (BH) {
+        uint2 h = buf_ld2(rBh, e * 2u);
+        h.x = (kin && n0 + c4 < N ? h.x & 0xffffu : 0u) | (kin && n0 + c4 + 1 < N ? h.x & 0xffff0000u : 0u);
+        h.y = (kin && n0 + c4 + 2 < N ? h.y & 0xffffu : 0u) | (kin && n0 + c4 + 3 < N ? h.y & 0xffff0000u : 0u);
+        gh[i] = h;
+      } else {
+        float4 y = buf_ld4(rB, e * 4u);
+        y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+        y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+        gb[i] = y;
+      }
     }
   };
   auto swrite = [&](int buf, int k0, bool fresh) {
@@ -1616,7 +1654,10 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (BH) *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = u2v{gh[i].x, gh[i].y};
+      else *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+    }
   };
   f4 acc[2][4];
 #pragma unroll
@@ -1749,9 +1790,12 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
         adam_elem(pp, mm, vv, v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
         if (af.G) af.G[abase + o] = v;
         d.C[o] = pp; af.M[abase + o] = mm; af.V[abase + o] = vv;
+        if (af.Ph) af.Ph[abase + o] = bf16_bits(pp);
         if (pol) {
           float* tp = af.T + abase - af.t_base + o;
-          *tp = polyak(*tp, pp, omtau, af.tau);
+          const float tn = polyak(*tp, pp, omtau, af.tau);
+          *tp = tn;
+          if (af.Th) af.Th[abase - af.t_base + o] = bf16_bits(tn);
         }
       } else {
         d.C[o] = v;
@@ -1844,6 +1888,17 @@ static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
   else hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, false>), dim3(grid), blk, 0, s, b);
 }
 
+// every desc's B operand has a bf16 shadow (SACMI_BF16_SHADOW 0: never read them)
+#ifndef SACMI_BF16_SHADOW
+#define SACMI_BF16_SHADOW 1
+#endif
+static bool all_bh(const GemmBatch& b) {
+  if (!SACMI_BF16_SHADOW) return false;
+  for (int i = 0; i < b.count; ++i)
+    if (!b.d[i].Bh) return false;
+  return true;
+}
+
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
@@ -1867,8 +1922,11 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (SACMI_AXK_LDS16) {
     const int ax = axk16_ok(b);
     if (ax >= 0) {
-      if (ax) hipLaunchKernelGGL(k_axk16<true>, dim3(b.total_tiles), dim3(256), 0, s, b);
-      else hipLaunchKernelGGL(k_axk16<false>, dim3(b.total_tiles), dim3(256), 0, s, b);
+      const bool bh = all_bh(b);
+      if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      else if (ax) hipLaunchKernelGGL((k_axk16<true, false>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      else if (bh) hipLaunchKernelGGL((k_axk16<false, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      else hipLaunchKernelGGL((k_axk16<false, false>), dim3(b.total_tiles), dim3(256), 0, s, b);
       HIP_LAUNCH_CHECK();
       return;
     }
@@ -1877,7 +1935,10 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
   if (fwd_big && fwd_big_ok(b)) {
     const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
-    if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    const bool bh = b.bf16 && all_bh(b);
+    if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    else if (b.bf16 && SACMI_FWD_LDS16 && bh) hipLaunchKernelGGL((k_fwd16<64, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    else if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16) hipLaunchKernelGGL((k_fwd16<64>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && n128) hipLaunchKernelGGL((k_fwd<true, 128>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16) hipLaunchKernelGGL((k_fwd<true, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
@@ -2074,6 +2135,18 @@ void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int c
   HIP_LAUNCH_CHECK();
 }
 
+__global__ void k_to_bf16(unsigned short* dst, const float* src, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = bf16_bits(src[i]);
+}
+
+void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_to_bf16, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, n);
+  HIP_LAUNCH_CHECK();
+}
+
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {
   const int grid = (a.rows + 15) / 16;
   const int n = 2 * a.A;
@@ -2247,6 +2320,10 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     *reinterpret_cast<float4*>(a.p + i) = p;
     *reinterpret_cast<float4*>(a.m + i) = m;
     *reinterpret_cast<float4*>(a.v + i) = v;
+    if (a.ph) {
+      a.ph[i] = bf16_bits(p.x); a.ph[i + 1] = bf16_bits(p.y);
+      a.ph[i + 2] = bf16_bits(p.z); a.ph[i + 3] = bf16_bits(p.w);
+    }
     if (a.tgt) {
       float4* tp = reinterpret_cast<float4*>(a.tgt + (i - a.tgt_base));
       float4 t = *tp;
@@ -2255,6 +2332,10 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
       t.z = polyak(t.z, p.z, omtau, a.tau);
       t.w = polyak(t.w, p.w, omtau, a.tau);
       *tp = t;
+      if (a.tgth) {
+        unsigned short* th = a.tgth + (i - a.tgt_base);
+        th[0] = bf16_bits(t.x); th[1] = bf16_bits(t.y); th[2] = bf16_bits(t.z); th[3] = bf16_bits(t.w);
+      }
     }
   }
   if (blockIdx.x != 0) return;

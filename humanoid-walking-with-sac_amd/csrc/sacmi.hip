@@ -99,6 +99,10 @@ struct sacmi_ctx {
   int64_t q_begin = 0, q_end = 0, pi_begin = 0, la_idx = 0, total = 0;
   // arenas
   sacmi::DevBuf<float> P, T, G, M, V;
+  // bf16 mode: bf16 shadows of P and T (RNE, as every bf16 consumer rounds at staging),
+  // kept current by every parameter store; the large-batch level kernels stage their
+  // weight operands from them (half the bytes)
+  sacmi::DevBuf<unsigned short> Ph, Th;
   sacmi::DevBuf<sacmi::DevScalars> sc;
   // replay
   int ldo = 0, ldact = 0;
@@ -244,6 +248,7 @@ static void alloc_all(sacmi_ctx* c) {
   const int Bm = c->Bm, S = c->S, A = c->A, H = c->H;
   c->P.alloc(c->total); c->G.alloc(c->total); c->M.alloc(c->total); c->V.alloc(c->total);
   c->T.alloc(c->q_end);
+  if (c->bf16) { c->Ph.alloc(c->total); c->Th.alloc(c->q_end); }
   c->sc.alloc(1);
   c->ldo = round_up(S, 4);
   c->ldact = round_up(A, 4);
@@ -586,8 +591,15 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   auto dW = [&](const Linear& l) { return G + l.off; };
   const Linear(&q)[2][4] = c->q_fc;
   const int nh = c->nh, L = nh - 1;   // L: the last hidden layer (its head is layer nh)
+  auto shadow = [&](const float* b) -> const unsigned short* {
+    if (!c->Ph.p || !b) return nullptr;
+    if (b >= c->P.p && b < c->P.p + c->P.n) return c->Ph.p + (b - c->P.p);
+    if (b >= c->T.p && b < c->T.p + c->T.n) return c->Th.p + (b - c->T.p);
+    return nullptr;
+  };
   auto run = [&](Level& lv, const std::string& name) {
     lv.b.bf16 = c->bf16 ? 1 : 0;
+    for (int i = 0; i < lv.b.count; ++i) lv.b.d[i].Bh = shadow(lv.b.d[i].B);
     lv.b.ws = c->dw_ws.p;
     lv.b.ws_floats = (int64_t)c->dw_ws.n;
     if (mark(c, name.c_str(), level_flops(lv.b), level_bytes(lv.b))) launch_gemm(lv.b, s);
@@ -709,6 +721,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.tau = (float)c->cfg.tau; f.step_offset = 1; f.sc = c->sc.p;
       f.loss_part = c->lpart_c.p; f.n_part = nb; f.loss_slot0 = 0; f.n_losses = 2;
       f.loss_host = c->loss_host_dev;
+      f.Ph = c->Ph.p; f.Th = c->Th.p;
       f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
     }
     run(l6, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1");
@@ -821,6 +834,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.step_offset = 0; f.sc = c->sc.p;
       f.loss_part = c->lpart_a.p; f.n_part = nb; f.loss_slot0 = 2; f.n_losses = 1;
       f.loss_host = c->loss_host_dev;
+      f.Ph = c->Ph.p; f.Th = c->Th.p;
       f.loss_div = (float)B; f.log_alpha_idx = c->la_idx; f.auto_entropy = c->cfg.auto_entropy;
       f.log_alpha_grad = G + c->la_idx;
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
@@ -856,6 +870,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.loss_part = c->lpart_a.p; ad.n_part = nb; ad.loss_slot0 = 2; ad.n_losses = 1;
     ad.loss_div = (float)B; ad.log_alpha_idx = c->la_idx; ad.auto_entropy = c->cfg.auto_entropy;
     ad.loss_ring = use_ring ? c->ring.p : nullptr; ad.ring = c->ring_slots;
+    ad.ph = c->Ph.p; ad.tgth = c->Th.p;
     if (mark(c, "adam_actor_alpha")) launch_adam(ad, s);
   }
 }
@@ -1111,6 +1126,7 @@ int sacmi_destroy(sacmi_ctx* c) {
       for (auto* b : {&c->hp[l], &c->hq[l], &c->hqt[l], &c->hqa[l], &c->dhc[l], &c->dha[l], &c->dhp[l]})
         b->release();
     c->sc.release(); c->mt.release(); c->idx32.release(); c->idx64.release();
+    c->Ph.release(); c->Th.release();
     c->idx32b.release(); c->idx64b.release();
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
     c->per_u.release(); c->per_uin.release(); c->per_owner.release(); c->per_bad.release();
@@ -1154,6 +1170,14 @@ static float* slot_base(sacmi_ctx* c, int slot, int net) {
   throw Error{SACMI_EVALUE, "bad slot"};
 }
 
+// re-derive the bf16 shadows after a host write into the parameter / target arenas
+static void refresh_shadows(sacmi_ctx* c) {
+  if (!c->Ph.p) return;
+  launch_to_bf16(c->Ph.p, c->P.p, (int64_t)c->P.n, c->stream);
+  launch_to_bf16(c->Th.p, c->T.p, (int64_t)c->T.n, c->stream);
+  CHECK_HIP(hipStreamSynchronize(c->stream));
+}
+
 static void tensor_io(sacmi_ctx* c, int slot, int net, int layer, int part, float* host,
                       const float* in, int64_t numel) {
   const Linear l = find_linear(c, net, layer);
@@ -1175,7 +1199,10 @@ static void tensor_io(sacmi_ctx* c, int slot, int net, int layer, int part, floa
       }
     }
   }
-  if (in) CHECK_HIP(hipMemcpy(base, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
+  if (in) {
+    CHECK_HIP(hipMemcpy(base, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
+    refresh_shadows(c);
+  }
 }
 
 int sacmi_set_tensor(sacmi_ctx* c, int slot, int net, int layer, int part, const float* host,

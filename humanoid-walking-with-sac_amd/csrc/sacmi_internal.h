@@ -70,6 +70,7 @@ enum Epi { EPI_STORE = 0, EPI_RELU = 1, EPI_MASK = 2,
 struct GemmDesc {
   const float* A;
   const float* B;
+  const unsigned short* Bh;   // bf16 mode: B's bf16 shadow (a parameter operand) or null
   float* C;
   const float* aux;
   int M, N, K;
@@ -125,6 +126,8 @@ struct AdamFuse {
   const float* log_alpha_grad;               // written by k_critic_rows
   float* loss_ring; int ring;
   float* loss_host;      // or null: the losses also stored to host-mapped memory (sync step)
+  unsigned short* Ph;    // bf16 mode: bf16 shadows of the parameter / target arenas, kept
+  unsigned short* Th;    //   in step with every parameter store (null otherwise)
 };
 
 struct GatherArgs {
@@ -239,6 +242,8 @@ struct SampleBwdArgs {
 // launchers (kernels.hip)
 void launch_gemm(const GemmBatch& batch, hipStream_t s);
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
+// dst[i] = bf16(src[i]) (round to nearest even), the parameter shadows of bf16 mode
+void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_t s);
 // rows [n][cols] from host-mapped memory (select_action's states) into a device matrix
 void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int cols, hipStream_t s);
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s);
@@ -261,6 +266,8 @@ struct AdamArgs {
   int64_t log_alpha_idx; int auto_entropy;
   float* loss_ring;        // [ring, 3] or null
   int ring;
+  unsigned short* ph;      // bf16 shadows of p / tgt (bf16 mode) or null
+  unsigned short* tgth;
 };
 void launch_adam(const AdamArgs& a, hipStream_t s);
 
