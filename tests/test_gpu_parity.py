@@ -397,6 +397,38 @@ def test_many_updates_per_launch_identical(shape):
     assert np.array_equal(res[0][2][0], res[1][2][0]) and res[0][2][1] == res[1][2][1]
 
 
+def test_bf16_shadows_stay_current():
+    """bf16 mode keeps bf16 shadows of the weights for the batch-4096 level kernels, written
+    by every Adam / Polyak store.  A context whose shadows are re-derived from its own
+    parameters between updates (set_net -> refresh) must update exactly like one that
+    relies on the in-kernel shadow writes: a stale shadow would change the next update."""
+    cfg = SacConfig(661, 23, 512)
+    B, nrows = 4096, 6000
+    params = init_params(cfg, 81, bias_scale=0.05)
+    rows = synthetic_rows(cfg, nrows, 82, state_scale=0.5)
+    key = (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32)
+    ctxs = []
+    for _ in range(2):
+        ctx = make_ctx(cfg, max_batch=B, capacity=nrows, compute_dtype="bf16")
+        load_params(ctx, params)
+        ctx.push(*rows)
+        ctx.set_mt(0, key, 624)
+        ctxs.append(ctx)
+    a, b = ctxs
+    for _ in range(2):
+        a.step_async(B)
+        b.step_async(B)
+    for n in NETS:                          # b: shadows re-derived from its own weights
+        b.set_net(n, b.get_net(n))
+    a.step_async(B)
+    b.step_async(B)
+    assert np.array_equal(a.fetch_losses(3), b.fetch_losses(3))
+    for n in NETS:
+        pa, pb = a.get_net(n), b.get_net(n)
+        for k in pa:
+            assert np.array_equal(pa[k], pb[k]), (n, k)
+
+
 def test_batch_larger_than_buffer_raises():
     cfg = SacConfig(3, 2, 16)
     ctx = make_ctx(cfg, max_batch=32, capacity=100)
