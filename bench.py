@@ -153,14 +153,27 @@ def pmc_traffic(config, networks="model1"):
         return None, None
 
 
-def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False, n_hidden=2):
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the CPU share the GPU box grants one GPU
+    (OMP_NUM_THREADS, 16 there), never more than the cores present."""
+    share = int(os.environ.get("OMP_NUM_THREADS") or 16)
+    return max(1, min(share, os.cpu_count() or 1))
+
+
+def median_windows(fn, windows):
+    """[fn() for each window] and their median."""
+    vals = [fn() for _ in range(windows)]
+    return float(np.median(vals)), vals
+
+
+def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False, n_hidden=2, windows=3):
     """The reference update on CPU (oracle torch port, fp32) + the reference's replay
     data path (deque + random.sample, or the prioritized buffer's numpy sampler), timed
     on this host's cores for a bounded number of steps."""
     import random
     from oracle.replay_ref import DequeReplay, PerReplayNumpy
     from oracle.sac_step import OracleSAC, SacConfig, init_params
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     s, a, r, s2, d = rows
     S, A = s.shape[1], a.shape[1]
@@ -185,12 +198,19 @@ def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False, n_hidden=
 
     for _ in range(warmup):
         one()
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        one()
-        n += 1
-    dt = time.perf_counter() - t0
+    counts = []
+
+    def window():
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds / windows:
+            one()
+            n += 1
+        dt = time.perf_counter() - t0
+        counts.append(n)
+        return n / dt
+
+    value, rates = median_windows(window, windows)
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -201,10 +221,12 @@ def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False, n_hidden=
         pass
     replay = ("PrioritizedReplayBuffer numpy sampler (np.random.choice over prios**alpha)"
               if per else "deque/random.sample replay")
-    return dict(value=n / dt, unit="grad-steps/s", cores=threads, kind="port",
-                sample=f"{n} updates (after {warmup} warm-up) in {dt:.1f}s at batch {batch}; oracle "
-                       f"torch-CPU fp32 port of sac_imp.update_parameters + {replay} over "
-                       f"{len(r)} rows (float32 rows); {threads} threads on {cpu}")
+    return dict(value=value, unit="grad-steps/s", cores=threads, kind="port",
+                windows=[round(x, 2) for x in rates],
+                sample=f"median of {windows} windows of {seconds / windows:.1f}s ({sum(counts)} updates "
+                       f"after {warmup} warm-up) at batch {batch}; oracle torch-CPU fp32 port of "
+                       f"sac_imp.update_parameters + {replay} over {len(r)} rows (float32 rows); "
+                       f"{threads} threads (the box's CPU share per GPU) on {cpu}")
 
 
 def trainer_loop(wl, steps=300, warmup=30, fill=20_000):
@@ -265,6 +287,9 @@ def parse_args(argv=None):
                     help="GEMM operand arithmetic (default: the config's)")
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--fill", type=int, default=1_000_000)
+    ap.add_argument("--windows", type=int, default=0,
+                    help="timed windows of --steps updates each (median reported); 0: enough "
+                         "windows for >= 2000 timed updates (at least 5)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -283,7 +308,15 @@ def parse_args(argv=None):
     args = ap.parse_args(argv)
     if args.batch is None:                 # both the single-GPU and the DP paths use it
         args.batch = CONFIGS[args.config]["batch"]
+    if args.windows <= 0:
+        args.windows = min(200, max(5, -(-2000 // max(1, args.steps))))
     return args
+
+
+def graph_sizes(steps, per_launch):
+    """Updates per launch of every launch the timed loop of `steps` updates makes."""
+    full, rem = divmod(steps, per_launch)
+    return sorted({n for n in ((per_launch if full else 0), rem) if n > 0})
 
 
 _RESULT_FD = None   # the process's original stdout while fd 1 is routed to stderr
@@ -325,6 +358,7 @@ def main():
         return run_dp_bench(args, rank, world, local_rank, emit)
 
     from sacmi import Config, Context
+    from sacmi import _lib as L
     torch.cuda.init()
     fill = args.fill
     ctx = Context(Config(S, A, H, max_batch=args.batch, capacity=fill, seed=1,
@@ -351,20 +385,29 @@ def main():
         if rem:
             ctx.step_many_async(args.batch, rem)
 
+    # every graph the timed loop replays is captured, instantiated and replayed once
+    # before the first timed window, whatever --warmup is
+    for n in graph_sizes(args.steps, upl):
+        ctx.step_many_async(args.batch, n)
     run_updates(args.warmup)
-    if args.steps % upl:
-        ctx.step_many_async(args.batch, args.steps % upl)     # build that graph untimed
     ctx.synchronize()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_updates(args.steps)
-    losses = ctx.fetch_losses(args.steps)      # D2H of every loss, inside the timed region
-    ctx.synchronize()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    assert losses.shape == (args.steps, 3) and np.all(np.isfinite(losses)), losses[-3:]
+
+    def window():
+        t0 = time.perf_counter()
+        run_updates(args.steps)
+        losses = ctx.fetch_losses(args.steps)      # D2H of every loss, inside the timed region
+        ctx.synchronize()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert losses.shape == (args.steps, 3) and np.all(np.isfinite(losses)), losses[-3:]
+        return dt
+
+    dt, dts = median_windows(window, args.windows)
+    graphs = ctx.get_scalar(L.S_GRAPH_COUNT)
     if args.profile_only:
-        emit(json.dumps({"steps": args.steps, "ms_per_step": 1e3 * dt / args.steps}))
+        emit(json.dumps({"steps": args.steps, "windows": args.windows,
+                         "ms_per_step": 1e3 * dt / args.steps}))
         return
     sps = args.steps / dt
 
@@ -419,13 +462,16 @@ def main():
     out = {
         "metric": f"SAC gradient-steps/sec, {env} batch={args.batch} (obs {S}, act {A}, hidden {H})",
         "value": round(sps, 2), "unit": "grad-steps/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(1e3 / sps, 4), "higher_is_better": True,
+        "warmup": args.warmup, "windows": args.windows,
+        "window_ms_min_med_max": [round(1e3 * min(dts), 3), round(1e3 * dt, 3), round(1e3 * max(dts), 3)],
+        "ms_per_step": round(1e3 / sps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": wl["dtype"], "data": "synthetic",
         "config": {"workload": wl["workload"] + (" [networks_model2: 3 hidden layers]"
                                                  if wl["n_hidden"] == 3 else ""),
                    "state_dim": S, "action_dim": A, "hidden": H, "n_hidden": wl["n_hidden"],
                    "global_batch": args.batch, "replay_fill": fill, "parallelism": "single GPU"},
         "updates_per_launch": upl,
+        "graphs_cached": int(graphs),
         "one_update_per_launch_steps_per_s": round(one_sps, 2),
         "api_faithful_steps_per_s": round(sync_sps, 2),
         "mfma_util_step": round(flops * sps / 1e12 / peak, 4),

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 
 namespace sacmi {
 
@@ -43,14 +44,23 @@ __device__ unsigned long long g_stamps[4096][40];
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 
-#define HIP_LAUNCH_CHECK()                                                          \
-  do {                                                                              \
-    hipError_t e_ = hipGetLastError();                                              \
-    if (e_ != hipSuccess) {                                                         \
-      fprintf(stderr, "sacmi: launch failed %s (%s:%d)\n", hipGetErrorString(e_),   \
-              __FILE__, __LINE__);                                                  \
-    }                                                                               \
-  } while (0)
+// per-(kernel, device) high-water mark of the dynamic-LDS attribute
+void ensure_dyn_lds(const void* kernel, size_t bytes) {
+  static std::map<std::pair<const void*, int>, size_t> seen;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  size_t& cur = seen[{kernel, dev}];
+  if (bytes <= cur) return;
+  const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess)
+    throw Error{SACMI_EDEVICE, std::string("dynamic LDS request of ") + std::to_string(bytes) +
+                                   " bytes refused: " + hipGetErrorString(e)};
+  cur = bytes;
+}
+
+#define SACMI_STR2(x) #x
+#define SACMI_STR(x) SACMI_STR2(x)
+#define HIP_LAUNCH_CHECK() launch_check(__FILE__ ":" SACMI_STR(__LINE__))
 
 // ---------------------------------------------------------------------------
 // Buffer-resource access (raw buffer ops): the base lives in a wave-uniform SGPR

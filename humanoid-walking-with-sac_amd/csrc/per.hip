@@ -55,6 +55,7 @@ void launch_per_push(float* prio, int64_t cap, int64_t pos, int64_t n, int empty
   if (fb > 1024) fb = 1024;
   if (fb < 1) fb = 1;
   hipLaunchKernelGGL(k_prio_fill, dim3((unsigned)fb), dim3(256), 0, s, prio, cap, pos, n, mb, empty);
+  launch_check("PER push");
 }
 
 // ---------------------------------------------------------------------------
@@ -433,6 +434,12 @@ __device__ void per_chunk_tree(float* buf, int n, float* chunk_out) {
   }
 }
 
+// The fused kernels take the fill from the device scalars (the last push published it),
+// and their grids cover the capacity: workgroups past the fill return at once.
+__device__ __forceinline__ int64_t per_len(const PerArgs& a) {
+  return __atomic_load_n(&a.sc->len, __ATOMIC_RELAXED);
+}
+
 __global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
   extern __shared__ __attribute__((aligned(16))) float dyn[];   // max(8192 floats, 2k words)
   if ((int)blockIdx.x == nchunk) {    // the uniforms workgroup (k_per_uniforms' body)
@@ -470,8 +477,10 @@ __global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
     return;
   }
   if (blockIdx.x == 0 && threadIdx.x < 4) a.bad[threadIdx.x] = 0;
+  const int64_t len = per_len(a);
   const int64_t c0 = (int64_t)blockIdx.x * kChunk;
-  const int n = (int)((a.len - c0) < kChunk ? (a.len - c0) : kChunk);
+  if (c0 >= len) return;
+  const int n = (int)((len - c0) < kChunk ? (len - c0) : kChunk);
   float* buf = dyn;
   if (n == kChunk) {
     for (int q = threadIdx.x; q < kChunk / 4; q += blockDim.x) {
@@ -496,10 +505,13 @@ __global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
 // workgroup is resident at once (the integer prefix is exact, so the grouping does not
 // change a bit of q)
 constexpr int kF2Threads = 256;
-__global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a, int nchunk, int nb) {
+__global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a) {
 #pragma clang fp contract(off)
   __shared__ float s_total;
   __shared__ int64_t wsum[kF2Threads / 64];
+  const int64_t len = per_len(a);
+  if ((int64_t)blockIdx.x * kScanBlock >= len) return;
+  const int nchunk = (int)((len + kChunk - 1) / kChunk);
   if (threadIdx.x < 64) {
     // the chunk sums added in chunk order (numpy): wave 0 loads 64 at a time in one
     // coalesced burst, the running sum takes them one by one with v_readlane (a scalar
@@ -517,7 +529,7 @@ __global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a, int nchunk, in
   const int64_t i0 = (int64_t)blockIdx.x * kScanBlock + 4 * threadIdx.x;
   float pin[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) pin[e] = i0 + e < a.len ? a.probs[i0 + e] : 0.f;
+  for (int e = 0; e < 4; ++e) pin[e] = i0 + e < len ? a.probs[i0 + e] : 0.f;
   __syncthreads();
   int64_t v[4];
   int64_t run = 0;
@@ -525,7 +537,7 @@ __global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a, int nchunk, in
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     v[e] = 0;
-    if (i0 + e < a.len) {
+    if (i0 + e < len) {
       const float p = pin[e] / s_total;
       a.probs[i0 + e] = p;
       badp = badp || (p != 0.f && !(p >= 1.862645149230957e-09f));   // 2^-29
@@ -547,7 +559,7 @@ __global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a, int nchunk, in
   for (int k = 0; k < w; ++k) base += wsum[k];
 #pragma unroll
   for (int e = 0; e < 4; ++e)
-    if (i0 + e < a.len) a.q[i0 + e] = base + v[e];
+    if (i0 + e < len) a.q[i0 + e] = base + v[e];
   if (threadIdx.x == kF2Threads - 1) a.block_sums[blockIdx.x] = base + v[3];
 }
 
@@ -556,22 +568,28 @@ __global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a, int nchunk, in
 // would need a device-scope release per workgroup (an L2 writeback each, ~1000 of them).
 __global__ void k_per_f2b(PerArgs a) {
   if (!*a.bad) return;
+  const int64_t len = per_len(a);
   double sum = 0.0;
-  for (int64_t j = 0; j < a.len; ++j) { sum = sum + (double)a.probs[j]; a.cdf[j] = sum; }
-  const double last = a.cdf[a.len - 1];
-  for (int64_t j = 0; j < a.len; ++j) a.cdf[j] = a.cdf[j] / last;
+  for (int64_t j = 0; j < len; ++j) { sum = sum + (double)a.probs[j]; a.cdf[j] = sum; }
+  const double last = a.cdf[len - 1];
+  for (int64_t j = 0; j < len; ++j) a.cdf[j] = a.cdf[j] / last;
 }
 
 #ifndef SACMI_PER_F4
 #define SACMI_PER_F4 1          // w /= max(w) in its own kernel (0: F3 last workgroup, fence + counter: 5 us slower)
 #endif
-__global__ __launch_bounds__(256) void k_per_f3(PerArgs a, int nb, int64_t stride, int ntop) {
+__global__ __launch_bounds__(256) void k_per_f3(PerArgs a) {
 #pragma clang fp contract(off)
   extern __shared__ int64_t off[];       // [nb] exclusive prefix of the block totals
   __shared__ double top[kTopMax];
   __shared__ int64_t wtot[4];
   __shared__ int s_last;
   const bool bad = __atomic_load_n(a.bad, __ATOMIC_RELAXED) != 0;
+  const int64_t len = per_len(a);
+  const int nb = (int)((len + kScanBlock - 1) / kScanBlock);
+  int64_t stride = 1024;
+  while ((len + stride - 1) / stride > kTopMax) stride *= 2;
+  const int ntop = (int)((len + stride - 1) / stride);
   // exclusive scan of block_sums[0..nb) in chunks of 256 (k_per_scan_blocks' sums)
   int64_t carry = 0;
   for (int b0 = 0; b0 < nb; b0 += 256) {
@@ -591,7 +609,6 @@ __global__ __launch_bounds__(256) void k_per_f3(PerArgs a, int nb, int64_t strid
     carry += wtot[0] + wtot[1] + wtot[2] + wtot[3];
     __syncthreads();
   }
-  const int64_t len = a.len;
   const double last = (double)(a.q[len - 1] + off[nb - 1]);
   auto cdf_at = [&](int64_t e) -> double {
     return bad ? a.cdf[e] : (double)(a.q[e] + off[e / kScanBlock]) / last;
@@ -650,34 +667,23 @@ __global__ void k_per_f4(PerArgs a) {
 }
 
 void launch_per_sample(const PerArgs& a, hipStream_t s) {
+  static_assert(kPerFusedMaxRows == (int64_t)kFusedBlocksMax * kScanBlock, "fused PER bound");
   const int64_t len = a.len;
-  const int nb0 = (int)((len + kScanBlock - 1) / kScanBlock);
-  if (nb0 <= kFusedBlocksMax) {
-    const int nchunk = (int)((len + kChunk - 1) / kChunk);
+  if (a.cap <= kPerFusedMaxRows) {
+    // geometry from the capacity; the kernels read the fill on the device
+    const int nb0 = (int)((a.cap + kScanBlock - 1) / kScanBlock);
+    const int nchunk = (int)((a.cap + kChunk - 1) / kChunk);
     size_t lds1 = (size_t)kChunk * 4;
     if ((size_t)a.k * 8 > lds1) lds1 = (size_t)a.k * 8;
-    static size_t attr1 = 0, attr3 = 0;
-    if (lds1 > attr1) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_per_f1),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
-      attr1 = lds1;
-    }
+    ensure_dyn_lds(reinterpret_cast<const void*>(&k_per_f1), lds1);
     hipLaunchKernelGGL(k_per_f1, dim3(nchunk + 1), dim3(256), lds1, s, a, nchunk);
-    hipLaunchKernelGGL(k_per_f2, dim3(nb0), dim3(kF2Threads), 0, s, a, nchunk, nb0);
+    hipLaunchKernelGGL(k_per_f2, dim3(nb0), dim3(kF2Threads), 0, s, a);
     hipLaunchKernelGGL(k_per_f2b, dim3(1), dim3(64), 0, s, a);
-    int64_t stride = 1024;
-    while ((len + stride - 1) / stride > kTopMax) stride *= 2;
-    const int ntop = (int)((len + stride - 1) / stride);
     const size_t lds3 = (size_t)nb0 * 8;
-    if (lds3 > attr3) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_per_f3),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds3);
-      attr3 = lds3;
-    }
-    hipLaunchKernelGGL(k_per_f3, dim3((a.k + 255) / 256), dim3(256), lds3, s, a, nb0, stride, ntop);
+    ensure_dyn_lds(reinterpret_cast<const void*>(&k_per_f3), lds3);
+    hipLaunchKernelGGL(k_per_f3, dim3((a.k + 255) / 256), dim3(256), lds3, s, a);
     if (SACMI_PER_F4) hipLaunchKernelGGL(k_per_f4, dim3((a.k + 255) / 256), dim3(256), 0, s, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) fprintf(stderr, "sacmi: PER launch failed: %s\n", hipGetErrorString(e));
+    launch_check("PER sample (fused)");
     return;
   }
   // very large rings: the unfused sequence
@@ -703,8 +709,7 @@ void launch_per_sample(const PerArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_per_search, dim3(sg), dim3(256), 0, s, a.cdf, a.probs, len, stride, ntop,
                      a.u_scratch, a.k, a.idx32, a.idx_out, a.w_out, wmax);
   hipLaunchKernelGGL(k_per_wnorm, dim3(sg), dim3(256), 0, s, a.w_out, a.k, wmax);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) fprintf(stderr, "sacmi: PER launch failed: %s\n", hipGetErrorString(e));
+  launch_check("PER sample");
 }
 
 // update_priorities (replay_buffer.py:84-87): sequential semantics, last duplicate wins
@@ -733,6 +738,7 @@ void launch_per_update(float* prio, const int64_t* idx, const float* val, int64_
   hipLaunchKernelGGL(k_owner_claim, dim3((unsigned)blocks), dim3(256), 0, s, idx, n, owner);
   hipLaunchKernelGGL(k_owner_write, dim3((unsigned)blocks), dim3(256), 0, s, idx, val, n, owner, prio);
   hipLaunchKernelGGL(k_owner_reset, dim3((unsigned)blocks), dim3(256), 0, s, idx, n, owner);
+  launch_check("PER update_priorities");
 }
 
 }  // namespace sacmi

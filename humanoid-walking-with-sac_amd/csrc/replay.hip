@@ -33,15 +33,9 @@ __global__ __launch_bounds__(1024) void k_mt_sample(MtSampleArgs a, int tbl_log2
 void launch_mt_sample(const MtSampleArgs& a, hipStream_t s) {
   const int tl = mt_sample_tbl_log2(a.k);
   const size_t lds = mt_sample_lds_words(tl, a.setsize) * 4;
-  static size_t attr_set = 0;
-  if (lds > attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mt_sample),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = lds;
-  }
+  ensure_dyn_lds(reinterpret_cast<const void*>(&k_mt_sample), lds);
   hipLaunchKernelGGL(k_mt_sample, dim3(1), dim3(1024), lds, s, a, tl);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) fprintf(stderr, "sacmi: k_mt_sample launch failed: %s\n", hipGetErrorString(e));
+  launch_check("k_mt_sample");
 }
 
 // one wave per ring row (grid-stride), lanes over the row's columns; coalesced both ways
@@ -75,8 +69,7 @@ void launch_push_rows(const PushArgs& a, hipStream_t s) {
   const int64_t blocks = (a.n + 3) / 4;
   const int grid = (int)(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024);
   hipLaunchKernelGGL(k_push_rows, dim3(grid), dim3(256), 0, s, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) fprintf(stderr, "sacmi: k_push_rows launch failed: %s\n", hipGetErrorString(e));
+  launch_check("k_push_rows");
 }
 
 }  // namespace sacmi

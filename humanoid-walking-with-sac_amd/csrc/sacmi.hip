@@ -22,11 +22,6 @@ namespace sacmi {
 
 static thread_local std::string g_last_error;
 
-struct Error {
-  int code;
-  std::string msg;
-};
-
 #define CHECK_HIP(expr)                                                              \
   do {                                                                               \
     hipError_t e_ = (expr);                                                          \
@@ -143,6 +138,7 @@ struct sacmi_ctx {
   float* loss_host = nullptr;               // [4] losses of the last fused update (mapped)
   float* loss_host_dev = nullptr;
   sacmi::DevScalars* sc_host = nullptr;
+  float* ring_host = nullptr;               // [ring_slots][3] loss readback staging
   // PER scratch (replay_kind == PER)
   sacmi::DevBuf<float> per_probs, per_chunk, per_w, per_val;
   sacmi::DevBuf<int64_t> per_q, per_blk, per_idx;
@@ -351,6 +347,8 @@ static void alloc_pinned(sacmi_ctx* c) {
   CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->loss_host_dev), c->loss_host, 0));
   CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->sc_host), sizeof(DevScalars),
                           hipHostMallocDefault));
+  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ring_host), (size_t)c->ring_slots * 12,
+                          hipHostMallocDefault));
 }
 
 static void free_pinned(sacmi_ctx* c) {
@@ -362,6 +360,8 @@ static void free_pinned(sacmi_ctx* c) {
   }
   if (c->act_host) (void)hipHostFree(c->act_host);
   if (c->sc_host) (void)hipHostFree(c->sc_host);
+  if (c->ring_host) (void)hipHostFree(c->ring_host);
+  c->ring_host = nullptr;
   c->act_host = nullptr;
   c->act_host_dev = nullptr;
   if (c->loss_host) (void)hipHostFree(c->loss_host);
@@ -515,7 +515,7 @@ static bool mark(sacmi_ctx* c, const char* name, double flops = 0, double bytes 
 
 static PerArgs per_args(sacmi_ctx* c, int k, int gen_u) {
   PerArgs a{};
-  a.prio = c->prio.p; a.len = c->len; a.alpha = (float)c->cfg.per_alpha;
+  a.prio = c->prio.p; a.len = c->len; a.cap = c->capacity; a.alpha = (float)c->cfg.per_alpha;
   a.probs = c->per_probs.p; a.chunk_sums = c->per_chunk.p; a.q = c->per_q.p;
   a.block_sums = c->per_blk.p; a.bad = c->per_bad.p; a.cdf = c->per_cdf.p;
   a.mt = c->mt.p + 625; a.gen_u = gen_u; a.u = c->per_uin.p; a.u_scratch = c->per_u.p;
@@ -884,6 +884,14 @@ struct PhaseRide {
   bool have_batch = false, ride_next = false;
 };
 
+// The fill a captured update depends on: none for uniform replay and for the fused PER
+// sampler (both read it from the device scalars); the unfused PER sequence of very large
+// rings is sized by the host's fill.
+static int64_t per_graph_len(const sacmi_ctx* c) {
+  if (c->cfg.replay_kind != SACMI_REPLAY_PER || c->capacity <= kPerFusedMaxRows) return 0;
+  return c->len;
+}
+
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
                        float grad_scale, bool use_ring, int reps = 1, PhaseRide pr = {}) {
   // consecutive fused updates hand the next update's sampling + gather to ride-along
@@ -917,7 +925,7 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
                phase_mask | (grad_scale != 1.f ? 8 : 0) | (c->keep_grads ? 16 : 0) |
                    (pr.parity ? 32 : 0) | (pr.have_batch ? 64 : 0) | (pr.ride_next ? 128 : 0),
                use_ring ? c->ring_slots : 0,
-               c->cfg.replay_kind == SACMI_REPLAY_PER ? c->len : 0, reps};
+               per_graph_len(c), reps};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g;
@@ -941,6 +949,13 @@ static void check_batch(sacmi_ctx* c, int B) {
   REQUIRE(B > 0 && B <= c->Bm, SACMI_EVALUE,
           "batch_size must be in [1, max_batch=" + std::to_string(c->Bm) + "]");
   REQUIRE(B <= c->len, SACMI_EVALUE, "Sample larger than population or is negative");
+}
+
+// batch of an update that samples on the device (random.sample: batch <= 4096; the PER
+// sampler's uniforms workgroup holds 2 words per draw in LDS)
+static void check_device_batch(sacmi_ctx* c, int B) {
+  check_batch(c, B);
+  REQUIRE(B <= 4096, SACMI_EVALUE, "device sampling supports batch <= 4096");
 }
 
 static void stage_inputs(sacmi_ctx* c, int B, const int64_t* idx, const float* eps1,
@@ -1233,6 +1248,10 @@ static void scalar_io(sacmi_ctx* c, int which, const double* in, double* out) {
     case SACMI_S_ADAM_M_LOG_ALPHA: arena_scalar(c, c->M.p, c->la_idx, in, out); return;
     case SACMI_S_ADAM_V_LOG_ALPHA: arena_scalar(c, c->V.p, c->la_idx, in, out); return;
     case SACMI_S_GRAD_LOG_ALPHA: arena_scalar(c, c->G.p, c->la_idx, in, out); return;
+    case SACMI_S_GRAPH_COUNT:
+      REQUIRE(!in, SACMI_EVALUE, "the graph count is read-only");
+      *out = (double)(c->graphs.size() + c->dp_graphs.size());
+      return;
     case SACMI_S_KEEP_GRADS:
       if (in) {
         if (c->keep_grads != (*in != 0)) destroy_graphs(c);
@@ -1425,16 +1444,14 @@ int sacmi_step(sacmi_ctx* c, int32_t batch, const int64_t* idx, const float* eps
 
 int sacmi_step_async(sacmi_ctx* c, int32_t batch) {
   return guard([&] {
-    check_batch(c, batch);
-    REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
+    check_device_batch(c, batch);
     run_update(c, batch, 1, 1, 7, 1.f, true);
   });
 }
 
 int sacmi_step_many_async(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   return guard([&] {
-    check_batch(c, batch);
-    REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
+    check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
     run_update(c, batch, 1, 1, 7, 1.f, true, n_updates);
   });
@@ -1442,17 +1459,22 @@ int sacmi_step_many_async(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
 
 int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_out) {
   return guard([&] {
+    REQUIRE(max_steps >= 0 && (max_steps == 0 || out), SACMI_EVALUE, "bad output buffer");
     DevScalars h = download_scalars(c);
     const int64_t avail = std::min<int64_t>(h.loss_ring_pos, c->ring_slots);
     const int64_t n = std::min<int64_t>(avail, max_steps);
-    std::vector<float> all((size_t)c->ring_slots * 3);
-    CHECK_HIP(hipMemcpy(all.data(), c->ring.p, all.size() * 4, hipMemcpyDeviceToHost));
-    // most recent n entries, oldest first
-    for (int64_t i = 0; i < n; ++i) {
-      const int64_t logical = h.loss_ring_pos - n + i;
-      const int64_t p = logical % c->ring_slots;
-      std::memcpy(out + i * 3, all.data() + p * 3, 12);
-    }
+    // most recent n entries, oldest first: at most two contiguous runs of the ring,
+    // copied into pinned staging with one stream sync
+    const int64_t first = (h.loss_ring_pos - n) % c->ring_slots;
+    const int64_t run1 = std::min<int64_t>(n, c->ring_slots - first);
+    if (run1 > 0)
+      CHECK_HIP(hipMemcpyAsync(c->ring_host, c->ring.p + first * 3, (size_t)run1 * 12,
+                               hipMemcpyDeviceToHost, c->stream));
+    if (n > run1)
+      CHECK_HIP(hipMemcpyAsync(c->ring_host + run1 * 3, c->ring.p, (size_t)(n - run1) * 12,
+                               hipMemcpyDeviceToHost, c->stream));
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    if (n > 0) std::memcpy(out, c->ring_host, (size_t)n * 12);
     *n_out = (int32_t)n;
   });
 }
@@ -1460,7 +1482,7 @@ int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_o
 int sacmi_step_phase(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scale) {
   return guard([&] {
     REQUIRE(phase >= 0 && phase <= 3, SACMI_EVALUE, "phase must be 0, 1, 2 or 3");
-    if (phase == 0 || phase == 3) check_batch(c, batch);
+    if (phase == 0 || phase == 3) check_device_batch(c, batch);
     run_update(c, batch, 1, 1, phase == 3 ? 5 : 1 << phase, grad_scale, false);
   });
 }
@@ -1470,7 +1492,7 @@ int sacmi_step_phase_ex(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_s
   return guard([&] {
     REQUIRE(phase >= 0 && phase <= 3, SACMI_EVALUE, "phase must be 0, 1, 2 or 3");
     REQUIRE(parity == 0 || parity == 1, SACMI_EVALUE, "parity must be 0 or 1");
-    if (phase == 0 || phase == 3) check_batch(c, batch);
+    if (phase == 0 || phase == 3) check_device_batch(c, batch);
     PhaseRide pr;
     pr.parity = parity;
     pr.have_batch = have_batch && (phase == 0 || phase == 3);
@@ -1510,7 +1532,7 @@ int sacmi_allreduce_init(sacmi_ctx* c, const void* id, int32_t nbytes, int32_t r
 int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   return guard([&] {
     REQUIRE(c->comm, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
-    check_batch(c, batch);
+    check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     CHECK_HIP(hipStreamIsCapturing(c->stream, &cap));
@@ -1519,8 +1541,7 @@ int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
       CHECK_HIP(hipGetLastError());
       return;
     }
-    const auto key = std::make_tuple((int)batch, (int)n_updates,
-                                     c->cfg.replay_kind == SACMI_REPLAY_PER ? c->len : (int64_t)0);
+    const auto key = std::make_tuple((int)batch, (int)n_updates, per_graph_len(c));
     auto it = c->dp_graphs.find(key);
     if (it == c->dp_graphs.end()) {
       hipGraph_t g;
@@ -1556,7 +1577,16 @@ int sacmi_attach_grad_arena(sacmi_ctx* c, void* ptr, int64_t numel) {
     CHECK_HIP(hipStreamSynchronize(c->stream));
     CHECK_HIP(hipMemset(ptr, 0, (size_t)numel * 4));
     CHECK_HIP(hipDeviceSynchronize());
-    c->G.release();
+    if (c->G_external) {
+      // the previous arena belongs to the caller: drop its registry entry, never free it
+      auto& reg = alloc_registry();
+      for (size_t i = 0; i < reg.size(); ++i)
+        if (reg[i].base == (uintptr_t)c->G.p) { reg.erase(reg.begin() + i); break; }
+      c->G.p = nullptr;
+      c->G.n = 0;
+    } else {
+      c->G.release();
+    }
     c->G.p = (float*)ptr;
     c->G.n = (size_t)numel;
     c->G_external = true;
@@ -1576,7 +1606,7 @@ int sacmi_grad_buffer(sacmi_ctx* c, int which, void** ptr, int64_t* numel) {
 int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_out,
                        float* ms_out, double* flops_out, int32_t max_sites, int32_t* n_sites) {
   return guard([&] {
-    check_batch(c, batch);
+    check_device_batch(c, batch);
     REQUIRE(iters > 0, SACMI_EVALUE, "iters must be > 0");
     std::vector<double> acc;
     std::vector<std::string> names;
@@ -1618,7 +1648,7 @@ int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_o
                         float* us_out, double* flops_out, double* bytes_out, int32_t max_sites,
                         int32_t* n_sites) {
   return guard([&] {
-    check_batch(c, batch);
+    check_device_batch(c, batch);
     REQUIRE(reps > 0 && reps <= 1000, SACMI_EVALUE, "reps must be in [1, 1000]");
     // enumerate the sites of the fused single-GPU update without launching anything
     c->prof_names.clear(); c->prof_flops.clear(); c->prof_bytes.clear();

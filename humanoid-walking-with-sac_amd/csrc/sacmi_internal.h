@@ -27,6 +27,25 @@ namespace sacmi {
 
 constexpr int kWave = 64;
 
+// Errors thrown inside the library and mapped to a status code by the C ABI's guard().
+struct Error {
+  int code;
+  std::string msg;
+};
+
+// A failed kernel launch (bad configuration, LDS over the limit, ...) is an error of the
+// call that enqueued it: the launchers throw instead of printing and carrying on with
+// stale outputs.
+inline void launch_check(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    throw Error{SACMI_EDEVICE, std::string("kernel launch failed (") + what + "): " + hipGetErrorString(e)};
+}
+
+// hipFuncAttributeMaxDynamicSharedMemorySize is a per-device attribute: raise it once per
+// (kernel, device) to the largest request seen.
+void ensure_dyn_lds(const void* kernel, size_t bytes);
+
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
@@ -294,8 +313,13 @@ void launch_set_column(float* p, int rows, int ld, int col, float v, hipStream_t
 void launch_increment_steps(DevScalars* sc, hipStream_t s);
 
 // PER (per.hip)
+// Rings up to this many rows take the fused PER path, whose kernels read the fill from
+// DevScalars::len (published by the last push): one captured graph serves every fill
+// level.  Larger rings take the unfused sequence, sized by the host's len.
+constexpr int64_t kPerFusedMaxRows = (int64_t)16384 * 1024;
 struct PerArgs {
   const float* prio; int64_t len;
+  int64_t cap;            // ring capacity (fused path: launch geometry)
   float alpha;
   float* probs;           // [len] scratch: prio^alpha, then normalised
   float* chunk_sums;      // [ceil(len/8192)]

@@ -36,7 +36,7 @@ POLICY, Q1, Q2, Q1_TARGET, Q2_TARGET = range(5)
 SLOT_PARAM, SLOT_GRAD, SLOT_ADAM_M, SLOT_ADAM_V = range(4)
 (S_LOG_ALPHA, S_ALPHA, S_ALPHA_IS_TENSOR, S_STEP_POLICY, S_STEP_Q1, S_STEP_Q2, S_STEP_ALPHA,
  S_ADAM_M_LOG_ALPHA, S_ADAM_V_LOG_ALPHA, S_GRAD_LOG_ALPHA, S_PER_FRAME,
- S_NOISE_COUNTER, S_KEEP_GRADS) = range(13)
+ S_NOISE_COUNTER, S_KEEP_GRADS, S_GRAPH_COUNT) = range(14)
 
 
 class SacmiConfig(ctypes.Structure):

@@ -109,7 +109,9 @@ enum sacmi_scalar {
   SACMI_S_KEEP_GRADS = 12,     /* host flag: 1 = single-GPU updates also export the   */
                                /* gradients to the GRAD slot (param.grad after        */
                                /* backward); 0 (default) skips those stores           */
-  SACMI_S_COUNT = 13
+  SACMI_S_GRAPH_COUNT = 13,    /* read-only: instantiated update graphs cached by the  */
+                               /* context (one per distinct update configuration)     */
+  SACMI_S_COUNT = 14
 };
 
 /* ---- lifecycle ---------------------------------------------------------------- */

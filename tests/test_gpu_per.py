@@ -136,3 +136,48 @@ def test_per_many_blocks_vs_oracle(n, batch, bad):
     assert np.array_equal(idx, ridx)
     ulp = np.spacing(np.maximum(np.abs(rw), np.float32(1e-30)))
     assert np.all(np.abs(w - rw) <= 4 * ulp)
+
+
+def test_per_filling_buffer_one_graph_and_eager_identical():
+    """A push-then-update loop on a PER context that is still filling (trainer.py:194-205
+    with the prioritized buffer): the fused PER sampler reads the fill on the device, so
+    ONE captured update graph serves every fill level (graph count constant), and the
+    results are bit-identical to the eager (SACMI_NO_GRAPH=1) updates."""
+    import torch  # noqa: F401
+    from oracle.sac_step import NETS, SacConfig, init_params, synthetic_rows
+    from sacmi import Config, Context
+    from sacmi import _lib as L
+    cfg = SacConfig(24, 4, 64)
+    params = init_params(cfg, 91, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 1200, 92, state_scale=0.5)
+    out = []
+    for ng in ("0", "1"):
+        os.environ["SACMI_NO_GRAPH"] = ng
+        try:
+            c = Context(Config(24, 4, 64, max_batch=64, capacity=20000, replay="per", seed=5), 0)
+        finally:
+            os.environ.pop("SACMI_NO_GRAPH", None)
+        for n in NETS:
+            c.set_net(n, params[n])
+        c.push(*[x[:200] for x in rows])
+        c.set_mt(1, np.arange(624, dtype=np.uint32) * 7 + 1, 624)
+        counts, losses = [], []
+        for i in range(50):
+            lo = 200 + 20 * i
+            c.push(*[x[lo:lo + 20] for x in rows])
+            c.step_async(64)
+            counts.append(int(c.get_scalar(L.S_GRAPH_COUNT)))
+        losses = c.fetch_losses(50)
+        out.append((counts, losses, {n: c.get_net(n) for n in NETS}, c.per_priorities(1200),
+                    c.get_mt(1)))
+        c.close()
+    counts, losses, nets, prio, mt = out[0]
+    assert len(c0 := set(counts)) == 1 and c0 == {1}, counts
+    assert set(out[1][0]) == {0}                       # eager context: no graphs
+    assert losses.shape == (50, 3) and np.all(np.isfinite(losses))
+    assert np.array_equal(losses, out[1][1])
+    for n in NETS:
+        for k in nets[n]:
+            assert np.array_equal(nets[n][k], out[1][2][n][k]), (n, k)
+    assert np.array_equal(prio, out[1][3])
+    assert np.array_equal(mt[0], out[1][4][0]) and mt[1] == out[1][4][1]
