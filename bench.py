@@ -115,42 +115,60 @@ def init_agent(ctx, seed):
     ctx.set_net("q2_target", q_sd["q2"])
 
 
-# launch sites whose kernel is the grouped GEMM `sacmi::k_gemm<TM,TN,KSPLIT,G>` (L10 is
-# k_gemm_sample_bwd, a different kernel)
-def _is_k_gemm(site):
-    return site.startswith("gemm_L") and not site.startswith("gemm_L10")
+# kernels that run the MLP GEMM levels (the dominant kernel family of the update); L10
+# (k_gemm_sample_bwd: dL/da + the sampling backward) and the heads kernel are not levels
+LEVEL_KERNELS = {"k_gemm", "k_fwd", "k_fwd16", "k_axk16", "k_dw_part", "k_dw_part16", "k_dw_fin"}
 
 
-def gemm_roofline(ctx, batch, reps=50):
-    """Dominant kernel = k_gemm.  Every launch site is replayed alone `reps` times in
-    one hipGraph and timed with HIP events on the context stream (the stream every
-    update kernel is launched on): achieved = algorithmic FLOPs per launch / mean
-    launch duration, over the k_gemm sites of one update."""
-    sites = ctx.profile_sites(batch, reps)
-    gemm = [(n, us, f, b) for (n, us, f, b) in sites if _is_k_gemm(n)]
-    gus = sum(x[1] for x in gemm)
-    gfl = sum(x[2] for x in gemm)
-    gby = sum(x[3] for x in gemm)
-    launches = len(gemm)
-    avg_us = gus / launches
-    achieved = (gfl / launches) / (avg_us * 1e-6) / 1e12
-    return dict(sites=sites, sites_sum_us=sum(x[1] for x in sites), gemm_us=gus,
-                gemm_flops=gfl, gemm_bytes=gby, launches=launches, avg_launch_us=avg_us,
-                achieved_tflops=achieved)
+def timeline_roofline(ctx, batch, n_updates):
+    """Roofline of the GEMM levels measured on the REAL update: the same n-update graph
+    the timed windows replay, instrumented so that every kernel stamps its first
+    workgroup's entry on the GPU clock (sacmi_profile_timeline), replayed once warm and
+    once measured, with HIP events on the context stream around the measured replay.
+    Kernels run back to back in the graph, so a launch's duration is the distance to the
+    next launch's start (the last: its own end); their sum must equal the event time."""
+    ks, graph_us = ctx.profile_timeline(batch, n_updates)
+    ks = sorted(ks, key=lambda k: k["start_us"])
+    for i, k in enumerate(ks):
+        nxt = ks[i + 1]["start_us"] if i + 1 < len(ks) else k["end_us"]
+        k["dur_us"] = nxt - k["start_us"]
+    lv = [k for k in ks if k["kernel"] in LEVEL_KERNELS]
+    gemm_us = sum(k["dur_us"] for k in lv)
+    gemm_flops = sum(k["flops"] for k in lv)
+    gemm_bytes = sum(k["bytes"] for k in lv)
+    levels = sum(1 for k in lv if k["flops"] > 0)          # a split-K pair is one level
+    kernel_launches = {}
+    for k in lv:
+        kernel_launches[k["kernel"]] = kernel_launches.get(k["kernel"], 0) + 1
+    sites = {}
+    for k in ks:
+        e = sites.setdefault(k["site"], [0.0, 0])
+        e[0] += k["dur_us"]
+        e[1] += 1 if k["flops"] > 0 or k["kernel"] not in LEVEL_KERNELS else 0
+    return dict(graph_us=graph_us, sum_us=sum(k["dur_us"] for k in ks), n_updates=n_updates,
+                gemm_us=gemm_us, gemm_flops=gemm_flops, gemm_bytes=gemm_bytes, levels=levels,
+                kernel_launches=kernel_launches,
+                achieved_tflops=gemm_flops / (gemm_us * 1e-6) / 1e12,
+                sites_us={n: round(t / max(c, 1), 2) for n, (t, c) in sites.items()})
 
 
-def pmc_traffic(config, networks="model1"):
-    """Measured bytes past L2 per k_gemm launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, two
-    separate --pmc passes over this bench command: tools/gpu_pmc.sh + tools/pmc_summary.py),
-    read from the committed summary; None when absent."""
-    suffix = "" if networks == "model1" else f"_{networks}"     # counters are per workload
-    path = os.path.join(ROOT, "profiles", (f"r01_pmc_traffic{suffix}.json" if config == 2 else
-                                           f"r01_pmc_traffic_c{config}{suffix}.json"))
+def pmc_counters(config, networks="model1"):
+    """Per-GEMM-level PMC figures of this workload (tools/gpu_pmc.sh + tools/pmc_summary.py:
+    bytes past L2 from separate FETCH_SIZE / WRITE_SIZE passes, MFMA busy fraction from
+    SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE), read from the committed summary ONLY while
+    the kernel sources are the ones it was measured on (csrc digest); else None."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_summary import csrc_digest
+    suffix = "" if networks == "model1" else f"_{networks}"
+    path = os.path.join(ROOT, "profiles", f"pmc_c{config}{suffix}.json")
     try:
-        per = json.load(open(path))["per_launch"]
-        return per["traffic_bytes"], os.path.relpath(path, ROOT)
-    except (OSError, KeyError, TypeError, ValueError):
-        return None, None
+        z = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if z.get("csrc_digest") != csrc_digest() or not z.get("per_level"):
+        return None
+    z["source"] = os.path.relpath(path, ROOT)
+    return z
 
 
 def cpu_threads() -> int:
@@ -270,6 +288,37 @@ def trainer_loop(wl, steps=300, warmup=30, fill=20_000):
             "us_update_parameters": round(1e6 * tt[2] / steps, 1),
             "note": "trainer.py:182-205 loop minus env.step: select_action + push + "
                     f"update_parameters({B}) per env step, drop-in SAC, {fill}-row replay"}
+
+
+def roofline_object(ctx, args, wl, peak):
+    """The line's `roofline` object: the GEMM levels of the real multi-update graph."""
+    upl = max(1, min(args.updates_per_launch, 256))
+    info = timeline_roofline(ctx, args.batch, upl)
+    pmc = pmc_counters(args.config, args.networks)
+    lvl = pmc["per_level"] if pmc else {}
+    per_level_flops = info["gemm_flops"] / max(info["levels"], 1)
+    avg_level_us = info["gemm_us"] / max(info["levels"], 1)
+    return {"bound": "mfma", "achieved": round(info["achieved_tflops"], 3), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(info["achieved_tflops"] / peak, 4),
+            "traffic": round(lvl["traffic_bytes"]) if lvl else None,
+            "traffic_unit": "bytes past L2 per GEMM level (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "mfma_busy": round(lvl["mfma_busy"], 4) if lvl and lvl.get("mfma_busy") else None,
+            "pmc_source": pmc["source"] if pmc else None,
+            "algorithmic_bytes_per_launch": round(info["gemm_bytes"] / max(info["levels"], 1)),
+            "kernel": "GEMM levels of the update: " + ", ".join(
+                f"sacmi::{k} x{n}" for k, n in sorted(info["kernel_launches"].items())) +
+                      f" per {upl} updates ({wl['dtype']} MFMA)",
+            "method": "launch timeline of the timed multi-update graph (per-kernel GPU-clock "
+                      "stamps, sacmi_profile_timeline); HIP events on the context stream "
+                      "around the same replay",
+            "levels_per_step": round(info["levels"] / upl, 2),
+            "avg_launch_us": round(avg_level_us, 3),
+            "flops_per_launch": round(per_level_flops),
+            "gemm_us_per_step": round(info["gemm_us"] / upl, 2),
+            "gemm_flops_per_step": round(info["gemm_flops"] / upl),
+            "step_us_timeline": round(info["sum_us"] / upl, 2),
+            "step_us_hip_events": round(info["graph_us"] / upl, 2),
+            "sites_us": info["sites_us"]}
 
 
 def parse_args(argv=None):
@@ -431,25 +480,7 @@ def main():
     roof = None
     peak = PEAK_BF16_MFMA_TFLOPS if wl["dtype"] == "bf16" else PEAK_FP32_MFMA_TFLOPS
     if not args.no_roofline:
-        info = gemm_roofline(ctx, args.batch)
-        traffic, traffic_src = pmc_traffic(args.config, args.networks)
-        roof = {"bound": "mfma", "achieved": round(info["achieved_tflops"], 3),
-                "peak": peak, "unit": "TFLOP/s",
-                "frac": round(info["achieved_tflops"] / peak, 4),
-                "traffic": None if traffic is None else round(traffic),
-                "traffic_unit": "bytes past L2 per k_gemm launch (PMC)",
-                "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": round(info["gemm_bytes"] / info["launches"]),
-                "kernel": f"sacmi::k_gemm (grouped {wl['dtype']} MFMA GEMM, all tile configs)"
-                          + (" + sacmi::k_fwd16 (bf16-LDS large-M forward levels) + "
-                             "sacmi::k_axk16 (dh levels) + "
-                             "sacmi::k_dw_part16/k_dw_fin (split-K weight-gradient levels)"
-                             if wl["dtype"] == "bf16" and args.batch >= 2048 else ""),
-                "launches_per_step": info["launches"],
-                "avg_launch_us": round(info["avg_launch_us"], 3),
-                "gemm_flops_per_step": info["gemm_flops"],
-                "sites_sum_us": round(info["sites_sum_us"], 2),
-                "sites_us": {x[0]: round(x[1], 2) for x in info["sites"]}}
+        roof = roofline_object(ctx, args, wl, peak)
     flops = necessary_flops(S, A, H, args.batch, wl["n_hidden"])
     loop = None if args.no_trainer_loop else trainer_loop(wl)
     cpu = None

@@ -699,6 +699,7 @@ constexpr int gemm_min_waves() { return 4; }   // 16 waves per CU: one 1024- or 
 // bf16 MFMA operands (GemmBatch::bf16), everything around them fp32
 template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false>
 __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_GEMM);
   constexpr int TMW = TM * MG;
   __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
   __shared__ float rsum[MG * KSPLIT * TM];
@@ -1014,6 +1015,7 @@ struct FwdEpi {
 
 template <bool BF16, int kFBN = 128>
 __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_FWD);
   constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
   __shared__ __attribute__((aligned(16))) float sA[2][kFBM][kFBK + kFPad];
   __shared__ __attribute__((aligned(16))) float sB[2][kFBN][kFBK + kFPad];
@@ -1132,6 +1134,7 @@ __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
 
 template <int kFBN, bool BH = false>
 __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_FWD16);
   constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
   constexpr int LDR = kHBK + kHPad;      // bf16 per LDS row: 144 B at 64 deep
   constexpr int TPR = kHBK / 4;          // staging threads per row (4 k each)
@@ -1290,6 +1293,7 @@ __device__ __forceinline__ int dw_work_index(int b, int tiles, int ns) {
 
 template <bool BF16>
 __global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int64_t ws_stride) {
+  const TlMark tl_mark(batch.tl, TL_DW_PART);
   __shared__ __attribute__((aligned(16))) float sA[2][kDBK][kDBM + kDPad];
   __shared__ __attribute__((aligned(16))) float sB[2][kDBK][kDBN + kDPad];
   const int tiles_tot = batch.total_tiles;
@@ -1422,6 +1426,7 @@ __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
 }
 
 __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
+  const TlMark tl_mark(batch.tl, TL_DW_PART16);
   constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
   __shared__ __attribute__((aligned(16))) __bf16 sA[2][kD16K][LDR];
   __shared__ __attribute__((aligned(16))) __bf16 sB[2][kD16K][LDR];
@@ -1579,6 +1584,7 @@ constexpr int kXBM = 64, kXBN = 128, kXBK = 64;
 
 template <bool AX, bool BH = false>
 __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_AXK16);
   constexpr int LDA_ = kXBK + 8;        // [row][k] bf16, 144-B rows
   constexpr int LDB_ = kXBN + 8;        // [k][n] bf16, 272-B rows
   __shared__ __attribute__((aligned(16))) __bf16 sA[2][kXBM][LDA_];
@@ -1765,6 +1771,7 @@ static int axk16_ok(GemmBatch& b) {
 }
 
 __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t ws_stride) {
+  const TlMark tl_mark(batch.tl, TL_DW_FIN);
   __shared__ AdamScalars s_k[3];
   const AdamFuse& af = batch.adam;
   const bool adam = batch.has_adam != 0;
@@ -1923,6 +1930,7 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
       const int fin_grid = (int)std::min<int64_t>((stride + 255) / 256, 4096);
+      if (b.tl) b.tl += kTlWords;          // the second kernel of the level
       hipLaunchKernelGGL(k_dw_fin, dim3(fin_grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
       return;
@@ -2055,6 +2063,7 @@ __device__ __forceinline__ float one_minus_tanh2(float x) {
 // (networks_model1.py:65-99, torch distributions/normal.py:83-103)
 template <int TN, int KSPLIT>
 __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) {
+  const TlMark tl_mark(a.tl, TL_HEADS);
   constexpr int TM = 16;
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   __shared__ float lp[TM][33];
@@ -2179,6 +2188,7 @@ void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {
 // NST: k-steps (of 4) of the dhp2 tail's K = 2A, a compile-time bound
 template <int TM, int TN, int KSPLIT, int NST>
 __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, SampleBwdArgs a) {
+  const TlMark tl_mark(a.tl, TL_SAMPLE_BWD);
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   __shared__ float s_dh[TM][64 + 1];     // this workgroup's dhead rows, zero beyond 2A
   for (int i = threadIdx.x; i < TM * 65; i += 64 * KSPLIT) (&s_dh[0][0])[i] = 0.f;
@@ -2300,6 +2310,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 // finalisation + the scalar log_alpha step and alpha = exp(log_alpha)
 // (sac_imp.py:128-135) + the loss ring slot of this update.
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+  const TlMark tl_mark(a.tl, TL_ADAM);
   __shared__ AdamScalars s_k[kMaxAdamSegs];
   __shared__ int64_t s_prefix[kMaxAdamSegs + 1];
   if (threadIdx.x < a.nseg) s_k[threadIdx.x] = adam_scalars(a, a.seg[threadIdx.x].step_idx);
@@ -2388,6 +2399,7 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
 // replay gather: deque positions -> ring slots -> critic input [s|1|a] and the
 // stacked policy input [s2|1|.. ; s|1|..]  (replay_buffer.py:15-19 + sac_imp.py:81-85)
 __global__ __launch_bounds__(128) void k_gather(GatherArgs a) {
+  const TlMark tl_mark(a.tl, TL_GATHER);
   gather_row(a, blockIdx.x, threadIdx.x, 128);
 }
 

@@ -441,6 +441,7 @@ __device__ __forceinline__ int64_t per_len(const PerArgs& a) {
 }
 
 __global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
+  const TlMark tl_mark(a.tl, TL_PER_F1);
   extern __shared__ __attribute__((aligned(16))) float dyn[];   // max(8192 floats, 2k words)
   if ((int)blockIdx.x == nchunk) {    // the uniforms workgroup (k_per_uniforms' body)
     __shared__ uint32_t key[kMtN];
@@ -507,6 +508,7 @@ __global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
 constexpr int kF2Threads = 256;
 __global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a) {
 #pragma clang fp contract(off)
+  const TlMark tl_mark(a.tl, TL_PER_F2);
   __shared__ float s_total;
   __shared__ int64_t wsum[kF2Threads / 64];
   const int64_t len = per_len(a);
@@ -567,6 +569,7 @@ __global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a) {
 // was seen); a no-op otherwise.  Its own launch: a last-workgroup hand-off inside F2
 // would need a device-scope release per workgroup (an L2 writeback each, ~1000 of them).
 __global__ void k_per_f2b(PerArgs a) {
+  const TlMark tl_mark(a.tl, TL_PER_F2B);
   if (!*a.bad) return;
   const int64_t len = per_len(a);
   double sum = 0.0;
@@ -580,6 +583,7 @@ __global__ void k_per_f2b(PerArgs a) {
 #endif
 __global__ __launch_bounds__(256) void k_per_f3(PerArgs a) {
 #pragma clang fp contract(off)
+  const TlMark tl_mark(a.tl, TL_PER_F3);
   extern __shared__ int64_t off[];       // [nb] exclusive prefix of the block totals
   __shared__ double top[kTopMax];
   __shared__ int64_t wtot[4];
@@ -660,6 +664,7 @@ __global__ __launch_bounds__(256) void k_per_f3(PerArgs a) {
 }
 
 __global__ void k_per_f4(PerArgs a) {
+  const TlMark tl_mark(a.tl, TL_PER_F4);
   const unsigned int* wmax = reinterpret_cast<const unsigned int*>(a.bad + 1);
   const float mx = __uint_as_float(*wmax);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -676,13 +681,15 @@ void launch_per_sample(const PerArgs& a, hipStream_t s) {
     size_t lds1 = (size_t)kChunk * 4;
     if ((size_t)a.k * 8 > lds1) lds1 = (size_t)a.k * 8;
     ensure_dyn_lds(reinterpret_cast<const void*>(&k_per_f1), lds1);
-    hipLaunchKernelGGL(k_per_f1, dim3(nchunk + 1), dim3(256), lds1, s, a, nchunk);
-    hipLaunchKernelGGL(k_per_f2, dim3(nb0), dim3(kF2Threads), 0, s, a);
-    hipLaunchKernelGGL(k_per_f2b, dim3(1), dim3(64), 0, s, a);
+    // timeline slots: one per kernel, in launch order
+    auto at = [&](int i) { PerArgs x = a; x.tl = a.tl ? a.tl + i * kTlWords : nullptr; return x; };
+    hipLaunchKernelGGL(k_per_f1, dim3(nchunk + 1), dim3(256), lds1, s, at(0), nchunk);
+    hipLaunchKernelGGL(k_per_f2, dim3(nb0), dim3(kF2Threads), 0, s, at(1));
+    hipLaunchKernelGGL(k_per_f2b, dim3(1), dim3(64), 0, s, at(2));
     const size_t lds3 = (size_t)nb0 * 8;
     ensure_dyn_lds(reinterpret_cast<const void*>(&k_per_f3), lds3);
-    hipLaunchKernelGGL(k_per_f3, dim3((a.k + 255) / 256), dim3(256), lds3, s, a);
-    if (SACMI_PER_F4) hipLaunchKernelGGL(k_per_f4, dim3((a.k + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_per_f3, dim3((a.k + 255) / 256), dim3(256), lds3, s, at(3));
+    if (SACMI_PER_F4) hipLaunchKernelGGL(k_per_f4, dim3((a.k + 255) / 256), dim3(256), 0, s, at(4));
     launch_check("PER sample (fused)");
     return;
   }

@@ -26,6 +26,7 @@
 namespace sacmi {
 
 __global__ __launch_bounds__(1024) void k_mt_sample(MtSampleArgs a, int tbl_log2) {
+  const TlMark tl_mark(a.tl, TL_MT_SAMPLE);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   mt_sample_body(a, tbl_log2, smem);
 }

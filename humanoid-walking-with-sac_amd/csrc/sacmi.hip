@@ -160,6 +160,12 @@ struct sacmi_ctx {
   std::vector<std::string> prof_names;
   std::vector<double> prof_flops, prof_bytes;
   std::vector<hipEvent_t> prof_events;
+  // launch timeline (sacmi_profile_timeline): kTlPerSite * kTlWords words per launch site
+  sacmi::tl_word* tl_dev = nullptr;
+  int tl_cap = 0, tl_sites = 0;
+  sacmi::tl_word* tl_cur = nullptr;   // the current site's slots (null: not recording)
+  std::vector<std::string> tl_names;
+  std::vector<double> tl_flops, tl_bytes;
 };
 
 namespace sacmi {
@@ -499,6 +505,14 @@ static double level_bytes(const GemmBatch& b) {
 // only site number prof_site runs (sacmi_profile_sites).
 static bool mark(sacmi_ctx* c, const char* name, double flops = 0, double bytes = 0) {
   const int site = c->site_counter++;
+  c->tl_cur = nullptr;
+  if (c->tl_dev) {
+    if (c->tl_sites >= c->tl_cap) throw Error{SACMI_ESTATE, "timeline buffer full"};
+    c->tl_cur = c->tl_dev + (size_t)c->tl_sites++ * kTlPerSite * kTlWords;
+    c->tl_names.push_back(name);
+    c->tl_flops.push_back(flops);
+    c->tl_bytes.push_back(bytes);
+  }
   if (c->prof || c->prof_collect) {
     c->prof_names.push_back(name);
     c->prof_flops.push_back(flops);
@@ -602,7 +616,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     for (int i = 0; i < lv.b.count; ++i) lv.b.d[i].Bh = shadow(lv.b.d[i].B);
     lv.b.ws = c->dw_ws.p;
     lv.b.ws_floats = (int64_t)c->dw_ws.n;
-    if (mark(c, name.c_str(), level_flops(lv.b), level_bytes(lv.b))) launch_gemm(lv.b, s);
+    if (mark(c, name.c_str(), level_flops(lv.b), level_bytes(lv.b))) {
+      lv.b.tl = c->tl_cur;
+      launch_gemm(lv.b, s);
+    }
   };
 
   if (phase_mask & 1) {
@@ -610,11 +627,23 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     if (have_batch) {
       // indices and rows were produced by the previous update (ride-along)
     } else if (dev_idx && per) {
-      if (mark(c, "per_sample")) launch_per_sample(per_args(c, B, 1), s);
+      if (mark(c, "per_sample")) {
+        PerArgs pa = per_args(c, B, 1);
+        pa.tl = c->tl_cur;
+        launch_per_sample(pa, s);
+      }
     } else if (dev_idx) {
-      if (mark(c, "mt_sample")) launch_mt_sample(mt_args(c, B, bb), s);
+      if (mark(c, "mt_sample")) {
+        MtSampleArgs ma = mt_args(c, B, bb);
+        ma.tl = c->tl_cur;
+        launch_mt_sample(ma, s);
+      }
     }
-    if (!have_batch && mark(c, "gather")) launch_gather(gather_args(c, B, bb, per), s);
+    if (!have_batch && mark(c, "gather")) {
+      GatherArgs ga = gather_args(c, B, bb, per);
+      ga.tl = c->tl_cur;
+      launch_gather(ga, s);
+    }
 
     // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
     Level l1;
@@ -643,7 +672,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
     hs.logp_part = c->lp_part.p; hs.split_row = B;    // sums of log pi(a~|s) for dL/dlog_alpha
-    if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) launch_heads_sample(hs, s);
+    if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) {
+      hs.tl = c->tl_cur;
+      launch_heads_sample(hs, s);
+    }
     // L3/L4 (.. L4b): target critics on [s2|1|a'] (head dot partials: slots 2 / 3)
     {
       Level l3;
@@ -749,7 +781,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.tau = (float)c->cfg.tau; ad.step_offset = 1; ad.sc = c->sc.p;
     ad.loss_part = c->lpart_c.p; ad.n_part = nb; ad.loss_slot0 = 0; ad.n_losses = 2;
     ad.loss_div = (float)B; ad.log_alpha_idx = -1; ad.auto_entropy = 0;
-    if (mark(c, "adam_critic_polyak")) launch_adam(ad, s);
+    if (mark(c, "adam_critic_polyak")) {
+      ad.tl = c->tl_cur;
+      launch_adam(ad, s);
+    }
    }
     // L7/L8 (.. L8b): updated critics on [s|1|a~] (head dot partials: slots 4 / 5)
     const float* xa = bb.x2 + (size_t)B * Kx;
@@ -807,8 +842,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     sb.Wh = W(c->p_head); sb.ldw = Hd; sb.H = H; sb.hp2 = hpa(L); sb.ldh = Hd; sb.dhp2 = c->dhp[L].p;
     check_span(sb.dhp2, (int64_t)B * H - 1, "dhp2");
     check_span(sb.Wh, (int64_t)(2 * A - 1) * Hd + H - 1, "Whead");
-    if (mark(c, "gemm_L10_dlda_sample_bwd_dhp2", 2.0 * B * A * (2.0 * H) + 2.0 * B * (2.0 * A) * H))
+    if (mark(c, "gemm_L10_dlda_sample_bwd_dhp2", 2.0 * B * A * (2.0 * H) + 2.0 * B * (2.0 * A) * H)) {
+      sb.tl = c->tl_cur;
       launch_gemm_sample_bwd(da, sb, s);
+    }
     // L11 (3 hidden layers) .. L12: dhp[l-1] = (dhp[l] Wpi[l]) * relu'(hp[l-1]);
     // L13: every policy dW (+ Adam, alpha step, policy loss, loss ring when fused)
     auto pdst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
@@ -871,7 +908,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.loss_div = (float)B; ad.log_alpha_idx = c->la_idx; ad.auto_entropy = c->cfg.auto_entropy;
     ad.loss_ring = use_ring ? c->ring.p : nullptr; ad.ring = c->ring_slots;
     ad.ph = c->Ph.p; ad.tgth = c->Th.p;
-    if (mark(c, "adam_actor_alpha")) launch_adam(ad, s);
+    if (mark(c, "adam_actor_alpha")) {
+      ad.tl = c->tl_cur;
+      launch_adam(ad, s);
+    }
   }
 }
 
@@ -1701,6 +1741,91 @@ int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_o
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     *n_sites = n;
+  });
+}
+
+int sacmi_profile_timeline(sacmi_ctx* c, int32_t batch, int32_t n_updates, int32_t max_kernels,
+                           char* names_out, int32_t* kind_out, int32_t* grid_out, int32_t* site_out,
+                           double* start_us, double* end_us, double* flops_out, double* bytes_out,
+                           int32_t* n_kernels, double* graph_us) {
+  return guard([&] {
+    check_device_batch(c, batch);
+    REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
+    REQUIRE(max_kernels > 0 && names_out && kind_out && grid_out && site_out && start_us && end_us &&
+                n_kernels && graph_us, SACMI_EVALUE, "null output");
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    DevBuf<tl_word> buf;
+    const int cap = 64 * n_updates;                // launch sites (an update has < 40)
+    buf.alloc((size_t)cap * kTlPerSite * kTlWords);
+    hipGraphExec_t ex = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    auto cleanup = [&]() {
+      c->tl_dev = nullptr; c->tl_cur = nullptr;
+      if (ex) (void)hipGraphExecDestroy(ex);
+      if (e0) (void)hipEventDestroy(e0);
+      if (e1) (void)hipEventDestroy(e1);
+      buf.release();
+    };
+    try {
+      // the same update sequence sacmi_step_many_async replays, captured with every
+      // kernel launch pointing at its own timeline slots
+      c->tl_dev = buf.p; c->tl_cap = cap; c->tl_sites = 0;
+      c->tl_names.clear(); c->tl_flops.clear(); c->tl_bytes.clear();
+      const bool ride = n_updates > 1 && ride_possible(c, batch);
+      hipGraph_t g;
+      CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      try {
+        for (int r = 0; r < n_updates; ++r)
+          enqueue_update(c, batch, 1, 1, 7, 1.f, true, ride ? (r & 1) : 0, ride && r > 0,
+                         ride && r + 1 < n_updates);
+      } catch (...) {
+        (void)hipStreamEndCapture(c->stream, &g);
+        throw;
+      }
+      CHECK_HIP(hipStreamEndCapture(c->stream, &g));
+      c->tl_dev = nullptr; c->tl_cur = nullptr;
+      CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      CHECK_HIP(hipGraphDestroy(g));
+      CHECK_HIP(hipEventCreate(&e0));
+      CHECK_HIP(hipEventCreate(&e1));
+      CHECK_HIP(hipGraphLaunch(ex, c->stream));     // warm (its stamps are discarded)
+      CHECK_HIP(hipMemsetAsync(buf.p, 0xFF, buf.n * sizeof(tl_word), c->stream));
+      CHECK_HIP(hipEventRecord(e0, c->stream));
+      CHECK_HIP(hipGraphLaunch(ex, c->stream));
+      CHECK_HIP(hipEventRecord(e1, c->stream));
+      CHECK_HIP(hipEventSynchronize(e1));
+      float ms = 0;
+      CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
+      *graph_us = ms * 1000.0;
+      std::vector<tl_word> h(buf.n);
+      CHECK_HIP(hipMemcpy(h.data(), buf.p, buf.n * sizeof(tl_word), hipMemcpyDeviceToHost));
+      tl_word t0 = ~(tl_word)0;
+      for (int sidx = 0; sidx < c->tl_sites; ++sidx)
+        for (int k = 0; k < kTlPerSite; ++k) t0 = std::min(t0, h[((size_t)sidx * kTlPerSite + k) * kTlWords]);
+      int n = 0;
+      for (int sidx = 0; sidx < c->tl_sites; ++sidx)
+        for (int k = 0; k < kTlPerSite; ++k) {
+          const tl_word* w = &h[((size_t)sidx * kTlPerSite + k) * kTlWords];
+          if (w[0] == ~(tl_word)0) continue;          // not launched
+          REQUIRE(n < max_kernels, SACMI_EVALUE, "max_kernels too small");
+          std::memset(names_out + 32 * n, 0, 32);
+          std::strncpy(names_out + 32 * n, c->tl_names[sidx].c_str(), 31);
+          kind_out[n] = (int32_t)w[2];
+          grid_out[n] = (int32_t)w[3];
+          site_out[n] = sidx;
+          start_us[n] = (double)(w[0] - t0) * 0.01;   // 100 MHz ticks -> us
+          end_us[n] = (double)(~w[1] - t0) * 0.01;
+          // the site's algorithmic work, on its first kernel
+          if (flops_out) flops_out[n] = k == 0 ? c->tl_flops[sidx] : 0.0;
+          if (bytes_out) bytes_out[n] = k == 0 ? c->tl_bytes[sidx] : 0.0;
+          ++n;
+        }
+      *n_kernels = n;
+    } catch (...) {
+      cleanup();
+      throw;
+    }
+    cleanup();
   });
 }
 

@@ -49,6 +49,39 @@ void ensure_dyn_lds(const void* kernel, size_t bytes);
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// ---------------------------------------------------------------------------
+// Launch timeline (sacmi_profile_timeline).  In an instrumented update graph every kernel
+// launch owns four words {start, ~end, kind, grid}: workgroups fold their entry clock into
+// `start` (atomicMin) and their exit clock into `~end` (atomicMin of the complement, so
+// both words start at all-ones), on the 100 MHz s_memrealtime clock.
+// Null pointer (every production graph): no instruction beyond the test.
+typedef unsigned long long tl_word;
+enum TlKind : int {
+  TL_GEMM = 1, TL_FWD, TL_FWD16, TL_AXK16, TL_DW_PART, TL_DW_PART16, TL_DW_FIN, TL_HEADS,
+  TL_SAMPLE_BWD, TL_MT_SAMPLE, TL_GATHER, TL_PER_F1, TL_PER_F2, TL_PER_F2B, TL_PER_F3,
+  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_KINDS
+};
+constexpr int kTlWords = 4;          // words per kernel launch
+constexpr int kTlPerSite = 8;        // kernel launches one launch site may make
+struct TlMark {
+  tl_word* p;
+  __device__ __forceinline__ TlMark(tl_word* q, int kind) : p(q) {
+    // the first 8 workgroups (the first dispatched, one per XCD) fold in their entry; the
+    // last 8 their exit: 16 atomics per launch (every workgroup's would cost ~1.5 us per
+    // launch on the one contended word).  Wave 0 only, as a wave-uniform branch (a
+    // divergent single-lane branch around the atomic costs the big GEMM kernels ~30 VGPRs
+    // and spills); its lanes' atomics on one address with one scalar value are combined.
+    if (p && blockIdx.x < 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u) {
+      atomicMin(p, (tl_word)wall_clock64());
+      if (blockIdx.x == 0) { p[2] = (tl_word)kind; p[3] = (tl_word)gridDim.x; }
+    }
+  }
+  __device__ __forceinline__ ~TlMark() {
+    if (p && blockIdx.x + 8 >= gridDim.x && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)
+      atomicMin(p + 1, ~(tl_word)wall_clock64());
+  }
+};
+
 // One bias-folded linear layer inside an arena.
 struct Linear {
   int64_t off = 0;   // float offset of W~ [n_out, ld]
@@ -159,6 +192,7 @@ struct GatherArgs {
   float* xq; float* x2; int ldx;   // xq [B, ldx], x2 [2B, ldx]
   float* r; float* d;
   int by_slot;            // 1: idx are ring slots (PER), 0: deque positions
+  tl_word* tl;
 };
 struct MtSampleArgs {
   uint32_t* mt;           // 624 key words + pos
@@ -168,6 +202,7 @@ struct MtSampleArgs {
   int32_t* idx_out;       // [k]
   int64_t* idx64_out;     // [k] or null
   int32_t* pool;          // scratch [max setsize] for the pool branch
+  tl_word* tl;
 };
 // Work of the NEXT update of a multi-update graph that rides along, as extra
 // workgroups, in a GEMM launch whose tiles leave CUs idle (1024-thread configs):
@@ -217,6 +252,7 @@ struct GemmBatch {
   int bf16;            // 1: bf16 MFMA operands (fp32 loads rounded to bf16 in registers)
   float* ws;           // bf16 deep-K weight-gradient levels: split-K partial workspace
   int64_t ws_floats;   //   (capacity; launch_gemm falls back when a level needs more)
+  tl_word* tl;         // launch timeline slots of this level (kTlPerSite), or null
 };
 
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked
@@ -239,6 +275,7 @@ struct HeadSampleArgs {
   float* logp_part;      // [grid][2] or null: per workgroup, sum of logp over its rows
   int split_row;         //   < split_row (slot 0) and >= split_row (slot 1)
   float* act_host;       // or null: the actions also stored [row][A] to host-mapped memory
+  tl_word* tl;
 };
 
 // Sample-backward epilogue of the dL/da GEMM.
@@ -255,6 +292,7 @@ struct SampleBwdArgs {
   const float* hp2;      // actor rows' hidden-2 [B, ldh] (ReLU mask source)
   int ldh;
   float* dhp2;           // [B, H]
+  tl_word* tl;
 };
 
 // ---------------------------------------------------------------------------
@@ -287,6 +325,7 @@ struct AdamArgs {
   int ring;
   unsigned short* ph;      // bf16 shadows of p / tgt (bf16 mode) or null
   unsigned short* tgth;
+  tl_word* tl;
 };
 void launch_adam(const AdamArgs& a, hipStream_t s);
 
@@ -337,6 +376,7 @@ struct PerArgs {
   int32_t* idx32;         // [k] ring slots (feeds the update's gather)
   int64_t* idx_out;       // [k]
   float* w_out;           // [k]
+  tl_word* tl;            // kernels F1, F2, F2b, F3, F4 (or the unfused sequence) in order
 };
 void launch_per_sample(const PerArgs& a, hipStream_t s);
 void launch_per_update(float* prio, const int64_t* idx, const float* val, int64_t n,

@@ -98,7 +98,15 @@ _PROTOS = {
                            ctypes.c_int32, c_i32p],
     "sacmi_profile_sites": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
                             c_f64p, ctypes.c_int32, c_i32p],
+    "sacmi_profile_timeline": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
+                               c_i32p, c_i32p, c_i32p, c_f64p, c_f64p, c_f64p, c_f64p, c_i32p,
+                               c_f64p],
 }
+# kernel kinds of the launch timeline (TlKind, csrc/sacmi_internal.h)
+TL_KINDS = {1: "k_gemm", 2: "k_fwd", 3: "k_fwd16", 4: "k_axk16", 5: "k_dw_part", 6: "k_dw_part16",
+            7: "k_dw_fin", 8: "k_heads_sample", 9: "k_gemm_sample_bwd", 10: "k_mt_sample",
+            11: "k_gather", 12: "k_per_f1", 13: "k_per_f2", 14: "k_per_f2b", 15: "k_per_f3",
+            16: "k_per_f4", 17: "per_unfused", 18: "k_adam"}
 EXPORTS = tuple(_PROTOS) + ("sacmi_abi_version", "sacmi_last_error")
 
 _lib = None
@@ -157,6 +165,10 @@ def dptr(a):
 
 def i64ptr(a):
     return a.ctypes.data_as(c_i64p) if a is not None else None
+
+
+def i32ptr(a):
+    return a.ctypes.data_as(c_i32p) if a is not None else None
 
 
 def u8ptr(a):

@@ -265,6 +265,21 @@ int sacmi_profile_sites(sacmi_ctx* ctx, int32_t batch, int32_t reps, char* names
                         float* us_out, double* flops_out, double* bytes_out, int32_t max_sites,
                         int32_t* n_sites);
 
+/* Launch timeline of the real update: n_updates consecutive updates exactly as
+ * sacmi_step_many_async runs them (device sampling + noise, ride-along sampling, one
+ * hipGraph), captured with every kernel stamping its first workgroup's entry and its last
+ * workgroup's exit on the GPU's 100 MHz real-time clock.  Replayed once to warm up, then
+ * once measured; returns per kernel launch, in launch order: the launch site's name (32
+ * bytes, NUL-padded), the kernel kind (TlKind in csrc/sacmi_internal.h), its grid, the
+ * site index (sites count across updates), start / end in microseconds from the first
+ * kernel's start, the site's algorithmic FLOPs / bytes (GEMM sites, on the site's first
+ * kernel; may be NULL); graph_us = HIP-event time of the measured replay.  Diagnostic: the model
+ * state advances by 2 * n_updates updates. */
+int sacmi_profile_timeline(sacmi_ctx* ctx, int32_t batch, int32_t n_updates, int32_t max_kernels,
+                           char* names_out, int32_t* kind_out, int32_t* grid_out, int32_t* site_out,
+                           double* start_us, double* end_us, double* flops_out, double* bytes_out,
+                           int32_t* n_kernels, double* graph_us);
+
 #ifdef __cplusplus
 }
 #endif

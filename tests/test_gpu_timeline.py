@@ -1,0 +1,52 @@
+"""Launch timeline of the real update graph (sacmi_profile_timeline): the instrumented
+graph runs the same kernels as the timed one, the stamps are ordered, the per-kernel slots
+add up to the HIP-event time of the replay, and the instrumented updates leave the model
+in the same state as uninstrumented ones (the stamps change no arithmetic)."""
+import numpy as np
+import pytest
+
+from oracle.sac_step import NETS, SacConfig, init_params, synthetic_rows
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(seed=7):
+    from sacmi import Config, Context
+    cfg = SacConfig(24, 4, 64)
+    params = init_params(cfg, 5, bias_scale=0.05)
+    c = Context(Config(24, 4, 64, max_batch=64, capacity=2000, seed=seed), 0)
+    for n in NETS:
+        c.set_net(n, params[n])
+    c.push(*synthetic_rows(cfg, 2000, 6, state_scale=0.5))
+    return c
+
+
+def test_timeline_covers_the_update_graph():
+    c = _ctx()
+    ks, graph_us = c.profile_timeline(64, 4)
+    names = [k["site"] for k in ks]
+    # first update samples for itself, the next three ride along in L12 / L13
+    assert names.count("mt_sample") == 1 and names.count("gather") == 1
+    for site in ("gemm_L1_fc1", "gemm_L6_critic_dW_adam", "gemm_L13_pi_dW_adam", "heads_sample",
+                 "gemm_L10_dlda_sample_bwd_dhp2"):
+        assert names.count(site) == 4, site
+    starts = [k["start_us"] for k in ks]
+    assert starts == sorted(starts)                    # graph kernels run in launch order
+    assert all(k["end_us"] >= k["start_us"] for k in ks)
+    span = ks[-1]["end_us"] - ks[0]["start_us"]
+    assert 0 < span <= graph_us * 1.05, (span, graph_us)
+    l1 = [k for k in ks if k["site"] == "gemm_L1_fc1"]
+    assert all(k["kernel"] == "k_gemm" and k["flops"] > 0 and k["grid"] > 0 for k in l1)
+
+
+def test_timeline_updates_equal_plain_updates():
+    a, b = _ctx(), _ctx()
+    a.profile_timeline(64, 3)                          # 6 instrumented updates
+    b.step_many_async(64, 3)
+    b.step_many_async(64, 3)
+    b.synchronize()
+    for n in NETS:
+        pa, pb = a.get_net(n), b.get_net(n)
+        for k in pa:
+            assert np.array_equal(pa[k], pb[k]), (n, k)
+    assert np.array_equal(a.fetch_losses(6), b.fetch_losses(6))

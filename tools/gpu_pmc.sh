@@ -1,16 +1,22 @@
 #!/bin/bash
-# HBM traffic counters for the bench command: FETCH_SIZE and WRITE_SIZE in separate
-# rocprofv3 passes (each with --kernel-trace only, MI355X_MICROARCH.md "rocprofv3 PMC").
+# PMC passes over one bench command (MI355X_MICROARCH.md "rocprofv3 PMC": one counter
+# group per run, --kernel-trace only, the program itself right after --):
+#   FETCH_SIZE | WRITE_SIZE | MFMA busy + MFMA ops + GUI active
+# then tools/pmc_summary.py -> $OUT/pmc_<tag>.json.  usage: tools/gpu_pmc.sh <tag> [bench args]
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-OUT=$GRAFT_REPO_ROOT/gpurun_out
-ARGS=${PMC_ARGS:---steps 100 --warmup 20 --fill 200000 --no-cpu-baseline --no-roofline --no-trainer-loop}
+TAG=${1:-c2}; shift
+OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG
+ARGS=${*:---steps 20 --warmup 5 --profile-only}
+mkdir -p $OUT
 cd /tmp
-for C in FETCH_SIZE WRITE_SIZE; do
-  rm -rf $OUT/pmc_$C
-  timeout -k 10 400 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$C -o run -- \
-    python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT/pmc_$C.log 2>&1
-  rc=$?; echo "pmc $C rc=$rc"; [ $rc -ne 0 ] && { tail -20 $OUT/pmc_$C.log; exit $rc; }
+i=0
+for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  rm -rf $OUT/p$i
+  timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
+    python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT/p$i.log 2>&1
+  rc=$?; echo "pmc pass $i ($C) rc=$rc"; [ $rc -ne 0 ] && { tail -20 $OUT/p$i.log; exit $rc; }
 done
-find $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE -name "*.csv" | head
+python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py $OUT $GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG.json "$ARGS"
