@@ -120,18 +120,28 @@ def init_agent(ctx, seed):
 LEVEL_KERNELS = {"k_gemm", "k_fwd", "k_fwd16", "k_axk16", "k_dw_part", "k_dw_part16", "k_dw_fin"}
 
 
-def timeline_roofline(ctx, batch, n_updates):
+def timeline_roofline(ctx, batch, n_updates, data_parallel=False):
     """Roofline of the GEMM levels measured on the REAL update: the same n-update graph
     the timed windows replay, instrumented so that every kernel stamps its first
     workgroup's entry on the GPU clock (sacmi_profile_timeline), replayed once warm and
     once measured, with HIP events on the context stream around the measured replay.
     Kernels run back to back in the graph, so a launch's duration is the distance to the
-    next launch's start (the last: its own end); their sum must equal the event time."""
-    ks, graph_us = ctx.profile_timeline(batch, n_updates)
+    next launch's start (the last: its own end); their sum must equal the event time.
+    data_parallel: the sequence of the data-parallel update (sacmi_profile_timeline_dp,
+    every rank calls), whose RCCL all-reduces stamp nothing: a kernel followed by one
+    ends at its own exit stamp, and the gap up to the next kernel is all-reduce time."""
+    ks, graph_us = ctx.profile_timeline(batch, n_updates, data_parallel)
     ks = sorted(ks, key=lambda k: k["start_us"])
+    allreduce_us = 0.0
     for i, k in enumerate(ks):
-        nxt = ks[i + 1]["start_us"] if i + 1 < len(ks) else k["end_us"]
-        k["dur_us"] = nxt - k["start_us"]
+        nxt = ks[i + 1] if i + 1 < len(ks) else None
+        if nxt is None:
+            k["dur_us"] = k["end_us"] - k["start_us"]
+        elif data_parallel and nxt["site_idx"] > k["site_idx"] + 1:
+            k["dur_us"] = k["end_us"] - k["start_us"]
+            allreduce_us += nxt["start_us"] - k["end_us"]
+        else:
+            k["dur_us"] = nxt["start_us"] - k["start_us"]
     lv = [k for k in ks if k["kernel"] in LEVEL_KERNELS]
     gemm_us = sum(k["dur_us"] for k in lv)
     gemm_flops = sum(k["flops"] for k in lv)
@@ -145,7 +155,8 @@ def timeline_roofline(ctx, batch, n_updates):
         e = sites.setdefault(k["site"], [0.0, 0])
         e[0] += k["dur_us"]
         e[1] += 1 if k["flops"] > 0 or k["kernel"] not in LEVEL_KERNELS else 0
-    return dict(graph_us=graph_us, sum_us=sum(k["dur_us"] for k in ks), n_updates=n_updates,
+    return dict(graph_us=graph_us, sum_us=sum(k["dur_us"] for k in ks) + allreduce_us,
+                allreduce_us=allreduce_us, n_updates=n_updates,
                 gemm_us=gemm_us, gemm_flops=gemm_flops, gemm_bytes=gemm_bytes, levels=levels,
                 kernel_launches=kernel_launches,
                 achieved_tflops=gemm_flops / (gemm_us * 1e-6) / 1e12,
@@ -290,11 +301,13 @@ def trainer_loop(wl, steps=300, warmup=30, fill=20_000):
                     f"update_parameters({B}) per env step, drop-in SAC, {fill}-row replay"}
 
 
-def roofline_object(ctx, args, wl, peak):
-    """The line's `roofline` object: the GEMM levels of the real multi-update graph."""
+def roofline_object(ctx, args, wl, peak, data_parallel=False):
+    """The line's `roofline` object: the GEMM levels of the real multi-update graph
+    (data_parallel: of the data-parallel update sequence, all-reduces included)."""
     upl = max(1, min(args.updates_per_launch, 256))
-    info = timeline_roofline(ctx, args.batch, upl)
-    pmc = pmc_counters(args.config, args.networks)
+    info = timeline_roofline(ctx, args.batch, upl, data_parallel)
+    # the committed PMC figures were collected on the single-GPU graph (fused Adam levels)
+    pmc = None if data_parallel else pmc_counters(args.config, args.networks)
     lvl = pmc["per_level"] if pmc else {}
     per_level_flops = info["gemm_flops"] / max(info["levels"], 1)
     avg_level_us = info["gemm_us"] / max(info["levels"], 1)
@@ -308,9 +321,11 @@ def roofline_object(ctx, args, wl, peak):
             "kernel": "GEMM levels of the update: " + ", ".join(
                 f"sacmi::{k} x{n}" for k, n in sorted(info["kernel_launches"].items())) +
                       f" per {upl} updates ({wl['dtype']} MFMA)",
-            "method": "launch timeline of the timed multi-update graph (per-kernel GPU-clock "
-                      "stamps, sacmi_profile_timeline); HIP events on the context stream "
-                      "around the same replay",
+            "method": ("launch timeline of the data-parallel update sequence (phases + RCCL "
+                       "all-reduces, sacmi_profile_timeline_dp, all ranks)" if data_parallel else
+                       "launch timeline of the timed multi-update graph (per-kernel GPU-clock "
+                       "stamps, sacmi_profile_timeline)") +
+                      "; HIP events on the context stream around the same replay",
             "levels_per_step": round(info["levels"] / upl, 2),
             "avg_launch_us": round(avg_level_us, 3),
             "flops_per_launch": round(per_level_flops),
@@ -318,6 +333,7 @@ def roofline_object(ctx, args, wl, peak):
             "gemm_flops_per_step": round(info["gemm_flops"] / upl),
             "step_us_timeline": round(info["sum_us"] / upl, 2),
             "step_us_hip_events": round(info["graph_us"] / upl, 2),
+            "allreduce_us_per_step": round(info["allreduce_us"] / upl, 2) if data_parallel else None,
             "sites_us": info["sites_us"]}
 
 

@@ -412,9 +412,9 @@ static GemmDesc gd_dw_h(const float* dY, int ldy, const float* X, int ldx, float
 // Host-side bounds check of one GEMM before it is ever launched: every element the
 // kernel can touch (incl. the 16-byte over-read of K-contiguous fetches) must lie in
 // one registered allocation, and vector-loaded operands must be 16-byte aligned.
-static void check_span(const void* p, int64_t max_index, const char* what) {
+static void check_span(const void* p, int64_t max_index, const char* what, int elem_bytes = 4) {
   if (!p) throw Error{SACMI_ESTATE, std::string("null GEMM operand ") + what};
-  const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)(max_index + 1) * 4;
+  const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)(max_index + 1) * elem_bytes;
   for (const AllocRec& r : alloc_registry())
     if (a >= r.base && e <= r.base + r.bytes) return;
   throw Error{SACMI_ESTATE, std::string("GEMM operand out of bounds: ") + what};
@@ -457,6 +457,31 @@ static void validate(const GemmDesc& d) {
     check_span(d.dotp, (int64_t)(d.M - 1) * d.dotp_ld + (d.N - 1) / 32, "dotp");
   }
   if (d.epi == EPI_MASK) check_span(d.aux, (int64_t)(d.M - 1) * d.ldaux + d.N - 1, "aux");
+}
+
+// The level-wide operands launch_gemm may route a level's work through, checked once the
+// level is complete (right before its launch):
+//   * Bh, the bf16 shadow of a weight operand: k_fwd16 / k_axk16 / k_gemm<bf16> read it
+//     over exactly B's element range (2 bytes per element, 8-byte vector loads);
+//   * ws, the split-K partial workspace: k_dw_part{,16} write and k_dw_fin reads
+//     ws[0, ws_floats) at most (dw_split_plan never plans past ws_floats), so the claimed
+//     capacity must lie inside one allocation.
+static void validate_batch(const GemmBatch& b) {
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    if (!d.Bh) continue;
+    REQUIRE(((uintptr_t)d.Bh & 7) == 0, SACMI_ESTATE, "Bh misaligned");
+    const int64_t klast = ((int64_t)(d.K - 1) / 4) * 4 + 3;
+    const int64_t last = d.b_kc ? (int64_t)(d.N - 1) * d.ldb + klast
+                                : (int64_t)(d.K - 1) * d.ldb + ((d.N - 1) & ~3) + 3;
+    check_span(d.Bh, last, "Bh (bf16 shadow)", 2);
+  }
+  if (b.ws) {
+    REQUIRE(b.ws_floats > 0 && ((uintptr_t)b.ws & 15) == 0, SACMI_ESTATE, "bad split-K workspace");
+    check_span(b.ws, b.ws_floats - 1, "ws (split-K workspace)");
+  } else {
+    REQUIRE(b.ws_floats == 0, SACMI_ESTATE, "split-K workspace capacity without a workspace");
+  }
 }
 
 struct Level {
@@ -616,6 +641,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     for (int i = 0; i < lv.b.count; ++i) lv.b.d[i].Bh = shadow(lv.b.d[i].B);
     lv.b.ws = c->dw_ws.p;
     lv.b.ws_floats = (int64_t)c->dw_ws.n;
+    validate_batch(lv.b);
     if (mark(c, name.c_str(), level_flops(lv.b), level_bytes(lv.b))) {
       lv.b.tl = c->tl_cur;
       launch_gemm(lv.b, s);
@@ -1073,6 +1099,7 @@ static void enqueue_dp(sacmi_ctx* c, int B, int n) {
   const float scale = 1.f / (float)c->dp_world;
   const bool ride = n > 1 && ride_possible(c, B);
   auto allreduce = [&](int64_t begin, int64_t end) {
+    (void)mark(c, begin == c->q_begin ? "allreduce_critic_grads" : "allreduce_actor_grads");
     float* g = c->G.p + begin;
     CHECK_RCCL(rccl().all_reduce(g, g, (size_t)(end - begin), ncclFloat32, ncclSum, c->comm, c->stream));
   };
@@ -1744,6 +1771,89 @@ int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_o
   });
 }
 
+// Launch timeline of whatever `enqueue` puts on the context stream, captured into one
+// hipGraph with every kernel launch pointing at its own timeline slots; replayed once
+// warm, then once measured between HIP events.  Sites that launch no stamping kernel (the
+// RCCL all-reduces of the data-parallel sequence) leave no entry.
+extern "C++" {
+template <class F>
+static void timeline_of(sacmi_ctx* c, int n_updates, F&& enqueue, int32_t max_kernels,
+                        char* names_out, int32_t* kind_out, int32_t* grid_out, int32_t* site_out,
+                        double* start_us, double* end_us, double* flops_out, double* bytes_out,
+                        int32_t* n_kernels, double* graph_us) {
+  REQUIRE(max_kernels > 0 && names_out && kind_out && grid_out && site_out && start_us && end_us &&
+              n_kernels && graph_us, SACMI_EVALUE, "null output");
+  CHECK_HIP(hipStreamSynchronize(c->stream));
+  DevBuf<tl_word> buf;
+  const int cap = 64 * n_updates;                // launch sites (an update has < 40)
+  buf.alloc((size_t)cap * kTlPerSite * kTlWords);
+  hipGraphExec_t ex = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  auto cleanup = [&]() {
+    c->tl_dev = nullptr; c->tl_cur = nullptr;
+    if (ex) (void)hipGraphExecDestroy(ex);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    buf.release();
+  };
+  try {
+    c->tl_dev = buf.p; c->tl_cap = cap; c->tl_sites = 0;
+    c->tl_names.clear(); c->tl_flops.clear(); c->tl_bytes.clear();
+    hipGraph_t g;
+    CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    try {
+      enqueue();
+    } catch (...) {
+      (void)hipStreamEndCapture(c->stream, &g);
+      throw;
+    }
+    CHECK_HIP(hipStreamEndCapture(c->stream, &g));
+    c->tl_dev = nullptr; c->tl_cur = nullptr;
+    CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    CHECK_HIP(hipGraphDestroy(g));
+    CHECK_HIP(hipEventCreate(&e0));
+    CHECK_HIP(hipEventCreate(&e1));
+    CHECK_HIP(hipGraphLaunch(ex, c->stream));     // warm (its stamps are discarded)
+    CHECK_HIP(hipMemsetAsync(buf.p, 0xFF, buf.n * sizeof(tl_word), c->stream));
+    CHECK_HIP(hipEventRecord(e0, c->stream));
+    CHECK_HIP(hipGraphLaunch(ex, c->stream));
+    CHECK_HIP(hipEventRecord(e1, c->stream));
+    CHECK_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
+    *graph_us = ms * 1000.0;
+    std::vector<tl_word> h(buf.n);
+    CHECK_HIP(hipMemcpy(h.data(), buf.p, buf.n * sizeof(tl_word), hipMemcpyDeviceToHost));
+    tl_word t0 = ~(tl_word)0;
+    for (int sidx = 0; sidx < c->tl_sites; ++sidx)
+      for (int k = 0; k < kTlPerSite; ++k) t0 = std::min(t0, h[((size_t)sidx * kTlPerSite + k) * kTlWords]);
+    int n = 0;
+    for (int sidx = 0; sidx < c->tl_sites; ++sidx)
+      for (int k = 0; k < kTlPerSite; ++k) {
+        const tl_word* w = &h[((size_t)sidx * kTlPerSite + k) * kTlWords];
+        if (w[0] == ~(tl_word)0) continue;          // not launched
+        REQUIRE(n < max_kernels, SACMI_EVALUE, "max_kernels too small");
+        std::memset(names_out + 32 * n, 0, 32);
+        std::strncpy(names_out + 32 * n, c->tl_names[sidx].c_str(), 31);
+        kind_out[n] = (int32_t)w[2];
+        grid_out[n] = (int32_t)w[3];
+        site_out[n] = sidx;
+        start_us[n] = (double)(w[0] - t0) * 0.01;   // 100 MHz ticks -> us
+        end_us[n] = (double)(~w[1] - t0) * 0.01;
+        // the site's algorithmic work, on its first kernel
+        if (flops_out) flops_out[n] = k == 0 ? c->tl_flops[sidx] : 0.0;
+        if (bytes_out) bytes_out[n] = k == 0 ? c->tl_bytes[sidx] : 0.0;
+        ++n;
+      }
+    *n_kernels = n;
+  } catch (...) {
+    cleanup();
+    throw;
+  }
+  cleanup();
+}
+}  // extern "C++"
+
 int sacmi_profile_timeline(sacmi_ctx* c, int32_t batch, int32_t n_updates, int32_t max_kernels,
                            char* names_out, int32_t* kind_out, int32_t* grid_out, int32_t* site_out,
                            double* start_us, double* end_us, double* flops_out, double* bytes_out,
@@ -1751,81 +1861,29 @@ int sacmi_profile_timeline(sacmi_ctx* c, int32_t batch, int32_t n_updates, int32
   return guard([&] {
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
-    REQUIRE(max_kernels > 0 && names_out && kind_out && grid_out && site_out && start_us && end_us &&
-                n_kernels && graph_us, SACMI_EVALUE, "null output");
-    CHECK_HIP(hipStreamSynchronize(c->stream));
-    DevBuf<tl_word> buf;
-    const int cap = 64 * n_updates;                // launch sites (an update has < 40)
-    buf.alloc((size_t)cap * kTlPerSite * kTlWords);
-    hipGraphExec_t ex = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    auto cleanup = [&]() {
-      c->tl_dev = nullptr; c->tl_cur = nullptr;
-      if (ex) (void)hipGraphExecDestroy(ex);
-      if (e0) (void)hipEventDestroy(e0);
-      if (e1) (void)hipEventDestroy(e1);
-      buf.release();
-    };
-    try {
-      // the same update sequence sacmi_step_many_async replays, captured with every
-      // kernel launch pointing at its own timeline slots
-      c->tl_dev = buf.p; c->tl_cap = cap; c->tl_sites = 0;
-      c->tl_names.clear(); c->tl_flops.clear(); c->tl_bytes.clear();
-      const bool ride = n_updates > 1 && ride_possible(c, batch);
-      hipGraph_t g;
-      CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-      try {
-        for (int r = 0; r < n_updates; ++r)
-          enqueue_update(c, batch, 1, 1, 7, 1.f, true, ride ? (r & 1) : 0, ride && r > 0,
-                         ride && r + 1 < n_updates);
-      } catch (...) {
-        (void)hipStreamEndCapture(c->stream, &g);
-        throw;
-      }
-      CHECK_HIP(hipStreamEndCapture(c->stream, &g));
-      c->tl_dev = nullptr; c->tl_cur = nullptr;
-      CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-      CHECK_HIP(hipGraphDestroy(g));
-      CHECK_HIP(hipEventCreate(&e0));
-      CHECK_HIP(hipEventCreate(&e1));
-      CHECK_HIP(hipGraphLaunch(ex, c->stream));     // warm (its stamps are discarded)
-      CHECK_HIP(hipMemsetAsync(buf.p, 0xFF, buf.n * sizeof(tl_word), c->stream));
-      CHECK_HIP(hipEventRecord(e0, c->stream));
-      CHECK_HIP(hipGraphLaunch(ex, c->stream));
-      CHECK_HIP(hipEventRecord(e1, c->stream));
-      CHECK_HIP(hipEventSynchronize(e1));
-      float ms = 0;
-      CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
-      *graph_us = ms * 1000.0;
-      std::vector<tl_word> h(buf.n);
-      CHECK_HIP(hipMemcpy(h.data(), buf.p, buf.n * sizeof(tl_word), hipMemcpyDeviceToHost));
-      tl_word t0 = ~(tl_word)0;
-      for (int sidx = 0; sidx < c->tl_sites; ++sidx)
-        for (int k = 0; k < kTlPerSite; ++k) t0 = std::min(t0, h[((size_t)sidx * kTlPerSite + k) * kTlWords]);
-      int n = 0;
-      for (int sidx = 0; sidx < c->tl_sites; ++sidx)
-        for (int k = 0; k < kTlPerSite; ++k) {
-          const tl_word* w = &h[((size_t)sidx * kTlPerSite + k) * kTlWords];
-          if (w[0] == ~(tl_word)0) continue;          // not launched
-          REQUIRE(n < max_kernels, SACMI_EVALUE, "max_kernels too small");
-          std::memset(names_out + 32 * n, 0, 32);
-          std::strncpy(names_out + 32 * n, c->tl_names[sidx].c_str(), 31);
-          kind_out[n] = (int32_t)w[2];
-          grid_out[n] = (int32_t)w[3];
-          site_out[n] = sidx;
-          start_us[n] = (double)(w[0] - t0) * 0.01;   // 100 MHz ticks -> us
-          end_us[n] = (double)(~w[1] - t0) * 0.01;
-          // the site's algorithmic work, on its first kernel
-          if (flops_out) flops_out[n] = k == 0 ? c->tl_flops[sidx] : 0.0;
-          if (bytes_out) bytes_out[n] = k == 0 ? c->tl_bytes[sidx] : 0.0;
-          ++n;
-        }
-      *n_kernels = n;
-    } catch (...) {
-      cleanup();
-      throw;
-    }
-    cleanup();
+    // the same update sequence sacmi_step_many_async replays
+    const bool ride = n_updates > 1 && ride_possible(c, batch);
+    timeline_of(c, n_updates, [&]() {
+      for (int r = 0; r < n_updates; ++r)
+        enqueue_update(c, batch, 1, 1, 7, 1.f, true, ride ? (r & 1) : 0, ride && r > 0,
+                       ride && r + 1 < n_updates);
+    }, max_kernels, names_out, kind_out, grid_out, site_out, start_us, end_us, flops_out,
+       bytes_out, n_kernels, graph_us);
+  });
+}
+
+int sacmi_profile_timeline_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates, int32_t max_kernels,
+                              char* names_out, int32_t* kind_out, int32_t* grid_out, int32_t* site_out,
+                              double* start_us, double* end_us, double* flops_out, double* bytes_out,
+                              int32_t* n_kernels, double* graph_us) {
+  return guard([&] {
+    REQUIRE(c->comm, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
+    check_device_batch(c, batch);
+    REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
+    // the sequence sacmi_step_dp replays: phases + the two RCCL all-reduces per update
+    timeline_of(c, n_updates, [&]() { enqueue_dp(c, batch, n_updates); }, max_kernels,
+                names_out, kind_out, grid_out, site_out, start_us, end_us, flops_out, bytes_out,
+                n_kernels, graph_us);
   });
 }
 
@@ -1949,6 +2007,63 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
                                  (size_t)A * 4, n, hipMemcpyDeviceToHost, s));
     CHECK_HIP(hipStreamSynchronize(s));
     if (pinned) std::memcpy(a_out, h_out, (size_t)n * A * 4);
+  });
+}
+
+// Host-only self test of the launch validator (no device needed): host arrays stand in
+// for registered allocations, and every case states whether validate() / validate_batch()
+// must accept or reject it.
+int sacmi_selftest_span_checker(int32_t* n_cases, int32_t* n_passed) {
+  return guard([&] {
+    REQUIRE(n_cases && n_passed, SACMI_EVALUE, "null argument");
+    const int M = 64, N = 64, K = 128, ld = 132;
+    std::vector<float> a((size_t)M * ld), w((size_t)N * ld), out((size_t)M * ld), ws(4096);
+    std::vector<unsigned short> wh((size_t)N * ld), wh_short((size_t)N * ld - 8);
+    auto& reg = alloc_registry();
+    const size_t reg0 = reg.size();
+    for (auto* v : {&a, &w, &out, &ws})
+      reg.push_back({(uintptr_t)v->data(), v->size() * sizeof(float)});
+    for (auto* v : {&wh, &wh_short})
+      reg.push_back({(uintptr_t)v->data(), v->size() * sizeof(unsigned short)});
+    struct Case { bool accept; GemmBatch b; };
+    std::vector<Case> cases;
+    auto base = [&]() {
+      GemmBatch b{};
+      b.count = 1;
+      b.d[0] = gd(a.data(), ld, 1, w.data(), ld, 1, out.data(), ld, M, N, K, EPI_RELU);
+      return b;
+    };
+    { Case k{true, base()}; cases.push_back(k); }                           // plain level
+    { Case k{true, base()}; k.b.d[0].Bh = wh.data(); cases.push_back(k); }  // full shadow
+    { Case k{false, base()}; k.b.d[0].Bh = wh_short.data(); cases.push_back(k); }   // short shadow
+    { Case k{false, base()}; k.b.d[0].Bh = wh.data() + 8; cases.push_back(k); }     // shadow past its end
+    { Case k{true, base()}; k.b.ws = ws.data(); k.b.ws_floats = 4096; cases.push_back(k); }
+    { Case k{false, base()}; k.b.ws = ws.data(); k.b.ws_floats = 4097; cases.push_back(k); }  // claims more
+    { Case k{false, base()}; k.b.ws = ws.data() + 4; k.b.ws_floats = 4096; cases.push_back(k); }
+    { Case k{false, base()}; k.b.ws_floats = 16; cases.push_back(k); }      // capacity, no buffer
+    { Case k{false, base()}; k.b.d[0].B = w.data() + 8; cases.push_back(k); }       // B past its end
+    {  // MN-contiguous operand read 4 wide from a 4-aligned start: M = 62 still spans 64
+      Case k{true, base()};
+      k.b.d[0] = gd(a.data(), ld, 0, w.data(), ld, 0, out.data(), ld, 62, 62, 64, EPI_STORE);
+      cases.push_back(k);
+      Case k2{false, base()};
+      k2.b.d[0] = gd(a.data() + ld * 64 - 64, ld, 0, w.data(), ld, 0, out.data(), ld, 62, 62, 64, EPI_STORE);
+      cases.push_back(k2);
+    }
+    int pass = 0;
+    for (const Case& k : cases) {
+      bool ok = true;
+      try {
+        for (int i = 0; i < k.b.count; ++i) validate(k.b.d[i]);
+        validate_batch(k.b);
+      } catch (const Error&) {
+        ok = false;
+      }
+      pass += ok == k.accept;
+    }
+    reg.resize(reg0);
+    *n_cases = (int32_t)cases.size();
+    *n_passed = pass;
   });
 }
 

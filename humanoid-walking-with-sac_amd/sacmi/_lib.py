@@ -98,9 +98,13 @@ _PROTOS = {
                            ctypes.c_int32, c_i32p],
     "sacmi_profile_sites": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
                             c_f64p, ctypes.c_int32, c_i32p],
+    "sacmi_selftest_span_checker": [c_i32p, c_i32p],
     "sacmi_profile_timeline": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
                                c_i32p, c_i32p, c_i32p, c_f64p, c_f64p, c_f64p, c_f64p, c_i32p,
                                c_f64p],
+    "sacmi_profile_timeline_dp": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
+                                  c_i32p, c_i32p, c_i32p, c_f64p, c_f64p, c_f64p, c_f64p, c_i32p,
+                                  c_f64p],
 }
 # kernel kinds of the launch timeline (TlKind, csrc/sacmi_internal.h)
 TL_KINDS = {1: "k_gemm", 2: "k_fwd", 3: "k_fwd16", 4: "k_axk16", 5: "k_dw_part", 6: "k_dw_part16",

@@ -26,6 +26,24 @@ from .replay import ReplayBuffer
 _OPT_NETS = ("policy", "q1", "q2")
 
 
+def _load_checkpoint_file(path):
+    """torch.load with the weights-only unpickler (nothing in the file is executed), plus the
+    numpy array / scalar reconstructors on its allowlist so that a replay buffer saved as
+    the reference's list of (state, action, reward, next_state, done) tuples of numpy
+    values (sac_imp.py:199 with PrioritizedReplayBuffer.buffer, replay_buffer.py:28) loads.
+    The uniform buffer's ``deque`` cannot be rebuilt by that unpickler at all: such a
+    checkpoint raises, and the buffer must be stored as a list (``list(buffer)``)."""
+    try:
+        import numpy._core.multiarray as _ma       # numpy >= 2
+    except ImportError:                            # pragma: no cover
+        import numpy.core.multiarray as _ma
+    allow = [_ma._reconstruct, _ma.scalar, np.ndarray, np.dtype]
+    allow += [type(np.dtype(t)) for t in (np.float64, np.float32, np.float16, np.int64,
+                                          np.int32, np.uint8, np.bool_)]
+    with torch.serialization.safe_globals(allow):
+        return torch.load(path, weights_only=True, map_location="cpu")
+
+
 def _device_index(device) -> int:
     if device is None:
         return 0
@@ -271,7 +289,7 @@ class SAC:
                     "alpha": self.alpha}, path)
 
     def load(self, path):
-        ck = torch.load(path, weights_only=True)
+        ck = _load_checkpoint_file(path)
         self._load_nets(ck)
         self.alpha = ck["alpha"]
 
@@ -307,7 +325,7 @@ class SAC:
         torch.save(ck, path)
 
     def load_checkpoint(self, path, load_replay_buffer=True):
-        ck = torch.load(path, weights_only=True)
+        ck = _load_checkpoint_file(path)
         self._load_nets(ck)
         for name in ("policy", "q1", "q2"):
             key = f"{name}_optimizer_state_dict"
@@ -319,7 +337,12 @@ class SAC:
         if "alpha_optimizer_state_dict" in ck and self.automatic_entropy_tuning:
             self.alpha_optimizer.load_state_dict(ck["alpha_optimizer_state_dict"])
         if load_replay_buffer and "replay_buffer" in ck:
+            # the reference REPLACES its buffer (sac_imp.py:229-230): restore only into an
+            # empty replay, after any transitions still staged on the host
             rb = ck["replay_buffer"]
+            self.replay_buffer._flush()
+            if len(self.replay_buffer):
+                raise ValueError("can only restore a buffer into an empty replay")
             if isinstance(rb, dict):
                 self._ctx.push(rb["state"].numpy(), rb["action"].numpy(), rb["reward"].numpy(),
                                rb["next_state"].numpy(), rb["done"].numpy())

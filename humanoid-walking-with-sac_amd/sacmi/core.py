@@ -328,13 +328,15 @@ class Context:
         return [(raw[32 * i:32 * i + 32].split(b"\0")[0].decode(), float(us[i]), float(fl[i]),
                  float(by[i])) for i in range(n.value)]
 
-    def profile_timeline(self, batch: int, n_updates: int):
+    def profile_timeline(self, batch: int, n_updates: int, data_parallel: bool = False):
         """Launch timeline of `n_updates` updates as step_many_async runs them (one graph,
         every kernel stamping its first-workgroup entry / last-workgroup exit on the GPU's
         100 MHz clock).  Returns (kernels, graph_us): kernels = [dict(site, site_idx,
         kernel, grid, start_us, end_us, flops, bytes)] in launch order (the site's algorithmic
         FLOPs / bytes on its first kernel); graph_us = HIP-event time of the
-        replay.  Advances the state by 2 * n_updates updates."""
+        replay.  Advances the state by 2 * n_updates updates.  ``data_parallel``: the
+        sequence step_dp replays (phases + RCCL all-reduces; every rank must call)."""
+        fn = "sacmi_profile_timeline_dp" if data_parallel else "sacmi_profile_timeline"
         mx = 64 * n_updates * 8
         names = ctypes.create_string_buffer(32 * mx)
         kind = np.zeros(mx, np.int32); grid = np.zeros(mx, np.int32); site = np.zeros(mx, np.int32)
@@ -342,7 +344,7 @@ class Context:
         fl = np.zeros(mx, np.float64); by = np.zeros(mx, np.float64)
         n = ctypes.c_int32()
         g = ctypes.c_double()
-        L.call("sacmi_profile_timeline", self._h, int(batch), int(n_updates), mx, names,
+        L.call(fn, self._h, int(batch), int(n_updates), mx, names,
                L.i32ptr(kind), L.i32ptr(grid), L.i32ptr(site), L.dptr(t0), L.dptr(t1), L.dptr(fl),
                L.dptr(by), ctypes.byref(n), ctypes.byref(g))
         raw = names.raw

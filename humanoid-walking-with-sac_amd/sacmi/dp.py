@@ -158,8 +158,24 @@ class CapturedDataParallelUpdates:
             self._graph(rem).replay()
 
 
+def _native_comm(ctx, rank: int, device, group=None) -> None:
+    """The library's own communicator over the same ranks (sacmi_allreduce_init): RCCL
+    unique id from rank 0, broadcast over the process group."""
+    from sacmi import Context
+    uid = torch.zeros(128, dtype=torch.uint8, device=device)
+    if rank == 0:
+        uid.copy_(torch.frombuffer(bytearray(Context.allreduce_unique_id()), dtype=torch.uint8))
+    dist.broadcast(uid, 0, group=group)
+    ctx.allreduce_init(bytes(uid.cpu().numpy().tobytes()), rank, dist.get_world_size(group))
+
+
 def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
-    """bench.py --gpus N under torch.distributed.run (one rank per GPU)."""
+    """bench.py --gpus N under torch.distributed.run (one rank per GPU): every rank owns a
+    replay shard of fill/N rows (uniform, or prioritized for --config 3 / BASELINE configs[3]:
+    each rank's PER sampler normalises over its own shard) and draws its own
+    batch from it with its own MT streams; the critic and actor gradients are all-reduced
+    over RCCL.  Timed as the median of windows of --steps updates (barrier + device sync on
+    both sides, max over ranks)."""
     import bench as B
     from sacmi import Config, Context
 
@@ -168,29 +184,33 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
     wl = B.workload(args)
     S, A, H = wl["S"], wl["A"], wl["H"]
+    per = wl["replay"] == "per"
     fill = args.fill // world                       # this rank's replay shard
     ctx = Context(Config(S, A, H, max_batch=args.batch, capacity=fill, seed=1000 + rank,
-                         n_hidden=wl["n_hidden"], compute_dtype=wl["dtype"]), local_rank)
+                         replay=wl["replay"], n_hidden=wl["n_hidden"],
+                         compute_dtype=wl["dtype"]), local_rank)
     B.init_agent(ctx, 0)                            # identical replicas
-    key = np.random.default_rng(77 + rank).integers(0, 2**32, size=624, dtype=np.uint32)
-    ctx.set_mt(0, key, 624)                         # per-shard sampling stream
+    for stream in (0, 1):                           # random.sample / numpy (PER) streams
+        key = np.random.default_rng(77 + 31 * stream + rank).integers(0, 2**32, size=624,
+                                                                      dtype=np.uint32)
+        ctx.set_mt(stream, key, 624)                # per-shard sampling streams
+    t_fill = time.perf_counter()
     chunk = 100_000
     for c0 in range(0, fill, chunk):
         ctx.push(*B.synth(min(chunk, fill - c0), 5000 + rank * 7919 + c0, S, A))
+    t_fill = time.perf_counter() - t_fill
     per_launch = max(1, min(args.updates_per_launch, 256))
+    sizes = B.graph_sizes(args.steps, per_launch)
     captured = None
     native = getattr(args, "dp_native", False)
+    # the library's communicator: the native driver's collectives, and the roofline's
+    # timeline of the data-parallel sequence (both paths)
+    want_roof = not getattr(args, "no_roofline", False)
+    if native or want_roof:
+        _native_comm(ctx, rank, device)
     if native:
-        # the library issues the all-reduces itself (sacmi_step_dp): RCCL unique id from
-        # rank 0, broadcast over the process group
-        uid = torch.zeros(128, dtype=torch.uint8, device=device)
-        if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(Context.allreduce_unique_id()), dtype=torch.uint8))
-        dist.broadcast(uid, 0)
-        ctx.allreduce_init(bytes(uid.cpu().numpy().tobytes()), rank, world)
-        for n in {min(per_launch, args.steps), args.steps % per_launch, args.warmup % per_launch}:
-            if n > 0:
-                ctx.step_dp(args.batch, n)        # build the graphs (the updates are warm-up)
+        for n in sizes:
+            ctx.step_dp(args.batch, n)            # build the graphs (the updates are warm-up)
         ctx.synchronize()
 
         def run(k):
@@ -202,8 +222,9 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     elif os.environ.get("SACMI_DP_GRAPH", "1") == "1":
         try:
             captured = CapturedDataParallelUpdates(ctx, device, args.batch)
-            captured.prepare(min(per_launch, args.steps), args.steps % per_launch,
-                             args.warmup % per_launch)
+            captured.prepare(*sizes)
+            for n in sizes:                       # every graph replayed once before timing
+                captured.run(n, per_launch)
         except Exception as e:                     # capture unsupported: eager driver
             if rank == 0:
                 print(f"sacmi.dp: graph capture failed ({e}); eager updates", flush=True)
@@ -218,44 +239,65 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
             for _ in range(k):
                 upd(args.batch)
             upd.flush()
-    elif captured is not None:
+    else:
         def run(k):
             captured.run(k, per_launch)
     run(args.warmup)
     torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    dt = torch.tensor([time.perf_counter() - t0], device=device)
-    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    dt = float(dt.item())
+
+    def window():
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(args.steps)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        dt = torch.tensor([time.perf_counter() - t0], device=device)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt.item())
+
+    dts = [window() for _ in range(args.windows)]
+    dt = float(np.median(dts))
     # replicas must have stayed identical: compare a parameter checksum across ranks
     w = torch.from_numpy(ctx.get_net("policy")["fc2.weight"]).to(device).double()
     chk = torch.stack([w.sum(), (w * w).sum()])
     allchk = [torch.zeros_like(chk) for _ in range(world)]
     dist.all_gather(allchk, chk)
     replicas_equal = all(bool(torch.equal(allchk[0], c)) for c in allchk)
+    peak = B.PEAK_BF16_MFMA_TFLOPS if wl["dtype"] == "bf16" else B.PEAK_FP32_MFMA_TFLOPS
+    roof = None
+    if want_roof:
+        # every rank replays the instrumented sequence (its graph holds the collectives)
+        roof = B.roofline_object(ctx, args, wl, peak, data_parallel=True)
+        torch.cuda.synchronize()
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        n_cpu = min(fill * world, 1_000_000)
+        cpu_rows = tuple(x[:n_cpu] for x in B.synth(n_cpu, 7, S, A))
+        cpu = B.cpu_baseline(cpu_rows, seconds=args.cpu_seconds, batch=args.batch, per=per,
+                             n_hidden=wl["n_hidden"])
+        cpu["sample"] += "; one rank's batch (the per-GPU work of one data-parallel iteration)"
     if rank == 0:
         iters = args.steps / dt
         value = world * iters
         flops = B.necessary_flops(S, A, H, args.batch, wl["n_hidden"])
-        peak = B.PEAK_BF16_MFMA_TFLOPS if wl["dtype"] == "bf16" else B.PEAK_FP32_MFMA_TFLOPS
         env = "Humanoid-v5" if args.config != 5 else "NAO-walk"
         out = {
             "metric": f"SAC gradient-steps/sec, {env} batch={args.batch} (obs {S}, act {A}, hidden {H})",
             "value": round(value, 2), "unit": f"grad-steps/s (batch-{args.batch} per GPU)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "windows": args.windows,
+            "window_ms_min_med_max": [round(1e3 * min(dts), 3), round(1e3 * dt, 3),
+                                      round(1e3 * max(dts), 3)],
             "ms_per_step": round(1e3 * dt / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": wl["dtype"], "data": "synthetic",
-            "config": {"workload": wl["workload"] + f"; {world} ranks: per-GPU replay shard + "
-                                   "RCCL gradient all-reduce over xGMI (uniform replay per shard)",
+            "config": {"workload": wl["workload"] + f"; {world} ranks: per-GPU replay shard of "
+                                   f"{fill} rows ({'prioritized' if per else 'uniform'} replay "
+                                   "per shard) + RCCL gradient all-reduce over xGMI",
                        "state_dim": S, "action_dim": A, "hidden": H, "n_hidden": wl["n_hidden"],
                        "global_batch": args.batch * world, "replay_fill": fill * world,
-                       "parallelism": f"dp{world}"},
+                       "replay": wl["replay"], "parallelism": f"dp{world}"},
             "iterations_per_s": round(iters, 2),
             "updates_per_launch": per_launch if (captured or native) else 1,
             "dp_graph": captured is not None or native,
@@ -263,7 +305,8 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
                          else "torch.distributed (RCCL) around sacmi phases",
             "mfma_util_step": round(flops * value / 1e12 / peak / world, 4),
             "replicas_bitwise_equal": replicas_equal,
-            "roofline": None, "cpu_baseline": None,
+            "roofline": roof, "cpu_baseline": cpu,
+            "fill_seconds": round(t_fill, 2),
         }
         emit(json.dumps(out))
     dist.barrier()

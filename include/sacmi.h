@@ -280,6 +280,23 @@ int sacmi_profile_timeline(sacmi_ctx* ctx, int32_t batch, int32_t n_updates, int
                            double* start_us, double* end_us, double* flops_out, double* bytes_out,
                            int32_t* n_kernels, double* graph_us);
 
+/* sacmi_profile_timeline over the data-parallel sequence sacmi_step_dp replays (phases +
+ * the two RCCL all-reduces of every update; needs sacmi_allreduce_init, and every rank of
+ * the communicator must make the same call, since the captured graph holds the
+ * collectives).  The all-reduces launch no stamping kernel: their time is the gap before
+ * the next kernel's start. */
+int sacmi_profile_timeline_dp(sacmi_ctx* ctx, int32_t batch, int32_t n_updates, int32_t max_kernels,
+                              char* names_out, int32_t* kind_out, int32_t* grid_out, int32_t* site_out,
+                              double* start_us, double* end_us, double* flops_out, double* bytes_out,
+                              int32_t* n_kernels, double* graph_us);
+
+/* Host-only self test of the launch validator every GEMM level passes before it is
+ * enqueued (operand spans against the registered device allocations, incl. the bf16
+ * weight shadows and the split-K workspace): runs a fixed set of accept / reject cases
+ * on host arrays; n_passed == n_cases when the validator decides each one correctly.
+ * Needs no device. */
+int sacmi_selftest_span_checker(int32_t* n_cases, int32_t* n_passed);
+
 #ifdef __cplusplus
 }
 #endif

@@ -113,3 +113,45 @@ def worker(rank, world, port, cfg, params, shards, idx, eps1, eps2, out_dir, ste
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **be.state())
     dist.barrier()
     dist.destroy_process_group()
+
+
+def per_shard_indices(prio, n, batch, key, steps, frame0=1):
+    """Per-rank prioritized sampling of a shard (replay_buffer.py:48-82 restated by
+    oracle/per.py): probabilities normalised over THIS shard only, uniforms from the rank's
+    own numpy MT stream, beta annealed by the rank's own frame counter."""
+    from oracle.per import beta_at, probs_from, sample_from_probs
+    from oracle.pyrandom import MT19937
+    mt = MT19937(np.asarray(key, np.uint32), 624)
+    out = []
+    for t in range(steps):
+        probs = probs_from(prio, n)
+        idx, w = sample_from_probs(probs, batch, mt, beta_at(frame0 + t))
+        out.append((idx, w))
+    return out
+
+
+def worker_per(rank, world, port, cfg, params, shards, prios, keys, eps1, eps2, out_dir, steps,
+               batch):
+    """A rank of the BASELINE configs[3] layout on CPU: its own prioritized replay shard,
+    its own sampler, the production DataParallelUpdate driver over gloo."""
+    import torch.distributed as dist
+    from sacmi.dp import DataParallelUpdate
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    be = OraclePhases(cfg, params, dtype=torch.float64)
+    upd = DataParallelUpdate(be)
+    rows = shards[rank]
+    draws = per_shard_indices(prios[rank], len(rows[2]), batch, keys[rank], steps)
+    for t in range(steps):
+        i = draws[t][0]
+        be.set_batch(*[x[i] for x in rows], eps1[t][rank], eps2[t][rank])
+        upd(len(i))
+    upd.flush()
+    st = be.state()
+    for t in range(steps):
+        st[f"idx{t}"] = draws[t][0]
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **st)
+    dist.barrier()
+    dist.destroy_process_group()

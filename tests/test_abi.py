@@ -66,3 +66,15 @@ def test_no_device_is_a_loud_error():
     from sacmi import Config, Context
     with pytest.raises(Exception):
         Context(Config(4, 2, 16, max_batch=8, capacity=64))
+
+
+def test_span_checker_rejects_undersized_workspace_and_shadows():
+    """The host-side launch validator (sacmi.hip validate / validate_batch) decides every
+    accept / reject case of its self test correctly: undersized bf16 weight shadows (Bh)
+    and split-K workspaces (ws), operands past their allocation, MN-contiguous 4-wide
+    reads.  Host-only: no device is touched."""
+    from sacmi import _lib as L
+    lib = L.load()
+    n, ok = ctypes.c_int32(), ctypes.c_int32()
+    assert lib.sacmi_selftest_span_checker(ctypes.byref(n), ctypes.byref(ok)) == 0
+    assert n.value >= 10 and ok.value == n.value, (ok.value, n.value)

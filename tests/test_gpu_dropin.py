@@ -115,23 +115,6 @@ def test_checkpoint_roundtrip(tmp_path):
     assert agent.update_parameters(64) == other.update_parameters(64)
 
 
-def test_loads_shipped_reference_checkpoint_shape():
-    """best_model.pt of the reference (H=256, S=376) has exactly this layout; build the
-    same layout from a fresh agent and load it back through SAC.load."""
-    from sac_imp import SAC
-    torch.manual_seed(0)
-    a = SAC(376, 17, hidden_dim=256, device="cuda", capacity=1000, max_batch=64)
-    sd = {f"{n}_state_dict": getattr(a, n).state_dict()
-          for n in ("policy", "q1", "q2", "q1_target", "q2_target")}
-    sd["alpha"] = torch.tensor([0.0868], requires_grad=True)
-    p = "/tmp/sacmi_bm.pt"
-    torch.save(sd, p)
-    b = SAC(376, 17, hidden_dim=256, device="cuda", capacity=1000, max_batch=64)
-    b.load(p)
-    assert abs(float(b.alpha) - 0.0868) < 1e-7
-    assert torch.equal(b.policy.state_dict()["fc1.weight"], a.policy.state_dict()["fc1.weight"])
-
-
 def test_standalone_replay_buffer_is_random_sample():
     from replay_buffer import ReplayBuffer
     rb = ReplayBuffer(capacity=500)
@@ -199,3 +182,90 @@ def test_select_action_graph_replays_track_state():
         mean, _ = agent.policy(torch.from_numpy(st).unsqueeze(0))
         ref = (torch.tanh(mean) * 0.4).numpy()[0]
     np.testing.assert_allclose(d2, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("tag", ["humanoid", "bipedal"])
+def test_loads_reference_checkpoint_fixture(tmp_path, tag):
+    """The reference's own best_model.pt layouts (tests/golden/ckpt_reference.npz, from the
+    shipped results/*/best_model.pt via a weights-only loader): the rebuilt dict, saved
+    with torch.save, loads through SAC.load (sac_imp.py:165-173); every device tensor is
+    the file's tensor bit for bit, alpha is the saved one, and the deterministic action of
+    the loaded policy equals the CPU forward of the same weights."""
+    import ckpt_fixture as cf
+    from sac_imp import SAC
+    from oracle.sac_step import _policy_forward
+    z, keys = cf.load_fixture()
+    d = keys[tag]["dims"]
+    ck = cf.rebuild(tag)
+    p = str(tmp_path / "best_model.pt")
+    torch.save(ck, p)
+    torch.manual_seed(1)
+    agent = SAC(d["S"], d["A"], hidden_dim=d["H"], device="cuda", capacity=1000, max_batch=64)
+    agent.load(p)
+    for n in cf.NETS:
+        live = agent._ctx.get_net(n)
+        for k, v in ck[f"{n}_state_dict"].items():
+            assert np.array_equal(live[k].reshape(v.shape), v.numpy()), (tag, n, k)
+            idx = z[f"{tag}.{n}.{k}.idx"]
+            assert np.array_equal(live[k].reshape(-1)[idx], z[f"{tag}.{n}.{k}.val"])
+    assert float(agent.alpha) == float(z[f"{tag}.alpha"][0])
+    st = np.random.default_rng(5).standard_normal((8, d["S"])).astype(np.float32)
+    got = agent.select_action(st, evaluate=True)
+    pol = {k: v.double() for k, v in ck["policy_state_dict"].items()}
+    with torch.no_grad():
+        mean, _ = _policy_forward(pol, torch.from_numpy(st).double())
+        want = (torch.tanh(mean) * 0.4).numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6)
+
+
+def test_checkpoint_restores_reference_list_buffer(tmp_path):
+    """The replay restore branch of load_checkpoint (sac_imp.py:229-230): a buffer saved as
+    the reference's list of (state, action, reward, next_state, done) tuples of numpy
+    values (PrioritizedReplayBuffer.buffer, replay_buffer.py:28) is restored in order,
+    bit for bit; restoring into a non-empty replay raises (the reference replaces)."""
+    rng = np.random.default_rng(8)
+    rows = [(rng.standard_normal(S), rng.uniform(-0.4, 0.4, A).astype(np.float32),
+             float(rng.standard_normal()), rng.standard_normal(S), bool(rng.random() < 0.2))
+            for _ in range(150)]
+    src = _agent()
+    p = str(tmp_path / "ck.pt")
+    src.save_checkpoint(p, episode=3, total_steps=150, replay_buffer=False)
+    ck = torch.load(p, weights_only=True)
+    ck["replay_buffer"] = rows
+    torch.save(ck, p)
+    dst = _agent()
+    assert dst.load_checkpoint(p) == (3, 150)
+    assert len(dst.replay_buffer) == 150
+    s, a, r, s2, d = dst.replay_buffer._rows_at(np.arange(150))
+    for i, (si, ai, ri, s2i, di) in enumerate(rows):
+        assert np.array_equal(s[i], si.astype(np.float32)) and np.array_equal(a[i], ai)
+        assert r[i] == np.float32(ri) and np.array_equal(s2[i], s2i.astype(np.float32))
+        assert bool(d[i]) == di
+    full = _agent()
+    _fill(full, 10)
+    with pytest.raises(ValueError, match="empty replay"):
+        full.load_checkpoint(p)
+
+
+def test_select_action_stochastic_vs_oracle():
+    """select_action(state, evaluate=False) (sac_imp.py:54-72 -> networks_model1.py:78-99)
+    with the Normal noise injected: the action equals the oracle's policy sample
+    tanh(mean + eps * std) * scale + bias on the same weights and eps within 1e-5."""
+    from oracle.sac_step import SacConfig, _policy_sample, init_params
+    cfg = SacConfig(376, 17, 512)
+    params = init_params(cfg, 17, bias_scale=0.05)
+    from sacmi import Config, Context
+    ctx = Context(Config(376, 17, 512, max_batch=256, capacity=1000), 0)
+    for n in ("policy", "q1", "q2", "q1_target", "q2_target"):
+        ctx.set_net(n, params[n])
+    rng = np.random.default_rng(18)
+    for n in (1, 7, 64, 200):      # env-rate (pinned zero-copy) and batched (copy) paths
+        st = (rng.standard_normal((n, 376)) * 0.5).astype(np.float32)
+        eps = rng.standard_normal((n, 17)).astype(np.float32)
+        got = ctx.act(st, deterministic=False, eps=eps)
+        pol = {k: torch.tensor(v, dtype=torch.float64) for k, v in params["policy"].items()}
+        with torch.no_grad():
+            want, _ = _policy_sample(pol, torch.from_numpy(st).double(),
+                                     torch.from_numpy(eps).double(), 0.4, 0.0)
+        np.testing.assert_allclose(got, want.numpy(), rtol=1e-5, atol=1e-6, err_msg=f"n={n}")
+    ctx.close()

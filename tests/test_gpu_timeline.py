@@ -50,3 +50,31 @@ def test_timeline_updates_equal_plain_updates():
         for k in pa:
             assert np.array_equal(pa[k], pb[k]), (n, k)
     assert np.array_equal(a.fetch_losses(6), b.fetch_losses(6))
+
+
+def test_timeline_of_the_data_parallel_sequence():
+    """sacmi_profile_timeline_dp over a 1-rank communicator: the phases' kernels are
+    stamped in order (plain dW levels + k_adam instead of the fused Adam levels), the
+    all-reduces leave gaps before the next phase, the model ends where sacmi_step_dp
+    leaves it, and bench.timeline_roofline accounts for the whole replay."""
+    import bench
+    from sacmi import Context
+    a, b = _ctx(), _ctx()
+    for c in (a, b):
+        c.allreduce_init(Context.allreduce_unique_id(), 0, 1)
+    ks, graph_us = a.profile_timeline(64, 3, data_parallel=True)
+    names = [k["site"] for k in ks]
+    assert not any(n.startswith("allreduce") for n in names)   # RCCL kernels do not stamp
+    assert sum(1 for k in ks if k["kernel"] == "k_adam") == 6   # critic + actor Adam x 3
+    starts = [k["start_us"] for k in ks]
+    assert starts == sorted(starts)
+    info = bench.timeline_roofline(a, 64, 3, data_parallel=True)
+    assert info["allreduce_us"] > 0 and info["gemm_flops"] > 0
+    assert abs(info["sum_us"] - info["graph_us"]) <= 0.25 * info["graph_us"], info
+    for _ in range(4):                                  # 2 profiles x (warm + measured) x 3
+        b.step_dp(64, 3)
+    b.synchronize()
+    for n in NETS:
+        pa, pb = a.get_net(n), b.get_net(n)
+        for k in pa:
+            assert np.array_equal(pa[k], pb[k]), (n, k)

@@ -153,3 +153,27 @@ def test_model2_key_layout():
     cfg2 = SacConfig(24, 4, 64)
     for net in ("policy", "q1"):
         assert [k for k, _l, _p in net_keys(net, 2)] == list(param_shapes(cfg2)[net])
+
+
+def test_reference_checkpoint_fixture_matches_dropin_layout():
+    """The reference's shipped best_model.pt files (Humanoid H=256 S=376 A=17, BipedalWalker
+    S=24 A=4; fixture from tools/make_ckpt_fixture.py, weights_only loader): key sets, file
+    order and shapes are exactly the drop-in networks' state_dict layout, and the rebuilt
+    dicts load strictly into them with the reference's values at every sampled position."""
+    import ckpt_fixture as cf
+    from sacmi.networks import GaussianPolicy, QNetwork
+    z, keys = cf.load_fixture()
+    for tag in ("humanoid", "bipedal"):
+        d = keys[tag]["dims"]
+        ck = cf.rebuild(tag)
+        mods = {"policy": GaussianPolicy(d["S"], d["A"], d["H"])}
+        for n in ("q1", "q2", "q1_target", "q2_target"):
+            mods[n] = QNetwork(d["S"], d["A"], d["H"])
+        for n, m in mods.items():
+            sd = ck[f"{n}_state_dict"]
+            assert list(sd) == list(m.state_dict()), (tag, n)
+            m.load_state_dict(sd)            # strict: same keys, same shapes
+            for k, v in m.state_dict().items():
+                p = f"{tag}.{n}.{k}"
+                assert np.array_equal(v.numpy().reshape(-1)[z[p + ".idx"]], z[p + ".val"]), p
+        assert torch.is_tensor(ck["alpha"]) and ck["alpha"].requires_grad
