@@ -78,6 +78,17 @@ __device__ __forceinline__ float buf_ld(rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void buf_st(rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)off, 0, 0);
 }
+// the store policy a level was launched with (GemmBatch::st_wt, wave-uniform): write-through
+// or plain
+__device__ __forceinline__ void buf_st_pol(rsrc_t r, uint32_t off, float v, bool wt) {
+  if (wt) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)off, 0, kStAux);
+  else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)off, 0, 0);
+}
+template <class T>
+__device__ __forceinline__ void st_pol(T* p, T v, bool wt) {
+  if (wt) st_wt<true>(p, v);
+  else *p = v;
+}
 
 // 16-byte buffer load.  The LLVM intrinsic is bound directly: on this toolchain (ROCm 7.2
 // hipcc) __builtin_amdgcn_raw_buffer_load_b128 lowers to a single buffer_load_dword.
@@ -97,8 +108,9 @@ __device__ __forceinline__ float4 buf_ld4(rsrc_t r, uint32_t off) {
 }
 __device__ void llvm_raw_buffer_store_v4f32(f4 v, rsrc_t r, int off, int soff, int aux)
     __asm("llvm.amdgcn.raw.ptr.buffer.store.v4f32");
+template <int AUX = 0>
 __device__ __forceinline__ void buf_st4(rsrc_t r, uint32_t off, f4 v) {
-  llvm_raw_buffer_store_v4f32(v, r, (int)off, 0, 0);
+  llvm_raw_buffer_store_v4f32(v, r, (int)off, 0, AUX);
 }
 
 // ---------------------------------------------------------------------------
@@ -761,6 +773,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
     n = d.rs_col;
     return rowsum && tid < TMW && m0 + row < d.M;
   };
+  const bool wt = SACMI_WT && batch.st_wt;   // output store policy of this level
   const bool pol = d.epi == EPI_ADAM_POLYAK;
   // byte span of this desc's output (tile rows, plus the rowsum column)
   const uint32_t span = (uint32_t)(((size_t)(d.M - 1) * d.ldc + (d.rs_col >= d.N ? d.rs_col + 1 : d.N)) * 4);
@@ -771,6 +784,8 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   const rsrc_t rV = make_rsrc(ADAM ? af.V + abase : d.C, ADAM ? span : 0);
   const rsrc_t rT = make_rsrc(ADAM && pol ? af.T + abase - af.t_base : d.C, ADAM && pol ? span : 0);
   const rsrc_t rG = make_rsrc(ADAM && af.G ? af.G + abase : d.C, ADAM && af.G ? span : 0);
+  const rsrc_t rCh = make_rsrc(!ADAM && d.Ch ? reinterpret_cast<const float*>(d.Ch) : d.C,
+                               !ADAM && d.Ch ? span / 2u : 0u);
   const rsrc_t rX = d.bias ? make_rsrc(d.bias, (uint32_t)(((size_t)(d.N - 1) * d.bias_ld + 1) * 4))
                   : d.epi == EPI_MASK ? make_rsrc(d.aux, (uint32_t)(((size_t)(d.M - 1) * d.ldaux + d.N) * 4))
                   : make_rsrc(d.C, 0);
@@ -849,19 +864,21 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
       }
       if constexpr (ADAM) {
         adam_elem(x0[s], x1[s], x2[s], v, omb1, af.beta2, omb2, af.eps, s_k);
-        if (af.G) buf_st(rG, o, v);
-        buf_st(rC, o, x0[s]); buf_st(rM, o, x1[s]); buf_st(rV, o, x2[s]);
-        if (af.Ph) af.Ph[abase + (o >> 2)] = bf16_bits(x0[s]);
+        if (af.G) buf_st_pol(rG, o, v, wt);
+        buf_st_pol(rC, o, x0[s], wt); buf_st_pol(rM, o, x1[s], wt); buf_st_pol(rV, o, x2[s], wt);
+        if (af.Ph) st_pol(af.Ph + abase + (o >> 2), bf16_bits(x0[s]), wt);
         if (pol) {
           const float tn = polyak(x3[s], x0[s], omtau, af.tau);
-          buf_st(rT, o, tn);
-          if (af.Th) af.Th[abase - af.t_base + (o >> 2)] = bf16_bits(tn);
+          buf_st_pol(rT, o, tn, wt);
+          if (af.Th) st_pol(af.Th + abase - af.t_base + (o >> 2), bf16_bits(tn), wt);
         }
       } else {
         if (d.bias) v += x0[s];
         if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
         else if (d.epi == EPI_MASK) v = x0[s] > 0.f ? v : 0.f;
-        buf_st(rC, o, v);
+        buf_st_pol(rC, o, v, wt);
+        // bf16 mode: the shadow a large-batch consumer stages from (zero-length range: none)
+        __builtin_amdgcn_raw_buffer_store_b16(bf16_bits(v), rCh, (int)(o >> 1), 0, 0);
       }
     }
     if constexpr (!ADAM) {
@@ -989,7 +1006,10 @@ struct FwdEpi {
           float v = acc[i][j][r];
           if (has_bias) v += bias_x[j];
           if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
-          if (row < M && col < N) d.C[(size_t)row * d.ldc + col] = v;
+          if (row < M && col < N) {
+            st_big(d.C + (size_t)row * d.ldc + col, v);
+            if (d.Ch) d.Ch[(size_t)row * d.ldc + col] = bf16_bits(v);
+          }
           if (has_dot) {
             // fc3 dot partial over the 32-column block (tiles j, j+1): 16 lanes per tile,
             // summed by DPP row rotations (VALU; the ds_bpermute butterfly it replaces
@@ -1132,7 +1152,7 @@ __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
   return __builtin_bit_cast(u2v, x);
 }
 
-template <int kFBN, bool BH = false>
+template <int kFBN, bool BH = false, bool AH = false>
 __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_FWD16);
   constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
@@ -1178,9 +1198,11 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
     offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
   }
   const int kq = 4 * (tid % TPR);
-  float4 ga[NA], gb[BH ? 1 : NB];
+  float4 ga[AH ? 1 : NA], gb[BH ? 1 : NB];
   uint2 gh[BH ? NB : 1];              // BH: B from its bf16 shadow, 4 k per 8 bytes
+  uint2 gah[AH ? NA : 1];             // AH: A from its bf16 shadow (the producer's rounding)
   const rsrc_t rBh = make_rsrc(BH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
+  const rsrc_t rAh = make_rsrc(AH ? reinterpret_cast<const float*>(d.Ah) : d.A, 0x7fffffffu);
   auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
     x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
     return x;
@@ -1193,8 +1215,13 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
   auto gload = [&](int k0) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
+    if constexpr (AH) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+      for (int i = 0; i < NA; ++i) gah[i] = zkh(buf_ld2(rAh, offA[i] / 2u + ko / 2u), k);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+    }
     if constexpr (BH) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) gh[i] = zkh(buf_ld2(rBh, offB[i] / 2u + ko / 2u), k);
@@ -1205,7 +1232,10 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(ga[i]);
+    for (int i = 0; i < NA; ++i) {
+      if constexpr (AH) *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = u2v{gah[i].x, gah[i].y};
+      else *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(ga[i]);
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (BH) *reinterpret_cast<u2v*>(&sB[buf][tid / TPR + RPP * i][kq]) = u2v{gh[i].x, gh[i].y};
@@ -1402,10 +1432,10 @@ __global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn + j * 16 + (lane & 15);
-        if (row < M && col < N) w[(int64_t)row * nc + col] = acc[i][j][r];
+        if (row < M && col < N) st_big(w + (int64_t)row * nc + col, acc[i][j][r]);
       }
     }
-  if (want_rs && tid < kDBM && m0 + tid < M) w[(int64_t)(m0 + tid) * nc + N] = rs;
+  if (want_rs && tid < kDBM && m0 + tid < M) st_big(w + (int64_t)(m0 + tid) * nc + N, rs);
 }
 
 // bf16 mode, bf16 in LDS: k_dw_part with the operands rounded once at staging and kept
@@ -1425,6 +1455,9 @@ __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
       (__attribute__((address_space(3))) s4t*)(p));
 }
 
+// XH: every desc's X operand (B) is staged from its bf16 shadow (the producer's rounding,
+// identical bits; half the staged bytes)
+template <bool XH = false>
 __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_PART16);
   constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
@@ -1466,7 +1499,9 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
   const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
   const bool want_rs = d.rs_col >= 0 && n0 == 0;
-  float4 ga[8], gb[8];
+  const rsrc_t rBh = make_rsrc(XH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
+  float4 ga[8], gb[XH ? 1 : 8];
+  uint2 gbh[XH ? 8 : 1];
   float rs4[4] = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](int k0) {
 #pragma unroll
@@ -1475,21 +1510,30 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
       const bool kin = k < ke;
       const uint32_t kk = (uint32_t)(kin ? k : 0);   // row 0 always exists (a split may start past K)
       float4 x = buf_ld4(rA, (kk * (uint32_t)d.lda + (uint32_t)ma) * 4u);
-      float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
       const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
       // columns past M / N (and rows past this split's K range) contribute zero
       x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
       x.z = kin && m0 + c4 + 2 < M ? x.z * f : 0.f; x.w = kin && m0 + c4 + 3 < M ? x.w * f : 0.f;
-      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
-      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
-      ga[i] = x; gb[i] = y;
+      ga[i] = x;
+      if constexpr (XH) {
+        uint2 h = buf_ld2(rBh, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 2u);
+        h.x = (kin && n0 + c4 < N ? h.x & 0xffffu : 0u) | (kin && n0 + c4 + 1 < N ? h.x & 0xffff0000u : 0u);
+        h.y = (kin && n0 + c4 + 2 < N ? h.y & 0xffffu : 0u) | (kin && n0 + c4 + 3 < N ? h.y & 0xffff0000u : 0u);
+        gbh[i] = h;
+      } else {
+        float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
+        y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+        y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+        gb[i] = y;
+      }
     }
   };
   auto swrite = [&](int buf, bool fresh) {   // fresh: a slab not staged before
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       *reinterpret_cast<u2v*>(&sA[buf][kr0 + 8 * i][c4]) = pack_bf16x4(ga[i]);
-      *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+      if constexpr (XH) *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = u2v{gbh[i].x, gbh[i].y};
+      else *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
     }
     if (want_rs && fresh) {
 #pragma clang fp contract(off)
@@ -1554,7 +1598,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wn + j * 16 + (lane & 15);
-        if (row < M && col < N) w[(int64_t)row * nc + col] = acc[i][j][r];
+        if (row < M && col < N) st_big(w + (int64_t)row * nc + col, acc[i][j][r]);
       }
     }
   if (want_rs) {
@@ -1565,7 +1609,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
 #pragma clang fp contract(off)
       float v = s_rs[0][tid];
       for (int g = 1; g < 8; ++g) v += s_rs[g][tid];
-      w[(int64_t)(m0 + tid) * nc + N] = v;
+      st_big(w + (int64_t)(m0 + tid) * nc + N, v);
     }
   }
 }
@@ -1744,7 +1788,7 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
         float v = acc[i][j][r];
         if (AX) v *= cf;
         v = hm[i][j][r] > 0.f ? v : 0.f;
-        if (row < M && col < N) d.C[(size_t)row * d.ldc + col] = v;
+        if (row < M && col < N) st_big(d.C + (size_t)row * d.ldc + col, v);
       }
     }
   if constexpr (AX) rows_loss<kXBM>(batch.rows, m0, writer, s_l);
@@ -1805,17 +1849,17 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
       if (adam) {
         float pp = d.C[o], mm = af.M[abase + o], vv = af.V[abase + o];
         adam_elem(pp, mm, vv, v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
-        if (af.G) af.G[abase + o] = v;
-        d.C[o] = pp; af.M[abase + o] = mm; af.V[abase + o] = vv;
-        if (af.Ph) af.Ph[abase + o] = bf16_bits(pp);
+        if (af.G) st_big(af.G + abase + o, v);
+        st_big(d.C + o, pp); st_big(af.M + abase + o, mm); st_big(af.V + abase + o, vv);
+        if (af.Ph) st_big(af.Ph + abase + o, bf16_bits(pp));
         if (pol) {
           float* tp = af.T + abase - af.t_base + o;
           const float tn = polyak(*tp, pp, omtau, af.tau);
-          *tp = tn;
-          if (af.Th) af.Th[abase - af.t_base + o] = bf16_bits(tn);
+          st_big(tp, tn);
+          if (af.Th) st_big(af.Th + abase - af.t_base + o, bf16_bits(tn));
         }
       } else {
-        d.C[o] = v;
+        st_big(d.C + o, v);
       }
     }
     off += n_el;
@@ -1915,6 +1959,20 @@ static bool all_bh(const GemmBatch& b) {
     if (!b.d[i].Bh) return false;
   return true;
 }
+// every desc's A operand has an activation shadow (k_fwd16)
+static bool all_ah(const GemmBatch& b) {
+  if (!SACMI_BF16_SHADOW) return false;
+  for (int i = 0; i < b.count; ++i)
+    if (!b.d[i].Ah) return false;
+  return true;
+}
+// every desc of a weight-gradient level has its X operand's shadow, 8-byte aligned rows
+static bool all_xh(const GemmBatch& b) {
+  if (!SACMI_BF16_SHADOW) return false;
+  for (int i = 0; i < b.count; ++i)
+    if (!b.d[i].Bh || ((uintptr_t)b.d[i].Bh & 7) || (b.d[i].ldb & 3)) return false;
+  return true;
+}
 
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
@@ -1925,7 +1983,10 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     if (ns > 0) {
       const int ride = b.ride.kind == 2 ? b.ride.nblocks : 0;
       const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
-      if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16, dim3(grid), dim3(256), 0, s, b, ns, stride);
+      if (b.bf16 && SACMI_DW_LDS16 && all_xh(b))
+        hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
+      else if (b.bf16 && SACMI_DW_LDS16)
+        hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
@@ -1953,8 +2014,10 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
   if (fwd_big && fwd_big_ok(b)) {
     const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
-    const bool bh = b.bf16 && all_bh(b);
-    if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    const bool bh = b.bf16 && all_bh(b), ah = b.bf16 && all_ah(b);
+    if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh && ah) hipLaunchKernelGGL((k_fwd16<128, true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    else if (b.bf16 && SACMI_FWD_LDS16 && bh && ah) hipLaunchKernelGGL((k_fwd16<64, true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    else if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16 && bh) hipLaunchKernelGGL((k_fwd16<64, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16) hipLaunchKernelGGL((k_fwd16<64>), dim3(b.total_tiles), dim3(256), 0, s, b);
@@ -1967,10 +2030,17 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   b = b0;
   const int extra = b.ride.kind ? b.ride.nblocks : 0;
   int maxk = 0, n_adam = 0;
+  int64_t outs = 0;
   for (int i = 0; i < b.count; ++i) {
     maxk = b.d[i].K > maxk ? b.d[i].K : maxk;
     n_adam += b.d[i].epi >= EPI_ADAM;
+    outs += (int64_t)b.d[i].M * b.d[i].N;
   }
+  // write-through epilogue stores where they shorten the boundary to the next level: the
+  // Adam levels (15-30 MB of optimizer state) and the batch-256-class levels (<= 4 MB of
+  // outputs: config 2 124.9 -> 121.3 us per update); the batch-4096 activation levels keep
+  // plain stores (config 3: 762 -> 774 us with every level write-through)
+  b.st_wt = (n_adam > 0 || outs <= (1 << 20)) ? 1 : 0;
   // (Level::add guarantees a level is all-Adam or all-plain)
   int axk = 0;
   for (int i = 0; i < b.count; ++i) axk = b.d[i].axk > axk ? b.d[i].axk : axk;
@@ -2109,6 +2179,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       const float x = a.deterministic ? mean : mean + eps * sd;
       const float y = tanhf(x);
       a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
+      if (a.act_h) a.act_h[(size_t)m * a.ldact + j] = bf16_bits(y * a.scale + a.bias);
       if (a.act_host) a.act_host[(size_t)m * A + j] = y * a.scale + a.bias;
       const float dx = x - mean;
       lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
@@ -2282,7 +2353,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
       for (int r = 0; r < 4; ++r) {
         const int rr = (lane >> 4) * 4 + r, n = n0 + t * 16 + (lane & 15);
         if (m0 + rr < d.M && n < a.H)
-          a.dhp2[(size_t)(m0 + rr) * a.H + n] = mk[t][r] > 0.f ? acc[t][r] : 0.f;
+          st_wt(a.dhp2 + (size_t)(m0 + rr) * a.H + n, mk[t][r] > 0.f ? acc[t][r] : 0.f);
       }
   }
 }
@@ -2322,6 +2393,11 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
   __syncthreads();
   const float om_b1 = 1.f - a.beta1, om_b2 = 1.f - a.beta2, omtau = 1.f - a.tau;
   const int64_t total4 = s_prefix[a.nseg];
+  // parameter / moment / target arenas: one descriptor each (offsets < 2 GiB: the arenas
+  // hold at most a few million floats)
+  const rsrc_t rP = make_rsrc(a.p, 0x7fffffffu), rM = make_rsrc(a.m, 0x7fffffffu),
+               rV = make_rsrc(a.v, 0x7fffffffu),
+               rT = make_rsrc(a.tgt ? a.tgt : a.p, 0x7fffffffu);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total4;
        e += (int64_t)gridDim.x * blockDim.x) {
     int sg = 0;
@@ -2338,12 +2414,12 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     adam_elem(p.y, m.y, v.y, g.y, om_b1, a.beta2, om_b2, a.eps, k);
     adam_elem(p.z, m.z, v.z, g.z, om_b1, a.beta2, om_b2, a.eps, k);
     adam_elem(p.w, m.w, v.w, g.w, om_b1, a.beta2, om_b2, a.eps, k);
-    *reinterpret_cast<float4*>(a.p + i) = p;
-    *reinterpret_cast<float4*>(a.m + i) = m;
-    *reinterpret_cast<float4*>(a.v + i) = v;
+    buf_st4<kStAux>(rP, (uint32_t)i * 4u, f4{p.x, p.y, p.z, p.w});
+    buf_st4<kStAux>(rM, (uint32_t)i * 4u, f4{m.x, m.y, m.z, m.w});
+    buf_st4<kStAux>(rV, (uint32_t)i * 4u, f4{v.x, v.y, v.z, v.w});
     if (a.ph) {
-      a.ph[i] = bf16_bits(p.x); a.ph[i + 1] = bf16_bits(p.y);
-      a.ph[i + 2] = bf16_bits(p.z); a.ph[i + 3] = bf16_bits(p.w);
+      st_wt(a.ph + i, bf16_bits(p.x)); st_wt(a.ph + i + 1, bf16_bits(p.y));
+      st_wt(a.ph + i + 2, bf16_bits(p.z)); st_wt(a.ph + i + 3, bf16_bits(p.w));
     }
     if (a.tgt) {
       float4* tp = reinterpret_cast<float4*>(a.tgt + (i - a.tgt_base));
@@ -2352,10 +2428,11 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
       t.y = polyak(t.y, p.y, omtau, a.tau);
       t.z = polyak(t.z, p.z, omtau, a.tau);
       t.w = polyak(t.w, p.w, omtau, a.tau);
-      *tp = t;
+      buf_st4<kStAux>(rT, (uint32_t)(i - a.tgt_base) * 4u, f4{t.x, t.y, t.z, t.w});
       if (a.tgth) {
         unsigned short* th = a.tgth + (i - a.tgt_base);
-        th[0] = bf16_bits(t.x); th[1] = bf16_bits(t.y); th[2] = bf16_bits(t.z); th[3] = bf16_bits(t.w);
+        st_wt(th, bf16_bits(t.x)); st_wt(th + 1, bf16_bits(t.y));
+        st_wt(th + 2, bf16_bits(t.z)); st_wt(th + 3, bf16_bits(t.w));
       }
     }
   }

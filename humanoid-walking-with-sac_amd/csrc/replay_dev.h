@@ -206,23 +206,37 @@ __device__ __forceinline__ void gather_row(const GatherArgs& a, int b, int lane,
   float* xq = a.xq + (size_t)b * a.ldx;
   float* xt = a.x2 + (size_t)b * a.ldx;
   float* xa = a.x2 + (size_t)(a.B + b) * a.ldx;
+  // write-through stores (sacmi_internal.h st_wt): the minibatch leaves no dirty L2 lines
   if ((a.S & 3) == 0) {
+    const uint32_t oq = (uint32_t)((size_t)b * a.ldx) * 4u, ot = oq;
+    const uint32_t oa = (uint32_t)((size_t)(a.B + b) * a.ldx) * 4u;
     for (int q = lane; q < a.S / 4; q += nl) {
       const float4 v = reinterpret_cast<const float4*>(so)[q];
-      reinterpret_cast<float4*>(xq)[q] = v;
-      reinterpret_cast<float4*>(xa)[q] = v;
-      reinterpret_cast<float4*>(xt)[q] = reinterpret_cast<const float4*>(s2)[q];
+      const float4 w = reinterpret_cast<const float4*>(s2)[q];
+      st_wt4(a.xq, oq + 16u * q, v);
+      st_wt4(a.x2, oa + 16u * q, v);
+      st_wt4(a.x2, ot + 16u * q, w);
     }
   } else {
     for (int q = lane; q < a.S; q += nl) {
       const float v = so[q];
-      xq[q] = v; xa[q] = v; xt[q] = s2[q];
+      st_wt(xq + q, v); st_wt(xa + q, v); st_wt(xt + q, s2[q]);
     }
   }
-  for (int j = lane; j < a.A; j += nl) xq[a.S + 1 + j] = ac[j];
+  for (int j = lane; j < a.A; j += nl) st_wt(xq + a.S + 1 + j, ac[j]);
+  if (a.xqh) {   // bf16 mode: the shadows the large-batch level kernels stage from
+    unsigned short* hq = a.xqh + (size_t)b * a.ldx;
+    unsigned short* ht = a.x2h + (size_t)b * a.ldx;
+    unsigned short* ha = a.x2h + (size_t)(a.B + b) * a.ldx;
+    for (int q = lane; q < a.S; q += nl) {
+      const unsigned short v = bf16_bits_dev(so[q]);
+      hq[q] = v; ha[q] = v; ht[q] = bf16_bits_dev(s2[q]);
+    }
+    for (int j = lane; j < a.A; j += nl) hq[a.S + 1 + j] = bf16_bits_dev(ac[j]);
+  }
   if (lane == 0) {
-    a.r[b] = a.rew[slot];
-    a.d[b] = a.done[slot];
+    st_wt(a.r + b, a.rew[slot]);
+    st_wt(a.d + b, a.done[slot]);
   }
 }
 

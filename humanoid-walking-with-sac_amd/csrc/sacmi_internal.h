@@ -46,6 +46,44 @@ inline void launch_check(const char* what) {
 // (kernel, device) to the largest request seen.
 void ensure_dyn_lds(const void* kernel, size_t bytes);
 
+// Output stores of the update's kernels are write-through (sc1): a kernel then leaves no
+// dirty L2 lines behind, and the end-of-kernel L2 writeback — serialised at the boundary
+// to the next dependent kernel, ~B / 6 TB/s for B dirty bytes — has nothing to do (the
+// Adam levels write 15-30 MB of optimizer state per update).  SACMI_WT 0: plain stores.
+#ifndef SACMI_WT
+#define SACMI_WT 1
+#endif
+constexpr int kStAux = SACMI_WT ? 16 : 0;   // raw buffer store cache-policy bits (16 = sc1)
+// The large-batch bf16 level kernels (k_fwd16 / k_axk16 / k_dw_part16 / k_dw_fin) store
+// tens of MB per launch as one dword per lane: there write-through measured slower (config
+// 5: 415 -> 447 us per update, the kernel bodies grew more than the boundaries shrank), so
+// they keep plain stores (SACMI_WT_BIG 0).
+#ifndef SACMI_WT_BIG
+#define SACMI_WT_BIG 0
+#endif
+template <bool WT = (SACMI_WT != 0), class T>
+__device__ __forceinline__ void st_wt(T* p, T v) {
+  if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <class T>
+__device__ __forceinline__ void st_big(T* p, T v) { st_wt<SACMI_WT_BIG != 0>(p, v); }
+
+// 16-byte write-through store at a wave-uniform base + per-lane byte offset (raw buffer
+// store; the LLVM intrinsic is bound directly, see kernels.hip buf_ld4)
+typedef float wt_f4 __attribute__((ext_vector_type(4)));
+__device__ void llvm_raw_buffer_store_wt_v4f32(wt_f4 v, __amdgpu_buffer_rsrc_t r, int off, int soff,
+                                               int aux) __asm("llvm.amdgcn.raw.ptr.buffer.store.v4f32");
+__device__ __forceinline__ void st_wt4(float* base, uint32_t byte_off, float4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  llvm_raw_buffer_store_wt_v4f32(wt_f4{v.x, v.y, v.z, v.w}, r, (int)byte_off, 0, kStAux);
+}
+
+// fp32 -> bf16 bits, round to nearest even (what every bf16 operand stage computes)
+__device__ __forceinline__ unsigned short bf16_bits_dev(float x) {
+  return __builtin_bit_cast(unsigned short, (__bf16)x);
+}
+
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
@@ -122,8 +160,11 @@ enum Epi { EPI_STORE = 0, EPI_RELU = 1, EPI_MASK = 2,
 struct GemmDesc {
   const float* A;
   const float* B;
-  const unsigned short* Bh;   // bf16 mode: B's bf16 shadow (a parameter operand) or null
+  const unsigned short* Bh;   // bf16 mode: B's bf16 shadow (a parameter operand, or the
+                              // activation operand X of a weight gradient) or null
+  const unsigned short* Ah;   // bf16 mode: A's bf16 shadow (an activation operand) or null
   float* C;
+  unsigned short* Ch;         // bf16 mode: the producer also stores bf16(C) here (null: no)
   const float* aux;
   int M, N, K;
   int lda, ldb, ldc, ldaux;
@@ -192,6 +233,8 @@ struct GatherArgs {
   float* xq; float* x2; int ldx;   // xq [B, ldx], x2 [2B, ldx]
   float* r; float* d;
   int by_slot;            // 1: idx are ring slots (PER), 0: deque positions
+  unsigned short* xqh;    // bf16 mode: shadows of xq / x2 (same layout), or null
+  unsigned short* x2h;
   tl_word* tl;
 };
 struct MtSampleArgs {
@@ -253,6 +296,7 @@ struct GemmBatch {
   float* ws;           // bf16 deep-K weight-gradient levels: split-K partial workspace
   int64_t ws_floats;   //   (capacity; launch_gemm falls back when a level needs more)
   tl_word* tl;         // launch timeline slots of this level (kTlPerSite), or null
+  int st_wt;           // k_gemm epilogue stores write-through (set by launch_gemm)
 };
 
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked
@@ -275,6 +319,7 @@ struct HeadSampleArgs {
   float* logp_part;      // [grid][2] or null: per workgroup, sum of logp over its rows
   int split_row;         //   < split_row (slot 0) and >= split_row (slot 1)
   float* act_host;       // or null: the actions also stored [row][A] to host-mapped memory
+  unsigned short* act_h; // or null: bf16 shadow of `act` (same layout)
   tl_word* tl;
 };
 

@@ -851,3 +851,37 @@ def test_dp_config4_per_shard_world1_matches_fused():
         _assert_same_agent(n, f, "native dp")
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_hidden", [2, 3])
+def test_bf16_activation_shadows_bit_identical(n_hidden):
+    """bf16 mode, batch >= 2048: the LDS-staged level kernels read the activation operands
+    from bf16 shadows written by their producers (gather, heads, forward epilogues) instead
+    of rounding the fp32 values at staging (opt-in: SACMI_ACT_SHADOW=1).  Same rounding, so
+    the updates must be bit for bit those of a context without shadows, at the config-5 shapes."""
+    from sacmi import _lib as L
+    cfg = SacConfig(661, 23, 512, n_hidden=n_hidden)
+    params = init_params(cfg, 131, bias_scale=0.02)
+    rows = synthetic_rows(cfg, 9000, 132, state_scale=0.3)
+    key = (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32)
+    out = []
+    for shadow in (True, False):
+        if shadow:
+            os.environ["SACMI_ACT_SHADOW"] = "1"
+        try:
+            ctx = make_ctx(cfg, max_batch=4096, capacity=9000, seed=7, compute_dtype="bf16")
+        finally:
+            os.environ.pop("SACMI_ACT_SHADOW", None)
+        load_params(ctx, params)
+        ctx.push(*rows)
+        ctx.set_mt(0, key, 624)
+        ctx.step_many_async(4096, 2)       # ride-along sampling / gather into both batch sets
+        ctx.step(4096)
+        out.append(({n: ctx.get_net(n) for n in NETS}, ctx.fetch_losses(3),
+                    ctx.get_scalar(L.S_LOG_ALPHA)))
+        ctx.close()
+    (a, la, xa), (b, lb, xb) = out
+    for n in NETS:
+        for k in a[n]:
+            assert np.array_equal(a[n][k], b[n][k]), (n, k)
+    assert np.array_equal(la, lb) and xa == xb
