@@ -717,6 +717,10 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   __shared__ float rsum[MG * KSPLIT * TM];
   __shared__ AdamScalars s_k;
   __shared__ float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
+  // dL/da partials (axk-1 levels of one 32-row wave group): the tile's outputs [TMW][TN+1]
+  // and its fc1 action weights [TN][32]
+  constexpr bool PA = AXK == 1 && MG == 1;
+  __shared__ float s_pa[PA ? TMW * (TN + 1) + TN * 32 : 1];
   const int bid = blockIdx.x;
   if (bid >= batch.total_tiles) {   // ride-along workgroups (next update's replay work)
     if constexpr (MG * KSPLIT == 16) {   // the host attaches rides to 1024-thread configs
@@ -784,8 +788,6 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   const rsrc_t rV = make_rsrc(ADAM ? af.V + abase : d.C, ADAM ? span : 0);
   const rsrc_t rT = make_rsrc(ADAM && pol ? af.T + abase - af.t_base : d.C, ADAM && pol ? span : 0);
   const rsrc_t rG = make_rsrc(ADAM && af.G ? af.G + abase : d.C, ADAM && af.G ? span : 0);
-  const rsrc_t rCh = make_rsrc(!ADAM && d.Ch ? reinterpret_cast<const float*>(d.Ch) : d.C,
-                               !ADAM && d.Ch ? span / 2u : 0u);
   const rsrc_t rX = d.bias ? make_rsrc(d.bias, (uint32_t)(((size_t)(d.N - 1) * d.bias_ld + 1) * 4))
                   : d.epi == EPI_MASK ? make_rsrc(d.aux, (uint32_t)(((size_t)(d.M - 1) * d.ldaux + d.N) * 4))
                   : make_rsrc(d.C, 0);
@@ -799,11 +801,26 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   // zero-length range where the level has none: no branch, so nothing waits for it early)
   // (loaded in pre(), after the operand burst; staged to LDS after the MFMAs)
   float dotw_x = 0.f, dotb_x = 0.f;
+  // dL/da partials (GemmDesc::pa_out, axk-1 levels only): this tile's columns of the fc1
+  // action weights, loaded under the MFMAs, staged [TN][32] in LDS after them
+  constexpr int PW = PA ? (TN * 32 + NTH - 1) / NTH : 1;
+  float paw_x[PW];
+  const bool has_pa = PA && d.pa_out != nullptr;
   auto pre = [&]() {
     // axk 1: the row prologue's loads.  Issued here, behind the operand burst, and
     // consumed after the MFMAs: anything in flight at the k-loop header is waited for by
     // the back-edge's conservative vmcnt on the first iteration.
     if constexpr (AXK == 1) rows_load<TMW, NTH>(batch.rows, d, m0, rows_x);   // unconditional
+    if constexpr (PA) {   // zero-length range where the level has no partials
+      const rsrc_t rPW = make_rsrc(has_pa ? d.pa_w : d.C,
+                                   has_pa ? (uint32_t)(((size_t)(d.N - 1) * d.pa_ld + d.pa_A) * 4) : 0u);
+#pragma unroll
+      for (int q = 0; q < PW; ++q) {
+        const int e = tid + q * NTH, c = e / 32, j = e % 32;
+        const bool okw = e < TN * 32 && j < d.pa_A && n0 + c < d.N;
+        paw_x[q] = buf_ld(rPW, okw ? (uint32_t)((n0 + c) * d.pa_ld + j) * 4u : 0xfffffff0u);
+      }
+    }
     {   // buffer ops with a zero-length range where the level has no dots: no branch
       const rsrc_t rDW = make_rsrc(d.dotp ? d.dotw : d.C, d.dotp ? (uint32_t)(d.N + 1) * 4u : 0u);
       const int nn = n0 + (tid < TN ? tid : 0);
@@ -835,6 +852,13 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
                      : (SACMI_PIPE_DW && G == 1 && ADAM && MG == 2) ? 2 : 0;
   gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
+  if constexpr (PA) {
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      const int e = tid + q * NTH;
+      if (e < TN * 32) s_pa[TMW * (TN + 1) + e] = paw_x[q];
+    }
+  }
   if constexpr (AXK == 1) {
     // the row prologue, after the MFMAs: its loads went out first and have long landed
     if (d.axk == 1)
@@ -877,8 +901,6 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
         if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
         else if (d.epi == EPI_MASK) v = x0[s] > 0.f ? v : 0.f;
         buf_st_pol(rC, o, v, wt);
-        // bf16 mode: the shadow a large-batch consumer stages from (zero-length range: none)
-        __builtin_amdgcn_raw_buffer_store_b16(bf16_bits(v), rCh, (int)(o >> 1), 0, 0);
       }
     }
     if constexpr (!ADAM) {
@@ -892,10 +914,35 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
           d.dotp[(size_t)(m0 + row) * d.dotp_ld + (n0 + col) / 32] = n0 + col == 0 ? c + dotb_x : c;
       }
     }
+    if constexpr (PA) {   // every tile element, 0 outside the output
+      if (s < EPT) s_pa[row * (TN + 1) + col] = ok ? v : 0.f;
+    }
   }
   if (threadIdx.x < 64) SACMI_STAMP(33);
   if constexpr (AXK == 1) {
     if (d.axk == 1) rows_loss<TMW>(batch.rows, m0, p == 0 && n0 == 0, s_l);
+  }
+  if constexpr (PA) {
+    if (has_pa) {
+      // dL/da partial of every row over each 32-column block of this tile:
+      // pa_out[((pa_base + (n0 + 32 sb) / 32) * M + row) * A + j] = sum_c C[row][c] w[c][j]
+      // (outside the tile's rows / columns the stored value is the masked 0 or never read)
+      const float* s_t = s_pa;
+      const float* s_w = s_pa + TMW * (TN + 1);
+      __syncthreads();
+      const int A = d.pa_A;
+      constexpr int NSB = TN / 32;
+      for (int e = tid; e < TMW * NSB * A; e += NTH) {
+        const int row = e / (NSB * A), rem = e - row * (NSB * A), sb = rem / A, j = rem - sb * A;
+        const float* tr = s_t + row * (TN + 1) + sb * 32;
+        const float* wc = s_w + sb * 32 * 32 + j;
+        float acc = 0.f;
+#pragma unroll 8
+        for (int c = 0; c < 32; ++c) acc = fmaf(tr[c], wc[c * 32], acc);
+        if (m0 + row < d.M)
+          st_wt(d.pa_out + ((size_t)(d.pa_base + n0 / 32 + sb) * d.M + m0 + row) * A + j, acc);
+      }
+    }
   }
   if (batch.has_adam && bid == 0) {
     __syncthreads();
@@ -1006,10 +1053,7 @@ struct FwdEpi {
           float v = acc[i][j][r];
           if (has_bias) v += bias_x[j];
           if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
-          if (row < M && col < N) {
-            st_big(d.C + (size_t)row * d.ldc + col, v);
-            if (d.Ch) d.Ch[(size_t)row * d.ldc + col] = bf16_bits(v);
-          }
+          if (row < M && col < N) st_big(d.C + (size_t)row * d.ldc + col, v);
           if (has_dot) {
             // fc3 dot partial over the 32-column block (tiles j, j+1): 16 lanes per tile,
             // summed by DPP row rotations (VALU; the ds_bpermute butterfly it replaces
@@ -1152,7 +1196,7 @@ __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
   return __builtin_bit_cast(u2v, x);
 }
 
-template <int kFBN, bool BH = false, bool AH = false>
+template <int kFBN, bool BH = false>
 __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_FWD16);
   constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
@@ -1198,11 +1242,9 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
     offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
   }
   const int kq = 4 * (tid % TPR);
-  float4 ga[AH ? 1 : NA], gb[BH ? 1 : NB];
+  float4 ga[NA], gb[BH ? 1 : NB];
   uint2 gh[BH ? NB : 1];              // BH: B from its bf16 shadow, 4 k per 8 bytes
-  uint2 gah[AH ? NA : 1];             // AH: A from its bf16 shadow (the producer's rounding)
   const rsrc_t rBh = make_rsrc(BH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
-  const rsrc_t rAh = make_rsrc(AH ? reinterpret_cast<const float*>(d.Ah) : d.A, 0x7fffffffu);
   auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
     x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
     return x;
@@ -1215,13 +1257,8 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
   auto gload = [&](int k0) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
-    if constexpr (AH) {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) gah[i] = zkh(buf_ld2(rAh, offA[i] / 2u + ko / 2u), k);
-    } else {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
-    }
+    for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
     if constexpr (BH) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) gh[i] = zkh(buf_ld2(rBh, offB[i] / 2u + ko / 2u), k);
@@ -1232,10 +1269,7 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      if constexpr (AH) *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = u2v{gah[i].x, gah[i].y};
-      else *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(ga[i]);
-    }
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(ga[i]);
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (BH) *reinterpret_cast<u2v*>(&sB[buf][tid / TPR + RPP * i][kq]) = u2v{gh[i].x, gh[i].y};
@@ -1455,9 +1489,6 @@ __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
       (__attribute__((address_space(3))) s4t*)(p));
 }
 
-// XH: every desc's X operand (B) is staged from its bf16 shadow (the producer's rounding,
-// identical bits; half the staged bytes)
-template <bool XH = false>
 __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_PART16);
   constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
@@ -1499,9 +1530,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
   const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
   const bool want_rs = d.rs_col >= 0 && n0 == 0;
-  const rsrc_t rBh = make_rsrc(XH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
-  float4 ga[8], gb[XH ? 1 : 8];
-  uint2 gbh[XH ? 8 : 1];
+  float4 ga[8], gb[8];
   float rs4[4] = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](int k0) {
 #pragma unroll
@@ -1515,25 +1544,17 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
       x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
       x.z = kin && m0 + c4 + 2 < M ? x.z * f : 0.f; x.w = kin && m0 + c4 + 3 < M ? x.w * f : 0.f;
       ga[i] = x;
-      if constexpr (XH) {
-        uint2 h = buf_ld2(rBh, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 2u);
-        h.x = (kin && n0 + c4 < N ? h.x & 0xffffu : 0u) | (kin && n0 + c4 + 1 < N ? h.x & 0xffff0000u : 0u);
-        h.y = (kin && n0 + c4 + 2 < N ? h.y & 0xffffu : 0u) | (kin && n0 + c4 + 3 < N ? h.y & 0xffff0000u : 0u);
-        gbh[i] = h;
-      } else {
-        float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
-        y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
-        y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
-        gb[i] = y;
-      }
+      float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
+      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+      gb[i] = y;
     }
   };
   auto swrite = [&](int buf, bool fresh) {   // fresh: a slab not staged before
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       *reinterpret_cast<u2v*>(&sA[buf][kr0 + 8 * i][c4]) = pack_bf16x4(ga[i]);
-      if constexpr (XH) *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = u2v{gbh[i].x, gbh[i].y};
-      else *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+      *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
     }
     if (want_rs && fresh) {
 #pragma clang fp contract(off)
@@ -1959,20 +1980,6 @@ static bool all_bh(const GemmBatch& b) {
     if (!b.d[i].Bh) return false;
   return true;
 }
-// every desc's A operand has an activation shadow (k_fwd16)
-static bool all_ah(const GemmBatch& b) {
-  if (!SACMI_BF16_SHADOW) return false;
-  for (int i = 0; i < b.count; ++i)
-    if (!b.d[i].Ah) return false;
-  return true;
-}
-// every desc of a weight-gradient level has its X operand's shadow, 8-byte aligned rows
-static bool all_xh(const GemmBatch& b) {
-  if (!SACMI_BF16_SHADOW) return false;
-  for (int i = 0; i < b.count; ++i)
-    if (!b.d[i].Bh || ((uintptr_t)b.d[i].Bh & 7) || (b.d[i].ldb & 3)) return false;
-  return true;
-}
 
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
@@ -1983,10 +1990,7 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     if (ns > 0) {
       const int ride = b.ride.kind == 2 ? b.ride.nblocks : 0;
       const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
-      if (b.bf16 && SACMI_DW_LDS16 && all_xh(b))
-        hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
-      else if (b.bf16 && SACMI_DW_LDS16)
-        hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
+      if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
@@ -2001,6 +2005,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (SACMI_AXK_LDS16) {
     const int ax = axk16_ok(b);
     if (ax >= 0) {
+      for (int i = 0; i < b.count; ++i)   // k_axk16 computes no dL/da partials
+        if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a k_axk16 level"};
       const bool bh = all_bh(b);
       if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
       else if (ax) hipLaunchKernelGGL((k_axk16<true, false>), dim3(b.total_tiles), dim3(256), 0, s, b);
@@ -2014,10 +2020,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
   if (fwd_big && fwd_big_ok(b)) {
     const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
-    const bool bh = b.bf16 && all_bh(b), ah = b.bf16 && all_ah(b);
-    if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh && ah) hipLaunchKernelGGL((k_fwd16<128, true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-    else if (b.bf16 && SACMI_FWD_LDS16 && bh && ah) hipLaunchKernelGGL((k_fwd16<64, true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-    else if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    const bool bh = b.bf16 && all_bh(b);
+    if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16 && bh) hipLaunchKernelGGL((k_fwd16<64, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16) hipLaunchKernelGGL((k_fwd16<64>), dim3(b.total_tiles), dim3(256), 0, s, b);
@@ -2062,6 +2066,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     // or as several smaller ones (4- / 2-way): then one workgroup's LDS reduction and
     // epilogue overlap another's operand loads and MFMAs.  Rides attach to 1024 threads.
     const int g = assign_tiles<64, 64>(b) + extra;
+    for (int i = 0; i < b.count; ++i)   // the two-wave-group tiles compute no dL/da partials
+      if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a 64-row tile level"};
     if (n_adam) {
       if (SACMI_DW_KS == 4 && !extra) launch_k<32, 64, 4, 1, 2, true, 0>(b, g, s);
       else launch_k<32, 64, 8, 1, 2, true, 0>(b, g, s);
@@ -2179,7 +2185,6 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       const float x = a.deterministic ? mean : mean + eps * sd;
       const float y = tanhf(x);
       a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
-      if (a.act_h) a.act_h[(size_t)m * a.ldact + j] = bf16_bits(y * a.scale + a.bias);
       if (a.act_host) a.act_host[(size_t)m * A + j] = y * a.scale + a.bias;
       const float dx = x - mean;
       lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
@@ -2365,6 +2370,112 @@ void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream
   else
     hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 16>), dim3(grid), dim3(1024), 0, s, d, a);
   HIP_LAUNCH_CHECK();
+}
+
+// The sample backward + dhp2 tail of the actor pass (sac_imp.py:116-125 backward through
+// GaussianPolicy.sample, networks_model1.py:78-99) from the dL/da partials the dha1 level's
+// epilogue wrote (GemmDesc::pa_out): one workgroup per (16-row block, 64-column slab of
+// dhp2).  dL/da = the n_pa column-block partials summed in fixed order; then the same
+// per-element algebra as k_gemm_sample_bwd; the slab-0 workgroups store dhead (the heads'
+// weight-gradient operand); dhp2 = (dhead Whead) * [hp2 > 0] for the slab.  Every
+// workgroup of a row block recomputes the row block's dhead (a few hundred FMAs).
+constexpr int kTailRows = 8, kTailCols = 64, kTailMaxPa = 64;
+__global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_pa, SampleBwdArgs a) {
+  const TlMark tl_mark(a.tl, TL_SAMPLE_TAIL);
+  __shared__ float s_dh[kTailRows][64 + 1];       // dhead rows, zero beyond 2A
+  __shared__ float s_w[64][kTailCols + 1];        // Whead[k][slab columns], k < 2A
+  const int A = a.A, B = a.B, K2 = 2 * A;
+  const int m0 = blockIdx.x * kTailRows, c0 = blockIdx.y * kTailCols;
+  const int tid = threadIdx.x;
+  // every global load of the kernel goes out first (one round trip): thread e < 8A owns
+  // (row e / A, action e % A) — its partials, cache and noise; all threads stage a share
+  // of the Whead slab and of the ReLU mask.  Buffer loads at out-of-range offsets return
+  // 0 without an access, so no load sits behind a guard.
+  const int prow = tid / A, pj = tid - prow * A, pm = m0 + prow;
+  const bool own = tid < kTailRows * A && pm < B;
+  const rsrc_t rP = make_rsrc(pa, (uint32_t)((size_t)n_pa * B * A * 4));
+  const uint32_t pstride = (uint32_t)B * (uint32_t)A * 4u, po = (uint32_t)((own ? pm : 0) * A + pj) * 4u;
+  float t[kTailMaxPa];
+#pragma unroll
+  for (int q = 0; q < kTailMaxPa; ++q)
+    t[q] = buf_ld(rP, own && q < n_pa ? po + (uint32_t)q * pstride : 0xfffffff0u);
+  const rsrc_t rC = make_rsrc(a.cache, (uint32_t)((size_t)B * 3 * A * 4));
+  const rsrc_t rE = make_rsrc(a.eps, (uint32_t)((size_t)B * A * 4));
+  const uint32_t co = own ? (uint32_t)(pm * 3 * A + pj) * 4u : 0xfffffff0u;
+  const float omy2 = buf_ld(rC, co), ls_raw = buf_ld(rC, co + (uint32_t)A * 4u),
+              y = buf_ld(rC, co + (uint32_t)(2 * A) * 4u);
+  const float eps = buf_ld(rE, own ? (uint32_t)(pm * A + pj) * 4u : 0xfffffff0u);
+  constexpr int WPT = 64 * kTailCols / 256;       // Whead slab elements per thread (k < 64)
+  const rsrc_t rW = make_rsrc(a.Wh, (uint32_t)(((size_t)(K2 - 1) * a.ldw + a.H) * 4));
+  float wv[WPT];
+#pragma unroll
+  for (int q = 0; q < WPT; ++q) {
+    const int e = tid + q * 256, k = e / kTailCols, col = c0 + (e - k * kTailCols);
+    wv[q] = buf_ld(rW, k < K2 && col < a.H ? (uint32_t)(k * a.ldw + col) * 4u : 0xfffffff0u);
+  }
+  // the dhp2 thread layout: row tid / 32 (8 rows), 2 consecutive slab columns
+  const int row = tid >> 5, cq = (tid & 31) * 2, m = m0 + row;
+  const rsrc_t rH = make_rsrc(a.hp2, (uint32_t)(((size_t)(B - 1) * a.ldh + a.H) * 4));
+  float mk[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int col = c0 + cq + u;
+    mk[u] = buf_ld(rH, m < B && col < a.H ? (uint32_t)(m * a.ldh + col) * 4u : 0xfffffff0u);
+  }
+  for (int e = tid; e < kTailRows * 65; e += 256) (&s_dh[0][0])[e] = 0.f;
+#pragma unroll
+  for (int q = 0; q < WPT; ++q) {
+    const int e = tid + q * 256, k = e / kTailCols;
+    s_w[k][e - k * kTailCols] = wv[q];
+  }
+  __syncthreads();
+  if (own) {
+    float ga = 0.f;                                 // fixed order over the column blocks
+#pragma unroll
+    for (int q = 0; q < kTailMaxPa; ++q)
+      if (q < n_pa) ga += t[q];
+    const float glogp = a.sc->alpha / (float)B;
+    const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
+    const float sd = expf(ls);
+    const float u = a.scale * omy2 + 1e-6f;
+    const float G = a.scale * ga + glogp * (2.f * a.scale * y / u);
+    const float dx = G * omy2;
+    float dls = dx * eps * sd - glogp;
+    if (!(ls_raw >= -20.f && ls_raw <= 2.f)) dls = 0.f;
+    if (blockIdx.y == 0) {
+      a.dhead[(size_t)pm * a.lddh + pj] = dx;
+      a.dhead[(size_t)pm * a.lddh + A + pj] = dls;
+    }
+    s_dh[prow][pj] = dx;
+    s_dh[prow][A + pj] = dls;
+  }
+  __syncthreads();
+  float acc[2] = {0.f, 0.f};
+  for (int k = 0; k < K2; ++k) {
+    const float hk = s_dh[row][k];
+    acc[0] = fmaf(hk, s_w[k][cq], acc[0]);
+    acc[1] = fmaf(hk, s_w[k][cq + 1], acc[1]);
+  }
+  if (m < B) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int col = c0 + cq + u;
+      if (col < a.H) st_wt(a.dhp2 + (size_t)m * a.H + col, mk[u] > 0.f ? acc[u] : 0.f);
+    }
+  }
+}
+
+void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, hipStream_t s) {
+  if (2 * a.A > 64 || kTailRows * a.A > 256 || n_pa > kTailMaxPa)
+    throw Error{SACMI_EVALUE, "sample backward tail: unsupported action_dim / hidden_dim"};
+  const dim3 grid((a.B + kTailRows - 1) / kTailRows, (a.H + kTailCols - 1) / kTailCols);
+  hipLaunchKernelGGL(k_sample_bwd_tail, grid, dim3(256), 0, s, pa, n_pa, a);
+  HIP_LAUNCH_CHECK();
+}
+
+bool gemm_level_on_axk16(const GemmBatch& b0) {
+  GemmBatch b = b0;
+  return SACMI_AXK_LDS16 && axk16_ok(b) >= 0;
 }
 
 // ---------------------------------------------------------------------------

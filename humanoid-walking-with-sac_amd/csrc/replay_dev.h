@@ -224,16 +224,6 @@ __device__ __forceinline__ void gather_row(const GatherArgs& a, int b, int lane,
     }
   }
   for (int j = lane; j < a.A; j += nl) st_wt(xq + a.S + 1 + j, ac[j]);
-  if (a.xqh) {   // bf16 mode: the shadows the large-batch level kernels stage from
-    unsigned short* hq = a.xqh + (size_t)b * a.ldx;
-    unsigned short* ht = a.x2h + (size_t)b * a.ldx;
-    unsigned short* ha = a.x2h + (size_t)(a.B + b) * a.ldx;
-    for (int q = lane; q < a.S; q += nl) {
-      const unsigned short v = bf16_bits_dev(so[q]);
-      hq[q] = v; ha[q] = v; ht[q] = bf16_bits_dev(s2[q]);
-    }
-    for (int j = lane; j < a.A; j += nl) hq[a.S + 1 + j] = bf16_bits_dev(ac[j]);
-  }
   if (lane == 0) {
     st_wt(a.r + b, a.rew[slot]);
     st_wt(a.d + b, a.done[slot]);

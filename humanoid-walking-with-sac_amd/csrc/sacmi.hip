@@ -113,15 +113,11 @@ struct sacmi_ctx {
   // side (B rows x [q1 | q2], each Hd wide with the bias-1 column at H): critic on (s, a),
   // target critics on (s2, a'), updated critics on (s, a~)
   sacmi::DevBuf<float> hp[3], hq[3], hqt[3], hqa[3];
-  // bf16 mode (batch >= 2048 class): bf16 shadows of the activation operands the LDS-staged
-  // level kernels read (same layout, written by the producers next to the fp32 values:
-  // identical bits to rounding at staging, half the staged bytes)
-  bool act_shadows = false;
-  sacmi::DevBuf<unsigned short> xqh, x2h, xqbh, x2bh, hph[3], hqh[3], hqth[3], hqah[3];
   // backward: critic dh per hidden layer ([nh-1] = the on-the-fly head-layer rows u,
   // stored for the weight gradient), actor-pass critic dh (layers 0..nh-2), policy dh
   sacmi::DevBuf<float> dq, dhead, dhc[3], dha[3], dhp[3];
   sacmi::DevBuf<float> dotp;       // fc3 dot partials [6 slots][B][nparts]
+  sacmi::DevBuf<float> pa;         // dL/da partials [2 * nparts][B][A] (L9 epilogue -> tail)
   sacmi::DevBuf<float> dw_ws;      // bf16 deep-K weight-gradient split-K partials
   int nparts = 0;
   sacmi::DevBuf<float> lpart_c, lpart_a, ring, lp_part;
@@ -302,6 +298,7 @@ static void alloc_all(sacmi_ctx* c) {
   // split-K dW partials (kernels.hip; bf16 only: the fp32 levels measured slower split)
   if (c->bf16 && Bm >= 2048) c->dw_ws.alloc((size_t)16 * c->total);
   c->dotp.alloc((size_t)6 * Bm * c->nparts);
+  c->pa.alloc((size_t)2 * c->nparts * Bm * A);
   c->dhead.alloc((size_t)Bm * c->lddh);
   const int nrb = (Bm + 31) / 32;    // row blocks of the L5 / L9 tiling (loss partials)
   c->lpart_c.alloc((size_t)nrb * 2); c->lpart_a.alloc(nrb);
@@ -319,43 +316,7 @@ static void alloc_all(sacmi_ctx* c) {
       launch_set_column(b->p, Bm, 2 * c->Hd, c->Hd + H, 1.f, s);
     }
   }
-  // opt-in (SACMI_ACT_SHADOW=1): measured slower at config 5 (408 -> 435 us per update: the
-  // LDS-staged levels are bound by their load latency per slab, not by the staged bytes, and
-  // the producers pay the extra stores) — kept for the LDS-DMA staging it enables
-  const char* ash = std::getenv("SACMI_ACT_SHADOW");
-  if (c->bf16 && Bm >= 2048 && ash && ash[0] == '1') {
-    c->act_shadows = true;
-    // every shadow starts as the bf16 image of its (initialised) fp32 buffer: the constant
-    // bias columns and the zero pads are never written again
-    auto mk = [&](DevBuf<unsigned short>& h, const DevBuf<float>& f) {
-      h.alloc(f.n);
-      launch_to_bf16(h.p, f.p, (int64_t)f.n, s);
-    };
-    mk(c->xqh, c->xq); mk(c->x2h, c->x2); mk(c->xqbh, c->xqb); mk(c->x2bh, c->x2b);
-    for (int l = 0; l < nh; ++l) {
-      mk(c->hph[l], c->hp[l]); mk(c->hqh[l], c->hq[l]); mk(c->hqth[l], c->hqt[l]);
-      mk(c->hqah[l], c->hqa[l]);
-    }
-  }
   CHECK_HIP(hipStreamSynchronize(s));
-}
-
-// the bf16 shadow of an activation buffer element (null when the buffer has none)
-static unsigned short* act_shadow(sacmi_ctx* c, const float* p) {
-  if (!c->act_shadows || !p) return nullptr;
-  auto in = [&](const DevBuf<float>& f, DevBuf<unsigned short>& h) -> unsigned short* {
-    if (f.p && h.p && p >= f.p && p < f.p + f.n) return h.p + (p - f.p);
-    return nullptr;
-  };
-  unsigned short* r = nullptr;
-  if ((r = in(c->xq, c->xqh)) || (r = in(c->x2, c->x2h)) || (r = in(c->xqb, c->xqbh)) ||
-      (r = in(c->x2b, c->x2bh)))
-    return r;
-  for (int l = 0; l < c->nh; ++l)
-    if ((r = in(c->hp[l], c->hph[l])) || (r = in(c->hq[l], c->hqh[l])) ||
-        (r = in(c->hqt[l], c->hqth[l])) || (r = in(c->hqa[l], c->hqah[l])))
-      return r;
-  return nullptr;
 }
 
 static void upload_scalars(sacmi_ctx* c, const DevScalars& h) {
@@ -510,14 +471,6 @@ static void validate(const GemmDesc& d) {
 static void validate_batch(const GemmBatch& b) {
   for (int i = 0; i < b.count; ++i) {
     const GemmDesc& d = b.d[i];
-    if (d.Ah) {   // k_fwd16 stages a K-contiguous A from its shadow, 8 bytes (4 k) per load
-      REQUIRE(d.a_kc && ((uintptr_t)d.Ah & 7) == 0 && (d.lda & 3) == 0, SACMI_ESTATE, "Ah misaligned");
-      check_span(d.Ah, (int64_t)(d.M - 1) * d.lda + ((int64_t)(d.K - 1) / 4) * 4 + 3, "Ah (bf16 shadow)", 2);
-    }
-    if (d.Ch) {   // every producer kernel writes bf16(C) at C's element positions
-      REQUIRE(d.epi < EPI_ADAM, SACMI_ESTATE, "an Adam level has no output shadow");
-      check_span(d.Ch, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "Ch (bf16 shadow)", 2);
-    }
     if (!d.Bh) continue;
     REQUIRE(((uintptr_t)d.Bh & 7) == 0, SACMI_ESTATE, "Bh misaligned");
     const int64_t klast = ((int64_t)(d.K - 1) / 4) * 4 + 3;
@@ -551,7 +504,10 @@ struct Level {
 
 static double level_flops(const GemmBatch& b) {
   double f = 0;
-  for (int i = 0; i < b.count; ++i) f += 2.0 * b.d[i].M * (double)b.d[i].N * b.d[i].K;
+  for (int i = 0; i < b.count; ++i) {
+    f += 2.0 * b.d[i].M * (double)b.d[i].N * b.d[i].K;
+    if (b.d[i].pa_out) f += 2.0 * b.d[i].M * (double)b.d[i].N * b.d[i].pa_A;   // dL/da partials
+  }
   return f;
 }
 
@@ -569,6 +525,7 @@ static double level_bytes(const GemmBatch& b) {
     } else {
       n += out + (d.epi == EPI_MASK ? out : 0) + (d.bias ? d.N : 0);
     }
+    if (d.pa_out) n += (double)d.N * d.pa_A + (double)d.M * ((d.N + 31) / 32) * d.pa_A;
   }
   return 4.0 * n;
 }
@@ -619,13 +576,10 @@ static PerArgs per_args(sacmi_ctx* c, int k, int gen_u) {
 // reads its rows.
 struct BatchBufs {
   int32_t* idx32; int64_t* idx64; float* xq; float* x2; float* r; float* d;
-  unsigned short* xqh; unsigned short* x2h;   // bf16 shadows of xq / x2 (or null)
 };
 static BatchBufs batch_bufs(sacmi_ctx* c, int parity) {
-  if (parity == 0) return BatchBufs{c->idx32.p, c->idx64.p, c->xq.p, c->x2.p, c->r.p, c->d.p,
-                                    c->xqh.p, c->x2h.p};
-  return BatchBufs{c->idx32b.p, c->idx64b.p, c->xqb.p, c->x2b.p, c->rb.p, c->db.p, c->xqbh.p,
-                   c->x2bh.p};
+  if (parity == 0) return BatchBufs{c->idx32.p, c->idx64.p, c->xq.p, c->x2.p, c->r.p, c->d.p};
+  return BatchBufs{c->idx32b.p, c->idx64b.p, c->xqb.p, c->x2b.p, c->rb.p, c->db.p};
 }
 
 static int sample_setsize(int k) {   // random.py:486-488
@@ -648,7 +602,6 @@ static GatherArgs gather_args(sacmi_ctx* c, int B, const BatchBufs& bb, bool per
   g.sc = c->sc.p; g.S = c->S; g.A = c->A; g.B = B; g.xq = bb.xq; g.x2 = bb.x2; g.ldx = c->Kx;
   g.r = bb.r; g.d = bb.d;
   g.by_slot = per ? 1 : 0;
-  g.xqh = bb.xqh; g.x2h = bb.x2h;
   return g;
 }
 
@@ -687,16 +640,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     if (!c->Ph.p || !b) return nullptr;
     if (b >= c->P.p && b < c->P.p + c->P.n) return c->Ph.p + (b - c->P.p);
     if (b >= c->T.p && b < c->T.p + c->T.n) return c->Th.p + (b - c->T.p);
-    return act_shadow(c, b);          // the X operand of a weight gradient
+    return nullptr;
   };
   auto run = [&](Level& lv, const std::string& name) {
     lv.b.bf16 = c->bf16 ? 1 : 0;
-    for (int i = 0; i < lv.b.count; ++i) {
-      GemmDesc& g = lv.b.d[i];
-      g.Bh = shadow(g.B);
-      g.Ah = g.a_kc ? act_shadow(c, g.A) : nullptr;    // forward activations
-      g.Ch = act_shadow(c, g.C);                        // producers keep the shadow current
-    }
+    for (int i = 0; i < lv.b.count; ++i) lv.b.d[i].Bh = shadow(lv.b.d[i].B);
     lv.b.ws = c->dw_ws.p;
     lv.b.ws_floats = (int64_t)c->dw_ws.n;
     validate_batch(lv.b);
@@ -756,7 +704,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
     hs.logp_part = c->lp_part.p; hs.split_row = B;    // sums of log pi(a~|s) for dL/dlog_alpha
-    hs.act_h = act_shadow(c, hs.act);
     if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) {
       hs.tl = c->tl_cur;
       launch_heads_sample(hs, s);
@@ -907,6 +854,24 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
         rf.target_entropy = (float)(-A);
       }
     }
+    // (decided on the complete level: launch_gemm picks the kernel from it)
+    // 2 hidden layers: the dL/da GEMM (over both critics' dha1, K = 2H) folds into L9's
+    // epilogue as per-32-column partials, and L10 shrinks to the sample-backward tail —
+    // except where the level runs on k_axk16 (bf16, batch-4096 class), which keeps L10
+    l9.b.bf16 = c->bf16 ? 1 : 0;
+    // (batch <= 1024: the standalone L10 runs on B / 16 workgroups, too few to stream dha1;
+    // at batch 4096 it fills the chip and the fold measured slower: config 3 L9 55 -> 71 us)
+    const bool fold_dlda = nh == 2 && B <= 1024 && !std::getenv("SACMI_NO_DLDA_FOLD") &&
+                           !gemm_level_on_axk16(l9.b);
+    if (fold_dlda) {
+      for (int i = 0; i < 2; ++i) {
+        GemmDesc& g = l9.b.d[i];
+        g.pa_w = W(q[i][0]) + S + 1; g.pa_ld = Kx; g.pa_A = A; g.pa_base = i * c->nparts;
+        g.pa_out = c->pa.p;
+        check_span(g.pa_w, (int64_t)(H - 1) * Kx + A - 1, "pa_w");
+        check_span(g.pa_out, ((int64_t)(g.pa_base + c->nparts) * B) * A - 1, "pa_out");
+      }
+    }
     run(l9, "gemm_L9_act_dh1");
     for (int l = L - 1; l >= 1; --l) {
       Level lv;
@@ -927,7 +892,12 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     sb.Wh = W(c->p_head); sb.ldw = Hd; sb.H = H; sb.hp2 = hpa(L); sb.ldh = Hd; sb.dhp2 = c->dhp[L].p;
     check_span(sb.dhp2, (int64_t)B * H - 1, "dhp2");
     check_span(sb.Wh, (int64_t)(2 * A - 1) * Hd + H - 1, "Whead");
-    if (mark(c, "gemm_L10_dlda_sample_bwd_dhp2", 2.0 * B * A * (2.0 * H) + 2.0 * B * (2.0 * A) * H)) {
+    if (fold_dlda) {
+      if (mark(c, "sample_bwd_tail_dhp2", 2.0 * B * (2.0 * A) * H)) {
+        sb.tl = c->tl_cur;
+        launch_sample_bwd_tail(c->pa.p, 2 * c->nparts, sb, s);
+      }
+    } else if (mark(c, "gemm_L10_dlda_sample_bwd_dhp2", 2.0 * B * A * (2.0 * H) + 2.0 * B * (2.0 * A) * H)) {
       sb.tl = c->tl_cur;
       launch_gemm_sample_bwd(da, sb, s);
     }
@@ -1259,7 +1229,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
                     &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->xqb, &c->x2b, &c->rb,
                     &c->db, &c->eps,
-                    &c->cache, &c->logp, &c->dq, &c->dotp, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
+                    &c->cache, &c->logp, &c->dq, &c->dotp, &c->pa, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
                     &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr, &c->per_probs,
                     &c->per_chunk, &c->per_w, &c->per_val})
       b->release();
@@ -1268,9 +1238,6 @@ int sacmi_destroy(sacmi_ctx* c) {
         b->release();
     c->sc.release(); c->mt.release(); c->idx32.release(); c->idx64.release();
     c->Ph.release(); c->Th.release();
-    for (auto* h : {&c->xqh, &c->x2h, &c->xqbh, &c->x2bh}) h->release();
-    for (int l = 0; l < 3; ++l)
-      for (auto* h : {&c->hph[l], &c->hqh[l], &c->hqth[l], &c->hqah[l]}) h->release();
     c->idx32b.release(); c->idx64b.release();
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
     c->per_u.release(); c->per_uin.release(); c->per_owner.release(); c->per_bad.release();

@@ -79,11 +79,6 @@ __device__ __forceinline__ void st_wt4(float* base, uint32_t byte_off, float4 v)
   llvm_raw_buffer_store_wt_v4f32(wt_f4{v.x, v.y, v.z, v.w}, r, (int)byte_off, 0, kStAux);
 }
 
-// fp32 -> bf16 bits, round to nearest even (what every bf16 operand stage computes)
-__device__ __forceinline__ unsigned short bf16_bits_dev(float x) {
-  return __builtin_bit_cast(unsigned short, (__bf16)x);
-}
-
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
@@ -97,7 +92,7 @@ typedef unsigned long long tl_word;
 enum TlKind : int {
   TL_GEMM = 1, TL_FWD, TL_FWD16, TL_AXK16, TL_DW_PART, TL_DW_PART16, TL_DW_FIN, TL_HEADS,
   TL_SAMPLE_BWD, TL_MT_SAMPLE, TL_GATHER, TL_PER_F1, TL_PER_F2, TL_PER_F2B, TL_PER_F3,
-  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_KINDS
+  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_KINDS
 };
 constexpr int kTlWords = 4;          // words per kernel launch
 constexpr int kTlPerSite = 8;        // kernel launches one launch site may make
@@ -160,11 +155,8 @@ enum Epi { EPI_STORE = 0, EPI_RELU = 1, EPI_MASK = 2,
 struct GemmDesc {
   const float* A;
   const float* B;
-  const unsigned short* Bh;   // bf16 mode: B's bf16 shadow (a parameter operand, or the
-                              // activation operand X of a weight gradient) or null
-  const unsigned short* Ah;   // bf16 mode: A's bf16 shadow (an activation operand) or null
+  const unsigned short* Bh;   // bf16 mode: B's bf16 shadow (a parameter operand) or null
   float* C;
-  unsigned short* Ch;         // bf16 mode: the producer also stores bf16(C) here (null: no)
   const float* aux;
   int M, N, K;
   int lda, ldb, ldc, ldaux;
@@ -200,6 +192,14 @@ struct GemmDesc {
   int rs_col;          // >= 0 (A row-contiguous only): also produce sum_k A(m,k) — the
                        // bias gradient — into column rs_col of C (n0 == 0 tiles), with
                        // the same epilogue (store or Adam) as the tile
+  // dL/da partials of the actor pass (sac_imp.py:116-125 backward through Q(s, a~)), from
+  // the dha1 tile in the epilogue of the level that produces it: for every output row and
+  // every 32-column block cb of this GEMM's output (hidden units of critic fc1),
+  //   pa_out[((pa_base + cb) * M + row) * pa_A + j] = sum_{n in cb} C[row][n] * pa_w[n * pa_ld + j]
+  // (pa_w: the fc1 weights' action columns); the sample-backward tail sums the blocks
+  const float* pa_w;
+  float* pa_out;
+  int pa_ld, pa_A, pa_base;
 };
 
 // Adam fused into weight-gradient epilogues (single-GPU path): the gradient tile never
@@ -233,8 +233,6 @@ struct GatherArgs {
   float* xq; float* x2; int ldx;   // xq [B, ldx], x2 [2B, ldx]
   float* r; float* d;
   int by_slot;            // 1: idx are ring slots (PER), 0: deque positions
-  unsigned short* xqh;    // bf16 mode: shadows of xq / x2 (same layout), or null
-  unsigned short* x2h;
   tl_word* tl;
 };
 struct MtSampleArgs {
@@ -319,7 +317,6 @@ struct HeadSampleArgs {
   float* logp_part;      // [grid][2] or null: per workgroup, sum of logp over its rows
   int split_row;         //   < split_row (slot 0) and >= split_row (slot 1)
   float* act_host;       // or null: the actions also stored [row][A] to host-mapped memory
-  unsigned short* act_h; // or null: bf16 shadow of `act` (same layout)
   tl_word* tl;
 };
 
@@ -349,6 +346,11 @@ void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_
 // rows [n][cols] from host-mapped memory (select_action's states) into a device matrix
 void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int cols, hipStream_t s);
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s);
+// the same sample backward + dhp2 tail from the dL/da partials of the dha1 level
+// (GemmDesc::pa_out): dL/da = sum over the n_pa column blocks, fixed order
+void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, hipStream_t s);
+// whether launch_gemm runs this level on k_axk16 (no dL/da partials there)
+bool gemm_level_on_axk16(const GemmBatch& b);
 
 
 constexpr int kMaxAdamSegs = 8;

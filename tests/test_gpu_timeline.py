@@ -27,9 +27,11 @@ def test_timeline_covers_the_update_graph():
     names = [k["site"] for k in ks]
     # first update samples for itself, the next three ride along in L12 / L13
     assert names.count("mt_sample") == 1 and names.count("gather") == 1
+    # (2 hidden layers, fp32: dL/da is folded into L9's epilogue, L10 is the sample tail)
     for site in ("gemm_L1_fc1", "gemm_L6_critic_dW_adam", "gemm_L13_pi_dW_adam", "heads_sample",
-                 "gemm_L10_dlda_sample_bwd_dhp2"):
+                 "gemm_L9_act_dh1", "sample_bwd_tail_dhp2"):
         assert names.count(site) == 4, site
+    assert "gemm_L10_dlda_sample_bwd_dhp2" not in names
     starts = [k["start_us"] for k in ks]
     assert starts == sorted(starts)                    # graph kernels run in launch order
     assert all(k["end_us"] >= k["start_us"] for k in ks)
