@@ -132,6 +132,12 @@ def timeline_roofline(ctx, batch, n_updates, data_parallel=False):
     ends at its own exit stamp, and the gap up to the next kernel is all-reduce time."""
     ks, graph_us = ctx.profile_timeline(batch, n_updates, data_parallel)
     ks = sorted(ks, key=lambda k: k["start_us"])
+    # the next update's sampling + gather on the side stream ("*_next" sites, batch-4096
+    # class and prioritized replay) overlap the chain: their own span, outside the chain
+    side = [k for k in ks if k["site"].endswith("_next")]
+    for k in side:
+        k["dur_us"] = k["end_us"] - k["start_us"]
+    ks = [k for k in ks if not k["site"].endswith("_next")]
     allreduce_us = 0.0
     for i, k in enumerate(ks):
         nxt = ks[i + 1] if i + 1 < len(ks) else None
@@ -155,6 +161,10 @@ def timeline_roofline(ctx, batch, n_updates, data_parallel=False):
         e = sites.setdefault(k["site"], [0.0, 0])
         e[0] += k["dur_us"]
         e[1] += 1 if k["flops"] > 0 or k["kernel"] not in LEVEL_KERNELS else 0
+    for k in side:
+        e = sites.setdefault(k["site"], [0.0, 0])
+        e[0] += k["dur_us"]
+        e[1] += 1
     return dict(graph_us=graph_us, sum_us=sum(k["dur_us"] for k in ks) + allreduce_us,
                 allreduce_us=allreduce_us, n_updates=n_updates,
                 gemm_us=gemm_us, gemm_flops=gemm_flops, gemm_bytes=gemm_bytes, levels=levels,

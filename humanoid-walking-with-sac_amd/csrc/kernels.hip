@@ -853,10 +853,12 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
   if constexpr (PA) {
+    if (has_pa) {
 #pragma unroll
-    for (int q = 0; q < PW; ++q) {
-      const int e = tid + q * NTH;
-      if (e < TN * 32) s_pa[TMW * (TN + 1) + e] = paw_x[q];
+      for (int q = 0; q < PW; ++q) {
+        const int e = tid + q * NTH;
+        if (e < TN * 32) s_pa[TMW * (TN + 1) + e] = paw_x[q];
+      }
     }
   }
   if constexpr (AXK == 1) {
@@ -915,7 +917,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
       }
     }
     if constexpr (PA) {   // every tile element, 0 outside the output
-      if (s < EPT) s_pa[row * (TN + 1) + col] = ok ? v : 0.f;
+      if (has_pa && s < EPT) s_pa[row * (TN + 1) + col] = ok ? v : 0.f;
     }
   }
   if (threadIdx.x < 64) SACMI_STAMP(33);

@@ -82,6 +82,11 @@ struct sacmi_ctx {
   sacmi_config cfg{};
   int device = 0;
   hipStream_t own_stream = nullptr;
+  // multi-update graphs that cannot ride the next update's sampling along (batch-4096
+  // class, prioritized replay): that sampling + gather run on this side stream, forked
+  // from / joined into the capture, concurrently with the current update
+  hipStream_t side_stream = nullptr;
+  std::vector<hipEvent_t> side_ev;
   hipStream_t stream = nullptr;
   bool keep_grads = false;             // SACMI_S_KEEP_GRADS
   int S = 0, A = 0, H = 0, Bm = 0;
@@ -558,14 +563,16 @@ static bool mark(sacmi_ctx* c, const char* name, double flops = 0, double bytes 
   return c->prof_site < 0 || site == c->prof_site;
 }
 
-static PerArgs per_args(sacmi_ctx* c, int k, int gen_u) {
+struct BatchBufs;
+static PerArgs per_args(sacmi_ctx* c, int k, int gen_u, const BatchBufs* bb = nullptr);
+static PerArgs per_args_impl(sacmi_ctx* c, int k, int gen_u, int32_t* idx32, int64_t* idx64) {
   PerArgs a{};
   a.prio = c->prio.p; a.len = c->len; a.cap = c->capacity; a.alpha = (float)c->cfg.per_alpha;
   a.probs = c->per_probs.p; a.chunk_sums = c->per_chunk.p; a.q = c->per_q.p;
   a.block_sums = c->per_blk.p; a.bad = c->per_bad.p; a.cdf = c->per_cdf.p;
   a.mt = c->mt.p + 625; a.gen_u = gen_u; a.u = c->per_uin.p; a.u_scratch = c->per_u.p;
   a.k = k; a.sc = c->sc.p; a.beta_start = c->cfg.per_beta_start;
-  a.beta_frames = c->cfg.per_beta_frames; a.idx32 = c->idx32.p; a.idx_out = c->idx64.p;
+  a.beta_frames = c->cfg.per_beta_frames; a.idx32 = idx32; a.idx_out = idx64;
   a.w_out = c->per_w.p;
   return a;
 }
@@ -580,6 +587,10 @@ struct BatchBufs {
 static BatchBufs batch_bufs(sacmi_ctx* c, int parity) {
   if (parity == 0) return BatchBufs{c->idx32.p, c->idx64.p, c->xq.p, c->x2.p, c->r.p, c->d.p};
   return BatchBufs{c->idx32b.p, c->idx64b.p, c->xqb.p, c->x2b.p, c->rb.p, c->db.p};
+}
+// the prioritized sampler writes the indices of batch set bb (set 0 by default)
+static PerArgs per_args(sacmi_ctx* c, int k, int gen_u, const BatchBufs* bb) {
+  return per_args_impl(c, k, gen_u, bb ? bb->idx32 : c->idx32.p, bb ? bb->idx64 : c->idx64.p);
 }
 
 static int sample_setsize(int k) {   // random.py:486-488
@@ -609,6 +620,34 @@ static GatherArgs gather_args(sacmi_ctx* c, int B, const BatchBufs& bb, bool per
 static bool ride_possible(sacmi_ctx* c, int B) {
   return c->cfg.replay_kind == SACMI_REPLAY_UNIFORM &&
          mt_sample_lds_words(mt_sample_tbl_log2(B), sample_setsize(B)) * 4 <= kRideLdsBytes;
+}
+
+// One update's minibatch: device sampling (random.sample or the prioritized sampler, unless
+// the indices were staged from the host) + gather, into batch set `parity`, on stream s.
+// `tag` names the launch sites ("" for the update's own, "_next" on the side stream).
+static void enqueue_sample_gather(sacmi_ctx* c, int B, int parity, bool dev_idx, hipStream_t s,
+                                  const char* tag = "") {
+  const BatchBufs bb = batch_bufs(c, parity);
+  const bool per = c->cfg.replay_kind == SACMI_REPLAY_PER;
+  const std::string t(tag);
+  if (dev_idx && per) {
+    if (mark(c, ("per_sample" + t).c_str())) {
+      PerArgs pa = per_args(c, B, 1, &bb);
+      pa.tl = c->tl_cur;
+      launch_per_sample(pa, s);
+    }
+  } else if (dev_idx) {
+    if (mark(c, ("mt_sample" + t).c_str())) {
+      MtSampleArgs ma = mt_args(c, B, bb);
+      ma.tl = c->tl_cur;
+      launch_mt_sample(ma, s);
+    }
+  }
+  if (mark(c, ("gather" + t).c_str())) {
+    GatherArgs ga = gather_args(c, B, bb, per);
+    ga.tl = c->tl_cur;
+    launch_gather(ga, s);
+  }
 }
 
 // parity: which batch buffer set this update uses; have_batch: its indices and rows
@@ -655,27 +694,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   };
 
   if (phase_mask & 1) {
-    const bool per = c->cfg.replay_kind == SACMI_REPLAY_PER;
-    if (have_batch) {
-      // indices and rows were produced by the previous update (ride-along)
-    } else if (dev_idx && per) {
-      if (mark(c, "per_sample")) {
-        PerArgs pa = per_args(c, B, 1);
-        pa.tl = c->tl_cur;
-        launch_per_sample(pa, s);
-      }
-    } else if (dev_idx) {
-      if (mark(c, "mt_sample")) {
-        MtSampleArgs ma = mt_args(c, B, bb);
-        ma.tl = c->tl_cur;
-        launch_mt_sample(ma, s);
-      }
-    }
-    if (!have_batch && mark(c, "gather")) {
-      GatherArgs ga = gather_args(c, B, bb, per);
-      ga.tl = c->tl_cur;
-      launch_gather(ga, s);
-    }
+    if (!have_batch)   // (have_batch: the previous update's rides / side stream produced them)
+      enqueue_sample_gather(c, B, parity, dev_idx != 0, s);
 
     // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
     Level l1;
@@ -987,11 +1007,52 @@ static int64_t per_graph_len(const sacmi_ctx* c) {
   return c->len;
 }
 
+// n consecutive fused updates (sacmi_step_many_async, the timeline's replica of it):
+// the next update's sampling + gather ride along in this update's launches where they fit
+// (uniform replay, batch <= ~2k), else run on the side stream concurrently with it
+static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use_ring, int reps) {
+  const bool ride = reps > 1 && dev_idx && ride_possible(c, B);
+  // prioritized replay only: its sampler is long and mostly serial (the numpy-MT uniforms
+  // of one workgroup, the 8192-row chunk trees), so overlapping it wins (config 3: 768 ->
+  // 719 us per update); the uniform batch-4096 sampler + gather beside the chip-filling
+  // bf16 levels measured slower (config 5: 408 -> 424 us: their workgroups push level
+  // workgroups into a second round), and a low-priority side stream far slower still
+  static const bool side_env = std::getenv("SACMI_NO_SIDE_SAMPLE") == nullptr;
+  const bool side = side_env && reps > 1 && dev_idx && !ride &&
+                    c->cfg.replay_kind == SACMI_REPLAY_PER;
+  if (side) {
+    if (!c->side_stream) CHECK_HIP(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+    while ((int)c->side_ev.size() < 2 * reps) {
+      hipEvent_t e;
+      CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->side_ev.push_back(e);
+    }
+    // update r uses batch set r & 1; its successor's set is free once update r - 1 has
+    // finished, i.e. at update r's start (fork); update r + 1 starts after the side
+    // stream's gather (join).  The side stream's own order keeps the sampling stream's
+    // state (MT / numpy MT + frame) sequential, exactly as n separate updates consume it.
+    enqueue_sample_gather(c, B, 0, true, c->stream);
+    for (int r = 0; r < reps; ++r) {
+      if (r > 0) CHECK_HIP(hipStreamWaitEvent(c->stream, c->side_ev[2 * r + 1], 0));
+      if (r + 1 < reps) {
+        CHECK_HIP(hipEventRecord(c->side_ev[2 * r], c->stream));
+        CHECK_HIP(hipStreamWaitEvent(c->side_stream, c->side_ev[2 * r], 0));
+        enqueue_sample_gather(c, B, (r + 1) & 1, true, c->side_stream, "_next");
+        CHECK_HIP(hipEventRecord(c->side_ev[2 * r + 3], c->side_stream));
+      }
+      enqueue_update(c, B, dev_idx, dev_eps, 7, 1.f, use_ring, r & 1, true, false);
+    }
+    return;
+  }
+  for (int r = 0; r < reps; ++r)
+    enqueue_update(c, B, dev_idx, dev_eps, 7, 1.f, use_ring, ride ? (r & 1) : 0, ride && r > 0,
+                   ride && r + 1 < reps);
+}
+
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
                        float grad_scale, bool use_ring, int reps = 1, PhaseRide pr = {}) {
   // consecutive fused updates hand the next update's sampling + gather to ride-along
   // workgroups of the current one
-  const bool ride = reps > 1 && phase_mask == 7 && dev_idx && ride_possible(c, B);
   auto enqueue_all = [&]() {
     if (phase_mask == 5) {   // phase 2 of the previous update, then phase 0 of the next
       enqueue_update(c, B, dev_idx, dev_eps, 4, grad_scale, use_ring, pr.parity ^ 1);
@@ -1003,9 +1064,7 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
                      pr.have_batch, pr.ride_next);
       return;
     }
-    for (int r = 0; r < reps; ++r)
-      enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring, ride ? (r & 1) : 0,
-                     ride && r > 0, ride && r + 1 < reps);
+    enqueue_many(c, B, dev_idx, dev_eps, use_ring, reps);
   };
   // the caller is capturing this stream into its own graph (e.g. torch.cuda.graph around
   // a data-parallel update and its collectives): enqueue into that capture directly
@@ -1242,6 +1301,8 @@ int sacmi_destroy(sacmi_ctx* c) {
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
     c->per_u.release(); c->per_uin.release(); c->per_owner.release(); c->per_bad.release();
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
+    for (hipEvent_t e : c->side_ev) (void)hipEventDestroy(e);
     delete c;
   });
 }
@@ -1891,12 +1952,7 @@ int sacmi_profile_timeline(sacmi_ctx* c, int32_t batch, int32_t n_updates, int32
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
     // the same update sequence sacmi_step_many_async replays
-    const bool ride = n_updates > 1 && ride_possible(c, batch);
-    timeline_of(c, n_updates, [&]() {
-      for (int r = 0; r < n_updates; ++r)
-        enqueue_update(c, batch, 1, 1, 7, 1.f, true, ride ? (r & 1) : 0, ride && r > 0,
-                       ride && r + 1 < n_updates);
-    }, max_kernels, names_out, kind_out, grid_out, site_out, start_us, end_us, flops_out,
+    timeline_of(c, n_updates, [&]() { enqueue_many(c, batch, 1, 1, true, n_updates); }, max_kernels, names_out, kind_out, grid_out, site_out, start_us, end_us, flops_out,
        bytes_out, n_kernels, graph_us);
   });
 }

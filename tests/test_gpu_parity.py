@@ -488,23 +488,32 @@ def test_polyak_bitexact_and_determinism():
             assert np.array_equal(outs[0][n][k], outs[1][n][k]), (n, k)
 
 
-@pytest.mark.parametrize("shape", ["small", "nao_b4096_bf16"])
+@pytest.mark.parametrize("shape", ["small", "nao_b4096_bf16", "per_b4096"])
 def test_many_updates_per_launch_identical(shape):
     """sacmi_step_many_async(n) (trainer.py:203-204 loop in one launch) == n single
     launches, bit for bit, losses included — also at the config-5 shapes (batch 4096,
     bf16: the LDS-staged level kernels, split-K dW with its XCD placement, device
-    sampling of 4096 rows)."""
+    sampling of 4096 rows; the next update's sampling + gather on the side stream) and
+    with prioritized replay at batch 4096 (config 3: the PER sampler on the side stream)."""
+    from sacmi import _lib as L
+    replay = "uniform"
     if shape == "small":
         cfg, B, nrows, dt = SacConfig(24, 4, 64), 64, 500, "fp32"
+    elif shape == "per_b4096":
+        cfg, B, nrows, dt, replay = SacConfig(376, 17, 512), 4096, 9000, "fp32", "per"
     else:
         cfg, B, nrows, dt = SacConfig(661, 23, 512), 4096, 6000, "bf16"
     params = init_params(cfg, 61, bias_scale=0.05)
     rows = synthetic_rows(cfg, nrows, 62, state_scale=0.5)
+    prio = np.random.default_rng(64).uniform(0.1, 2.0, nrows).astype(np.float32)
     res = []
     for many in (True, False):
-        ctx = make_ctx(cfg, max_batch=B, capacity=nrows, compute_dtype=dt)
+        ctx = make_ctx(cfg, max_batch=B, capacity=nrows, compute_dtype=dt, replay=replay)
         load_params(ctx, params)
         ctx.push(*rows)
+        if replay == "per":
+            ctx.per_set_priorities(prio)
+            ctx.set_mt(1, (np.arange(624, dtype=np.uint64) * 69069 % (2**32)).astype(np.uint32), 624)
         ctx.set_mt(0, (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32), 624)
         if many:
             ctx.step_many_async(B, 5)
@@ -512,12 +521,15 @@ def test_many_updates_per_launch_identical(shape):
         else:
             for _ in range(7):
                 ctx.step_async(B)
-        res.append((ctx.fetch_losses(7), {n: ctx.get_net(n) for n in NETS}, ctx.get_mt(0)))
+        res.append((ctx.fetch_losses(7), {n: ctx.get_net(n) for n in NETS},
+                    ctx.get_mt(0 if replay == "uniform" else 1), ctx.get_scalar(L.S_PER_FRAME)))
+        ctx.close()
     assert np.array_equal(res[0][0], res[1][0]) and res[0][0].shape == (7, 3)
     for n in NETS:
         for k in res[0][1][n]:
             assert np.array_equal(res[0][1][n][k], res[1][1][n][k]), (n, k)
     assert np.array_equal(res[0][2][0], res[1][2][0]) and res[0][2][1] == res[1][2][1]
+    assert res[0][3] == res[1][3]
 
 
 def test_bf16_shadows_stay_current():
