@@ -1485,6 +1485,8 @@ __global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int
 typedef short s4t __attribute__((ext_vector_type(4)));
 typedef short s8t __attribute__((ext_vector_type(8)));
 constexpr int kD16K = 64, kD16Pad = 8;
+constexpr int kDw16OpBytes = 2 * kD16K * (kDBM + kD16Pad) * 2;      // one operand, 2 slabs
+static_assert(kDw16LdsBytes == 2 * kDw16OpBytes + 8 * kDBM * 4, "k_dw_part16 LDS layout");
 
 __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -1494,15 +1496,22 @@ __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
 __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_PART16);
   constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
-  __shared__ __attribute__((aligned(16))) __bf16 sA[2][kD16K][LDR];
-  __shared__ __attribute__((aligned(16))) __bf16 sB[2][kD16K][LDR];
-  __shared__ float s_rs[8][kDBM];
+  // one LDS block (kDw16LdsBytes): the two operand slabs and the row-sum scratch, or a
+  // ride-along sampler's table
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kDw16LdsBytes];
+  auto& sA = *reinterpret_cast<__bf16 (*)[2][kD16K][LDR]>(lds_raw);
+  auto& sB = *reinterpret_cast<__bf16 (*)[2][kD16K][LDR]>(lds_raw + kDw16OpBytes);
+  auto& s_rs = *reinterpret_cast<float (*)[8][kDBM]>(lds_raw + 2 * kDw16OpBytes);
   const int tiles_tot = batch.total_tiles;
   const int nwg = dw_grid_tiles(tiles_tot, ns);
-  if ((int)blockIdx.x >= nwg) {   // ride-along: the next update's gather
+  if ((int)blockIdx.x >= nwg) {   // ride-along: the next update's sampling or gather
     const int rb = blockIdx.x - nwg, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int b = rb * 4 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 4)
-      gather_row(batch.ride.ga, b, lane, 64);
+    if (batch.ride.kind == 1) {
+      if (rb == 0) mt_sample_body(batch.ride.mt, batch.ride.tbl_log2, reinterpret_cast<uint32_t*>(lds_raw));
+    } else {
+      for (int b = rb * 4 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 4)
+        gather_row(batch.ride.ga, b, lane, 64);
+    }
     return;
   }
   const int wk = dw_work_index(blockIdx.x, tiles_tot, ns);
@@ -1658,6 +1667,12 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
   __shared__ __attribute__((aligned(16))) __bf16 sB[2][kXBK][LDB_];
   __shared__ float s_q[kXBM][4], s_coef[2][kXBM], s_l[kXBM][2];
   const int bid = blockIdx.x;
+  if (bid >= batch.total_tiles) {   // ride-along: the next update's gather, 4 rows a wave
+    const int wv = (bid - batch.total_tiles) * 4 + (int)(threadIdx.x >> 6), nwv = batch.ride.nblocks * 4;
+    for (int b0 = wv; b0 < batch.ride.ga.B; b0 += 4 * nwv)
+      gather_rows_wave<4, 4>(batch.ride.ga, b0, nwv, threadIdx.x & 63);
+    return;
+  }
   int p = 0;
   for (int q = 1; q < batch.count; ++q)
     if (bid >= batch.d[q].tile_begin) p = q;
@@ -1822,7 +1837,7 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
 // and at least one 64x128 tile per CU
 // (-1: no; 1: the row-prologue form; 0: the plain dh form)
 static int axk16_ok(GemmBatch& b) {
-  if (!b.bf16 || b.ride.kind) return -1;
+  if (!b.bf16 || (b.ride.kind && b.ride.kind != 2)) return -1;   // (hosts the gather ride)
   const int ax = b.d[0].axk == 1 ? 1 : 0;
   if (ax != (b.rows.kind != 0 ? 1 : 0)) return -1;
   for (int i = 0; i < b.count; ++i) {
@@ -1918,7 +1933,9 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
 
 // bf16 deep-K weight-gradient levels: split count and workspace need, or 0 (old path)
 static int dw_split_plan(GemmBatch& b, int64_t* stride) {
-  if ((!b.bf16 && !SACMI_DW_SPLIT_FP32) || !b.ws || (b.ride.kind && b.ride.kind != 2)) return 0;
+  // (rides: the gather on any split-K kernel, the sampler on k_dw_part16 only)
+  if ((!b.bf16 && !SACMI_DW_SPLIT_FP32) || !b.ws || (b.ride.kind == 1 && !(b.bf16 && SACMI_DW_LDS16)))
+    return 0;
   int64_t el = 0;
   int tiles = 0;
   for (int i = 0; i < b.count; ++i) {
@@ -1990,7 +2007,10 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     int64_t stride = 0;
     const int ns = SACMI_DW_SPLIT ? dw_split_plan(b, &stride) : 0;
     if (ns > 0) {
-      const int ride = b.ride.kind == 2 ? b.ride.nblocks : 0;
+      const int ride = b.ride.kind ? b.ride.nblocks : 0;
+      if (b.ride.kind == 1 &&
+          mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > (size_t)kDw16LdsBytes)
+        throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_dw_part16's LDS"};
       const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
       if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
@@ -2010,10 +2030,11 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       for (int i = 0; i < b.count; ++i)   // k_axk16 computes no dL/da partials
         if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a k_axk16 level"};
       const bool bh = all_bh(b);
-      if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-      else if (ax) hipLaunchKernelGGL((k_axk16<true, false>), dim3(b.total_tiles), dim3(256), 0, s, b);
-      else if (bh) hipLaunchKernelGGL((k_axk16<false, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-      else hipLaunchKernelGGL((k_axk16<false, false>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      const dim3 grid(b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0));
+      if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true>), grid, dim3(256), 0, s, b);
+      else if (ax) hipLaunchKernelGGL((k_axk16<true, false>), grid, dim3(256), 0, s, b);
+      else if (bh) hipLaunchKernelGGL((k_axk16<false, true>), grid, dim3(256), 0, s, b);
+      else hipLaunchKernelGGL((k_axk16<false, false>), grid, dim3(256), 0, s, b);
       HIP_LAUNCH_CHECK();
       return;
     }
@@ -2035,6 +2056,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   }
   b = b0;
   const int extra = b.ride.kind ? b.ride.nblocks : 0;
+  if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > kRideLdsBytes)
+    throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_gemm's LDS"};
   int maxk = 0, n_adam = 0;
   int64_t outs = 0;
   for (int i = 0; i < b.count; ++i) {

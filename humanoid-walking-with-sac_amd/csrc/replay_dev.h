@@ -61,43 +61,31 @@ __device__ void mt_twist_serial(uint32_t* key) {
     key[i] = mt_mix(key[i], key[(i + 1) % kMtN], key[(i + kMtM) % kMtN]);
 }
 
-// Block-wide exclusive scan of a 0/1 flag; returns the rank and writes the total.
-__device__ __forceinline__ int block_scan_flag(bool f, int* wave_tot, int* total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned long long m = __ballot(f);
-  const int in_wave = __popcll(m & ((1ull << lane) - 1ull));
-  if (lane == 0) wave_tot[w] = __popcll(m);
-  __syncthreads();
-  int base = 0, tot = 0;
-  const int nw = blockDim.x >> 6;
-  for (int q = 0; q < nw; ++q) {
-    const int c = wave_tot[q];
-    if (q < w) base += c;
-    tot += c;
-  }
-  *total = tot;
-  __syncthreads();
-  return base + in_wave;
-}
-
 __device__ __forceinline__ uint32_t hash_slot(uint32_t r, uint32_t mask) {
   return (r * 0x9E3779B1u) & mask;
 }
 
-// hash table size (log2) for k selections: >= 2 * (k + 624) slots
-__host__ __device__ constexpr int mt_sample_tbl_log2(int k) {
+// hash table size (log2) for k selections: >= 2 (k + 624) slots.  At most k - 1 + 624
+// distinct values are ever inserted (fewer than k first occurrences before the last block
+// of 624 words), so the load factor stays <= 1/2.  compact: >= 1.5 (k + 624) slots (load
+// <= 2/3, a few more probes) — batch 4096 then needs 68 KB of LDS instead of 134, which
+// fits k_dw_part16's LDS block (the ride-along placement B, sacmi.hip)
+__host__ __device__ constexpr int mt_sample_tbl_log2(int k, bool compact = false) {
   int tl = 4;
-  while ((1 << tl) < 2 * (k + kMtN)) ++tl;
+  while ((1 << tl) < (compact ? 3 * (k + kMtN) / 2 : 2 * (k + kMtN))) ++tl;
   return tl;
 }
 
 // LDS words the body needs: the hash table (set branch) or the pool, + key + scratch
+// (two 16-word rounds of wave totals, the last selector, the position)
+constexpr int kMtScratch = 40;
+constexpr int kMtCpt = 3;      // candidate words per thread and round at >= 256 threads
 __host__ __device__ constexpr size_t mt_sample_lds_words(int tbl_log2, int setsize) {
-  return ((size_t)2 << tbl_log2) > (size_t)setsize ? ((size_t)2 << tbl_log2) + kMtN + 32
-                                                   : (size_t)setsize + kMtN + 32;
+  return ((size_t)2 << tbl_log2) > (size_t)setsize ? ((size_t)2 << tbl_log2) + kMtN + kMtScratch
+                                                   : (size_t)setsize + kMtN + kMtScratch;
 }
 
-// Body of the sampler for one workgroup of 1024 threads; `lds` holds
+// Body of the sampler for one workgroup of 256..1024 threads; `lds` holds
 // mt_sample_lds_words(tbl_log2, setsize) words.  Used by k_mt_sample and, riding along
 // in a GEMM launch, for the next update of a multi-update graph.
 __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_log2, uint32_t* lds) {
@@ -106,8 +94,8 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
   uint32_t* smem = lds;
   uint32_t* key = lds + tbl_words;
   int* wave_tot = reinterpret_cast<int*>(key + kMtN);
-  int& s_last = wave_tot[16];
-  int& s_pos = wave_tot[17];
+  int& s_last = wave_tot[32];
+  int& s_pos = wave_tot[33];
   const int t = threadIdx.x;
   const int64_t n64 = a.sc->len;
   const uint32_t n = (uint32_t)n64;
@@ -147,47 +135,79 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
     int32_t* hseq = reinterpret_cast<int32_t*>(smem + T);
     for (uint32_t i = t; i < T; i += blockDim.x) { hkey[i] = kEmpty; hseq[i] = 0x7FFFFFFF; }
     const int kb = 32 - __clz((int)n);   // bit_length(n), n < 2^31
+    const int lane = t & 63, w = t >> 6, nw = (int)blockDim.x >> 6;
     int count = 0, seqbase = 0;
     __syncthreads();
-    for (;;) {
+    // one round per block of 624 words (the rest of the current one): thread t takes the
+    // cpt consecutive words t * cpt + j (cpt = 3 at 256 threads, 1 at 1024).  Two barriers a
+    // round (inserts done; wave totals written): the totals alternate between two 16-word
+    // halves by round, so no trailing barrier orders their reuse, and the next round's
+    // inserts follow every thread's table reads of this one (before barrier 2)
+    const int cpt = (kMtN + (int)blockDim.x - 1) / (int)blockDim.x;
+    for (int par = 0;; par ^= 1) {
       if (pos >= kMtN) { mt_twist_block(key); pos = 0; }
       const int avail = kMtN - pos;
-      const bool valid = t < avail;
-      uint32_t r = 0;
-      bool acc = false;
-      if (valid) {
-        r = mt_temper(key[pos + t]) >> (32 - kb);
-        acc = r < n;
+      uint32_t r[kMtCpt], slot[kMtCpt];
+      bool first[kMtCpt];
+#pragma unroll
+      for (int j = 0; j < kMtCpt; ++j) {
+        const int o = t * cpt + j;
+        r[j] = 0; slot[j] = 0; first[j] = false;
+        if (j < cpt && o < avail) {
+          r[j] = mt_temper(key[pos + o]) >> (32 - kb);
+          first[j] = r[j] < n;        // accepted; "first" after the table read below
+        }
       }
       // a candidate's order key is its word's position in the stream (monotone in draw
       // order, so the smallest key per value is its first occurrence): no scan needed
-      const int seq = seqbase + t;
-      uint32_t slot = 0;
-      if (acc) {
-        slot = hash_slot(r, mask);
+#pragma unroll
+      for (int j = 0; j < kMtCpt; ++j) {
+        if (!first[j]) continue;
+        uint32_t sl = hash_slot(r[j], mask);
         for (;;) {
-          const uint32_t prev = atomicCAS(&hkey[slot], kEmpty, r);
-          if (prev == kEmpty || prev == r) { atomicMin(&hseq[slot], seq); break; }
-          slot = (slot + 1) & mask;
+          const uint32_t prev = atomicCAS(&hkey[sl], kEmpty, r[j]);
+          if (prev == kEmpty || prev == r[j]) { atomicMin(&hseq[sl], seqbase + t * cpt + j); break; }
+          sl = (sl + 1) & mask;
         }
+        slot[j] = sl;
       }
       __syncthreads();
-      const bool first = acc && hseq[slot] == seq;
-      int nfirst;
-      const int srank = block_scan_flag(first, wave_tot, &nfirst);
-      if (first && count + srank < k) {
-        a.idx_out[count + srank] = (int32_t)r;
-        if (a.idx64_out) a.idx64_out[count + srank] = (int64_t)r;
-        if (count + srank == k - 1) s_last = t;
+      int mine = 0;
+#pragma unroll
+      for (int j = 0; j < kMtCpt; ++j) {
+        first[j] = first[j] && hseq[slot[j]] == seqbase + t * cpt + j;
+        mine += first[j] ? 1 : 0;
       }
+      // per-lane counts 0..3 as two bit planes: the wave's exclusive prefix and total
+      const unsigned long long b0 = __ballot(mine & 1), b1 = __ballot(mine & 2);
+      const unsigned long long below = (1ull << lane) - 1ull;
+      int* wt = wave_tot + 16 * par;
+      if (lane == 0) wt[w] = __popcll(b0) + 2 * __popcll(b1);
       __syncthreads();
-      if (count + nfirst >= k) { pos = pos + s_last + 1; break; }
+      int base = 0, nfirst = 0;
+      for (int q = 0; q < nw; ++q) {
+        const int c = wt[q];
+        base += q < w ? c : 0;
+        nfirst += c;
+      }
+      int rank = count + base + __popcll(b0 & below) + 2 * __popcll(b1 & below);
+#pragma unroll
+      for (int j = 0; j < kMtCpt; ++j) {
+        if (!first[j]) continue;
+        if (rank < k) {
+          a.idx_out[rank] = (int32_t)r[j];
+          if (a.idx64_out) a.idx64_out[rank] = (int64_t)r[j];
+          if (rank == k - 1) s_last = t * cpt + j;
+        }
+        ++rank;
+      }
+      if (count + nfirst >= k) break;    // (uniform: every thread summed the same totals)
       count += nfirst;
       seqbase += avail;
       pos = kMtN;
-      // (no barrier here: the next twist reads key only after this iteration's last
-      // barrier, and the scans' own barriers order every wave_tot reuse)
     }
+    __syncthreads();
+    pos += s_last + 1;
   }
   __syncthreads();
   for (int i = t; i < kMtN; i += blockDim.x) a.mt[i] = key[i];
@@ -206,27 +226,90 @@ __device__ __forceinline__ void gather_row(const GatherArgs& a, int b, int lane,
   float* xq = a.xq + (size_t)b * a.ldx;
   float* xt = a.x2 + (size_t)b * a.ldx;
   float* xa = a.x2 + (size_t)(a.B + b) * a.ldx;
-  // write-through stores (sacmi_internal.h st_wt): the minibatch leaves no dirty L2 lines
-  if ((a.S & 3) == 0) {
-    const uint32_t oq = (uint32_t)((size_t)b * a.ldx) * 4u, ot = oq;
-    const uint32_t oa = (uint32_t)((size_t)(a.B + b) * a.ldx) * 4u;
-    for (int q = lane; q < a.S / 4; q += nl) {
-      const float4 v = reinterpret_cast<const float4*>(so)[q];
-      const float4 w = reinterpret_cast<const float4*>(s2)[q];
-      st_wt4(a.xq, oq + 16u * q, v);
-      st_wt4(a.x2, oa + 16u * q, v);
-      st_wt4(a.x2, ot + 16u * q, w);
-    }
-  } else {
-    for (int q = lane; q < a.S; q += nl) {
-      const float v = so[q];
-      st_wt(xq + q, v); st_wt(xa + q, v); st_wt(xt + q, s2[q]);
-    }
+  // write-through stores (sacmi_internal.h st_wt): the minibatch leaves no dirty L2 lines.
+  // The state's whole float4s (replay rows and minibatch rows are 16-B aligned: ldo, ldx
+  // multiples of 4), then its S % 4 tail (NAO-walk: S = 661)
+  const uint32_t oq = (uint32_t)((size_t)b * a.ldx) * 4u, ot = oq;
+  const uint32_t oa = (uint32_t)((size_t)(a.B + b) * a.ldx) * 4u;
+  const int s4 = a.S >> 2;
+  for (int q = lane; q < s4; q += nl) {
+    const float4 v = reinterpret_cast<const float4*>(so)[q];
+    const float4 w = reinterpret_cast<const float4*>(s2)[q];
+    st_wt4(a.xq, oq + 16u * q, v);
+    st_wt4(a.x2, oa + 16u * q, v);
+    st_wt4(a.x2, ot + 16u * q, w);
+  }
+  for (int q = 4 * s4 + lane; q < a.S; q += nl) {
+    const float v = so[q];
+    st_wt(xq + q, v); st_wt(xa + q, v); st_wt(xt + q, s2[q]);
   }
   for (int j = lane; j < a.A; j += nl) st_wt(xq + a.S + 1 + j, ac[j]);
   if (lane == 0) {
     st_wt(a.r + b, a.rew[slot]);
     st_wt(a.d + b, a.done[slot]);
+  }
+}
+
+// Rows b0 + i * bstep (i < R) by one wave, every load of the R rows issued before any
+// store: one latency chain for R rows instead of R (the ride-along form — a few hundred
+// waves beside a level gather the whole batch).  Loads at clamped addresses, results
+// discarded by predicated stores (a guarded load would drain at its guard).  States wider
+// than 256 Q floats take gather_row.
+template <int R, int Q>
+__device__ __forceinline__ void gather_rows_wave(const GatherArgs& a, int b0, int bstep, int lane) {
+  const int s4 = a.S >> 2, st = a.S & 3;
+  if (s4 > 64 * Q || s4 == 0) {
+    for (int i = 0; i < R; ++i)
+      if (b0 + i * bstep < a.B) gather_row(a, b0 + i * bstep, lane, 64);
+    return;
+  }
+  int64_t slot[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int b = b0 + i * bstep;
+    const int32_t ix = a.idx[b < a.B ? b : 0];
+    slot[i] = a.by_slot ? (int64_t)ix : (a.sc->head + (int64_t)ix) % a.capacity;
+  }
+  float4 v[R][Q], w[R][Q];
+  float tv[R], tw[R], av[R], rv[R], dv[R];
+  const int jt = 4 * s4 + (lane < st ? lane : 0), ja = lane < a.A ? lane : 0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const float4* so = reinterpret_cast<const float4*>(a.obs + slot[i] * a.ldo);
+    const float4* s2 = reinterpret_cast<const float4*>(a.obs2 + slot[i] * a.ldo);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int qq = lane + 64 * q < s4 ? lane + 64 * q : s4 - 1;
+      v[i][q] = so[qq];
+      w[i][q] = s2[qq];
+    }
+    tv[i] = a.obs[slot[i] * a.ldo + (st ? jt : 0)];
+    tw[i] = a.obs2[slot[i] * a.ldo + (st ? jt : 0)];
+    av[i] = a.act[slot[i] * a.lda_ + ja];
+    rv[i] = a.rew[slot[i]];
+    dv[i] = a.done[slot[i]];
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int b = b0 + i * bstep;
+    if (b >= a.B) break;
+    const uint32_t oq = (uint32_t)((size_t)b * a.ldx) * 4u, ot = oq;
+    const uint32_t oa = (uint32_t)((size_t)(a.B + b) * a.ldx) * 4u;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int qq = lane + 64 * q;
+      if (qq < s4) {
+        st_wt4(a.xq, oq + 16u * qq, v[i][q]);
+        st_wt4(a.x2, oa + 16u * qq, v[i][q]);
+        st_wt4(a.x2, ot + 16u * qq, w[i][q]);
+      }
+    }
+    float* xq = a.xq + (size_t)b * a.ldx;
+    float* xt = a.x2 + (size_t)b * a.ldx;
+    float* xa = a.x2 + (size_t)(a.B + b) * a.ldx;
+    if (lane < st) { st_wt(xq + jt, tv[i]); st_wt(xa + jt, tv[i]); st_wt(xt + jt, tw[i]); }
+    if (lane < a.A) st_wt(xq + a.S + 1 + lane, av[i]);
+    if (lane == 0) { st_wt(a.r + b, rv[i]); st_wt(a.d + b, dv[i]); }
   }
 }
 

@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -622,9 +623,21 @@ static bool ride_possible(sacmi_ctx* c, int B) {
          mt_sample_lds_words(mt_sample_tbl_log2(B), sample_setsize(B)) * 4 <= kRideLdsBytes;
 }
 
+// ... or, in a fused multi-update graph whose batch is too large for that (the batch-4096
+// class, bf16): the sampler (compact table, 256 threads) rides in L6's split-K kernel
+// (k_dw_part16, 440 of 512 slots at config 5) and the gather in L12 (k_axk16, 256 of 512
+// slots; 4 rows a wave, every load before any store).  (The gather in L10 measured no
+// overlap: k_gemm_sample_bwd's 1024-thread workgroups fit one per CU)
+static bool ride_b_possible(sacmi_ctx* c, int B) {
+  return c->cfg.replay_kind == SACMI_REPLAY_UNIFORM && c->bf16 && B >= 2048 &&
+         mt_sample_lds_words(mt_sample_tbl_log2(B, true), sample_setsize(B)) * 4 <=
+             (size_t)kDw16LdsBytes &&
+         std::getenv("SACMI_NO_RIDE_B") == nullptr;
+}
+
 // One update's minibatch: device sampling (random.sample or the prioritized sampler, unless
 // the indices were staged from the host) + gather, into batch set `parity`, on stream s.
-// `tag` names the launch sites ("" for the update's own, "_next" on the side stream).
+// `tag` names the launch sites ("" for the update's own, "_next" on the side stream);
 static void enqueue_sample_gather(sacmi_ctx* c, int B, int parity, bool dev_idx, hipStream_t s,
                                   const char* tag = "") {
   const BatchBufs bb = batch_bufs(c, parity);
@@ -659,6 +672,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   hipStream_t s = c->stream;
   c->site_counter = 0;
   const BatchBufs bb = batch_bufs(c, parity);
+  // where the next update's sampling + gather ride: L12 / L13 (placement A, batch <= ~2k,
+  // any phase split) or L6 / L10 (placement B, fused updates of the batch-4096 class)
+  const bool ride_b = ride_next && !ride_possible(c, B);
+  REQUIRE(!ride_b || (phase_mask == 7 && ride_b_possible(c, B)), SACMI_ESTATE,
+          "no ride-along placement for this batch");
   const int S = c->S, A = c->A, H = c->H, Kx = c->Kx, Hd = c->Hd;
   float* P = c->P.p;
   float* G = c->G.p;
@@ -808,6 +826,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.Ph = c->Ph.p; f.Th = c->Th.p;
       f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
     }
+    if (ride_b) {   // the next update's random.sample rides in L6 (placement B)
+      l6.b.ride.kind = 1; l6.b.ride.nblocks = 1;
+      l6.b.ride.tbl_log2 = mt_sample_tbl_log2(B, true);
+      l6.b.ride.mt = mt_args(c, B, batch_bufs(c, parity ^ 1));
+    }
     run(l6, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1");
   }
   const float lr = (float)c->cfg.lr;
@@ -932,6 +955,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     }
     Level l12, l13;
     l12.add(gd(c->dhp[1].p, H, 1, W(c->p_fc[1]), Hd, 0, c->dhp[0].p, H, B, H, H, EPI_MASK, hpa(0), Hd));
+    if (ride_b) {   // ... and its gather in L12 (256 of 512 slots at config 5), 4 rows a wave
+      l12.b.ride.kind = 2; l12.b.ride.nblocks = (B + 15) / 16;
+      l12.b.ride.ga = gather_args(c, B, batch_bufs(c, parity ^ 1), false);
+    }
     // same level structure fused or not: identical reduction order
     l13.add(gd_dw_h(c->dhead.p, c->lddh, hpa(L), Hd, pdst(c->p_head), Hd, 2 * A, H, B, pepi, 0));
     for (int l = L; l >= 1; --l)
@@ -951,7 +978,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.log_alpha_grad = G + c->la_idx;
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
     }
-    if (ride_next) {
+    if (ride_next && !ride_b) {
       // the next update's random.sample rides in L12 (128 tiles: idle CUs)
       const BatchBufs nb2 = batch_bufs(c, parity ^ 1);
       l12.b.ride.kind = 1; l12.b.ride.nblocks = 1;
@@ -1011,12 +1038,14 @@ static int64_t per_graph_len(const sacmi_ctx* c) {
 // the next update's sampling + gather ride along in this update's launches where they fit
 // (uniform replay, batch <= ~2k), else run on the side stream concurrently with it
 static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use_ring, int reps) {
-  const bool ride = reps > 1 && dev_idx && ride_possible(c, B);
+  const bool ride = reps > 1 && dev_idx && (ride_possible(c, B) || ride_b_possible(c, B));
   // prioritized replay only: its sampler is long and mostly serial (the numpy-MT uniforms
   // of one workgroup, the 8192-row chunk trees), so overlapping it wins (config 3: 768 ->
-  // 719 us per update); the uniform batch-4096 sampler + gather beside the chip-filling
-  // bf16 levels measured slower (config 5: 408 -> 424 us: their workgroups push level
-  // workgroups into a second round), and a low-priority side stream far slower still
+  // 719 us per update).  The uniform batch-4096 sampler + gather on the side stream
+  // measured slower, forked at the update's start (config 5: 408 -> 424 us: their
+  // workgroups push level workgroups of the chip-filling levels into a second round) and
+  // forked beside the levels with free slots (L6 / L12: 422 -> 430-450 us — every
+  // cross-stream edge of the graph cost the main chain ~10 us); they ride (placement B)
   static const bool side_env = std::getenv("SACMI_NO_SIDE_SAMPLE") == nullptr;
   const bool side = side_env && reps > 1 && dev_idx && !ride &&
                     c->cfg.replay_kind == SACMI_REPLAY_PER;
@@ -1027,6 +1056,8 @@ static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use
       CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       c->side_ev.push_back(e);
     }
+  }
+  if (side) {
     // update r uses batch set r & 1; its successor's set is free once update r - 1 has
     // finished, i.e. at update r's start (fork); update r + 1 starts after the side
     // stream's gather (join).  The side stream's own order keeps the sampling stream's

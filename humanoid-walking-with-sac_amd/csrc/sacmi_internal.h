@@ -251,6 +251,9 @@ struct MtSampleArgs {
 // every k_gemm config launch_gemm picks has 1024 threads and a reduction buffer of at
 // least 16*32*33 floats: the LDS a ride-along random.sample may use
 constexpr size_t kRideLdsBytes = (size_t)16 * 32 * 33 * 4;
+// k_dw_part16's LDS block (two bf16 operand slab pairs + row-sum scratch), which a
+// ride-along sampler may use instead
+constexpr int kDw16LdsBytes = 73728;
 struct RideAlong {
   int kind;        // 0 none, 1 random.sample, 2 gather
   int nblocks;

@@ -488,12 +488,13 @@ def test_polyak_bitexact_and_determinism():
             assert np.array_equal(outs[0][n][k], outs[1][n][k]), (n, k)
 
 
-@pytest.mark.parametrize("shape", ["small", "nao_b4096_bf16", "per_b4096"])
+@pytest.mark.parametrize("shape", ["small", "nao_b4096_bf16", "nao_b4096_bf16_set", "per_b4096"])
 def test_many_updates_per_launch_identical(shape):
     """sacmi_step_many_async(n) (trainer.py:203-204 loop in one launch) == n single
     launches, bit for bit, losses included — also at the config-5 shapes (batch 4096,
     bf16: the LDS-staged level kernels, split-K dW with its XCD placement, device
-    sampling of 4096 rows; the next update's sampling + gather on the side stream) and
+    sampling of 4096 rows — the pool branch at 6,000 rows, the set branch at 20,000; the
+    next update's sampler forked beside L6 and its gather beside L12 on the side stream) and
     with prioritized replay at batch 4096 (config 3: the PER sampler on the side stream)."""
     from sacmi import _lib as L
     replay = "uniform"
@@ -503,6 +504,8 @@ def test_many_updates_per_launch_identical(shape):
         cfg, B, nrows, dt, replay = SacConfig(376, 17, 512), 4096, 9000, "fp32", "per"
     else:
         cfg, B, nrows, dt = SacConfig(661, 23, 512), 4096, 6000, "bf16"
+        if shape.endswith("_set"):
+            nrows = 20000
     params = init_params(cfg, 61, bias_scale=0.05)
     rows = synthetic_rows(cfg, nrows, 62, state_scale=0.5)
     prio = np.random.default_rng(64).uniform(0.1, 2.0, nrows).astype(np.float32)
