@@ -99,6 +99,9 @@ __device__ __forceinline__ uint2 buf_ld2(rsrc_t r, uint32_t off) {
   const u2_t v = __builtin_bit_cast(u2_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
   return make_uint2(v.x, v.y);
 }
+__device__ __forceinline__ uint32_t buf_ld_u16(rsrc_t r, uint32_t off) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)off, 0, 0);
+}
 __device__ __forceinline__ unsigned short bf16_bits(float x) {
   return __builtin_bit_cast(unsigned short, (__bf16)x);
 }
@@ -139,22 +142,40 @@ __device__ __forceinline__ T gld_off(const char* base, uint32_t off) {
   return *reinterpret_cast<const T*>(base + off);
 }
 
-template <int NT, bool KC>
+// H16: the operand is stored as bf16 (K-contiguous only: the policy heads' input under
+// act16), fetched 4 k per 8-byte load and widened exactly to fp32
+template <int NT, bool KC, bool H16 = false>
 __device__ __forceinline__ void row_offs(const float* P, int ld, int row0, int nrows, int lane,
                                          OpFetch<NT>& f) {
+  static_assert(!H16 || KC, "bf16 operands are K-contiguous");
   f.r = make_rsrc(P, 0x7fffffffu);
   f.p = reinterpret_cast<const char*>(P);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     int row = row0 + t * 16 + (lane & 15);
     row = row < nrows ? row : nrows - 1;
-    f.off[t] = KC ? (uint32_t)row * (uint32_t)ld * 4u : (uint32_t)row * 4u;
+    f.off[t] = KC ? (uint32_t)row * (uint32_t)ld * (H16 ? 2u : 4u) : (uint32_t)row * 4u;
   }
 }
 
-template <int NT, bool KC>
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+template <int NT, bool KC, bool H16 = false>
 __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, int K,
                                          float (&v)[NT][4]) {
+  if constexpr (H16) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const uint32_t o = f.off[t] + (uint32_t)(k < K ? k : 0) * 2u;
+      const uint2 x = buf_ld2(f.r, o);
+      v[t][0] = (k < K) ? bf16_lo(x.x) : 0.f;
+      v[t][1] = (k + 1 < K) ? bf16_hi(x.x) : 0.f;
+      v[t][2] = (k + 2 < K) ? bf16_lo(x.y) : 0.f;
+      v[t][3] = (k + 3 < K) ? bf16_hi(x.y) : 0.f;
+    }
+    return;
+  }
 #ifdef SACMI_EXP_NOLOAD
   // timing experiment only: no operand loads at all (MFMA + epilogue floor)
 #pragma unroll
@@ -241,7 +262,8 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // registers then hold the second buffer instead).  Same chunk order per wave: bitwise
 // identical sums.
 template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
-          int AXF = 0, bool BF16 = false, int PIPE = 0, class Pre, class Early = void (*)()>
+          int AXF = 0, bool BF16 = false, int PIPE = 0, bool A16 = false, class Pre,
+          class Early = void (*)()>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
                                             float* rsum, Pre&& pre, bool store_a = false,
                                             Early&& early = [] {}) {
@@ -263,7 +285,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   for (int i = 0; i < MT; ++i) rs[i] = 0.f;
   OpFetch<MT> ra;
   OpFetch<NT> rb;
-  row_offs<MT, AKC>(d.A, d.lda, m0, d.M, lane, ra);
+  row_offs<MT, AKC, A16>(d.A, d.lda, m0, d.M, lane, ra);
   row_offs<NT, BKC>(d.B, d.ldb, n0, d.N, lane, rb);
   const int nch = (d.K + 15) >> 4;
   const int nmine = nch > ks ? (nch - ks + KSPLIT - 1) / KSPLIT : 0;
@@ -288,7 +310,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
     auto issue = [&](int jj, float (&av)[MT][4], float (&bv)[NT][4], float (&xv)[4]) {
       jj = jj < nmine ? jj : nmine - 1;   // unconditional: past the end re-reads the last chunk
       const int k = (ks + jj * KSPLIT) * 16 + kl;
-      fetch_op<MT, AKC>(ra, d.lda, k, d.K, av);
+      fetch_op<MT, AKC, A16>(ra, d.lda, k, d.K, av);
       fetch_op<NT, BKC>(rb, d.ldb, k, d.K, bv);
       if constexpr (!AKC) {
 #pragma unroll
@@ -340,7 +362,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       // chunk re-reads that chunk and is skipped below
       const int jj = j + g < nmine ? j + g : nmine - 1;
       const int k = (ks + jj * KSPLIT) * 16 + kl;
-      fetch_op<MT, AKC>(ra, d.lda, k, d.K, a[g]);
+      fetch_op<MT, AKC, A16>(ra, d.lda, k, d.K, a[g]);
       fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
       if constexpr (AXF == 1) {          // w3 rows are float4-aligned (parameter arena)
         const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
@@ -1019,6 +1041,13 @@ constexpr int kFBM = 128, kFBK = 32, kFPad = 4, kFBN128 = 128;
 #define SACMI_FWD_LDS16 1       // bf16 mode: k_fwd16 (bf16 LDS slabs, 16x16x32 MFMA)
 #endif
 
+__device__ __forceinline__ float swap_adj(float x) {   // lane ^ 1's x (DPP quad_perm 1,0,3,2)
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)bf16_bits(lo) | ((uint32_t)bf16_bits(hi) << 16);
+}
+
 // k_fwd / k_fwd16 epilogue: bias, ReLU, store, per-32-column fc3 dot partials.  A wave
 // owns a 64 x (16 NT) sub-tile at (r0, c0); lane holds D[row = (lane >> 4) * 4 + r]
 // [col = lane & 15] of each 16x16 tile.  The operands are loaded before the K loop.
@@ -1039,7 +1068,11 @@ struct FwdEpi {
     }
     dotb = buf_ld(rW, (uint32_t)N * 4u);
   }
-  __device__ __forceinline__ void store(const GemmDesc& d, const f4 (&acc)[4][NT], int r0, int c0,
+  // C16 (act16): C is bf16 — the fp32 values (the dot partials use them unrounded) are
+  // rounded once, and adjacent lanes swap one value (DPP) so every lane stores a column
+  // pair of one row as a 32-bit word: lane 2c row r4+rp, lane 2c+1 row r4+rp+1
+  template <bool C16 = false>
+  __device__ __forceinline__ void store(const GemmDesc& d, f4 (&acc)[4][NT], int r0, int c0,
                                         int lane) const {
     const int M = d.M, N = d.N;
     const bool has_bias = d.bias != nullptr, has_dot = d.dotp != nullptr;
@@ -1055,7 +1088,8 @@ struct FwdEpi {
           float v = acc[i][j][r];
           if (has_bias) v += bias_x[j];
           if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
-          if (row < M && col < N) st_big(d.C + (size_t)row * d.ldc + col, v);
+          if constexpr (C16) acc[i][j][r] = v;
+          else if (row < M && col < N) st_big(d.C + (size_t)row * d.ldc + col, v);
           if (has_dot) {
             // fc3 dot partial over the 32-column block (tiles j, j+1): 16 lanes per tile,
             // summed by DPP row rotations (VALU; the ds_bpermute butterfly it replaces
@@ -1074,6 +1108,23 @@ struct FwdEpi {
           }
         }
       }
+    }
+    if constexpr (C16) {
+      unsigned short* C = reinterpret_cast<unsigned short*>(d.C);
+      const bool odd = lane & 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int rp = 0; rp < 4; rp += 2) {
+            const float a0 = acc[i][j][rp], a1 = acc[i][j][rp + 1];
+            const float b0 = swap_adj(a0), b1 = swap_adj(a1);
+            const int row = r0 + i * 16 + (lane >> 4) * 4 + rp + (odd ? 1 : 0);
+            const int col = c0 + j * 16 + (lane & 14);
+            const uint32_t w = odd ? pack_bf16x2(b1, a1) : pack_bf16x2(a0, b0);
+            if (row < M && col < N) st_big(reinterpret_cast<uint32_t*>(C + (size_t)row * d.ldc + col), w);
+          }
     }
   }
 };
@@ -1198,7 +1249,8 @@ __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
   return __builtin_bit_cast(u2v, x);
 }
 
-template <int kFBN, bool BH = false>
+// AH (act16): A is bf16 (4 k per 8-byte load, straight into the slab) and C is bf16
+template <int kFBN, bool BH = false, bool AH = false>
 __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_FWD16);
   constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
@@ -1236,7 +1288,7 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int ra = min(m0 + tid / TPR + RPP * i, M - 1);
-    offA[i] = (uint32_t)ra * (uint32_t)d.lda * 4u;
+    offA[i] = (uint32_t)ra * (uint32_t)d.lda * (AH ? 2u : 4u);
   }
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
@@ -1244,7 +1296,8 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
     offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
   }
   const int kq = 4 * (tid % TPR);
-  float4 ga[NA], gb[BH ? 1 : NB];
+  float4 ga[AH ? 1 : NA], gb[BH ? 1 : NB];
+  uint2 gah[AH ? NA : 1];             // AH: A rows in bf16, 4 k per 8 bytes
   uint2 gh[BH ? NB : 1];              // BH: B from its bf16 shadow, 4 k per 8 bytes
   const rsrc_t rBh = make_rsrc(BH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
   auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
@@ -1259,8 +1312,13 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
   auto gload = [&](int k0) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
+    if constexpr (AH) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+      for (int i = 0; i < NA; ++i) gah[i] = zkh(buf_ld2(rA, offA[i] + ko / 2u), k);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+    }
     if constexpr (BH) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) gh[i] = zkh(buf_ld2(rBh, offB[i] / 2u + ko / 2u), k);
@@ -1271,7 +1329,10 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(ga[i]);
+    for (int i = 0; i < NA; ++i) {
+      if constexpr (AH) *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = u2v{gah[i].x, gah[i].y};
+      else *reinterpret_cast<u2v*>(&sA[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(ga[i]);
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (BH) *reinterpret_cast<u2v*>(&sB[buf][tid / TPR + RPP * i][kq]) = u2v{gh[i].x, gh[i].y};
@@ -1309,7 +1370,7 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
     swrite(cur ^ 1);
     __syncthreads();
   }
-  ep.store(d, acc, m0 + wm, n0 + wn, lane);
+  ep.template store<AH>(d, acc, m0 + wm, n0 + wn, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1493,6 +1554,8 @@ __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
       (__attribute__((address_space(3))) s4t*)(p));
 }
 
+// X16 (act16): the B operand (X: activations / minibatch inputs) is bf16
+template <bool X16 = false>
 __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_PART16);
   constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
@@ -1541,7 +1604,8 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
   const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
   const bool want_rs = d.rs_col >= 0 && n0 == 0;
-  float4 ga[8], gb[8];
+  float4 ga[8], gb[X16 ? 1 : 8];
+  uint2 gbh[X16 ? 8 : 1];
   float rs4[4] = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](int k0) {
 #pragma unroll
@@ -1555,17 +1619,25 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
       x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
       x.z = kin && m0 + c4 + 2 < M ? x.z * f : 0.f; x.w = kin && m0 + c4 + 3 < M ? x.w * f : 0.f;
       ga[i] = x;
-      float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
-      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
-      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
-      gb[i] = y;
+      if constexpr (X16) {
+        uint2 h = buf_ld2(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 2u);
+        h.x = (kin && n0 + c4 < N ? h.x & 0xffffu : 0u) | (kin && n0 + c4 + 1 < N ? h.x & 0xffff0000u : 0u);
+        h.y = (kin && n0 + c4 + 2 < N ? h.y & 0xffffu : 0u) | (kin && n0 + c4 + 3 < N ? h.y & 0xffff0000u : 0u);
+        gbh[i] = h;
+      } else {
+        float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
+        y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+        y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+        gb[i] = y;
+      }
     }
   };
   auto swrite = [&](int buf, bool fresh) {   // fresh: a slab not staged before
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       *reinterpret_cast<u2v*>(&sA[buf][kr0 + 8 * i][c4]) = pack_bf16x4(ga[i]);
-      *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+      if constexpr (X16) *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = u2v{gbh[i].x, gbh[i].y};
+      else *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
     }
     if (want_rs && fresh) {
 #pragma clang fp contract(off)
@@ -1658,7 +1730,9 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
 // model2 L5b / L9b / L11), no transform, no prologue.
 constexpr int kXBM = 64, kXBN = 128, kXBK = 64;
 
-template <bool AX, bool BH = false>
+// ACT16 (act16 updates): the ReLU-mask source (aux) is bf16, and so is A where it is the
+// activation whose sign the transform reads (AX); the plain levels' A is a gradient, fp32
+template <bool AX, bool BH = false, bool ACT16 = false>
 __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_AXK16);
   constexpr int LDA_ = kXBK + 8;        // [row][k] bf16, 144-B rows
@@ -1702,9 +1776,10 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
   // (t >> 5) + 8 i (i < 8) at columns 4 (t & 31)
   const int kq = 4 * (tid & 15), c4 = 4 * (tid & 31), kr0 = tid >> 5;
   uint32_t offA[4];
+  constexpr bool A16 = AX && ACT16;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    offA[i] = (uint32_t)min(m0 + (tid >> 4) + 16 * i, M - 1) * (uint32_t)d.lda * 4u;
+    offA[i] = (uint32_t)min(m0 + (tid >> 4) + 16 * i, M - 1) * (uint32_t)d.lda * (A16 ? 2u : 4u);
   const int nb = min(n0 + c4, N - 1);
   float4 ga[4], gb[BH ? 1 : 8], gw;
   uint2 gh[BH ? 8 : 1];               // BH: W from its bf16 shadow
@@ -1713,7 +1788,14 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ga[i] = buf_ld4(rA, offA[i] + ko);
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (A16) {   // (only the sign is read: exact widening)
+        const uint2 h = buf_ld2(rA, offA[i] + ko / 2u);
+        ga[i] = make_float4(bf16_lo(h.x), bf16_hi(h.x), bf16_lo(h.y), bf16_hi(h.y));
+      } else {
+        ga[i] = buf_ld4(rA, offA[i] + ko);
+      }
+    }
     gw = buf_ld4(rW, ko);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -1768,7 +1850,8 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
   if constexpr (AX) rows_load<kXBM, 256>(batch.rows, d, m0, rows_x);
   float hm[2][4][4];
   {
-    const rsrc_t rX = make_rsrc(d.aux, (uint32_t)(((size_t)(M - 1) * d.ldaux + N) * 4));
+    constexpr uint32_t xe = ACT16 ? 2u : 4u;   // mask-source element bytes
+    const rsrc_t rX = make_rsrc(d.aux, (uint32_t)(((size_t)(M - 1) * d.ldaux + N) * xe));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1777,7 +1860,8 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int col = n0 + wn + j * 16 + (lane & 15);
-          hm[i][j][r] = buf_ld(rX, row < M && col < N ? (uint32_t)(row * d.ldaux + col) * 4u : 0xfffffff0u);
+          const uint32_t off = row < M && col < N ? (uint32_t)(row * d.ldaux + col) * xe : 0xfffffff0u;
+          hm[i][j][r] = ACT16 ? bf16_lo(buf_ld_u16(rX, off)) : buf_ld(rX, off);
         }
       }
   }
@@ -1845,7 +1929,7 @@ static int axk16_ok(GemmBatch& b) {
     if (d.axk != ax || !d.a_kc || d.b_kc || d.epi != EPI_MASK || d.bias || d.dotp || d.a_ksc ||
         d.rs_col >= 0)
       return -1;
-    if (((uintptr_t)d.A & 15) || (d.lda & 3) || ((uintptr_t)d.B & 15) || (d.ldb & 3) ||
+    if (((uintptr_t)d.A & (d.a16 ? 7 : 15)) || (d.lda & 3) || ((uintptr_t)d.B & 15) || (d.ldb & 3) ||
         (ax && ((uintptr_t)d.ax_w & 15)) || (d.N & 3))
       return -1;
   }
@@ -1931,6 +2015,14 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
   }
 }
 
+// 1 when the level carries bf16 activation operands (any GemmDesc a16 / b16 / c16 / x16);
+// each kernel that takes them checks the per-desc pattern it supports
+static int level_act16(const GemmBatch& b) {
+  int any = 0;
+  for (int i = 0; i < b.count; ++i) any |= b.d[i].a16 | b.d[i].b16 | b.d[i].c16 | b.d[i].x16;
+  return any ? 1 : 0;
+}
+
 // bf16 deep-K weight-gradient levels: split count and workspace need, or 0 (old path)
 static int dw_split_plan(GemmBatch& b, int64_t* stride) {
   // (rides: the gather on any split-K kernel, the sampler on k_dw_part16 only)
@@ -1971,7 +2063,7 @@ static bool fwd_big_ok(GemmBatch& b) {
   for (int i = 0; i < b.count; ++i) {
     const GemmDesc& d = b.d[i];
     if (!d.a_kc || !d.b_kc || d.axk || d.a_ksc || d.rs_col >= 0) return false;
-    if (((uintptr_t)d.A & 15) || (d.lda & 3) || ((uintptr_t)d.B & 15) || (d.ldb & 3)) return false;
+    if (((uintptr_t)d.A & (d.a16 ? 7 : 15)) || (d.lda & 3) || ((uintptr_t)d.B & 15) || (d.ldb & 3)) return false;
     if (d.epi != EPI_RELU && d.epi != EPI_STORE) return false;
     if (d.dotp && (d.N % 32)) return false;
   }
@@ -2012,7 +2104,14 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
           mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > (size_t)kDw16LdsBytes)
         throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_dw_part16's LDS"};
       const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
-      if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16, dim3(grid), dim3(256), 0, s, b, ns, stride);
+      const int form = level_act16(b);   // act16: every X operand bf16
+      for (int i = 0; i < b.count; ++i)
+        if (b.d[i].a16 || b.d[i].c16 || b.d[i].x16 || (form && !b.d[i].b16) || form < 0)
+          throw Error{SACMI_ESTATE, "split-K weight gradient: unsupported bf16 activation operand"};
+      if (form && !(b.bf16 && SACMI_DW_LDS16))
+        throw Error{SACMI_ESTATE, "bf16 activation operands need k_dw_part16"};
+      if (b.bf16 && SACMI_DW_LDS16 && form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
+      else if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
@@ -2031,10 +2130,25 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
         if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a k_axk16 level"};
       const bool bh = all_bh(b);
       const dim3 grid(b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0));
-      if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true>), grid, dim3(256), 0, s, b);
-      else if (ax) hipLaunchKernelGGL((k_axk16<true, false>), grid, dim3(256), 0, s, b);
-      else if (bh) hipLaunchKernelGGL((k_axk16<false, true>), grid, dim3(256), 0, s, b);
-      else hipLaunchKernelGGL((k_axk16<false, false>), grid, dim3(256), 0, s, b);
+      const int form = level_act16(b);   // act16: mask sources (and AX sources) bf16
+      if (form < 0) throw Error{SACMI_ESTATE, "k_axk16 level with mixed bf16 activation flags"};
+      for (int i = 0; i < b.count; ++i)
+        if (b.d[i].c16 || b.d[i].b16 || b.d[i].x16 != form || b.d[i].a16 != (form && b.d[i].axk == 1))
+          throw Error{SACMI_ESTATE, "k_axk16: unsupported bf16 activation operand"};
+      if (form) {
+        if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true, true>), grid, dim3(256), 0, s, b);
+        else if (ax) hipLaunchKernelGGL((k_axk16<true, false, true>), grid, dim3(256), 0, s, b);
+        else if (bh) hipLaunchKernelGGL((k_axk16<false, true, true>), grid, dim3(256), 0, s, b);
+        else hipLaunchKernelGGL((k_axk16<false, false, true>), grid, dim3(256), 0, s, b);
+      } else if (ax && bh) {
+        hipLaunchKernelGGL((k_axk16<true, true>), grid, dim3(256), 0, s, b);
+      } else if (ax) {
+        hipLaunchKernelGGL((k_axk16<true, false>), grid, dim3(256), 0, s, b);
+      } else if (bh) {
+        hipLaunchKernelGGL((k_axk16<false, true>), grid, dim3(256), 0, s, b);
+      } else {
+        hipLaunchKernelGGL((k_axk16<false, false>), grid, dim3(256), 0, s, b);
+      }
       HIP_LAUNCH_CHECK();
       return;
     }
@@ -2044,6 +2158,18 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (fwd_big && fwd_big_ok(b)) {
     const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
     const bool bh = b.bf16 && all_bh(b);
+    if (level_act16(b)) {   // act16: bf16 input rows and bf16 output (k_fwd16 only)
+      for (int i = 0; i < b.count; ++i)
+        if (!b.d[i].a16 || !b.d[i].c16 || b.d[i].b16 || b.d[i].x16 || (b.d[i].N & 1) || (b.d[i].ldc & 1))
+          throw Error{SACMI_ESTATE, "k_fwd16: unsupported bf16 activation operands"};
+      if (!(b.bf16 && SACMI_FWD_LDS16)) throw Error{SACMI_ESTATE, "bf16 activations need k_fwd16"};
+      if (n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      else if (bh) hipLaunchKernelGGL((k_fwd16<64, true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      else if (n128) hipLaunchKernelGGL((k_fwd16<128, false, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      else hipLaunchKernelGGL((k_fwd16<64, false, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      HIP_LAUNCH_CHECK();
+      return;
+    }
     if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16 && bh) hipLaunchKernelGGL((k_fwd16<64, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(256), 0, s, b);
@@ -2055,6 +2181,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     return;
   }
   b = b0;
+  if (level_act16(b))
+    throw Error{SACMI_ESTATE, "bf16 activation operands on a level outside the batch-4096-class kernels"};
   const int extra = b.ride.kind ? b.ride.nblocks : 0;
   if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > kRideLdsBytes)
     throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_gemm's LDS"};
@@ -2162,7 +2290,9 @@ __device__ __forceinline__ float one_minus_tanh2(float x) {
 // ---------------------------------------------------------------------------
 // policy heads (mean | log_std) GEMM + GaussianPolicy.sample epilogue
 // (networks_model1.py:65-99, torch distributions/normal.py:83-103)
-template <int TN, int KSPLIT>
+// H16 (act16 updates): h is bf16 (widened exactly; Wh fp32, fp32 MFMAs) and the actions
+// go to act as bf16 (the next levels' input columns)
+template <int TN, int KSPLIT, bool H16 = false>
 __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) {
   const TlMark tl_mark(a.tl, TL_HEADS);
   constexpr int TM = 16;
@@ -2188,7 +2318,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
     eps_in = buf_ld(make_rsrc(want ? a.eps : a.Wh, want ? 0x7fffffffu : 0u),
                     (uint32_t)((size_t)mm * A + jj) * 4u);
   };
-  gemm_core_l<TM, TN, KSPLIT, 2, true, true, false>(d, m0, 0, red, nullptr, pre);
+  gemm_core_l<TM, TN, KSPLIT, 2, true, true, false, 1, 0, false, 0, H16>(d, m0, 0, red, nullptr, pre);
   __syncthreads();
   const uint64_t ctr = a.ctr_override ? a.ctr_override : a.sc->noise_counter;
   if (e < TM * A) {
@@ -2209,7 +2339,10 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       }
       const float x = a.deterministic ? mean : mean + eps * sd;
       const float y = tanhf(x);
-      a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
+      if constexpr (H16)
+        reinterpret_cast<unsigned short*>(a.act)[(size_t)m * a.ldact + j] = bf16_bits(y * a.scale + a.bias);
+      else
+        a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
       if (a.act_host) a.act_host[(size_t)m * A + j] = y * a.scale + a.bias;
       const float dx = x - mean;
       lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
@@ -2244,10 +2377,13 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   }
 }
 
+// rows of `cols` floats in, and the constant-1 column right after them (a batch-4096 bf16
+// update may have overwritten the fp32 layout's ones column: the buffers are shared)
 __global__ void k_rows_in(float* dst, int ldd, const float* src, int lds, int cols) {
   const float* s = src + (size_t)blockIdx.x * lds;
   float* d = dst + (size_t)blockIdx.x * ldd;
   for (int c = threadIdx.x; c < cols; c += blockDim.x) d[c] = s[c];
+  if (threadIdx.x == 0) d[cols] = 1.f;
 }
 
 void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int cols, hipStream_t s) {
@@ -2270,12 +2406,17 @@ void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {
   const int grid = (a.rows + 15) / 16;
   const int n = 2 * a.A;
-  if (n <= 32)
+  if (a.h16) {
+    if (n <= 32) hipLaunchKernelGGL((k_heads_sample<32, 16, true>), dim3(grid), dim3(1024), 0, s, a);
+    else if (n <= 48) hipLaunchKernelGGL((k_heads_sample<48, 16, true>), dim3(grid), dim3(1024), 0, s, a);
+    else hipLaunchKernelGGL((k_heads_sample<64, 16, true>), dim3(grid), dim3(1024), 0, s, a);
+  } else if (n <= 32) {
     hipLaunchKernelGGL((k_heads_sample<32, 16>), dim3(grid), dim3(1024), 0, s, a);
-  else if (n <= 48)
+  } else if (n <= 48) {
     hipLaunchKernelGGL((k_heads_sample<48, 16>), dim3(grid), dim3(1024), 0, s, a);
-  else
+  } else {
     hipLaunchKernelGGL((k_heads_sample<64, 16>), dim3(grid), dim3(1024), 0, s, a);
+  }
   HIP_LAUNCH_CHECK();
 }
 
@@ -2287,7 +2428,7 @@ void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {
 // (the Normal.log_prob quadratic term's gradients w.r.t. mean and std cancel
 // exactly: x - mean = eps*std).
 // NST: k-steps (of 4) of the dhp2 tail's K = 2A, a compile-time bound
-template <int TM, int TN, int KSPLIT, int NST>
+template <int TM, int TN, int KSPLIT, int NST, bool H16 = false>
 __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, SampleBwdArgs a) {
   const TlMark tl_mark(a.tl, TL_SAMPLE_BWD);
   __shared__ float red[KSPLIT * TM * (TN + 1)];
@@ -2317,7 +2458,8 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
       for (int r = 0; r < 4; ++r) {
         const int mr = m0 + (lane >> 4) * 4 + r;
         const bool ok = mr < d.M && n < a.H;
-        const float x = a.hp2[ok ? (size_t)mr * a.ldh + n : 0];
+        const size_t ix = ok ? (size_t)mr * a.ldh + n : 0;
+        const float x = H16 ? bf16_lo(reinterpret_cast<const unsigned short*>(a.hp2)[ix]) : a.hp2[ix];
         mk[t][r] = ok ? x : 0.f;
       }
     }
@@ -2390,10 +2532,11 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_gemm_sample_bwd(GemmDesc d, Sam
 
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s) {
   const int grid = (d.M + 15) / 16;
-  if ((2 * a.A + 3) / 4 <= 10)
-    hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 10>), dim3(grid), dim3(1024), 0, s, d, a);
-  else
-    hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 16>), dim3(grid), dim3(1024), 0, s, d, a);
+  const bool n10 = (2 * a.A + 3) / 4 <= 10;
+  if (a.hp2_16 && n10) hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 10, true>), dim3(grid), dim3(1024), 0, s, d, a);
+  else if (a.hp2_16) hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 16, true>), dim3(grid), dim3(1024), 0, s, d, a);
+  else if (n10) hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 10>), dim3(grid), dim3(1024), 0, s, d, a);
+  else hipLaunchKernelGGL((k_gemm_sample_bwd<16, 32, 16, 16>), dim3(grid), dim3(1024), 0, s, d, a);
   HIP_LAUNCH_CHECK();
 }
 
@@ -2493,6 +2636,7 @@ __global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_
 void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, hipStream_t s) {
   if (2 * a.A > 64 || kTailRows * a.A > 256 || n_pa > kTailMaxPa)
     throw Error{SACMI_EVALUE, "sample backward tail: unsupported action_dim / hidden_dim"};
+  if (a.hp2_16) throw Error{SACMI_ESTATE, "sample backward tail: bf16 hp2 not supported"};
   const dim3 grid((a.B + kTailRows - 1) / kTailRows, (a.H + kTailCols - 1) / kTailCols);
   hipLaunchKernelGGL(k_sample_bwd_tail, grid, dim3(256), 0, s, pa, n_pa, a);
   HIP_LAUNCH_CHECK();

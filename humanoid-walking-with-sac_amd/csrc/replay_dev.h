@@ -217,9 +217,43 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
 
 // One replay row b into the minibatch buffers (replay_buffer.py:13-19 stacking):
 // xq[b] = [s | 1 | a], x2[b] = [s2 | 1 | .], x2[B+b] = [s | 1 | .], r[b], d[b].
-// Lanes lane, lane+nl, ... of the caller share the row.
+// Lanes lane, lane+nl, ... of the caller share the row.  x16 (act16 updates): the rows
+// are bf16 (rounded once here: every consumer rounds its operands to bf16 anyway).  The
+// ones column is written with the row (the two layouts share the buffers).
+__device__ __forceinline__ void gather_row16(const GatherArgs& a, int64_t slot, int b, int lane, int nl) {
+  const float* so = a.obs + slot * a.ldo;
+  const float* s2 = a.obs2 + slot * a.ldo;
+  const float* ac = a.act + slot * a.lda_;
+  const uint32_t oq = (uint32_t)((size_t)b * a.ldx) * 2u, ot = oq;
+  const uint32_t oa = (uint32_t)((size_t)(a.B + b) * a.ldx) * 2u;
+  const int s4 = a.S >> 2;
+  for (int q = lane; q < s4; q += nl) {
+    const float4 v = reinterpret_cast<const float4*>(so)[q];
+    const float4 w = reinterpret_cast<const float4*>(s2)[q];
+    const uint32_t vl = f2bf2(v.x, v.y), vh = f2bf2(v.z, v.w);
+    st_wt8(a.xq, oq + 8u * q, vl, vh);
+    st_wt8(a.x2, oa + 8u * q, vl, vh);
+    st_wt8(a.x2, ot + 8u * q, f2bf2(w.x, w.y), f2bf2(w.z, w.w));
+  }
+  for (int q = 4 * s4 + lane; q < a.S; q += nl) {
+    const unsigned short v = f2bf(so[q]);
+    st_wt2(a.xq, oq + 2u * q, v); st_wt2(a.x2, oa + 2u * q, v); st_wt2(a.x2, ot + 2u * q, f2bf(s2[q]));
+  }
+  for (int j = lane; j < a.A; j += nl) st_wt2(a.xq, oq + 2u * (a.S + 1 + j), f2bf(ac[j]));
+  if (lane == 0) {
+    st_wt2(a.xq, oq + 2u * a.S, kBf16One); st_wt2(a.x2, oa + 2u * a.S, kBf16One);
+    st_wt2(a.x2, ot + 2u * a.S, kBf16One);
+    st_wt(a.r + b, a.rew[slot]);
+    st_wt(a.d + b, a.done[slot]);
+  }
+}
+
 __device__ __forceinline__ void gather_row(const GatherArgs& a, int b, int lane, int nl) {
   const int64_t slot = a.by_slot ? (int64_t)a.idx[b] : (a.sc->head + (int64_t)a.idx[b]) % a.capacity;
+  if (a.x16) {
+    gather_row16(a, slot, b, lane, nl);
+    return;
+  }
   const float* so = a.obs + slot * a.ldo;
   const float* s2 = a.obs2 + slot * a.ldo;
   const float* ac = a.act + slot * a.lda_;
@@ -245,6 +279,7 @@ __device__ __forceinline__ void gather_row(const GatherArgs& a, int b, int lane,
   }
   for (int j = lane; j < a.A; j += nl) st_wt(xq + a.S + 1 + j, ac[j]);
   if (lane == 0) {
+    st_wt(xq + a.S, 1.f); st_wt(xa + a.S, 1.f); st_wt(xt + a.S, 1.f);
     st_wt(a.r + b, a.rew[slot]);
     st_wt(a.d + b, a.done[slot]);
   }
@@ -289,6 +324,36 @@ __device__ __forceinline__ void gather_rows_wave(const GatherArgs& a, int b0, in
     rv[i] = a.rew[slot[i]];
     dv[i] = a.done[slot[i]];
   }
+  if (a.x16) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int b = b0 + i * bstep;
+      if (b >= a.B) break;
+      const uint32_t oq = (uint32_t)((size_t)b * a.ldx) * 2u, ot = oq;
+      const uint32_t oa = (uint32_t)((size_t)(a.B + b) * a.ldx) * 2u;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int qq = lane + 64 * q;
+        if (qq < s4) {
+          const uint32_t vl = f2bf2(v[i][q].x, v[i][q].y), vh = f2bf2(v[i][q].z, v[i][q].w);
+          st_wt8(a.xq, oq + 8u * qq, vl, vh);
+          st_wt8(a.x2, oa + 8u * qq, vl, vh);
+          st_wt8(a.x2, ot + 8u * qq, f2bf2(w[i][q].x, w[i][q].y), f2bf2(w[i][q].z, w[i][q].w));
+        }
+      }
+      if (lane < st) {
+        st_wt2(a.xq, oq + 2u * jt, f2bf(tv[i])); st_wt2(a.x2, oa + 2u * jt, f2bf(tv[i]));
+        st_wt2(a.x2, ot + 2u * jt, f2bf(tw[i]));
+      }
+      if (lane < a.A) st_wt2(a.xq, oq + 2u * (a.S + 1 + lane), f2bf(av[i]));
+      if (lane == 0) {
+        st_wt2(a.xq, oq + 2u * a.S, kBf16One); st_wt2(a.x2, oa + 2u * a.S, kBf16One);
+        st_wt2(a.x2, ot + 2u * a.S, kBf16One);
+        st_wt(a.r + b, rv[i]); st_wt(a.d + b, dv[i]);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int b = b0 + i * bstep;
@@ -309,7 +374,10 @@ __device__ __forceinline__ void gather_rows_wave(const GatherArgs& a, int b0, in
     float* xa = a.x2 + (size_t)(a.B + b) * a.ldx;
     if (lane < st) { st_wt(xq + jt, tv[i]); st_wt(xa + jt, tv[i]); st_wt(xt + jt, tw[i]); }
     if (lane < a.A) st_wt(xq + a.S + 1 + lane, av[i]);
-    if (lane == 0) { st_wt(a.r + b, rv[i]); st_wt(a.d + b, dv[i]); }
+    if (lane == 0) {
+      st_wt(xq + a.S, 1.f); st_wt(xa + a.S, 1.f); st_wt(xt + a.S, 1.f);
+      st_wt(a.r + b, rv[i]); st_wt(a.d + b, dv[i]);
+    }
   }
 }
 

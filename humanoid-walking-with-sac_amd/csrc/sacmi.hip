@@ -431,21 +431,28 @@ static void check_span(const void* p, int64_t max_index, const char* what, int e
 static void validate(const GemmDesc& d) {
   if (d.M <= 0 || d.N <= 0 || d.K <= 0) throw Error{SACMI_ESTATE, "empty GEMM"};
   const int64_t klast = ((int64_t)(d.K - 1) / 4) * 4 + 3;
+  // element bytes: bf16 activation operands (act16) are read 4 elements = 8 bytes at a time
+  const int ea = d.a16 ? 2 : 4, eb = d.b16 ? 2 : 4, ec = d.c16 ? 2 : 4, ex = d.x16 ? 2 : 4;
   if (d.a_kc) {
-    if (((uintptr_t)d.A & 15) || (d.lda & 3)) throw Error{SACMI_ESTATE, "A misaligned"};
-    check_span(d.A, (int64_t)(d.M - 1) * d.lda + klast, "A");
+    if (((uintptr_t)d.A & (4 * ea - 1)) || (d.lda & 3)) throw Error{SACMI_ESTATE, "A misaligned"};
+    check_span(d.A, (int64_t)(d.M - 1) * d.lda + klast, "A", ea);
   } else {
     // MN-contiguous operands are read 4 columns wide from a 4-aligned start (the split-K
     // dW kernels): the span covers the last such group
+    REQUIRE(!d.a16, SACMI_ESTATE, "bf16 A operands are K-contiguous");
     check_span(d.A, (int64_t)(d.K - 1) * d.lda + ((d.M - 1) & ~3) + 3, "A");
   }
   if (d.b_kc) {
+    REQUIRE(!d.b16, SACMI_ESTATE, "bf16 B operands are row-contiguous (weight-gradient X)");
     if (((uintptr_t)d.B & 15) || (d.ldb & 3)) throw Error{SACMI_ESTATE, "B misaligned"};
     check_span(d.B, (int64_t)(d.N - 1) * d.ldb + klast, "B");
   } else {
-    check_span(d.B, (int64_t)(d.K - 1) * d.ldb + ((d.N - 1) & ~3) + 3, "B");
+    if (d.b16 && (((uintptr_t)d.B & 7) || (d.ldb & 3))) throw Error{SACMI_ESTATE, "B misaligned"};
+    check_span(d.B, (int64_t)(d.K - 1) * d.ldb + ((d.N - 1) & ~3) + 3, "B", eb);
   }
-  if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C");
+  if (d.c16) REQUIRE(d.rs_col < 0 && d.epi < EPI_ADAM && ((uintptr_t)d.C & 3) == 0 && d.N % 2 == 0 && d.ldc % 2 == 0,
+                     SACMI_ESTATE, "bf16 C: a forward output of even width");
+  if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C", ec);
   if (d.bias) check_span(d.bias, (int64_t)(d.N - 1) * d.bias_ld, "bias");
   REQUIRE(!(d.bias && d.epi == EPI_MASK), SACMI_ESTATE, "GEMM epilogue: bias and mask are exclusive");
   if (d.axk) {
@@ -464,7 +471,8 @@ static void validate(const GemmDesc& d) {
     check_span(d.dotw, d.N, "dotw");      // w3 and the head bias w3~[N]
     check_span(d.dotp, (int64_t)(d.M - 1) * d.dotp_ld + (d.N - 1) / 32, "dotp");
   }
-  if (d.epi == EPI_MASK) check_span(d.aux, (int64_t)(d.M - 1) * d.ldaux + d.N - 1, "aux");
+  if (d.epi == EPI_MASK) check_span(d.aux, (int64_t)(d.M - 1) * d.ldaux + d.N - 1, "aux", ex);
+  else REQUIRE(!d.x16, SACMI_ESTATE, "bf16 mask source without a mask epilogue");
 }
 
 // The level-wide operands launch_gemm may route a level's work through, checked once the
@@ -521,19 +529,19 @@ static double level_flops(const GemmBatch& b) {
 // epilogue's own operands (ReLU-mask source, bias) read once, and for a fused Adam the
 // optimizer state (param, exp_avg, exp_avg_sq [+ target]) read and written once.
 static double level_bytes(const GemmBatch& b) {
-  double n = 0;
+  double n = 0;    // bytes
   for (int i = 0; i < b.count; ++i) {
     const GemmDesc& d = b.d[i];
     const double out = (double)d.M * (d.N + (d.rs_col >= 0 ? 1 : 0));
-    n += (double)d.M * d.K + (double)d.N * d.K;
+    n += (double)d.M * d.K * (d.a16 ? 2 : 4) + (double)d.N * d.K * (d.b16 ? 2 : 4);
     if (d.epi >= EPI_ADAM) {
-      n += out * (d.epi == EPI_ADAM_POLYAK ? 8 : 6) + (b.adam.G ? out : 0);
+      n += 4.0 * (out * (d.epi == EPI_ADAM_POLYAK ? 8 : 6) + (b.adam.G ? out : 0));
     } else {
-      n += out + (d.epi == EPI_MASK ? out : 0) + (d.bias ? d.N : 0);
+      n += out * (d.c16 ? 2 : 4) + (d.epi == EPI_MASK ? out * (d.x16 ? 2 : 4) : 0) + (d.bias ? 4.0 * d.N : 0);
     }
-    if (d.pa_out) n += (double)d.N * d.pa_A + (double)d.M * ((d.N + 31) / 32) * d.pa_A;
+    if (d.pa_out) n += 4.0 * ((double)d.N * d.pa_A + (double)d.M * ((d.N + 31) / 32) * d.pa_A);
   }
-  return 4.0 * n;
+  return n;
 }
 
 // profiling mark: records an event BEFORE the launch it names
@@ -607,6 +615,19 @@ static MtSampleArgs mt_args(sacmi_ctx* c, int B, const BatchBufs& bb) {
   return m;
 }
 
+// bf16 activations (act16): in bf16 mode at the batch-4096 class, every activation the
+// update produces (hidden layers, minibatch rows, the sampled actions) is stored as bf16
+// — every consumer rounds its MFMA operands to bf16 anyway, the ReLU masks read signs only,
+// and the critic head dots use the unrounded epilogue values — halving the activation
+// bytes written and staged.  Only the policy heads read values outside an MFMA operand:
+// they see h rounded (the oracle's emulation rounds the same operand).  Needs every level
+// on the batch-4096-class kernels (k_fwd16 / k_axk16 / k_dw_part16: launch_gemm refuses
+// anything else), so batch >= 4096 and hidden a multiple of 128, >= 512.
+static bool act16_on(const sacmi_ctx* c, int B) {
+  static const bool env = std::getenv("SACMI_NO_ACT16") == nullptr;
+  return env && c->bf16 && B >= 4096 && c->H >= 512 && c->H % 128 == 0;
+}
+
 static GatherArgs gather_args(sacmi_ctx* c, int B, const BatchBufs& bb, bool per) {
   GatherArgs g{};
   g.idx = bb.idx32; g.obs = c->obs.p; g.act = c->act.p; g.rew = c->rew.p; g.obs2 = c->obs2.p;
@@ -614,6 +635,7 @@ static GatherArgs gather_args(sacmi_ctx* c, int B, const BatchBufs& bb, bool per
   g.sc = c->sc.p; g.S = c->S; g.A = c->A; g.B = B; g.xq = bb.xq; g.x2 = bb.x2; g.ldx = c->Kx;
   g.r = bb.r; g.d = bb.d;
   g.by_slot = per ? 1 : 0;
+  g.x16 = act16_on(c, B) ? 1 : 0;
   return g;
 }
 
@@ -699,6 +721,15 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     if (b >= c->T.p && b < c->T.p + c->T.n) return c->Th.p + (b - c->T.p);
     return nullptr;
   };
+  // activation buffers: element offsets in the update's activation format
+  const bool act16 = act16_on(c, B);
+  const int a16 = act16 ? 1 : 0;
+  auto E = [&](float* base, size_t off) -> float* {
+    return act16 ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(base) + off) : base + off;
+  };
+  auto fw = [&](GemmDesc g) { g.a16 = a16; g.c16 = a16; return g; };        // forward level
+  auto dh = [&](GemmDesc g) { g.x16 = a16; g.a16 = g.axk == 1 ? a16 : 0; return g; };   // dh level
+  auto dwx = [&](GemmDesc g) { g.b16 = a16; return g; };                     // dW level (X)
   auto run = [&](Level& lv, const std::string& name) {
     lv.b.bf16 = c->bf16 ? 1 : 0;
     for (int i = 0; i < lv.b.count; ++i) lv.b.d[i].Bh = shadow(lv.b.d[i].B);
@@ -717,18 +748,18 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
 
     // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
     Level l1;
-    l1.add(gd(bb.x2, Kx, 1, W(c->p_fc[0]), c->p_fc[0].ld, 1, c->hp[0].p, Hd, 2 * B, H, S + 1, EPI_RELU));
+    l1.add(fw(gd(bb.x2, Kx, 1, W(c->p_fc[0]), c->p_fc[0].ld, 1, c->hp[0].p, Hd, 2 * B, H, S + 1, EPI_RELU)));
     for (int i = 0; i < 2; ++i)
-      l1.add(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, c->hq[0].p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+      l1.add(fw(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
     run(l1, "gemm_L1_fc1");
     // L2 (.. L2b): the remaining hidden layers (K = H, bias in the epilogue); the last one
     // also accumulates the critic head (fc3 / fc4) dot partials of q1 / q2 (slots 0 / 1)
     for (int l = 1; l < nh; ++l) {
       Level lv;
-      lv.add(gd_fwd_h(c->hp[l - 1].p, Hd, W(c->p_fc[l]), Hd, c->hp[l].p, Hd, 2 * B, H, H));
+      lv.add(fw(gd_fwd_h(c->hp[l - 1].p, Hd, W(c->p_fc[l]), Hd, c->hp[l].p, Hd, 2 * B, H, H)));
       for (int i = 0; i < 2; ++i) {
-        GemmDesc g = gd_fwd_h(c->hq[l - 1].p + i * Hd, 2 * Hd, W(q[i][l]), Hd, c->hq[l].p + i * Hd,
-                              2 * Hd, B, H, H);
+        GemmDesc g = fw(gd_fwd_h(E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd, W(q[i][l]), Hd,
+                                 E(c->hq[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
         lv.add(l == L ? with_dot(g, W(q[i][nh]), i) : g);
       }
       run(lv, l == 1 ? "gemm_L2_fc2" : "gemm_L2b_fc3");
@@ -737,7 +768,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     HeadSampleArgs hs{};
     hs.h = c->hp[L].p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
     hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = dev_eps; hs.seed = c->cfg.seed;
-    hs.sc = c->sc.p; hs.act = bb.x2 + S + 1; hs.ldact = Kx; hs.logp = c->logp.p;
+    hs.sc = c->sc.p; hs.act = E(bb.x2, (size_t)S + 1); hs.ldact = Kx; hs.logp = c->logp.p;
+    hs.h16 = a16;
     hs.cache = c->cache.p;
     hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
@@ -750,14 +782,14 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     {
       Level l3;
       for (int i = 0; i < 2; ++i)
-        l3.add(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, c->hqt[0].p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+        l3.add(fw(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, E(c->hqt[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
       run(l3, "gemm_L3_tgt_fc1");
     }
     for (int l = 1; l < nh; ++l) {
       Level lv;
       for (int i = 0; i < 2; ++i) {
-        GemmDesc g = gd_fwd_h(c->hqt[l - 1].p + i * Hd, 2 * Hd, Wt(q[i][l]), Hd, c->hqt[l].p + i * Hd,
-                              2 * Hd, B, H, H);
+        GemmDesc g = fw(gd_fwd_h(E(c->hqt[l - 1].p, (size_t)i * Hd), 2 * Hd, Wt(q[i][l]), Hd,
+                                 E(c->hqt[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
         lv.add(l == L ? with_dot(g, Wt(q[i][nh]), 2 + i) : g);
       }
       run(lv, l == 1 ? "gemm_L4_tgt_fc2" : "gemm_L4b_tgt_fc3");
@@ -770,10 +802,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     const bool fuse = phase_mask == 7;     // single-GPU update: Adam in the dW epilogues
     Level l5;
     for (int i = 0; i < 2; ++i) {
-      GemmDesc g = gd(c->hq[L].p + i * Hd, 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dhc[L - 1].p + i * H, 2 * H,
-                      B, H, H, EPI_MASK, c->hq[L - 1].p + i * Hd, 2 * Hd);
+      GemmDesc g = gd(E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dhc[L - 1].p + i * H, 2 * H,
+                      B, H, H, EPI_MASK, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd);
       g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]); g.ax_out = c->dhc[L].p + i * H; g.ax_ld = 2 * H;
-      l5.add(g);
+      l5.add(dh(g));
     }
     {
       RowsFuse& rf = l5.b.rows;
@@ -787,8 +819,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     for (int l = L - 1; l >= 1; --l) {
       Level lv;
       for (int i = 0; i < 2; ++i)
-        lv.add(gd(c->dhc[l].p + i * H, 2 * H, 1, W(q[i][l]), Hd, 0, c->dhc[l - 1].p + i * H, 2 * H,
-                  B, H, H, EPI_MASK, c->hq[l - 1].p + i * Hd, 2 * Hd));
+        lv.add(dh(gd(c->dhc[l].p + i * H, 2 * H, 1, W(q[i][l]), Hd, 0, c->dhc[l - 1].p + i * H, 2 * H,
+                     B, H, H, EPI_MASK, E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd)));
       run(lv, "gemm_L5b_critic_dh");
     }
     // L6: every critic weight gradient: into the gradient arena, or (fused) straight into
@@ -799,20 +831,20 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     const int wepi = fuse ? EPI_ADAM_POLYAK : EPI_STORE;
     Level l6;
     for (int i = 0; i < 2; ++i)
-      l6.add(gd(c->dhc[0].p + i * H, 2 * H, 0, bb.xq, Kx, 0, dst(q[i][0]), Kx, H, S + A + 1, B,
-                wepi, nullptr, 0, 1 + i));
+      l6.add(dwx(gd(c->dhc[0].p + i * H, 2 * H, 0, bb.xq, Kx, 0, dst(q[i][0]), Kx, H, S + A + 1, B,
+                    wepi, nullptr, 0, 1 + i)));
     for (int i = 0; i < 2; ++i) {
       for (int l = 1; l < L; ++l)
-        l6.add(gd_dw_h(c->dhc[l].p + i * H, 2 * H, c->hq[l - 1].p + i * Hd, 2 * Hd, dst(q[i][l]), Hd,
-                       H, H, B, wepi, 1 + i));
+        l6.add(dwx(gd_dw_h(c->dhc[l].p + i * H, 2 * H, E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd,
+                           dst(q[i][l]), Hd, H, H, B, wepi, 1 + i)));
       // L5 stored u = dh[L] / coef (the coefficient factored out of its rows): the layer-L
       // weight gradient applies coef = dL/dq_i (dq) as a per-batch-row K-scale
-      GemmDesc wl = gd_dw_h(c->dhc[L].p + i * H, 2 * H, c->hq[L - 1].p + i * Hd, 2 * Hd, dst(q[i][L]),
-                            Hd, H, H, B, wepi, 1 + i);
+      GemmDesc wl = dwx(gd_dw_h(c->dhc[L].p + i * H, 2 * H, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd,
+                                dst(q[i][L]), Hd, H, H, B, wepi, 1 + i));
       wl.a_ksc = c->dq.p + i * B;
       l6.add(wl);
-      l6.add(gd_dw_h(c->dq.p + i * B, 1, c->hq[L].p + i * Hd, 2 * Hd, dst(q[i][nh]), Hd, 1, H, B,
-                     wepi, 1 + i));
+      l6.add(dwx(gd_dw_h(c->dq.p + i * B, 1, E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, dst(q[i][nh]), Hd, 1, H, B,
+                         wepi, 1 + i)));
     }
     if (fuse) {
       AdamFuse& f = l6.b.adam;
@@ -862,18 +894,18 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     }
    }
     // L7/L8 (.. L8b): updated critics on [s|1|a~] (head dot partials: slots 4 / 5)
-    const float* xa = bb.x2 + (size_t)B * Kx;
+    const float* xa = E(bb.x2, (size_t)B * Kx);
     {
       Level l7;
       for (int i = 0; i < 2; ++i)
-        l7.add(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, c->hqa[0].p + i * Hd, 2 * Hd, B, H, S + A + 1, EPI_RELU));
+        l7.add(fw(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, E(c->hqa[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
       run(l7, "gemm_L7_act_fc1");
     }
     for (int l = 1; l < nh; ++l) {
       Level lv;
       for (int i = 0; i < 2; ++i) {
-        GemmDesc g = gd_fwd_h(c->hqa[l - 1].p + i * Hd, 2 * Hd, W(q[i][l]), Hd, c->hqa[l].p + i * Hd,
-                              2 * Hd, B, H, H);
+        GemmDesc g = fw(gd_fwd_h(E(c->hqa[l - 1].p, (size_t)i * Hd), 2 * Hd, W(q[i][l]), Hd,
+                                 E(c->hqa[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
         lv.add(l == L ? with_dot(g, W(q[i][nh]), 4 + i) : g);
       }
       run(lv, l == 1 ? "gemm_L8_act_fc2" : "gemm_L8b_act_fc3");
@@ -883,10 +915,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     // partials, step counters; dha[L] = dqa * w_head * [ha[L] > 0] is formed on the fly
     Level l9;
     for (int i = 0; i < 2; ++i) {
-      GemmDesc g = gd(c->hqa[L].p + i * Hd, 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dha[L - 1].p + i * H, 2 * H,
-                      B, H, H, EPI_MASK, c->hqa[L - 1].p + i * Hd, 2 * Hd);
+      GemmDesc g = gd(E(c->hqa[L].p, (size_t)i * Hd), 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dha[L - 1].p + i * H, 2 * H,
+                      B, H, H, EPI_MASK, E(c->hqa[L - 1].p, (size_t)i * Hd), 2 * Hd);
       g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]);
-      l9.add(g);
+      l9.add(dh(g));
     }
     {
       RowsFuse& rf = l9.b.rows;
@@ -919,20 +951,21 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     for (int l = L - 1; l >= 1; --l) {
       Level lv;
       for (int i = 0; i < 2; ++i)
-        lv.add(gd(c->dha[l].p + i * H, 2 * H, 1, W(q[i][l]), Hd, 0, c->dha[l - 1].p + i * H, 2 * H,
-                  B, H, H, EPI_MASK, c->hqa[l - 1].p + i * Hd, 2 * Hd));
+        lv.add(dh(gd(c->dha[l].p + i * H, 2 * H, 1, W(q[i][l]), Hd, 0, c->dha[l - 1].p + i * H, 2 * H,
+                     B, H, H, EPI_MASK, E(c->hqa[l - 1].p, (size_t)i * Hd), 2 * Hd)));
       run(lv, "gemm_L9b_act_dh");
     }
     // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
     GemmDesc da = gd(c->dha[0].p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
     validate(da);
     // ... and, for the same rows, dhp[L] = (dhead Whead) * relu'(hp[L]) (policy heads backward)
-    auto hpa = [&](int l) { return c->hp[l].p + (size_t)B * Hd; };   // actor rows
+    auto hpa = [&](int l) { return E(c->hp[l].p, (size_t)B * Hd); };   // actor rows
     SampleBwdArgs sb{};
     sb.cache = c->cache.p + (size_t)B * 3 * A; sb.eps = c->eps.p + (size_t)B * A;
     sb.dhead = c->dhead.p; sb.lddh = c->lddh; sb.A = A; sb.B = B; sb.sc = c->sc.p;
     sb.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     sb.Wh = W(c->p_head); sb.ldw = Hd; sb.H = H; sb.hp2 = hpa(L); sb.ldh = Hd; sb.dhp2 = c->dhp[L].p;
+    sb.hp2_16 = a16;
     check_span(sb.dhp2, (int64_t)B * H - 1, "dhp2");
     check_span(sb.Wh, (int64_t)(2 * A - 1) * Hd + H - 1, "Whead");
     if (fold_dlda) {
@@ -950,20 +983,20 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     const int pepi = fuse ? EPI_ADAM : EPI_STORE;
     for (int l = L; l >= 2; --l) {
       Level lv;
-      lv.add(gd(c->dhp[l].p, H, 1, W(c->p_fc[l]), Hd, 0, c->dhp[l - 1].p, H, B, H, H, EPI_MASK, hpa(l - 1), Hd));
+      lv.add(dh(gd(c->dhp[l].p, H, 1, W(c->p_fc[l]), Hd, 0, c->dhp[l - 1].p, H, B, H, H, EPI_MASK, hpa(l - 1), Hd)));
       run(lv, "gemm_L11_pi_dhp");
     }
     Level l12, l13;
-    l12.add(gd(c->dhp[1].p, H, 1, W(c->p_fc[1]), Hd, 0, c->dhp[0].p, H, B, H, H, EPI_MASK, hpa(0), Hd));
+    l12.add(dh(gd(c->dhp[1].p, H, 1, W(c->p_fc[1]), Hd, 0, c->dhp[0].p, H, B, H, H, EPI_MASK, hpa(0), Hd)));
     if (ride_b) {   // ... and its gather in L12 (256 of 512 slots at config 5), 4 rows a wave
       l12.b.ride.kind = 2; l12.b.ride.nblocks = (B + 15) / 16;
       l12.b.ride.ga = gather_args(c, B, batch_bufs(c, parity ^ 1), false);
     }
     // same level structure fused or not: identical reduction order
-    l13.add(gd_dw_h(c->dhead.p, c->lddh, hpa(L), Hd, pdst(c->p_head), Hd, 2 * A, H, B, pepi, 0));
+    l13.add(dwx(gd_dw_h(c->dhead.p, c->lddh, hpa(L), Hd, pdst(c->p_head), Hd, 2 * A, H, B, pepi, 0)));
     for (int l = L; l >= 1; --l)
-      l13.add(gd_dw_h(c->dhp[l].p, H, hpa(l - 1), Hd, pdst(c->p_fc[l]), Hd, H, H, B, pepi, 0));
-    l13.add(gd(c->dhp[0].p, H, 0, xa, Kx, 0, pdst(c->p_fc[0]), c->p_fc[0].ld, H, S + 1, B, pepi));
+      l13.add(dwx(gd_dw_h(c->dhp[l].p, H, hpa(l - 1), Hd, pdst(c->p_fc[l]), Hd, H, H, B, pepi, 0)));
+    l13.add(dwx(gd(c->dhp[0].p, H, 0, xa, Kx, 0, pdst(c->p_fc[0]), c->p_fc[0].ld, H, S + 1, B, pepi)));
     if (fuse) {
       AdamFuse& f = l13.b.adam;
       l13.b.has_adam = 1;
@@ -1750,6 +1783,10 @@ int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   });
 }
 
+int sacmi_step_act16(sacmi_ctx* c, int32_t batch, int32_t* out) {
+  return guard([&] { *out = act16_on(c, batch) ? 1 : 0; });
+}
+
 int sacmi_step_ride_possible(sacmi_ctx* c, int32_t batch, int32_t* out) {
   return guard([&] { *out = ride_possible(c, batch) ? 1 : 0; });
 }
@@ -2091,9 +2128,11 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     const bool zc = pinned && zc_env && c->act_host_dev;
     if (zc)
       launch_rows_in(c->x2.p, Kx, c->act_host_dev, S, n, S, s);
-    else
+    else {
       CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, src, (size_t)S * 4, (size_t)S * 4, n,
                                  hipMemcpyHostToDevice, s));
+      launch_set_column(c->x2.p, n, Kx, S, 1.f, s);   // (a bf16-activation update may have
+    }                                                   //  overwritten the fp32 ones column)
     if (eps && !deterministic)
       CHECK_HIP(hipMemcpyAsync(c->eps.p, esrc, (size_t)n * A * 4, hipMemcpyHostToDevice, s));
     Level l1;

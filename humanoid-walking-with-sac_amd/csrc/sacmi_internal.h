@@ -79,6 +79,26 @@ __device__ __forceinline__ void st_wt4(float* base, uint32_t byte_off, float4 v)
   llvm_raw_buffer_store_wt_v4f32(wt_f4{v.x, v.y, v.z, v.w}, r, (int)byte_off, 0, kStAux);
 }
 
+// 8-byte and 2-byte write-through stores (bf16 minibatch rows under act16)
+typedef int wt_i2 __attribute__((ext_vector_type(2)));
+__device__ void llvm_raw_buffer_store_wt_v2i32(wt_i2 v, __amdgpu_buffer_rsrc_t r, int off, int soff,
+                                               int aux) __asm("llvm.amdgcn.raw.ptr.buffer.store.v2i32");
+__device__ __forceinline__ void st_wt8(void* base, uint32_t byte_off, uint32_t lo, uint32_t hi) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  llvm_raw_buffer_store_wt_v2i32(wt_i2{(int)lo, (int)hi}, r, (int)byte_off, 0, kStAux);
+}
+__device__ __forceinline__ void st_wt2(void* base, uint32_t byte_off, unsigned short v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b16(v, r, (int)byte_off, 0, kStAux);
+}
+__device__ __forceinline__ unsigned short f2bf(float x) {   // round to nearest even
+  return __builtin_bit_cast(unsigned short, (__bf16)x);
+}
+__device__ __forceinline__ uint32_t f2bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+constexpr unsigned short kBf16One = 0x3F80;
+
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
@@ -200,6 +220,12 @@ struct GemmDesc {
   const float* pa_w;
   float* pa_out;
   int pa_ld, pa_A, pa_base;
+  // bf16 activations (bf16 mode, batch-4096 class: sacmi.hip act16): the operand is stored
+  // as bf16 at its element offsets (pointer = bf16 base reinterpreted; ld in elements).
+  // a16: A (k_fwd16 input rows; k_axk16's h transform source), b16: B (k_dw_part16's X),
+  // c16: C (k_fwd16 output), x16: aux (the ReLU-mask source of EPI_MASK).  launch_gemm
+  // accepts them only on the kernels that read / write that form
+  int a16, b16, c16, x16;
 };
 
 // Adam fused into weight-gradient epilogues (single-GPU path): the gradient tile never
@@ -233,6 +259,7 @@ struct GatherArgs {
   float* xq; float* x2; int ldx;   // xq [B, ldx], x2 [2B, ldx]
   float* r; float* d;
   int by_slot;            // 1: idx are ring slots (PER), 0: deque positions
+  int x16;                // 1: xq / x2 rows stored as bf16 (act16 updates)
   tl_word* tl;
 };
 struct MtSampleArgs {
@@ -304,6 +331,7 @@ struct GemmBatch {
 // [target rows ; actor rows] matrix.
 struct HeadSampleArgs {
   const float* h;        // [rows, ldh] policy hidden (h~ incl. ones col)
+  int h16;               // 1: h is bf16 and the actions go to act as bf16 (act16 updates)
   const float* Wh;       // [2A, ldw] head weights (mean rows ; log_std rows)
   int rows, A, K, ldh, ldw;   // K = H: the bias (column K of Wh) is added in the epilogue
   float* eps;            // [rows, A] standard normals (read, or written when gen)
@@ -337,6 +365,7 @@ struct SampleBwdArgs {
   const float* hp2;      // actor rows' hidden-2 [B, ldh] (ReLU mask source)
   int ldh;
   float* dhp2;           // [B, H]
+  int hp2_16;            // 1: hp2 is bf16 (act16 updates; only its sign is read)
   tl_word* tl;
 };
 
@@ -347,6 +376,7 @@ void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
 // dst[i] = bf16(src[i]) (round to nearest even), the parameter shadows of bf16 mode
 void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_t s);
 // rows [n][cols] from host-mapped memory (select_action's states) into a device matrix
+// n rows of `cols` floats (row stride lds) into dst (row stride ldd), plus 1.0 at column cols
 void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int cols, hipStream_t s);
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s);
 // the same sample backward + dhp2 tail from the dL/da partials of the dha1 level

@@ -258,6 +258,12 @@ class Context:
         L.call("sacmi_step_ride_possible", self._h, int(batch), ctypes.byref(out))
         return bool(out.value)
 
+    def act16(self, batch: int) -> bool:
+        """Whether updates of this batch keep their activations in bf16 (sacmi.h)."""
+        out = ctypes.c_int32()
+        L.call("sacmi_step_act16", self._h, int(batch), ctypes.byref(out))
+        return bool(out.value)
+
     def grad_arena_numel(self) -> int:
         n = ctypes.c_int64()
         L.call("sacmi_grad_arena_numel", self._h, ctypes.byref(n))

@@ -203,6 +203,10 @@ int sacmi_step_phase(sacmi_ctx* ctx, int32_t batch, int32_t phase, float grad_sc
 int sacmi_step_phase_ex(sacmi_ctx* ctx, int32_t batch, int32_t phase, float grad_scale,
                         int32_t parity, int32_t have_batch, int32_t ride_next);
 int sacmi_step_ride_possible(sacmi_ctx* ctx, int32_t batch, int32_t* out);
+/* 1 when updates of this batch store their activations as bf16 (compute_dtype bf16 at the
+ * batch-4096 class: hidden layers, minibatch rows and sampled actions; the policy heads
+ * then read a bf16-rounded input), else 0. */
+int sacmi_step_act16(sacmi_ctx* ctx, int32_t batch, int32_t* out);
 int sacmi_grad_buffer(sacmi_ctx* ctx, int which, void** device_ptr, int64_t* numel);
 /* Gradient arena size (floats) and adoption of a caller-allocated device buffer of
  * that size (e.g. a torch tensor), so collectives run on it in place.  Must be on the

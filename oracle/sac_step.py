@@ -163,7 +163,11 @@ def _n_hidden(p) -> int:
 #   hid  later hidden layers: forward, dX and dW rounded; bias add / bias grad fp32
 #   head critic fc{n+1}: forward and dX unrounded (dot epilogue / row transform), dW
 #        rounded;  phead: policy mean / log_std, the same
-_ROUND = {"on": False}
+# act (bf16 activations, sacmi_step_act16: batch-4096 class): the HIP path stores every
+# activation as bf16, so the policy heads' forward input is the rounded h (straight-through
+# for the gradient: their dX stays unrounded); every other operand is rounded as above
+# already, and the critic head dots read the unrounded epilogue values.
+_ROUND = {"on": False, "act": False}
 
 
 def _bf(t):
@@ -209,6 +213,8 @@ def _policy_forward(p, state):
     x = state
     for i in range(1, _n_hidden(p) + 1):
         x = F.relu(_lin(x, p[f"fc{i}.weight"], p[f"fc{i}.bias"], "in" if i == 1 else "hid"))
+    if _ROUND["on"] and _ROUND["act"]:
+        x = x + (_bf(x) - x).detach()
     mean = _lin(x, p["mean.weight"], p["mean.bias"], "head")
     log_std = _lin(x, p["log_std.weight"], p["log_std.bias"], "head")
     return mean, torch.clamp(log_std, -20, 2)
@@ -251,13 +257,17 @@ class OracleSAC:
             self.opt["alpha"] = torch.optim.Adam([self.log_alpha], lr=lr)
         self.alpha = self.cfg.alpha                     # python float until 1st update
 
-    def step(self, s, a, r, s2, d, eps1, eps2, bf16_operands: bool = False) -> dict:
-        """``bf16_operands``: emulate compute_dtype=bf16 (see _EmuLinear)."""
+    def step(self, s, a, r, s2, d, eps1, eps2, bf16_operands: bool = False,
+             bf16_act: bool = False) -> dict:
+        """``bf16_operands``: emulate compute_dtype=bf16 (see _EmuLinear); ``bf16_act``:
+        with bf16-stored activations (sacmi_step_act16)."""
         _ROUND["on"] = bool(bf16_operands)
+        _ROUND["act"] = bool(bf16_act)
         try:
             return self._step(s, a, r, s2, d, eps1, eps2)
         finally:
             _ROUND["on"] = False
+            _ROUND["act"] = False
 
     def _step(self, s, a, r, s2, d, eps1, eps2) -> dict:
         cfg, dt = self.cfg, self.dtype

@@ -714,10 +714,14 @@ def test_bf16_compute_vs_emulation(n_hidden, B):
     e1 = rng.standard_normal((B, cfg.action_dim)).astype(np.float32)
     e2 = rng.standard_normal((B, cfg.action_dim)).astype(np.float32)
     res = {}
+    act16 = None
     for dt in ("fp32", "bf16"):
         ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]), compute_dtype=dt)
         load_params(ctx, params)
         ctx.push(*rows)
+        if dt == "bf16":
+            act16 = ctx.act16(B)
+            assert act16 == (B >= 4096)        # bf16-stored activations at the batch-4096 class
         lg = ctx.step(B, idx=idx, eps1=e1, eps2=e2)
         res[dt] = (lg, ctx_grads(ctx, cfg))
         # one update = one step of each optimizer (the actor-pass row prologue advances
@@ -730,7 +734,7 @@ def test_bf16_compute_vs_emulation(n_hidden, B):
         ctx.close()
     batch = [x[idx] for x in rows]
     emu = OracleSAC(cfg, params, torch.float64)
-    l_emu = emu.step(*batch, e1, e2, bf16_operands=True)
+    l_emu = emu.step(*batch, e1, e2, bf16_operands=True, bf16_act=act16)
     g_emu = emu.grads_flat()
     exact = OracleSAC(cfg, params, torch.float64)
     exact.step(*batch, e1, e2)
