@@ -1953,6 +1953,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
     const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
     const float* wsd = batch.ws + off;
     const rsrc_t rWs = make_rsrc(wsd, (uint32_t)(((int64_t)(ns - 1) * ws_stride + n_el) * 4));
+    const rsrc_t rTg = make_rsrc(adam && pol ? af.T : wsd, adam && pol ? 0x7fffffffu : 0u);
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n_el; e += gridDim.x * blockDim.x) {
       const int row = e / nc, col = e - row * nc;
       const int n = col < d.N ? col : d.rs_col;
@@ -1970,13 +1971,15 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
       const int64_t o = (int64_t)row * d.ldc + n;
       if (adam) {
         float pp = d.C[o], mm = af.M[abase + o], vv = af.V[abase + o];
+        // the Polyak target with the state loads (after the stores it would wait for them)
+        const float tt = buf_ld(rTg, pol ? (uint32_t)(abase - af.t_base + o) * 4u : 0u);
         adam_elem(pp, mm, vv, v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
         if (af.G) st_big(af.G + abase + o, v);
         st_big(d.C + o, pp); st_big(af.M + abase + o, mm); st_big(af.V + abase + o, vv);
         if (af.Ph) st_big(af.Ph + abase + o, bf16_bits(pp));
         if (pol) {
           float* tp = af.T + abase - af.t_base + o;
-          const float tn = polyak(*tp, pp, omtau, af.tau);
+          const float tn = polyak(tt, pp, omtau, af.tau);
           st_big(tp, tn);
           if (af.Th) st_big(af.Th + abase - af.t_base + o, bf16_bits(tn));
         }
@@ -2677,7 +2680,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
   // hold at most a few million floats)
   const rsrc_t rP = make_rsrc(a.p, 0x7fffffffu), rM = make_rsrc(a.m, 0x7fffffffu),
                rV = make_rsrc(a.v, 0x7fffffffu),
-               rT = make_rsrc(a.tgt ? a.tgt : a.p, 0x7fffffffu);
+               rT = make_rsrc(a.tgt ? a.tgt : a.p, a.tgt ? 0x7fffffffu : 0u);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total4;
        e += (int64_t)gridDim.x * blockDim.x) {
     int sg = 0;
@@ -2689,6 +2692,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     float4 p = *reinterpret_cast<const float4*>(a.p + i);
     float4 m = *reinterpret_cast<const float4*>(a.m + i);
     float4 v = *reinterpret_cast<const float4*>(a.v + i);
+    // the Polyak target with the other operands (one round trip: issued after the stores it
+    // would wait for them), through a zero-length range where there is none
+    float4 t = buf_ld4(rT, a.tgt ? (uint32_t)(i - a.tgt_base) * 4u : 0u);
     g.x *= a.grad_scale; g.y *= a.grad_scale; g.z *= a.grad_scale; g.w *= a.grad_scale;
     adam_elem(p.x, m.x, v.x, g.x, om_b1, a.beta2, om_b2, a.eps, k);
     adam_elem(p.y, m.y, v.y, g.y, om_b1, a.beta2, om_b2, a.eps, k);
@@ -2702,8 +2708,6 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
       st_wt(a.ph + i + 2, bf16_bits(p.z)); st_wt(a.ph + i + 3, bf16_bits(p.w));
     }
     if (a.tgt) {
-      float4* tp = reinterpret_cast<float4*>(a.tgt + (i - a.tgt_base));
-      float4 t = *tp;
       t.x = polyak(t.x, p.x, omtau, a.tau);
       t.y = polyak(t.y, p.y, omtau, a.tau);
       t.z = polyak(t.z, p.z, omtau, a.tau);
