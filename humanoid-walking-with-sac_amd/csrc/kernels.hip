@@ -1051,7 +1051,7 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 // k_fwd / k_fwd16 epilogue: bias, ReLU, store, per-32-column fc3 dot partials.  A wave
 // owns a 64 x (16 NT) sub-tile at (r0, c0); lane holds D[row = (lane >> 4) * 4 + r]
 // [col = lane & 15] of each 16x16 tile.  The operands are loaded before the K loop.
-template <int NT>
+template <int NT, int MI = 4>
 struct FwdEpi {
   float bias_x[NT], dotw_x[NT], dotb;
   __device__ __forceinline__ void load(const GemmDesc& d, int c0, int lane) {
@@ -1072,12 +1072,12 @@ struct FwdEpi {
   // rounded once, and adjacent lanes swap one value (DPP) so every lane stores a column
   // pair of one row as a 32-bit word: lane 2c row r4+rp, lane 2c+1 row r4+rp+1
   template <bool C16 = false>
-  __device__ __forceinline__ void store(const GemmDesc& d, f4 (&acc)[4][NT], int r0, int c0,
+  __device__ __forceinline__ void store(const GemmDesc& d, f4 (&acc)[MI][NT], int r0, int c0,
                                         int lane) const {
     const int M = d.M, N = d.N;
     const bool has_bias = d.bias != nullptr, has_dot = d.dotp != nullptr;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MI; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = r0 + i * 16 + (lane >> 4) * 4 + r;
@@ -1113,7 +1113,7 @@ struct FwdEpi {
       unsigned short* C = reinterpret_cast<unsigned short*>(d.C);
       const bool odd = lane & 1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -1249,14 +1249,29 @@ __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
   return __builtin_bit_cast(u2v, x);
 }
 
-// AH (act16): A is bf16 (4 k per 8-byte load, straight into the slab) and C is bf16
+// AH (act16): A is bf16 (4 k per 8-byte load, straight into the slab) and C is bf16.
+// Waves: 2 x fwd16_wc<kFBN>() of 64 x (kFBN / wc) sub-tiles
+// 8 waves (4 per SIMD at two workgroups per CU) hide each other's LDS / barrier latency
+// behind MFMAs: config 5 L1 / L2 28.8 / 25.4 -> 24.8 / 21.1 us, the 64-column levels
+// L3 / L4 / L7 / L8 18.9 / 16.9 -> 16.4 / 14.7 (4 waves: one wave per SIMD per workgroup)
+#ifndef SACMI_FWD16_WAVES
+#define SACMI_FWD16_WAVES 8     // waves per k_fwd16 workgroup at 128-column tiles (4 or 8)
+#endif
+#ifndef SACMI_FWD16_WAVES64
+#define SACMI_FWD16_WAVES64 8   // ... at 64-column tiles (4: 2 x 2 waves of 64x32; 8: 4 x 2 of 32x32)
+#endif
+template <int kFBN>
+__host__ __device__ constexpr int fwd16_waves() { return kFBN == 128 ? SACMI_FWD16_WAVES : SACMI_FWD16_WAVES64; }
 template <int kFBN, bool BH = false, bool AH = false>
-__global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
+__global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_FWD16);
-  constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
+  // NWV waves as WR x WC, each an MW x NW sub-tile: MI x NT 16x16 MFMA tiles
+  constexpr int NWV = fwd16_waves<kFBN>(), WC = kFBN == 128 ? NWV / 2 : 2, WR = NWV / WC;
+  constexpr int MW = kFBM / WR, MI = MW / 16, NW = kFBN / WC, NT = NW / 16;
+  static_assert(NT >= 2 && MI >= 1, "a wave covers whole 32-column dot blocks");
   constexpr int LDR = kHBK + kHPad;      // bf16 per LDS row: 144 B at 64 deep
   constexpr int TPR = kHBK / 4;          // staging threads per row (4 k each)
-  constexpr int RPP = 256 / TPR;         // rows per staging pass
+  constexpr int RPP = 64 * NWV / TPR;    // rows per staging pass
   constexpr int NA = kFBM / RPP;         // A rows staged per thread
   constexpr int NB = kFBN / RPP;         // B rows staged per thread
   __shared__ __attribute__((aligned(16))) __bf16 sA[2][kFBM][LDR];
@@ -1280,7 +1295,7 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
   }
   const int m0 = tr * kFBM, n0 = tc * kFBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (kFBN / 2);
+  const int wm = (wave / WC) * MW, wn = (wave % WC) * NW;
   const int M = d.M, N = d.N, K = d.K;
   // staging: thread t moves rows t / TPR + RPP i at k = 4 (t % TPR) of both slabs
   const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
@@ -1339,12 +1354,12 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
       else *reinterpret_cast<u2v*>(&sB[buf][tid / TPR + RPP * i][kq]) = pack_bf16x4(gb[i]);
     }
   };
-  f4 acc[4][NT];
+  f4 acc[MI][NT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  FwdEpi<NT> ep;
+  FwdEpi<NT, MI> ep;
   ep.load(d, n0 + wn, lane);
   gload(0);
   swrite(0);
@@ -1356,13 +1371,13 @@ __global__ __launch_bounds__(256, SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch)
 #pragma unroll
     for (int kk = 0; kk < kHBK / 32; ++kk) {
       const int kc = kk * 32 + 8 * (lane >> 4);
-      bf16x8 a[4], b[NT];
+      bf16x8 a[MI], b[NT];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][wm + i * 16 + (lane & 15)][kc]);
+      for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][wm + i * 16 + (lane & 15)][kc]);
 #pragma unroll
       for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][wn + j * 16 + (lane & 15)][kc]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
@@ -2166,17 +2181,17 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
         if (!b.d[i].a16 || !b.d[i].c16 || b.d[i].b16 || b.d[i].x16 || (b.d[i].N & 1) || (b.d[i].ldc & 1))
           throw Error{SACMI_ESTATE, "k_fwd16: unsupported bf16 activation operands"};
       if (!(b.bf16 && SACMI_FWD_LDS16)) throw Error{SACMI_ESTATE, "bf16 activations need k_fwd16"};
-      if (n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-      else if (bh) hipLaunchKernelGGL((k_fwd16<64, true, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-      else if (n128) hipLaunchKernelGGL((k_fwd16<128, false, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-      else hipLaunchKernelGGL((k_fwd16<64, false, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
+      if (n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
+      else if (bh) hipLaunchKernelGGL((k_fwd16<64, true, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
+      else if (n128) hipLaunchKernelGGL((k_fwd16<128, false, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
+      else hipLaunchKernelGGL((k_fwd16<64, false, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
       HIP_LAUNCH_CHECK();
       return;
     }
-    if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-    else if (b.bf16 && SACMI_FWD_LDS16 && bh) hipLaunchKernelGGL((k_fwd16<64, true>), dim3(b.total_tiles), dim3(256), 0, s, b);
-    else if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(256), 0, s, b);
-    else if (b.bf16 && SACMI_FWD_LDS16) hipLaunchKernelGGL((k_fwd16<64>), dim3(b.total_tiles), dim3(256), 0, s, b);
+    if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
+    else if (b.bf16 && SACMI_FWD_LDS16 && bh) hipLaunchKernelGGL((k_fwd16<64, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
+    else if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
+    else if (b.bf16 && SACMI_FWD_LDS16) hipLaunchKernelGGL((k_fwd16<64>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
     else if (b.bf16 && n128) hipLaunchKernelGGL((k_fwd<true, 128>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else if (b.bf16) hipLaunchKernelGGL((k_fwd<true, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
     else hipLaunchKernelGGL((k_fwd<false, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
