@@ -1562,7 +1562,11 @@ typedef short s4t __attribute__((ext_vector_type(4)));
 typedef short s8t __attribute__((ext_vector_type(8)));
 constexpr int kD16K = 64, kD16Pad = 8;
 constexpr int kDw16OpBytes = 2 * kD16K * (kDBM + kD16Pad) * 2;      // one operand, 2 slabs
-static_assert(kDw16LdsBytes == 2 * kDw16OpBytes + 8 * kDBM * 4, "k_dw_part16 LDS layout");
+#ifndef SACMI_DW16_WAVES
+#define SACMI_DW16_WAVES 8      // waves per k_dw_part16 workgroup (4: 2 x 2 of 64x64; 8: 2 x 4 of 64x32)
+#endif
+constexpr int kDw16Waves = SACMI_DW16_WAVES, kDw16Krp = 64 * kDw16Waves / 32;   // k rows per staging pass
+static_assert(kDw16LdsBytes >= 2 * kDw16OpBytes + kDw16Krp * kDBM * 4, "k_dw_part16 LDS layout");
 
 __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -1571,7 +1575,7 @@ __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
 
 // X16 (act16): the B operand (X: activations / minibatch inputs) is bf16
 template <bool X16 = false>
-__global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
+__global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_PART16);
   constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
   // one LDS block (kDw16LdsBytes): the two operand slabs and the row-sum scratch, or a
@@ -1579,7 +1583,9 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kDw16LdsBytes];
   auto& sA = *reinterpret_cast<__bf16 (*)[2][kD16K][LDR]>(lds_raw);
   auto& sB = *reinterpret_cast<__bf16 (*)[2][kD16K][LDR]>(lds_raw + kDw16OpBytes);
-  auto& s_rs = *reinterpret_cast<float (*)[8][kDBM]>(lds_raw + 2 * kDw16OpBytes);
+  auto& s_rs = *reinterpret_cast<float (*)[kDw16Krp][kDBM]>(lds_raw + 2 * kDw16OpBytes);
+  constexpr int NWV = kDw16Waves, WC = NWV / 2, NJ = kDBN / WC / 16;   // 2 x WC waves of 64 x (128 / WC)
+  constexpr int KRP = kDw16Krp, NI = kD16K / KRP;                       // staging: KRP k rows a pass
   const int tiles_tot = batch.total_tiles;
   const int nwg = dw_grid_tiles(tiles_tot, ns);
   if ((int)blockIdx.x >= nwg) {   // ride-along: the next update's sampling or gather
@@ -1587,7 +1593,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
     if (batch.ride.kind == 1) {
       if (rb == 0) mt_sample_body(batch.ride.mt, batch.ride.tbl_log2, reinterpret_cast<uint32_t*>(lds_raw));
     } else {
-      for (int b = rb * 4 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 4)
+      for (int b = rb * NWV + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * NWV)
         gather_row(batch.ride.ga, b, lane, 64);
     }
     return;
@@ -1606,8 +1612,8 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   const int kc = ((K + ns - 1) / ns + kD16K - 1) / kD16K * kD16K;
   const int kb = split * kc, ke = min(K, kb + kc);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  // staging: thread t moves k rows (t >> 5) + 8 i (i < 8), columns 4 (t & 31) .. +3
+  const int wm = (wave / WC) * 64, wn = (wave % WC) * (kDBN / WC);
+  // staging: thread t moves k rows (t >> 5) + KRP i (i < NI), columns 4 (t & 31) .. +3
   const int c4 = 4 * (tid & 31), kr0 = tid >> 5;
   const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
   const rsrc_t rS = make_rsrc(d.a_ksc ? d.a_ksc : d.A, d.a_ksc ? (uint32_t)K * 4u : 0u);
@@ -1619,13 +1625,13 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
   const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
   const bool want_rs = d.rs_col >= 0 && n0 == 0;
-  float4 ga[8], gb[X16 ? 1 : 8];
-  uint2 gbh[X16 ? 8 : 1];
+  float4 ga[NI], gb[X16 ? 1 : NI];
+  uint2 gbh[X16 ? NI : 1];
   float rs4[4] = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int k = k0 + kr0 + 8 * i;
+    for (int i = 0; i < NI; ++i) {
+      const int k = k0 + kr0 + KRP * i;
       const bool kin = k < ke;
       const uint32_t kk = (uint32_t)(kin ? k : 0);   // row 0 always exists (a split may start past K)
       float4 x = buf_ld4(rA, (kk * (uint32_t)d.lda + (uint32_t)ma) * 4u);
@@ -1649,24 +1655,24 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
   };
   auto swrite = [&](int buf, bool fresh) {   // fresh: a slab not staged before
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      *reinterpret_cast<u2v*>(&sA[buf][kr0 + 8 * i][c4]) = pack_bf16x4(ga[i]);
-      if constexpr (X16) *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = u2v{gbh[i].x, gbh[i].y};
-      else *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+    for (int i = 0; i < NI; ++i) {
+      *reinterpret_cast<u2v*>(&sA[buf][kr0 + KRP * i][c4]) = pack_bf16x4(ga[i]);
+      if constexpr (X16) *reinterpret_cast<u2v*>(&sB[buf][kr0 + KRP * i][c4]) = u2v{gbh[i].x, gbh[i].y};
+      else *reinterpret_cast<u2v*>(&sB[buf][kr0 + KRP * i][c4]) = pack_bf16x4(gb[i]);
     }
     if (want_rs && fresh) {
 #pragma clang fp contract(off)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < NI; ++i) {
         rs4[0] += ga[i].x; rs4[1] += ga[i].y; rs4[2] += ga[i].z; rs4[3] += ga[i].w;
       }
     }
   };
-  f4 acc[4][4];
+  f4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   const int nslab = (ke - kb + kD16K - 1) / kD16K;
   // transposed-read lane roles: group g = lane >> 4 takes k 8g..8g+7; lane 4q+p of the
   // group addresses k row q (+4 for the second half), columns 4p..4p+3 of a 16-column block
@@ -1680,7 +1686,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
 #pragma unroll
     for (int kk = 0; kk < kD16K / 32; ++kk) {
       const int kr = kk * 32 + 8 * tg + tq;
-      bf16x8 a[4], b[4];
+      bf16x8 a[4], b[NJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const s4t lo = lds_tr16(&sA[cur][kr][wm + i * 16 + 4 * tp]);
@@ -1689,7 +1695,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
         a[i] = __builtin_bit_cast(bf16x8, v);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const s4t lo = lds_tr16(&sB[cur][kr][wn + j * 16 + 4 * tp]);
         const s4t hi = lds_tr16(&sB[cur][kr + 4][wn + j * 16 + 4 * tp]);
         const s8t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -1698,7 +1704,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     swrite(cur ^ 1, sl + 1 < nslab);
@@ -1715,7 +1721,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int col = n0 + wn + j * 16 + (lane & 15);
         if (row < M && col < N) st_big(w + (int64_t)row * nc + col, acc[i][j][r]);
       }
@@ -1727,7 +1733,7 @@ __global__ __launch_bounds__(256, 2) void k_dw_part16(GemmBatch batch, int ns, i
     if (tid < kDBM && m0 + tid < M) {
 #pragma clang fp contract(off)
       float v = s_rs[0][tid];
-      for (int g = 1; g < 8; ++g) v += s_rs[g][tid];
+      for (int g = 1; g < KRP; ++g) v += s_rs[g][tid];
       st_big(w + (int64_t)(m0 + tid) * nc + N, v);
     }
   }
@@ -2128,8 +2134,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
           throw Error{SACMI_ESTATE, "split-K weight gradient: unsupported bf16 activation operand"};
       if (form && !(b.bf16 && SACMI_DW_LDS16))
         throw Error{SACMI_ESTATE, "bf16 activation operands need k_dw_part16"};
-      if (b.bf16 && SACMI_DW_LDS16 && form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
-      else if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
+      if (b.bf16 && SACMI_DW_LDS16 && form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
+      else if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
       else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();

@@ -280,7 +280,7 @@ struct MtSampleArgs {
 constexpr size_t kRideLdsBytes = (size_t)16 * 32 * 33 * 4;
 // k_dw_part16's LDS block (two bf16 operand slab pairs + row-sum scratch), which a
 // ride-along sampler may use instead
-constexpr int kDw16LdsBytes = 73728;
+constexpr int kDw16LdsBytes = 77824;   // 2 x 34,816 (slabs) + 16 x 128 x 4 (row sums)
 struct RideAlong {
   int kind;        // 0 none, 1 random.sample, 2 gather
   int nblocks;
