@@ -1753,19 +1753,28 @@ constexpr int kXBM = 64, kXBN = 128, kXBK = 64;
 
 // ACT16 (act16 updates): the ReLU-mask source (aux) is bf16, and so is A where it is the
 // activation whose sign the transform reads (AX); the plain levels' A is a gradient, fp32
+#ifndef SACMI_AXK16_WAVES
+#define SACMI_AXK16_WAVES 8     // waves per k_axk16 workgroup (4: 2 x 2 of 32x64; 8: 2 x 4 of 32x32)
+#endif
+constexpr int kAxWaves = SACMI_AXK16_WAVES;
 template <bool AX, bool BH = false, bool ACT16 = false>
-__global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
+__global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_AXK16);
   constexpr int LDA_ = kXBK + 8;        // [row][k] bf16, 144-B rows
   constexpr int LDB_ = kXBN + 8;        // [k][n] bf16, 272-B rows
   __shared__ __attribute__((aligned(16))) __bf16 sA[2][kXBM][LDA_];
   __shared__ __attribute__((aligned(16))) __bf16 sB[2][kXBK][LDB_];
   __shared__ float s_q[kXBM][4], s_coef[2][kXBM], s_l[kXBM][2];
+  constexpr int NWV = kAxWaves, NTH = 64 * NWV, WC = NWV / 2, NJ = kXBN / WC / 16;
+  constexpr int ARP = NTH / 16, NAI = kXBM / ARP;   // A staging: rows a pass, passes
+  constexpr int BKP = NTH / 32, NBI = kXBK / BKP;   // B staging: k rows a pass, passes
   const int bid = blockIdx.x;
-  if (bid >= batch.total_tiles) {   // ride-along: the next update's gather, 4 rows a wave
-    const int wv = (bid - batch.total_tiles) * 4 + (int)(threadIdx.x >> 6), nwv = batch.ride.nblocks * 4;
-    for (int b0 = wv; b0 < batch.ride.ga.B; b0 += 4 * nwv)
-      gather_rows_wave<4, 4>(batch.ride.ga, b0, nwv, threadIdx.x & 63);
+  if (bid >= batch.total_tiles) {   // ride-along: the next update's gather, a row a wave
+    // (one row of 3 float4 per lane: the branch's registers stay under the tiles' 128 —
+    // two rows a wave took the kernel to 131 VGPRs, one 8-wave workgroup per CU)
+    const int wv = (bid - batch.total_tiles) * NWV + (int)(threadIdx.x >> 6), nwv = batch.ride.nblocks * NWV;
+    for (int b0 = wv; b0 < batch.ride.ga.B; b0 += nwv)
+      gather_rows_wave<1, 3>(batch.ride.ga, b0, nwv, threadIdx.x & 63);
     return;
   }
   int p = 0;
@@ -1786,30 +1795,30 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
   }
   const int m0 = tr * kXBM, n0 = tc * kXBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 64;
+  const int wm = (wave / WC) * 32, wn = (wave % WC) * (kXBN / WC);
   const int M = d.M, N = d.N, K = d.K;
   const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
   const rsrc_t rW = make_rsrc(AX ? d.ax_w : d.A, AX ? (uint32_t)K * 4u : 0u);
   const bool store_a = AX && n0 == 0 && d.ax_out != nullptr;
   const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
                                store_a ? (uint32_t)(((size_t)(M - 1) * d.ax_ld + K) * 4) : 0u);
-  // A staging: rows (t >> 4) + 16 i (i < 4) at k = 4 (t & 15); B staging: k rows
-  // (t >> 5) + 8 i (i < 8) at columns 4 (t & 31)
+  // A staging: rows (t >> 4) + ARP i (i < NAI) at k = 4 (t & 15); B staging: k rows
+  // (t >> 5) + BKP i (i < NBI) at columns 4 (t & 31)
   const int kq = 4 * (tid & 15), c4 = 4 * (tid & 31), kr0 = tid >> 5;
-  uint32_t offA[4];
+  uint32_t offA[NAI];
   constexpr bool A16 = AX && ACT16;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    offA[i] = (uint32_t)min(m0 + (tid >> 4) + 16 * i, M - 1) * (uint32_t)d.lda * (A16 ? 2u : 4u);
+  for (int i = 0; i < NAI; ++i)
+    offA[i] = (uint32_t)min(m0 + (tid >> 4) + ARP * i, M - 1) * (uint32_t)d.lda * (A16 ? 2u : 4u);
   const int nb = min(n0 + c4, N - 1);
-  float4 ga[4], gb[BH ? 1 : 8], gw;
-  uint2 gh[BH ? 8 : 1];               // BH: W from its bf16 shadow
+  float4 ga[NAI], gb[BH ? 1 : NBI], gw;
+  uint2 gh[BH ? NBI : 1];               // BH: W from its bf16 shadow
   const rsrc_t rBh = make_rsrc(BH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
   auto gload = [&](int k0) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NAI; ++i) {
       if constexpr (A16) {   // (only the sign is read: exact widening)
         const uint2 h = buf_ld2(rA, offA[i] + ko / 2u);
         ga[i] = make_float4(bf16_lo(h.x), bf16_hi(h.x), bf16_lo(h.y), bf16_hi(h.y));
@@ -1819,8 +1828,8 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
     }
     gw = buf_ld4(rW, ko);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int kb = k0 + kr0 + 8 * i;
+    for (int i = 0; i < NBI; ++i) {
+      const int kb = k0 + kr0 + BKP * i;
       const bool kin = kb < K;
       const uint32_t e = (uint32_t)(kin ? kb : 0) * (uint32_t)d.ldb + (uint32_t)nb;
       if constexpr (BH) {
@@ -1839,14 +1848,14 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
   auto swrite = [&](int buf, int k0, bool fresh) {
     const int k = k0 + kq;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NAI; ++i) {
       // u = [h2 > 0] w3 (exact fp32 values: w3 or 0), rounded to bf16 for the MFMAs
       const float4 a = ga[i];
       const float4 u = AX ? make_float4(a.x > 0.f && k < K ? gw.x : 0.f, a.y > 0.f && k + 1 < K ? gw.y : 0.f,
                                         a.z > 0.f && k + 2 < K ? gw.z : 0.f, a.w > 0.f && k + 3 < K ? gw.w : 0.f)
                           : make_float4(k < K ? a.x : 0.f, k + 1 < K ? a.y : 0.f,
                                         k + 2 < K ? a.z : 0.f, k + 3 < K ? a.w : 0.f);
-      const int r = (tid >> 4) + 16 * i;
+      const int r = (tid >> 4) + ARP * i;
       *reinterpret_cast<u2v*>(&sA[buf][r][kq]) = pack_bf16x4(u);
       if (fresh) {
         const int rr = m0 + r;
@@ -1855,21 +1864,21 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if constexpr (BH) *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = u2v{gh[i].x, gh[i].y};
-      else *reinterpret_cast<u2v*>(&sB[buf][kr0 + 8 * i][c4]) = pack_bf16x4(gb[i]);
+    for (int i = 0; i < NBI; ++i) {
+      if constexpr (BH) *reinterpret_cast<u2v*>(&sB[buf][kr0 + BKP * i][c4]) = u2v{gh[i].x, gh[i].y};
+      else *reinterpret_cast<u2v*>(&sB[buf][kr0 + BKP * i][c4]) = pack_bf16x4(gb[i]);
     }
   };
-  f4 acc[2][4];
+  f4 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   gload(0);
   // the row prologue's loads and the ReLU-mask source, behind the first slab's loads
   RowsRegs rows_x{};
-  if constexpr (AX) rows_load<kXBM, 256>(batch.rows, d, m0, rows_x);
-  float hm[2][4][4];
+  if constexpr (AX) rows_load<kXBM, NTH>(batch.rows, d, m0, rows_x);
+  float hm[2][NJ][4];
   {
     constexpr uint32_t xe = ACT16 ? 2u : 4u;   // mask-source element bytes
     const rsrc_t rX = make_rsrc(d.aux, (uint32_t)(((size_t)(M - 1) * d.ldaux + N) * xe));
@@ -1879,7 +1888,7 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           const int col = n0 + wn + j * 16 + (lane & 15);
           const uint32_t off = row < M && col < N ? (uint32_t)(row * d.ldaux + col) * xe : 0xfffffff0u;
           hm[i][j][r] = ACT16 ? bf16_lo(buf_ld_u16(rX, off)) : buf_ld(rX, off);
@@ -1897,11 +1906,11 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
 #pragma unroll
     for (int kk = 0; kk < kXBK / 32; ++kk) {
       const int kc = kk * 32 + 8 * tg;
-      bf16x8 a[2], b[4];
+      bf16x8 a[2], b[NJ];
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][wm + i * 16 + (lane & 15)][kc]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const s4t lo = lds_tr16(&sB[cur][kc + tq][wn + j * 16 + 4 * tp]);
         const s4t hi = lds_tr16(&sB[cur][kc + tq + 4][wn + j * 16 + 4 * tp]);
         const s8t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -1910,14 +1919,14 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     swrite(cur ^ 1, knext, store_a && sl + 1 < nslab);
     __syncthreads();
   }
   const bool writer = p == 0 && n0 == 0;
-  if constexpr (AX) rows_finish<kXBM, 256>(batch.rows, d, m0, writer, bid == 0, rows_x, s_q, s_coef, s_l);
+  if constexpr (AX) rows_finish<kXBM, NTH>(batch.rows, d, m0, writer, bid == 0, rows_x, s_q, s_coef, s_l);
   // epilogue: coefficient, ReLU-backward mask, store (k_gemm's op order)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1926,7 +1935,7 @@ __global__ __launch_bounds__(256, 2) void k_axk16(GemmBatch batch) {
       const int lr = wm + i * 16 + (lane >> 4) * 4 + r, row = m0 + lr;
       const float cf = AX ? s_coef[d.ax_slot][lr] : 1.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int col = n0 + wn + j * 16 + (lane & 15);
         float v = acc[i][j][r];
         if (AX) v *= cf;
@@ -2153,25 +2162,25 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       for (int i = 0; i < b.count; ++i)   // k_axk16 computes no dL/da partials
         if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a k_axk16 level"};
       const bool bh = all_bh(b);
-      const dim3 grid(b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0));
+      const dim3 grid(b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0)), blk(64 * kAxWaves);
       const int form = level_act16(b);   // act16: mask sources (and AX sources) bf16
       if (form < 0) throw Error{SACMI_ESTATE, "k_axk16 level with mixed bf16 activation flags"};
       for (int i = 0; i < b.count; ++i)
         if (b.d[i].c16 || b.d[i].b16 || b.d[i].x16 != form || b.d[i].a16 != (form && b.d[i].axk == 1))
           throw Error{SACMI_ESTATE, "k_axk16: unsupported bf16 activation operand"};
       if (form) {
-        if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true, true>), grid, dim3(256), 0, s, b);
-        else if (ax) hipLaunchKernelGGL((k_axk16<true, false, true>), grid, dim3(256), 0, s, b);
-        else if (bh) hipLaunchKernelGGL((k_axk16<false, true, true>), grid, dim3(256), 0, s, b);
-        else hipLaunchKernelGGL((k_axk16<false, false, true>), grid, dim3(256), 0, s, b);
+        if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true, true>), grid, blk, 0, s, b);
+        else if (ax) hipLaunchKernelGGL((k_axk16<true, false, true>), grid, blk, 0, s, b);
+        else if (bh) hipLaunchKernelGGL((k_axk16<false, true, true>), grid, blk, 0, s, b);
+        else hipLaunchKernelGGL((k_axk16<false, false, true>), grid, blk, 0, s, b);
       } else if (ax && bh) {
-        hipLaunchKernelGGL((k_axk16<true, true>), grid, dim3(256), 0, s, b);
+        hipLaunchKernelGGL((k_axk16<true, true>), grid, blk, 0, s, b);
       } else if (ax) {
-        hipLaunchKernelGGL((k_axk16<true, false>), grid, dim3(256), 0, s, b);
+        hipLaunchKernelGGL((k_axk16<true, false>), grid, blk, 0, s, b);
       } else if (bh) {
-        hipLaunchKernelGGL((k_axk16<false, true>), grid, dim3(256), 0, s, b);
+        hipLaunchKernelGGL((k_axk16<false, true>), grid, blk, 0, s, b);
       } else {
-        hipLaunchKernelGGL((k_axk16<false, false>), grid, dim3(256), 0, s, b);
+        hipLaunchKernelGGL((k_axk16<false, false>), grid, blk, 0, s, b);
       }
       HIP_LAUNCH_CHECK();
       return;

@@ -648,7 +648,7 @@ static bool ride_possible(sacmi_ctx* c, int B) {
 // ... or, in a fused multi-update graph whose batch is too large for that (the batch-4096
 // class, bf16): the sampler (compact table, 256 threads) rides in L6's split-K kernel
 // (k_dw_part16, 440 of 512 slots at config 5) and the gather in L12 (k_axk16, 256 of 512
-// slots; 4 rows a wave, every load before any store).  (The gather in L10 measured no
+// slots; a row a wave, every load before any store).  (The gather in L10 measured no
 // overlap: k_gemm_sample_bwd's 1024-thread workgroups fit one per CU)
 static bool ride_b_possible(sacmi_ctx* c, int B) {
   return c->cfg.replay_kind == SACMI_REPLAY_UNIFORM && c->bf16 && B >= 2048 &&
@@ -988,8 +988,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     }
     Level l12, l13;
     l12.add(dh(gd(c->dhp[1].p, H, 1, W(c->p_fc[1]), Hd, 0, c->dhp[0].p, H, B, H, H, EPI_MASK, hpa(0), Hd)));
-    if (ride_b) {   // ... and its gather in L12 (256 of 512 slots at config 5), 4 rows a wave
-      l12.b.ride.kind = 2; l12.b.ride.nblocks = (B + 15) / 16;
+    if (ride_b) {   // ... and its gather in L12 (256 of 512 slots at config 5), a row a wave
+      l12.b.ride.kind = 2; l12.b.ride.nblocks = (B + 7) / 8;   // (8 waves)
       l12.b.ride.ga = gather_args(c, B, batch_bufs(c, parity ^ 1), false);
     }
     // same level structure fused or not: identical reduction order
