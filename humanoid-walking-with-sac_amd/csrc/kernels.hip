@@ -1402,6 +1402,10 @@ constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
 #define SACMI_DW_TARGET 512     // k_dw_part workgroup slots (256 CUs x 2)
 #endif
 constexpr int kDwMaxSplit = 16;
+#ifndef SACMI_DWFIN_EPT
+#define SACMI_DWFIN_EPT 1       // k_dw_fin elements per thread (1, 2, 4 measured alike)
+#endif
+constexpr int kDwFinEpt = SACMI_DWFIN_EPT;
 #ifndef SACMI_DW_SPLIT_FP32
 #define SACMI_DW_SPLIT_FP32 0   // the split-K dW path for fp32 levels too (k_dw_part<false>)
 #endif
@@ -1974,50 +1978,73 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
   if (adam && threadIdx.x < 3) s_k[threadIdx.x] = fuse_scalars(af, threadIdx.x, af.step_offset);
   __syncthreads();
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
+  // kDwFinEpt elements per thread (element e = block base + k * 256 + thread: coalesced),
+  // the workgroups dealt to the descs in order: every workgroup belongs to one desc, and
+  // every load of a thread's elements (partials, parameter, moments, target) is issued
+  // before any use — one round trip, and all of the level's threads resident at once
+  int q = -1, bstart = 0, acc = 0;
   int64_t off = 0;
-  for (int q = 0; q < batch.count; ++q) {
+  for (int qq = 0; qq < batch.count; ++qq) {
+    const int n_el_q = batch.d[qq].M * dw_ncols(batch.d[qq]);
+    const int nb = (n_el_q + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
+    if (q < 0 && (int)blockIdx.x < acc + nb) { q = qq; bstart = acc; }
+    if (q < 0) off += n_el_q;
+    acc += nb;
+  }
+  if (q >= 0) {
     const GemmDesc& d = batch.d[q];
     const int nc = dw_ncols(d);
     const int n_el = d.M * nc;                  // < 2^31 (checked by dw_split_plan)
     const bool pol = d.epi == EPI_ADAM_POLYAK;
     const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
     const float* wsd = batch.ws + off;
+    const uint32_t oob = 0xfffffff0u;
     const rsrc_t rWs = make_rsrc(wsd, (uint32_t)(((int64_t)(ns - 1) * ws_stride + n_el) * 4));
     const rsrc_t rTg = make_rsrc(adam && pol ? af.T : wsd, adam && pol ? 0x7fffffffu : 0u);
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n_el; e += gridDim.x * blockDim.x) {
-      const int row = e / nc, col = e - row * nc;
+    const rsrc_t rC = make_rsrc(d.C, 0x7fffffffu);
+    const rsrc_t rM = make_rsrc(adam ? af.M : d.C, adam ? 0x7fffffffu : 0u);
+    const rsrc_t rV = make_rsrc(adam ? af.V : d.C, adam ? 0x7fffffffu : 0u);
+    int e[kDwFinEpt];
+    int64_t o[kDwFinEpt];
+    float t[kDwFinEpt][kDwMaxSplit], pp[kDwFinEpt], mm[kDwFinEpt], vv[kDwFinEpt], tt[kDwFinEpt];
+#pragma unroll
+    for (int k = 0; k < kDwFinEpt; ++k) {
+      e[k] = (blockIdx.x - bstart) * (256 * kDwFinEpt) + k * 256 + threadIdx.x;
+      const bool live = e[k] < n_el;
+      const int row = e[k] / nc, col = e[k] - row * nc;
       const int n = col < d.N ? col : d.rs_col;
-      // all NS partial loads in flight at once, then the fixed-order sum.  Buffer loads
-      // with an out-of-range offset past NS (return 0, no access): no guard, so nothing
-      // drains the load queue between them (a guarded load waits at its guard's end)
-      float t[kDwMaxSplit];
+      o[k] = (int64_t)row * d.ldc + n;
+      // all partial loads in flight at once (offsets past NS / past the desc return 0, no
+      // access): no guard, so nothing drains the load queue between them
 #pragma unroll
       for (int s = 0; s < kDwMaxSplit; ++s)
-        t[s] = buf_ld(rWs, s < ns ? (uint32_t)((int64_t)s * ws_stride + e) * 4u : 0xfffffff0u);
-      float v = t[0];
+        t[k][s] = buf_ld(rWs, live && s < ns ? (uint32_t)((int64_t)s * ws_stride + e[k]) * 4u : oob);
+      pp[k] = buf_ld(rC, adam && live ? (uint32_t)o[k] * 4u : oob);
+      mm[k] = buf_ld(rM, live ? (uint32_t)(abase + o[k]) * 4u : oob);
+      vv[k] = buf_ld(rV, live ? (uint32_t)(abase + o[k]) * 4u : oob);
+      tt[k] = buf_ld(rTg, pol && live ? (uint32_t)(abase - af.t_base + o[k]) * 4u : oob);
+    }
+#pragma unroll
+    for (int k = 0; k < kDwFinEpt; ++k) {
+      if (e[k] >= n_el) continue;
+      float v = t[k][0];
 #pragma unroll
       for (int s = 1; s < kDwMaxSplit; ++s)
-        if (s < ns) v += t[s];
-      const int64_t o = (int64_t)row * d.ldc + n;
+        if (s < ns) v += t[k][s];
       if (adam) {
-        float pp = d.C[o], mm = af.M[abase + o], vv = af.V[abase + o];
-        // the Polyak target with the state loads (after the stores it would wait for them)
-        const float tt = buf_ld(rTg, pol ? (uint32_t)(abase - af.t_base + o) * 4u : 0u);
-        adam_elem(pp, mm, vv, v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
-        if (af.G) st_big(af.G + abase + o, v);
-        st_big(d.C + o, pp); st_big(af.M + abase + o, mm); st_big(af.V + abase + o, vv);
-        if (af.Ph) st_big(af.Ph + abase + o, bf16_bits(pp));
+        adam_elem(pp[k], mm[k], vv[k], v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
+        if (af.G) st_big(af.G + abase + o[k], v);
+        st_big(d.C + o[k], pp[k]); st_big(af.M + abase + o[k], mm[k]); st_big(af.V + abase + o[k], vv[k]);
+        if (af.Ph) st_big(af.Ph + abase + o[k], bf16_bits(pp[k]));
         if (pol) {
-          float* tp = af.T + abase - af.t_base + o;
-          const float tn = polyak(tt, pp, omtau, af.tau);
-          st_big(tp, tn);
-          if (af.Th) st_big(af.Th + abase - af.t_base + o, bf16_bits(tn));
+          const float tn = polyak(tt[k], pp[k], omtau, af.tau);
+          st_big(af.T + abase - af.t_base + o[k], tn);
+          if (af.Th) st_big(af.Th + abase - af.t_base + o[k], bf16_bits(tn));
         }
       } else {
-        st_big(d.C + o, v);
+        st_big(d.C + o[k], v);
       }
     }
-    off += n_el;
   }
   if (adam && blockIdx.x == 0) {
     __syncthreads();
@@ -2148,7 +2175,9 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
-      const int fin_grid = (int)std::min<int64_t>((stride + 255) / 256, 4096);
+      int fin_grid = 0;                    // k_dw_fin: kDwFinEpt elements per thread, per desc
+      for (int i = 0; i < b.count; ++i)
+        fin_grid += (b.d[i].M * (b.d[i].rs_col >= 0 ? b.d[i].N + 1 : b.d[i].N) + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
       if (b.tl) b.tl += kTlWords;          // the second kernel of the level
       hipLaunchKernelGGL(k_dw_fin, dim3(fin_grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
@@ -2325,10 +2354,11 @@ __device__ __forceinline__ float one_minus_tanh2(float x) {
 // (networks_model1.py:65-99, torch distributions/normal.py:83-103)
 // H16 (act16 updates): h is bf16 (widened exactly; Wh fp32, fp32 MFMAs) and the actions
 // go to act as bf16 (the next levels' input columns)
-template <int TN, int KSPLIT, bool H16 = false>
+// TM rows per workgroup (heads_rows_per_wg: 32 at the batch-4096 class — one workgroup
+// per CU covers all rows in one round and the head weights are re-read half as often)
+template <int TN, int KSPLIT, bool H16 = false, int TM = 16>
 __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) {
   const TlMark tl_mark(a.tl, TL_HEADS);
-  constexpr int TM = 16;
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   __shared__ float lp[TM][33];
   const int A = a.A;
@@ -2336,7 +2366,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   d.A = a.h; d.lda = a.ldh; d.a_kc = 1; d.M = a.rows;
   d.B = a.Wh; d.ldb = a.ldw; d.b_kc = 1; d.N = 2 * A; d.K = a.K;
   const int m0 = blockIdx.x * TM;
-  static_assert(TM * 64 <= 64 * KSPLIT, "one (row, action) element per thread");
+  static_assert(TM * 32 <= 64 * KSPLIT, "one (row, action) element per thread (A <= 32)");
   // element e = threadIdx.x -> (row, action j); its bias values (and stored noise)
   // are loaded while the MFMAs run
   const int e = threadIdx.x;
@@ -2437,9 +2467,18 @@ void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_
 }
 
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s) {
-  const int grid = (a.rows + 15) / 16;
+  const int tm = heads_rows_per_wg(a.rows);
+  const int grid = (a.rows + tm - 1) / tm;
   const int n = 2 * a.A;
-  if (a.h16) {
+  if (a.A > 32) throw Error{SACMI_EVALUE, "heads: action_dim > 32"};
+  if (tm == 32) {
+    if (a.h16 && n <= 32) hipLaunchKernelGGL((k_heads_sample<32, 16, true, 32>), dim3(grid), dim3(1024), 0, s, a);
+    else if (a.h16 && n <= 48) hipLaunchKernelGGL((k_heads_sample<48, 16, true, 32>), dim3(grid), dim3(1024), 0, s, a);
+    else if (a.h16) hipLaunchKernelGGL((k_heads_sample<64, 16, true, 32>), dim3(grid), dim3(1024), 0, s, a);
+    else if (n <= 32) hipLaunchKernelGGL((k_heads_sample<32, 16, false, 32>), dim3(grid), dim3(1024), 0, s, a);
+    else if (n <= 48) hipLaunchKernelGGL((k_heads_sample<48, 16, false, 32>), dim3(grid), dim3(1024), 0, s, a);
+    else hipLaunchKernelGGL((k_heads_sample<64, 16, false, 32>), dim3(grid), dim3(1024), 0, s, a);
+  } else if (a.h16) {
     if (n <= 32) hipLaunchKernelGGL((k_heads_sample<32, 16, true>), dim3(grid), dim3(1024), 0, s, a);
     else if (n <= 48) hipLaunchKernelGGL((k_heads_sample<48, 16, true>), dim3(grid), dim3(1024), 0, s, a);
     else hipLaunchKernelGGL((k_heads_sample<64, 16, true>), dim3(grid), dim3(1024), 0, s, a);

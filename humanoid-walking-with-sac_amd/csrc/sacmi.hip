@@ -925,7 +925,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       rf.kind = 2; rf.part = dotp(4); rf.nparts = c->nparts; rf.B = B;
       rf.logp = c->logp.p + B; rf.sc = c->sc.p; rf.loss_part = c->lpart_a.p;
       if (c->cfg.auto_entropy) {
-        rf.alpha_grad = G + c->la_idx; rf.logp_part = c->lp_part.p; rf.n_lp = (2 * B + 15) / 16;
+        rf.alpha_grad = G + c->la_idx; rf.logp_part = c->lp_part.p; rf.n_lp = (2 * B + heads_rows_per_wg(2 * B) - 1) / heads_rows_per_wg(2 * B);
         rf.target_entropy = (float)(-A);
       }
     }

@@ -373,6 +373,11 @@ struct SampleBwdArgs {
 // launchers (kernels.hip)
 void launch_gemm(const GemmBatch& batch, hipStream_t s);
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
+// rows per heads workgroup (and per log-prob partial): 32 from 8192 stacked rows on
+#ifndef SACMI_HEADS_TM32
+#define SACMI_HEADS_TM32 1
+#endif
+inline int heads_rows_per_wg(int rows) { return SACMI_HEADS_TM32 && rows >= 8192 ? 32 : 16; }
 // dst[i] = bf16(src[i]) (round to nearest even), the parameter shadows of bf16 mode
 void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_t s);
 // rows [n][cols] from host-mapped memory (select_action's states) into a device matrix
