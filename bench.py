@@ -373,8 +373,11 @@ def parse_args(argv=None):
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel path even at world size 1 (overhead check)")
     ap.add_argument("--dp-native", action="store_true",
-                    help="data parallel through sacmi_step_dp (the library issues the RCCL "
-                         "all-reduces) instead of torch.distributed around the phases")
+                    help="(default) data parallel through sacmi_step_dp: the library issues "
+                         "the RCCL all-reduces inside its own captured graph")
+    ap.add_argument("--dp-torch", action="store_true",
+                    help="data parallel through torch.distributed all-reduces around the "
+                         "library's phases, captured into torch.cuda.CUDAGraphs")
     ap.add_argument("--no-trainer-loop", action="store_true",
                     help="skip the env-free trainer-loop measurement (select_action + push + "
                          "update_parameters per env step)")

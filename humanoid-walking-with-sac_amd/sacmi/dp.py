@@ -137,7 +137,9 @@ class CapturedDataParallelUpdates:
         g = self.graphs.get(n)
         if g is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.stream):
+            # thread_local: API calls of other threads (the process group's watchdog
+            # polling its work events) do not invalidate this thread's capture
+            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self.upd.begin_sequence(n, self.batch)
                 for _ in range(n):
                     self.upd(self.batch)
@@ -202,7 +204,11 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     per_launch = max(1, min(args.updates_per_launch, 256))
     sizes = B.graph_sizes(args.steps, per_launch)
     captured = None
-    native = getattr(args, "dp_native", False)
+    # default: the library's own RCCL sequence (sacmi_step_dp, one hipGraph per n updates).
+    # The torch.distributed driver (--dp-torch) captures torch's collectives into
+    # CUDAGraphs, where ProcessGroupNCCL's watchdog thread can query a work event recorded
+    # during the capture and abort the process (seen once in a world-1 run this round)
+    native = not getattr(args, "dp_torch", False)
     # the library's communicator: the native driver's collectives, and the roofline's
     # timeline of the data-parallel sequence (both paths)
     want_roof = not getattr(args, "no_roofline", False)
