@@ -888,6 +888,9 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.tau = (float)c->cfg.tau; ad.step_offset = 1; ad.sc = c->sc.p;
     ad.loss_part = c->lpart_c.p; ad.n_part = nb; ad.loss_slot0 = 0; ad.n_losses = 2;
     ad.loss_div = (float)B; ad.log_alpha_idx = -1; ad.auto_entropy = 0;
+    // the bf16 shadows of the updated critics and targets (read by the bf16 level kernels
+    // of L7 on: without them the data-parallel bf16 update read stale critic weights)
+    ad.ph = c->Ph.p; ad.tgth = c->Th.p;
     if (mark(c, "adam_critic_polyak")) {
       ad.tl = c->tl_cur;
       launch_adam(ad, s);

@@ -488,7 +488,8 @@ def test_polyak_bitexact_and_determinism():
             assert np.array_equal(outs[0][n][k], outs[1][n][k]), (n, k)
 
 
-@pytest.mark.parametrize("shape", ["small", "nao_b4096_bf16", "nao_b4096_bf16_set", "per_b4096"])
+@pytest.mark.parametrize("shape", ["small", "nao_b4096_bf16", "nao_b4096_bf16_set", "nao_b4096_bf16_m2",
+                                   "per_b4096"])
 def test_many_updates_per_launch_identical(shape):
     """sacmi_step_many_async(n) (trainer.py:203-204 loop in one launch) == n single
     launches, bit for bit, losses included — also at the config-5 shapes (batch 4096,
@@ -506,6 +507,8 @@ def test_many_updates_per_launch_identical(shape):
         cfg, B, nrows, dt = SacConfig(661, 23, 512), 4096, 6000, "bf16"
         if shape.endswith("_set"):
             nrows = 20000
+        if shape.endswith("_m2"):                  # networks_model2: L2b / L5b / L9b / L11
+            cfg, nrows = SacConfig(661, 23, 512, n_hidden=3), 20000
     params = init_params(cfg, 61, bias_scale=0.05)
     rows = synthetic_rows(cfg, nrows, 62, state_scale=0.5)
     prio = np.random.default_rng(64).uniform(0.1, 2.0, nrows).astype(np.float32)
@@ -792,6 +795,39 @@ def test_native_dp_world1_matches_fused(n_hidden):
     assert hist.shape == (6, 3) and np.all(np.isfinite(hist))
     with pytest.raises(Exception):
         ctxs[1].step_dp(64, 1)            # no communicator on this context
+
+
+def test_native_dp_world1_matches_fused_act16():
+    """The same at config 5's per-GPU shape (NAO S661 A23 H512, batch 4096, bf16): the
+    phase-split levels store bf16 activations exactly as the fused ones (act16), the
+    split-K weight gradients go through the same k_dw_part16 / k_dw_fin path (plain store
+    + k_adam instead of the fused Adam epilogue): bit for bit after three updates."""
+    from sacmi import Context
+    cfg = SacConfig(661, 23, 512)
+    B = 4096
+    params = init_params(cfg, 93, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 20000, 94, state_scale=0.5)
+    key = (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32)
+    ctxs = []
+    for _ in range(2):
+        ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]), seed=5, compute_dtype="bf16")
+        load_params(ctx, params)
+        ctx.push(*rows)
+        ctx.set_mt(0, key, 624)
+        ctxs.append(ctx)
+    assert ctxs[0].act16(B)
+    ctxs[0].allreduce_init(Context.allreduce_unique_id(), 0, 1)
+    ctxs[0].step_dp(B, 3)
+    fused = np.stack([ctxs[1].step(B) for _ in range(3)])
+    ctxs[0].synchronize()
+    for n in NETS:
+        a, b = ctxs[0].get_net(n), ctxs[1].get_net(n)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (n, k)
+    # the loss ring of the data-parallel updates against the losses step() returns
+    hist = ctxs[0].fetch_losses(3)
+    assert hist.shape == (3, 3)
+    np.testing.assert_allclose(hist, fused, rtol=1e-6, atol=1e-7)
 
 
 def _config4_ctxs(k, cfg, params, rows, prio, key, B):
