@@ -1389,6 +1389,175 @@ __global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), SACMI_FWD16_OCC) void k_f
 }
 
 // ---------------------------------------------------------------------------
+// k_fwd16p: the act16 forward levels (bf16 activations AND bf16 weight shadows) with a
+// multi-slab LDS ring filled by LDS-DMA (global_load_lds_dwordx4: no VGPR per slab in
+// flight).  k_fwd16 keeps one slab in flight per workgroup (its register stage), and at
+// batch 4096 a slab's load round trip (~2 us under the chip-wide load) is ~5x the slab's
+// MFMA time; here one workgroup per CU (1024 threads, 16 waves of (BM/4) x 32) holds
+// NST = 144 KiB / stage slabs, NST - 1 of them in flight across the barriers: a counted
+// `s_waitcnt vmcnt` (never 0 inside the loop) and a raw s_barrier — a __syncthreads()
+// fence would drain the DMA queue (cdna_hip_programming.md, "Pipelining across barriers").
+// Tiles BM x 128 (BM = 256 where that still gives a workgroup per CU, else 128), 64-deep
+// slabs.  The DMA image is lane-linear (lane l of a 1 KiB piece writes bytes 16 l..), so
+// the bank swizzle sits on the SOURCE address: LDS row R holds its 16-byte k-chunk c at
+// position c ^ ((R >> 1) & 7) — a fragment read (16 rows at one chunk) hits 16 distinct
+// 16-byte slots of a 256-byte bank row.  Chunks past K read a clamped in-row address and
+// are zeroed in the fragment registers (last slab only).  Epilogue: FwdEpi (bias, ReLU,
+// fc3 dot partials, bf16 column-pair stores), as k_fwd16.
+#ifndef SACMI_FWD16P
+#define SACMI_FWD16P 1
+#endif
+constexpr int kPLds = 144 * 1024;
+template <int BM>
+__host__ __device__ constexpr int fwd16p_stages() { return kPLds / ((BM + 128) * 128); }
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+template <int N>
+__device__ __forceinline__ void vm_wait_lgkm0() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ bf16x8 zero_past(bf16x8 x, int nvalid) {   // keep elements < nvalid
+  uint4 u = __builtin_bit_cast(uint4, x);
+  auto m = [&](unsigned w, int e) {
+    return (e < nvalid ? w & 0xffffu : 0u) | (e + 1 < nvalid ? w & 0xffff0000u : 0u);
+  };
+  u.x = m(u.x, 0); u.y = m(u.y, 2); u.z = m(u.z, 4); u.w = m(u.w, 6);
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+template <int BM>
+__global__ __launch_bounds__(1024, 1) void k_fwd16p(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_FWD16P);
+  constexpr int BN = 128, BK = 64, NST = fwd16p_stages<BM>();
+  constexpr int WR = 4, WC = 4, MW = BM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
+  constexpr int ROWB = BK * 2;                       // bytes per LDS row (64 bf16)
+  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int PPW = (BM + BN) / 8 / 16;            // 1 KiB pieces per wave per slab
+  constexpr int APW = BM / 8 / 16;                   // ... of them A pieces
+  static_assert(NST >= 3 && PPW * 16 * 8 == BM + BN && APW * 16 * 8 == BM, "k_fwd16p geometry");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NST * STAGE];
+  const int bid = blockIdx.x;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  int tr, tc;
+  if (d.xcd_gr) {
+    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
+    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
+    tr = (x / gc) * sr + j / sc;
+    tc = (x % gc) * sc + j % sc;
+  } else {
+    tr = t / d.tiles_n;
+    tc = t % d.tiles_n;
+  }
+  const int m0 = tr * BM, n0 = tc * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WC) * MW, wn = (wave % WC) * NW;
+  const int M = d.M, N = d.N, K = d.K;
+  // DMA sources: wave w moves pieces w + 16 i (A rows 8 pc.., then B rows); lane l of a
+  // piece: LDS row 8 pc + (l >> 3), position l & 7, global chunk (l & 7) ^ swizzle
+  const unsigned char* src[PPW];
+  int cko[PPW];                                      // the lane's chunk, in bf16 elements
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int pc = wave + 16 * i;
+    const bool isA = i < APW;
+    const int R = (isA ? pc : pc - BM / 8) * 8 + (lane >> 3);
+    const int sw = (R >> 1) & 7;
+    cko[i] = 8 * ((lane & 7) ^ sw);
+    if (isA) {
+      const int ra = min(m0 + R, M - 1);
+      src[i] = reinterpret_cast<const unsigned char*>(d.A) + (size_t)ra * d.lda * 2;
+    } else {
+      const int rb = min(n0 + R, N - 1);
+      src[i] = reinterpret_cast<const unsigned char*>(d.Bh) + (size_t)rb * d.ldb * 2;
+    }
+  }
+  auto issue = [&](int sl) {                         // slab sl into ring slot sl % NST
+    unsigned char* dst = lds + (sl % NST) * STAGE;
+    const int k0 = sl * BK;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int k = k0 + cko[i];
+      const unsigned char* g = src[i] + (k < K ? k : 0) * 2;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(dst + (wave + 16 * i) * 1024), 16, 0, 0);
+    }
+  };
+  f4 acc[MI][NT];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  FwdEpi<NT, MI> ep;                                 // issued first: oldest on the vm queue
+  ep.load(d, n0 + wn, lane);
+  const int nslab = (K + BK - 1) / BK;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nslab) issue(s);
+  const int r16 = lane & 15, sx = r16 >> 1;
+  for (int sl = 0; sl < nslab; ++sl) {
+    // slabs sl .. min(sl + NST - 2, nslab - 1) are outstanding: retire sl only
+    const int ahead = min(NST - 2, nslab - 1 - sl);
+    if (ahead >= 2) vm_wait_lgkm0<2 * PPW>();
+    else if (ahead == 1) vm_wait_lgkm0<PPW>();
+    else vm_wait_lgkm0<0>();
+    __builtin_amdgcn_s_barrier();                    // every wave's slab sl landed; slot (sl-1) free
+    asm volatile("" ::: "memory");
+    if (sl + NST - 1 < nslab) issue(sl + NST - 1);
+    const unsigned char* st = lds + (sl % NST) * STAGE;
+    const int kval = K - sl * BK;                    // valid k of this slab (>= BK but the last)
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int c = kk * 4 + (lane >> 4);
+      const int off = (c ^ sx) << 4;
+      bf16x8 a[MI], b[NT];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(st + (wm + i * 16 + r16) * ROWB + off);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(st + (BM + wn + j * 16 + r16) * ROWB + off);
+      if (kval < BK) {                               // the last, partial slab: zero k >= K
+        const int nv = kval - 8 * c;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) a[i] = zero_past(a[i], nv);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) b[j] = zero_past(b[j], nv);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  ep.template store<true>(d, acc, m0 + wm, n0 + wn, lane);
+}
+
+// whether an act16 level can run on k_fwd16p, and its row tile (0: no).  Every operand row
+// must start 16-byte aligned (the DMA moves 16-byte chunks) and hold round_up(K, 8)
+// elements inside its stride (a chunk straddling K stays in its row).
+static int fwd16p_plan(GemmBatch& b) {
+  if (!SACMI_FWD16P || !b.bf16 || b.ride.kind) return 0;
+  static const bool off = std::getenv("SACMI_NO_FWD16P") != nullptr;
+  if (off) return 0;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    const int k8 = (d.K + 7) & ~7;
+    if (!d.a16 || !d.c16 || d.b16 || d.x16 || !d.Bh || (d.N & 1) || (d.ldc & 1)) return 0;
+    if (((uintptr_t)d.A & 15) || ((uintptr_t)d.Bh & 15) || (d.lda & 7) || (d.ldb & 7)) return 0;
+    if (k8 > d.lda || k8 > d.ldb || d.K < 1) return 0;
+  }
+  if (assign_tiles<256, 128>(b) >= 256) return 256;
+  if (assign_tiles<128, 128>(b) >= 256) return 128;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // Deep-K weight-gradient levels in bf16 mode (batch 4096 class): dW = dY^T X with both
 // operands row-contiguous.  k_dw_part: 128x128 output tiles, K split NS ways across
 // workgroups; each workgroup stages 32-row slabs of dY (128 columns) and X (128 columns)
@@ -2225,7 +2394,17 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
         if (!b.d[i].a16 || !b.d[i].c16 || b.d[i].b16 || b.d[i].x16 || (b.d[i].N & 1) || (b.d[i].ldc & 1))
           throw Error{SACMI_ESTATE, "k_fwd16: unsupported bf16 activation operands"};
       if (!(b.bf16 && SACMI_FWD_LDS16)) throw Error{SACMI_ESTATE, "bf16 activations need k_fwd16"};
-      if (n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
+      if (bh) {
+        GemmBatch bp = b;
+        const int bm = fwd16p_plan(bp);
+        if (bm) {
+          if (bm == 256) hipLaunchKernelGGL((k_fwd16p<256>), dim3(bp.total_tiles), dim3(1024), 0, s, bp);
+          else hipLaunchKernelGGL((k_fwd16p<128>), dim3(bp.total_tiles), dim3(1024), 0, s, bp);
+          HIP_LAUNCH_CHECK();
+          return;
+        }
+      }
+      if (n128 && bh)hipLaunchKernelGGL((k_fwd16<128, true, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
       else if (bh) hipLaunchKernelGGL((k_fwd16<64, true, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
       else if (n128) hipLaunchKernelGGL((k_fwd16<128, false, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
       else hipLaunchKernelGGL((k_fwd16<64, false, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);

@@ -203,9 +203,13 @@ static void destroy_graphs(sacmi_ctx* c) {
 // ---------------------------------------------------------------------------
 static void build_layout(sacmi_ctx* c) {
   const int S = c->S, A = c->A, H = c->H;
-  c->Kx = round_up(S + 1 + A, 4);
-  c->Hd = round_up(H + 1, 4);
-  c->Kp1 = round_up(S + 1, 4);
+  // bf16 mode: rows of 8-element multiples, so every bf16 activation / weight-shadow row
+  // starts 16-byte aligned (k_fwd16p's LDS-DMA moves 16-byte chunks)
+  int pad = c->bf16 ? 8 : 4;
+  if (c->bf16 && std::getenv("SACMI_ROW_PAD")) pad = std::max(8, std::atoi(std::getenv("SACMI_ROW_PAD")) / 8 * 8);
+  c->Kx = round_up(S + 1 + A, pad);
+  c->Hd = round_up(H + 1, pad);
+  c->Kp1 = round_up(S + 1, pad);
   c->lddh = round_up(2 * A, 4);
   int64_t off = 0;
   auto take = [&](Linear& l, int n_out, int k_in, int ld, int bias_col, int split, bool align) {

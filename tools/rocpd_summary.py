@@ -14,7 +14,7 @@ import re
 import sqlite3
 import sys
 
-LEVEL = ("k_gemm<", "k_fwd<", "k_fwd16<", "k_axk16<", "k_dw_part<", "k_dw_part16")
+LEVEL = ("k_gemm<", "k_fwd<", "k_fwd16<", "k_fwd16p<", "k_axk16<", "k_dw_part<", "k_dw_part16")
 
 
 def load(path):
