@@ -1071,9 +1071,12 @@ struct FwdEpi {
   // C16 (act16): C is bf16 — the fp32 values (the dot partials use them unrounded) are
   // rounded once, and adjacent lanes swap one value (DPP) so every lane stores a column
   // pair of one row as a 32-bit word: lane 2c row r4+rp, lane 2c+1 row r4+rp+1
+  // tile (C16 only): the column-pair words go to an LDS tile image at (row - tm0, col - tn0),
+  // tld words per row, instead of global memory (k_fwd16p's staged epilogue)
   template <bool C16 = false>
   __device__ __forceinline__ void store(const GemmDesc& d, f4 (&acc)[MI][NT], int r0, int c0,
-                                        int lane) const {
+                                        int lane, uint32_t* tile = nullptr, int tm0 = 0,
+                                        int tn0 = 0, int tld = 0) const {
     const int M = d.M, N = d.N;
     const bool has_bias = d.bias != nullptr, has_dot = d.dotp != nullptr;
 #pragma unroll
@@ -1123,7 +1126,8 @@ struct FwdEpi {
             const int row = r0 + i * 16 + (lane >> 4) * 4 + rp + (odd ? 1 : 0);
             const int col = c0 + j * 16 + (lane & 14);
             const uint32_t w = odd ? pack_bf16x2(b1, a1) : pack_bf16x2(a0, b0);
-            if (row < M && col < N) st_big(reinterpret_cast<uint32_t*>(C + (size_t)row * d.ldc + col), w);
+            if (tile) tile[(row - tm0) * tld + ((col - tn0) >> 1)] = w;
+            else if (row < M && col < N) st_big(reinterpret_cast<uint32_t*>(C + (size_t)row * d.ldc + col), w);
           }
     }
   }
@@ -1535,7 +1539,29 @@ __global__ __launch_bounds__(1024, 1) void k_fwd16p(GemmBatch batch) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   }
-  ep.template store<true>(d, acc, m0 + wm, n0 + wn, lane);
+  // staged epilogue: the bf16 tile image in the (now idle) ring, then 16 bytes a lane per
+  // store — full 128-byte lines, write-through when the level asks (batch.st_wt): the
+  // kernel-end L2 writeback in front of the dependent level has less to do
+  constexpr int TLD = BN / 2 + 4;                    // words per tile row (272 B: conflict-free reads)
+  static_assert(BM * TLD * 4 <= NST * STAGE, "k_fwd16p epilogue tile");
+  __syncthreads();                                   // every wave is past its last ring read
+  uint32_t* tile = reinterpret_cast<uint32_t*>(lds);
+  ep.template store<true>(d, acc, m0 + wm, n0 + wn, lane, tile, m0, n0, TLD);
+  __syncthreads();
+  const bool wt = batch.st_wt != 0;
+  const rsrc_t rC = make_rsrc(d.C, 0x7fffffffu);
+  const int ch = tid & 15;                           // 16-byte chunk of a 256-byte tile row
+#pragma unroll
+  for (int pass = 0; pass < BM / 64; ++pass) {
+    const int r = pass * 64 + (tid >> 4), row = m0 + r, col = n0 + 8 * ch;
+    const uint4 v = *reinterpret_cast<const uint4*>(tile + r * TLD + 4 * ch);
+    if (row < M && col < N) {
+      const uint32_t off = (uint32_t)(((size_t)row * d.ldc + col) * 2);
+      const wt_f4 x = __builtin_bit_cast(wt_f4, v);
+      if (wt) llvm_raw_buffer_store_wt_v4f32(x, rC, (int)off, 0, kStAux);
+      else llvm_raw_buffer_store_wt_v4f32(x, rC, (int)off, 0, 0);
+    }
+  }
 }
 
 // whether an act16 level can run on k_fwd16p, and its row tile (0: no).  Every operand row
@@ -1551,7 +1577,10 @@ static int fwd16p_plan(GemmBatch& b) {
     if (!d.a16 || !d.c16 || d.b16 || d.x16 || !d.Bh || (d.N & 1) || (d.ldc & 1)) return 0;
     if (((uintptr_t)d.A & 15) || ((uintptr_t)d.Bh & 15) || (d.lda & 7) || (d.ldb & 7)) return 0;
     if (k8 > d.lda || k8 > d.ldb || d.K < 1) return 0;
+    if ((d.N & 7) || (d.ldc & 7) || ((uintptr_t)d.C & 15)) return 0;   // 16-byte epilogue stores
   }
+  static const bool wt = std::getenv("SACMI_FWD16P_WT") == nullptr || std::atoi(std::getenv("SACMI_FWD16P_WT")) != 0;
+  b.st_wt = wt ? 1 : 0;
   if (assign_tiles<256, 128>(b) >= 256) return 256;
   if (assign_tiles<128, 128>(b) >= 256) return 128;
   return 0;
@@ -1573,6 +1602,9 @@ constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
 constexpr int kDwMaxSplit = 16;
 #ifndef SACMI_DWFIN_EPT
 #define SACMI_DWFIN_EPT 1       // k_dw_fin elements per thread (1, 2, 4 measured alike)
+#endif
+#ifndef SACMI_DWFIN_NSL
+#define SACMI_DWFIN_NSL 1       // k_dw_fin instantiated per split count (0: one 16-load form)
 #endif
 constexpr int kDwFinEpt = SACMI_DWFIN_EPT;
 #ifndef SACMI_DW_SPLIT_FP32
@@ -2139,6 +2171,9 @@ static int axk16_ok(GemmBatch& b) {
   return assign_tiles<kXBM, kXBN>(b) >= 256 ? ax : -1;
 }
 
+// NSL: the partial loads each thread issues (= ns where instantiated, else kDwMaxSplit with
+// the loads past ns at an out-of-range offset): no VMEM issue slots for absent splits
+template <int NSL>
 __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_FIN);
   __shared__ AdamScalars s_k[3];
@@ -2175,7 +2210,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
     const rsrc_t rV = make_rsrc(adam ? af.V : d.C, adam ? 0x7fffffffu : 0u);
     int e[kDwFinEpt];
     int64_t o[kDwFinEpt];
-    float t[kDwFinEpt][kDwMaxSplit], pp[kDwFinEpt], mm[kDwFinEpt], vv[kDwFinEpt], tt[kDwFinEpt];
+    float t[kDwFinEpt][NSL], pp[kDwFinEpt], mm[kDwFinEpt], vv[kDwFinEpt], tt[kDwFinEpt];
 #pragma unroll
     for (int k = 0; k < kDwFinEpt; ++k) {
       e[k] = (blockIdx.x - bstart) * (256 * kDwFinEpt) + k * 256 + threadIdx.x;
@@ -2186,7 +2221,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
       // all partial loads in flight at once (offsets past NS / past the desc return 0, no
       // access): no guard, so nothing drains the load queue between them
 #pragma unroll
-      for (int s = 0; s < kDwMaxSplit; ++s)
+      for (int s = 0; s < NSL; ++s)
         t[k][s] = buf_ld(rWs, live && s < ns ? (uint32_t)((int64_t)s * ws_stride + e[k]) * 4u : oob);
       pp[k] = buf_ld(rC, adam && live ? (uint32_t)o[k] * 4u : oob);
       mm[k] = buf_ld(rM, live ? (uint32_t)(abase + o[k]) * 4u : oob);
@@ -2198,7 +2233,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
       if (e[k] >= n_el) continue;
       float v = t[k][0];
 #pragma unroll
-      for (int s = 1; s < kDwMaxSplit; ++s)
+      for (int s = 1; s < NSL; ++s)
         if (s < ns) v += t[k][s];
       if (adam) {
         adam_elem(pp[k], mm[k], vv[k], v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
@@ -2348,7 +2383,19 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       for (int i = 0; i < b.count; ++i)
         fin_grid += (b.d[i].M * (b.d[i].rs_col >= 0 ? b.d[i].N + 1 : b.d[i].N) + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
       if (b.tl) b.tl += kTlWords;          // the second kernel of the level
-      hipLaunchKernelGGL(k_dw_fin, dim3(fin_grid), dim3(256), 0, s, b, ns, stride);
+      const dim3 fg(fin_grid), fb(256);
+      static const bool nsl = SACMI_DWFIN_NSL && std::getenv("SACMI_NO_DWFIN_NSL") == nullptr;
+      switch (nsl ? ns : 0) {
+        case 1: hipLaunchKernelGGL(k_dw_fin<1>, fg, fb, 0, s, b, ns, stride); break;
+        case 2: hipLaunchKernelGGL(k_dw_fin<2>, fg, fb, 0, s, b, ns, stride); break;
+        case 3: hipLaunchKernelGGL(k_dw_fin<3>, fg, fb, 0, s, b, ns, stride); break;
+        case 4: hipLaunchKernelGGL(k_dw_fin<4>, fg, fb, 0, s, b, ns, stride); break;
+        case 5: hipLaunchKernelGGL(k_dw_fin<5>, fg, fb, 0, s, b, ns, stride); break;
+        case 6: hipLaunchKernelGGL(k_dw_fin<6>, fg, fb, 0, s, b, ns, stride); break;
+        case 8: hipLaunchKernelGGL(k_dw_fin<8>, fg, fb, 0, s, b, ns, stride); break;
+        case 10: hipLaunchKernelGGL(k_dw_fin<10>, fg, fb, 0, s, b, ns, stride); break;
+        default: hipLaunchKernelGGL(k_dw_fin<kDwMaxSplit>, fg, fb, 0, s, b, ns, stride); break;
+      }
       HIP_LAUNCH_CHECK();
       return;
     }
