@@ -2202,6 +2202,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
     const bool pol = d.epi == EPI_ADAM_POLYAK;
     const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
     const float* wsd = batch.ws + off;
+    const bool wt = batch.st_wt != 0;            // write-through parameter / state stores
     const uint32_t oob = 0xfffffff0u;
     const rsrc_t rWs = make_rsrc(wsd, (uint32_t)(((int64_t)(ns - 1) * ws_stride + n_el) * 4));
     const rsrc_t rTg = make_rsrc(adam && pol ? af.T : wsd, adam && pol ? 0x7fffffffu : 0u);
@@ -2237,16 +2238,17 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
         if (s < ns) v += t[k][s];
       if (adam) {
         adam_elem(pp[k], mm[k], vv[k], v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
-        if (af.G) st_big(af.G + abase + o[k], v);
-        st_big(d.C + o[k], pp[k]); st_big(af.M + abase + o[k], mm[k]); st_big(af.V + abase + o[k], vv[k]);
-        if (af.Ph) st_big(af.Ph + abase + o[k], bf16_bits(pp[k]));
+        if (af.G) st_pol(af.G + abase + o[k], v, wt);
+        st_pol(d.C + o[k], pp[k], wt); st_pol(af.M + abase + o[k], mm[k], wt);
+        st_pol(af.V + abase + o[k], vv[k], wt);
+        if (af.Ph) st_pol(af.Ph + abase + o[k], (unsigned short)bf16_bits(pp[k]), wt);
         if (pol) {
           const float tn = polyak(tt[k], pp[k], omtau, af.tau);
-          st_big(af.T + abase - af.t_base + o[k], tn);
-          if (af.Th) st_big(af.Th + abase - af.t_base + o[k], bf16_bits(tn));
+          st_pol(af.T + abase - af.t_base + o[k], tn, wt);
+          if (af.Th) st_pol(af.Th + abase - af.t_base + o[k], (unsigned short)bf16_bits(tn), wt);
         }
       } else {
-        st_big(d.C + o[k], v);
+        st_pol(d.C + o[k], v, wt);
       }
     }
   }
@@ -2384,6 +2386,10 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
         fin_grid += (b.d[i].M * (b.d[i].rs_col >= 0 ? b.d[i].N + 1 : b.d[i].N) + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
       if (b.tl) b.tl += kTlWords;          // the second kernel of the level
       const dim3 fg(fin_grid), fb(256);
+      // the fin's stores: plain (SACMI_FIN_WT=1: write-through, measured slower at config 5:
+      // 3,412 -> 3,357 updates/s, the boundary behind the level unchanged)
+      static const bool fin_wt = std::getenv("SACMI_FIN_WT") != nullptr && std::atoi(std::getenv("SACMI_FIN_WT")) != 0;
+      b.st_wt = fin_wt ? 1 : 0;
       static const bool nsl = SACMI_DWFIN_NSL && std::getenv("SACMI_NO_DWFIN_NSL") == nullptr;
       switch (nsl ? ns : 0) {
         case 1: hipLaunchKernelGGL(k_dw_fin<1>, fg, fb, 0, s, b, ns, stride); break;
