@@ -1411,6 +1411,9 @@ __global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), SACMI_FWD16_OCC) void k_f
 #ifndef SACMI_FWD16P
 #define SACMI_FWD16P 1
 #endif
+#ifndef SACMI_FWD16P_WAVES
+#define SACMI_FWD16P_WAVES 16   // k_fwd16p waves per workgroup (8 or 16)
+#endif
 constexpr int kPLds = 144 * 1024;
 template <int BM>
 __host__ __device__ constexpr int fwd16p_stages() { return kPLds / ((BM + 128) * 128); }
@@ -1432,16 +1435,18 @@ __device__ __forceinline__ bf16x8 zero_past(bf16x8 x, int nvalid) {   // keep el
   return __builtin_bit_cast(bf16x8, u);
 }
 
-template <int BM>
-__global__ __launch_bounds__(1024, 1) void k_fwd16p(GemmBatch batch) {
+template <int BM, int NWV = 16>
+__global__ __launch_bounds__(64 * NWV, 1) void k_fwd16p(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_FWD16P);
   constexpr int BN = 128, BK = 64, NST = fwd16p_stages<BM>();
-  constexpr int WR = 4, WC = 4, MW = BM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
+  // NWV waves as WR x WC: 16 -> 4 x 4 of (BM/4) x 32; 8 -> BM 256: 4 x 2 of 64 x 64, BM 128: 2 x 4 of 64 x 32
+  constexpr int WR = NWV == 16 ? 4 : (BM == 256 ? 4 : 2), WC = NWV / WR;
+  constexpr int MW = BM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
   constexpr int ROWB = BK * 2;                       // bytes per LDS row (64 bf16)
   constexpr int STAGE = (BM + BN) * ROWB;
-  constexpr int PPW = (BM + BN) / 8 / 16;            // 1 KiB pieces per wave per slab
-  constexpr int APW = BM / 8 / 16;                   // ... of them A pieces
-  static_assert(NST >= 3 && PPW * 16 * 8 == BM + BN && APW * 16 * 8 == BM, "k_fwd16p geometry");
+  constexpr int PPW = (BM + BN) / 8 / NWV;           // 1 KiB pieces per wave per slab
+  constexpr int APW = BM / 8 / NWV;                  // ... of them A pieces
+  static_assert(NST >= 3 && PPW * NWV * 8 == BM + BN && APW * NWV * 8 == BM, "k_fwd16p geometry");
   __shared__ __attribute__((aligned(16))) unsigned char lds[NST * STAGE];
   const int bid = blockIdx.x;
   int p = 0;
@@ -1470,7 +1475,7 @@ __global__ __launch_bounds__(1024, 1) void k_fwd16p(GemmBatch batch) {
   int cko[PPW];                                      // the lane's chunk, in bf16 elements
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
-    const int pc = wave + 16 * i;
+    const int pc = wave + NWV * i;
     const bool isA = i < APW;
     const int R = (isA ? pc : pc - BM / 8) * 8 + (lane >> 3);
     const int sw = (R >> 1) & 7;
@@ -1490,7 +1495,7 @@ __global__ __launch_bounds__(1024, 1) void k_fwd16p(GemmBatch batch) {
     for (int i = 0; i < PPW; ++i) {
       const int k = k0 + cko[i];
       const unsigned char* g = src[i] + (k < K ? k : 0) * 2;
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(dst + (wave + 16 * i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(dst + (wave + NWV * i) * 1024), 16, 0, 0);
     }
   };
   f4 acc[MI][NT];
@@ -1552,8 +1557,8 @@ __global__ __launch_bounds__(1024, 1) void k_fwd16p(GemmBatch batch) {
   const rsrc_t rC = make_rsrc(d.C, 0x7fffffffu);
   const int ch = tid & 15;                           // 16-byte chunk of a 256-byte tile row
 #pragma unroll
-  for (int pass = 0; pass < BM / 64; ++pass) {
-    const int r = pass * 64 + (tid >> 4), row = m0 + r, col = n0 + 8 * ch;
+  for (int pass = 0; pass < BM / (4 * NWV); ++pass) {
+    const int r = pass * 4 * NWV + (tid >> 4), row = m0 + r, col = n0 + 8 * ch;
     const uint4 v = *reinterpret_cast<const uint4*>(tile + r * TLD + 4 * ch);
     if (row < M && col < N) {
       const uint32_t off = (uint32_t)(((size_t)row * d.ldc + col) * 2);
@@ -2451,8 +2456,12 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
         GemmBatch bp = b;
         const int bm = fwd16p_plan(bp);
         if (bm) {
-          if (bm == 256) hipLaunchKernelGGL((k_fwd16p<256>), dim3(bp.total_tiles), dim3(1024), 0, s, bp);
-          else hipLaunchKernelGGL((k_fwd16p<128>), dim3(bp.total_tiles), dim3(1024), 0, s, bp);
+          static const int nwv = std::getenv("SACMI_FWD16P_WAVES") ? std::atoi(std::getenv("SACMI_FWD16P_WAVES")) : SACMI_FWD16P_WAVES;
+          const dim3 g(bp.total_tiles);
+          if (bm == 256 && nwv == 8) hipLaunchKernelGGL((k_fwd16p<256, 8>), g, dim3(512), 0, s, bp);
+          else if (bm == 256) hipLaunchKernelGGL((k_fwd16p<256, 16>), g, dim3(1024), 0, s, bp);
+          else if (nwv == 8) hipLaunchKernelGGL((k_fwd16p<128, 8>), g, dim3(512), 0, s, bp);
+          else hipLaunchKernelGGL((k_fwd16p<128, 16>), g, dim3(1024), 0, s, bp);
           HIP_LAUNCH_CHECK();
           return;
         }
