@@ -2316,7 +2316,8 @@ static int dw_split_plan(GemmBatch& b, int64_t* stride) {
   // as many K splits as fit in one pass over the chip's workgroup slots (2 per CU at
   // 67 KB of LDS each): a partial second pass costs a whole slab loop (config 5: a
   // 528-workgroup L6 took 96 us, 440 workgroups 82 us)
-  int ns = SACMI_DW_TARGET / tiles;
+  static const int target = std::getenv("SACMI_DW_TARGET") ? std::atoi(std::getenv("SACMI_DW_TARGET")) : SACMI_DW_TARGET;
+  int ns = target / tiles;
   ns = ns < 1 ? 1 : ns > kDwMaxSplit ? kDwMaxSplit : ns;
   if ((int64_t)ns * el > b.ws_floats) return 0;
   *stride = el;
@@ -2403,8 +2404,12 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
         case 4: hipLaunchKernelGGL(k_dw_fin<4>, fg, fb, 0, s, b, ns, stride); break;
         case 5: hipLaunchKernelGGL(k_dw_fin<5>, fg, fb, 0, s, b, ns, stride); break;
         case 6: hipLaunchKernelGGL(k_dw_fin<6>, fg, fb, 0, s, b, ns, stride); break;
+        case 7: hipLaunchKernelGGL(k_dw_fin<7>, fg, fb, 0, s, b, ns, stride); break;
         case 8: hipLaunchKernelGGL(k_dw_fin<8>, fg, fb, 0, s, b, ns, stride); break;
+        case 9: hipLaunchKernelGGL(k_dw_fin<9>, fg, fb, 0, s, b, ns, stride); break;
         case 10: hipLaunchKernelGGL(k_dw_fin<10>, fg, fb, 0, s, b, ns, stride); break;
+        case 11: hipLaunchKernelGGL(k_dw_fin<11>, fg, fb, 0, s, b, ns, stride); break;
+        case 12: hipLaunchKernelGGL(k_dw_fin<12>, fg, fb, 0, s, b, ns, stride); break;
         default: hipLaunchKernelGGL(k_dw_fin<kDwMaxSplit>, fg, fb, 0, s, b, ns, stride); break;
       }
       HIP_LAUNCH_CHECK();
