@@ -529,6 +529,41 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   p = p + (-k.step_size * m) / denom;
 }
 
+// Block 0 of a fused-Adam level (k_gemm / k_dw_fin): the level's losses, the scalar
+// log_alpha step (alpha = exp(log_alpha), sac_imp.py:128-135) and the loss ring slot —
+// none of them after a non-finite sample (the reference raised first; err: ErrBits this
+// update saw) — and the error bits for the synchronous step's host-mapped readback.
+__device__ __forceinline__ void adam_block0(const AdamFuse& af, int err, float omb1, float omb2) {
+  {
+    __syncthreads();
+    if (threadIdx.x == 0 && af.loss_host) af.loss_host[3] = __int_as_float(err);
+    if (threadIdx.x < af.n_losses && !err) {
+      float sum = 0.f;
+      for (int w = 0; w < af.n_part; ++w) sum += af.loss_part[w * af.n_losses + threadIdx.x];
+      af.sc->losses[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
+      if (af.loss_host) af.loss_host[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
+    }
+    if (threadIdx.x == 0 && af.log_alpha_idx >= 0 && af.auto_entropy && !err) {
+      const AdamScalars k = fuse_scalars(af, 3, af.step_offset);
+      const int64_t i = af.log_alpha_idx;
+      float pp = af.P[i], mm = af.M[i], vv = af.V[i];
+      adam_elem(pp, mm, vv, *af.log_alpha_grad, omb1, af.beta2, omb2, af.eps, k);
+      af.P[i] = pp; af.M[i] = mm; af.V[i] = vv;
+      af.sc->alpha = expf(pp);
+      af.sc->alpha_is_tensor = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && af.loss_ring && !err) {
+      const int64_t pos = af.sc->loss_ring_pos;
+      const int64_t q = pos % af.ring;
+      af.loss_ring[q * 3 + 0] = af.sc->losses[0];
+      af.loss_ring[q * 3 + 1] = af.sc->losses[1];
+      af.loss_ring[q * 3 + 2] = af.sc->losses[2];
+      af.sc->loss_ring_pos = pos + 1;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // grouped GEMM: one launch runs every independent GEMM of one dependency level.
 // One workgroup (16 waves, K split 16 ways) per output tile, one workgroup per CU.
@@ -629,13 +664,22 @@ __device__ void rows_finish(const RowsFuse& rf, const GemmDesc& d, int m0, bool 
       for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
       if (lane == 0) {
         if (rf.alpha_grad) *rf.alpha_grad = -(acc + (float)rf.B * rf.target_entropy) / (float)rf.B;
-        // step counters: the critic Adam ran before this level, the actor Adam after
+        // step counters: the critic Adam ran before this level, the actor Adam after.  After
+        // a non-finite policy sample (ErrBits) only the steps the reference took advance —
+        // none (target batch / PER / an earlier update), or the critics' (actor batch,
+        // sac_imp.py:116 raises after the q optimizers stepped) — selected, not branched:
+        // every load goes out at once
+        const int err = rf.sc->err;
+        const bool any = (err & kErrSkipAll) == 0;
+        const bool all = any && (err & ERR_NAN_ACT) == 0;
         for (int i = 0; i < 4; ++i) {
-          rf.sc->step[i] += 1.0;
-          rf.sc->beta_pow[i][0] *= 0.9;   // torch Adam default betas (sac_imp.py:39-49)
-          rf.sc->beta_pow[i][1] *= 0.999;
+          const bool adv = all || (any && (i == 1 || i == 2));
+          rf.sc->step[i] += adv ? 1.0 : 0.0;
+          rf.sc->beta_pow[i][0] *= adv ? 0.9 : 1.0;   // torch Adam default betas (sac_imp.py:39-49)
+          rf.sc->beta_pow[i][1] *= adv ? 0.999 : 1.0;
         }
-        rf.sc->noise_counter += 1;
+        rf.sc->noise_counter += all ? 1 : 0;
+        if (any && !all) atomicOr(&rf.sc->err, (int)ERR_ABORT);
       }
     }
   }
@@ -738,6 +782,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
   __shared__ float rsum[MG * KSPLIT * TM];
   __shared__ AdamScalars s_k;
+  __shared__ int s_err;
   __shared__ float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
   // dL/da partials (axk-1 levels of one 32-row wave group): the tile's outputs [TMW][TN+1]
   // and its fc1 action weights [TN][32]
@@ -775,8 +820,10 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   }
   const int m0 = tr * TMW, n0 = tc * TN;
   const bool rowsum = d.rs_col >= 0 && n0 == 0;
-  if (ADAM && threadIdx.x == 0)
+  if (ADAM && threadIdx.x == 0) {
     s_k = fuse_scalars(batch.adam, d.adam_step, batch.adam.step_offset);
+    s_err = batch.adam.sc->err;     // (loaded with the step scalars: no extra round trip)
+  }
   const AdamFuse& af = batch.adam;
   // Element slots: EPT tile outputs per thread (e = tid + s*NTH) plus one slot for the
   // rowsum (bias-gradient) column.  Their epilogue operands (bias, ReLU mask, Adam
@@ -892,10 +939,15 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   __syncthreads();
   if (threadIdx.x < 64) SACMI_STAMP(32);
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
+  // a non-finite policy sample / PER draw of this update (ErrBits): the reference raised
+  // before this step (no stores), or after the critic step but before Polyak
+  const int err = ADAM ? s_err : 0;
+  const bool void_st = ADAM && (err & af.err_skip) != 0;
+  const bool pol_st = pol && (err & af.err_nopolyak) == 0;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     int row, col, n;
-    const bool ok = slot(s, row, col, n);
+    const bool ok = slot(s, row, col, n) && !void_st;
     float v = 0.f;
     if (ok) {
       if (s < EPT) {
@@ -915,14 +967,14 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
         if (af.G) buf_st_pol(rG, o, v, wt);
         buf_st_pol(rC, o, x0[s], wt); buf_st_pol(rM, o, x1[s], wt); buf_st_pol(rV, o, x2[s], wt);
         if (af.Ph) st_pol(af.Ph + abase + (o >> 2), bf16_bits(x0[s]), wt);
-        if (pol) {
+        if (pol_st) {
           const float tn = polyak(x3[s], x0[s], omtau, af.tau);
           buf_st_pol(rT, o, tn, wt);
           if (af.Th) st_pol(af.Th + abase - af.t_base + (o >> 2), bf16_bits(tn), wt);
         }
       } else {
         if (d.bias) v += x0[s];
-        if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
+        if (d.epi == EPI_RELU) v = v <= 0.f ? 0.f : v;   // F.relu: NaN stays NaN
         else if (d.epi == EPI_MASK) v = x0[s] > 0.f ? v : 0.f;
         buf_st_pol(rC, o, v, wt);
       }
@@ -969,31 +1021,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
     }
   }
   if (batch.has_adam && bid == 0) {
-    __syncthreads();
-    if (threadIdx.x < af.n_losses) {
-      float sum = 0.f;
-      for (int w = 0; w < af.n_part; ++w) sum += af.loss_part[w * af.n_losses + threadIdx.x];
-      af.sc->losses[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
-      if (af.loss_host) af.loss_host[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
-    }
-    if (threadIdx.x == 0 && af.log_alpha_idx >= 0 && af.auto_entropy) {
-      const AdamScalars k = fuse_scalars(af, 3, af.step_offset);
-      const int64_t i = af.log_alpha_idx;
-      float pp = af.P[i], mm = af.M[i], vv = af.V[i];
-      adam_elem(pp, mm, vv, *af.log_alpha_grad, omb1, af.beta2, omb2, af.eps, k);
-      af.P[i] = pp; af.M[i] = mm; af.V[i] = vv;
-      af.sc->alpha = expf(pp);
-      af.sc->alpha_is_tensor = 1;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && af.loss_ring) {
-      const int64_t pos = af.sc->loss_ring_pos;
-      const int64_t q = pos % af.ring;
-      af.loss_ring[q * 3 + 0] = af.sc->losses[0];
-      af.loss_ring[q * 3 + 1] = af.sc->losses[1];
-      af.loss_ring[q * 3 + 2] = af.sc->losses[2];
-      af.sc->loss_ring_pos = pos + 1;
-    }
+    adam_block0(af, err, omb1, omb2);
   }
 }
 
@@ -1090,7 +1118,7 @@ struct FwdEpi {
           const int col = c0 + j * 16 + (lane & 15);
           float v = acc[i][j][r];
           if (has_bias) v += bias_x[j];
-          if (d.epi == EPI_RELU) v = v > 0.f ? v : 0.f;
+          if (d.epi == EPI_RELU) v = v <= 0.f ? 0.f : v;   // F.relu: NaN stays NaN
           if constexpr (C16) acc[i][j][r] = v;
           else if (row < M && col < N) st_big(d.C + (size_t)row * d.ldc + col, v);
           if (has_dot) {
@@ -2182,10 +2210,14 @@ template <int NSL>
 __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_FIN);
   __shared__ AdamScalars s_k[3];
+  __shared__ int s_err;
   const AdamFuse& af = batch.adam;
   const bool adam = batch.has_adam != 0;
   if (adam && threadIdx.x < 3) s_k[threadIdx.x] = fuse_scalars(af, threadIdx.x, af.step_offset);
+  if (threadIdx.x == 0) s_err = adam ? af.sc->err : 0;
   __syncthreads();
+  // a non-finite policy sample / PER draw of this update (ErrBits, see k_gemm)
+  const bool void_st = (s_err & af.err_skip) != 0;
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
   // kDwFinEpt elements per thread (element e = block base + k * 256 + thread: coalesced),
   // the workgroups dealt to the descs in order: every workgroup belongs to one desc, and
@@ -2200,11 +2232,12 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
     if (q < 0) off += n_el_q;
     acc += nb;
   }
-  if (q >= 0) {
+  if (q >= 0 && !void_st) {
     const GemmDesc& d = batch.d[q];
     const int nc = dw_ncols(d);
     const int n_el = d.M * nc;                  // < 2^31 (checked by dw_split_plan)
     const bool pol = d.epi == EPI_ADAM_POLYAK;
+    const bool pol_st = pol && (s_err & af.err_nopolyak) == 0;
     const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
     const float* wsd = batch.ws + off;
     const bool wt = batch.st_wt != 0;            // write-through parameter / state stores
@@ -2247,7 +2280,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
         st_pol(d.C + o[k], pp[k], wt); st_pol(af.M + abase + o[k], mm[k], wt);
         st_pol(af.V + abase + o[k], vv[k], wt);
         if (af.Ph) st_pol(af.Ph + abase + o[k], (unsigned short)bf16_bits(pp[k]), wt);
-        if (pol) {
+        if (pol_st) {
           const float tn = polyak(tt[k], pp[k], omtau, af.tau);
           st_pol(af.T + abase - af.t_base + o[k], tn, wt);
           if (af.Th) st_pol(af.Th + abase - af.t_base + o[k], (unsigned short)bf16_bits(tn), wt);
@@ -2257,33 +2290,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
       }
     }
   }
-  if (adam && blockIdx.x == 0) {
-    __syncthreads();
-    if (threadIdx.x < af.n_losses) {
-      float sum = 0.f;
-      for (int w = 0; w < af.n_part; ++w) sum += af.loss_part[w * af.n_losses + threadIdx.x];
-      af.sc->losses[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
-      if (af.loss_host) af.loss_host[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
-    }
-    if (threadIdx.x == 0 && af.log_alpha_idx >= 0 && af.auto_entropy) {
-      const AdamScalars k = fuse_scalars(af, 3, af.step_offset);
-      const int64_t i = af.log_alpha_idx;
-      float pp = af.P[i], mm = af.M[i], vv = af.V[i];
-      adam_elem(pp, mm, vv, *af.log_alpha_grad, omb1, af.beta2, omb2, af.eps, k);
-      af.P[i] = pp; af.M[i] = mm; af.V[i] = vv;
-      af.sc->alpha = expf(pp);
-      af.sc->alpha_is_tensor = 1;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && af.loss_ring) {
-      const int64_t pos = af.sc->loss_ring_pos;
-      const int64_t q = pos % af.ring;
-      af.loss_ring[q * 3 + 0] = af.sc->losses[0];
-      af.loss_ring[q * 3 + 1] = af.sc->losses[1];
-      af.loss_ring[q * 3 + 2] = af.sc->losses[2];
-      af.sc->loss_ring_pos = pos + 1;
-    }
-  }
+  if (adam && blockIdx.x == 0) adam_block0(af, s_err, omb1, omb2);
 }
 
 // 1 when the level carries bf16 activation operands (any GemmDesc a16 / b16 / c16 / x16);
@@ -2637,6 +2644,15 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       const float ls_raw = reduce_partials<TM, TN, KSPLIT>(red, row, A + j) + bl;
       const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
       const float sd = expf(ls);
+      // Normal(mean, std) argument validation (networks_model1.py:87): loc must be real (not
+      // NaN) and scale positive — std = exp(clamp(log_std)) is NaN only for a NaN log_std
+      // (torch.clamp keeps NaN; fmaxf above does not, hence the raw value).  evaluate=True
+      // (deterministic) builds no Normal, so nothing is checked there (sac_imp.py:59-65).
+      if (a.nan_flag && !a.deterministic && (__builtin_isnan(mean) || __builtin_isnan(ls_raw))) {
+        const int bit = m < a.split_row ? a.nan_bit_lo : a.nan_bit_hi;
+        if (a.nan_plain) *a.nan_flag = bit;
+        else atomicOr(a.nan_flag, bit);
+      }
       float eps;
       if (a.deterministic) {
         eps = 0.f;
@@ -2965,6 +2981,26 @@ bool gemm_level_on_axk16(const GemmBatch& b0) {
   return SACMI_AXK_LDS16 && axk16_ok(b) >= 0;
 }
 
+// launch_gemm's own kernel choice for an axk-1 level, asked ahead of its launch: true when
+// it runs on the one-wave-group k_gemm tiles (<32, 32, 16, 2, 1, false, 1>: MG == 1, AXK ==
+// 1), the only form that computes dL/da partials.  Mirrors launch_gemm's order: split-K and
+// the LDS-staged forward kernels never take an axk level; k_axk16 (bf16, batch-4096 class);
+// then the 64-row-tile branch (more than 512 32x64 tiles, e.g. batch 1024 with hidden > 512)
+bool gemm_level_pa_capable(const GemmBatch& b0) {
+  if (gemm_level_on_axk16(b0)) return false;
+  GemmBatch b = b0;
+  bool dw = true;
+  int axk = 0, n_adam = 0;
+  for (int i = 0; i < b.count; ++i) {
+    dw = dw && !b.d[i].a_kc && !b.d[i].b_kc;
+    axk = b.d[i].axk > axk ? b.d[i].axk : axk;
+    n_adam += b.d[i].epi >= EPI_ADAM;
+  }
+  const int t64 = assign_tiles<32, 64>(b);
+  if (dw || n_adam || t64 > 512) return false;
+  return axk == 1;
+}
+
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -2982,14 +3018,21 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
   const TlMark tl_mark(a.tl, TL_ADAM);
   __shared__ AdamScalars s_k[kMaxAdamSegs];
   __shared__ int64_t s_prefix[kMaxAdamSegs + 1];
+  __shared__ int s_err;
   if (threadIdx.x < a.nseg) s_k[threadIdx.x] = adam_scalars(a, a.seg[threadIdx.x].step_idx);
   if (threadIdx.x == 0) {
     int64_t p = 0;
     for (int i = 0; i < a.nseg; ++i) { s_prefix[i] = p; p += a.seg[i].n / 4; }
     s_prefix[a.nseg] = p;
+    s_err = a.sc->err;
   }
   __syncthreads();
   const float om_b1 = 1.f - a.beta1, om_b2 = 1.f - a.beta2, omtau = 1.f - a.tau;
+  // a non-finite policy sample / PER draw of this update (ErrBits, see k_gemm): no step,
+  // or (critic, actor-batch NaN) the step without Polyak
+  const int err = s_err;
+  if (err & a.err_skip) return;
+  const bool pol = a.tgt && (err & a.err_nopolyak) == 0;
   const int64_t total4 = s_prefix[a.nseg];
   // parameter / moment / target arenas: one descriptor each (offsets < 2 GiB: the arenas
   // hold at most a few million floats)
@@ -3022,7 +3065,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
       st_wt(a.ph + i, bf16_bits(p.x)); st_wt(a.ph + i + 1, bf16_bits(p.y));
       st_wt(a.ph + i + 2, bf16_bits(p.z)); st_wt(a.ph + i + 3, bf16_bits(p.w));
     }
-    if (a.tgt) {
+    if (pol) {
       t.x = polyak(t.x, p.x, omtau, a.tau);
       t.y = polyak(t.y, p.y, omtau, a.tau);
       t.z = polyak(t.z, p.z, omtau, a.tau);
@@ -3035,7 +3078,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
       }
     }
   }
-  if (blockIdx.x != 0) return;
+  if (blockIdx.x != 0 || err) return;
   if (threadIdx.x == 0 && a.log_alpha_idx >= 0 && a.auto_entropy) {
     const AdamScalars k = adam_scalars(a, 3);
     const int64_t i = a.log_alpha_idx;

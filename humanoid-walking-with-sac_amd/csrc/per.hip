@@ -175,10 +175,14 @@ __global__ __launch_bounds__(256) void k_per_chunk_sum(const float* probs, int64
 }
 
 // 3. normalise + fixed point + block-local inclusive scan
+// NaN / inf / zero normaliser: np.random.choice(p=probs) raises "probabilities contain NaN"
+// (replay_buffer.py:60-64; a NaN, negative or infinite priority, or none positive)
+__device__ __forceinline__ bool per_total_bad(float t) { return !(t > 0.f && t <= 3.402823466e38f); }
+
 __global__ __launch_bounds__(kScanBlock) void k_per_norm_scan(float* probs, int64_t len,
                                                               const float* chunk_sum, int nchunk,
                                                               int64_t* q, int64_t* block_sum,
-                                                              int* bad) {
+                                                              int* bad, int* err) {
 #pragma clang fp contract(off)
   __shared__ float s_total;
   __shared__ int64_t wsum[kScanBlock / 64];
@@ -186,6 +190,10 @@ __global__ __launch_bounds__(kScanBlock) void k_per_norm_scan(float* probs, int6
     float t = -0.0f;
     for (int c = 0; c < nchunk; ++c) t = t + chunk_sum[c];
     s_total = t;
+    if (blockIdx.x == 0 && per_total_bad(t)) {   // bad[5]: this draw's own NaN
+      bad[5] = 1;
+      atomicOr(err, (int)ERR_NAN_PER);
+    }
   }
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kScanBlock + threadIdx.x;
@@ -263,11 +271,17 @@ __global__ void k_per_cdf(const int64_t* q, const int64_t* block_off, const floa
 // (replay_buffer.py:54; -beta stored after the k uniforms) and frame += 1.
 __global__ __launch_bounds__(1024) void k_per_uniforms(uint32_t* mt, int gen_u, const double* u_in,
                                                        double* u_out, int k, DevScalars* sc,
-                                                       double beta_start, double beta_frames) {
+                                                       double beta_start, double beta_frames,
+                                                       const int* bad, const int* err,
+                                                       int skip_on_err) {
   extern __shared__ uint32_t words[];   // 2k words
   __shared__ uint32_t key[kMtN];
   const int t = threadIdx.x;
-  if (gen_u) {
+  // this draw's probabilities are NaN (bad[5]): the frame advances, the stream does not;
+  // an update graph's draw after an earlier non-finite sample: nothing happens at all
+  const bool own_nan = bad[5] != 0;
+  if (!own_nan && skip_on_err && *err) return;
+  if (gen_u && !own_nan) {
     for (int i = t; i < kMtN; i += blockDim.x) key[i] = mt[i];
     int pos = (int)mt[kMtN];
     __syncthreads();
@@ -447,9 +461,18 @@ __global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
     __shared__ uint32_t key[kMtN];
     uint32_t* words = reinterpret_cast<uint32_t*>(dyn);
     const int t = threadIdx.x;
+    // an update graph's draw after an earlier non-finite sample (ErrBits): the reference
+    // never reached it — no draw, no frame step.  Otherwise the stream's words are backed up
+    // (bad[4] = 1): F2 puts them back if these probabilities turn out NaN
+    if (a.skip_on_err && *a.err) {
+      if (t == 0) a.bad[4] = 0;
+      return;
+    }
     if (a.gen_u) {
       for (int i = t; i < kMtN; i += blockDim.x) key[i] = a.mt[i];
       int pos = (int)a.mt[kMtN];
+      for (int i = t; i < kMtN; i += blockDim.x) a.mt_backup[i] = key[i];
+      if (t == 0) a.mt_backup[kMtN] = (uint32_t)pos;
       __syncthreads();
       const int need = 2 * a.k;
       for (int done = 0; done < need;) {
@@ -474,6 +497,7 @@ __global__ __launch_bounds__(256) void k_per_f1(PerArgs a, int nchunk) {
       if (beta > 1.0) beta = 1.0;
       a.u_scratch[a.k] = -beta;
       a.sc->per_frame += 1;
+      a.bad[4] = a.gen_u ? 1 : 0;
     }
     return;
   }
@@ -527,6 +551,15 @@ __global__ __launch_bounds__(kF2Threads) void k_per_f2(PerArgs a) {
         t = t + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
     }
     if (threadIdx.x == 0) s_total = t;
+  }
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    if (per_total_bad(s_total)) {
+      // "probabilities contain NaN": report, and give the numpy stream its words back
+      if (threadIdx.x == 0) atomicOr(a.err, (int)ERR_NAN_PER);
+      if (a.bad[4])
+        for (int i = threadIdx.x; i <= kMtN; i += blockDim.x) a.mt[i] = a.mt_backup[i];
+    }
   }
   const int64_t i0 = (int64_t)blockIdx.x * kScanBlock + 4 * threadIdx.x;
   float pin[4];
@@ -700,14 +733,15 @@ void launch_per_sample(const PerArgs& a, hipStream_t s) {
   const int nchunk = (int)((len + kChunk - 1) / kChunk);
   hipLaunchKernelGGL(k_per_chunk_sum, dim3(nchunk), dim3(128), 0, s, a.probs, len, a.chunk_sums);
   const int nb = (int)((len + kScanBlock - 1) / kScanBlock);
-  (void)hipMemsetAsync(a.bad, 0, 8, s);     // bad flag, max-weight bits
+  (void)hipMemsetAsync(a.bad, 0, 24, s);    // bad flag, max-weight bits, .., own-NaN flag
   hipLaunchKernelGGL(k_per_norm_scan, dim3(nb), dim3(kScanBlock), 0, s, a.probs, len,
-                     a.chunk_sums, nchunk, a.q, a.block_sums, a.bad);
+                     a.chunk_sums, nchunk, a.q, a.block_sums, a.bad, a.err);
   hipLaunchKernelGGL(k_per_scan_blocks, dim3(1), dim3(1024), 0, s, a.block_sums, nb);
   hipLaunchKernelGGL(k_per_cdf, dim3((unsigned)blocks), dim3(256), 0, s, a.q, a.block_sums,
                      a.probs, len, a.bad, a.cdf);
   hipLaunchKernelGGL(k_per_uniforms, dim3(1), dim3(1024), (size_t)a.k * 8, s, a.mt, a.gen_u,
-                     a.u, a.u_scratch, a.k, a.sc, a.beta_start, a.beta_frames);
+                     a.u, a.u_scratch, a.k, a.sc, a.beta_start, a.beta_frames, a.bad, a.err,
+                     a.skip_on_err);
   int64_t stride = 1024;
   while ((len + stride - 1) / stride > kTopMax) stride *= 2;
   const int ntop = (int)((len + stride - 1) / stride);

@@ -100,6 +100,10 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
   const int64_t n64 = a.sc->len;
   const uint32_t n = (uint32_t)n64;
   const int k = a.k;
+  // an update graph's sampler after a non-finite policy sample / PER draw (ErrBits): the
+  // reference raised and never reached this sample, so the stream is left as it is (read
+  // with the key: no extra round trip; the indices it writes belong to a voided update)
+  const bool keep = !(a.skip_on_err && a.sc->err);
   for (int i = t; i < kMtN; i += blockDim.x) key[i] = a.mt[i];
   if (t == 0) s_pos = (int)a.mt[kMtN];
   __syncthreads();
@@ -210,6 +214,7 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
     pos += s_last + 1;
   }
   __syncthreads();
+  if (!keep) return;
   for (int i = t; i < kMtN; i += blockDim.x) a.mt[i] = key[i];
   if (t == 0) a.mt[kMtN] = (uint32_t)pos;
 }

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -35,12 +36,29 @@ static thread_local std::string g_last_error;
     if (!(cond)) throw Error{code, (msg)}; \
   } while (0)
 
-// every device allocation of the process, for the host-side bounds validator
+// every device allocation of the process, for the host-side bounds validator; guarded by
+// registry_mutex() (contexts may live on several host threads)
 struct AllocRec { uintptr_t base; size_t bytes; };
 static std::vector<AllocRec>& alloc_registry() {
   static std::vector<AllocRec> r;
   return r;
 }
+static std::mutex& registry_mutex() {
+  static std::mutex m;
+  return m;
+}
+static void registry_add(uintptr_t base, size_t bytes) {
+  std::lock_guard<std::mutex> g(registry_mutex());
+  alloc_registry().push_back({base, bytes});
+}
+static void registry_remove(uintptr_t base) {
+  std::lock_guard<std::mutex> g(registry_mutex());
+  auto& reg = alloc_registry();
+  for (size_t i = 0; i < reg.size(); ++i)
+    if (reg[i].base == base) { reg.erase(reg.begin() + i); break; }
+}
+// the validator self test checks against its own host arrays instead (this thread only)
+static thread_local const std::vector<AllocRec>* g_registry_override = nullptr;
 
 template <class T>
 struct DevBuf {
@@ -54,13 +72,11 @@ struct DevBuf {
       // zero-fill before anything is enqueued there (init writes the 1-columns).
       CHECK_HIP(hipMemset(p, 0, count * sizeof(T)));
       CHECK_HIP(hipDeviceSynchronize());
-      alloc_registry().push_back({(uintptr_t)p, count * sizeof(T)});
+      registry_add((uintptr_t)p, count * sizeof(T));
     }
   }
   void release() {
-    auto& reg = alloc_registry();
-    for (size_t i = 0; i < reg.size(); ++i)
-      if (reg[i].base == (uintptr_t)p) { reg.erase(reg.begin() + i); break; }
+    if (p) registry_remove((uintptr_t)p);
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
@@ -110,6 +126,7 @@ struct sacmi_ctx {
   int64_t capacity = 0, len = 0, wpos = 0;
   sacmi::DevBuf<float> obs, act, rew, obs2, done, prio;
   sacmi::DevBuf<uint32_t> mt;      // [2][625]: random / numpy streams
+  sacmi::DevBuf<uint32_t> mt_backup;   // [625]: the numpy stream before a PER draw (NaN probs)
   // scratch
   sacmi::DevBuf<int32_t> idx32, idx32b;   // b: second batch set (odd updates of a graph)
   sacmi::DevBuf<int64_t> idx64, idx64b;
@@ -142,7 +159,10 @@ struct sacmi_ctx {
   int push_slot = 0;
   float* act_host = nullptr;                // [kActPinned][S] states, then [..][A] eps / out
   float* act_host_dev = nullptr;            // the same memory, device-mapped
-  float* loss_host = nullptr;               // [4] losses of the last fused update (mapped)
+  int* act_nan_host = nullptr;              // select_action's Normal validation flag (mapped)
+  int* act_nan_dev = nullptr;
+  float* loss_host = nullptr;               // [4] losses of the last fused update (mapped),
+                                            //   word 3: its ErrBits
   float* loss_host_dev = nullptr;
   sacmi::DevScalars* sc_host = nullptr;
   float* ring_host = nullptr;               // [ring_slots][3] loss readback staging
@@ -278,7 +298,8 @@ static void alloc_all(sacmi_ctx* c) {
     c->per_cdf.alloc(cap);
     c->per_chunk.alloc(cap / 8192 + 2);
     c->per_blk.alloc(cap / 1024 + 2);
-    c->per_bad.alloc(4);
+    c->per_bad.alloc(8);
+    c->mt_backup.alloc(kMtN + 1);
     c->per_owner.alloc(cap);
     CHECK_HIP(hipMemset(c->per_owner.p, 0xFF, (size_t)cap * 4));   // -1: no writer
     CHECK_HIP(hipDeviceSynchronize());
@@ -355,9 +376,11 @@ static void alloc_pinned(sacmi_ctx* c) {
   // select_action staging: fine-grained (coherent) and mapped, so the kernels read the
   // states and write the actions in place (no copy commands on the env-rate path)
   CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->act_host),
-                          (size_t)kActPinned * (S + 2 * A) * 4,
+                          (size_t)kActPinned * (S + 2 * A) * 4 + 16,
                           hipHostMallocMapped | hipHostMallocCoherent));
   CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->act_host_dev), c->act_host, 0));
+  c->act_nan_host = reinterpret_cast<int*>(c->act_host + (size_t)kActPinned * (S + 2 * A));
+  c->act_nan_dev = reinterpret_cast<int*>(c->act_host_dev + (size_t)kActPinned * (S + 2 * A));
   // update_parameters' three losses, stored here by the fused Adam levels' block 0: the
   // synchronous step reads them after the stream sync, no copy command
   CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->loss_host), 16,
@@ -382,6 +405,8 @@ static void free_pinned(sacmi_ctx* c) {
   c->ring_host = nullptr;
   c->act_host = nullptr;
   c->act_host_dev = nullptr;
+  c->act_nan_host = nullptr;
+  c->act_nan_dev = nullptr;
   if (c->loss_host) (void)hipHostFree(c->loss_host);
   c->loss_host = nullptr;
   c->loss_host_dev = nullptr;
@@ -427,8 +452,14 @@ static GemmDesc gd_dw_h(const float* dY, int ldy, const float* X, int ldx, float
 static void check_span(const void* p, int64_t max_index, const char* what, int elem_bytes = 4) {
   if (!p) throw Error{SACMI_ESTATE, std::string("null GEMM operand ") + what};
   const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)(max_index + 1) * elem_bytes;
-  for (const AllocRec& r : alloc_registry())
-    if (a >= r.base && e <= r.base + r.bytes) return;
+  if (g_registry_override) {
+    for (const AllocRec& r : *g_registry_override)
+      if (a >= r.base && e <= r.base + r.bytes) return;
+  } else {
+    std::lock_guard<std::mutex> g(registry_mutex());
+    for (const AllocRec& r : alloc_registry())
+      if (a >= r.base && e <= r.base + r.bytes) return;
+  }
   throw Error{SACMI_ESTATE, std::string("GEMM operand out of bounds: ") + what};
 }
 
@@ -587,6 +618,8 @@ static PerArgs per_args_impl(sacmi_ctx* c, int k, int gen_u, int32_t* idx32, int
   a.k = k; a.sc = c->sc.p; a.beta_start = c->cfg.per_beta_start;
   a.beta_frames = c->cfg.per_beta_frames; a.idx32 = idx32; a.idx_out = idx64;
   a.w_out = c->per_w.p;
+  a.err = &c->sc.p->err; a.mt_backup = c->mt_backup.p;
+  a.skip_on_err = 1;       // update graphs; the host API (sacmi_per_sample) clears it
   return a;
 }
 
@@ -616,6 +649,7 @@ static MtSampleArgs mt_args(sacmi_ctx* c, int B, const BatchBufs& bb) {
   MtSampleArgs m{};
   m.mt = c->mt.p; m.sc = c->sc.p; m.k = B;
   m.setsize = sample_setsize(B); m.idx_out = bb.idx32; m.idx64_out = bb.idx64;
+  m.skip_on_err = 1;       // update graphs; the host API (sacmi_sample_indices) clears it
   return m;
 }
 
@@ -778,6 +812,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     hs.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
     hs.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
     hs.logp_part = c->lp_part.p; hs.split_row = B;    // sums of log pi(a~|s) for dL/dlog_alpha
+    // Normal validation of policy.sample(next_state) / policy.sample(state) (sac_imp.py:89,116)
+    hs.nan_flag = &c->sc.p->err; hs.nan_bit_lo = ERR_NAN_TGT; hs.nan_bit_hi = ERR_NAN_ACT;
     if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) {
       hs.tl = c->tl_cur;
       launch_heads_sample(hs, s);
@@ -861,6 +897,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.loss_host = c->loss_host_dev;
       f.Ph = c->Ph.p; f.Th = c->Th.p;
       f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
+      f.err_skip = kErrSkipAll; f.err_nopolyak = ERR_NAN_ACT;
     }
     if (ride_b) {   // the next update's random.sample rides in L6 (placement B)
       l6.b.ride.kind = 1; l6.b.ride.nblocks = 1;
@@ -895,6 +932,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     // the bf16 shadows of the updated critics and targets (read by the bf16 level kernels
     // of L7 on: without them the data-parallel bf16 update read stale critic weights)
     ad.ph = c->Ph.p; ad.tgth = c->Th.p;
+    ad.err_skip = kErrSkipAll; ad.err_nopolyak = ERR_NAN_ACT;
     if (mark(c, "adam_critic_polyak")) {
       ad.tl = c->tl_cur;
       launch_adam(ad, s);
@@ -943,8 +981,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     l9.b.bf16 = c->bf16 ? 1 : 0;
     // (batch <= 1024: the standalone L10 runs on B / 16 workgroups, too few to stream dha1;
     // at batch 4096 it fills the chip and the fold measured slower: config 3 L9 55 -> 71 us)
+    // (and only where launch_gemm takes the one-wave-group tiles that form the partials:
+    // batch 1024 with hidden > 512 goes to the 64-row tiles and keeps L10)
     const bool fold_dlda = nh == 2 && B <= 1024 && !std::getenv("SACMI_NO_DLDA_FOLD") &&
-                           !gemm_level_on_axk16(l9.b);
+                           gemm_level_pa_capable(l9.b);
     if (fold_dlda) {
       for (int i = 0; i < 2; ++i) {
         GemmDesc& g = l9.b.d[i];
@@ -1017,6 +1057,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.loss_div = (float)B; f.log_alpha_idx = c->la_idx; f.auto_entropy = c->cfg.auto_entropy;
       f.log_alpha_grad = G + c->la_idx;
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
+      f.err_skip = ~0; f.err_nopolyak = 0;
     }
     if (ride_next && !ride_b) {
       // the next update's random.sample rides in L12 (128 tiles: idle CUs)
@@ -1050,6 +1091,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     ad.loss_div = (float)B; ad.log_alpha_idx = c->la_idx; ad.auto_entropy = c->cfg.auto_entropy;
     ad.loss_ring = use_ring ? c->ring.p : nullptr; ad.ring = c->ring_slots;
     ad.ph = c->Ph.p; ad.tgth = c->Th.p;
+    ad.err_skip = ~0; ad.err_nopolyak = 0;
     if (mark(c, "adam_actor_alpha")) {
       ad.tl = c->tl_cur;
       launch_adam(ad, s);
@@ -1181,6 +1223,25 @@ static void check_batch(sacmi_ctx* c, int B) {
 static void check_device_batch(sacmi_ctx* c, int B) {
   check_batch(c, B);
   REQUIRE(B <= 4096, SACMI_EVALUE, "device sampling supports batch <= 4096");
+}
+
+// ErrBits -> the ValueError text the reference raises there (SACMI_ENAN)
+static std::string nan_message(const sacmi_ctx* c, int err, int B, const std::string& where) {
+  const std::string shp = "(" + std::to_string(B) + ", " + std::to_string(c->A) + ")";
+  const std::string normal = "Expected parameters loc / scale (Tensor of shape " + shp +
+                             ") of distribution Normal to satisfy the constraints Real() / "
+                             "GreaterThan(lower_bound=0.0), but found invalid values (NaN) in ";
+  std::string m;
+  if (err & ERR_NAN_PER) m = "probabilities contain NaN (PrioritizedReplayBuffer.sample, replay_buffer.py:64)";
+  else if (err & ERR_NAN_TGT) m = normal + "policy.sample(next_state_batch) (sac_imp.py:89)";
+  else if (err & (ERR_NAN_ACT | ERR_ABORT)) m = normal + "policy.sample(state_batch) (sac_imp.py:116)";
+  else m = "non-finite value (error bits " + std::to_string(err) + ")";
+  return m + where;
+}
+
+// forget the device error bits once reported (stream-ordered: the next update starts clean)
+static void clear_err(sacmi_ctx* c) {
+  CHECK_HIP(hipMemsetAsync(&c->sc.p->err, 0, sizeof(int32_t), c->stream));
 }
 
 static void stage_inputs(sacmi_ctx* c, int B, const int64_t* idx, const float* eps1,
@@ -1351,9 +1412,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     if (c->comm) (void)rccl().destroy(c->comm);
     c->comm = nullptr;
     if (c->G_external) {
-      auto& reg = alloc_registry();
-      for (size_t i = 0; i < reg.size(); ++i)
-        if (reg[i].base == (uintptr_t)c->G.p) { reg.erase(reg.begin() + i); break; }
+      registry_remove((uintptr_t)c->G.p);
       c->G.p = nullptr;
     }
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
@@ -1366,7 +1425,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (int l = 0; l < 3; ++l)
       for (auto* b : {&c->hp[l], &c->hq[l], &c->hqt[l], &c->hqa[l], &c->dhc[l], &c->dha[l], &c->dhp[l]})
         b->release();
-    c->sc.release(); c->mt.release(); c->idx32.release(); c->idx64.release();
+    c->sc.release(); c->mt.release(); c->mt_backup.release(); c->idx32.release(); c->idx64.release();
     c->Ph.release(); c->Th.release();
     c->idx32b.release(); c->idx64b.release();
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
@@ -1575,6 +1634,18 @@ int sacmi_len(sacmi_ctx* c, int64_t* n) {
   return guard([&] { *n = c->len; });
 }
 
+int sacmi_replay_clear(sacmi_ctx* c) {
+  return guard([&] {
+    REQUIRE(c, SACMI_EVALUE, "null ctx");
+    DevScalars h = download_scalars(c);
+    h.len = 0;
+    h.head = 0;
+    upload_scalars(c, h);
+    c->len = 0;
+    c->wpos = 0;
+  });
+}
+
 int sacmi_get_rows(sacmi_ctx* c, const int64_t* idx, int64_t n, float* s, float* a, float* r,
                    float* s2, uint8_t* d) {
   return guard([&] {
@@ -1649,7 +1720,9 @@ int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
     REQUIRE(batch <= c->Bm, SACMI_EVALUE, "batch > max_batch");
     REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
     if (batch == 0) return;
-    launch_mt_sample(mt_args(c, batch, batch_bufs(c, 0)), c->stream);
+    MtSampleArgs ma = mt_args(c, batch, batch_bufs(c, 0));
+    ma.skip_on_err = 0;                // a host call: the reference's random.sample always runs
+    launch_mt_sample(ma, c->stream);
     CHECK_HIP(hipGetLastError());
     CHECK_HIP(hipMemcpyAsync(idx_out, c->idx64.p, (size_t)batch * 8, hipMemcpyDeviceToHost, c->stream));
     CHECK_HIP(hipStreamSynchronize(c->stream));
@@ -1665,6 +1738,12 @@ int sacmi_step(sacmi_ctx* c, int32_t batch, const int64_t* idx, const float* eps
     run_update(c, batch, idx ? 0 : 1, (eps1 || eps2) ? 0 : 1, 7, 1.f, false);
     if (losses_out) {
       CHECK_HIP(hipStreamSynchronize(c->stream));
+      int err = 0;                                   // ErrBits the update's L6 saw
+      std::memcpy(&err, c->loss_host + 3, 4);
+      if (err) {
+        clear_err(c);
+        throw Error{SACMI_ENAN, nan_message(c, err, batch, " during update_parameters")};
+      }
       std::memcpy(losses_out, c->loss_host, 12);    // stored by the update's last kernels
     }
   });
@@ -1704,6 +1783,11 @@ int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_o
     CHECK_HIP(hipStreamSynchronize(c->stream));
     if (n > 0) std::memcpy(out, c->ring_host, (size_t)n * 12);
     *n_out = (int32_t)n;
+    if (h.err) {   // the completed updates' losses are out; the first voided one is reported
+      clear_err(c);
+      throw Error{SACMI_ENAN, nan_message(c, h.err, c->Bm, " at update #" + std::to_string(h.loss_ring_pos) +
+                                                              " of this agent (0-based; later updates of that launch were skipped)")};
+    }
   });
 }
 
@@ -1811,9 +1895,7 @@ int sacmi_attach_grad_arena(sacmi_ctx* c, void* ptr, int64_t numel) {
     CHECK_HIP(hipDeviceSynchronize());
     if (c->G_external) {
       // the previous arena belongs to the caller: drop its registry entry, never free it
-      auto& reg = alloc_registry();
-      for (size_t i = 0; i < reg.size(); ++i)
-        if (reg[i].base == (uintptr_t)c->G.p) { reg.erase(reg.begin() + i); break; }
+      registry_remove((uintptr_t)c->G.p);
       c->G.p = nullptr;
       c->G.n = 0;
     } else {
@@ -1822,7 +1904,7 @@ int sacmi_attach_grad_arena(sacmi_ctx* c, void* ptr, int64_t numel) {
     c->G.p = (float*)ptr;
     c->G.n = (size_t)numel;
     c->G_external = true;
-    alloc_registry().push_back({(uintptr_t)ptr, (size_t)numel * 4});
+    registry_add((uintptr_t)ptr, (size_t)numel * 4);
     destroy_graphs(c);
   });
 }
@@ -2004,7 +2086,10 @@ static void timeline_of(sacmi_ctx* c, int n_updates, F&& enqueue, int32_t max_ke
         grid_out[n] = (int32_t)w[3];
         site_out[n] = sidx;
         start_us[n] = (double)(w[0] - t0) * 0.01;   // 100 MHz ticks -> us
-        end_us[n] = (double)(~w[1] - t0) * 0.01;
+        tl_word end = 0;                            // the latest exit slot (all-ones: none)
+        for (int x = 0; x < kTlEndSlots; ++x)
+          if (w[kTlEnd + x] != ~(tl_word)0) end = std::max(end, ~w[kTlEnd + x]);
+        end_us[n] = (double)(end - t0) * 0.01;
         // the site's algorithmic work, on its first kernel
         if (flops_out) flops_out[n] = k == 0 ? c->tl_flops[sidx] : 0.0;
         if (bytes_out) bytes_out[n] = k == 0 ? c->tl_bytes[sidx] : 0.0;
@@ -2060,11 +2145,22 @@ int sacmi_per_sample(sacmi_ctx* c, int32_t batch, const double* u, int64_t* idx_
     const int k = (int)std::min<int64_t>(batch, c->len);    // replay_buffer.py:50
     if (k == 0) return;
     if (u) CHECK_HIP(hipMemcpyAsync(c->per_uin.p, u, (size_t)k * 8, hipMemcpyHostToDevice, c->stream));
-    launch_per_sample(per_args(c, k, u ? 0 : 1), c->stream);
+    PerArgs pa = per_args(c, k, u ? 0 : 1);
+    pa.skip_on_err = 0;                // a host call: the reference's sample always runs
+    launch_per_sample(pa, c->stream);
     CHECK_HIP(hipGetLastError());
     if (idx_out) CHECK_HIP(hipMemcpyAsync(idx_out, c->idx64.p, (size_t)k * 8, hipMemcpyDeviceToHost, c->stream));
     if (weights_out) CHECK_HIP(hipMemcpyAsync(weights_out, c->per_w.p, (size_t)k * 4, hipMemcpyDeviceToHost, c->stream));
+    int32_t err = 0;
+    CHECK_HIP(hipMemcpyAsync(&c->sc_host->err, &c->sc.p->err, 4, hipMemcpyDeviceToHost, c->stream));
     CHECK_HIP(hipStreamSynchronize(c->stream));
+    err = c->sc_host->err;
+    if (err & ERR_NAN_PER) {           // this draw's probabilities: report and forget the bit
+      c->sc_host->err = err & ~ERR_NAN_PER;
+      CHECK_HIP(hipMemcpyAsync(&c->sc.p->err, &c->sc_host->err, 4, hipMemcpyHostToDevice, c->stream));
+      CHECK_HIP(hipStreamSynchronize(c->stream));
+      throw Error{SACMI_ENAN, "probabilities contain NaN (PrioritizedReplayBuffer.sample, replay_buffer.py:64)"};
+    }
   });
 }
 
@@ -2162,12 +2258,21 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     hs.deterministic = deterministic ? 1 : 0;
     hs.ctr_override = (1ull << 63) | (++c->act_calls);   // disjoint from update noise
     if (zc) hs.act_host = c->act_host_dev + (h_out - c->act_host);
+    // Normal(mean, std) validation of policy.sample (networks_model1.py:87; evaluate=True
+    // takes tanh(mean) without one): a plain store into host-mapped memory
+    *c->act_nan_host = 0;
+    hs.nan_flag = c->act_nan_dev; hs.nan_bit_lo = hs.nan_bit_hi = 1; hs.nan_plain = 1;
     launch_heads_sample(hs, s);
     CHECK_HIP(hipGetLastError());
     if (!zc)
       CHECK_HIP(hipMemcpy2DAsync(pinned ? h_out : a_out, (size_t)A * 4, c->x2.p + S + 1, (size_t)Kx * 4,
                                  (size_t)A * 4, n, hipMemcpyDeviceToHost, s));
     CHECK_HIP(hipStreamSynchronize(s));
+    if (!deterministic && *reinterpret_cast<volatile int*>(c->act_nan_host))
+      throw Error{SACMI_ENAN, "Expected parameters loc / scale (Tensor of shape (" + std::to_string(n) + ", " +
+                                  std::to_string(A) + ")) of distribution Normal to satisfy the constraints "
+                                  "Real() / GreaterThan(lower_bound=0.0), but found invalid values (NaN) in "
+                                  "policy.sample(state) (select_action, sac_imp.py:70)"};
     if (pinned) std::memcpy(a_out, h_out, (size_t)n * A * 4);
   });
 }
@@ -2181,12 +2286,17 @@ int sacmi_selftest_span_checker(int32_t* n_cases, int32_t* n_passed) {
     const int M = 64, N = 64, K = 128, ld = 132;
     std::vector<float> a((size_t)M * ld), w((size_t)N * ld), out((size_t)M * ld), ws(4096);
     std::vector<unsigned short> wh((size_t)N * ld), wh_short((size_t)N * ld - 8);
-    auto& reg = alloc_registry();
-    const size_t reg0 = reg.size();
+    // a registry of its own (thread-local override): the process registry, which other
+    // threads' contexts may be changing, is neither read nor written
+    std::vector<AllocRec> reg;
     for (auto* v : {&a, &w, &out, &ws})
       reg.push_back({(uintptr_t)v->data(), v->size() * sizeof(float)});
     for (auto* v : {&wh, &wh_short})
       reg.push_back({(uintptr_t)v->data(), v->size() * sizeof(unsigned short)});
+    struct Override {
+      explicit Override(const std::vector<AllocRec>* r) { g_registry_override = r; }
+      ~Override() { g_registry_override = nullptr; }
+    } use_local(&reg);
     struct Case { bool accept; GemmBatch b; };
     std::vector<Case> cases;
     auto base = [&]() {
@@ -2223,7 +2333,6 @@ int sacmi_selftest_span_checker(int32_t* n_cases, int32_t* n_passed) {
       }
       pass += ok == k.accept;
     }
-    reg.resize(reg0);
     *n_cases = (int32_t)cases.size();
     *n_passed = pass;
   });

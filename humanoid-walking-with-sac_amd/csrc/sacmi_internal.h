@@ -104,9 +104,12 @@ inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // ---------------------------------------------------------------------------
 // Launch timeline (sacmi_profile_timeline).  In an instrumented update graph every kernel
-// launch owns four words {start, ~end, kind, grid}: workgroups fold their entry clock into
-// `start` (atomicMin) and their exit clock into `~end` (atomicMin of the complement, so
-// both words start at all-ones), on the 100 MHz s_memrealtime clock.
+// launch owns kTlWords words {start, -, kind, grid, ~end[256]}: the first 8 workgroups fold
+// their entry clock into `start` (atomicMin), and each of the last 256 workgroups (the last
+// round over the CUs) stores its exit clock, complemented, into a slot of its own — no
+// contended word, so the stamps cost the kernel's tail nothing (atomics of every workgroup
+// on per-XCD words added ~0.4 us per kernel) — on the 100 MHz s_memrealtime clock; the
+// buffer starts at all-ones and the host takes the latest stored slot as the kernel's end.
 // Null pointer (every production graph): no instruction beyond the test.
 typedef unsigned long long tl_word;
 enum TlKind : int {
@@ -114,24 +117,27 @@ enum TlKind : int {
   TL_SAMPLE_BWD, TL_MT_SAMPLE, TL_GATHER, TL_PER_F1, TL_PER_F2, TL_PER_F2B, TL_PER_F3,
   TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_KINDS
 };
-constexpr int kTlWords = 4;          // words per kernel launch
+constexpr int kTlEnd = 4;            // first of the ~end slots
+constexpr int kTlEndSlots = 256;
+constexpr int kTlWords = kTlEnd + kTlEndSlots;   // words per kernel launch
 constexpr int kTlPerSite = 8;        // kernel launches one launch site may make
 struct TlMark {
   tl_word* p;
   __device__ __forceinline__ TlMark(tl_word* q, int kind) : p(q) {
-    // the first 8 workgroups (the first dispatched, one per XCD) fold in their entry; the
-    // last 8 their exit: 16 atomics per launch (every workgroup's would cost ~1.5 us per
-    // launch on the one contended word).  Wave 0 only, as a wave-uniform branch (a
-    // divergent single-lane branch around the atomic costs the big GEMM kernels ~30 VGPRs
-    // and spills); its lanes' atomics on one address with one scalar value are combined.
+    // the first 8 workgroups (the first dispatched, one per XCD) fold in their entry.  Wave
+    // 0 only, as a wave-uniform branch (a divergent single-lane branch around the atomic
+    // costs the big GEMM kernels ~30 VGPRs and spills); its lanes' atomics on one address
+    // with one scalar value are combined.
     if (p && blockIdx.x < 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u) {
       atomicMin(p, (tl_word)wall_clock64());
       if (blockIdx.x == 0) { p[2] = (tl_word)kind; p[3] = (tl_word)gridDim.x; }
     }
   }
   __device__ __forceinline__ ~TlMark() {
-    if (p && blockIdx.x + 8 >= gridDim.x && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)
-      atomicMin(p + 1, ~(tl_word)wall_clock64());
+    // wave 0 of each of the last kTlEndSlots workgroups at its exit, one slot each (the 64
+    // lanes store one scalar to one address: one store)
+    if (p && blockIdx.x + kTlEndSlots >= gridDim.x && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)
+      p[kTlEnd + (blockIdx.x & (kTlEndSlots - 1))] = ~(tl_word)wall_clock64();
   }
 };
 
@@ -147,6 +153,21 @@ struct Linear {
   int64_t numel_padded() const { return (int64_t)n_out * ld; }
 };
 
+// Non-finite inputs the reference rejects with ValueError (include/sacmi.h SACMI_ENAN),
+// kept as bits of DevScalars::err.  Set on the device where the reference would raise:
+//   ERR_NAN_TGT  policy.sample(next_state): NaN mean / log_std (Normal(validate_args),
+//                networks_model1.py:87, sac_imp.py:89) — nothing of the update has happened
+//   ERR_NAN_ACT  policy.sample(state) (sac_imp.py:116) — the critic step (sac_imp.py:101-113)
+//                has happened, the actor / alpha / Polyak steps have not
+//   ERR_NAN_PER  np.random.choice(p=probs) with NaN probabilities (replay_buffer.py:60-64):
+//                the frame has advanced, the numpy stream has not
+//   ERR_ABORT    set once an ERR_NAN_ACT update has taken its critic step: every later
+//                kernel of the stream skips its state writes
+// The host reports and clears them (sacmi_step / sacmi_fetch_losses / sacmi_per_sample).
+enum ErrBits : int { ERR_NAN_TGT = 1, ERR_NAN_ACT = 2, ERR_NAN_PER = 4, ERR_ABORT = 8 };
+// an update that sees any of these takes none of its steps
+constexpr int kErrSkipAll = ERR_NAN_TGT | ERR_NAN_PER | ERR_ABORT;
+
 // Scalars shared by kernels (device resident, one struct per context).
 struct DevScalars {
   float alpha;          // alpha used by this update (0.2 until the first update)
@@ -160,7 +181,7 @@ struct DevScalars {
   int64_t head;         // ring slot of deque position 0
   int64_t per_frame;
   int32_t alpha_is_tensor;
-  int32_t err;
+  int32_t err;          // ErrBits (0: no non-finite input seen)
   int64_t loss_ring_pos;
 };
 
@@ -244,7 +265,10 @@ struct AdamFuse {
   int64_t log_alpha_idx; int auto_entropy;   // scalar alpha Adam (step idx 3), -1: none
   const float* log_alpha_grad;               // written by k_critic_rows
   float* loss_ring; int ring;
-  float* loss_host;      // or null: the losses also stored to host-mapped memory (sync step)
+  float* loss_host;      // or null: the losses also stored to host-mapped memory (sync step);
+                         //   block 0 stores sc->err's bits into word 3
+  int err_skip;          // ErrBits that void this level's stores (critic: kErrSkipAll,
+  int err_nopolyak;      //   actor: every bit); ... that void only its Polyak stores (ACT)
   unsigned short* Ph;    // bf16 mode: bf16 shadows of the parameter / target arenas, kept
   unsigned short* Th;    //   in step with every parameter store (null otherwise)
 };
@@ -270,6 +294,8 @@ struct MtSampleArgs {
   int32_t* idx_out;       // [k]
   int64_t* idx64_out;     // [k] or null
   int32_t* pool;          // scratch [max setsize] for the pool branch
+  int skip_on_err;        // 1 (update graphs): leave the MT state untouched when sc->err is
+                          // set — the reference never reaches a later update's sample
   tl_word* tl;
 };
 // Work of the NEXT update of a multi-update graph that rides along, as extra
@@ -348,6 +374,11 @@ struct HeadSampleArgs {
   float* logp_part;      // [grid][2] or null: per workgroup, sum of logp over its rows
   int split_row;         //   < split_row (slot 0) and >= split_row (slot 1)
   float* act_host;       // or null: the actions also stored [row][A] to host-mapped memory
+  // Normal(mean, std) validation (networks_model1.py:87): a NaN mean or log_std of row m
+  // sets bit (m < split_row ? nan_bit_lo : nan_bit_hi) of *nan_flag — by atomicOr on the
+  // device scalars (update), by a plain store on host-mapped memory (select_action)
+  int* nan_flag;
+  int nan_bit_lo, nan_bit_hi, nan_plain;
   tl_word* tl;
 };
 
@@ -389,6 +420,8 @@ void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream
 void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, hipStream_t s);
 // whether launch_gemm runs this level on k_axk16 (no dL/da partials there)
 bool gemm_level_on_axk16(const GemmBatch& b);
+// whether launch_gemm runs this axk-1 level on the tiles that compute dL/da partials
+bool gemm_level_pa_capable(const GemmBatch& b);
 
 
 constexpr int kMaxAdamSegs = 8;
@@ -410,6 +443,7 @@ struct AdamArgs {
   int ring;
   unsigned short* ph;      // bf16 shadows of p / tgt (bf16 mode) or null
   unsigned short* tgth;
+  int err_skip, err_nopolyak;   // as AdamFuse
   tl_word* tl;
 };
 void launch_adam(const AdamArgs& a, hipStream_t s);
@@ -461,6 +495,12 @@ struct PerArgs {
   int32_t* idx32;         // [k] ring slots (feeds the update's gather)
   int64_t* idx_out;       // [k]
   float* w_out;           // [k]
+  // np.random.choice's "probabilities contain NaN" (replay_buffer.py:64): the normaliser is
+  // NaN / inf / 0 -> ERR_NAN_PER into *err, and the numpy stream is left as it was (the
+  // draw's words are restored from mt_backup); the frame still advances (:54-55 run first)
+  int* err;
+  uint32_t* mt_backup;    // [625]
+  int skip_on_err;        // 1 (update graphs): no draw, no frame step when *err is set
   tl_word* tl;            // kernels F1, F2, F2b, F3, F4 (or the unfused sequence) in order
 };
 void launch_per_sample(const PerArgs& a, hipStream_t s);

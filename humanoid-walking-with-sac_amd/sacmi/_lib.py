@@ -69,6 +69,7 @@ _PROTOS = {
     "sacmi_get_scalar": [c_vp, ctypes.c_int, c_f64p],
     "sacmi_push": [c_vp, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p, ctypes.c_int64],
     "sacmi_len": [c_vp, c_i64p],
+    "sacmi_replay_clear": [c_vp],
     "sacmi_get_rows": [c_vp, c_i64p, ctypes.c_int64, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p],
     "sacmi_get_slots": [c_vp, c_i64p, ctypes.c_int64, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p],
     "sacmi_rng_set_mt": [c_vp, ctypes.c_int, c_u32p, ctypes.c_int32],

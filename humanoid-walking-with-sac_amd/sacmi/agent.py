@@ -231,15 +231,17 @@ class SAC:
         if len(self.replay_buffer) < batch_size:
             raise ValueError("Sample larger than population or is negative")
         rb = self.replay_buffer
+        self._stale = True     # (also when it raises: the critic step may have been taken)
         if rb.sync_python_random:
             st = random.getstate()
             self._ctx.set_mt(0, np.array(st[1][:624], np.uint32), st[1][624])
-            out = self._ctx.step(batch_size)
-            key, pos = self._ctx.get_mt(0)
-            random.setstate((3, tuple(int(x) for x in key) + (pos,), st[2]))
+            try:
+                out = self._ctx.step(batch_size)
+            finally:           # the update's random.sample ran even if the update raised
+                key, pos = self._ctx.get_mt(0)
+                random.setstate((3, tuple(int(x) for x in key) + (pos,), st[2]))
         else:
             out = self._ctx.step(batch_size)
-        self._stale = True
         return {"q1_loss": float(out[0]), "q2_loss": float(out[1]), "policy_loss": float(out[2])}
 
     def update_parameters_async(self, batch_size=256):
@@ -259,11 +261,13 @@ class SAC:
         if rb.sync_python_random:
             st = random.getstate()
             self._ctx.set_mt(0, np.array(st[1][:624], np.uint32), st[1][624])
+        self._stale = True
         self._ctx.step_many_async(batch_size, n_updates)
         if rb.sync_python_random:
             key, pos = self._ctx.get_mt(0)
             random.setstate((3, tuple(int(x) for x in key) + (pos,), st[2]))
-        self._stale = True
+        # raises ValueError at the first update whose policy sample was NaN (the loop of
+        # trainer.py:203-204 stops there; the later updates of the launch took no step)
         out = self._ctx.fetch_losses(1)[0]
         return {"q1_loss": float(out[0]), "q2_loss": float(out[1]), "policy_loss": float(out[2])}
 
@@ -326,6 +330,12 @@ class SAC:
 
     def load_checkpoint(self, path, load_replay_buffer=True):
         ck = _load_checkpoint_file(path)
+        # the replay rows are checked before anything is overwritten (a checkpoint whose rows
+        # do not fit this agent leaves it untouched), and replace the buffer at the end, as
+        # the reference's assignment does (sac_imp.py:229-230)
+        rows = None
+        if load_replay_buffer and "replay_buffer" in ck:
+            rows = self._checkpoint_rows(ck["replay_buffer"])
         self._load_nets(ck)
         for name in ("policy", "q1", "q2"):
             key = f"{name}_optimizer_state_dict"
@@ -336,16 +346,29 @@ class SAC:
             self.log_alpha = ck["log_alpha"]
         if "alpha_optimizer_state_dict" in ck and self.automatic_entropy_tuning:
             self.alpha_optimizer.load_state_dict(ck["alpha_optimizer_state_dict"])
-        if load_replay_buffer and "replay_buffer" in ck:
-            # the reference REPLACES its buffer (sac_imp.py:229-230): restore only into an
-            # empty replay, after any transitions still staged on the host
-            rb = ck["replay_buffer"]
-            self.replay_buffer._flush()
-            if len(self.replay_buffer):
-                raise ValueError("can only restore a buffer into an empty replay")
-            if isinstance(rb, dict):
-                self._ctx.push(rb["state"].numpy(), rb["action"].numpy(), rb["reward"].numpy(),
-                               rb["next_state"].numpy(), rb["done"].numpy())
-            else:
-                self.replay_buffer.buffer = rb
+        if rows is not None:
+            self.replay_buffer._replace_arrays(*rows)
         return ck.get("episode", 0), ck.get("total_steps", 0)
+
+    def _checkpoint_rows(self, rb):
+        """The checkpoint's replay as stacked float32 arrays (s, a, r, s2, d), shape-checked
+        against this agent: the drop-in's dict of tensors, or the reference's sequence of
+        (state, action, reward, next_state, done) tuples."""
+        S, A = self._cfg.state_dim, self._cfg.action_dim
+        if isinstance(rb, dict):
+            s, a, r, s2, d = (np.asarray(rb[k].numpy() if torch.is_tensor(rb[k]) else rb[k])
+                              for k in ("state", "action", "reward", "next_state", "done"))
+        else:
+            rb = list(rb)
+            if not rb:
+                z = np.zeros((0, S), np.float32)
+                return z, np.zeros((0, A), np.float32), np.zeros(0, np.float32), z, np.zeros(0, bool)
+            s, a, r, s2, d = (np.asarray(x) for x in zip(*rb))
+        n = len(r)
+        try:
+            out = (np.asarray(s, np.float32).reshape(n, S), np.asarray(a, np.float32).reshape(n, A),
+                   np.asarray(r, np.float32).reshape(n), np.asarray(s2, np.float32).reshape(n, S),
+                   np.asarray(d).astype(bool).reshape(n))
+        except ValueError as e:
+            raise ValueError(f"checkpoint replay rows do not fit state_dim={S}, action_dim={A}: {e}")
+        return out

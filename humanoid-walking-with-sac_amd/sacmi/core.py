@@ -168,6 +168,10 @@ class Context:
         L.call("sacmi_len", self._h, ctypes.byref(n))
         return n.value
 
+    def replay_clear(self) -> None:
+        """Empty the ring (the checkpoint restore's buffer replacement, sac_imp.py:229-230)."""
+        L.call("sacmi_replay_clear", self._h)
+
     def get_rows(self, idx):
         idx = np.ascontiguousarray(idx, np.int64)
         n = idx.size

@@ -91,15 +91,26 @@ class _Staged:
 
     @buffer.setter
     def buffer(self, rows):
+        """``buffer = rows`` REPLACES the contents, as the reference's attribute assignment
+        does (sac_imp.py:229-230): the ring is emptied, then the rows are pushed in order
+        (a deque(maxlen) keeps the last `capacity` of them)."""
         rows = list(rows)
-        if not rows:
-            return
-        self._ensure_ctx(rows[0][0], rows[0][1])
-        if len(self._ctx):
-            raise ValueError("can only restore a buffer into an empty replay")
+        self._rows.clear()
+        if self._ctx is None:
+            if not rows:
+                return
+            self._ensure_ctx(rows[0][0], rows[0][1])
+        self._ctx.replay_clear()
         for row in rows:
             self.push(*row)
         self._flush()
+
+    def _replace_arrays(self, s, a, r, s2, d):
+        """Replace the contents with the rows of stacked arrays (the drop-in's checkpoint form)."""
+        self._rows.clear()
+        self._ensure_ctx(s[0], a[0])
+        self._ctx.replay_clear()
+        self._ctx.push(s, a, r, s2, d)
 
 
 class ReplayBuffer(_Staged):

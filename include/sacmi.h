@@ -141,6 +141,11 @@ int sacmi_get_scalar(sacmi_ctx* ctx, int which, double* value);
 int sacmi_push(sacmi_ctx* ctx, const float* s, const float* a, const float* r,
                const float* s2, const uint8_t* d, int64_t n);
 int sacmi_len(sacmi_ctx* ctx, int64_t* n);
+/* Empty the replay: the assignment `replay_buffer.buffer = rows` of checkpoint loading
+ * (sac_imp.py:229-230) replaces the contents, so the rows pushed next start a fresh deque.
+ * PER priorities are left as they are (the reference's list assignment does not touch its
+ * priority array, replay_buffer.py:28-30). */
+int sacmi_replay_clear(sacmi_ctx* ctx);
 /* Copy rows at deque positions idx[0..n) out (materialises ReplayBuffer.buffer). */
 int sacmi_get_rows(sacmi_ctx* ctx, const int64_t* idx, int64_t n, float* s, float* a,
                    float* r, float* s2, uint8_t* d);
@@ -174,6 +179,16 @@ int sacmi_sample_indices(sacmi_ctx* ctx, int32_t batch, int64_t* idx_out);
  * losses_out (may be NULL): {q1_loss, q2_loss, policy_loss} — synchronises. */
 int sacmi_step(sacmi_ctx* ctx, int32_t batch, const int64_t* idx, const float* eps1,
                const float* eps2, float* losses_out);
+/* Non-finite inputs (SACMI_ENAN -> ValueError), where the reference raises:
+ *   - a NaN policy mean / log_std fed to Normal(mean, std) (networks_model1.py:87) in
+ *     policy.sample(next_state) (sac_imp.py:89: the update takes no step) or in
+ *     policy.sample(state) (:116: the critic step is taken, the actor / alpha / Polyak
+ *     steps are not); select_action(evaluate=False) likewise (sacmi_act);
+ *   - NaN PER probabilities (np.random.choice, replay_buffer.py:64: the frame advances, the
+ *     numpy stream does not).
+ * The device records it and every later update of the stream takes no step (a
+ * multi-update launch stops where the reference's loop raised).  sacmi_step (with
+ * losses_out), sacmi_fetch_losses, sacmi_per_sample and sacmi_act report it and forget it. */
 /* Same work, enqueued only (no host sync, no host writes); losses stay on device
  * in a ring of `ring` slots, fetched by sacmi_fetch_losses. */
 int sacmi_step_async(sacmi_ctx* ctx, int32_t batch);

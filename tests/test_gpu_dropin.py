@@ -222,7 +222,8 @@ def test_checkpoint_restores_reference_list_buffer(tmp_path):
     """The replay restore branch of load_checkpoint (sac_imp.py:229-230): a buffer saved as
     the reference's list of (state, action, reward, next_state, done) tuples of numpy
     values (PrioritizedReplayBuffer.buffer, replay_buffer.py:28) is restored in order,
-    bit for bit; restoring into a non-empty replay raises (the reference replaces)."""
+    bit for bit, and REPLACES a non-empty replay as the reference's assignment does; rows
+    that do not fit the agent raise before anything of it is overwritten."""
     rng = np.random.default_rng(8)
     rows = [(rng.standard_normal(S), rng.uniform(-0.4, 0.4, A).astype(np.float32),
              float(rng.standard_normal()), rng.standard_normal(S), bool(rng.random() < 0.2))
@@ -242,9 +243,31 @@ def test_checkpoint_restores_reference_list_buffer(tmp_path):
         assert r[i] == np.float32(ri) and np.array_equal(s2[i], s2i.astype(np.float32))
         assert bool(d[i]) == di
     full = _agent()
-    _fill(full, 10)
-    with pytest.raises(ValueError, match="empty replay"):
-        full.load_checkpoint(p)
+    _fill(full, 300)                     # 300 rows (some still staged on the host) ...
+    full.load_checkpoint(p)              # ... replaced by the checkpoint's 150
+    assert len(full.replay_buffer) == 150
+    s3, a3, r3, s23, d3 = full.replay_buffer._rows_at(np.arange(150))
+    assert np.array_equal(s3, s) and np.array_equal(a3, a) and np.array_equal(r3, r)
+    assert np.array_equal(s23, s2) and np.array_equal(d3, d)
+    _fill(full, 5, seed=9)               # pushes continue after the restored rows
+    assert len(full.replay_buffer) == 155
+    # a checkpoint whose rows do not fit: nothing of the agent is overwritten
+    bad = dict(ck)
+    bad["replay_buffer"] = [(np.zeros(S + 1), np.zeros(A, np.float32), 0.0, np.zeros(S + 1), False)]
+    torch.save(bad, p)
+    other = _agent()
+    _fill(other, 100, seed=4)
+    before = other._ctx.get_net("policy")
+    with torch.no_grad():
+        for prm in src.policy.parameters():
+            prm.add_(1.0)
+    bad["policy_state_dict"] = src.policy.state_dict()
+    torch.save(bad, p)
+    with pytest.raises(ValueError, match="do not fit"):
+        other.load_checkpoint(p)
+    after = other._ctx.get_net("policy")
+    assert all(np.array_equal(before[k], after[k]) for k in before)
+    assert len(other.replay_buffer) == 100
 
 
 def test_select_action_stochastic_vs_oracle():

@@ -908,13 +908,14 @@ def test_dp_config4_per_shard_world1_matches_fused():
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("B", [256, 1024])
-def test_dlda_fold_matches_unfolded(B):
+@pytest.mark.parametrize("B,H", [(256, 512), (1024, 512), (1024, 768)])
+def test_dlda_fold_matches_unfolded(B, H):
     """dL/da folded into the dha1 level's epilogue (per-32-column partials, summed by the
     sample-backward tail) vs the standalone dL/da GEMM (SACMI_NO_DLDA_FOLD=1): the same
     update up to fp32 summation order — every gradient within 1e-5 normwise, losses equal
-    (they are computed before the actor backward)."""
-    cfg = SacConfig(376, 17, 512)
+    (they are computed before the actor backward).  Batch 1024 with hidden 768 has more
+    32x64 tiles than the one-wave-group form takes: the fold steps aside (no error)."""
+    cfg = SacConfig(376, 17, H)
     params = init_params(cfg, 141, bias_scale=0.02)
     rows = synthetic_rows(cfg, max(3000, B + 500), 142, state_scale=0.1)
     rng = np.random.default_rng(143)
