@@ -221,6 +221,14 @@ __device__ __forceinline__ s4 to_bf16x4(const float (&v)[4]) {
 template <int MT, int NT, bool BF16 = false>
 __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[MT][4],
                                            const float (&b)[NT][4]) {
+#ifdef SACMI_EXP_NOMFMA
+  // timing experiment only: the operands are consumed by one add, no MFMA
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j][0] += a[i][0] + b[j][0];
+  return;
+#endif
   if constexpr (BF16) {
     s4 ab[MT], bb[NT];
 #pragma unroll
@@ -564,6 +572,37 @@ __device__ __forceinline__ void adam_block0(const AdamFuse& af, int err, float o
   }
 }
 
+// Polyak workgroup w of nw (RideAlong::pk): grid-stride float4 groups of the critic arena,
+// every load of a thread's groups issued before its stores; the same three separately
+// rounded fp32 ops as the Adam epilogue's form (bit-exact with the reference)
+__device__ __forceinline__ void polyak_ride(const PolyakArgs& a, int w, int nw) {
+  if (a.sc->err) return;   // the reference raised before sac_imp.py:138 (ErrBits)
+  const float omtau = 1.f - a.tau;
+  const rsrc_t rT = make_rsrc(a.T, 0x7fffffffu), rP = make_rsrc(a.P, 0x7fffffffu);
+  constexpr int kPer = 2;     // groups per thread per pass
+  const int64_t stride = (int64_t)nw * blockDim.x * kPer;
+  for (int64_t g0 = (int64_t)w * blockDim.x * kPer + threadIdx.x; g0 < a.n4; g0 += stride) {
+    float4 t[kPer], p[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int64_t g = g0 + (int64_t)k * blockDim.x;
+      const uint32_t o = g < a.n4 ? (uint32_t)g * 16u : 0xfffffff0u;
+      t[k] = buf_ld4(rT, o);
+      p[k] = buf_ld4(rP, o);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int64_t g = g0 + (int64_t)k * blockDim.x;
+      if (g >= a.n4) break;
+      const float x = polyak(t[k].x, p[k].x, omtau, a.tau), y = polyak(t[k].y, p[k].y, omtau, a.tau),
+                  z = polyak(t[k].z, p[k].z, omtau, a.tau), u = polyak(t[k].w, p[k].w, omtau, a.tau);
+      buf_st4<kStAux>(rT, (uint32_t)g * 16u, f4{x, y, z, u});
+      if (a.Th) st_wt8(a.Th, (uint32_t)g * 8u, (uint32_t)bf16_bits(x) | ((uint32_t)bf16_bits(y) << 16),
+                       (uint32_t)bf16_bits(z) | ((uint32_t)bf16_bits(u) << 16));
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // grouped GEMM: one launch runs every independent GEMM of one dependency level.
 // One workgroup (16 waves, K split 16 ways) per output tile, one workgroup per CU.
@@ -777,7 +816,22 @@ constexpr int gemm_min_waves() { return 4; }   // 16 waves per CU: one 1024- or 
 // bf16 MFMA operands (GemmBatch::bf16), everything around them fp32
 template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false>
 __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
-  const TlMark tl_mark(batch.tl, TL_GEMM);
+  // The scalars that locate this workgroup's work come in ONE kernarg round trip: left to
+  // the compiler, each load sat behind a branch on the previous one (timeline pointer, tile
+  // count, one desc's tile_begin per loop trip, then the desc's fields as they were used),
+  // ~1-1.5 us of dependent scalar round trips before the first operand load of every level
+  // (phase stamps, tools/phase_dump.py).  The asm pins force each value into an SGPR
+  // there, so every load is issued before the one wait.
+  tl_word* const tl = batch.tl;
+  const int n_tiles = batch.total_tiles, n_desc = batch.count;
+  int tbeg[kMaxGemms];
+#pragma unroll
+  for (int q = 0; q < kMaxGemms; ++q) tbeg[q] = batch.d[q].tile_begin;
+  asm volatile("" :: "s"(tl), "s"(n_tiles), "s"(n_desc));
+#pragma unroll
+  for (int q = 0; q < kMaxGemms; ++q) asm volatile("" :: "s"(tbeg[q]));
+  const TlMark tl_mark(tl, TL_GEMM);
+  SACMI_PHASE(tl, 0);
   constexpr int TMW = TM * MG;
   __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
   __shared__ float rsum[MG * KSPLIT * TM];
@@ -789,9 +843,25 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   constexpr bool PA = AXK == 1 && MG == 1;
   __shared__ float s_pa[PA ? TMW * (TN + 1) + TN * 32 : 1];
   const int bid = blockIdx.x;
-  if (bid >= batch.total_tiles) {   // ride-along workgroups (next update's replay work)
+#ifdef SACMI_EXP_EMPTY
+  if (bid < batch.total_tiles) return;   // timing experiment only: the launch, nothing else
+#endif
+#ifdef SACMI_EXP_DESC
+  {   // timing experiment only: the launch + this workgroup's descriptor, then out
+    int pq = 0;
+    for (int q = 1; q < batch.count; ++q)
+      if (bid >= batch.d[q].tile_begin) pq = q;
+    if (bid < batch.total_tiles && batch.d[pq].M == -7) red[threadIdx.x] = 1.f;
+    if (bid < batch.total_tiles) return;
+  }
+#endif
+  if (bid >= n_tiles) {   // ride-along workgroups (next update's replay work, Polyak)
     if constexpr (MG * KSPLIT == 16) {   // the host attaches rides to 1024-thread configs
-      const int rb = bid - batch.total_tiles;
+      const int rb = bid - n_tiles;
+      if (rb >= (batch.ride.kind ? batch.ride.nblocks : 0)) {
+        polyak_ride(batch.ride.pk, rb - (batch.ride.kind ? batch.ride.nblocks : 0), batch.ride.pk_blocks);
+        return;
+      }
       if (batch.ride.kind == 1) {
         mt_sample_body(batch.ride.mt, batch.ride.tbl_log2, reinterpret_cast<uint32_t*>(red));
       } else {
@@ -803,10 +873,15 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
     return;
   }
   int p = 0;
-  for (int q = 1; q < batch.count; ++q)
-    if (bid >= batch.d[q].tile_begin) p = q;
+#pragma unroll
+  for (int q = 1; q < kMaxGemms; ++q)
+    if (q < n_desc && bid >= tbeg[q]) p = q;
+  // the fields the K loop needs, in the second (and last) round trip before the operand
+  // loads; the epilogue's fields load lazily, under the MFMAs
   const GemmDesc d = batch.d[p];
-  const int t = bid - d.tile_begin;
+  asm volatile("" :: "s"(d.A), "s"(d.B), "s"(d.M), "s"(d.N), "s"(d.K), "s"(d.lda), "s"(d.ldb),
+               "s"(d.a_kc), "s"(d.b_kc), "s"(d.tiles_n), "s"(d.tiles_m), "s"(d.xcd_gr));
+  const int t = bid - tbeg[p];
   if (t >= d.tiles_m * d.tiles_n) return;   // padding to a multiple of 8 blocks
   int tr, tc;
   if (d.xcd_gr) {
@@ -820,11 +895,10 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   }
   const int m0 = tr * TMW, n0 = tc * TN;
   const bool rowsum = d.rs_col >= 0 && n0 == 0;
-  if (ADAM && threadIdx.x == 0) {
-    s_k = fuse_scalars(batch.adam, d.adam_step, batch.adam.step_offset);
-    s_err = batch.adam.sc->err;     // (loaded with the step scalars: no extra round trip)
-  }
   const AdamFuse& af = batch.adam;
+  // Adam bias corrections and the error bits: thread 0 reads them in pre(), behind its
+  // wave's operand loads (at the kernel's start they put a device-memory round trip in
+  // front of wave 0's operand loads), into LDS for the epilogue
   // Element slots: EPT tile outputs per thread (e = tid + s*NTH) plus one slot for the
   // rowsum (bias-gradient) column.  Their epilogue operands (bias, ReLU mask, Adam
   // state) are loaded by pre() while the MFMAs run.
@@ -848,8 +922,10 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   };
   const bool wt = SACMI_WT && batch.st_wt;   // output store policy of this level
   const bool pol = d.epi == EPI_ADAM_POLYAK;
-  // byte span of this desc's output (tile rows, plus the rowsum column)
-  const uint32_t span = (uint32_t)(((size_t)(d.M - 1) * d.ldc + (d.rs_col >= d.N ? d.rs_col + 1 : d.N)) * 4);
+  // byte span of this desc's output (tile rows, plus the rowsum column; the fused-Adam
+  // 4-column groups reach the row's padding up to a multiple of 4: ldc is one)
+  const int ncov = ADAM ? (d.N + 3) & ~3 : d.N;
+  const uint32_t span = (uint32_t)(((size_t)(d.M - 1) * d.ldc + (d.rs_col >= ncov ? d.rs_col + 1 : ncov)) * 4);
   const size_t abase = ADAM ? (size_t)(d.C - af.P) : 0;
   const rsrc_t rC = make_rsrc(d.C, span);
   // (unused descriptors get a zero-length range: any access through them is dropped)
@@ -862,7 +938,22 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
                   : make_rsrc(d.C, 0);
   // Adam: param, exp_avg, exp_avg_sq, target; otherwise x0 = the bias or the ReLU-mask
   // source (a level has one or the other: validate())
-  float x0[NS], x1[ADAM ? NS : 1], x2[ADAM ? NS : 1], x3[ADAM ? NS : 1];
+  // Fused-Adam levels work on 4-column groups instead of single elements: their optimizer
+  // state moves as 16-byte loads and write-through stores — a write-through dword store
+  // is one fabric write per lane, ~6x the 16-byte form per byte (MI355X_MICROARCH.md
+  // "stores of each flavour"), and these levels store 12-16 bytes of state per parameter.
+  // x0..x3 then hold only the rowsum (bias-gradient) slot.
+  constexpr int NG = TMW * TN / 4;                         // 4-column groups of the tile
+  constexpr int EPG = ADAM ? (NG + NTH - 1) / NTH : 1;     // groups per thread
+  auto group = [&](int s, int& row, int& c4, int& n) -> bool {
+    const int g = tid + s * NTH;
+    row = g / (TN / 4);
+    c4 = (g % (TN / 4)) * 4;
+    n = n0 + c4;
+    return g < NG && m0 + row < d.M && n < d.N;
+  };
+  float4 q0[EPG], q1[EPG], q2[EPG], q3[EPG];
+  float x0[ADAM ? 1 : NS], x1[1], x2[1], x3[1];
   RowsRegs rows_x{};
   // the epilogue operands (Adam state, or the bias / mask) go out under the MFMAs; the
   // fc3 dot weights of the tile go to LDS; an axk-1 level runs its row prologue
@@ -876,6 +967,12 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   float paw_x[PW];
   const bool has_pa = PA && d.pa_out != nullptr;
   auto pre = [&]() {
+    if constexpr (ADAM) {
+      if (threadIdx.x == 0) {
+        s_k = fuse_scalars(af, d.adam_step, af.step_offset);
+        s_err = af.sc->err;
+      }
+    }
     // axk 1: the row prologue's loads.  Issued here, behind the operand burst, and
     // consumed after the MFMAs: anything in flight at the k-loop header is waited for by
     // the back-edge's conservative vmcnt on the first iteration.
@@ -899,15 +996,31 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
     // unconditional: an empty slot reads past its descriptor's range (returns 0, no
     // access), and the level's unused operands have zero-length descriptors
     constexpr uint32_t kOob = 0xfffffff0u;
+    if constexpr (ADAM) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
+      for (int s = 0; s < EPG; ++s) {
+        int row, c4, n;
+        const bool ok = group(s, row, c4, n);
+        const uint32_t o = ok ? (uint32_t)((m0 + row) * d.ldc + n) * 4u : kOob;
+#ifdef SACMI_EXP_NOADAMIO
+        // timing experiment only: no optimizer-state traffic
+        q0[s] = q1[s] = q2[s] = q3[s] = float4{0.f, 0.f, 0.f, (float)o};
+#else
+        q0[s] = buf_ld4(rC, o); q1[s] = buf_ld4(rM, o); q2[s] = buf_ld4(rV, o);
+        q3[s] = buf_ld4(rT, o);
+#endif
+      }
+      int row, col, n;
+      const bool ok = slot(EPT, row, col, n);      // the rowsum slot
+      const uint32_t o = ok ? (uint32_t)((m0 + row) * d.ldc + n) * 4u : kOob;
+      x0[0] = buf_ld(rC, o); x1[0] = buf_ld(rM, o); x2[0] = buf_ld(rV, o);
+      x3[0] = buf_ld(rT, o);
+    }
+#pragma unroll
+    for (int s = 0; s < (ADAM ? 0 : NS); ++s) {
       int row, col, n;
       const bool ok = slot(s, row, col, n);
-      if constexpr (ADAM) {
-        const uint32_t o = ok ? (uint32_t)((m0 + row) * d.ldc + n) * 4u : kOob;
-        x0[s] = buf_ld(rC, o); x1[s] = buf_ld(rM, o); x2[s] = buf_ld(rV, o);
-        x3[s] = buf_ld(rT, o);
-      } else {
+      {
         const uint32_t o = !ok ? kOob
                          : d.bias ? (uint32_t)(n * d.bias_ld) * 4u
                                   : (uint32_t)((m0 + row) * d.ldaux + n) * 4u;
@@ -919,7 +1032,9 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   // K loop (register budget: the Adam and transform variants already sit near 128 VGPRs)
   constexpr int PIPE = (SACMI_PIPE && G == 1 && !ADAM && AXK == 0) ? 1
                      : (SACMI_PIPE_DW && G == 1 && ADAM && MG == 2) ? 2 : 0;
+  SACMI_PHASE(batch.tl, 1);
   gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
+  SACMI_PHASE(batch.tl, 2);
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
   if constexpr (PA) {
     if (has_pa) {
@@ -938,14 +1053,55 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   }
   __syncthreads();
   if (threadIdx.x < 64) SACMI_STAMP(32);
+  SACMI_PHASE(batch.tl, 3);
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
   // a non-finite policy sample / PER draw of this update (ErrBits): the reference raised
   // before this step (no stores), or after the critic step but before Polyak
   const int err = ADAM ? s_err : 0;
+  const AdamScalars k_ad = s_k;
   const bool void_st = ADAM && (err & af.err_skip) != 0;
   const bool pol_st = pol && (err & af.err_nopolyak) == 0;
+  if constexpr (ADAM) {
+    // 4-column groups: the gradient of a column past N (a row pad) is taken as 0, so the
+    // Adam / Polyak arithmetic leaves the pad (0) exactly 0 and the 16-byte stores rewrite it
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
+    for (int s = 0; s < EPG; ++s) {
+      int row, c4, n;
+      if (!group(s, row, c4, n) || void_st) continue;
+      float g[4], p[4] = {q0[s].x, q0[s].y, q0[s].z, q0[s].w}, m[4] = {q1[s].x, q1[s].y, q1[s].z, q1[s].w},
+            v[4] = {q2[s].x, q2[s].y, q2[s].z, q2[s].w}, t[4] = {q3[s].x, q3[s].y, q3[s].z, q3[s].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        g[j] = n + j < d.N ? reduce_partials<TM, TN, KSPLIT, MG>(red, row, c4 + j) : 0.f;
+        adam_elem(p[j], m[j], v[j], g[j], omb1, af.beta2, omb2, af.eps, k_ad);
+        t[j] = polyak(t[j], p[j], omtau, af.tau);
+      }
+      const uint32_t o = (uint32_t)((m0 + row) * d.ldc + n) * 4u;
+      auto st4 = [&](rsrc_t r, const float (&x)[4]) {
+        if (wt) buf_st4<kStAux>(r, o, f4{x[0], x[1], x[2], x[3]});
+        else buf_st4<0>(r, o, f4{x[0], x[1], x[2], x[3]});
+      };
+      auto st_bf4 = [&](unsigned short* h, const float (&x)[4]) {   // 4 bf16 shadows, 8 bytes
+        const uint32_t lo = (uint32_t)bf16_bits(x[0]) | ((uint32_t)bf16_bits(x[1]) << 16);
+        const uint32_t hi = (uint32_t)bf16_bits(x[2]) | ((uint32_t)bf16_bits(x[3]) << 16);
+        if (wt) st_wt8(h, 0u, lo, hi);
+        else *reinterpret_cast<uint2*>(h) = make_uint2(lo, hi);
+      };
+#ifdef SACMI_EXP_NOADAMIO
+      if (p[0] + m[1] + v[2] + t[3] == 12345.f) st4(rC, p);   // (keeps the math alive)
+      continue;
+#endif
+      if (af.G) st4(rG, g);
+      st4(rC, p); st4(rM, m); st4(rV, v);
+      if (af.Ph) st_bf4(af.Ph + abase + (o >> 2), p);
+      if (pol_st) {
+        st4(rT, t);
+        if (af.Th) st_bf4(af.Th + abase - af.t_base + (o >> 2), t);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = ADAM ? EPT : 0; s < NS; ++s) {
     int row, col, n;
     const bool ok = slot(s, row, col, n) && !void_st;
     float v = 0.f;
@@ -962,13 +1118,13 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
       if constexpr (AXK == 1) {
         if (d.axk == 1) v *= s_coef[d.ax_slot][row];   // dh = coef[b] * (u W2)
       }
-      if constexpr (ADAM) {
-        adam_elem(x0[s], x1[s], x2[s], v, omb1, af.beta2, omb2, af.eps, s_k);
+      if constexpr (ADAM) {   // (the rowsum slot)
+        adam_elem(x0[0], x1[0], x2[0], v, omb1, af.beta2, omb2, af.eps, k_ad);
         if (af.G) buf_st_pol(rG, o, v, wt);
-        buf_st_pol(rC, o, x0[s], wt); buf_st_pol(rM, o, x1[s], wt); buf_st_pol(rV, o, x2[s], wt);
-        if (af.Ph) st_pol(af.Ph + abase + (o >> 2), bf16_bits(x0[s]), wt);
+        buf_st_pol(rC, o, x0[0], wt); buf_st_pol(rM, o, x1[0], wt); buf_st_pol(rV, o, x2[0], wt);
+        if (af.Ph) st_pol(af.Ph + abase + (o >> 2), bf16_bits(x0[0]), wt);
         if (pol_st) {
-          const float tn = polyak(x3[s], x0[s], omtau, af.tau);
+          const float tn = polyak(x3[0], x0[0], omtau, af.tau);
           buf_st_pol(rT, o, tn, wt);
           if (af.Th) st_pol(af.Th + abase - af.t_base + (o >> 2), bf16_bits(tn), wt);
         }
@@ -976,6 +1132,9 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
         if (d.bias) v += x0[s];
         if (d.epi == EPI_RELU) v = v <= 0.f ? 0.f : v;   // F.relu: NaN stays NaN
         else if (d.epi == EPI_MASK) v = x0[s] > 0.f ? v : 0.f;
+#ifdef SACMI_EXP_NOSTORE
+        if (v == 12345.f)   // timing experiment only: no output stores
+#endif
         buf_st_pol(rC, o, v, wt);
       }
     }
@@ -995,6 +1154,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
     }
   }
   if (threadIdx.x < 64) SACMI_STAMP(33);
+  SACMI_PHASE(batch.tl, 4);
   if constexpr (AXK == 1) {
     if (d.axk == 1) rows_loss<TMW>(batch.rows, m0, p == 0 && n0 == 0, s_l);
   }
@@ -1023,6 +1183,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   if (batch.has_adam && bid == 0) {
     adam_block0(af, err, omb1, omb2);
   }
+  SACMI_PHASE(batch.tl, 5);
 }
 
 // Tile order and XCD placement.  Workgroups are dealt round-robin over the 8 XCDs
@@ -2374,10 +2535,14 @@ static bool all_bh(const GemmBatch& b) {
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
+  // Polyak rides (RideAlong::pk) run on k_gemm's 1024-thread configurations only: a level
+  // that goes to a split-K / LDS-staged kernel must not carry them
+  const Error pk_err{SACMI_ESTATE, "Polyak ride on a level outside k_gemm"};
   {
     int64_t stride = 0;
     const int ns = SACMI_DW_SPLIT ? dw_split_plan(b, &stride) : 0;
     if (ns > 0) {
+      if (b.ride.pk_blocks) throw pk_err;
       const int ride = b.ride.kind ? b.ride.nblocks : 0;
       if (b.ride.kind == 1 &&
           mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > (size_t)kDw16LdsBytes)
@@ -2427,6 +2592,7 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (SACMI_AXK_LDS16) {
     const int ax = axk16_ok(b);
     if (ax >= 0) {
+      if (b.ride.pk_blocks) throw pk_err;
       for (int i = 0; i < b.count; ++i)   // k_axk16 computes no dL/da partials
         if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a k_axk16 level"};
       const bool bh = all_bh(b);
@@ -2457,6 +2623,7 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   b = b0;
   static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
   if (fwd_big && fwd_big_ok(b)) {
+    if (b.ride.pk_blocks) throw pk_err;
     const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
     const bool bh = b.bf16 && all_bh(b);
     if (level_act16(b)) {   // act16: bf16 input rows and bf16 output (k_fwd16 only)
@@ -2498,7 +2665,7 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   b = b0;
   if (level_act16(b))
     throw Error{SACMI_ESTATE, "bf16 activation operands on a level outside the batch-4096-class kernels"};
-  const int extra = b.ride.kind ? b.ride.nblocks : 0;
+  const int extra = (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
   if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > kRideLdsBytes)
     throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_gemm's LDS"};
   int maxk = 0, n_adam = 0;
@@ -2648,7 +2815,12 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       // NaN) and scale positive — std = exp(clamp(log_std)) is NaN only for a NaN log_std
       // (torch.clamp keeps NaN; fmaxf above does not, hence the raw value).  evaluate=True
       // (deterministic) builds no Normal, so nothing is checked there (sac_imp.py:59-65).
+#if defined(SACMI_EXP_NOMFMA) || defined(SACMI_EXP_NOLOAD) || defined(SACMI_EXP_NOADAMIO) || \
+    defined(SACMI_EXP_EMPTY) || defined(SACMI_EXP_DESC) || defined(SACMI_EXP_NOSTORE)
+      if (false) {   // timing experiments compute garbage: never void their updates
+#else
       if (a.nan_flag && !a.deterministic && (__builtin_isnan(mean) || __builtin_isnan(ls_raw))) {
+#endif
         const int bit = m < a.split_row ? a.nan_bit_lo : a.nan_bit_hi;
         if (a.nan_plain) *a.nan_flag = bit;
         else atomicOr(a.nan_flag, bit);
@@ -3138,6 +3310,19 @@ void launch_fill(float* p, int64_t n, float v, hipStream_t s) {
   int64_t blocks = (n + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(256), 0, s, p, n, v);
+  HIP_LAUNCH_CHECK();
+}
+
+__global__ void k_scale(float* p, int64_t n, float f) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] *= f;
+}
+void launch_scale(float* p, int64_t n, float f, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_scale, dim3((unsigned)blocks), dim3(256), 0, s, p, n, f);
   HIP_LAUNCH_CHECK();
 }
 

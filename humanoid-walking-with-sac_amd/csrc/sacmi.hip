@@ -177,6 +177,7 @@ struct sacmi_ctx {
   // native data parallel (sacmi_allreduce_init / sacmi_step_dp)
   ncclComm_t comm = nullptr;
   int dp_world = 0;
+  bool dp_loopback = false;   // sacmi_dp_loopback_init: x world in place of the all-reduce
   std::map<std::tuple<int, int, int64_t>, hipGraphExec_t> dp_graphs;   // (batch, n, PER fill)
   uint64_t act_calls = 0;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
   // profiling (sacmi_profile_step): one event per launch site
@@ -780,6 +781,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     }
   };
 
+  // fused updates whose policy dhp1 level (L12) leaves CUs idle on k_gemm: Polyak rides there
+  static const bool pk_env = std::getenv("SACMI_NO_POLYAK_RIDE") == nullptr;
+  const bool polyak_ride = phase_mask == 7 && pk_env && !act16 &&
+                           (int64_t)((B + 31) / 32) * ((H + 31) / 32) <= 192;
   if (phase_mask & 1) {
     if (!have_batch)   // (have_batch: the previous update's rides / side stream produced them)
       enqueue_sample_gather(c, B, parity, dev_idx != 0, s);
@@ -866,9 +871,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     // L6: every critic weight gradient: into the gradient arena, or (fused) straight into
     // Adam + Polyak on the parameters.  The hidden weights are read by the dh levels
     // above, so every critic dW runs here — in both modes, so the reduction order (and
-    // the bits) are the same.
+    // the bits) are the same.  Where the policy's dhp1 level (L12) leaves CUs idle and runs
+    // on k_gemm (batch <= ~1k), the Polyak step rides there instead (polyak_ride): off the
+    // critic Adam level, the longest of the update
     auto dst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
-    const int wepi = fuse ? EPI_ADAM_POLYAK : EPI_STORE;
+    const int wepi = fuse ? (polyak_ride ? EPI_ADAM : EPI_ADAM_POLYAK) : EPI_STORE;
     Level l6;
     for (int i = 0; i < 2; ++i)
       l6.add(dwx(gd(c->dhc[0].p + i * H, 2 * H, 0, bb.xq, Kx, 0, dst(q[i][0]), Kx, H, S + A + 1, B,
@@ -1058,6 +1065,12 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.log_alpha_grad = G + c->la_idx;
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
       f.err_skip = ~0; f.err_nopolyak = 0;
+    }
+    if (polyak_ride) {   // (polyak_ride: the critic Adam above left the targets alone)
+      PolyakArgs& pk = l12.b.ride.pk;
+      pk.T = c->T.p; pk.P = P + c->q_begin; pk.Th = c->Th.p;
+      pk.n4 = (c->q_end - c->q_begin) / 4; pk.tau = (float)c->cfg.tau; pk.sc = c->sc.p;
+      l12.b.ride.pk_blocks = std::max(8, 248 - ((B + 31) / 32) * ((H + 31) / 32)) / 8 * 8;
     }
     if (ride_next && !ride_b) {
       // the next update's random.sample rides in L12 (128 tiles: idle CUs)
@@ -1321,7 +1334,10 @@ static void enqueue_dp(sacmi_ctx* c, int B, int n) {
   auto allreduce = [&](int64_t begin, int64_t end) {
     (void)mark(c, begin == c->q_begin ? "allreduce_critic_grads" : "allreduce_actor_grads");
     float* g = c->G.p + begin;
-    CHECK_RCCL(rccl().all_reduce(g, g, (size_t)(end - begin), ncclFloat32, ncclSum, c->comm, c->stream));
+    if (c->dp_loopback)   // what `world` ranks holding identical shards would all-reduce to
+      launch_scale(g, end - begin, (float)c->dp_world, c->stream);
+    else
+      CHECK_RCCL(rccl().all_reduce(g, g, (size_t)(end - begin), ncclFloat32, ncclSum, c->comm, c->stream));
   };
   int parity = 0;
   bool have = false;
@@ -1830,7 +1846,7 @@ int sacmi_allreduce_init(sacmi_ctx* c, const void* id, int32_t nbytes, int32_t r
   return guard([&] {
     REQUIRE(id && nbytes == (int32_t)sizeof(ncclUniqueId), SACMI_EVALUE, "bad RCCL unique id");
     REQUIRE(world >= 1 && rank >= 0 && rank < world, SACMI_EVALUE, "bad rank / world");
-    REQUIRE(!c->comm, SACMI_ESTATE, "communicator already initialised");
+    REQUIRE(!c->comm && !c->dp_loopback, SACMI_ESTATE, "communicator already initialised");
     CHECK_HIP(hipSetDevice(c->device));
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
@@ -1841,9 +1857,20 @@ int sacmi_allreduce_init(sacmi_ctx* c, const void* id, int32_t nbytes, int32_t r
   });
 }
 
+int sacmi_dp_loopback_init(sacmi_ctx* c, int32_t world) {
+  return guard([&] {
+    REQUIRE(c, SACMI_EVALUE, "null ctx");
+    REQUIRE(world >= 1 && world <= 1024, SACMI_EVALUE, "world must be in [1, 1024]");
+    REQUIRE(!c->comm, SACMI_ESTATE, "communicator already initialised");
+    c->dp_world = world;
+    c->dp_loopback = true;
+    destroy_graphs(c);
+  });
+}
+
 int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   return guard([&] {
-    REQUIRE(c->comm, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
+    REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -2071,6 +2098,21 @@ static void timeline_of(sacmi_ctx* c, int n_updates, F&& enqueue, int32_t max_ke
     *graph_us = ms * 1000.0;
     std::vector<tl_word> h(buf.n);
     CHECK_HIP(hipMemcpy(h.data(), buf.p, buf.n * sizeof(tl_word), hipMemcpyDeviceToHost));
+    if (const char* path = std::getenv("SACMI_DIAG_DUMP")) {
+      // raw buffer for tools/phase_dump.py: header {sites, per-site launches, words per
+      // launch, phases}, the site names (32 bytes each), then the words
+      if (FILE* f = std::fopen(path, "wb")) {
+        const int64_t hdr[4] = {c->tl_sites, kTlPerSite, kTlWords, kTlPhases};
+        std::fwrite(hdr, sizeof(hdr), 1, f);
+        for (int i = 0; i < c->tl_sites; ++i) {
+          char nm[32] = {};
+          std::strncpy(nm, c->tl_names[i].c_str(), 31);
+          std::fwrite(nm, 32, 1, f);
+        }
+        std::fwrite(h.data(), sizeof(tl_word), (size_t)c->tl_sites * kTlPerSite * kTlWords, f);
+        std::fclose(f);
+      }
+    }
     tl_word t0 = ~(tl_word)0;
     for (int sidx = 0; sidx < c->tl_sites; ++sidx)
       for (int k = 0; k < kTlPerSite; ++k) t0 = std::min(t0, h[((size_t)sidx * kTlPerSite + k) * kTlWords]);
@@ -2122,7 +2164,7 @@ int sacmi_profile_timeline_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates, in
                               double* start_us, double* end_us, double* flops_out, double* bytes_out,
                               int32_t* n_kernels, double* graph_us) {
   return guard([&] {
-    REQUIRE(c->comm, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
+    REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
     // the sequence sacmi_step_dp replays: phases + the two RCCL all-reduces per update

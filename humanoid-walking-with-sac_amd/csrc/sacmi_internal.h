@@ -119,7 +119,16 @@ enum TlKind : int {
 };
 constexpr int kTlEnd = 4;            // first of the ~end slots
 constexpr int kTlEndSlots = 256;
-constexpr int kTlWords = kTlEnd + kTlEndSlots;   // words per kernel launch
+// Diagnostic builds (-DSACMI_DIAG_PHASES, tools/build_variant.sh): the first 256 workgroups
+// of a stamping kernel also record kTlPhases clocks each (SACMI_PHASE), after the end slots;
+// sacmi_profile_timeline then dumps the raw buffer to $SACMI_DIAG_DUMP (tools/phase_dump.py)
+#ifdef SACMI_DIAG_PHASES
+constexpr int kTlPhases = 8;
+#else
+constexpr int kTlPhases = 0;
+#endif
+constexpr int kTlPhase0 = kTlEnd + kTlEndSlots;
+constexpr int kTlWords = kTlPhase0 + 256 * kTlPhases;   // words per kernel launch
 constexpr int kTlPerSite = 8;        // kernel launches one launch site may make
 struct TlMark {
   tl_word* p;
@@ -140,6 +149,16 @@ struct TlMark {
       p[kTlEnd + (blockIdx.x & (kTlEndSlots - 1))] = ~(tl_word)wall_clock64();
   }
 };
+
+#ifdef SACMI_DIAG_PHASES
+#define SACMI_PHASE(tl, k)                                                                      \
+  do {                                                                                         \
+    if ((tl) && blockIdx.x < 256 && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)          \
+      (tl)[kTlPhase0 + blockIdx.x * kTlPhases + (k)] = (tl_word)wall_clock64();                 \
+  } while (0)
+#else
+#define SACMI_PHASE(tl, k) do { } while (0)
+#endif
 
 // One bias-folded linear layer inside an arena.
 struct Linear {
@@ -307,12 +326,28 @@ constexpr size_t kRideLdsBytes = (size_t)16 * 32 * 33 * 4;
 // k_dw_part16's LDS block (two bf16 operand slab pairs + row-sum scratch), which a
 // ride-along sampler may use instead
 constexpr int kDw16LdsBytes = 77824;   // 2 x 34,816 (slabs) + 16 x 128 x 4 (row sums)
+// The Polyak target update (sac_imp.py:146-152), riding as extra workgroups in a level after
+// the critic step: t <- t * (1 - tau) + p * tau over the critic arena, float4-wide (the
+// critic region is float4-aligned), skipped after a non-finite sample (ErrBits: the
+// reference raised before its Polyak step).  Targets are read only by the next update's
+// target levels, so the update's critical path (the critic Adam level) does not carry it.
+struct PolyakArgs {
+  float* T;                 // target arena (critic part)
+  const float* P;           // the critic parameters it tracks (same layout)
+  unsigned short* Th;       // bf16 shadow of T or null
+  int64_t n4;               // float4 groups
+  float tau;
+  const DevScalars* sc;
+};
+
 struct RideAlong {
   int kind;        // 0 none, 1 random.sample, 2 gather
   int nblocks;
   int tbl_log2;    // kind 1: hash table size
   MtSampleArgs mt;
   GatherArgs ga;
+  int pk_blocks;   // > 0: Polyak workgroups after the kind's (k_gemm levels only)
+  PolyakArgs pk;
 };
 
 // Row prologue of a level whose A operand is transformed with axk 1: per batch row,
@@ -467,6 +502,8 @@ struct PushArgs {
 void launch_push_rows(const PushArgs& a, hipStream_t s);
 
 void launch_fill(float* p, int64_t n, float v, hipStream_t s);
+// p[i] *= f (the data-parallel loopback's stand-in for an all-reduce over identical ranks)
+void launch_scale(float* p, int64_t n, float f, hipStream_t s);
 void launch_set_column(float* p, int rows, int ld, int col, float v, hipStream_t s);
 void launch_increment_steps(DevScalars* sc, hipStream_t s);
 

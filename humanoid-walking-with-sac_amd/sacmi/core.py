@@ -253,6 +253,11 @@ class Context:
     def allreduce_init(self, unique_id: bytes, rank: int, world: int) -> None:
         L.call("sacmi_allreduce_init", self._h, unique_id, len(unique_id), int(rank), int(world))
 
+    def dp_loopback_init(self, world: int) -> None:
+        """Test hook: step_dp on this one context with every all-reduce replaced by an
+        in-place x world (identical shards on `world` ranks), see include/sacmi.h."""
+        L.call("sacmi_dp_loopback_init", self._h, int(world))
+
     def step_dp(self, batch: int, n_updates: int = 1) -> None:
         """n complete data-parallel updates (phases + library-issued RCCL all-reduces)."""
         L.call("sacmi_step_dp", self._h, int(batch), int(n_updates))

@@ -248,6 +248,13 @@ int sacmi_allreduce_init(sacmi_ctx* ctx, const void* id, int32_t nbytes, int32_t
  * the replay allows it.  Captured into one hipGraph per (batch, n_updates); losses land in
  * the loss ring (sacmi_fetch_losses).  Each rank samples its own replay shard. */
 int sacmi_step_dp(sacmi_ctx* ctx, int32_t batch, int32_t n_updates);
+/* Test hook for the sequence above on ONE context, no RCCL: every all-reduce becomes an
+ * in-place x world over the same gradient range — what `world` ranks holding identical
+ * shards would reduce to — while the Adam kernels apply 1/world as in a real run.  For a
+ * power-of-two world both scalings are exact, so sacmi_step_dp must equal the fused
+ * updates bit for bit: every gradient element, dL/dlog_alpha included, must sit inside an
+ * all-reduced range and 1/world must be applied exactly once. */
+int sacmi_dp_loopback_init(sacmi_ctx* ctx, int32_t world);
 
 /* ---- prioritized replay ------------------------------------------------------------ */
 /* PrioritizedReplayBuffer.sample(batch) indices + IS weights; u: NULL -> draw from

@@ -940,3 +940,49 @@ def test_dlda_fold_matches_unfolded(B, H):
     assert abs(la[2] - lb[2]) <= 1e-6 * abs(lb[2]) + 1e-9
     for k in gb:
         assert rel(ga[k], gb[k]) <= 1e-5, (k, rel(ga[k], gb[k]))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("shape", ["config2", "config5_act16"])
+def test_native_dp_loopback_world_k_bitexact(world, shape):
+    """The library's data-parallel sequence (sacmi_step_dp, sacmi.hip enqueue_dp) with
+    world > 1 arithmetic on one GPU: each all-reduce becomes an in-place x world over the
+    same range (what `world` ranks with identical shards produce) and Adam applies 1/world.
+    Both scalings are exact for a power-of-two world, so the result equals the fused
+    updates BIT FOR BIT only if every gradient element — dL/dlog_alpha included — lies
+    inside [q_begin, q_end) or [pi_begin, total) and 1/world is applied exactly once
+    (global batch = the ranks' batches concatenated)."""
+    from sacmi import _lib as L
+    if shape == "config2":
+        cfg, B, dt, nrows, n = SacConfig(376, 17, 512), 256, "fp32", 4000, 4
+    else:
+        cfg, B, dt, nrows, n = SacConfig(661, 23, 512), 4096, "bf16", 20000, 2
+    params = init_params(cfg, 95, bias_scale=0.05)
+    rows = synthetic_rows(cfg, nrows, 96, state_scale=0.5)
+    key = (np.arange(624, dtype=np.uint64) * 1812433 % (2**32)).astype(np.uint32)
+    ctxs = []
+    for _ in range(2):
+        ctx = make_ctx(cfg, max_batch=B, capacity=nrows, seed=5, compute_dtype=dt)
+        load_params(ctx, params)
+        ctx.push(*rows)
+        ctx.set_mt(0, key, 624)
+        ctxs.append(ctx)
+    ctxs[0].dp_loopback_init(world)
+    ctxs[0].step_dp(B, n)
+    fused = np.stack([ctxs[1].step(B) for _ in range(n)])
+    ctxs[0].synchronize()
+    for nm in NETS:
+        a, b = ctxs[0].get_net(nm), ctxs[1].get_net(nm)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (world, shape, nm, k)
+        if nm in ("policy", "q1", "q2"):
+            for slot in ("m", "v"):
+                a, b = ctxs[0].get_net(nm, slot), ctxs[1].get_net(nm, slot)
+                for k in a:
+                    assert np.array_equal(a[k], b[k]), (world, shape, nm, slot, k)
+    for sid in (L.S_LOG_ALPHA, L.S_ADAM_M_LOG_ALPHA, L.S_ADAM_V_LOG_ALPHA, L.S_ALPHA):
+        assert ctxs[0].get_scalar(sid) == ctxs[1].get_scalar(sid), sid
+    hist = ctxs[0].fetch_losses(n)
+    assert np.array_equal(hist, fused)
+    for c in ctxs:
+        c.close()
