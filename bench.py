@@ -377,7 +377,7 @@ def parse_args(argv=None):
                          "the RCCL all-reduces inside its own captured graph")
     ap.add_argument("--dp-torch", action="store_true",
                     help="data parallel through torch.distributed all-reduces around the "
-                         "library's phases, captured into torch.cuda.CUDAGraphs")
+                         "library's phase graphs (eager)")
     ap.add_argument("--no-trainer-loop", action="store_true",
                     help="skip the env-free trainer-loop measurement (select_action + push + "
                          "update_parameters per env step)")

@@ -24,7 +24,6 @@ on torch's current stream, on which the library also runs.
 from __future__ import annotations
 
 import json
-import os
 import time
 
 import numpy as np
@@ -51,12 +50,8 @@ class GpuBackend:
 
     supports_fused_tail = True     # library phase 3 = phase 2 + next phase 0
 
-    def phase(self, p: int, batch: int, grad_scale: float, parity: int = 0,
-              have_batch: bool = False, ride_next: bool = False) -> None:
-        self.ctx.step_phase(batch, p, grad_scale, parity, have_batch, ride_next)
-
-    def ride_possible(self, batch: int) -> bool:
-        return self.ctx.ride_possible(batch)
+    def phase(self, p: int, batch: int, grad_scale: float) -> None:
+        self.ctx.step_phase(batch, p, grad_scale)
 
 
 class DataParallelUpdate:
@@ -68,40 +63,17 @@ class DataParallelUpdate:
         self.group = group
         self.world = dist.get_world_size(group)
         self._pending = None       # batch of an update whose phase 2 has not run
-        # ride-along sequence (begin_sequence): the next update's sampling + gather run
-        # inside this update's phase-1 launches, into the other minibatch buffer set
-        self._seq_left = 0
-        self._parity = 0
-        self._have = False
-
-    def begin_sequence(self, n: int, batch: int) -> None:
-        """The next `n` calls form one uninterrupted sequence (nothing touches the replay
-        buffer or the sampling stream in between, e.g. one captured graph): updates
-        1..n-1 get their minibatch from the previous update's ride-along work."""
-        ok = getattr(self.backend, "ride_possible", None)
-        self._seq_left = n if (ok is not None and ok(batch)) else 0
-        self._parity, self._have = 0, False
 
     def __call__(self, batch: int) -> None:
         b, scale = self.backend, 1.0 / self.world
-        ride_next = self._seq_left > 1
-        kw = {}
-        if self._seq_left > 0:
-            kw = dict(parity=self._parity, have_batch=self._have)
         if self._pending is not None and getattr(b, "supports_fused_tail", False):
-            b.phase(3, batch, scale, **kw)
+            b.phase(3, batch, scale)
         else:
             self.flush()
-            b.phase(0, batch, scale, **kw)
+            b.phase(0, batch, scale)
         self._pending = None
         dist.all_reduce(b.critic_grads, op=dist.ReduceOp.SUM, group=self.group)
-        if self._seq_left > 0:
-            b.phase(1, batch, scale, parity=self._parity, ride_next=ride_next)
-            self._seq_left -= 1
-            self._have = ride_next
-            self._parity = self._parity ^ 1 if ride_next else 0
-        else:
-            b.phase(1, batch, scale)
+        b.phase(1, batch, scale)
         dist.all_reduce(b.actor_grads, op=dist.ReduceOp.SUM, group=self.group)
         self._pending = batch
 
@@ -109,55 +81,6 @@ class DataParallelUpdate:
         if self._pending is not None:
             self.backend.phase(2, self._pending, 1.0 / self.world)
             self._pending = None
-
-
-class CapturedDataParallelUpdates:
-    """Runs data-parallel updates as replays of torch.cuda.CUDAGraphs, each holding `n`
-    consecutive updates — library launches and RCCL all-reduces — on one dedicated
-    stream (the trainer's updates_per_step loop without per-update host launches).
-    Every rank captures the same sequence, so the collectives pair up across ranks on
-    replay.  Results are bit-identical to the eager driver (tests/test_gpu_parity.py)."""
-
-    def __init__(self, ctx, device: torch.device, batch: int, group=None):
-        self.device, self.batch = device, batch
-        self.stream = torch.cuda.Stream(device)
-        with torch.cuda.stream(self.stream):
-            self.backend = GpuBackend(ctx, device)
-        ctx.set_stream(self.stream.cuda_stream)
-        self.upd = DataParallelUpdate(self.backend, group)
-        self.graphs = {}
-        # one eager update on the capture stream first: the library's phase graphs and
-        # the communicator's buffers exist before any capture begins
-        with torch.cuda.stream(self.stream):
-            self.upd(batch)
-            self.upd.flush()
-        torch.cuda.synchronize(device)
-
-    def _graph(self, n: int):
-        g = self.graphs.get(n)
-        if g is None:
-            g = torch.cuda.CUDAGraph()
-            # thread_local: API calls of other threads (the process group's watchdog
-            # polling its work events) do not invalidate this thread's capture
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
-                self.upd.begin_sequence(n, self.batch)
-                for _ in range(n):
-                    self.upd(self.batch)
-                self.upd.flush()
-            self.graphs[n] = g
-        return g
-
-    def prepare(self, *sizes: int) -> None:
-        for n in sizes:
-            if n > 0:
-                self._graph(n)
-
-    def run(self, updates: int, per_launch: int) -> None:
-        full, rem = divmod(updates, per_launch)
-        for _ in range(full):
-            self._graph(per_launch).replay()
-        if rem:
-            self._graph(rem).replay()
 
 
 def _native_comm(ctx, rank: int, device, group=None) -> None:
@@ -203,11 +126,10 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     t_fill = time.perf_counter() - t_fill
     per_launch = max(1, min(args.updates_per_launch, 256))
     sizes = B.graph_sizes(args.steps, per_launch)
-    captured = None
     # default: the library's own RCCL sequence (sacmi_step_dp, one hipGraph per n updates).
-    # The torch.distributed driver (--dp-torch) captures torch's collectives into
-    # CUDAGraphs, where ProcessGroupNCCL's watchdog thread can query a work event recorded
-    # during the capture and abort the process (seen once in a world-1 run this round)
+    # --dp-torch: the torch.distributed driver, eager (torch's all-reduces between the
+    # library's phase graphs).  Its torch.cuda.CUDAGraph-captured form was dropped: a world-1
+    # run aborted in ProcessGroupNCCL's watchdog during a capture
     native = not getattr(args, "dp_torch", False)
     # the library's communicator: the native driver's collectives, and the roofline's
     # timeline of the data-parallel sequence (both paths)
@@ -225,29 +147,13 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
                 ctx.step_dp(args.batch, per_launch)
             if rem:
                 ctx.step_dp(args.batch, rem)
-    elif os.environ.get("SACMI_DP_GRAPH", "1") == "1":
-        try:
-            captured = CapturedDataParallelUpdates(ctx, device, args.batch)
-            captured.prepare(*sizes)
-            for n in sizes:                       # every graph replayed once before timing
-                captured.run(n, per_launch)
-        except Exception as e:                     # capture unsupported: eager driver
-            if rank == 0:
-                print(f"sacmi.dp: graph capture failed ({e}); eager updates", flush=True)
-            captured = None
-            torch.cuda.synchronize()
-    if native:
-        pass
-    elif captured is None:
+    else:
         upd = DataParallelUpdate(GpuBackend(ctx, device))
 
         def run(k):
             for _ in range(k):
                 upd(args.batch)
             upd.flush()
-    else:
-        def run(k):
-            captured.run(k, per_launch)
     run(args.warmup)
     torch.cuda.synchronize()
 
@@ -305,8 +211,8 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
                        "global_batch": args.batch * world, "replay_fill": fill * world,
                        "replay": wl["replay"], "parallelism": f"dp{world}"},
             "iterations_per_s": round(iters, 2),
-            "updates_per_launch": per_launch if (captured or native) else 1,
-            "dp_graph": captured is not None or native,
+            "updates_per_launch": per_launch if native else 1,
+            "dp_graph": native,
             "dp_driver": "library (sacmi_step_dp: RCCL issued by libsacmi)" if native
                          else "torch.distributed (RCCL) around sacmi phases",
             "mfma_util_step": round(flops * value / 1e12 / peak / world, 4),

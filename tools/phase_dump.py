@@ -10,6 +10,9 @@ import sys
 import numpy as np
 
 
+SLOW = 0
+
+
 def main(path):
     raw = open(path, "rb").read()
     sites, per, words, nph = struct.unpack("4q", raw[:32])
@@ -40,6 +43,13 @@ def main(path):
             "wgmax": np.max(ph[:, 5] - ph[:, 0]) * 0.01,
         }
         acc.setdefault(names[s], []).append(d)
+        if SLOW:   # the slowest workgroups of this site's first launch, phase by phase
+            bids = np.nonzero(live)[0]
+            tot = ph[:, 5] - ph[:, 0]
+            for r in np.argsort(tot)[::-1][:SLOW]:
+                seg = np.diff(ph[r]) * 0.01
+                print(f"  slow {names[s]:28s} wg {bids[r]:4d} start {(ph[r, 0] - start) * 0.01:6.2f} "
+                      f"total {tot[r] * 0.01:6.2f} phases " + " ".join(f"{v:5.2f}" for v in seg))
     keys = ["start", "startmax", "setup", "core0", "wait", "epi", "tail", "wg", "wgmax"]
     print(f"{'site':32s} " + " ".join(f"{k:>8s}" for k in keys))
     for n, lst in acc.items():
@@ -47,4 +57,6 @@ def main(path):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2:
+        SLOW = int(sys.argv[2])
     main(sys.argv[1])
