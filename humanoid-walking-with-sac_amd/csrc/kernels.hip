@@ -569,6 +569,12 @@ __device__ __forceinline__ void adam_block0(const AdamFuse& af, int err, float o
       af.loss_ring[q * 3 + 2] = af.sc->losses[2];
       af.sc->loss_ring_pos = pos + 1;
     }
+    if (threadIdx.x == 0 && af.done_word) {   // (voided updates too: the host waits on it)
+      const int v = af.sc->done_seq + 1;
+      af.sc->done_seq = v;
+      __threadfence_system();                  // the losses and error bits land first
+      *reinterpret_cast<volatile int*>(af.done_word) = v;
+    }
   }
 }
 
@@ -2872,20 +2878,11 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
       a.logp_part[2 * blockIdx.x + threadIdx.x] = s;
     }
   }
-}
-
-// rows of `cols` floats in, and the constant-1 column right after them (a batch-4096 bf16
-// update may have overwritten the fp32 layout's ones column: the buffers are shared)
-__global__ void k_rows_in(float* dst, int ldd, const float* src, int lds, int cols) {
-  const float* s = src + (size_t)blockIdx.x * lds;
-  float* d = dst + (size_t)blockIdx.x * ldd;
-  for (int c = threadIdx.x; c < cols; c += blockDim.x) d[c] = s[c];
-  if (threadIdx.x == 0) d[cols] = 1.f;
-}
-
-void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int cols, hipStream_t s) {
-  hipLaunchKernelGGL(k_rows_in, dim3(n), dim3(256), 0, s, dst, ldd, src, lds, cols);
-  HIP_LAUNCH_CHECK();
+  if (a.done_word) {   // (one workgroup) every store above lands first
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) *reinterpret_cast<volatile int*>(a.done_word) = a.done_value;
+  }
 }
 
 __global__ void k_to_bf16(unsigned short* dst, const float* src, int64_t n) {

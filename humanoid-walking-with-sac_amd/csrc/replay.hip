@@ -25,17 +25,50 @@
 
 namespace sacmi {
 
-__global__ __launch_bounds__(1024) void k_mt_sample(MtSampleArgs a, int tbl_log2) {
-  const TlMark tl_mark(a.tl, TL_MT_SAMPLE);
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  mt_sample_body(a, tbl_log2, smem);
+// The mailbox's rows into the ring slots pos0.. (k_push_rows' stores, from the packed
+// host-mapped rows), then the replay's len / head; returns the new len (-1: no rows)
+__device__ int64_t mailbox_scatter(const MailboxArgs& mb, DevScalars* sc) {
+  __shared__ int s_n;
+  __shared__ int64_t s_hdr[3];
+  if (threadIdx.x == 0) {
+    const volatile PushMailbox* h = mb.hdr;
+    s_n = h->n;
+    s_hdr[0] = h->pos0; s_hdr[1] = h->len; s_hdr[2] = h->head;
+  }
+  __syncthreads();
+  const int n = s_n;
+  if (n <= 0) return -1;
+  const int S = mb.S, A = mb.A, rowf = 2 * S + A + 2;
+  for (int e = threadIdx.x; e < n * rowf; e += blockDim.x) {
+    const int j = e / rowf, c = e - j * rowf;
+    const int64_t w = (s_hdr[0] + j) % mb.cap;
+    const float v = mb.rows[e];
+    if (c < S) mb.obs[w * mb.ldo + c] = v;
+    else if (c < S + A) mb.act[w * mb.ldact + c - S] = v;
+    else if (c == S + A) mb.rew[w] = v;
+    else if (c < 2 * S + A + 1) mb.obs2[w * mb.ldo + c - S - A - 1] = v;
+    else mb.done[w] = v;
+  }
+  if (threadIdx.x == 0) {
+    sc->len = s_hdr[1];
+    sc->head = s_hdr[2];
+  }
+  return s_hdr[1];
 }
 
-void launch_mt_sample(const MtSampleArgs& a, hipStream_t s) {
+__global__ __launch_bounds__(1024) void k_mt_sample(MtSampleArgs a, int tbl_log2, MailboxArgs mb) {
+  const TlMark tl_mark(a.tl, TL_MT_SAMPLE);
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int64_t len = mb.hdr ? mailbox_scatter(mb, const_cast<DevScalars*>(a.sc)) : -1;
+  mt_sample_body(a, tbl_log2, smem, len);
+}
+
+void launch_mt_sample(const MtSampleArgs& a, hipStream_t s, const MailboxArgs* mb) {
   const int tl = mt_sample_tbl_log2(a.k);
   const size_t lds = mt_sample_lds_words(tl, a.setsize) * 4;
   ensure_dyn_lds(reinterpret_cast<const void*>(&k_mt_sample), lds);
-  hipLaunchKernelGGL(k_mt_sample, dim3(1), dim3(1024), lds, s, a, tl);
+  const MailboxArgs m = mb ? *mb : MailboxArgs{};
+  hipLaunchKernelGGL(k_mt_sample, dim3(1), dim3(1024), lds, s, a, tl, m);
   launch_check("k_mt_sample");
 }
 

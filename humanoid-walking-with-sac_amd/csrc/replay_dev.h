@@ -88,7 +88,9 @@ __host__ __device__ constexpr size_t mt_sample_lds_words(int tbl_log2, int setsi
 // Body of the sampler for one workgroup of 256..1024 threads; `lds` holds
 // mt_sample_lds_words(tbl_log2, setsize) words.  Used by k_mt_sample and, riding along
 // in a GEMM launch, for the next update of a multi-update graph.
-__device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_log2, uint32_t* lds) {
+// len_override >= 0: the population size (the mailbox rows this kernel just stored)
+__device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_log2, uint32_t* lds,
+                                               int64_t len_override = -1) {
   const size_t tbl_words = ((size_t)2 << tbl_log2) > (size_t)a.setsize ? ((size_t)2 << tbl_log2)
                                                                         : (size_t)a.setsize;
   uint32_t* smem = lds;
@@ -97,7 +99,7 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
   int& s_last = wave_tot[32];
   int& s_pos = wave_tot[33];
   const int t = threadIdx.x;
-  const int64_t n64 = a.sc->len;
+  const int64_t n64 = len_override >= 0 ? len_override : a.sc->len;
   const uint32_t n = (uint32_t)n64;
   const int k = a.k;
   // an update graph's sampler after a non-finite policy sample / PER draw (ErrBits): the

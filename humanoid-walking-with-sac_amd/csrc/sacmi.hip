@@ -9,6 +9,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -141,6 +142,10 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> dq, dhead, dhc[3], dha[3], dhp[3];
   sacmi::DevBuf<float> dotp;       // fc3 dot partials [6 slots][B][nparts]
   sacmi::DevBuf<float> pa;         // dL/da partials [2 * nparts][B][A] (L9 epilogue -> tail)
+  int pending_step = 0;             // batch of a sacmi_step_launch not yet waited for
+  bool inflight = false;            // updates enqueued since the last full wait
+  int pending_done = -1;            // the done word before that launch (step_finish)
+  int act_seq = 0;                  // select_action launches (their heads' done word)
   sacmi::DevBuf<float> dw_ws;      // bf16 deep-K weight-gradient split-K partials
   int nparts = 0;
   sacmi::DevBuf<float> lpart_c, lpart_a, ring, lp_part;
@@ -156,8 +161,26 @@ struct sacmi_ctx {
   int push_rows = 0;                        // rows per ingest chunk
   float* push_host[kPushSlots] = {};
   hipEvent_t push_ev[kPushSlots] = {};
+  // small pushes (the trainer's row per env step): mapped staging the scatter kernel reads
+  // directly (no copy command in front of the next update)
+  static constexpr int kPushZcRows = 16;
+  float* push_zc_host[kPushSlots] = {};
+  float* push_zc_dev[kPushSlots] = {};
+  int64_t push_zc_epoch[kPushSlots] = {};  // the stream epoch that read the slot
+  int push_zc_slot = 0;
+  // the push mailbox (PushMailbox): rows pending for the next synchronous update's sampler
+  static constexpr int kMbRows = 16;
+  sacmi::PushMailbox* mb_host = nullptr;
+  sacmi::PushMailbox* mb_dev = nullptr;
+  int mb_pending = 0;               // rows in it
+  bool mb_graph = false;            // the update being enqueued consumes them
+  // stream epochs: bumped by every zero-copy push; `done_epoch` = the epoch of the last
+  // completed wait (step / act / synchronize): every earlier launch has finished, so a
+  // staging slot read at an earlier epoch is free without an event (an event record is
+  // one more packet between the push and the update behind it)
+  int64_t epoch = 1, done_epoch = 0;
   int push_slot = 0;
-  float* act_host = nullptr;                // [kActPinned][S] states, then [..][A] eps / out
+  float* act_host = nullptr;                // [kActPinned][Kx] states (| 1 | 0..), then [..][A] eps / out
   float* act_host_dev = nullptr;            // the same memory, device-mapped
   int* act_nan_host = nullptr;              // select_action's Normal validation flag (mapped)
   int* act_nan_dev = nullptr;
@@ -356,7 +379,10 @@ static void upload_scalars(sacmi_ctx* c, const DevScalars& h) {
   CHECK_HIP(hipMemcpyAsync(c->sc.p, c->sc_host, sizeof(h), hipMemcpyHostToDevice, c->stream));
   CHECK_HIP(hipStreamSynchronize(c->stream));
 }
+static void mb_flush(sacmi_ctx* c);
+static MailboxArgs mailbox_args(sacmi_ctx* c);
 static DevScalars download_scalars(sacmi_ctx* c) {
+  mb_flush(c);
   CHECK_HIP(hipMemcpyAsync(c->sc_host, c->sc.p, sizeof(DevScalars), hipMemcpyDeviceToHost, c->stream));
   CHECK_HIP(hipStreamSynchronize(c->stream));
   return *c->sc_host;
@@ -374,19 +400,35 @@ static void alloc_pinned(sacmi_ctx* c) {
     CHECK_HIP(hipEventCreateWithFlags(&c->push_ev[i], hipEventDisableTiming));
   }
   c->stage.alloc(row * c->push_rows);
+  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->mb_host), sizeof(PushMailbox) + row * sacmi_ctx::kMbRows * 4,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->mb_dev), c->mb_host, 0));
+  c->mb_host->n = 0;
+  for (int i = 0; i < sacmi_ctx::kPushSlots; ++i) {
+    CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->push_zc_host[i]), row * sacmi_ctx::kPushZcRows * 4,
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->push_zc_dev[i]), c->push_zc_host[i], 0));
+  }
   // select_action staging: fine-grained (coherent) and mapped, so the kernels read the
   // states and write the actions in place (no copy commands on the env-rate path)
-  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->act_host),
-                          (size_t)kActPinned * (S + 2 * A) * 4 + 16,
+  // (the state rows in fc1's input layout, the ones column set here once: fc1 reads them
+  // as its A operand in place)
+  const size_t act_floats = (size_t)kActPinned * (c->Kx + 2 * A);
+  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->act_host), act_floats * 4 + 16,
                           hipHostMallocMapped | hipHostMallocCoherent));
   CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->act_host_dev), c->act_host, 0));
-  c->act_nan_host = reinterpret_cast<int*>(c->act_host + (size_t)kActPinned * (S + 2 * A));
-  c->act_nan_dev = reinterpret_cast<int*>(c->act_host_dev + (size_t)kActPinned * (S + 2 * A));
+  std::memset(c->act_host, 0, act_floats * 4 + 16);
+  for (int i = 0; i < kActPinned; ++i) c->act_host[(size_t)i * c->Kx + S] = 1.f;
+  registry_add((uintptr_t)c->act_host_dev, act_floats * 4);
+  c->act_nan_host = reinterpret_cast<int*>(c->act_host + act_floats);
+  c->act_nan_dev = reinterpret_cast<int*>(c->act_host_dev + act_floats);
+  c->act_nan_host[1] = 0;                        // (select_action's done word: sacmi_act)
   // update_parameters' three losses, stored here by the fused Adam levels' block 0: the
   // synchronous step reads them after the stream sync, no copy command
-  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->loss_host), 16,
+  CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->loss_host), 32,
                           hipHostMallocMapped | hipHostMallocCoherent));
   CHECK_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->loss_host_dev), c->loss_host, 0));
+  std::memset(c->loss_host, 0, 32);             // (word 4: the done word, step_finish)
   CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->sc_host), sizeof(DevScalars),
                           hipHostMallocDefault));
   CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ring_host), (size_t)c->ring_slots * 12,
@@ -399,7 +441,13 @@ static void free_pinned(sacmi_ctx* c) {
     if (c->push_host[i]) (void)hipHostFree(c->push_host[i]);
     c->push_ev[i] = nullptr;
     c->push_host[i] = nullptr;
+    if (c->push_zc_host[i]) (void)hipHostFree(c->push_zc_host[i]);
+    if (i == 0 && c->mb_host) (void)hipHostFree(c->mb_host);
+    if (i == 0) { c->mb_host = nullptr; c->mb_dev = nullptr; }
+    c->push_zc_host[i] = nullptr;
+    c->push_zc_dev[i] = nullptr;
   }
+  if (c->act_host_dev) registry_remove((uintptr_t)c->act_host_dev);
   if (c->act_host) (void)hipHostFree(c->act_host);
   if (c->sc_host) (void)hipHostFree(c->sc_host);
   if (c->ring_host) (void)hipHostFree(c->ring_host);
@@ -714,7 +762,8 @@ static void enqueue_sample_gather(sacmi_ctx* c, int B, int parity, bool dev_idx,
     if (mark(c, ("mt_sample" + t).c_str())) {
       MtSampleArgs ma = mt_args(c, B, bb);
       ma.tl = c->tl_cur;
-      launch_mt_sample(ma, s);
+      const MailboxArgs mb = mailbox_args(c);
+      launch_mt_sample(ma, s, c->mb_graph && t.empty() ? &mb : nullptr);
     }
   }
   if (mark(c, ("gather" + t).c_str())) {
@@ -1064,6 +1113,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.loss_div = (float)B; f.log_alpha_idx = c->la_idx; f.auto_entropy = c->cfg.auto_entropy;
       f.log_alpha_grad = G + c->la_idx;
       f.loss_ring = use_ring ? c->ring.p : nullptr; f.ring = c->ring_slots;
+      f.done_word = reinterpret_cast<int*>(c->loss_host_dev + 4);
       f.err_skip = ~0; f.err_nopolyak = 0;
     }
     if (polyak_ride) {   // (polyak_ride: the critic Adam above left the targets alone)
@@ -1177,6 +1227,8 @@ static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use
 
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
                        float grad_scale, bool use_ring, int reps = 1, PhaseRide pr = {}) {
+  if (!c->mb_graph) mb_flush(c);   // (mb_graph: this update's sampler takes them)
+  c->inflight = true;
   // consecutive fused updates hand the next update's sampling + gather to ride-along
   // workgroups of the current one
   auto enqueue_all = [&]() {
@@ -1203,7 +1255,8 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
   }
   GraphKey key{B, dev_idx, dev_eps,
                phase_mask | (grad_scale != 1.f ? 8 : 0) | (c->keep_grads ? 16 : 0) |
-                   (pr.parity ? 32 : 0) | (pr.have_batch ? 64 : 0) | (pr.ride_next ? 128 : 0),
+                   (pr.parity ? 32 : 0) | (pr.have_batch ? 64 : 0) | (pr.ride_next ? 128 : 0) |
+                   (c->mb_graph ? 256 : 0),
                use_ring ? c->ring_slots : 0,
                per_graph_len(c), reps};
   auto it = c->graphs.find(key);
@@ -1463,7 +1516,11 @@ int sacmi_set_stream(sacmi_ctx* c, void* stream) {
 }
 
 int sacmi_synchronize(sacmi_ctx* c) {
-  return guard([&] { CHECK_HIP(hipStreamSynchronize(c->stream)); });
+  return guard([&] {
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    c->inflight = false;
+    c->done_epoch = c->epoch;
+  });
 }
 
 int sacmi_tensor_numel(sacmi_ctx* c, int net, int layer, int part, int64_t* numel) {
@@ -1594,56 +1651,179 @@ int sacmi_get_scalar(sacmi_ctx* c, int which, double* value) {
   return guard([&] { scalar_io(c, which, nullptr, value); });
 }
 
-int sacmi_push(sacmi_ctx* c, const float* s, const float* a, const float* r, const float* s2,
-               const uint8_t* d, int64_t n) {
-  return guard([&] {
-    REQUIRE(n >= 0, SACMI_EVALUE, "n < 0");
-    if (n == 0) return;
-    REQUIRE(s && a && r && s2 && d, SACMI_EVALUE, "null transition array");
-    // only the last `capacity` rows of a huge batch survive (deque(maxlen))
-    const int64_t skip = n > c->capacity ? n - c->capacity : 0;
+namespace sacmi {
+static float* mb_rows_host(sacmi_ctx* c) { return reinterpret_cast<float*>(c->mb_host + 1); }
+
+// The mailbox's rows through the scatter kernel (every path but the synchronous update
+// that would have consumed them): staged SoA in a zero-copy slot, rows and len / head as
+// the mailbox recorded them (the host's len / wpos already count them)
+static void mb_flush(sacmi_ctx* c) {
+  if (c->mb_pending == 0) return;
+  const int S = c->S, A = c->A, m = c->mb_pending;
+  const int64_t rowf = 2 * S + A + 2;
+  const int k = c->push_zc_slot;
+  c->push_zc_slot = (k + 1) % sacmi_ctx::kPushSlots;
+  if (c->push_zc_epoch[k] > c->done_epoch) {
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    c->done_epoch = c->epoch;
+  }
+  c->push_zc_epoch[k] = ++c->epoch;
+  float* h = c->push_zc_host[k];
+  const float* src = mb_rows_host(c);
+  for (int j = 0; j < m; ++j) {
+    const float* p = src + j * rowf;
+    std::memcpy(h + j * S, p, (size_t)S * 4);
+    std::memcpy(h + m * S + j * A, p + S, (size_t)A * 4);
+    h[m * (S + A) + j] = p[S + A];
+    std::memcpy(h + m * (S + A + 1) + j * S, p + S + A + 1, (size_t)S * 4);
+    h[m * (2 * S + A + 1) + j] = p[2 * S + A + 1];
+  }
+  PushArgs pa{};
+  pa.stage = c->push_zc_dev[k];
+  pa.obs = c->obs.p; pa.obs2 = c->obs2.p; pa.act = c->act.p; pa.rew = c->rew.p; pa.done = c->done.p;
+  pa.S = S; pa.A = A; pa.ldo = c->ldo; pa.ldact = c->ldact;
+  pa.n = m; pa.pos0 = c->mb_host->pos0; pa.cap = c->capacity;
+  pa.sc = c->sc.p;
+  pa.len = c->mb_host->len;
+  pa.head = c->mb_host->head;
+  launch_push_rows(pa, c->stream);
+  CHECK_HIP(hipGetLastError());
+  c->mb_pending = 0;
+}
+
+static MailboxArgs mailbox_args(sacmi_ctx* c) {
+  MailboxArgs m{};
+  m.hdr = c->mb_dev; m.rows = reinterpret_cast<const float*>(c->mb_dev + 1);
+  m.obs = c->obs.p; m.obs2 = c->obs2.p; m.act = c->act.p; m.rew = c->rew.p; m.done = c->done.p;
+  m.S = c->S; m.A = c->A; m.ldo = c->ldo; m.ldact = c->ldact; m.cap = c->capacity;
+  return m;
+}
+}  // namespace sacmi
+
+// Rows [n] of transitions into the ring (deque(maxlen) semantics), from either layout:
+// separate arrays (packed == nullptr) or packed rows [n][2S + A + 2] = s | a | r | s2 | d.
+static void push_impl(sacmi_ctx* c, const float* s, const float* a, const float* r, const float* s2,
+                      const uint8_t* d, const float* packed, int64_t n) {
+  REQUIRE(n >= 0, SACMI_EVALUE, "n < 0");
+  if (n == 0) return;
+  REQUIRE(packed || (s && a && r && s2 && d), SACMI_EVALUE, "null transition array");
+  {
+    // a few rows while no update is in flight: into the mailbox, for the next synchronous
+    // update's sampler (uniform replay; every other path flushes them first)
+    static const bool mb_env = std::getenv("SACMI_NO_PUSH_MAILBOX") == nullptr;
     const int S = c->S, A = c->A;
-    const bool was_empty = c->len == 0;
-    const int64_t cap = c->capacity;
-    const int64_t pos0 = (c->wpos + skip) % cap;   // ring slot of row `skip`
-    // chunks of push_rows rows: pack into a pinned slot (SoA), one async H2D copy, one
-    // scatter kernel; the slot is reused once its copy has completed (event)
-    for (int64_t i = skip; i < n; i += c->push_rows) {
-      const int64_t m = std::min<int64_t>(c->push_rows, n - i);
-      const int k = c->push_slot;
+    const int64_t rowf = 2 * S + A + 2;
+    if (mb_env && c->mb_host && !c->inflight && c->cfg.replay_kind == SACMI_REPLAY_UNIFORM &&
+        c->mb_pending + n <= sacmi_ctx::kMbRows) {
+      float* dst = mb_rows_host(c) + (size_t)c->mb_pending * rowf;
+      for (int64_t j = 0; j < n; ++j, dst += rowf) {
+        if (packed) {
+          std::memcpy(dst, packed + j * rowf, (size_t)rowf * 4);
+        } else {
+          std::memcpy(dst, s + j * S, (size_t)S * 4);
+          std::memcpy(dst + S, a + j * A, (size_t)A * 4);
+          dst[S + A] = r[j];
+          std::memcpy(dst + S + A + 1, s2 + j * S, (size_t)S * 4);
+          dst[rowf - 1] = d[j] ? 1.f : 0.f;
+        }
+        dst[rowf - 1] = dst[rowf - 1] != 0.f ? 1.f : 0.f;
+      }
+      if (c->mb_pending == 0) c->mb_host->pos0 = c->wpos;
+      c->mb_pending += (int)n;
+      c->wpos = (c->wpos + n) % c->capacity;
+      c->len = std::min<int64_t>(c->capacity, c->len + n);
+      c->mb_host->len = c->len;
+      c->mb_host->head = c->len < c->capacity ? 0 : c->wpos;
+      c->mb_host->n = c->mb_pending;
+      return;
+    }
+  }
+  mb_flush(c);                     // (rows keep their order)
+  // only the last `capacity` rows of a huge batch survive (deque(maxlen))
+  const int64_t skip = n > c->capacity ? n - c->capacity : 0;
+  const int S = c->S, A = c->A;
+  const int64_t rowf = 2 * S + A + 2;
+  const bool was_empty = c->len == 0;
+  const int64_t cap = c->capacity;
+  const int64_t pos0 = (c->wpos + skip) % cap;   // ring slot of row `skip`
+  // chunks of push_rows rows: pack into a pinned slot (SoA), one async H2D copy, one
+  // scatter kernel; the slot is reused once its copy has completed (event).  Chunks of at
+  // most kPushZcRows rows go through mapped staging instead: the scatter kernel reads it
+  for (int64_t i = skip; i < n; i += c->push_rows) {
+    const int64_t m = std::min<int64_t>(c->push_rows, n - i);
+    const bool zc = m <= sacmi_ctx::kPushZcRows;
+    int k;
+    float* h;
+    if (zc) {
+      k = c->push_zc_slot;
+      c->push_zc_slot = (k + 1) % sacmi_ctx::kPushSlots;
+      if (c->push_zc_epoch[k] > c->done_epoch) {   // its reader may still be queued
+        CHECK_HIP(hipStreamSynchronize(c->stream));
+        c->done_epoch = c->epoch;
+      }
+      c->push_zc_epoch[k] = ++c->epoch;
+      h = c->push_zc_host[k];
+    } else {
+      k = c->push_slot;
       c->push_slot = (k + 1) % sacmi_ctx::kPushSlots;
       CHECK_HIP(hipEventSynchronize(c->push_ev[k]));
-      float* h = c->push_host[k];
+      h = c->push_host[k];
+    }
+    float* hd = h + m * (2 * S + A + 1);
+    if (packed) {
+      if (m == 1) {                    // one row: the packed layout IS the SoA layout
+        std::memcpy(h, packed + i * rowf, (size_t)rowf * 4);
+      } else {
+        for (int64_t j = 0; j < m; ++j) {
+          const float* p = packed + (i + j) * rowf;
+          std::memcpy(h + j * S, p, (size_t)S * 4);
+          std::memcpy(h + m * S + j * A, p + S, (size_t)A * 4);
+          h[m * (S + A) + j] = p[S + A];
+          std::memcpy(h + m * (S + A + 1) + j * S, p + S + A + 1, (size_t)S * 4);
+          hd[j] = p[2 * S + A + 1];
+        }
+      }
+      for (int64_t j = 0; j < m; ++j) hd[j] = hd[j] != 0.f ? 1.f : 0.f;
+    } else {
       std::memcpy(h, s + i * S, (size_t)m * S * 4);
       std::memcpy(h + m * S, a + i * A, (size_t)m * A * 4);
       std::memcpy(h + m * (S + A), r + i, (size_t)m * 4);
       std::memcpy(h + m * (S + A + 1), s2 + i * S, (size_t)m * S * 4);
-      float* hd = h + m * (2 * S + A + 1);
       for (int64_t j = 0; j < m; ++j) hd[j] = d[i + j] ? 1.f : 0.f;
-      CHECK_HIP(hipMemcpyAsync(c->stage.p, h, (size_t)m * (2 * S + A + 2) * 4, hipMemcpyHostToDevice,
-                               c->stream));
+    }
+    if (!zc) {
+      CHECK_HIP(hipMemcpyAsync(c->stage.p, h, (size_t)m * rowf * 4, hipMemcpyHostToDevice, c->stream));
       CHECK_HIP(hipEventRecord(c->push_ev[k], c->stream));
-      const int64_t done_rows = i + m - skip;
-      PushArgs pa{};
-      pa.stage = c->stage.p;
-      pa.obs = c->obs.p; pa.obs2 = c->obs2.p; pa.act = c->act.p; pa.rew = c->rew.p; pa.done = c->done.p;
-      pa.S = S; pa.A = A; pa.ldo = c->ldo; pa.ldact = c->ldact;
-      pa.n = m; pa.pos0 = (pos0 + (i - skip)) % cap; pa.cap = cap;
-      pa.sc = c->sc.p;
-      const int64_t len = std::min<int64_t>(cap, c->len + skip + done_rows);
-      const int64_t wpos = (c->wpos + skip + done_rows) % cap;
-      pa.len = len;
-      pa.head = len < cap ? 0 : wpos;
-      launch_push_rows(pa, c->stream);
-      CHECK_HIP(hipGetLastError());
     }
-    const int64_t added = n - skip;
-    if (c->cfg.replay_kind == SACMI_REPLAY_PER) {
-      launch_per_push(c->prio.p, c->capacity, pos0, added, was_empty ? 1 : 0, c->per_scr.p, c->stream);
-    }
-    c->wpos = (c->wpos + n) % c->capacity;
-    c->len = std::min<int64_t>(c->capacity, c->len + n);
-  });
+    const int64_t done_rows = i + m - skip;
+    PushArgs pa{};
+    pa.stage = zc ? c->push_zc_dev[k] : c->stage.p;
+    pa.obs = c->obs.p; pa.obs2 = c->obs2.p; pa.act = c->act.p; pa.rew = c->rew.p; pa.done = c->done.p;
+    pa.S = S; pa.A = A; pa.ldo = c->ldo; pa.ldact = c->ldact;
+    pa.n = m; pa.pos0 = (pos0 + (i - skip)) % cap; pa.cap = cap;
+    pa.sc = c->sc.p;
+    const int64_t len = std::min<int64_t>(cap, c->len + skip + done_rows);
+    const int64_t wpos = (c->wpos + skip + done_rows) % cap;
+    pa.len = len;
+    pa.head = len < cap ? 0 : wpos;
+    launch_push_rows(pa, c->stream);
+    CHECK_HIP(hipGetLastError());
+  }
+  const int64_t added = n - skip;
+  if (c->cfg.replay_kind == SACMI_REPLAY_PER) {
+    launch_per_push(c->prio.p, c->capacity, pos0, added, was_empty ? 1 : 0, c->per_scr.p, c->stream);
+  }
+  c->wpos = (c->wpos + n) % c->capacity;
+  c->len = std::min<int64_t>(c->capacity, c->len + n);
+}
+
+int sacmi_push(sacmi_ctx* c, const float* s, const float* a, const float* r, const float* s2,
+               const uint8_t* d, int64_t n) {
+  return guard([&] { push_impl(c, s, a, r, s2, d, nullptr, n); });
+}
+
+int sacmi_push_packed(sacmi_ctx* c, const float* rows, int64_t n) {
+  return guard([&] { push_impl(c, nullptr, nullptr, nullptr, nullptr, nullptr, rows, n); });
 }
 
 int sacmi_len(sacmi_ctx* c, int64_t* n) {
@@ -1665,6 +1845,7 @@ int sacmi_replay_clear(sacmi_ctx* c) {
 int sacmi_get_rows(sacmi_ctx* c, const int64_t* idx, int64_t n, float* s, float* a, float* r,
                    float* s2, uint8_t* d) {
   return guard([&] {
+    mb_flush(c);
     CHECK_HIP(hipStreamSynchronize(c->stream));
     const int64_t head = c->len < c->capacity ? 0 : c->wpos;
     for (int64_t i = 0; i < n; ++i) {
@@ -1736,6 +1917,7 @@ int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
     REQUIRE(batch <= c->Bm, SACMI_EVALUE, "batch > max_batch");
     REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
     if (batch == 0) return;
+    mb_flush(c);
     MtSampleArgs ma = mt_args(c, batch, batch_bufs(c, 0));
     ma.skip_on_err = 0;                // a host call: the reference's random.sample always runs
     launch_mt_sample(ma, c->stream);
@@ -1745,23 +1927,92 @@ int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
   });
 }
 
+// A synchronous single update (sacmi_step / sacmi_step_launch): with device sampling the
+// update's sampler also stores the rows waiting in the push mailbox (its graph variant)
+static void run_update_mb(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool mb_ok) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;   // (a caller's capture would
+  CHECK_HIP(hipStreamIsCapturing(c->stream, &cap));          //  replay the mailbox read)
+  c->mb_graph = mb_ok && dev_idx && c->mb_pending > 0 && cap == hipStreamCaptureStatusNone &&
+                c->cfg.replay_kind == SACMI_REPLAY_UNIFORM;
+  try {
+    run_update(c, B, dev_idx, dev_eps, 7, 1.f, false);
+  } catch (...) {
+    c->mb_graph = false;
+    throw;
+  }
+  if (c->mb_graph) c->mb_pending = 0;
+  c->mb_graph = false;
+}
+
+// The done word's value before a synchronous step's launch: with nothing else in flight, its
+// next change is that update's (step_finish polls for it); -1 otherwise (stream sync)
+static int done_prev(sacmi_ctx* c) {
+  static const bool poll = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
+  if (!poll || c->inflight) return -1;
+  return *reinterpret_cast<volatile int*>(c->loss_host + 4);
+}
+
+// the synchronous step's second half: wait, then the losses (or the error bits) the
+// update's last kernels stored into host-mapped memory
+// done_prev >= 0: the done word's value before the launch, with no other update in flight:
+// the host polls the word the update's last level stores (host-mapped, behind a
+// system-scope fence) instead of waiting for the stream's completion signal
+static void step_finish(sacmi_ctx* c, int batch, float* losses_out, int done_prev = -1) {
+  bool done = false;
+  if (done_prev >= 0) {
+    volatile int* w = reinterpret_cast<volatile int*>(c->loss_host + 4);
+    for (int it = 1;; ++it) {
+      if (*w != done_prev) { done = true; break; }
+      if ((it & 1023) == 0) {   // finished without the store (or failed): the sync reports
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q != hipErrorNotReady) break;
+        (void)hipGetLastError();
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
+  if (!done) CHECK_HIP(hipStreamSynchronize(c->stream));
+  c->inflight = false;
+  c->done_epoch = c->epoch;             // (the update ran after everything enqueued before it)
+  int err = 0;                                   // ErrBits the update's L6 saw
+  std::memcpy(&err, c->loss_host + 3, 4);
+  if (err) {
+    clear_err(c);
+    throw Error{SACMI_ENAN, nan_message(c, err, batch, " during update_parameters")};
+  }
+  std::memcpy(losses_out, c->loss_host, 12);    // stored by the update's last kernels
+}
+
 int sacmi_step(sacmi_ctx* c, int32_t batch, const int64_t* idx, const float* eps1,
                const float* eps2, float* losses_out) {
   return guard([&] {
     check_batch(c, batch);
     REQUIRE(idx || batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
     stage_inputs(c, batch, idx, eps1, eps2);
-    run_update(c, batch, idx ? 0 : 1, (eps1 || eps2) ? 0 : 1, 7, 1.f, false);
-    if (losses_out) {
-      CHECK_HIP(hipStreamSynchronize(c->stream));
-      int err = 0;                                   // ErrBits the update's L6 saw
-      std::memcpy(&err, c->loss_host + 3, 4);
-      if (err) {
-        clear_err(c);
-        throw Error{SACMI_ENAN, nan_message(c, err, batch, " during update_parameters")};
-      }
-      std::memcpy(losses_out, c->loss_host, 12);    // stored by the update's last kernels
-    }
+    const int prev = done_prev(c);
+    run_update_mb(c, batch, idx ? 0 : 1, (eps1 || eps2) ? 0 : 1, !idx && batch <= 4096);
+    if (losses_out) step_finish(c, batch, losses_out, prev);
+  });
+}
+
+int sacmi_step_launch(sacmi_ctx* c, int32_t batch) {
+  return guard([&] {
+    REQUIRE(c->pending_step == 0, SACMI_ESTATE, "sacmi_step_launch: the previous launch was not waited for");
+    check_device_batch(c, batch);
+    stage_inputs(c, batch, nullptr, nullptr, nullptr);
+    c->pending_done = done_prev(c);
+    run_update_mb(c, batch, 1, 1, true);           // (sacmi_step's graph: the same bits)
+    c->pending_step = batch;
+  });
+}
+
+int sacmi_step_wait(sacmi_ctx* c, float* losses_out) {
+  return guard([&] {
+    REQUIRE(c->pending_step > 0, SACMI_ESTATE, "sacmi_step_wait without a launch");
+    REQUIRE(losses_out, SACMI_EVALUE, "losses_out is NULL");
+    const int batch = c->pending_step;
+    c->pending_step = 0;
+    step_finish(c, batch, losses_out, c->pending_done);
   });
 }
 
@@ -1870,6 +2121,7 @@ int sacmi_dp_loopback_init(sacmi_ctx* c, int32_t world) {
 
 int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   return guard([&] {
+    mb_flush(c);
     REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
@@ -1947,6 +2199,7 @@ int sacmi_grad_buffer(sacmi_ctx* c, int which, void** ptr, int64_t* numel) {
 int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_out,
                        float* ms_out, double* flops_out, int32_t max_sites, int32_t* n_sites) {
   return guard([&] {
+    mb_flush(c);
     check_device_batch(c, batch);
     REQUIRE(iters > 0, SACMI_EVALUE, "iters must be > 0");
     std::vector<double> acc;
@@ -1989,6 +2242,7 @@ int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_o
                         float* us_out, double* flops_out, double* bytes_out, int32_t max_sites,
                         int32_t* n_sites) {
   return guard([&] {
+    mb_flush(c);
     check_device_batch(c, batch);
     REQUIRE(reps > 0 && reps <= 1000, SACMI_EVALUE, "reps must be in [1, 1000]");
     // enumerate the sites of the fused single-GPU update without launching anything
@@ -2151,6 +2405,7 @@ int sacmi_profile_timeline(sacmi_ctx* c, int32_t batch, int32_t n_updates, int32
                            double* start_us, double* end_us, double* flops_out, double* bytes_out,
                            int32_t* n_kernels, double* graph_us) {
   return guard([&] {
+    mb_flush(c);
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
     // the same update sequence sacmi_step_many_async replays
@@ -2164,6 +2419,7 @@ int sacmi_profile_timeline_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates, in
                               double* start_us, double* end_us, double* flops_out, double* bytes_out,
                               int32_t* n_kernels, double* graph_us) {
   return guard([&] {
+    mb_flush(c);
     REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
@@ -2253,35 +2509,34 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     const int S = c->S, A = c->A, H = c->H, Kx = c->Kx, Hd = c->Hd;
     // env-rate calls (n <= kActPinned) go through pinned staging: no pageable-copy syncs
     const bool pinned = n <= kActPinned;
-    float* h_in = c->act_host;
-    float* h_eps = c->act_host + (size_t)kActPinned * S;
+    float* h_in = c->act_host;                          // [kActPinned][Kx]
+    float* h_eps = c->act_host + (size_t)kActPinned * Kx;
     float* h_out = h_eps + (size_t)kActPinned * A;
     const float* src = states;
     const float* esrc = eps;
     if (pinned) {
-      std::memcpy(h_in, states, (size_t)n * S * 4);
+      for (int i = 0; i < n; ++i) std::memcpy(h_in + (size_t)i * Kx, states + (size_t)i * S, (size_t)S * 4);
       src = h_in;
       if (eps && !deterministic) {
         std::memcpy(h_eps, eps, (size_t)n * A * 4);
         esrc = h_eps;
       }
     }
-    // zero-copy (default for env-rate calls): the first kernel reads the states from the
-    // mapped staging and the heads kernel writes the actions back into it
+    // zero-copy (default for env-rate calls): fc1 reads the states from the mapped staging
+    // (its A operand, the ones column in place) and the heads kernel writes the actions back
     static const bool zc_env = std::getenv("SACMI_ACT_ZEROCOPY") == nullptr ||
                                std::getenv("SACMI_ACT_ZEROCOPY")[0] != '0';
     const bool zc = pinned && zc_env && c->act_host_dev;
-    if (zc)
-      launch_rows_in(c->x2.p, Kx, c->act_host_dev, S, n, S, s);
-    else {
-      CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, src, (size_t)S * 4, (size_t)S * 4, n,
+    if (!zc) {
+      CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, src, (size_t)(pinned ? Kx : S) * 4, (size_t)S * 4, n,
                                  hipMemcpyHostToDevice, s));
       launch_set_column(c->x2.p, n, Kx, S, 1.f, s);   // (a bf16-activation update may have
     }                                                   //  overwritten the fp32 ones column)
     if (eps && !deterministic)
       CHECK_HIP(hipMemcpyAsync(c->eps.p, esrc, (size_t)n * A * 4, hipMemcpyHostToDevice, s));
     Level l1;
-    l1.add(gd(c->x2.p, Kx, 1, c->P.p + c->p_fc[0].off, c->p_fc[0].ld, 1, c->hp[0].p, Hd, n, H, S + 1, EPI_RELU));
+    l1.add(gd(zc ? c->act_host_dev : c->x2.p, Kx, 1, c->P.p + c->p_fc[0].off, c->p_fc[0].ld, 1, c->hp[0].p, Hd,
+              n, H, S + 1, EPI_RELU));
     l1.b.bf16 = c->bf16;
     launch_gemm(l1.b, s);
     for (int l = 1; l < c->nh; ++l) {
@@ -2300,6 +2555,14 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     hs.deterministic = deterministic ? 1 : 0;
     hs.ctr_override = (1ull << 63) | (++c->act_calls);   // disjoint from update noise
     if (zc) hs.act_host = c->act_host_dev + (h_out - c->act_host);
+    // one heads workgroup: the host polls its done word instead of the stream's completion
+    static const bool poll = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
+    const bool poll_done = poll && zc && n <= heads_rows_per_wg(n);
+    volatile int* done_host = reinterpret_cast<volatile int*>(c->act_nan_host + 1);
+    if (poll_done) {
+      hs.done_word = c->act_nan_dev + 1;
+      hs.done_value = ++c->act_seq;
+    }
     // Normal(mean, std) validation of policy.sample (networks_model1.py:87; evaluate=True
     // takes tanh(mean) without one): a plain store into host-mapped memory
     *c->act_nan_host = 0;
@@ -2309,7 +2572,20 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     if (!zc)
       CHECK_HIP(hipMemcpy2DAsync(pinned ? h_out : a_out, (size_t)A * 4, c->x2.p + S + 1, (size_t)Kx * 4,
                                  (size_t)A * 4, n, hipMemcpyDeviceToHost, s));
-    CHECK_HIP(hipStreamSynchronize(s));
+    bool done = false;
+    if (poll_done) {
+      for (int it = 1;; ++it) {
+        if (*done_host == hs.done_value) { done = true; break; }
+        if ((it & 1023) == 0) {   // finished without the store (or failed): the sync reports
+          const hipError_t q = hipStreamQuery(s);
+          if (q != hipErrorNotReady) break;
+          (void)hipGetLastError();
+        }
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (!done) CHECK_HIP(hipStreamSynchronize(s));
+    c->done_epoch = c->epoch;
     if (!deterministic && *reinterpret_cast<volatile int*>(c->act_nan_host))
       throw Error{SACMI_ENAN, "Expected parameters loc / scale (Tensor of shape (" + std::to_string(n) + ", " +
                                   std::to_string(A) + ")) of distribution Normal to satisfy the constraints "

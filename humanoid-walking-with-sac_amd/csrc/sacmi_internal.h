@@ -202,6 +202,8 @@ struct DevScalars {
   int32_t alpha_is_tensor;
   int32_t err;          // ErrBits (0: no non-finite input seen)
   int64_t loss_ring_pos;
+  int32_t done_seq;     // fused updates finished (their last level's block 0 counts them)
+  int32_t pad1;
 };
 
 enum Epi { EPI_STORE = 0, EPI_RELU = 1, EPI_MASK = 2,
@@ -286,6 +288,8 @@ struct AdamFuse {
   float* loss_ring; int ring;
   float* loss_host;      // or null: the losses also stored to host-mapped memory (sync step);
                          //   block 0 stores sc->err's bits into word 3
+  int* done_word;        // or null (host-mapped): the update's last level, after everything
+                         //   else block 0 stores: sc->done_seq, incremented (sacmi_step's wait)
   int err_skip;          // ErrBits that void this level's stores (critic: kErrSkipAll,
   int err_nopolyak;      //   actor: every bit); ... that void only its Polyak stores (ACT)
   unsigned short* Ph;    // bf16 mode: bf16 shadows of the parameter / target arenas, kept
@@ -414,6 +418,10 @@ struct HeadSampleArgs {
   // device scalars (update), by a plain store on host-mapped memory (select_action)
   int* nan_flag;
   int nan_bit_lo, nan_bit_hi, nan_plain;
+  // or null (host-mapped; a one-workgroup launch only): done_value stored after every other
+  // store of the workgroup, behind a system-scope fence (sacmi_act polls it)
+  int* done_word;
+  int done_value;
   tl_word* tl;
 };
 
@@ -446,9 +454,6 @@ void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
 inline int heads_rows_per_wg(int rows) { return SACMI_HEADS_TM32 && rows >= 8192 ? 32 : 16; }
 // dst[i] = bf16(src[i]) (round to nearest even), the parameter shadows of bf16 mode
 void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_t s);
-// rows [n][cols] from host-mapped memory (select_action's states) into a device matrix
-// n rows of `cols` floats (row stride lds) into dst (row stride ldd), plus 1.0 at column cols
-void launch_rows_in(float* dst, int ldd, const float* src, int lds, int n, int cols, hipStream_t s);
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s);
 // the same sample backward + dhp2 tail from the dL/da partials of the dha1 level
 // (GemmDesc::pa_out): dL/da = sum over the n_pa column blocks, fixed order
@@ -485,7 +490,21 @@ void launch_adam(const AdamArgs& a, hipStream_t s);
 
 void launch_gather(const GatherArgs& a, hipStream_t s);
 
-void launch_mt_sample(const MtSampleArgs& a, hipStream_t s);
+// Rows sacmi_push left in host-mapped staging for the next synchronous update (the
+// trainer's row per env step): that update's sampler kernel scatters them into the ring
+// before it draws, instead of a scatter launch of their own ahead of the update
+struct PushMailbox {      // host-mapped header; rows [n][2S + A + 2] (s | a | r | s2 | d) follow
+  int32_t n, pad;
+  int64_t pos0, len, head;  // ring slot of row 0; the replay's len / deque head after them
+};
+struct MailboxArgs {
+  const PushMailbox* hdr;   // null: no mailbox
+  const float* rows;
+  float *obs, *obs2, *act, *rew, *done;
+  int S, A, ldo, ldact;
+  int64_t cap;
+};
+void launch_mt_sample(const MtSampleArgs& a, hipStream_t s, const MailboxArgs* mb = nullptr);
 
 // Transition ingest (replay_buffer.py:10-11 push, batched): one host->device copy of n
 // packed rows [s n*S | a n*A | r n | s2 n*S | d n] (from a pinned staging slot), scattered

@@ -68,6 +68,7 @@ _PROTOS = {
     "sacmi_set_scalar": [c_vp, ctypes.c_int, ctypes.c_double],
     "sacmi_get_scalar": [c_vp, ctypes.c_int, c_f64p],
     "sacmi_push": [c_vp, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p, ctypes.c_int64],
+    "sacmi_push_packed": [c_vp, c_vp, ctypes.c_int64],
     "sacmi_len": [c_vp, c_i64p],
     "sacmi_replay_clear": [c_vp],
     "sacmi_get_rows": [c_vp, c_i64p, ctypes.c_int64, c_f32p, c_f32p, c_f32p, c_f32p, c_u8p],
@@ -78,6 +79,8 @@ _PROTOS = {
     "sacmi_sample_indices": [c_vp, ctypes.c_int32, c_i64p],
     "sacmi_step": [c_vp, ctypes.c_int32, c_i64p, c_f32p, c_f32p, c_f32p],
     "sacmi_step_async": [c_vp, ctypes.c_int32],
+    "sacmi_step_launch": [c_vp, ctypes.c_int32],
+    "sacmi_step_wait": [c_vp, c_f32p],
     "sacmi_step_many_async": [c_vp, ctypes.c_int32, ctypes.c_int32],
     "sacmi_step_phase_ex": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_int32,
                             ctypes.c_int32, ctypes.c_int32],

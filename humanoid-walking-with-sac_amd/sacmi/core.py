@@ -163,6 +163,13 @@ class Context:
         d = np.ascontiguousarray(np.asarray(d).astype(bool), np.uint8).reshape(n)
         L.call("sacmi_push", self._h, L.fptr(s), L.fptr(a), L.fptr(r), L.fptr(s2), L.u8ptr(d), n)
 
+    def push_packed(self, rows: np.ndarray, n: int) -> None:
+        """n packed rows (float32 [>= n][2S + A + 2]: s | a | r | s2 | d), copy-in."""
+        S, A = self.cfg.state_dim, self.cfg.action_dim
+        assert rows.dtype == np.float32 and rows.flags.c_contiguous and rows.shape[-1] == 2 * S + A + 2
+        assert rows.size >= n * (2 * S + A + 2)
+        L.call("sacmi_push_packed", self._h, rows.ctypes.data, int(n))
+
     def __len__(self) -> int:
         n = ctypes.c_int64()
         L.call("sacmi_len", self._h, ctypes.byref(n))
@@ -219,6 +226,16 @@ class Context:
         out = np.zeros(3, np.float32) if want_losses else None
         L.call("sacmi_step", self._h, int(batch), L.i64ptr(idx_a), L.fptr(e1), L.fptr(e2),
                L.fptr(out))
+        return out
+
+    def step_launch(self, batch: int) -> None:
+        """First half of step(batch) (device indices + noise): enqueue and return."""
+        L.call("sacmi_step_launch", self._h, int(batch))
+
+    def step_wait(self) -> np.ndarray:
+        """Second half: wait for the launched update; its losses (ValueError on ENAN)."""
+        out = np.zeros(3, np.float32)
+        L.call("sacmi_step_wait", self._h, L.fptr(out))
         return out
 
     def step_async(self, batch: int) -> None:
@@ -374,6 +391,14 @@ class Context:
         S, A = self.cfg.state_dim, self.cfg.action_dim
         s = np.ascontiguousarray(states, np.float32).reshape(-1, S)
         n = s.shape[0]
+        if n == 1 and eps is None:     # the env-rate call: reused buffers and pointers
+            if getattr(self, "_act1", None) is None:
+                bufs = (np.empty(S, np.float32), np.empty((1, A), np.float32))
+                self._act1 = bufs + (L.fptr(bufs[0]), L.fptr(bufs[1]))
+            bi, bo, pi, po = self._act1
+            bi[...] = s[0]
+            L.call("sacmi_act", self._h, pi, 1, int(bool(deterministic)), None, po)
+            return bo.copy()
         e = None if eps is None else np.ascontiguousarray(eps, np.float32).reshape(n, A)
         out = np.empty((n, A), np.float32)
         L.call("sacmi_act", self._h, L.fptr(s), n, int(bool(deterministic)), L.fptr(e), L.fptr(out))

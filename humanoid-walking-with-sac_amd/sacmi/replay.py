@@ -33,6 +33,7 @@ class _Staged:
         self._ctx = ctx
         self._replay = replay
         self._rows = []            # pending (s, a, r, s2, d)
+        self._pack = None          # packed staging for sacmi_push_packed
 
     # -- device binding ------------------------------------------------------------
     def _ensure_ctx(self, s, a):
@@ -52,16 +53,19 @@ class _Staged:
         ctx = self._ctx
         S, A = ctx.cfg.state_dim, ctx.cfg.action_dim
         n = len(self._rows)
-        s = np.empty((n, S), np.float32); s2 = np.empty((n, S), np.float32)
-        a = np.empty((n, A), np.float32); r = np.empty(n, np.float32); d = np.empty(n, np.uint8)
+        # packed rows s | a | r | s2 | d in a reused buffer (sacmi_push_packed)
+        w = 2 * S + A + 2
+        if self._pack is None or self._pack.shape[0] < n:
+            self._pack = np.empty((max(n, _STAGE), w), np.float32)
+        p = self._pack
         for i, (si, ai, ri, s2i, di) in enumerate(self._rows):
-            s[i] = np.asarray(si, np.float32).reshape(S)
-            a[i] = np.asarray(ai, np.float32).reshape(A)
-            r[i] = np.float32(ri)
-            s2[i] = np.asarray(s2i, np.float32).reshape(S)
-            d[i] = bool(di)
+            p[i, :S] = np.asarray(si, np.float32).reshape(S)
+            p[i, S:S + A] = np.asarray(ai, np.float32).reshape(A)
+            p[i, S + A] = ri
+            p[i, S + A + 1:w - 1] = np.asarray(s2i, np.float32).reshape(S)
+            p[i, w - 1] = 1.0 if di else 0.0
         self._rows.clear()
-        ctx.push(s, a, r, s2, d)
+        ctx.push_packed(p, n)
 
     def push(self, state, action, reward, next_state, done):
         self._ensure_ctx(state, action)

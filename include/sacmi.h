@@ -140,6 +140,10 @@ int sacmi_get_scalar(sacmi_ctx* ctx, int which, double* value);
  * new rows get max(priorities) (or 1.0 when empty), replay_buffer.py:36-46. */
 int sacmi_push(sacmi_ctx* ctx, const float* s, const float* a, const float* r,
                const float* s2, const uint8_t* d, int64_t n);
+/* The same from packed rows [n][2S + A + 2] f32: s | a | r | s2 | d (d: 0 or 1).  Up to
+ * 16 rows a chunk are read by the scatter kernel straight from mapped staging (the
+ * trainer's row per env step: no copy command ahead of the next update). */
+int sacmi_push_packed(sacmi_ctx* ctx, const float* rows, int64_t n);
 int sacmi_len(sacmi_ctx* ctx, int64_t* n);
 /* Empty the replay: the assignment `replay_buffer.buffer = rows` of checkpoint loading
  * (sac_imp.py:229-230) replaces the contents, so the rows pushed next start a fresh deque.
@@ -189,6 +193,14 @@ int sacmi_step(sacmi_ctx* ctx, int32_t batch, const int64_t* idx, const float* e
  * The device records it and every later update of the stream takes no step (a
  * multi-update launch stops where the reference's loop raised).  sacmi_step (with
  * losses_out), sacmi_fetch_losses, sacmi_per_sample and sacmi_act report it and forget it. */
+/* sacmi_step(ctx, batch, NULL, NULL, NULL, losses_out) in two halves: the launch
+ * (device indices + device noise; returns at once) and the wait (synchronises, writes the
+ * losses, reports SACMI_ENAN like sacmi_step).  Between them the caller's thread is free
+ * — the drop-in advances Python's `random` there by the reference's own random.sample
+ * (sac_imp.py:75 -> replay_memory.py sample) while the GPU runs the update.  Every launch
+ * is followed by exactly one wait; nothing else may be called on the context between. */
+int sacmi_step_launch(sacmi_ctx* ctx, int32_t batch);
+int sacmi_step_wait(sacmi_ctx* ctx, float* losses_out);
 /* Same work, enqueued only (no host sync, no host writes); losses stay on device
  * in a ring of `ring` slots, fetched by sacmi_fetch_losses. */
 int sacmi_step_async(sacmi_ctx* ctx, int32_t batch);

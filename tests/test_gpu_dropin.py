@@ -16,7 +16,8 @@ S, A, H = 24, 4, 64
 def _agent(**kw):
     from sac_imp import SAC
     torch.manual_seed(0)
-    return SAC(S, A, hidden_dim=H, device="cuda", capacity=5000, max_batch=256, **kw)
+    kw.setdefault("capacity", 5000)
+    return SAC(S, A, hidden_dim=H, device="cuda", max_batch=256, **kw)
 
 
 def _fill(agent, n, seed=0):
@@ -292,3 +293,74 @@ def test_select_action_stochastic_vs_oracle():
                                      torch.from_numpy(eps).double(), 0.4, 0.0)
         np.testing.assert_allclose(got, want.numpy(), rtol=1e-5, atol=1e-6, err_msg=f"n={n}")
     ctx.close()
+
+
+def test_push_paths_store_identical_rows():
+    """sacmi_push_packed (the drop-in's staged rows: mapped staging read by the scatter
+    kernel for chunks of <= 16 rows, the copy path beyond) and sacmi_push store the same
+    rows with the same deque(maxlen) positions — single rows, small and large chunks, across
+    the ring's wrap (replay_memory.py push / deque semantics)."""
+    from collections import deque
+
+    from sacmi import Config, Context
+    cap = 700
+    ref = deque(maxlen=cap)
+    rng = np.random.default_rng(5)
+    ctx = Context(Config(S, A, hidden_dim=16, max_batch=64, capacity=cap), 0)
+    w = 2 * S + A + 2
+    for n, packed in [(1, True), (300, False), (5, True), (1, True), (40, True), (16, True),
+                      (17, True), (250, False), (1, True), (123, True)]:
+        s = rng.standard_normal((n, S)).astype(np.float32)
+        a = rng.standard_normal((n, A)).astype(np.float32)
+        r = rng.standard_normal(n).astype(np.float32)
+        s2 = rng.standard_normal((n, S)).astype(np.float32)
+        d = rng.random(n) < 0.3
+        if packed:
+            p = np.concatenate([s, a, r[:, None], s2, d[:, None].astype(np.float32)], axis=1)
+            assert p.shape == (n, w)
+            ctx.push_packed(np.ascontiguousarray(p), n)
+        else:
+            ctx.push(s, a, r, s2, d)
+        for i in range(n):
+            ref.append((s[i], a[i], r[i], s2[i], d[i]))
+    assert len(ctx) == len(ref) == cap
+    got = ctx.get_rows(np.arange(cap, dtype=np.int64))
+    for k, col in enumerate(zip(*ref)):
+        want = np.stack(col).astype(np.float32).reshape(got[k].shape)
+        assert np.array_equal(got[k], want), k
+
+
+def test_push_mailbox_updates_match_scatter_path():
+    """The trainer's row per env step waits in the push mailbox and is stored by the next
+    synchronous update's sampler kernel (sacmi.hip PushMailbox): the same updates as when
+    every row goes through the scatter kernel first (here forced by a replay read before
+    each update), bit for bit — across the ring's wrap (deque(maxlen)), with done flags,
+    and with two rows between updates."""
+    agents = []
+    for _ in range(2):
+        a = _agent(capacity=400)
+        _fill(a, 380, seed=9)
+        agents.append(a)
+    rng = np.random.default_rng(10)
+    for t in range(40):
+        rows = [(rng.standard_normal(S), rng.uniform(-0.4, 0.4, A).astype(np.float32),
+                 float(rng.standard_normal()), rng.standard_normal(S), bool(rng.random() < 0.2))
+                for _ in range(1 if t % 5 else 2)]
+        losses = []
+        for k, a in enumerate(agents):
+            for row in rows:
+                a.replay_buffer.push(*row)
+            if k == 1:                                   # the scatter path
+                a.replay_buffer._flush()
+                a._ctx.get_rows(np.zeros(1, np.int64))
+            losses.append(a.update_parameters(64))
+        assert losses[0] == losses[1], t
+    for n in ("policy", "q1", "q2", "q1_target", "q2_target"):
+        sa, sb = agents[0]._ctx.get_net(n), agents[1]._ctx.get_net(n)
+        for k in sa:
+            assert np.array_equal(sa[k], sb[k]), (n, k)
+    n = len(agents[0].replay_buffer)
+    ra = agents[0]._ctx.get_rows(np.arange(n, dtype=np.int64))
+    rb = agents[1]._ctx.get_rows(np.arange(n, dtype=np.int64))
+    for x, y in zip(ra, rb):
+        assert np.array_equal(x, y)

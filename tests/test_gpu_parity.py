@@ -679,23 +679,51 @@ BF16_EMU_GRAD_TOL = 2e-2   # per-tensor normwise, vs that emulation (rounding fl
 BF16_TRUTH_GRAD_TOL = 0.15  # vs the exact fp64 oracle (cosine >= ~0.99)
 
 
-@pytest.mark.parametrize("n_hidden,B", [(2, 256), (3, 256), (2, 4096), (3, 4096)])
-def test_bf16_compute_vs_emulation(n_hidden, B):
-    """compute_dtype bf16 (BASELINE configs[4]): bf16 MFMA operands, fp32 accumulation,
-    fp32 master weights / Adam / losses.  No reference counterpart: checked against the
-    fp64 oracle with the same operands rounded to bf16 where the HIP path rounds them
-    (oracle/sac_step.py _EmuLinear) — the deviation from exact arithmetic is bf16's own
-    (fc1 dW ~7 %: strong cancellation over the batch), the kernel's extra error is
-    accumulation-order level."""
-    cfg = SacConfig(376, 17, 512, n_hidden=n_hidden)
+def _check_bf16_update(cfg, lb, gb, emu, exact, l_emu):
+    """One bf16 update against the fp64 oracle with the HIP path's bf16 operand roundings
+    (emu, after its step) and the exact fp64 oracle (exact, after its step)."""
+    g_emu = emu.grads_flat()
+    g64 = exact.grads_flat()
+    for i, k in enumerate(("q1_loss", "q2_loss", "policy_loss")):
+        assert abs(lb[i] - l_emu[k]) <= BF16_EMU_LOSS_TOL * max(abs(l_emu[k]), 1e-2), (k, lb[i], l_emu[k])
+    keys = [k for k in g64 if k != "log_alpha"]
+    e_emu = {k: rel(gb[k], g_emu[k]) for k in keys}
+    e_true = {k: rel(gb[k], g64[k]) for k in keys}
+    print("bf16 grad error vs emulation", {k: f"{e:.2e}" for k, e in e_emu.items()})
+    print("bf16 grad error vs exact", {k: f"{e:.2e}" for k, e in e_true.items()})
+    assert max(e_emu.values()) <= BF16_EMU_GRAD_TOL, e_emu
+    # where bf16 moves a gradient most, the emulation accounts for most of the move
+    worst = max(keys, key=lambda k: e_true[k])
+    assert e_emu[worst] <= 0.25 * e_true[worst], (worst, e_emu[worst], e_true[worst])
+    assert max(e_true.values()) <= BF16_TRUTH_GRAD_TOL, e_true
+    # the bf16 operands really were used: the fp32 path is ~1e-6 from the truth
+    assert max(e_true.values()) > 1e-3, e_true
+
+
+@pytest.mark.parametrize("S,A,n_hidden,B", [(376, 17, 2, 256), (376, 17, 3, 256), (376, 17, 2, 4096),
+                                           (376, 17, 3, 4096), (661, 23, 2, 4096)])
+def test_bf16_compute_vs_emulation(S, A, n_hidden, B):
+    """compute_dtype bf16 (BASELINE configs[4]; (661, 23, 512, B=4096): configs[4]'s own
+    NAO shapes): bf16 MFMA operands, fp32 accumulation, fp32 master weights / Adam / losses.
+    No reference counterpart: checked against the fp64 oracle with the same operands
+    rounded to bf16 where the HIP path rounds them (oracle/sac_step.py _EmuLinear) — the
+    deviation from exact arithmetic is bf16's own (fc1 dW ~7 %: strong cancellation over the
+    batch), the kernel's extra error is accumulation-order level.  A second update is held
+    to the same bars on oracles re-anchored on the GPU's state after the first
+    (oracle_from_ctx: Adam past its first step, alpha = exp(log_alpha), sac_imp.py:135)."""
+    cfg = SacConfig(S, A, 512, n_hidden=n_hidden)
     params = init_params(cfg, 71, bias_scale=0.02)
     rows = synthetic_rows(cfg, max(2000, B + 1000), 72, state_scale=0.1)
     rng = np.random.default_rng(73)
-    idx = rng.choice(len(rows[2]), B, replace=False)
-    e1 = rng.standard_normal((B, cfg.action_dim)).astype(np.float32)
-    e2 = rng.standard_normal((B, cfg.action_dim)).astype(np.float32)
+    draws = []
+    for _ in range(2):
+        draws.append((rng.choice(len(rows[2]), B, replace=False),
+                      rng.standard_normal((B, cfg.action_dim)).astype(np.float32),
+                      rng.standard_normal((B, cfg.action_dim)).astype(np.float32)))
+    idx, e1, e2 = draws[0]
     res = {}
     act16 = None
+    ctx_b = None
     for dt in ("fp32", "bf16"):
         ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]), compute_dtype=dt)
         load_params(ctx, params)
@@ -712,30 +740,32 @@ def test_bf16_compute_vs_emulation(n_hidden, B):
             assert ctx.get_scalar(which) == 1.0, (dt, which)
         la = ctx.get_scalar(L.S_LOG_ALPHA)
         assert abs(ctx.get_scalar(L.S_ALPHA) - np.exp(np.float32(la))) <= 1e-6
-        ctx.close()
+        if dt == "bf16":
+            ctx_b = ctx
+        else:
+            ctx.close()
     batch = [x[idx] for x in rows]
     emu = OracleSAC(cfg, params, torch.float64)
     l_emu = emu.step(*batch, e1, e2, bf16_operands=True, bf16_act=act16)
-    g_emu = emu.grads_flat()
     exact = OracleSAC(cfg, params, torch.float64)
     exact.step(*batch, e1, e2)
-    g64 = exact.grads_flat()
     lb, gb = res["bf16"]
-    for i, k in enumerate(("q1_loss", "q2_loss", "policy_loss")):
-        assert abs(lb[i] - l_emu[k]) <= BF16_EMU_LOSS_TOL * max(abs(l_emu[k]), 1e-2), (k, lb[i], l_emu[k])
-    keys = [k for k in g64 if k != "log_alpha"]
-    e_emu = {k: rel(gb[k], g_emu[k]) for k in keys}
-    e_true = {k: rel(gb[k], g64[k]) for k in keys}
-    print("bf16 grad error vs emulation", {k: f"{e:.2e}" for k, e in e_emu.items()})
-    print("bf16 grad error vs exact", {k: f"{e:.2e}" for k, e in e_true.items()})
-    assert max(e_emu.values()) <= BF16_EMU_GRAD_TOL, e_emu
-    # where bf16 moves a gradient most, the emulation accounts for most of the move
-    worst = max(keys, key=lambda k: e_true[k])
-    assert e_emu[worst] <= 0.25 * e_true[worst], (worst, e_emu[worst], e_true[worst])
-    assert max(e_true.values()) <= BF16_TRUTH_GRAD_TOL, e_true
-    # the bf16 operands really were used: the fp32 path is ~1e-6 from the truth
-    assert max(e_true.values()) > 1e-3, e_true
+    _check_bf16_update(cfg, lb, gb, emu, exact, l_emu)
     assert not np.array_equal(res["fp32"][0], lb)
+    # update 2 on re-anchored oracles
+    emu2 = oracle_from_ctx(ctx_b, cfg, torch.float64)
+    exact2 = oracle_from_ctx(ctx_b, cfg, torch.float64)
+    assert abs(float(emu2.alpha.reshape(-1)[0]) - float(np.exp(np.float32(ctx_b.get_scalar(L.S_LOG_ALPHA))))) <= 1e-6
+    idx, e1, e2 = draws[1]
+    lb2 = ctx_b.step(B, idx=idx, eps1=e1, eps2=e2)
+    gb2 = ctx_grads(ctx_b, cfg)
+    batch = [x[idx] for x in rows]
+    l_emu2 = emu2.step(*batch, e1, e2, bf16_operands=True, bf16_act=act16)
+    exact2.step(*batch, e1, e2)
+    _check_bf16_update(cfg, lb2, gb2, emu2, exact2, l_emu2)
+    for which in (L.S_STEP_POLICY, L.S_STEP_Q1, L.S_STEP_Q2, L.S_STEP_ALPHA):
+        assert ctx_b.get_scalar(which) == 2.0, which
+    ctx_b.close()
 
 
 @pytest.mark.parametrize("n_hidden", [2, 3])
