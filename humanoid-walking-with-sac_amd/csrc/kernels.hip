@@ -2890,6 +2890,67 @@ __global__ void k_to_bf16(unsigned short* dst, const float* src, int64_t n) {
     dst[i] = bf16_bits(src[i]);
 }
 
+// ---------------------------------------------------------------------------
+// select_action for one state (sacmi_act, n = 1): a 32-row level tile uses one of its rows,
+// ~5-6 us a level at M = 1; here a wave per output, its lanes over K (16-byte loads of the
+// weight row and of x), a fixed butterfly, 16 outputs a workgroup
+__device__ __forceinline__ float gemv_dot(const float* x, const float* w, int K) {
+  const int lane = threadIdx.x & 63;
+  float acc = 0.f;
+  for (int k = 4 * lane; k < K; k += 256) {
+    const float4 wv = *reinterpret_cast<const float4*>(w + k);
+    const float4 xv = *reinterpret_cast<const float4*>(x + k);
+    acc = fmaf(wv.x, xv.x, acc); acc = fmaf(wv.y, xv.y, acc);
+    acc = fmaf(wv.z, xv.z, acc); acc = fmaf(wv.w, xv.w, acc);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  return acc;
+}
+
+__global__ __launch_bounds__(1024) void k_act_gemv(GemvArgs a) {
+  const int n = blockIdx.x * 16 + (threadIdx.x >> 6);
+  if (n >= a.N) return;
+  const float v = gemv_dot(a.x, a.W + (size_t)n * a.ldw, a.K);
+  if ((threadIdx.x & 63) == 0) a.y[n] = a.relu ? (v <= 0.f ? 0.f : v) : v;   // F.relu keeps NaN
+}
+
+void launch_act_gemv(const GemvArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_act_gemv, dim3((a.N + 15) / 16), dim3(1024), 0, s, a);
+  HIP_LAUNCH_CHECK();
+}
+
+// heads + GaussianPolicy.sample of one row (k_heads_sample's per-element algebra,
+// networks_model1.py:65-99): 2A dot products over 16 waves, then thread j < A
+__global__ __launch_bounds__(1024) void k_act_heads(ActHeadsArgs a) {
+  __shared__ float s_h[64];
+  const int wave = threadIdx.x >> 6, A = a.A;
+  for (int o = wave; o < 2 * A; o += 16) {
+    const float v = gemv_dot(a.x, a.Wh + (size_t)o * a.ldw, a.K);
+    if ((threadIdx.x & 63) == 0) s_h[o] = v;
+  }
+  __syncthreads();
+  const int j = threadIdx.x;
+  if (j < A) {
+    const float mean = s_h[j], ls_raw = s_h[A + j];
+    const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
+    const float sd = expf(ls);
+    if (!a.deterministic && (__builtin_isnan(mean) || __builtin_isnan(ls_raw))) *a.nan_flag = 1;
+    const float eps = a.deterministic ? 0.f : a.gen_eps ? philox_normal(a.seed, a.ctr, (uint32_t)j) : a.eps[j];
+    const float x = a.deterministic ? mean : mean + eps * sd;
+    a.out[j] = tanhf(x) * a.scale + a.bias;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) *reinterpret_cast<volatile int*>(a.done_word) = a.done_value;
+}
+
+void launch_act_heads(const ActHeadsArgs& a, hipStream_t s) {
+  if (a.A > 32) throw Error{SACMI_EVALUE, "heads: action_dim > 32"};
+  hipLaunchKernelGGL(k_act_heads, dim3(1), dim3(1024), 0, s, a);
+  HIP_LAUNCH_CHECK();
+}
+
 void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);

@@ -30,6 +30,15 @@ namespace sacmi {
 __device__ int64_t mailbox_scatter(const MailboxArgs& mb, DevScalars* sc) {
   __shared__ int s_n;
   __shared__ int64_t s_hdr[3];
+  const int S = mb.S, A = mb.A, rowf = 2 * S + A + 2;
+  // row 0 (the trainer's one row) is read together with the header: one PCIe round trip
+  constexpr int kR0 = 2;
+  float r0[kR0];
+#pragma unroll
+  for (int q = 0; q < kR0; ++q) {
+    const int e = threadIdx.x + q * blockDim.x;
+    r0[q] = e < rowf ? mb.rows[e] : 0.f;
+  }
   if (threadIdx.x == 0) {
     const volatile PushMailbox* h = mb.hdr;
     s_n = h->n;
@@ -38,11 +47,11 @@ __device__ int64_t mailbox_scatter(const MailboxArgs& mb, DevScalars* sc) {
   __syncthreads();
   const int n = s_n;
   if (n <= 0) return -1;
-  const int S = mb.S, A = mb.A, rowf = 2 * S + A + 2;
   for (int e = threadIdx.x; e < n * rowf; e += blockDim.x) {
     const int j = e / rowf, c = e - j * rowf;
     const int64_t w = (s_hdr[0] + j) % mb.cap;
-    const float v = mb.rows[e];
+    const int q = (e - (int)threadIdx.x) / (int)blockDim.x;
+    const float v = e < rowf && q < kR0 ? r0[q < kR0 ? q : 0] : mb.rows[e];
     if (c < S) mb.obs[w * mb.ldo + c] = v;
     else if (c < S + A) mb.act[w * mb.ldact + c - S] = v;
     else if (c == S + A) mb.rew[w] = v;

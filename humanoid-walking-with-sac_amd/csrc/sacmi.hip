@@ -142,6 +142,7 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> dq, dhead, dhc[3], dha[3], dhp[3];
   sacmi::DevBuf<float> dotp;       // fc3 dot partials [6 slots][B][nparts]
   sacmi::DevBuf<float> pa;         // dL/da partials [2 * nparts][B][A] (L9 epilogue -> tail)
+  sacmi::DevBuf<float> act_h;      // select_action's one-state hidden rows [nh][Hd] (1 at H)
   int pending_step = 0;             // batch of a sacmi_step_launch not yet waited for
   bool inflight = false;            // updates enqueued since the last full wait
   int pending_done = -1;            // the done word before that launch (step_finish)
@@ -346,6 +347,7 @@ static void alloc_all(sacmi_ctx* c) {
     c->dhp[l].alloc((size_t)Bm * H);
   }
   c->eps.alloc((size_t)2 * Bm * A);
+  c->act_h.alloc((size_t)nh * c->Hd);
   c->cache.alloc((size_t)2 * Bm * 3 * A);
   c->logp.alloc((size_t)2 * Bm);
   c->dq.alloc((size_t)2 * Bm + 16);   // + slack: the split-K dW kernels read 4 wide (kernels.hip)
@@ -366,6 +368,7 @@ static void alloc_all(sacmi_ctx* c) {
   launch_set_column(c->x2b.p, 2 * Bm, c->Kx, S, 1.f, s);
   for (int l = 0; l < nh; ++l) {
     launch_set_column(c->hp[l].p, 2 * Bm, c->Hd, H, 1.f, s);
+    launch_set_column(c->act_h.p + (size_t)l * c->Hd, 1, c->Hd, H, 1.f, s);
     for (auto* b : {&c->hq[l], &c->hqt[l], &c->hqa[l]}) {
       launch_set_column(b->p, Bm, 2 * c->Hd, H, 1.f, s);
       launch_set_column(b->p, Bm, 2 * c->Hd, c->Hd + H, 1.f, s);
@@ -1487,7 +1490,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
                     &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->xqb, &c->x2b, &c->rb,
                     &c->db, &c->eps,
-                    &c->cache, &c->logp, &c->dq, &c->dotp, &c->pa, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
+                    &c->cache, &c->logp, &c->dq, &c->dotp, &c->pa, &c->act_h, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
                     &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr, &c->per_probs,
                     &c->per_chunk, &c->per_w, &c->per_val})
       b->release();
@@ -2532,6 +2535,55 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
                                  hipMemcpyHostToDevice, s));
       launch_set_column(c->x2.p, n, Kx, S, 1.f, s);   // (a bf16-activation update may have
     }                                                   //  overwritten the fp32 ones column)
+    // one state (the env-rate call): the policy forward as GEMVs (k_act_gemv / k_act_heads:
+    // a wave per output instead of 32-row level tiles that use one row), fp32, from the
+    // mapped staging, the action back into it, the host polling the heads' done word
+    static const bool gemv_env = std::getenv("SACMI_NO_ACT_GEMV") == nullptr;
+    static const bool poll1 = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
+    if (zc && n == 1 && gemv_env && poll1 && A <= 32) {
+      const float* x = c->act_host_dev;
+      int K = S + 1, ldw = c->p_fc[0].ld;
+      const float* Wl = c->P.p + c->p_fc[0].off;
+      for (int l = 0; l < c->nh; ++l) {
+        GemvArgs g{x, Wl, ldw, K, H, c->act_h.p + (size_t)l * Hd, 1};
+        launch_act_gemv(g, s);
+        x = g.y; K = H + 1; ldw = Hd;
+        if (l + 1 < c->nh) Wl = c->P.p + c->p_fc[l + 1].off;
+      }
+      ActHeadsArgs ha{};
+      ha.x = x; ha.Wh = c->P.p + c->p_head.off; ha.ldw = Hd; ha.K = H + 1; ha.A = A;
+      ha.deterministic = deterministic ? 1 : 0; ha.gen_eps = eps ? 0 : 1;
+      ha.eps = c->act_host_dev + (h_eps - c->act_host);
+      ha.seed = c->cfg.seed; ha.ctr = (1ull << 63) | (++c->act_calls);   // disjoint from update noise
+      ha.scale = (float)((c->cfg.action_high - c->cfg.action_low) / 2);
+      ha.bias = (float)((c->cfg.action_high + c->cfg.action_low) / 2);
+      ha.out = c->act_host_dev + (h_out - c->act_host);
+      *c->act_nan_host = 0;
+      ha.nan_flag = c->act_nan_dev;
+      ha.done_word = c->act_nan_dev + 1;
+      ha.done_value = ++c->act_seq;
+      launch_act_heads(ha, s);
+      volatile int* done_host = reinterpret_cast<volatile int*>(c->act_nan_host + 1);
+      bool done = false;
+      for (int it = 1;; ++it) {
+        if (*done_host == ha.done_value) { done = true; break; }
+        if ((it & 1023) == 0) {   // finished without the store (or failed): the sync reports
+          const hipError_t q = hipStreamQuery(s);
+          if (q != hipErrorNotReady) break;
+          (void)hipGetLastError();
+        }
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+      if (!done) CHECK_HIP(hipStreamSynchronize(s));
+      c->done_epoch = c->epoch;
+      if (!deterministic && *reinterpret_cast<volatile int*>(c->act_nan_host))
+        throw Error{SACMI_ENAN, "Expected parameters loc / scale (Tensor of shape (1, " + std::to_string(A) +
+                                    ")) of distribution Normal to satisfy the constraints Real() / "
+                                    "GreaterThan(lower_bound=0.0), but found invalid values (NaN) in "
+                                    "policy.sample(state) (select_action, sac_imp.py:70)"};
+      std::memcpy(a_out, h_out, (size_t)A * 4);
+      return;
+    }
     if (eps && !deterministic)
       CHECK_HIP(hipMemcpyAsync(c->eps.p, esrc, (size_t)n * A * 4, hipMemcpyHostToDevice, s));
     Level l1;

@@ -447,6 +447,33 @@ struct SampleBwdArgs {
 // launchers (kernels.hip)
 void launch_gemm(const GemmBatch& batch, hipStream_t s);
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
+
+// select_action for one state (sacmi_act, n = 1): the policy forward as GEMVs.
+// y[n] = relu?(sum_{k < K} x[k] W[n * ldw + k]) (K counts the bias: x[K - 1] = 1); x and W
+// are read 4-wide up to round4(K) (zeros past K in both: padded rows).
+struct GemvArgs {
+  const float* x;
+  const float* W;
+  int ldw, K, N;
+  float* y;
+  int relu;
+};
+void launch_act_gemv(const GemvArgs& a, hipStream_t s);
+// ... and its heads (mean | log_std rows of Wh over x) + GaussianPolicy.sample for the row
+struct ActHeadsArgs {
+  const float* x;
+  const float* Wh;
+  int ldw, K, A;
+  int deterministic, gen_eps;
+  const float* eps;       // [A] (gen_eps == 0, not deterministic)
+  uint64_t seed, ctr;
+  float scale, bias;
+  float* out;             // [A] actions (host-mapped)
+  int* nan_flag;          // plain store of 1 (host-mapped)
+  int* done_word;         // done_value stored last (host-mapped)
+  int done_value;
+};
+void launch_act_heads(const ActHeadsArgs& a, hipStream_t s);
 // rows per heads workgroup (and per log-prob partial): 32 from 8192 stacked rows on
 #ifndef SACMI_HEADS_TM32
 #define SACMI_HEADS_TM32 1

@@ -174,6 +174,7 @@ class SAC:
                                           sync_python_random=sync_python_random)
         st = random.getstate()             # device sampling stream starts at `random`'s
         self._ctx.set_mt(0, np.array(st[1][:624], np.uint32), st[1][624])
+        self._mt_adopted = st[1]           # (the Python stream state the device holds)
 
     # -- mirrored attributes ---------------------------------------------------------
     def _flush_device(self):
@@ -232,7 +233,23 @@ class SAC:
             raise ValueError("Sample larger than population or is negative")
         rb = self.replay_buffer
         self._stale = True     # (also when it raises: the critic step may have been taken)
-        if rb.sync_python_random:
+        if rb.sync_python_random and batch_size <= 4096 and self._ctx.cfg.replay == "uniform":
+            st = random.getstate()
+            if st[1] != self._mt_adopted:   # the stream moved (drawn from, seeded): adopt it
+                self._ctx.set_mt(0, np.array(st[1][:624], np.uint32), st[1][624])
+            self._ctx.step_launch(batch_size)
+            try:
+                # while the GPU runs the update, the reference's own random.sample
+                # (sac_imp.py:75) advances Python's stream: its draws depend only on the
+                # population size and k, and the device drew the same indices from the
+                # same state (test_sync_python_random_consumes_like_reference)
+                random.sample(range(len(rb)), batch_size)
+            finally:           # (the sample ran even if the update raises)
+                try:
+                    out = self._ctx.step_wait()
+                finally:
+                    self._mt_adopted = random.getstate()[1]
+        elif rb.sync_python_random:
             st = random.getstate()
             self._ctx.set_mt(0, np.array(st[1][:624], np.uint32), st[1][624])
             try:

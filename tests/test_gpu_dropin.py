@@ -84,6 +84,28 @@ def test_sync_python_random_consumes_like_reference():
     sample_indices(mt, 2000, 256)
     assert random.getstate() == mt.to_pystate()
 
+    def device_state():
+        key, pos = agent._ctx.get_mt(0)
+        return tuple(int(x) for x in key) + (pos,)
+    # the device sampler drew from the same state as Python's random.sample (the drop-in
+    # runs the latter on the host while the GPU runs the update): the streams stay equal
+    # through pushes, batch sizes on both sample branches, and the caller drawing from
+    # `random` between updates (adopted by the next update)
+    assert device_state() == random.getstate()[1]
+    rng = np.random.default_rng(4)
+    for t in range(6):
+        agent.replay_buffer.push(rng.standard_normal(S), rng.uniform(-0.4, 0.4, A).astype(np.float32),
+                                 0.5, rng.standard_normal(S), False)
+        if t == 3:
+            random.random()
+        b = (256, 64, 8)[t % 3]
+        pre = random.getstate()
+        agent.update_parameters(b)
+        mt = MT19937.from_pystate(pre)
+        sample_indices(mt, len(agent.replay_buffer), b)
+        assert random.getstate() == mt.to_pystate(), t
+        assert device_state() == random.getstate()[1], t
+
 
 def test_checkpoint_roundtrip(tmp_path):
     agent = _agent()
