@@ -16,6 +16,7 @@
 #include "replay_dev.h"
 
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -541,40 +542,83 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // log_alpha step (alpha = exp(log_alpha), sac_imp.py:128-135) and the loss ring slot —
 // none of them after a non-finite sample (the reference raised first; err: ErrBits this
 // update saw) — and the error bits for the synchronous step's host-mapped readback.
+// Scalar loads through a buffer descriptor (s_buffer_load): counted by lgkmcnt, so their
+// wait never includes the vector stores the workgroup has in flight (vmcnt retires loads and
+// stores in order: a vector load issued behind the fused-Adam epilogue's write-through
+// stores waits for their acknowledgements, ~2 us).  Only for data an earlier kernel wrote
+// (the scalar cache is invalidated at every kernel start, and this kernel has not stored it).
+typedef int sbuf_i4 __attribute__((ext_vector_type(4)));
+__device__ int llvm_s_buffer_load_i32(sbuf_i4 rsrc, int off, int aux) __asm("llvm.amdgcn.s.buffer.load.i32");
+__device__ __forceinline__ sbuf_i4 s_rsrc(const void* p) {
+  const uint64_t a = (uint64_t)p;
+  return sbuf_i4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffffu), 0x7fffffff, kBufDword3};
+}
+__device__ __forceinline__ uint32_t s_ld(sbuf_i4 r, uint32_t byte_off) {
+  return (uint32_t)llvm_s_buffer_load_i32(r, (int)byte_off, 0);
+}
+
 __device__ __forceinline__ void adam_block0(const AdamFuse& af, int err, float omb1, float omb2) {
-  {
-    __syncthreads();
-    if (threadIdx.x == 0 && af.loss_host) af.loss_host[3] = __int_as_float(err);
-    if (threadIdx.x < af.n_losses && !err) {
-      float sum = 0.f;
-      for (int w = 0; w < af.n_part; ++w) sum += af.loss_part[w * af.n_losses + threadIdx.x];
-      af.sc->losses[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
-      if (af.loss_host) af.loss_host[af.loss_slot0 + threadIdx.x] = sum / af.loss_div;
+  __syncthreads();
+  // wave 0 only, on wave-uniform values read by scalar loads (s_ld): the block's tail used
+  // to wait behind its own epilogue stores and then walk a chain of dependent round trips
+  // (loss partials; log_alpha's state and bias corrections; the ring position; done_seq) —
+  // 2.5-4 us past the other workgroups of the Adam levels (phase stamps).  Every value read
+  // here was written by an earlier level.
+  if (threadIdx.x >= 64) return;
+  const sbuf_i4 rLp = s_rsrc(af.loss_part), rSc = s_rsrc(af.sc);
+  const bool alpha = af.log_alpha_idx >= 0 && af.auto_entropy;
+  const uint32_t ao = (uint32_t)(alpha ? af.log_alpha_idx : 0) * 4u;
+  float pp = __uint_as_float(s_ld(s_rsrc(af.P), ao)), mm = __uint_as_float(s_ld(s_rsrc(af.M), ao));
+  float vv = __uint_as_float(s_ld(s_rsrc(af.V), ao));
+  const float ga = __uint_as_float(s_ld(s_rsrc(alpha ? af.log_alpha_grad : af.P), 0u));   // (used only with alpha)
+  auto s_ld64 = [&](size_t off) {
+    return (uint64_t)s_ld(rSc, (uint32_t)off) | ((uint64_t)s_ld(rSc, (uint32_t)off + 4u) << 32);
+  };
+  double bp1 = __longlong_as_double((long long)s_ld64(offsetof(DevScalars, beta_pow) + 3 * 16));
+  double bp2 = __longlong_as_double((long long)s_ld64(offsetof(DevScalars, beta_pow) + 3 * 16 + 8));
+  const int64_t pos = (int64_t)s_ld64(offsetof(DevScalars, loss_ring_pos));
+  float l_prev[3];
+#pragma unroll
+  for (int sl = 0; sl < 3; ++sl)
+    l_prev[sl] = __uint_as_float(s_ld(rSc, (uint32_t)(offsetof(DevScalars, losses) + 4 * sl)));
+  const int dseq = (int)s_ld(rSc, (uint32_t)offsetof(DevScalars, done_seq));
+  const bool lane0 = threadIdx.x == 0;
+  if (lane0 && af.loss_host) af.loss_host[3] = __int_as_float(err);
+  // the level's losses: partials summed in block order (as k_adam does)
+  float loss[2] = {0.f, 0.f};
+#pragma unroll
+  for (int l = 0; l < 2; ++l) {
+    if (l >= af.n_losses) break;
+    float sum = 0.f;
+    for (int w = 0; w < af.n_part; ++w) sum += __uint_as_float(s_ld(rLp, (uint32_t)(w * af.n_losses + l) * 4u));
+    loss[l] = sum / af.loss_div;
+    if (lane0 && !err) {
+      af.sc->losses[af.loss_slot0 + l] = loss[l];
+      if (af.loss_host) af.loss_host[af.loss_slot0 + l] = loss[l];
     }
-    if (threadIdx.x == 0 && af.log_alpha_idx >= 0 && af.auto_entropy && !err) {
-      const AdamScalars k = fuse_scalars(af, 3, af.step_offset);
-      const int64_t i = af.log_alpha_idx;
-      float pp = af.P[i], mm = af.M[i], vv = af.V[i];
-      adam_elem(pp, mm, vv, *af.log_alpha_grad, omb1, af.beta2, omb2, af.eps, k);
-      af.P[i] = pp; af.M[i] = mm; af.V[i] = vv;
-      af.sc->alpha = expf(pp);
-      af.sc->alpha_is_tensor = 1;
+  }
+  if (lane0 && alpha && !err) {
+    if (af.step_offset) { bp1 *= (double)af.beta1; bp2 *= (double)af.beta2; }
+    const AdamScalars k{(float)((double)af.lr / (1.0 - bp1)), (float)sqrt(1.0 - bp2)};
+    adam_elem(pp, mm, vv, ga, omb1, af.beta2, omb2, af.eps, k);
+    af.P[af.log_alpha_idx] = pp; af.M[af.log_alpha_idx] = mm; af.V[af.log_alpha_idx] = vv;
+    af.sc->alpha = expf(pp);
+    af.sc->alpha_is_tensor = 1;
+  }
+  if (lane0 && af.loss_ring && !err) {
+    const int64_t q = pos % af.ring;
+#pragma unroll
+    for (int sl = 0; sl < 3; ++sl) {
+      const int src = sl - af.loss_slot0;
+      af.loss_ring[q * 3 + sl] = src == 0 ? loss[0] : src == 1 && af.n_losses > 1 ? loss[1] : l_prev[sl];
     }
-    __syncthreads();
-    if (threadIdx.x == 0 && af.loss_ring && !err) {
-      const int64_t pos = af.sc->loss_ring_pos;
-      const int64_t q = pos % af.ring;
-      af.loss_ring[q * 3 + 0] = af.sc->losses[0];
-      af.loss_ring[q * 3 + 1] = af.sc->losses[1];
-      af.loss_ring[q * 3 + 2] = af.sc->losses[2];
-      af.sc->loss_ring_pos = pos + 1;
-    }
-    if (threadIdx.x == 0 && af.done_word) {   // (voided updates too: the host waits on it)
-      const int v = af.sc->done_seq + 1;
-      af.sc->done_seq = v;
-      __threadfence_system();                  // the losses and error bits land first
-      *reinterpret_cast<volatile int*>(af.done_word) = v;
-    }
+    af.sc->loss_ring_pos = pos + 1;
+  }
+  if (lane0 && af.done_word) {   // (voided updates too: the host waits on it)
+    const int v = dseq + 1;
+    af.sc->done_seq = v;
+    __threadfence_system();                  // the losses and error bits land first
+    *reinterpret_cast<volatile int*>(af.done_word) = v;
   }
 }
 
@@ -838,6 +882,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   for (int q = 0; q < kMaxGemms; ++q) asm volatile("" :: "s"(tbeg[q]));
   const TlMark tl_mark(tl, TL_GEMM);
   SACMI_PHASE(tl, 0);
+  SACMI_PHASE_LAST(tl, 6);
   constexpr int TMW = TM * MG;
   __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
   __shared__ float rsum[MG * KSPLIT * TM];
@@ -1041,6 +1086,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   SACMI_PHASE(batch.tl, 1);
   gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   SACMI_PHASE(batch.tl, 2);
+  SACMI_PHASE_LAST(batch.tl, 7);
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
   if constexpr (PA) {
     if (has_pa) {
@@ -1818,8 +1864,11 @@ constexpr int kDwFinEpt = SACMI_DWFIN_EPT;
 #endif
 
 // workspace layout: partial s of desc p at ws + s * ws_stride + desc_off[p], row-major
-// [M][ncols] with ncols = N (+1 for the row-sum column)
-__device__ __forceinline__ int dw_ncols(const GemmDesc& d) { return d.rs_col >= 0 ? d.N + 1 : d.N; }
+// [M][ncols] with ncols = N (+1 for the row-sum column) rounded up to a multiple of 4: every
+// partial row starts 16-byte aligned, so k_dw_fin moves 4-column groups (the pad columns are
+// never written and never used)
+__host__ __device__ __forceinline__ int dw_ncols_real(const GemmDesc& d) { return d.rs_col >= 0 ? d.N + 1 : d.N; }
+__host__ __device__ __forceinline__ int dw_ncols(const GemmDesc& d) { return (dw_ncols_real(d) + 3) & ~3; }
 
 // XCD placement of the split-K work (workgroup b runs on XCD b % 8): the split-major work
 // list w = split * tiles + tile is dealt to the XCDs in contiguous eighths, so each XCD's
@@ -2386,74 +2435,101 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
   // a non-finite policy sample / PER draw of this update (ErrBits, see k_gemm)
   const bool void_st = (s_err & af.err_skip) != 0;
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
-  // kDwFinEpt elements per thread (element e = block base + k * 256 + thread: coalesced),
-  // the workgroups dealt to the descs in order: every workgroup belongs to one desc, and
-  // every load of a thread's elements (partials, parameter, moments, target) is issued
-  // before any use — one round trip, and all of the level's threads resident at once
+  // kDwFinEpt 4-column groups per thread (group g = block base + k * 256 + thread: 16-byte
+  // loads and stores of the partials and of the optimizer state, coalesced), the workgroups
+  // dealt to the descs in order: every workgroup belongs to one desc, and every load of a
+  // thread's groups (partials, parameter, moments, target) is issued before any use — one
+  // round trip, and all of the level's threads resident at once
   int q = -1, bstart = 0, acc = 0;
   int64_t off = 0;
   for (int qq = 0; qq < batch.count; ++qq) {
     const int n_el_q = batch.d[qq].M * dw_ncols(batch.d[qq]);
-    const int nb = (n_el_q + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
+    const int nb = (n_el_q / 4 + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
     if (q < 0 && (int)blockIdx.x < acc + nb) { q = qq; bstart = acc; }
     if (q < 0) off += n_el_q;
     acc += nb;
   }
   if (q >= 0 && !void_st) {
     const GemmDesc& d = batch.d[q];
-    const int nc = dw_ncols(d);
-    const int n_el = d.M * nc;                  // < 2^31 (checked by dw_split_plan)
+    const int nc = dw_ncols(d), ncr = dw_ncols_real(d), gpr = nc / 4;
+    const int n_gr = d.M * gpr;                 // 4-column groups (n_el < 2^31: dw_split_plan)
     const bool pol = d.epi == EPI_ADAM_POLYAK;
     const bool pol_st = pol && (s_err & af.err_nopolyak) == 0;
     const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
     const float* wsd = batch.ws + off;
     const bool wt = batch.st_wt != 0;            // write-through parameter / state stores
     const uint32_t oob = 0xfffffff0u;
-    const rsrc_t rWs = make_rsrc(wsd, (uint32_t)(((int64_t)(ns - 1) * ws_stride + n_el) * 4));
-    const rsrc_t rTg = make_rsrc(adam && pol ? af.T : wsd, adam && pol ? 0x7fffffffu : 0u);
+    const rsrc_t rWs = make_rsrc(wsd, (uint32_t)(((int64_t)(ns - 1) * ws_stride + (int64_t)n_gr * 4) * 4));
+    const rsrc_t rTg = make_rsrc(adam && pol ? af.T + abase - af.t_base : wsd, adam && pol ? 0x7fffffffu : 0u);
     const rsrc_t rC = make_rsrc(d.C, 0x7fffffffu);
-    const rsrc_t rM = make_rsrc(adam ? af.M : d.C, adam ? 0x7fffffffu : 0u);
-    const rsrc_t rV = make_rsrc(adam ? af.V : d.C, adam ? 0x7fffffffu : 0u);
-    int e[kDwFinEpt];
-    int64_t o[kDwFinEpt];
-    float t[kDwFinEpt][NSL], pp[kDwFinEpt], mm[kDwFinEpt], vv[kDwFinEpt], tt[kDwFinEpt];
+    const rsrc_t rM = make_rsrc(adam ? af.M + abase : d.C, adam ? 0x7fffffffu : 0u);
+    const rsrc_t rV = make_rsrc(adam ? af.V + abase : d.C, adam ? 0x7fffffffu : 0u);
+    const rsrc_t rG = make_rsrc(adam && af.G ? af.G + abase : d.C, adam && af.G ? 0x7fffffffu : 0u);
+    const rsrc_t rT = make_rsrc(adam && pol ? af.T + abase - af.t_base : d.C, adam && pol ? 0x7fffffffu : 0u);
+    int g[kDwFinEpt], c4[kDwFinEpt];
+    uint32_t o[kDwFinEpt];
+    float4 t[kDwFinEpt][NSL], pp[kDwFinEpt], mm[kDwFinEpt], vv[kDwFinEpt], tt[kDwFinEpt];
 #pragma unroll
     for (int k = 0; k < kDwFinEpt; ++k) {
-      e[k] = (blockIdx.x - bstart) * (256 * kDwFinEpt) + k * 256 + threadIdx.x;
-      const bool live = e[k] < n_el;
-      const int row = e[k] / nc, col = e[k] - row * nc;
-      const int n = col < d.N ? col : d.rs_col;
-      o[k] = (int64_t)row * d.ldc + n;
+      g[k] = (blockIdx.x - bstart) * (256 * kDwFinEpt) + k * 256 + threadIdx.x;
+      const bool live = g[k] < n_gr;
+      const int row = g[k] / gpr;
+      c4[k] = (g[k] - row * gpr) * 4;
+      o[k] = (uint32_t)(row * d.ldc + c4[k]) * 4u;
       // all partial loads in flight at once (offsets past NS / past the desc return 0, no
       // access): no guard, so nothing drains the load queue between them
 #pragma unroll
-      for (int s = 0; s < NSL; ++s)
-        t[k][s] = buf_ld(rWs, live && s < ns ? (uint32_t)((int64_t)s * ws_stride + e[k]) * 4u : oob);
-      pp[k] = buf_ld(rC, adam && live ? (uint32_t)o[k] * 4u : oob);
-      mm[k] = buf_ld(rM, live ? (uint32_t)(abase + o[k]) * 4u : oob);
-      vv[k] = buf_ld(rV, live ? (uint32_t)(abase + o[k]) * 4u : oob);
-      tt[k] = buf_ld(rTg, pol && live ? (uint32_t)(abase - af.t_base + o[k]) * 4u : oob);
+      for (int sp = 0; sp < NSL; ++sp)
+        t[k][sp] = buf_ld4(rWs, live && sp < ns ? (uint32_t)((int64_t)sp * ws_stride + (int64_t)g[k] * 4) * 4u : oob);
+      pp[k] = buf_ld4(rC, adam && live ? o[k] : oob);
+      mm[k] = buf_ld4(rM, live ? o[k] : oob);
+      vv[k] = buf_ld4(rV, live ? o[k] : oob);
+      tt[k] = buf_ld4(rTg, pol && live ? o[k] : oob);
     }
 #pragma unroll
     for (int k = 0; k < kDwFinEpt; ++k) {
-      if (e[k] >= n_el) continue;
-      float v = t[k][0];
+      if (g[k] >= n_gr) continue;
+      // the partial sums in split order; a column past the output (the pad of the last
+      // group of a row) takes gradient 0: Adam / Polyak leave its zero parameter, moments
+      // and target exactly 0, and the 16-byte stores rewrite them
+      float v[4] = {t[k][0].x, t[k][0].y, t[k][0].z, t[k][0].w};
 #pragma unroll
-      for (int s = 1; s < NSL; ++s)
-        if (s < ns) v += t[k][s];
+      for (int sp = 1; sp < NSL; ++sp)
+        if (sp < ns) {
+#pragma clang fp contract(off)
+          v[0] += t[k][sp].x; v[1] += t[k][sp].y; v[2] += t[k][sp].z; v[3] += t[k][sp].w;
+        }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = c4[k] + j < ncr ? v[j] : 0.f;
+      auto st4 = [&](rsrc_t r, float a0, float a1, float a2, float a3) {
+        if (wt) buf_st4<kStAux>(r, o[k], f4{a0, a1, a2, a3});
+        else buf_st4<0>(r, o[k], f4{a0, a1, a2, a3});
+      };
       if (adam) {
-        adam_elem(pp[k], mm[k], vv[k], v, omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
-        if (af.G) st_pol(af.G + abase + o[k], v, wt);
-        st_pol(d.C + o[k], pp[k], wt); st_pol(af.M + abase + o[k], mm[k], wt);
-        st_pol(af.V + abase + o[k], vv[k], wt);
-        if (af.Ph) st_pol(af.Ph + abase + o[k], (unsigned short)bf16_bits(pp[k]), wt);
+        float p4[4] = {pp[k].x, pp[k].y, pp[k].z, pp[k].w}, m4[4] = {mm[k].x, mm[k].y, mm[k].z, mm[k].w};
+        float v4[4] = {vv[k].x, vv[k].y, vv[k].z, vv[k].w}, t4[4] = {tt[k].x, tt[k].y, tt[k].z, tt[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          adam_elem(p4[j], m4[j], v4[j], v[j], omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
+          t4[j] = polyak(t4[j], p4[j], omtau, af.tau);
+        }
+        if (af.G) st4(rG, v[0], v[1], v[2], v[3]);
+        st4(rC, p4[0], p4[1], p4[2], p4[3]);
+        st4(rM, m4[0], m4[1], m4[2], m4[3]);
+        st4(rV, v4[0], v4[1], v4[2], v4[3]);
+        auto st_bf4 = [&](unsigned short* h, const float (&x)[4]) {   // 4 bf16 shadows, 8 bytes
+          const uint32_t lo = (uint32_t)bf16_bits(x[0]) | ((uint32_t)bf16_bits(x[1]) << 16);
+          const uint32_t hi = (uint32_t)bf16_bits(x[2]) | ((uint32_t)bf16_bits(x[3]) << 16);
+          if (wt) st_wt8(h, 0u, lo, hi);
+          else *reinterpret_cast<uint2*>(h) = make_uint2(lo, hi);
+        };
+        if (af.Ph) st_bf4(af.Ph + abase + o[k] / 4u, p4);
         if (pol_st) {
-          const float tn = polyak(tt[k], pp[k], omtau, af.tau);
-          st_pol(af.T + abase - af.t_base + o[k], tn, wt);
-          if (af.Th) st_pol(af.Th + abase - af.t_base + o[k], (unsigned short)bf16_bits(tn), wt);
+          st4(rT, t4[0], t4[1], t4[2], t4[3]);
+          if (af.Th) st_bf4(af.Th + abase - af.t_base + o[k] / 4u, t4);
         }
       } else {
-        st_pol(d.C + o[k], v, wt);
+        st4(rC, v[0], v[1], v[2], v[3]);
       }
     }
   }
@@ -2479,11 +2555,19 @@ static int dw_split_plan(GemmBatch& b, int64_t* stride) {
     GemmDesc& d = b.d[i];
     if (d.a_kc || d.b_kc || d.axk || d.K < 2048) return 0;
     if (d.epi != EPI_STORE && d.epi < EPI_ADAM) return 0;
+    // k_dw_fin's 4-column groups: the row-sum column is the bias column right after the
+    // last output column, and output rows (and their Adam state) are 16-byte aligned with
+    // room for a whole last group
+    if ((d.rs_col >= 0 && d.rs_col != d.N) || (d.ldc & 3) || ((uintptr_t)d.C & 15) ||
+        d.ldc < dw_ncols(d))
+      return 0;
+    if (d.epi >= EPI_ADAM && (((d.C - b.adam.P) & 3) || (b.adam.T && ((d.C - b.adam.P - b.adam.t_base) & 3))))
+      return 0;
     d.tiles_m = (d.M + kDBM - 1) / kDBM;
     d.tiles_n = (d.N + kDBN - 1) / kDBN;
     d.tile_begin = tiles;
     tiles += d.tiles_m * d.tiles_n;
-    el += (int64_t)d.M * (d.rs_col >= 0 ? d.N + 1 : d.N);
+    el += (int64_t)d.M * dw_ncols(d);
   }
   b.total_tiles = tiles;
   if (el >= (1LL << 31)) return 0;
@@ -2565,9 +2649,9 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       HIP_LAUNCH_CHECK();
-      int fin_grid = 0;                    // k_dw_fin: kDwFinEpt elements per thread, per desc
+      int fin_grid = 0;                    // k_dw_fin: kDwFinEpt 4-column groups per thread, per desc
       for (int i = 0; i < b.count; ++i)
-        fin_grid += (b.d[i].M * (b.d[i].rs_col >= 0 ? b.d[i].N + 1 : b.d[i].N) + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
+        fin_grid += (b.d[i].M * (dw_ncols(b.d[i]) / 4) + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
       if (b.tl) b.tl += kTlWords;          // the second kernel of the level
       const dim3 fg(fin_grid), fb(256);
       // the fin's stores: plain (SACMI_FIN_WT=1: write-through, measured slower at config 5:

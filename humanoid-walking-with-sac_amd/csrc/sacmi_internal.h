@@ -143,10 +143,13 @@ struct TlMark {
     }
   }
   __device__ __forceinline__ ~TlMark() {
-    // wave 0 of each of the last kTlEndSlots workgroups at its exit, one slot each (the 64
-    // lanes store one scalar to one address: one store)
-    if (p && blockIdx.x + kTlEndSlots >= gridDim.x && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)
-      p[kTlEnd + (blockIdx.x & (kTlEndSlots - 1))] = ~(tl_word)wall_clock64();
+    // wave 0 of EVERY workgroup at its exit folds ~clock into slot (block & 255) by a
+    // non-returning atomic min (the host takes the latest over the slots): the kernel's end
+    // is the last workgroup to retire, whatever its index — the highest-numbered (last
+    // dispatched) workgroups alone can retire early, e.g. a grid-stride epilogue's empty
+    // tail.  grid / 256 workgroups share a slot, at different times: no contention to speak of
+    if (p && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)
+      atomicMin(p + kTlEnd + (blockIdx.x & (kTlEndSlots - 1)), ~(tl_word)wall_clock64());
   }
 };
 
@@ -156,8 +159,17 @@ struct TlMark {
     if ((tl) && blockIdx.x < 256 && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)          \
       (tl)[kTlPhase0 + blockIdx.x * kTlPhases + (k)] = (tl_word)wall_clock64();                 \
   } while (0)
+// the same clock taken by the workgroup's LAST wave (slots 6 / 7: its entry and the end of
+// its K loop): the dispatch skew between a workgroup's first and last waves
+#define SACMI_PHASE_LAST(tl, k)                                                                 \
+  do {                                                                                         \
+    if ((tl) && blockIdx.x < 256 &&                                                            \
+        __builtin_amdgcn_readfirstlane(threadIdx.x) >= blockDim.x - 64u)                       \
+      (tl)[kTlPhase0 + blockIdx.x * kTlPhases + (k)] = (tl_word)wall_clock64();                 \
+  } while (0)
 #else
 #define SACMI_PHASE(tl, k) do { } while (0)
+#define SACMI_PHASE_LAST(tl, k) do { } while (0)
 #endif
 
 // One bias-folded linear layer inside an arena.

@@ -2,7 +2,8 @@
 """Per-phase medians of the GEMM levels from a diagnostic timeline dump (SACMI_DIAG_DUMP,
 a -DSACMI_DIAG_PHASES build).  k_gemm phases (wave 0 of the first 256 workgroups):
 0 entry, 1 setup done (before the K loop), 2 wave 0's K loop + MFMAs done, 3 every wave
-done (the pre-epilogue barrier; incl. the row prologue), 4 epilogue stores issued, 5 exit.
+done (the pre-epilogue barrier; incl. the row prologue), 4 epilogue stores issued, 5 exit;
+6 / 7 the last wave's entry and K-loop end (lastin: its entry after wave 0's).
 usage: tools/phase_dump.py dump.bin"""
 import struct
 import sys
@@ -42,6 +43,9 @@ def main(path):
             "wg": np.median(ph[:, 5] - ph[:, 0]) * 0.01,
             "wgmax": np.max(ph[:, 5] - ph[:, 0]) * 0.01,
         }
+        if nph >= 8 and np.all(ph[:, 6] > 0):   # the last wave's entry / K-loop end
+            d["lastin"] = np.median(ph[:, 6] - ph[:, 0]) * 0.01
+            d["lastcore"] = np.median(ph[:, 7] - ph[:, 6]) * 0.01
         acc.setdefault(names[s], []).append(d)
         if SLOW:   # the slowest workgroups of this site's first launch, phase by phase
             bids = np.nonzero(live)[0]
@@ -50,10 +54,10 @@ def main(path):
                 seg = np.diff(ph[r]) * 0.01
                 print(f"  slow {names[s]:28s} wg {bids[r]:4d} start {(ph[r, 0] - start) * 0.01:6.2f} "
                       f"total {tot[r] * 0.01:6.2f} phases " + " ".join(f"{v:5.2f}" for v in seg))
-    keys = ["start", "startmax", "setup", "core0", "wait", "epi", "tail", "wg", "wgmax"]
+    keys = ["start", "startmax", "setup", "core0", "wait", "epi", "tail", "wg", "wgmax", "lastin", "lastcore"]
     print(f"{'site':32s} " + " ".join(f"{k:>8s}" for k in keys))
     for n, lst in acc.items():
-        print(f"{n:32s} " + " ".join(f"{np.median([d[k] for d in lst]):8.2f}" for k in keys))
+        print(f"{n:32s} " + " ".join(f"{np.median([d.get(k, np.nan) for d in lst]):8.2f}" for k in keys))
 
 
 if __name__ == "__main__":
