@@ -110,6 +110,10 @@ __device__ __forceinline__ void mt_sample_body(const MtSampleArgs& a, int tbl_lo
   if (t == 0) s_pos = (int)a.mt[kMtN];
   __syncthreads();
   int pos = s_pos;
+  if (a.mt_save) {   // (unconditional: after a non-finite sample the state is kept, and so is this)
+    for (int i = t; i < kMtN; i += blockDim.x) a.mt_save[i] = key[i];
+    if (t == 0) a.mt_save[kMtN] = (uint32_t)pos;
+  }
 
   if (n64 <= (int64_t)a.setsize) {
     // ---- pool branch: sequential partial Fisher-Yates (random.py:492-499)

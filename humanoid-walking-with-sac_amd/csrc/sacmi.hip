@@ -146,6 +146,19 @@ struct sacmi_ctx {
   int pending_step = 0;             // batch of a sacmi_step_launch not yet waited for
   bool inflight = false;            // updates enqueued since the last full wait
   int pending_done = -1;            // the done word before that launch (step_finish)
+  // The next single update's minibatch, drawn ahead: a device-sampled single update
+  // (sacmi_step / _async / _launch) also runs the NEXT update's random.sample + gather as
+  // ride-along workgroups (L12 / L13, as inside multi-update graphs) into the other batch
+  // set, saving the MT state it started from in mt_pf.  The next such update of the same
+  // batch size consumes it (no sampler / gather of its own); any other call first restores
+  // the MT state (pf_settle): the stream is then exactly as if nothing had been drawn ahead.
+  sacmi::DevBuf<uint32_t> mt_pf;    // [625]: the random stream before the draw ahead
+  bool pf_on = true;                // SACMI_NO_PREFETCH at creation: off
+  bool pf_valid = false;            // a drawn-ahead batch waits in set pf_parity
+  bool pf_save = false;             // (enqueue_update: the draw ahead saves mt_pf)
+  bool pf_touched = false;          // another call since the last single update: draw
+                                    //   nothing ahead (a push per update would drop it)
+  int pf_parity = 0, pf_B = 0;
   int act_seq = 0;                  // select_action launches (their heads' done word)
   sacmi::DevBuf<float> dw_ws;      // bf16 deep-K weight-gradient split-K partials
   int nparts = 0;
@@ -333,6 +346,8 @@ static void alloc_all(sacmi_ctx* c) {
     c->per_w.alloc(c->Bm + 2);
   }
   c->mt.alloc(2 * 625);
+  c->mt_pf.alloc(625);
+  c->pf_on = std::getenv("SACMI_NO_PREFETCH") == nullptr;
   c->per_scr.alloc(16);
   c->idx32.alloc(Bm); c->idx64.alloc(Bm); c->idx32b.alloc(Bm); c->idx64b.alloc(Bm);
   c->xq.alloc((size_t)Bm * c->Kx); c->xqb.alloc((size_t)Bm * c->Kx);
@@ -1131,6 +1146,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l12.b.ride.kind = 1; l12.b.ride.nblocks = 1;
       l12.b.ride.tbl_log2 = mt_sample_tbl_log2(B);
       l12.b.ride.mt = mt_args(c, B, nb2);
+      if (c->pf_save) l12.b.ride.mt.mt_save = c->mt_pf.p;   // (a single update's draw ahead)
       // ... and its gather in L13
       l13.b.ride.kind = 2; l13.b.ride.nblocks = 16;
       l13.b.ride.ga = gather_args(c, B, nb2, false);
@@ -1230,6 +1246,7 @@ static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use
 
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
                        float grad_scale, bool use_ring, int reps = 1, PhaseRide pr = {}) {
+  c->pf_save = false;
   if (!c->mb_graph) mb_flush(c);   // (mb_graph: this update's sampler takes them)
   c->inflight = true;
   // consecutive fused updates hand the next update's sampling + gather to ride-along
@@ -1243,6 +1260,12 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
     if (phase_mask != 7) {   // one phase of a split update
       enqueue_update(c, B, dev_idx, dev_eps, phase_mask, grad_scale, use_ring, pr.parity,
                      pr.have_batch, pr.ride_next);
+      return;
+    }
+    if (pr.ride_next || pr.have_batch) {   // one fused update drawing the next one's batch ahead
+      c->pf_save = true;
+      enqueue_update(c, B, dev_idx, dev_eps, 7, grad_scale, use_ring, pr.parity, pr.have_batch, pr.ride_next);
+      c->pf_save = false;
       return;
     }
     enqueue_many(c, B, dev_idx, dev_eps, use_ring, reps);
@@ -1417,6 +1440,22 @@ using namespace sacmi;
 // ============================================================================
 extern "C" {
 
+// A batch drawn ahead by the previous single update is dropped by any other call: the MT
+// state goes back to the save point (stream-ordered, before whatever the call enqueues), so
+// the random stream is exactly as if nothing had been drawn ahead.
+static void pf_settle(sacmi_ctx* c) {
+  if (!c || !c->pf_valid) return;
+  c->pf_valid = false;
+  CHECK_HIP(hipMemcpyAsync(c->mt.p, c->mt_pf.p, 625 * 4, hipMemcpyDeviceToDevice, c->stream));
+}
+
+// Every API call other than the single updates and the read-only queries
+static void pf_touch(sacmi_ctx* c) {
+  if (!c) return;
+  c->pf_touched = true;
+  pf_settle(c);
+}
+
 int sacmi_abi_version(void) { return SACMI_ABI_VERSION; }
 const char* sacmi_last_error(void) { return g_last_error.c_str(); }
 
@@ -1497,7 +1536,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (int l = 0; l < 3; ++l)
       for (auto* b : {&c->hp[l], &c->hq[l], &c->hqt[l], &c->hqa[l], &c->dhc[l], &c->dha[l], &c->dhp[l]})
         b->release();
-    c->sc.release(); c->mt.release(); c->mt_backup.release(); c->idx32.release(); c->idx64.release();
+    c->sc.release(); c->mt.release(); c->mt_backup.release(); c->mt_pf.release(); c->idx32.release(); c->idx64.release();
     c->Ph.release(); c->Th.release();
     c->idx32b.release(); c->idx64b.release();
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
@@ -1511,6 +1550,7 @@ int sacmi_destroy(sacmi_ctx* c) {
 
 int sacmi_set_stream(sacmi_ctx* c, void* stream) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(c, SACMI_EVALUE, "null ctx");
     CHECK_HIP(hipStreamSynchronize(c->stream));
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
@@ -1585,7 +1625,8 @@ static void tensor_io(sacmi_ctx* c, int slot, int net, int layer, int part, floa
 
 int sacmi_set_tensor(sacmi_ctx* c, int slot, int net, int layer, int part, const float* host,
                      int64_t numel) {
-  return guard([&] { tensor_io(c, slot, net, layer, part, nullptr, host, numel); });
+  return guard([&] {
+    pf_touch(c); tensor_io(c, slot, net, layer, part, nullptr, host, numel); });
 }
 
 int sacmi_get_tensor(sacmi_ctx* c, int slot, int net, int layer, int part, float* host,
@@ -1648,7 +1689,8 @@ static void scalar_io(sacmi_ctx* c, int which, const double* in, double* out) {
 }
 
 int sacmi_set_scalar(sacmi_ctx* c, int which, double value) {
-  return guard([&] { scalar_io(c, which, &value, nullptr); });
+  return guard([&] {
+    pf_touch(c); scalar_io(c, which, &value, nullptr); });
 }
 int sacmi_get_scalar(sacmi_ctx* c, int which, double* value) {
   return guard([&] { scalar_io(c, which, nullptr, value); });
@@ -1822,11 +1864,13 @@ static void push_impl(sacmi_ctx* c, const float* s, const float* a, const float*
 
 int sacmi_push(sacmi_ctx* c, const float* s, const float* a, const float* r, const float* s2,
                const uint8_t* d, int64_t n) {
-  return guard([&] { push_impl(c, s, a, r, s2, d, nullptr, n); });
+  return guard([&] {
+    pf_touch(c); push_impl(c, s, a, r, s2, d, nullptr, n); });
 }
 
 int sacmi_push_packed(sacmi_ctx* c, const float* rows, int64_t n) {
-  return guard([&] { push_impl(c, nullptr, nullptr, nullptr, nullptr, nullptr, rows, n); });
+  return guard([&] {
+    pf_touch(c); push_impl(c, nullptr, nullptr, nullptr, nullptr, nullptr, rows, n); });
 }
 
 int sacmi_len(sacmi_ctx* c, int64_t* n) {
@@ -1835,6 +1879,7 @@ int sacmi_len(sacmi_ctx* c, int64_t* n) {
 
 int sacmi_replay_clear(sacmi_ctx* c) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(c, SACMI_EVALUE, "null ctx");
     DevScalars h = download_scalars(c);
     h.len = 0;
@@ -1848,6 +1893,7 @@ int sacmi_replay_clear(sacmi_ctx* c) {
 int sacmi_get_rows(sacmi_ctx* c, const int64_t* idx, int64_t n, float* s, float* a, float* r,
                    float* s2, uint8_t* d) {
   return guard([&] {
+    pf_touch(c);
     mb_flush(c);
     CHECK_HIP(hipStreamSynchronize(c->stream));
     const int64_t head = c->len < c->capacity ? 0 : c->wpos;
@@ -1870,6 +1916,7 @@ int sacmi_get_rows(sacmi_ctx* c, const int64_t* idx, int64_t n, float* s, float*
 int sacmi_get_slots(sacmi_ctx* c, const int64_t* slots, int64_t n, float* s, float* a, float* r,
                     float* s2, uint8_t* d) {
   return guard([&] {
+    pf_touch(c);
     std::vector<int64_t> pos(n);
     const int64_t head = c->len < c->capacity ? 0 : c->wpos;
     for (int64_t i = 0; i < n; ++i) {
@@ -1883,6 +1930,7 @@ int sacmi_get_slots(sacmi_ctx* c, const int64_t* slots, int64_t n, float* s, flo
 
 int sacmi_rng_set_mt(sacmi_ctx* c, int stream, const uint32_t* key, int32_t pos) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(stream == 0 || stream == 1, SACMI_EVALUE, "stream must be 0 or 1");
     REQUIRE(pos >= 0 && pos <= 624, SACMI_EVALUE, "MT position must be in [0, 624]");
     std::vector<uint32_t> k(key, key + 624);
@@ -1894,6 +1942,7 @@ int sacmi_rng_set_mt(sacmi_ctx* c, int stream, const uint32_t* key, int32_t pos)
 
 int sacmi_rng_get_mt(sacmi_ctx* c, int stream, uint32_t* key, int32_t* pos) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(stream == 0 || stream == 1, SACMI_EVALUE, "stream must be 0 or 1");
     std::vector<uint32_t> k(625);
     CHECK_HIP(hipStreamSynchronize(c->stream));
@@ -1905,6 +1954,7 @@ int sacmi_rng_get_mt(sacmi_ctx* c, int stream, uint32_t* key, int32_t* pos) {
 
 int sacmi_rng_seed_device(sacmi_ctx* c, uint64_t seed, uint64_t offset) {
   return guard([&] {
+    pf_touch(c);
     CHECK_HIP(hipStreamSynchronize(c->stream));   // no graph holding the old key in flight
     destroy_graphs(c);                             // the key is a captured kernel argument
     c->cfg.seed = seed;
@@ -1916,6 +1966,7 @@ int sacmi_rng_seed_device(sacmi_ctx* c, uint64_t seed, uint64_t offset) {
 
 int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(batch >= 0 && batch <= c->len, SACMI_EVALUE, "Sample larger than population or is negative");
     REQUIRE(batch <= c->Bm, SACMI_EVALUE, "batch > max_batch");
     REQUIRE(batch <= 4096, SACMI_EVALUE, "device random.sample supports batch <= 4096");
@@ -1930,15 +1981,48 @@ int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
   });
 }
 
+// A device-sampled single update (sacmi_step / _async / _launch): it takes the batch drawn
+// ahead for its batch size (no sampler / gather of its own), and draws the next one ahead
+// where the ride-along fits (uniform replay, batch <= ~2k; in a graph, not under a caller's
+// capture).  Anything else first settles.
+static PhaseRide pf_begin(sacmi_ctx* c, int B, bool dev_idx) {
+  PhaseRide pr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  CHECK_HIP(hipStreamIsCapturing(c->stream, &cap));
+  const bool graphs = c->use_graphs && cap == hipStreamCaptureStatusNone;
+  // (only while single updates follow each other: the trainer's push between updates
+  // would drop every batch drawn ahead, at the price of a restore each)
+  const bool ahead = c->pf_on && dev_idx && graphs && !c->pf_touched && ride_possible(c, B);
+  const bool use = ahead && c->pf_valid && c->pf_B == B && c->mb_pending == 0;
+  if (!use) pf_settle(c);
+  c->pf_valid = false;
+  c->pf_touched = false;
+  if (!ahead) return pr;
+  pr.parity = use ? c->pf_parity : 0;
+  pr.have_batch = use;
+  pr.ride_next = true;
+  return pr;
+}
+static void pf_end(sacmi_ctx* c, int B, const PhaseRide& pr) {
+  if (!pr.ride_next) return;
+  c->pf_valid = true;
+  c->pf_parity = pr.parity ^ 1;
+  c->pf_B = B;
+}
+
 // A synchronous single update (sacmi_step / sacmi_step_launch): with device sampling the
 // update's sampler also stores the rows waiting in the push mailbox (its graph variant)
-static void run_update_mb(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool mb_ok) {
+static void run_update_mb(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool mb_ok,
+                          bool use_ring = false) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;   // (a caller's capture would
   CHECK_HIP(hipStreamIsCapturing(c->stream, &cap));          //  replay the mailbox read)
+  const PhaseRide pr = pf_begin(c, B, dev_idx != 0);
+  // (a batch drawn ahead: no push since, so no mailbox rows either)
   c->mb_graph = mb_ok && dev_idx && c->mb_pending > 0 && cap == hipStreamCaptureStatusNone &&
-                c->cfg.replay_kind == SACMI_REPLAY_UNIFORM;
+                c->cfg.replay_kind == SACMI_REPLAY_UNIFORM && !pr.have_batch;
   try {
-    run_update(c, B, dev_idx, dev_eps, 7, 1.f, false);
+    run_update(c, B, dev_idx, dev_eps, 7, 1.f, use_ring, 1, pr);
+    pf_end(c, B, pr);
   } catch (...) {
     c->mb_graph = false;
     throw;
@@ -1981,6 +2065,7 @@ static void step_finish(sacmi_ctx* c, int batch, float* losses_out, int done_pre
   std::memcpy(&err, c->loss_host + 3, 4);
   if (err) {
     clear_err(c);
+    pf_settle(c);     // (the batch drawn ahead belongs to a voided update)
     throw Error{SACMI_ENAN, nan_message(c, err, batch, " during update_parameters")};
   }
   std::memcpy(losses_out, c->loss_host, 12);    // stored by the update's last kernels
@@ -2022,12 +2107,13 @@ int sacmi_step_wait(sacmi_ctx* c, float* losses_out) {
 int sacmi_step_async(sacmi_ctx* c, int32_t batch) {
   return guard([&] {
     check_device_batch(c, batch);
-    run_update(c, batch, 1, 1, 7, 1.f, true);
+    run_update_mb(c, batch, 1, 1, false, true);
   });
 }
 
 int sacmi_step_many_async(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   return guard([&] {
+    pf_touch(c);
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
     run_update(c, batch, 1, 1, 7, 1.f, true, n_updates);
@@ -2036,6 +2122,7 @@ int sacmi_step_many_async(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
 
 int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_out) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(max_steps >= 0 && (max_steps == 0 || out), SACMI_EVALUE, "bad output buffer");
     DevScalars h = download_scalars(c);
     const int64_t avail = std::min<int64_t>(h.loss_ring_pos, c->ring_slots);
@@ -2063,6 +2150,7 @@ int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_o
 
 int sacmi_step_phase(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scale) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(phase >= 0 && phase <= 3, SACMI_EVALUE, "phase must be 0, 1, 2 or 3");
     if (phase == 0 || phase == 3) check_device_batch(c, batch);
     run_update(c, batch, 1, 1, phase == 3 ? 5 : 1 << phase, grad_scale, false);
@@ -2072,6 +2160,7 @@ int sacmi_step_phase(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scal
 int sacmi_step_phase_ex(sacmi_ctx* c, int32_t batch, int32_t phase, float grad_scale,
                         int32_t parity, int32_t have_batch, int32_t ride_next) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(phase >= 0 && phase <= 3, SACMI_EVALUE, "phase must be 0, 1, 2 or 3");
     REQUIRE(parity == 0 || parity == 1, SACMI_EVALUE, "parity must be 0 or 1");
     if (phase == 0 || phase == 3) check_device_batch(c, batch);
@@ -2098,6 +2187,7 @@ int sacmi_allreduce_unique_id(void* id_out, int32_t nbytes) {
 
 int sacmi_allreduce_init(sacmi_ctx* c, const void* id, int32_t nbytes, int32_t rank, int32_t world) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(id && nbytes == (int32_t)sizeof(ncclUniqueId), SACMI_EVALUE, "bad RCCL unique id");
     REQUIRE(world >= 1 && rank >= 0 && rank < world, SACMI_EVALUE, "bad rank / world");
     REQUIRE(!c->comm && !c->dp_loopback, SACMI_ESTATE, "communicator already initialised");
@@ -2113,6 +2203,7 @@ int sacmi_allreduce_init(sacmi_ctx* c, const void* id, int32_t nbytes, int32_t r
 
 int sacmi_dp_loopback_init(sacmi_ctx* c, int32_t world) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(c, SACMI_EVALUE, "null ctx");
     REQUIRE(world >= 1 && world <= 1024, SACMI_EVALUE, "world must be in [1, 1024]");
     REQUIRE(!c->comm, SACMI_ESTATE, "communicator already initialised");
@@ -2124,6 +2215,7 @@ int sacmi_dp_loopback_init(sacmi_ctx* c, int32_t world) {
 
 int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   return guard([&] {
+    pf_touch(c);
     mb_flush(c);
     REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
     check_device_batch(c, batch);
@@ -2157,7 +2249,8 @@ int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
 }
 
 int sacmi_step_act16(sacmi_ctx* c, int32_t batch, int32_t* out) {
-  return guard([&] { *out = act16_on(c, batch) ? 1 : 0; });
+  return guard([&] {
+    pf_touch(c); *out = act16_on(c, batch) ? 1 : 0; });
 }
 
 int sacmi_step_ride_possible(sacmi_ctx* c, int32_t batch, int32_t* out) {
@@ -2170,6 +2263,7 @@ int sacmi_grad_arena_numel(sacmi_ctx* c, int64_t* numel) {
 
 int sacmi_attach_grad_arena(sacmi_ctx* c, void* ptr, int64_t numel) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(ptr && numel == c->total, SACMI_EVALUE, "grad arena must hold exactly grad_arena_numel floats");
     REQUIRE(((uintptr_t)ptr & 15) == 0, SACMI_EVALUE, "grad arena must be 16-byte aligned");
     CHECK_HIP(hipStreamSynchronize(c->stream));
@@ -2193,6 +2287,7 @@ int sacmi_attach_grad_arena(sacmi_ctx* c, void* ptr, int64_t numel) {
 
 int sacmi_grad_buffer(sacmi_ctx* c, int which, void** ptr, int64_t* numel) {
   return guard([&] {
+    pf_touch(c);
     REQUIRE(which == 0 || which == 1, SACMI_EVALUE, "which must be 0 (critic) or 1 (actor)");
     if (which == 0) { *ptr = c->G.p + c->q_begin; *numel = c->q_end - c->q_begin; }
     else { *ptr = c->G.p + c->pi_begin; *numel = c->total - c->pi_begin; }
@@ -2202,6 +2297,7 @@ int sacmi_grad_buffer(sacmi_ctx* c, int which, void** ptr, int64_t* numel) {
 int sacmi_profile_step(sacmi_ctx* c, int32_t batch, int32_t iters, char* names_out,
                        float* ms_out, double* flops_out, int32_t max_sites, int32_t* n_sites) {
   return guard([&] {
+    pf_touch(c);
     mb_flush(c);
     check_device_batch(c, batch);
     REQUIRE(iters > 0, SACMI_EVALUE, "iters must be > 0");
@@ -2408,6 +2504,7 @@ int sacmi_profile_timeline(sacmi_ctx* c, int32_t batch, int32_t n_updates, int32
                            double* start_us, double* end_us, double* flops_out, double* bytes_out,
                            int32_t* n_kernels, double* graph_us) {
   return guard([&] {
+    pf_touch(c);
     mb_flush(c);
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
@@ -2422,6 +2519,7 @@ int sacmi_profile_timeline_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates, in
                               double* start_us, double* end_us, double* flops_out, double* bytes_out,
                               int32_t* n_kernels, double* graph_us) {
   return guard([&] {
+    pf_touch(c);
     mb_flush(c);
     REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
     check_device_batch(c, batch);
@@ -2440,6 +2538,7 @@ static void require_per(sacmi_ctx* c) {
 int sacmi_per_sample(sacmi_ctx* c, int32_t batch, const double* u, int64_t* idx_out,
                      float* weights_out) {
   return guard([&] {
+    pf_touch(c);
     require_per(c);
     REQUIRE(c->len > 0, SACMI_EVALUE, "probabilities do not sum to 1");   // empty buffer
     REQUIRE(batch >= 0 && batch <= c->Bm, SACMI_EVALUE, "batch must be in [0, max_batch]");
@@ -2467,6 +2566,7 @@ int sacmi_per_sample(sacmi_ctx* c, int32_t batch, const double* u, int64_t* idx_
 
 int sacmi_per_update(sacmi_ctx* c, const int64_t* idx, const float* values, int64_t n) {
   return guard([&] {
+    pf_touch(c);
     require_per(c);
     if (n <= 0) return;
     for (int64_t i = 0; i < n; ++i)
@@ -2485,6 +2585,7 @@ int sacmi_per_update(sacmi_ctx* c, const int64_t* idx, const float* values, int6
 
 int sacmi_per_get_priorities(sacmi_ctx* c, float* out, int64_t n) {
   return guard([&] {
+    pf_touch(c);
     require_per(c);
     REQUIRE(n >= 0 && n <= c->capacity, SACMI_EVALUE, "n > capacity");
     CHECK_HIP(hipStreamSynchronize(c->stream));
@@ -2494,6 +2595,7 @@ int sacmi_per_get_priorities(sacmi_ctx* c, float* out, int64_t n) {
 
 int sacmi_per_set_priorities(sacmi_ctx* c, const float* in, int64_t n) {
   return guard([&] {
+    pf_touch(c);
     require_per(c);
     REQUIRE(n >= 0 && n <= c->capacity, SACMI_EVALUE, "n > capacity");
     CHECK_HIP(hipStreamSynchronize(c->stream));

@@ -105,11 +105,12 @@ inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // ---------------------------------------------------------------------------
 // Launch timeline (sacmi_profile_timeline).  In an instrumented update graph every kernel
 // launch owns kTlWords words {start, -, kind, grid, ~end[256]}: the first 8 workgroups fold
-// their entry clock into `start` (atomicMin), and each of the last 256 workgroups (the last
-// round over the CUs) stores its exit clock, complemented, into a slot of its own — no
-// contended word, so the stamps cost the kernel's tail nothing (atomics of every workgroup
-// on per-XCD words added ~0.4 us per kernel) — on the 100 MHz s_memrealtime clock; the
-// buffer starts at all-ones and the host takes the latest stored slot as the kernel's end.
+// their entry clock into `start` (atomicMin), and every workgroup folds its exit clock,
+// complemented, into slot (block & 255) with a non-returning atomicMin — grid / 256
+// workgroups per slot, retiring at different times (8 per-XCD words cost ~0.4 us per kernel;
+// 256 slots measured within noise of no stamps: timeline 115.97 vs HIP events 116.57 us per
+// update at config 2) — on the 100 MHz s_memrealtime clock; the buffer starts at all-ones
+// and the host takes the latest stored slot as the kernel's end.
 // Null pointer (every production graph): no instruction beyond the test.
 typedef unsigned long long tl_word;
 enum TlKind : int {
@@ -332,6 +333,8 @@ struct MtSampleArgs {
   int skip_on_err;        // 1 (update graphs): leave the MT state untouched when sc->err is
                           // set — the reference never reaches a later update's sample
   tl_word* tl;
+  uint32_t* mt_save;      // or null: the state before this draw (625 words) is stored here —
+                          // the restore point of a draw made ahead for the next single update
 };
 // Work of the NEXT update of a multi-update graph that rides along, as extra
 // workgroups, in a GEMM launch whose tiles leave CUs idle (1024-thread configs):

@@ -985,3 +985,62 @@ def test_native_dp_loopback_world_k_bitexact(world, shape):
     assert np.array_equal(hist, fused)
     for c in ctxs:
         c.close()
+
+
+def test_single_updates_drawn_ahead_identical():
+    """A device-sampled single update draws the NEXT single update's batch ahead (its
+    random.sample + gather ride in L12 / L13 into the other batch set, the MT state saved);
+    the next single update of the same size takes it, any other call restores the MT state.
+    Against a context with the draw-ahead off (SACMI_NO_PREFETCH at creation), over a call
+    sequence that consumes, drops and re-arms it — sync, async and launch / wait updates,
+    a push (mailbox) between updates, a host random.sample, a batch-size change, a query
+    of the MT state — every loss, every parameter, the MT stream and the indices of the
+    host sample must be identical, bit for bit."""
+    cfg, B, nrows = SacConfig(24, 4, 64), 64, 500
+    params = init_params(cfg, 91, bias_scale=0.05)
+    rows = synthetic_rows(cfg, nrows + 40, 92, state_scale=0.5)
+    key = (np.arange(624, dtype=np.uint64) * 40503 % (2**32)).astype(np.uint32)
+    res = []
+    for ahead in (True, False):
+        if not ahead:
+            os.environ["SACMI_NO_PREFETCH"] = "1"
+        try:
+            ctx = make_ctx(cfg, max_batch=B, capacity=nrows + 40)
+        finally:
+            os.environ.pop("SACMI_NO_PREFETCH", None)
+        load_params(ctx, params)
+        ctx.push(*[x[:nrows] for x in rows])
+        ctx.set_mt(0, key, 624)
+        out = []
+        for _ in range(3):
+            out.append(ctx.step(B))                   # consumed by the next
+        ctx.step_async(B); ctx.step_async(B)
+        out.append(ctx.fetch_losses(2).ravel())    # (drops the one drawn ahead)
+        out.append(ctx.step(B))
+        ctx.push(*[x[nrows:nrows + 1] for x in rows])   # between updates: dropped
+        out.append(ctx.step(B))
+        out.append(ctx.step(B))
+        out.append(ctx.step(B))
+        idx = ctx.sample_indices(B)                 # a host random.sample in between
+        out.append(ctx.step(B))
+        out.append(ctx.step(B))
+        out.append(ctx.step(B // 2))                # another batch size
+        ctx.step_launch(B // 2)
+        out.append(ctx.step_wait())
+        ctx.step_launch(B // 2)
+        out.append(ctx.step_wait())
+        mt_mid = ctx.get_mt(0)
+        out.append(ctx.step(B))
+        out.append(ctx.step(B))
+        res.append((out, idx, mt_mid, ctx.get_mt(0), {n: ctx.get_net(n) for n in NETS}))
+        ctx.close()
+    (o1, i1, m1, e1, p1), (o2, i2, m2, e2, p2) = res
+    assert len(o1) == len(o2)
+    for a, b in zip(o1, o2):
+        assert np.array_equal(a, b)
+    assert np.array_equal(i1, i2)
+    for m, n in ((m1, m2), (e1, e2)):
+        assert np.array_equal(m[0], n[0]) and m[1] == n[1]
+    for n in NETS:
+        for k in p1[n]:
+            assert np.array_equal(p1[n][k], p2[n][k]), (n, k)
