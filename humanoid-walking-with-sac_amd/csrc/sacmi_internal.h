@@ -105,12 +105,12 @@ inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // ---------------------------------------------------------------------------
 // Launch timeline (sacmi_profile_timeline).  In an instrumented update graph every kernel
 // launch owns kTlWords words {start, -, kind, grid, ~end[256]}: the first 8 workgroups fold
-// their entry clock into `start` (atomicMin), and every workgroup folds its exit clock,
-// complemented, into slot (block & 255) with a non-returning atomicMin — grid / 256
-// workgroups per slot, retiring at different times (8 per-XCD words cost ~0.4 us per kernel;
-// 256 slots measured within noise of no stamps: timeline 115.97 vs HIP events 116.57 us per
-// update at config 2) — on the 100 MHz s_memrealtime clock; the buffer starts at all-ones
-// and the host takes the latest stored slot as the kernel's end.
+// their entry clock into `start` (atomicMin), and each of the last 4096 workgroups (every
+// workgroup of the update's grids) stores its exit clock, complemented, into a slot of its
+// own — no contended word (atomics of every workgroup on shared words cost ~0.4 us per
+// kernel on 8 per-XCD words, ~70 us per config-5 update on 256 slots) — on the 100 MHz
+// s_memrealtime clock; the buffer starts at all-ones and the host takes the latest stored
+// slot as the kernel's end.
 // Null pointer (every production graph): no instruction beyond the test.
 typedef unsigned long long tl_word;
 enum TlKind : int {
@@ -119,7 +119,7 @@ enum TlKind : int {
   TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_KINDS
 };
 constexpr int kTlEnd = 4;            // first of the ~end slots
-constexpr int kTlEndSlots = 256;
+constexpr int kTlEndSlots = 4096;
 // Diagnostic builds (-DSACMI_DIAG_PHASES, tools/build_variant.sh): the first 256 workgroups
 // of a stamping kernel also record kTlPhases clocks each (SACMI_PHASE), after the end slots;
 // sacmi_profile_timeline then dumps the raw buffer to $SACMI_DIAG_DUMP (tools/phase_dump.py)
@@ -144,13 +144,14 @@ struct TlMark {
     }
   }
   __device__ __forceinline__ ~TlMark() {
-    // wave 0 of EVERY workgroup at its exit folds ~clock into slot (block & 255) by a
-    // non-returning atomic min (the host takes the latest over the slots): the kernel's end
-    // is the last workgroup to retire, whatever its index — the highest-numbered (last
-    // dispatched) workgroups alone can retire early, e.g. a grid-stride epilogue's empty
-    // tail.  grid / 256 workgroups share a slot, at different times: no contention to speak of
-    if (p && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)
-      atomicMin(p + kTlEnd + (blockIdx.x & (kTlEndSlots - 1)), ~(tl_word)wall_clock64());
+    // wave 0 of each of the last kTlEndSlots (4096) workgroups — every workgroup of the
+    // update's grids — stores ~clock into a slot of its own (the host takes the latest): the
+    // kernel's end is the last workgroup to retire, whatever its index (the highest-numbered,
+    // last dispatched workgroups alone can retire early, e.g. a grid-stride epilogue's empty
+    // tail).  Plain stores: atomics from every workgroup onto shared slots cost the
+    // instrumented config-5 update ~70 us (361 vs 290 us)
+    if (p && blockIdx.x + kTlEndSlots >= gridDim.x && __builtin_amdgcn_readfirstlane(threadIdx.x) < 64u)
+      p[kTlEnd + (blockIdx.x & (kTlEndSlots - 1))] = ~(tl_word)wall_clock64();
   }
 };
 

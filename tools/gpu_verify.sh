@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-v}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > $O/pytest_gpu.log 2>&1
+eval "timeout -k 10 600 python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}" > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest_rc=$rc" >> $O/pytest_gpu.log; tail -3 $O/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/b_driver.json 2> $O/b_driver.err || { tail $O/b_driver.err; exit 1; }

@@ -26,7 +26,8 @@ def main(path):
         x = w[s, k]
         if x[0] == 2**64 - 1 or int(x[2]) != 1:      # k_gemm only (TL_GEMM)
             continue
-        ph = x[4 + 256:4 + 256 + 256 * nph].reshape(256, nph).astype(np.int64)
+        p0 = words - 256 * nph                        # phase words follow the end slots
+        ph = x[p0:p0 + 256 * nph].reshape(256, nph).astype(np.int64)
         live = ph[:, 0] > 0
         ph = ph[live]
         if len(ph) == 0:
