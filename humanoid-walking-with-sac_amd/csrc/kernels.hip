@@ -852,6 +852,9 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
 #ifndef SACMI_PIPE
 #define SACMI_PIPE 0
 #endif
+#ifndef SACMI_PIN_EPI
+#define SACMI_PIN_EPI 0         // k_gemm: the epilogue's desc fields in the K loop's round trip (measured: no gain)
+#endif
 #ifndef SACMI_PIPE_DW
 #define SACMI_PIPE_DW 0
 #endif
@@ -930,8 +933,32 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   // the fields the K loop needs, in the second (and last) round trip before the operand
   // loads; the epilogue's fields load lazily, under the MFMAs
   const GemmDesc d = batch.d[p];
-  asm volatile("" :: "s"(d.A), "s"(d.B), "s"(d.M), "s"(d.N), "s"(d.K), "s"(d.lda), "s"(d.ldb),
-               "s"(d.a_kc), "s"(d.b_kc), "s"(d.tiles_n), "s"(d.tiles_m), "s"(d.xcd_gr));
+#define SACMI_DESC_PIN_K "s"(d.A), "s"(d.B), "s"(d.M), "s"(d.N), "s"(d.K), "s"(d.lda), "s"(d.ldb), \
+    "s"(d.a_kc), "s"(d.b_kc), "s"(d.tiles_n), "s"(d.tiles_m), "s"(d.xcd_gr)
+#if SACMI_PIN_EPI
+  // ... and, in the same round trip (one asm statement: every load issued before the one
+  // wait), the fields the epilogue's buffer descriptors and scalars are formed from — the
+  // compiler forms them before the K loop, behind branches on the fields: two or three more
+  // dependent round trips before the first operand load otherwise (ISA)
+#define SACMI_DESC_PIN_E "s"(d.C), "s"(d.aux), "s"(d.ldc), "s"(d.ldaux), "s"(d.epi), "s"(d.bias), \
+    "s"(d.bias_ld), "s"(d.dotw), "s"(d.dotp), "s"(d.rs_col), "s"(d.axk), "s"(d.ax_w), "s"(d.ax_out), \
+    "s"(d.ax_ld), "s"(d.a_ksc)
+  if constexpr (ADAM) {
+    const AdamFuse& a = batch.adam;
+    asm volatile("" :: SACMI_DESC_PIN_K, SACMI_DESC_PIN_E, "s"(a.P), "s"(a.M), "s"(a.V), "s"(a.T),
+                 "s"(a.G), "s"(a.t_base), "s"(a.lr), "s"(a.beta1), "s"(a.beta2), "s"(a.eps),
+                 "s"(a.tau), "s"(a.step_offset), "s"(a.sc), "s"(d.adam_step));
+  } else if constexpr (AXK == 1) {
+    const RowsFuse& r = batch.rows;
+    asm volatile("" :: SACMI_DESC_PIN_K, SACMI_DESC_PIN_E, "s"(d.pa_w), "s"(d.pa_out), "s"(d.pa_ld),
+                 "s"(d.pa_A), "s"(d.pa_base), "s"(r.part), "s"(r.logp), "s"(r.r), "s"(r.d),
+                 "s"(r.kind), "s"(r.nparts), "s"(r.B), "s"(r.sc), "s"(r.logp_part), "s"(r.n_lp));
+  } else {
+    asm volatile("" :: SACMI_DESC_PIN_K, SACMI_DESC_PIN_E);
+  }
+#else
+  asm volatile("" :: SACMI_DESC_PIN_K);
+#endif
   const int t = bid - tbeg[p];
   if (t >= d.tiles_m * d.tiles_n) return;   // padding to a multiple of 8 blocks
   int tr, tc;
