@@ -520,7 +520,17 @@ def main():
     roof = None
     peak = PEAK_BF16_MFMA_TFLOPS if wl["dtype"] == "bf16" else PEAK_FP32_MFMA_TFLOPS
     if not args.no_roofline:
-        roof = roofline_object(ctx, args, wl, peak, step_us_real=1e6 * dt / args.steps)
+        # the timed graph's GPU time per update, for the instrumentation correction: 10
+        # launches back to back, one wait (the window above also pays fetch + sync each)
+        ctx.synchronize()
+        reps = []
+        for _ in range(3):
+            t1 = time.perf_counter()
+            for _ in range(10):
+                ctx.step_many_async(args.batch, upl)
+            ctx.synchronize()
+            reps.append((time.perf_counter() - t1) / (10 * upl))
+        roof = roofline_object(ctx, args, wl, peak, step_us_real=1e6 * float(np.median(reps)))
     flops = necessary_flops(S, A, H, args.batch, wl["n_hidden"])
     loop = None if args.no_trainer_loop else trainer_loop(wl)
     cpu = None
