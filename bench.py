@@ -502,7 +502,7 @@ def main():
 
     # one update per launch (update_parameters_async), and the API-faithful mode with
     # the losses synced every update (sac_imp.py:140-144 .item())
-    n_one = max(50, args.steps // 2)
+    n_one = max(200, args.steps // 2)      # (~30 ms: host scheduling noise averages out)
     ctx.step_async(args.batch)
     ctx.synchronize()
     t1 = time.perf_counter()
@@ -511,7 +511,7 @@ def main():
     ctx.fetch_losses(n_one)
     ctx.synchronize()
     one_sps = n_one / (time.perf_counter() - t1)
-    n_sync = max(20, args.steps // 4)
+    n_sync = max(200, args.steps // 4)
     t1 = time.perf_counter()
     for _ in range(n_sync):
         ctx.step(args.batch)
