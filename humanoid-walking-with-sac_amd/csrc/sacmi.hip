@@ -1201,7 +1201,8 @@ static int64_t per_graph_len(const sacmi_ctx* c) {
 // n consecutive fused updates (sacmi_step_many_async, the timeline's replica of it):
 // the next update's sampling + gather ride along in this update's launches where they fit
 // (uniform replay, batch <= ~2k), else run on the side stream concurrently with it
-static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use_ring, int reps) {
+static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use_ring, int reps,
+                         const PhaseRide& pr = {}) {
   const bool ride = reps > 1 && dev_idx && (ride_possible(c, B) || ride_b_possible(c, B));
   // prioritized replay only: its sampler is long and mostly serial (the numpy-MT uniforms
   // of one workgroup, the 8192-row chunk trees), so overlapping it wins (config 3: 768 ->
@@ -1239,9 +1240,16 @@ static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use
     }
     return;
   }
-  for (int r = 0; r < reps; ++r)
-    enqueue_update(c, B, dev_idx, dev_eps, 7, 1.f, use_ring, ride ? (r & 1) : 0, ride && r > 0,
-                   ride && r + 1 < reps);
+  // (pr: a batch drawn ahead by the previous launch — the first update takes it, from set
+  // pr.parity — and / or the next launch's drawn ahead by the last update: placement A)
+  const int p0 = pr.have_batch ? pr.parity : 0;
+  for (int r = 0; r < reps; ++r) {
+    const bool last_ahead = r + 1 == reps && pr.ride_next;
+    c->pf_save = last_ahead;
+    enqueue_update(c, B, dev_idx, dev_eps, 7, 1.f, use_ring, ride || pr.have_batch ? ((p0 + r) & 1) : 0,
+                   (ride && r > 0) || (r == 0 && pr.have_batch), (ride && r + 1 < reps) || last_ahead);
+    c->pf_save = false;
+  }
 }
 
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
@@ -1262,13 +1270,13 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
                      pr.have_batch, pr.ride_next);
       return;
     }
-    if (pr.ride_next || pr.have_batch) {   // one fused update drawing the next one's batch ahead
+    if (reps == 1 && (pr.ride_next || pr.have_batch)) {   // one fused update drawing the next one's batch ahead
       c->pf_save = true;
       enqueue_update(c, B, dev_idx, dev_eps, 7, grad_scale, use_ring, pr.parity, pr.have_batch, pr.ride_next);
       c->pf_save = false;
       return;
     }
-    enqueue_many(c, B, dev_idx, dev_eps, use_ring, reps);
+    enqueue_many(c, B, dev_idx, dev_eps, use_ring, reps, pr);
   };
   // the caller is capturing this stream into its own graph (e.g. torch.cuda.graph around
   // a data-parallel update and its collectives): enqueue into that capture directly
@@ -1449,7 +1457,8 @@ static void pf_settle(sacmi_ctx* c) {
   CHECK_HIP(hipMemcpyAsync(c->mt.p, c->mt_pf.p, 625 * 4, hipMemcpyDeviceToDevice, c->stream));
 }
 
-// Every API call other than the single updates and the read-only queries
+// Every API call other than the device-sampled updates (single or multi-update launches)
+// and the read-only queries (losses, tensors, scalars, select_action)
 static void pf_touch(sacmi_ctx* c) {
   if (!c) return;
   c->pf_touched = true;
@@ -1981,7 +1990,8 @@ int sacmi_sample_indices(sacmi_ctx* c, int32_t batch, int64_t* idx_out) {
   });
 }
 
-// A device-sampled single update (sacmi_step / _async / _launch): it takes the batch drawn
+// A device-sampled update launch (sacmi_step / _async / _launch, and the first / last update
+// of sacmi_step_many_async): it takes the batch drawn
 // ahead for its batch size (no sampler / gather of its own), and draws the next one ahead
 // where the ride-along fits (uniform replay, batch <= ~2k; in a graph, not under a caller's
 // capture).  Anything else first settles.
@@ -2003,10 +2013,10 @@ static PhaseRide pf_begin(sacmi_ctx* c, int B, bool dev_idx) {
   pr.ride_next = true;
   return pr;
 }
-static void pf_end(sacmi_ctx* c, int B, const PhaseRide& pr) {
+static void pf_end(sacmi_ctx* c, int B, const PhaseRide& pr, int reps = 1) {
   if (!pr.ride_next) return;
   c->pf_valid = true;
-  c->pf_parity = pr.parity ^ 1;
+  c->pf_parity = (pr.parity + reps) & 1;    // (the set after the launch's last update)
   c->pf_B = B;
 }
 
@@ -2113,16 +2123,16 @@ int sacmi_step_async(sacmi_ctx* c, int32_t batch) {
 
 int sacmi_step_many_async(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   return guard([&] {
-    pf_touch(c);
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
-    run_update(c, batch, 1, 1, 7, 1.f, true, n_updates);
+    const PhaseRide pr = pf_begin(c, batch, true);   // (draws the next launch's batch ahead)
+    run_update(c, batch, 1, 1, 7, 1.f, true, n_updates, pr);
+    pf_end(c, batch, pr, n_updates);
   });
 }
 
 int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_out) {
   return guard([&] {
-    pf_touch(c);
     REQUIRE(max_steps >= 0 && (max_steps == 0 || out), SACMI_EVALUE, "bad output buffer");
     DevScalars h = download_scalars(c);
     const int64_t avail = std::min<int64_t>(h.loss_ring_pos, c->ring_slots);
@@ -2142,6 +2152,7 @@ int sacmi_fetch_losses(sacmi_ctx* c, float* out, int32_t max_steps, int32_t* n_o
     *n_out = (int32_t)n;
     if (h.err) {   // the completed updates' losses are out; the first voided one is reported
       clear_err(c);
+      pf_settle(c);     // (a batch drawn ahead belongs to a voided update)
       throw Error{SACMI_ENAN, nan_message(c, h.err, c->Bm, " at update #" + std::to_string(h.loss_ring_pos) +
                                                               " of this agent (0-based; later updates of that launch were skipped)")};
     }

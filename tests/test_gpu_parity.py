@@ -988,9 +988,10 @@ def test_native_dp_loopback_world_k_bitexact(world, shape):
 
 
 def test_single_updates_drawn_ahead_identical():
-    """A device-sampled single update draws the NEXT single update's batch ahead (its
+    """A device-sampled update launch draws the NEXT launch's first batch ahead (its
     random.sample + gather ride in L12 / L13 into the other batch set, the MT state saved);
-    the next single update of the same size takes it, any other call restores the MT state.
+    the next launch of the same batch size takes it (single or multi-update), any other call
+    but a read restores the MT state.
     Against a context with the draw-ahead off (SACMI_NO_PREFETCH at creation), over a call
     sequence that consumes, drops and re-arms it — sync, async and launch / wait updates,
     a push (mailbox) between updates, a host random.sample, a batch-size change, a query
@@ -1015,13 +1016,19 @@ def test_single_updates_drawn_ahead_identical():
         for _ in range(3):
             out.append(ctx.step(B))                   # consumed by the next
         ctx.step_async(B); ctx.step_async(B)
-        out.append(ctx.fetch_losses(2).ravel())    # (drops the one drawn ahead)
+        out.append(ctx.fetch_losses(2).ravel())    # (a read: the one drawn ahead stays)
+        ctx.step_many_async(B, 3)                  # takes it, draws the next launch's ahead
+        ctx.step_many_async(B, 2)
+        ctx.step_async(B)
+        out.append(ctx.fetch_losses(6).ravel())
         out.append(ctx.step(B))
         ctx.push(*[x[nrows:nrows + 1] for x in rows])   # between updates: dropped
         out.append(ctx.step(B))
         out.append(ctx.step(B))
         out.append(ctx.step(B))
         idx = ctx.sample_indices(B)                 # a host random.sample in between
+        ctx.step_many_async(B, 4)
+        out.append(ctx.fetch_losses(4).ravel())
         out.append(ctx.step(B))
         out.append(ctx.step(B))
         out.append(ctx.step(B // 2))                # another batch size
