@@ -137,6 +137,9 @@ struct OpFetch {
 #ifndef SACMI_FETCH_SADDR
 #define SACMI_FETCH_SADDR 0
 #endif
+#ifndef SACMI_KCONTIG
+#define SACMI_KCONTIG 0         // k_gemm: contiguous K-chunk ranges per wave (experiment)
+#endif
 // global load with a uniform 64-bit base and a 32-bit per-lane byte offset (saddr form)
 template <class T>
 __device__ __forceinline__ T gld_off(const char* base, uint32_t off) {
@@ -297,7 +300,16 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   row_offs<MT, AKC, A16>(d.A, d.lda, m0, d.M, lane, ra);
   row_offs<NT, BKC>(d.B, d.ldb, n0, d.N, lane, rb);
   const int nch = (d.K + 15) >> 4;
+#if SACMI_KCONTIG
+  // contiguous chunk ranges per wave (chunks ks*cpw .. +cpw-1): a wave reads whole
+  // 128-byte rows of a K-contiguous operand instead of 64-byte halves shared with another wave
+  const int cpw = (nch + KSPLIT - 1) / KSPLIT;
+  const int nmine = nch > ks * cpw ? (nch - ks * cpw < cpw ? nch - ks * cpw : cpw) : 0;
+#define SACMI_CHUNK(jj) (ks * cpw + (jj))
+#else
   const int nmine = nch > ks ? (nch - ks + KSPLIT - 1) / KSPLIT : 0;
+#define SACMI_CHUNK(jj) (ks + (jj) * KSPLIT)
+#endif
   const int kl = 4 * (lane >> 4);
   float a[G][MT][4], b[G][NT][4];
   // per-group side operands: AXF 1 the transform weights w[k..k+3]; !AKC the A K-scale
@@ -318,7 +330,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
     float a1[MT][4], b1[NT][4], xw1[4];
     auto issue = [&](int jj, float (&av)[MT][4], float (&bv)[NT][4], float (&xv)[4]) {
       jj = jj < nmine ? jj : nmine - 1;   // unconditional: past the end re-reads the last chunk
-      const int k = (ks + jj * KSPLIT) * 16 + kl;
+      const int k = SACMI_CHUNK(jj) * 16 + kl;
       fetch_op<MT, AKC, A16>(ra, d.lda, k, d.K, av);
       fetch_op<NT, BKC>(rb, d.ldb, k, d.K, bv);
       if constexpr (!AKC) {
@@ -370,7 +382,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       // drain the loads at the end of the guarded block): a group past the wave's last
       // chunk re-reads that chunk and is skipped below
       const int jj = j + g < nmine ? j + g : nmine - 1;
-      const int k = (ks + jj * KSPLIT) * 16 + kl;
+      const int k = SACMI_CHUNK(jj) * 16 + kl;
       fetch_op<MT, AKC, A16>(ra, d.lda, k, d.K, a[g]);
       fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
       if constexpr (AXF == 1) {          // w3 rows are float4-aligned (parameter arena)
@@ -394,7 +406,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
         // tile configuration's code generation
 #pragma clang fp contract(off)
         if constexpr (AXF == 1) {
-          const int k = (ks + (j + g) * KSPLIT) * 16 + kl;
+          const int k = SACMI_CHUNK(j + g) * 16 + kl;
 #pragma unroll
           for (int i = 0; i < MT; ++i) {
             const int r = mloc + i * 16 + (lane & 15);
@@ -423,6 +435,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       }
   }
   }   // !PIPE
+#undef SACMI_CHUNK
   SACMI_STAMP(16 + wave);
   float* my = red + wave * TM * (TN + 1);
   const int rq = (lane >> 4) * 4, cc = lane & 15;

@@ -1768,7 +1768,9 @@ static void push_impl(sacmi_ctx* c, const float* s, const float* a, const float*
     const int S = c->S, A = c->A;
     const int64_t rowf = 2 * S + A + 2;
     if (mb_env && c->mb_host && !c->inflight && c->cfg.replay_kind == SACMI_REPLAY_UNIFORM &&
-        c->mb_pending + n <= sacmi_ctx::kMbRows) {
+        c->mb_pending + n <= sacmi_ctx::kMbRows && c->mb_pending + n <= c->capacity) {
+      // (rows pending beyond the capacity would map two rows onto one ring slot in the
+      // sampler's scatter, stored in no fixed order: the chunked path's `skip` handles that)
       float* dst = mb_rows_host(c) + (size_t)c->mb_pending * rowf;
       for (int64_t j = 0; j < n; ++j, dst += rowf) {
         if (packed) {
@@ -2049,6 +2051,25 @@ static int done_prev(sacmi_ctx* c) {
   return *reinterpret_cast<volatile int*>(c->loss_host + 4);
 }
 
+// Host wait on a word a kernel stores into host-mapped memory behind a system-scope fence
+// (the update's done counter, select_action's heads).  Returns true once `done(value)` holds;
+// false when the stream finished (or failed) without the store — the caller then
+// synchronises the stream, which reports any error.  hipStreamQuery runs every 1024 spins.
+// Done when (*w == value) == equal.
+static bool poll_done(volatile int* w, hipStream_t s, int value, bool equal) {
+  for (int it = 1;; ++it) {
+    if ((*w == value) == equal) {
+      std::atomic_thread_fence(std::memory_order_acquire);
+      return true;
+    }
+    if ((it & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q != hipErrorNotReady) return false;
+      (void)hipGetLastError();
+    }
+  }
+}
+
 // the synchronous step's second half: wait, then the losses (or the error bits) the
 // update's last kernels stored into host-mapped memory
 // done_prev >= 0: the done word's value before the launch, with no other update in flight:
@@ -2058,15 +2079,7 @@ static void step_finish(sacmi_ctx* c, int batch, float* losses_out, int done_pre
   bool done = false;
   if (done_prev >= 0) {
     volatile int* w = reinterpret_cast<volatile int*>(c->loss_host + 4);
-    for (int it = 1;; ++it) {
-      if (*w != done_prev) { done = true; break; }
-      if ((it & 1023) == 0) {   // finished without the store (or failed): the sync reports
-        const hipError_t q = hipStreamQuery(c->stream);
-        if (q != hipErrorNotReady) break;
-        (void)hipGetLastError();
-      }
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
+    done = poll_done(w, c->stream, done_prev, false);
   }
   if (!done) CHECK_HIP(hipStreamSynchronize(c->stream));
   c->inflight = false;
@@ -2643,6 +2656,12 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     static const bool zc_env = std::getenv("SACMI_ACT_ZEROCOPY") == nullptr ||
                                std::getenv("SACMI_ACT_ZEROCOPY")[0] != '0';
     const bool zc = pinned && zc_env && c->act_host_dev;
+    static const bool gemv_env = std::getenv("SACMI_NO_ACT_GEMV") == nullptr;
+    static const bool poll1 = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
+    const bool gemv = zc && n == 1 && gemv_env && poll1 && A <= 32;
+    // every path but the one-state GEMVs writes rows of batch set 0's x2 (the states here,
+    // the actions from the heads kernel): a batch drawn ahead there is given up first
+    if (!gemv) pf_touch(c);
     if (!zc) {
       CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, src, (size_t)(pinned ? Kx : S) * 4, (size_t)S * 4, n,
                                  hipMemcpyHostToDevice, s));
@@ -2651,9 +2670,7 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     // one state (the env-rate call): the policy forward as GEMVs (k_act_gemv / k_act_heads:
     // a wave per output instead of 32-row level tiles that use one row), fp32, from the
     // mapped staging, the action back into it, the host polling the heads' done word
-    static const bool gemv_env = std::getenv("SACMI_NO_ACT_GEMV") == nullptr;
-    static const bool poll1 = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
-    if (zc && n == 1 && gemv_env && poll1 && A <= 32) {
+    if (gemv) {
       const float* x = c->act_host_dev;
       int K = S + 1, ldw = c->p_fc[0].ld;
       const float* Wl = c->P.p + c->p_fc[0].off;
@@ -2677,16 +2694,7 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
       ha.done_value = ++c->act_seq;
       launch_act_heads(ha, s);
       volatile int* done_host = reinterpret_cast<volatile int*>(c->act_nan_host + 1);
-      bool done = false;
-      for (int it = 1;; ++it) {
-        if (*done_host == ha.done_value) { done = true; break; }
-        if ((it & 1023) == 0) {   // finished without the store (or failed): the sync reports
-          const hipError_t q = hipStreamQuery(s);
-          if (q != hipErrorNotReady) break;
-          (void)hipGetLastError();
-        }
-      }
-      std::atomic_thread_fence(std::memory_order_acquire);
+      const bool done = poll_done(done_host, s, ha.done_value, true);
       if (!done) CHECK_HIP(hipStreamSynchronize(s));
       c->done_epoch = c->epoch;
       if (!deterministic && *reinterpret_cast<volatile int*>(c->act_nan_host))
@@ -2722,9 +2730,9 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     if (zc) hs.act_host = c->act_host_dev + (h_out - c->act_host);
     // one heads workgroup: the host polls its done word instead of the stream's completion
     static const bool poll = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
-    const bool poll_done = poll && zc && n <= heads_rows_per_wg(n);
+    const bool poll_wait = poll && zc && n <= heads_rows_per_wg(n);
     volatile int* done_host = reinterpret_cast<volatile int*>(c->act_nan_host + 1);
-    if (poll_done) {
+    if (poll_wait) {
       hs.done_word = c->act_nan_dev + 1;
       hs.done_value = ++c->act_seq;
     }
@@ -2738,17 +2746,7 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
       CHECK_HIP(hipMemcpy2DAsync(pinned ? h_out : a_out, (size_t)A * 4, c->x2.p + S + 1, (size_t)Kx * 4,
                                  (size_t)A * 4, n, hipMemcpyDeviceToHost, s));
     bool done = false;
-    if (poll_done) {
-      for (int it = 1;; ++it) {
-        if (*done_host == hs.done_value) { done = true; break; }
-        if ((it & 1023) == 0) {   // finished without the store (or failed): the sync reports
-          const hipError_t q = hipStreamQuery(s);
-          if (q != hipErrorNotReady) break;
-          (void)hipGetLastError();
-        }
-      }
-      std::atomic_thread_fence(std::memory_order_acquire);
-    }
+    if (poll_wait) done = poll_done(done_host, s, hs.done_value, true);
     if (!done) CHECK_HIP(hipStreamSynchronize(s));
     c->done_epoch = c->epoch;
     if (!deterministic && *reinterpret_cast<volatile int*>(c->act_nan_host))

@@ -334,13 +334,20 @@ class SAC:
         if replay_buffer:
             # the reference pickles its deque of tuples; stored here as plain arrays so
             # the checkpoint loads with torch.load(weights_only=True)
+            # (an empty replay is saved too: loading it empties the buffer, as assigning
+            # the reference's empty deque does)
             n = len(self.replay_buffer)
+            S, A = self._cfg.state_dim, self._cfg.action_dim
             if n:
                 s, a, r, s2, d = self.replay_buffer._rows_at(np.arange(n))
-                ck["replay_buffer"] = {"state": torch.from_numpy(s), "action": torch.from_numpy(a),
-                                       "reward": torch.from_numpy(r),
-                                       "next_state": torch.from_numpy(s2),
-                                       "done": torch.from_numpy(d)}
+            else:
+                s, a, r, s2 = (np.zeros((0, S), np.float32), np.zeros((0, A), np.float32),
+                               np.zeros(0, np.float32), np.zeros((0, S), np.float32))
+                d = np.zeros(0, bool)
+            ck["replay_buffer"] = {"state": torch.from_numpy(s), "action": torch.from_numpy(a),
+                                   "reward": torch.from_numpy(r),
+                                   "next_state": torch.from_numpy(s2),
+                                   "done": torch.from_numpy(d)}
         # NB: the reference only calls torch.save when replay_buffer=True (an
         # indentation slip at sac_imp.py:198-201); the drop-in always saves.
         torch.save(ck, path)

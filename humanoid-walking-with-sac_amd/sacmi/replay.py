@@ -112,6 +112,12 @@ class _Staged:
     def _replace_arrays(self, s, a, r, s2, d):
         """Replace the contents with the rows of stacked arrays (the drop-in's checkpoint form)."""
         self._rows.clear()
+        if len(s) == 0:
+            # an empty replay (the reference assigns an empty buffer): nothing to push, and
+            # no context to create from rows that do not exist
+            if self._ctx is not None:
+                self._ctx.replay_clear()
+            return
         self._ensure_ctx(s[0], a[0])
         self._ctx.replay_clear()
         self._ctx.push(s, a, r, s2, d)

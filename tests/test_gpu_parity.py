@@ -995,7 +995,7 @@ def test_single_updates_drawn_ahead_identical():
     Against a context with the draw-ahead off (SACMI_NO_PREFETCH at creation), over a call
     sequence that consumes, drops and re-arms it — sync, async and launch / wait updates,
     a push (mailbox) between updates, a host random.sample, a batch-size change, a query
-    of the MT state — every loss, every parameter, the MT stream and the indices of the
+    of the MT state, select_action of 100 / 7 / 1 states between updates — every loss, every parameter, the MT stream and the indices of the
     host sample must be identical, bit for bit."""
     cfg, B, nrows = SacConfig(24, 4, 64), 64, 500
     params = init_params(cfg, 91, bias_scale=0.05)
@@ -1039,6 +1039,13 @@ def test_single_updates_drawn_ahead_identical():
         mt_mid = ctx.get_mt(0)
         out.append(ctx.step(B))
         out.append(ctx.step(B))
+        # select_action between single updates: n > 64 states go through batch set 0's
+        # x2 rows (the non-zero-copy path), n <= 64 write their actions there, one state
+        # takes the GEMVs (writes no batch set) — a batch drawn ahead must not be clobbered
+        st = np.asarray(rows[0][:100], np.float32)
+        for n_act in (100, 7, 1, 100):
+            out.append(ctx.act(st[:n_act], deterministic=True).ravel())
+            out.append(ctx.step(B))
         res.append((out, idx, mt_mid, ctx.get_mt(0), {n: ctx.get_net(n) for n in NETS}))
         ctx.close()
     (o1, i1, m1, e1, p1), (o2, i2, m2, e2, p2) = res
