@@ -268,16 +268,22 @@ def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False, n_hidden=
                        f"{threads} threads (the box's CPU share per GPU) on {cpu}")
 
 
-def trainer_loop(wl, steps=300, warmup=30, fill=20_000):
+def trainer_loop(wl, steps=300, warmup=30, fill=20_000, sync_python_random=False):
     """The reference trainer's inner loop without the environment (trainer.py:182-205):
     per env step select_action(state) -> replay_buffer.push(transition) ->
     update_parameters(batch) (losses synced, as .item() in sac_imp.py:140-144), through
-    the drop-in SAC (sac_imp module name).  Returns env-steps/s and the split."""
+    the drop-in SAC (sac_imp module name).  Returns env-steps/s and the split.
+    sync_python_random=True: the reference-faithful index stream — every update also
+    advances Python's `random` exactly as the reference's random.sample does
+    (replay_buffer.py:15, sac_imp.py:77), the device drawing the same indices."""
+    import random
     from sac_imp import SAC
     S, A, H, B = wl["S"], wl["A"], wl["H"], wl["batch"]
     torch.manual_seed(0)
+    random.seed(5)
     agent = SAC(S, A, hidden_dim=H, device="cuda", capacity=max(fill * 2, 100_000),
-                max_batch=B, seed=3, networks=wl["networks"], compute_dtype=wl["dtype"])
+                max_batch=B, seed=3, networks=wl["networks"], compute_dtype=wl["dtype"],
+                sync_python_random=sync_python_random)
     agent._ctx.push(*synth(fill, 11, S, A))
     rng = np.random.default_rng(12)
     states = rng.standard_normal((steps + warmup + 1, S)).astype(np.float32)
@@ -307,8 +313,11 @@ def trainer_loop(wl, steps=300, warmup=30, fill=20_000):
             "us_select_action": round(1e6 * tt[0] / steps, 1),
             "us_push": round(1e6 * tt[1] / steps, 1),
             "us_update_parameters": round(1e6 * tt[2] / steps, 1),
+            "sync_python_random": sync_python_random,
             "note": "trainer.py:182-205 loop minus env.step: select_action + push + "
-                    f"update_parameters({B}) per env step, drop-in SAC, {fill}-row replay"}
+                    f"update_parameters({B}) per env step, drop-in SAC, {fill}-row replay"
+                    + ("; Python's random stream advanced as the reference's (faithful indices)"
+                       if sync_python_random else "; device index stream (default)")}
 
 
 def roofline_object(ctx, args, wl, peak, data_parallel=False, step_us_real=None):
@@ -533,6 +542,7 @@ def main():
         roof = roofline_object(ctx, args, wl, peak, step_us_real=1e6 * float(np.median(reps)))
     flops = necessary_flops(S, A, H, args.batch, wl["n_hidden"])
     loop = None if args.no_trainer_loop else trainer_loop(wl)
+    loop_f = None if args.no_trainer_loop else trainer_loop(wl, sync_python_random=True)
     cpu = None
     if not args.no_cpu_baseline:
         n_cpu = min(fill, 1_000_000)
@@ -558,6 +568,7 @@ def main():
         "mfma_util_step": round(flops * sps / 1e12 / peak, 4),
         "necessary_gflop_per_step": round(flops / 1e9, 4),
         "trainer_loop": loop,
+        "trainer_loop_faithful": loop_f,
         "roofline": roof, "cpu_baseline": cpu,
         "fill_seconds": round(t_fill, 2),
     }

@@ -481,6 +481,316 @@ __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, flo
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-staged core (k_gemm CORE 1: the batch-256-class fp32 levels).
+//
+// Why: the register-direct core above reads its operands as 16 rows x 64 bytes per
+// wave-instruction (the 16x16x4 fragment: 4 lane groups x 16 B of each of 16 rows).  Measured
+// per CU with every CU loading at once (tools/l2_rate_bench.hip, profiles/r04/l2_rate.txt),
+// that shape takes 43 GB/s from an L2-resident operand, against ~150 GB/s for 128- to 1024-byte
+// row segments per instruction — the level bodies' "operand delivery" bound (round-3 phase
+// stamps: the last wave's K loop 2.2-2.5x wave 0's).
+//
+// How: the workgroup (16 waves) streams K in slabs of BK = 16 KSP through a ring of NST LDS
+// slots by LDS-DMA (global_load_lds_dwordx4: 1 KB per wave-instruction, 2-8 rows of
+// 128-512 contiguous bytes), slab s + NST - 1 issued right after the barrier that retires
+// slab s (counted vmcnt waits, no drain).  The tile TMW x TN is cut into NSUB sub-tiles of
+// 32 x WN, and the K of each slab into KSP 16-deep parts: wave (sub, part) runs the 16x16x4
+// MFMAs of its sub-tile over its part of every slab, reading fragments from LDS
+// (ds_read_b128 for a K-contiguous operand, 4 x ds_read_b32 for an MN-contiguous one; 16-byte
+// chunks XOR-swizzled by row on the DMA source address: conflict-free).  The KSP partial
+// tiles go to `red` in k_gemm's layout ([row / TM][part][TM][TN + 1]) and k_gemm's epilogue
+// (bias / ReLU / mask / fc3 dots / Adam / rowsum / dL/da partials) runs unchanged.  The ring
+// aliases `red` (the partials are written after the last slab is consumed).
+// Chunks past K are read from a clamped in-row address and zeroed in the fragments (last slab
+// only); rows past M / N read a clamped row and are discarded by the epilogue.
+typedef __attribute__((address_space(3))) void stg_lds_t;
+typedef __attribute__((address_space(1))) const void stg_gbl_t;
+
+template <int N>
+__device__ __forceinline__ void stg_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+// s_waitcnt vmcnt(n) for a wave-uniform n (an immediate per case)
+__device__ __forceinline__ void stg_vmwait_n(int n) {
+  switch (n) {
+    case 0: stg_vmwait<0>(); break;   case 1: stg_vmwait<1>(); break;
+    case 2: stg_vmwait<2>(); break;   case 3: stg_vmwait<3>(); break;
+    case 4: stg_vmwait<4>(); break;   case 5: stg_vmwait<5>(); break;
+    case 6: stg_vmwait<6>(); break;   case 7: stg_vmwait<7>(); break;
+    case 8: stg_vmwait<8>(); break;   case 9: stg_vmwait<9>(); break;
+    case 10: stg_vmwait<10>(); break; case 11: stg_vmwait<11>(); break;
+    case 12: stg_vmwait<12>(); break; case 13: stg_vmwait<13>(); break;
+    case 14: stg_vmwait<14>(); break; default: stg_vmwait<15>(); break;
+  }
+}
+
+constexpr int kStgKW = 1024;     // K words staged for ax_w / a_ksc (launch_gemm checks K)
+constexpr int kStgRing = 144 * 1024;
+
+// geometry of a staged tile: TMW x TN, KSP K parts, 16 waves
+template <int TMW, int TN, int KSP>
+struct StgGeo {
+  static constexpr int NSUB = 16 / KSP, NSM = TMW / 32, NSN = NSUB / NSM;
+  static constexpr int WM = 32, WN = TN / NSN, MI = WM / 16, NJ = WN / 16;
+  static constexpr int BK = 16 * KSP;
+  static constexpr int SLOT = (TMW + TN) * BK * 4;                 // bytes per ring slot
+  static constexpr int NST = kStgRing / SLOT < 4 ? kStgRing / SLOT : 4;
+  static constexpr int RING = NST * SLOT;
+  static_assert(NSUB * KSP == 16 && NSM * 32 == TMW && NSN * NSM == NSUB && NJ * 16 * NSN == TN,
+                "staged tile geometry");
+  static_assert(NST >= 3 && SLOT % (16 * 1024) == 0, "staged ring");
+};
+
+// one operand's slab image: KC -> R rows (M or N) of BK k; MN -> BK rows (k) of R columns
+template <int R, int BK, bool KC>
+struct StgOp {
+  static constexpr int RB = KC ? BK * 4 : R * 4;        // bytes per LDS row
+  static constexpr int NR = KC ? R : BK;                 // LDS rows
+  static constexpr int CPR = RB / 16;                    // 16-byte chunks per row
+  static constexpr int SWZ = (CPR < 16 ? CPR : 16) - 1;  // chunk swizzle mask
+  static constexpr int RPP = 1024 / RB;                  // rows per 1 KB piece
+  static constexpr int BYTES = NR * RB, PIECES = BYTES / 1024;
+  static_assert(RB >= 128 && RB <= 1024 && BYTES % 1024 == 0, "staged operand shape");
+};
+
+template <int TM, int TN, int KSP, int MG, bool AKC, bool BKC, bool ROWSUM, int AXF, class Pre>
+__device__ __forceinline__ void gemm_core_s(const GemmDesc& d, int m0, int n0, unsigned char* ring,
+                                            float* rsum, float* s_kw, Pre&& pre, bool store_a) {
+  constexpr int TMW = TM * MG;
+  using G = StgGeo<TMW, TN, KSP>;
+  using OA = StgOp<TMW, G::BK, AKC>;
+  using OB = StgOp<TN, G::BK, BKC>;
+  constexpr int BK = G::BK, NST = G::NST, SLOT = G::SLOT, MI = G::MI, NJ = G::NJ;
+  constexpr int PPW = (OA::PIECES + OB::PIECES) / 16;
+  static_assert(OA::PIECES + OB::PIECES == SLOT / 1024 && PPW * 16 == SLOT / 1024 && OA::PIECES % 16 == 0,
+                "staged pieces: whole pieces per wave, A pieces first");
+  // store_a (AXF): every workgroup issues the same number of stores per slab (zero-length
+  // descriptor where it stores nothing), so the counted waits are uniform
+  constexpr int SST = AXF == 1 ? (TMW * BK / 4 + 1023) / 1024 : 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = wave % G::NSUB, kp = wave / G::NSUB;
+  const int wm = (sub / G::NSN) * G::WM, wn = (sub % G::NSN) * G::WN;
+  const int g4 = lane >> 4, l16 = lane & 15;
+  const int K = d.K;
+  const int nslab = (K + BK - 1) / BK;
+  // staged K vector (AXF: the fc3 weights w; !AKC: the per-k scale, where the desc has one)
+  const bool has_ksc = AXF != 1 && !AKC && d.a_ksc != nullptr;
+  const float* kwsrc = AXF == 1 ? d.ax_w : d.a_ksc;
+  const bool has_kw = AXF == 1 || has_ksc;
+  // the K vector goes global -> LDS by DMA too (a ds_write behind the slab DMAs would wait for
+  // all of them: the compiler orders LDS stores after an LDS-DMA that may alias): one dword a
+  // lane, 64 words a wave, zeros past K (buffer range; zero-length where the level has none)
+  static_assert(kStgKW == 16 * 64, "one K-vector DMA per wave");
+  {
+    const rsrc_t rkw = make_rsrc(has_kw ? kwsrc : d.A, has_kw ? (uint32_t)K * 4u : 0u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rkw, (stg_lds_t*)(s_kw + wave * 64), 4,
+                                             (uint32_t)(wave * 64 + lane) * 4u, 0, 0, 0);
+  }
+  pre();     // the epilogue's loads: the oldest vector-memory operations of the wave
+  // DMA source of each piece this wave moves: piece pc = wave + 16 q (A pieces first)
+  const char* pbase[PPW];
+  int kofs[PPW];
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) {
+    const int pc = wave + 16 * q;
+    const bool isA = q < OA::PIECES / 16;
+    const int RPP = isA ? OA::RPP : OB::RPP, CPR = isA ? OA::CPR : OB::CPR, SW = isA ? OA::SWZ : OB::SWZ;
+    const bool kc = isA ? AKC : BKC;
+    const int Rr = (isA ? pc : pc - OA::PIECES) * RPP + lane / CPR;   // LDS row
+    const int c = (lane % CPR) ^ (Rr & SW);                           // global chunk it holds
+    const float* base = isA ? d.A : d.B;
+    const int ld = isA ? d.lda : d.ldb;
+    const int lim = isA ? d.M : d.N;
+    const int mn0 = isA ? m0 : n0;
+    if (kc) {   // row mn0 + Rr (clamped), k = slab k0 + 4 c
+      const int row = mn0 + Rr < lim ? mn0 + Rr : lim - 1;
+      pbase[q] = reinterpret_cast<const char*>(base + (size_t)row * ld);
+      kofs[q] = 4 * c;
+    } else {    // k row = slab k0 + Rr (clamped), column mn0 + 4 c (clamped)
+      const int col = mn0 + 4 * c < lim ? mn0 + 4 * c : 0;
+      pbase[q] = reinterpret_cast<const char*>(base + col);
+      kofs[q] = Rr;
+    }
+  }
+  auto issue = [&](int sl) {
+    unsigned char* dst = ring + (sl % NST) * SLOT;
+    const int k0 = sl * BK;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const bool isA = q < OA::PIECES / 16;
+      const bool kc = isA ? AKC : BKC;
+      const int ld = isA ? d.lda : d.ldb;
+      const char* g;
+      if (kc) {
+        const int k = k0 + kofs[q];
+        g = pbase[q] + (size_t)(k < K ? k : 0) * 4;
+      } else {
+        const int k = k0 + kofs[q];
+        g = pbase[q] + (size_t)(k < K ? k : K - 1) * ld * 4;
+      }
+      __builtin_amdgcn_global_load_lds((stg_gbl_t*)g, (stg_lds_t*)(dst + (wave + 16 * q) * 1024), 16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int sl = 0; sl < NST - 1; ++sl)
+    if (sl < nslab) issue(sl);
+  const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
+                               store_a ? (uint32_t)(((size_t)(d.M - 1) * d.ax_ld + d.K) * 4) : 0u);
+  f4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float rs[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) rs[i] = 0.f;
+  const bool rs_wave = ROWSUM && wn == 0;   // one column of sub-tiles sums the rows
+  for (int sl = 0; sl < nslab; ++sl) {
+    // vector-memory ops issued after slab sl's DMA: the later prologue slabs, then per
+    // iteration i < sl its stores and (while slabs remain) the DMA of slab i + NST - 1
+    int younger = 0;
+    if (sl < NST - 1) younger += ((NST - 2 < nslab - 1 ? NST - 2 : nslab - 1) - sl) * PPW;
+    for (int i = (sl - NST + 2 > 0 ? sl - NST + 2 : 0); i < sl; ++i)
+      younger += SST + (i + NST - 1 < nslab ? PPW : 0);
+    stg_vmwait_n(younger);
+    __builtin_amdgcn_s_barrier();          // slab sl landed for every wave; slot (sl - 1) free
+    asm volatile("" ::: "memory");
+    const unsigned char* st = ring + (sl % NST) * SLOT;
+    const int kb = sl * BK;
+    if constexpr (AXF == 1) {
+      // u = transformed A rows of this slab, stored by the column-tile-0 workgroups
+#pragma unroll
+      for (int q = 0; q < SST; ++q) {
+        const int e = tid + 1024 * q, row = e / (BK / 4), c = e % (BK / 4);
+        const int k = kb + 4 * c;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (row < TMW) {
+          const f4 h = *reinterpret_cast<const f4*>(st + row * OA::RB + ((c ^ (row & OA::SWZ)) << 4));
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) v[s2] = (h[s2] > 0.f && k + s2 < K) ? s_kw[k + s2] : 0.f;
+        }
+        const bool ok = row < TMW && m0 + row < d.M && k < K;
+        buf_st4(rAx, ok ? (uint32_t)((m0 + row) * d.ax_ld + k) * 4u : 0xfffffff0u, v);
+      }
+    }
+    if (sl + NST - 1 < nslab) issue(sl + NST - 1);
+    // this wave's 16-deep part of the slab
+    float a[MI][4], b[NJ][4];
+    const int kk = kp * 16 + 4 * g4;       // the lane group's first k inside the slab
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int r = wm + i * 16 + l16;
+      if constexpr (AKC) {
+        const int c = kk >> 2;
+        const f4 x = *reinterpret_cast<const f4*>(st + r * OA::RB + ((c ^ (r & OA::SWZ)) << 4));
+        a[i][0] = x[0]; a[i][1] = x[1]; a[i][2] = x[2]; a[i][3] = x[3];
+      } else {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int R = kk + s2;
+          a[i][s2] = *reinterpret_cast<const float*>(st + R * OA::RB + ((((r >> 2) ^ (R & OA::SWZ))) << 4) + (r & 3) * 4);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = wn + j * 16 + l16;
+      const unsigned char* sb = st + OA::BYTES;
+      if constexpr (BKC) {
+        const int c = kk >> 2;
+        const f4 x = *reinterpret_cast<const f4*>(sb + n * OB::RB + ((c ^ (n & OB::SWZ)) << 4));
+        b[j][0] = x[0]; b[j][1] = x[1]; b[j][2] = x[2]; b[j][3] = x[3];
+      } else {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int R = kk + s2;
+          b[j][s2] = *reinterpret_cast<const float*>(sb + R * OB::RB + ((((n >> 2) ^ (R & OB::SWZ))) << 4) + (n & 3) * 4);
+        }
+      }
+    }
+    {
+#pragma clang fp contract(off)
+      const int k = kb + kk;
+      if (K - kb < BK) {   // the last, partial slab: k >= K contributes nothing
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const bool in = k + s2 < K;
+#pragma unroll
+          for (int i = 0; i < MI; ++i) a[i][s2] = in ? a[i][s2] : 0.f;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) b[j][s2] = in ? b[j][s2] : 0.f;
+        }
+      }
+      if constexpr (AXF == 1) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const float w = s_kw[k + s2 < kStgKW ? k + s2 : 0];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) a[i][s2] = (a[i][s2] > 0.f && k + s2 < K) ? w : 0.f;
+        }
+      } else if constexpr (!AKC) {
+        if (has_ksc) {
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) {
+            const float f = s_kw[k + s2 < kStgKW ? k + s2 : 0];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) a[i][s2] *= f;
+          }
+        }
+      }
+      mfma_chunk<MI, NJ, false>(acc, a, b);
+      if (ROWSUM && rs_wave) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) rs[i] += (a[i][0] + a[i][1]) + (a[i][2] + a[i][3]);
+      }
+    }
+  }
+  __syncthreads();                          // every wave is past its last ring read
+  // partial tiles into red = the ring: red[((row / TM) * KSP + kp) * TM * (TN + 1) + (row % TM) * (TN + 1) + col]
+  float* red = reinterpret_cast<float*>(ring);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm + i * 16 + g4 * 4 + r, col = wn + j * 16 + l16;
+        red[((row / TM) * KSP + kp) * TM * (TN + 1) + (row % TM) * (TN + 1) + col] = acc[i][j][r];
+      }
+  if (ROWSUM && rs_wave) {
+    // lanes l, l+16, l+32, l+48 hold the same row: fold the 4 lane groups, fixed order
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int row = wm + i * 16 + lane;
+      if (lane < 16) rsum[((row / TM) * KSP + kp) * TM + row % TM] = v;
+    }
+  }
+}
+
+template <int TM, int TN, int KSP, int MG, int AXK, class Pre>
+__device__ __forceinline__ void gemm_core_stg(const GemmDesc& d, int m0, int n0, unsigned char* ring,
+                                              float* rsum, float* s_kw, bool rowsum, Pre&& pre) {
+  if constexpr (AXK == 1) {
+    if (d.axk == 1) {
+      gemm_core_s<TM, TN, KSP, MG, true, false, false, 1>(d, m0, n0, ring, rsum, s_kw, pre,
+                                                          n0 == 0 && d.ax_out != nullptr);
+      return;
+    }
+  }
+  if (d.a_kc) {
+    if (d.b_kc) gemm_core_s<TM, TN, KSP, MG, true, true, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
+    else gemm_core_s<TM, TN, KSP, MG, true, false, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
+  } else {
+    if (d.b_kc) gemm_core_s<TM, TN, KSP, MG, false, true, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
+    else if (rowsum) gemm_core_s<TM, TN, KSP, MG, false, false, true, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
+    else gemm_core_s<TM, TN, KSP, MG, false, false, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
+  }
+}
+
 // DPP row rotation (within each 16-lane row) of a float
 template <int CTRL>
 __device__ __forceinline__ float dpp_row(float x) {
@@ -808,6 +1118,7 @@ __device__ void rows_finish(const RowsFuse& rf, const GemmDesc& d, int m0, bool 
         c1 = g * (1.f - w1);
       }
       if (writer && rf.dq) { rf.dq[b] = c0; rf.dq[rf.B + b] = c1; }
+      if (writer && rf.dq4) { rf.dq4[(size_t)b * 4] = c0; rf.dq4[((size_t)rf.B + b) * 4] = c1; }
     }
     s_coef[0][t] = c0; s_coef[1][t] = c1;
     s_l[t][0] = l0; s_l[t][1] = l1;
@@ -880,8 +1191,17 @@ constexpr int gemm_min_waves() { return 4; }   // 16 waves per CU: one 1024- or 
 // TM x TN per wave group, MG wave groups (workgroup tile MG*TM x TN), K split KSPLIT
 // ways inside each group; ADAM: fused optimizer epilogue (every desc EPI_ADAM*); BF16:
 // bf16 MFMA operands (GemmBatch::bf16), everything around them fp32
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false>
-__global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
+// CORE 0: register-direct operand loads, K split KSPLIT ways across 64*KSPLIT*MG threads;
+// CORE 1: the LDS-staged core (gemm_core_s), 1024 threads, KSPLIT = its K parts (partial tiles)
+template <int KSPLIT, int MG, int CORE>
+constexpr int gemm_threads() { return CORE ? 1024 : 64 * KSPLIT * MG; }
+template <int CORE, int TMW, int TN, int KSP>
+constexpr int stg_ring() {
+  if constexpr (CORE == 1) return StgGeo<TMW, TN, KSP>::RING;
+  else return 1;
+}
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false, int CORE = 0>
+__global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
   // The scalars that locate this workgroup's work come in ONE kernarg round trip: left to
   // the compiler, each load sat behind a branch on the previous one (timeline pointer, tile
   // count, one desc's tile_begin per loop trip, then the desc's fields as they were used),
@@ -900,7 +1220,15 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   SACMI_PHASE(tl, 0);
   SACMI_PHASE_LAST(tl, 6);
   constexpr int TMW = TM * MG;
-  __shared__ float red[MG * KSPLIT * TM * (TN + 1)];
+  static_assert(!CORE || !BF16, "the staged core is fp32");
+  // CORE 1: the operand ring, which the partial tiles (`red`) alias after the K loop; its
+  // K vector (ax_w / a_ksc) staging
+  constexpr int RING = stg_ring<CORE, TMW, TN, KSPLIT>();
+  static_assert(!CORE || RING >= MG * KSPLIT * TM * (TN + 1) * 4, "staged ring holds the partial tiles");
+  __shared__ __attribute__((aligned(16))) unsigned char ring[RING];
+  __shared__ float red_l[CORE ? 1 : MG * KSPLIT * TM * (TN + 1)];
+  __shared__ float s_kw[CORE ? kStgKW : 1];
+  float* const red = CORE ? reinterpret_cast<float*>(ring) : red_l;
   __shared__ float rsum[MG * KSPLIT * TM];
   __shared__ AdamScalars s_k;
   __shared__ int s_err;
@@ -923,7 +1251,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   }
 #endif
   if (bid >= n_tiles) {   // ride-along workgroups (next update's replay work, Polyak)
-    if constexpr (MG * KSPLIT == 16) {   // the host attaches rides to 1024-thread configs
+    if constexpr (gemm_threads<KSPLIT, MG, CORE>() == 1024) {   // the host attaches rides to 1024-thread configs
       const int rb = bid - n_tiles;
       if (rb >= (batch.ride.kind ? batch.ride.nblocks : 0)) {
         polyak_ride(batch.ride.pk, rb - (batch.ride.kind ? batch.ride.nblocks : 0), batch.ride.pk_blocks);
@@ -993,7 +1321,7 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   // Element slots: EPT tile outputs per thread (e = tid + s*NTH) plus one slot for the
   // rowsum (bias-gradient) column.  Their epilogue operands (bias, ReLU mask, Adam
   // state) are loaded by pre() while the MFMAs run.
-  constexpr int NTH = 64 * KSPLIT * MG, EPT = TMW * TN / NTH, NS = EPT + 1;
+  constexpr int NTH = gemm_threads<KSPLIT, MG, CORE>(), EPT = TMW * TN / NTH, NS = EPT + 1;
   static_assert(TMW * TN % NTH == 0 && TMW <= NTH, "epilogue slot layout");
   const int tid = threadIdx.x;
   // slot s -> (row, col in tile, output column n, valid); recomputed where needed so
@@ -1057,8 +1385,17 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   constexpr int PW = PA ? (TN * 32 + NTH - 1) / NTH : 1;
   float paw_x[PW];
   const bool has_pa = PA && d.pa_out != nullptr;
+  // CORE 1: the Adam scalars by scalar loads into every wave (lgkmcnt: no vector-memory round
+  // trip in front of the slab DMAs, and no LDS store that would wait for them)
+  uint32_t skw[5] = {0u, 0u, 0u, 0u, 0u};
   auto pre = [&]() {
-    if constexpr (ADAM) {
+    if constexpr (ADAM && CORE == 1) {
+      const sbuf_i4 r = s_rsrc(af.sc);
+      const uint32_t o = (uint32_t)(offsetof(DevScalars, beta_pow) + d.adam_step * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) skw[q] = s_ld(r, o + 4u * q);
+      skw[4] = s_ld(r, (uint32_t)offsetof(DevScalars, err));
+    } else if constexpr (ADAM) {
       if (threadIdx.x == 0) {
         s_k = fuse_scalars(af, d.adam_step, af.step_offset);
         s_err = af.sc->err;
@@ -1124,7 +1461,10 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   constexpr int PIPE = (SACMI_PIPE && G == 1 && !ADAM && AXK == 0) ? 1
                      : (SACMI_PIPE_DW && G == 1 && ADAM && MG == 2) ? 2 : 0;
   SACMI_PHASE(batch.tl, 1);
-  gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
+  if constexpr (CORE == 1)
+    gemm_core_stg<TM, TN, KSPLIT, MG, AXK>(d, m0, n0, ring, rsum, s_kw, rowsum, pre);
+  else
+    gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   SACMI_PHASE(batch.tl, 2);
   SACMI_PHASE_LAST(batch.tl, 7);
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
@@ -1149,8 +1489,15 @@ __global__ __launch_bounds__(64 * KSPLIT * MG, (gemm_min_waves<KSPLIT * MG>())) 
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
   // a non-finite policy sample / PER draw of this update (ErrBits): the reference raised
   // before this step (no stores), or after the critic step but before Polyak
-  const int err = ADAM ? s_err : 0;
-  const AdamScalars k_ad = s_k;
+  int err = ADAM ? s_err : 0;
+  AdamScalars k_ad = s_k;
+  if constexpr (ADAM && CORE == 1) {
+    double p1 = __longlong_as_double((long long)((uint64_t)skw[0] | ((uint64_t)skw[1] << 32)));
+    double p2 = __longlong_as_double((long long)((uint64_t)skw[2] | ((uint64_t)skw[3] << 32)));
+    if (af.step_offset) { p1 *= (double)af.beta1; p2 *= (double)af.beta2; }
+    k_ad = AdamScalars{(float)((double)af.lr / (1.0 - p1)), (float)sqrt(1.0 - p2)};
+    err = (int)skw[4];
+  }
   const bool void_st = ADAM && (err & af.err_skip) != 0;
   const bool pol_st = pol && (err & af.err_nopolyak) == 0;
   if constexpr (ADAM) {
@@ -2651,6 +2998,31 @@ static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
   else hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, false>), dim3(grid), blk, 0, s, b);
 }
 
+// the LDS-staged core (CORE 1), 1024 threads
+template <int TM, int TN, int KSP, int MG, bool ADAM, int AXK>
+static void launch_ks(const GemmBatch& b, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((k_gemm<TM, TN, KSP, 1, MG, ADAM, AXK, false, 1>), dim3(grid), dim3(1024), 0, s, b);
+}
+
+// whether a level can take the staged core: fp32 operands, 16-byte-aligned rows, every
+// 16-byte chunk a DMA lane reads inside its row (KC: ld >= round4(K); MN: ld >= round4(M|N)),
+// and the K vector it stages (ax_w / a_ksc) within kStgKW
+#ifndef SACMI_STAGED
+#define SACMI_STAGED 0
+#endif
+static bool staged_ok(const GemmBatch& b) {
+  static const bool env = SACMI_STAGED && std::getenv("SACMI_NO_STAGED") == nullptr;
+  if (!env || b.bf16) return false;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    if (d.a16 || d.b16 || d.c16 || d.x16) return false;
+    if (d.K < 1 || d.K > kStgKW || d.M < 1 || d.N < 1) return false;
+    if (((uintptr_t)d.A & 15) || ((uintptr_t)d.B & 15) || (d.lda & 3) || (d.ldb & 3)) return false;
+    if (d.lda < round_up(d.a_kc ? d.K : d.M, 4) || d.ldb < round_up(d.b_kc ? d.K : d.N, 4)) return false;
+  }
+  return true;
+}
+
 // every desc's B operand has a bf16 shadow (SACMI_BF16_SHADOW 0: never read them)
 #ifndef SACMI_BF16_SHADOW
 #define SACMI_BF16_SHADOW 1
@@ -2818,6 +3190,29 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   bool dw = true;
   for (int i = 0; i < b.count; ++i) dw = dw && !b.d[i].a_kc && !b.d[i].b_kc;
   const int t64 = assign_tiles<32, 64>(b);
+  // the batch-256 class on the LDS-staged core (same tile geometries as below)
+  if (staged_ok(b) && (dw || (!n_adam && t64 <= 512))) {
+    if (dw && t64 <= 256) {
+      if (n_adam) launch_ks<32, 64, 8, 1, true, 0>(b, b.total_tiles + extra, s);
+      else launch_ks<32, 64, 8, 1, false, 0>(b, b.total_tiles + extra, s);
+    } else if (dw) {
+      for (int i = 0; i < b.count; ++i)
+        if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a 64-row tile level"};
+      const int g = assign_tiles<64, 64>(b) + extra;
+      if (n_adam) launch_ks<32, 64, 4, 2, true, 0>(b, g, s);
+      else launch_ks<32, 64, 4, 2, false, 0>(b, g, s);
+    } else if (axk == 1) {
+      const int g = assign_tiles<32, 32>(b) + extra;
+      launch_ks<32, 32, 8, 1, false, 1>(b, g, s);
+    } else if (t64 >= 192) {
+      launch_ks<32, 64, 8, 1, false, 0>(b, b.total_tiles + extra, s);
+    } else {
+      const int g = assign_tiles<32, 32>(b) + extra;
+      launch_ks<32, 32, 8, 1, false, 0>(b, g, s);
+    }
+    HIP_LAUNCH_CHECK();
+    return;
+  }
   if (dw && t64 <= 256) {
     // one 32x64 tile per CU (policy level): 16 waves, K split 16 ways
     if (n_adam) launch_k<32, 64, 16, 1, 1, true, 0>(b, b.total_tiles + extra, s);

@@ -139,7 +139,7 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> hp[3], hq[3], hqt[3], hqa[3];
   // backward: critic dh per hidden layer ([nh-1] = the on-the-fly head-layer rows u,
   // stored for the weight gradient), actor-pass critic dh (layers 0..nh-2), policy dh
-  sacmi::DevBuf<float> dq, dhead, dhc[3], dha[3], dhp[3];
+  sacmi::DevBuf<float> dq, dq4, dhead, dhc[3], dha[3], dhp[3];
   sacmi::DevBuf<float> dotp;       // fc3 dot partials [6 slots][B][nparts]
   sacmi::DevBuf<float> pa;         // dL/da partials [2 * nparts][B][A] (L9 epilogue -> tail)
   sacmi::DevBuf<float> act_h;      // select_action's one-state hidden rows [nh][Hd] (1 at H)
@@ -366,6 +366,7 @@ static void alloc_all(sacmi_ctx* c) {
   c->cache.alloc((size_t)2 * Bm * 3 * A);
   c->logp.alloc((size_t)2 * Bm);
   c->dq.alloc((size_t)2 * Bm + 16);   // + slack: the split-K dW kernels read 4 wide (kernels.hip)
+  c->dq4.alloc((size_t)2 * Bm * 4);    // dq one value per 16-byte row (pads stay 0)
   c->nparts = (H + 31) / 32;
   // split-K dW partials (kernels.hip; bf16 only: the fp32 levels measured slower split)
   if (c->bf16 && Bm >= 2048) c->dw_ws.alloc((size_t)16 * c->total);
@@ -924,7 +925,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       rf.kind = 1; rf.part = dotp(0); rf.nparts = c->nparts; rf.B = B;
       rf.r = bb.r; rf.d = bb.d; rf.logp = c->logp.p; rf.logp_a = c->logp.p + B;
       rf.gamma = (float)c->cfg.gamma;
-      rf.sc = c->sc.p; rf.dq = c->dq.p; rf.loss_part = c->lpart_c.p;
+      rf.sc = c->sc.p; rf.dq = c->dq.p; rf.dq4 = c->dq4.p; rf.loss_part = c->lpart_c.p;
     }
     run(l5, "gemm_L5_critic_dh1");
     // L5b (3 hidden layers): dh[l-1] = (dh[l] W[l]) * relu'(h[l-1]) down to dh[0]
@@ -957,7 +958,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
                                 dst(q[i][L]), Hd, H, H, B, wepi, 1 + i));
       wl.a_ksc = c->dq.p + i * B;
       l6.add(wl);
-      l6.add(dwx(gd_dw_h(c->dq.p + i * B, 1, E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, dst(q[i][nh]), Hd, 1, H, B,
+      l6.add(dwx(gd_dw_h(c->dq4.p + (size_t)i * B * 4, 4, E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, dst(q[i][nh]), Hd, 1, H, B,
                          wepi, 1 + i)));
     }
     if (fuse) {
@@ -1538,7 +1539,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
                     &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->xqb, &c->x2b, &c->rb,
                     &c->db, &c->eps,
-                    &c->cache, &c->logp, &c->dq, &c->dotp, &c->pa, &c->act_h, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
+                    &c->cache, &c->logp, &c->dq, &c->dq4, &c->dotp, &c->pa, &c->act_h, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
                     &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr, &c->per_probs,
                     &c->per_chunk, &c->per_w, &c->per_val})
       b->release();

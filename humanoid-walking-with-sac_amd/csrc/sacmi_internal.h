@@ -384,6 +384,8 @@ struct RowsFuse {
   int auto_entropy;
   DevScalars* sc;
   float* dq;                 // [2][B] out: the per-row head gradients (read by later levels)
+  float* dq4;                // [2][B][4]: the same, one per 16-byte row (column 0; the fc3
+                             //   weight gradient's A operand: 16-byte rows for the staged core)
   float* loss_part;          // critic [row blocks][2] squared errors; actor [row blocks]
   // actor: dL/dlog_alpha = -mean(logp_a + te) (sac_imp.py:128-133) from the heads
   // kernel's per-workgroup logp sums (slot 1 of each of n_lp workgroups)

@@ -24,7 +24,12 @@ from oracle.sac_step import NETS, OracleSAC, SacConfig, init_params, param_shape
 pytestmark = pytest.mark.gpu
 
 LOSS_TOL = 1e-5
-GRAD_TOL = 5e-5
+# gradients, per tensor normwise vs fp64: 1e-5 at batch <= 1024 on
+# well-conditioned inputs, or 4x the reference's own fp32 deviation where that is larger;
+# the achieved errors are printed (and appended to $SACMI_GRAD_TABLE as JSON lines)
+GRAD_TOL = 1e-5
+# batch 4096 (allow_flips): 5e-5 before the flip allowances below
+GRAD_TOL_B4096 = 5e-5
 # batch 4096: a few of the ~2-4 M ReLU pre-activations land within fp32 rounding of zero,
 # and WHICH ones flip against fp64 depends on the fp32 summation order; a flipped mask
 # bit in a deep layer perturbs every shallower layer's gradient through the chain (the
@@ -181,6 +186,20 @@ def check_delta_vs_reference(d_gpu, d_o64, ref, what):
     assert e_g <= 4 * e_o + 1e-4, (what, "delta", e_g, e_o)
 
 
+def report_grad_errors(name, tol, table):
+    """Print the achieved per-tensor gradient errors (GPU vs fp64, and the reference's own
+    fp32 vs fp64) and append them to $SACMI_GRAD_TABLE when set."""
+    print(f"\n[grad errors] {name} (bar {tol:g} or 4x fp32 ref)")
+    for k, (e, e_ref) in sorted(table.items()):
+        print(f"  {k:28s} gpu {e:9.3e}  fp32-ref {e_ref:9.3e}  {'ok' if e <= max(tol, 4 * e_ref) else 'OVER'}")
+    path = os.environ.get("SACMI_GRAD_TABLE")
+    if path:
+        import json
+        with open(path, "a") as f:
+            f.write(json.dumps({"case": name, "bar": tol,
+                                "tensors": {k: {"gpu": e, "fp32_ref": r} for k, (e, r) in table.items()}}) + "\n")
+
+
 def check_step(res, prev, name, allow_flips=False):
     lg, sg, gg = res["gpu"]
     l32, s32, g32 = res["o32"]
@@ -188,13 +207,17 @@ def check_step(res, prev, name, allow_flips=False):
     for i, k in enumerate(("q1_loss", "q2_loss", "policy_loss")):
         assert abs(lg[i] - l64[k]) <= LOSS_TOL * max(abs(l64[k]), 1e-3), (name, k, lg[i], l64[k])
     bad = {}
+    tol = GRAD_TOL_B4096 if allow_flips else GRAD_TOL
+    table = {}
     for k, v in g64.items():
         # the bar, or 4x the reference's own fp32 deviation where that is larger
         e, e_ref = rel(gg[k], v), rel(g32[k], v)
-        if e > max(GRAD_TOL, 4 * e_ref):
-            if allow_flips and (rel_without_flips(gg[k], v) <= GRAD_TOL or e <= GRAD_TOL_FLIPS):
+        table[k] = (e, e_ref)
+        if e > max(tol, 4 * e_ref):
+            if allow_flips and (rel_without_flips(gg[k], v) <= tol or e <= GRAD_TOL_FLIPS):
                 continue
             bad[k] = (e, e_ref)
+    report_grad_errors(name, tol, table)
     assert not bad, (name, "grad", bad)
     for k in sg:
         p0 = prev.get(k, np.zeros(1))            # log_alpha starts at 0 (sac_imp.py:49)
@@ -227,7 +250,7 @@ def check_step(res, prev, name, allow_flips=False):
         al = res["alpha"]
         for key in ("adam.log_alpha.m", "adam.log_alpha.v"):
             want = float(np.asarray(s64[key]).reshape(-1)[0])
-            assert abs(al[key] - want) <= GRAD_TOL * abs(want) + 1e-12, (name, key, al[key], want)
+            assert abs(al[key] - want) <= GRAD_TOL_B4096 * abs(want) + 1e-12, (name, key, al[key], want)
         a64 = float(s64["alpha"])
         assert abs(al["alpha"] - a64) <= LOSS_TOL * a64, (name, "alpha", al["alpha"], a64)
         st64 = float(np.asarray(s64["adam.policy.step"]))
