@@ -3011,7 +3011,9 @@ static void launch_ks(const GemmBatch& b, int grid, hipStream_t s) {
 #define SACMI_STAGED 0
 #endif
 static bool staged_ok(const GemmBatch& b) {
-  static const bool env = SACMI_STAGED && std::getenv("SACMI_NO_STAGED") == nullptr;
+  // $SACMI_STAGED=0/1 overrides the build default; SACMI_NO_STAGED forces it off
+  static const bool env = std::getenv("SACMI_NO_STAGED") == nullptr &&
+                          (std::getenv("SACMI_STAGED") ? std::atoi(std::getenv("SACMI_STAGED")) != 0 : SACMI_STAGED != 0);
   if (!env || b.bf16) return false;
   for (int i = 0; i < b.count; ++i) {
     const GemmDesc& d = b.d[i];
@@ -3860,6 +3862,28 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  HIP_LAUNCH_CHECK();
+}
+
+__global__ __launch_bounds__(256) void k_polyak(PolyakArgs a) { polyak_ride(a, blockIdx.x, gridDim.x); }
+void launch_polyak(const PolyakArgs& a, hipStream_t s) {
+  int64_t blocks = (a.n4 + 511) / 512;     // polyak_ride: 2 groups per thread per pass
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_polyak, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  HIP_LAUNCH_CHECK();
+}
+
+// the alpha step's visible result (k_adam block 0: sac_imp.py:135) on every rank of a sharded
+// data-parallel update, from the all-gathered log_alpha
+__global__ void k_alpha_sync(DevScalars* sc, const float* log_alpha, int err_skip) {
+  if (threadIdx.x == 0 && (sc->err & err_skip) == 0) {
+    sc->alpha = expf(*log_alpha);
+    sc->alpha_is_tensor = 1;
+  }
+}
+void launch_alpha_sync(DevScalars* sc, const float* log_alpha, int err_skip, hipStream_t s) {
+  hipLaunchKernelGGL(k_alpha_sync, dim3(1), dim3(64), 0, s, sc, log_alpha, err_skip);
   HIP_LAUNCH_CHECK();
 }
 

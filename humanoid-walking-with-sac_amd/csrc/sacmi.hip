@@ -214,7 +214,12 @@ struct sacmi_ctx {
   // native data parallel (sacmi_allreduce_init / sacmi_step_dp)
   ncclComm_t comm = nullptr;
   int dp_world = 0;
+  int dp_rank = 0;
   bool dp_loopback = false;   // sacmi_dp_loopback_init: x world in place of the all-reduce
+  // sharded optimizer step (ZeRO-1): reduce-scatter the gradients, Adam on this rank's
+  // 1/world of the parameters, all-gather the parameters (enqueue_dp)
+  bool dp_shard = false;
+  bool dp_sharding_now = false;   // enqueue_dp is enqueueing a sharded sequence
   std::map<std::tuple<int, int, int64_t>, hipGraphExec_t> dp_graphs;   // (batch, n, PER fill)
   uint64_t act_calls = 0;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
   // profiling (sacmi_profile_step): one event per launch site
@@ -317,7 +322,10 @@ static Linear find_linear(const sacmi_ctx* c, int net, int layer) {
 
 static void alloc_all(sacmi_ctx* c) {
   const int Bm = c->Bm, S = c->S, A = c->A, H = c->H;
-  c->P.alloc(c->total); c->G.alloc(c->total); c->M.alloc(c->total); c->V.alloc(c->total);
+  // P and G carry kShardSlack floats past the layout: the sharded data-parallel step's
+  // last chunk of the actor range (chunks of 64-float multiples) reaches past `total`
+  c->P.alloc(c->total + kShardSlack); c->G.alloc(c->total + kShardSlack);
+  c->M.alloc(c->total); c->V.alloc(c->total);
   c->T.alloc(c->q_end);
   if (c->bf16) { c->Ph.alloc(c->total); c->Th.alloc(c->q_end); }
   c->sc.alloc(1);
@@ -792,6 +800,48 @@ static void enqueue_sample_gather(sacmi_ctx* c, int B, int parity, bool dev_idx,
   }
 }
 
+// The data-parallel Adam step of one range over the whole range: critic (+ Polyak, + the q
+// losses) or actor (+ the alpha step, policy loss, loss ring), grad_scale = 1/world
+static AdamArgs dp_adam_args(sacmi_ctx* c, bool critic, int B, float grad_scale, bool use_ring) {
+  AdamArgs ad{};
+  ad.p = c->P.p; ad.g = c->G.p; ad.m = c->M.p; ad.v = c->V.p;
+  ad.nseg = 0;
+  const int nh = c->nh, nb = (B + 31) / 32;
+  auto seg = [&](const Linear& l, int idx) {
+    REQUIRE(ad.nseg < kMaxAdamSegs, SACMI_ESTATE, "too many Adam segments");
+    ad.seg[ad.nseg++] = AdamSeg{l.off, l.numel_padded(), idx};
+  };
+  if (critic) {
+    for (int layer = 0; layer <= nh; ++layer)
+      for (int i = 0; i < 2; ++i) seg(c->q_fc[i][layer], i == 0 ? 1 : 2);
+  } else {
+    for (int l = 0; l <= nh; ++l) seg(l < nh ? c->p_fc[l] : c->p_head, 0);
+  }
+  ad.total = 0;
+  for (int i = 0; i < ad.nseg; ++i) {
+    REQUIRE(ad.seg[i].n % 4 == 0 && ad.seg[i].off % 4 == 0, SACMI_ESTATE, "Adam segment not float4-aligned");
+    ad.total += ad.seg[i].n;
+  }
+  ad.lr = (float)c->cfg.lr; ad.beta1 = 0.9f; ad.beta2 = 0.999f; ad.eps = 1e-8f; ad.grad_scale = grad_scale;
+  ad.sc = c->sc.p; ad.n_part = nb; ad.loss_div = (float)B;
+  // the bf16 shadows of the updated parameters / targets (read by the bf16 level kernels)
+  ad.ph = c->Ph.p; ad.tgth = c->Th.p;
+  if (critic) {
+    ad.tgt = c->T.p; ad.tgt_base = c->q_begin;
+    ad.tau = (float)c->cfg.tau; ad.step_offset = 1;
+    ad.loss_part = c->lpart_c.p; ad.loss_slot0 = 0; ad.n_losses = 2;
+    ad.log_alpha_idx = -1; ad.auto_entropy = 0;
+    ad.err_skip = kErrSkipAll; ad.err_nopolyak = ERR_NAN_ACT;
+  } else {
+    ad.tgt = nullptr; ad.tau = 0.f; ad.step_offset = 0;
+    ad.loss_part = c->lpart_a.p; ad.loss_slot0 = 2; ad.n_losses = 1;
+    ad.log_alpha_idx = c->la_idx; ad.auto_entropy = c->cfg.auto_entropy;
+    ad.loss_ring = use_ring ? c->ring.p : nullptr; ad.ring = c->ring_slots;
+    ad.err_skip = ~0; ad.err_nopolyak = 0;
+  }
+  return ad;
+}
+
 // parity: which batch buffer set this update uses; have_batch: its indices and rows
 // were produced by the previous update's ride-along work; ride_next: produce the next
 // update's (into the other set) inside this update's L11 / L13 launches.
@@ -851,8 +901,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
 
   // fused updates whose policy dhp1 level (L12) leaves CUs idle on k_gemm: Polyak rides there
   static const bool pk_env = std::getenv("SACMI_NO_POLYAK_RIDE") == nullptr;
-  const bool polyak_ride = phase_mask == 7 && pk_env && !act16 &&
-                           (int64_t)((B + 31) / 32) * ((H + 31) / 32) <= 192;
+  const bool polyak_ride = (phase_mask == 7 || (c->dp_sharding_now && (phase_mask & 2))) && pk_env &&
+                           !act16 && (int64_t)((B + 31) / 32) * ((H + 31) / 32) <= 192;
   if (phase_mask & 1) {
     if (!have_batch)   // (have_batch: the previous update's rides / side stream produced them)
       enqueue_sample_gather(c, B, parity, dev_idx != 0, s);
@@ -981,33 +1031,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     }
     run(l6, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1");
   }
-  const float lr = (float)c->cfg.lr;
   if (phase_mask & 2) {
    const bool fuse = phase_mask == 7;
-   if (!fuse) {
+   if (!fuse && !c->dp_sharding_now) {   // (sharded: enqueue_dp takes the critic step)
     // critic Adam (+ Polyak, + q-loss finalisation)
-    AdamArgs ad{};
-    ad.p = P; ad.g = G; ad.m = c->M.p; ad.v = c->V.p; ad.tgt = c->T.p; ad.tgt_base = c->q_begin;
-    ad.nseg = 0;
-    for (int layer = 0; layer <= nh; ++layer)
-      for (int i = 0; i < 2; ++i) {
-        const Linear& l = q[i][layer];
-        REQUIRE(ad.nseg < kMaxAdamSegs, SACMI_ESTATE, "too many Adam segments");
-        ad.seg[ad.nseg++] = AdamSeg{l.off, l.numel_padded(), i == 0 ? 1 : 2};
-      }
-    ad.total = 0;
-    for (int i = 0; i < ad.nseg; ++i) {
-      REQUIRE(ad.seg[i].n % 4 == 0 && ad.seg[i].off % 4 == 0, SACMI_ESTATE, "Adam segment not float4-aligned");
-      ad.total += ad.seg[i].n;
-    }
-    ad.lr = lr; ad.beta1 = 0.9f; ad.beta2 = 0.999f; ad.eps = 1e-8f; ad.grad_scale = grad_scale;
-    ad.tau = (float)c->cfg.tau; ad.step_offset = 1; ad.sc = c->sc.p;
-    ad.loss_part = c->lpart_c.p; ad.n_part = nb; ad.loss_slot0 = 0; ad.n_losses = 2;
-    ad.loss_div = (float)B; ad.log_alpha_idx = -1; ad.auto_entropy = 0;
-    // the bf16 shadows of the updated critics and targets (read by the bf16 level kernels
-    // of L7 on: without them the data-parallel bf16 update read stale critic weights)
-    ad.ph = c->Ph.p; ad.tgth = c->Th.p;
-    ad.err_skip = kErrSkipAll; ad.err_nopolyak = ERR_NAN_ACT;
+    AdamArgs ad = dp_adam_args(c, true, B, grad_scale, use_ring);
     if (mark(c, "adam_critic_polyak")) {
       ad.tl = c->tl_cur;
       launch_adam(ad, s);
@@ -1156,25 +1184,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     run(l13, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1");
   }
   if ((phase_mask & 4) && phase_mask != 7) {
-    AdamArgs ad{};
-    ad.p = P; ad.g = G; ad.m = c->M.p; ad.v = c->V.p; ad.tgt = nullptr;
-    ad.nseg = 0;
-    for (int l = 0; l <= nh; ++l) {
-      const Linear& lin = l < nh ? c->p_fc[l] : c->p_head;
-      ad.seg[ad.nseg++] = AdamSeg{lin.off, lin.numel_padded(), 0};
-    }
-    ad.total = 0;
-    for (int i = 0; i < ad.nseg; ++i) {
-      REQUIRE(ad.seg[i].n % 4 == 0 && ad.seg[i].off % 4 == 0, SACMI_ESTATE, "Adam segment not float4-aligned");
-      ad.total += ad.seg[i].n;
-    }
-    ad.lr = lr; ad.beta1 = 0.9f; ad.beta2 = 0.999f; ad.eps = 1e-8f; ad.grad_scale = grad_scale;
-    ad.tau = 0.f; ad.step_offset = 0; ad.sc = c->sc.p;
-    ad.loss_part = c->lpart_a.p; ad.n_part = nb; ad.loss_slot0 = 2; ad.n_losses = 1;
-    ad.loss_div = (float)B; ad.log_alpha_idx = c->la_idx; ad.auto_entropy = c->cfg.auto_entropy;
-    ad.loss_ring = use_ring ? c->ring.p : nullptr; ad.ring = c->ring_slots;
-    ad.ph = c->Ph.p; ad.tgth = c->Th.p;
-    ad.err_skip = ~0; ad.err_nopolyak = 0;
+    AdamArgs ad = dp_adam_args(c, false, B, grad_scale, use_ring);
     if (mark(c, "adam_actor_alpha")) {
       ad.tl = c->tl_cur;
       launch_adam(ad, s);
@@ -1374,6 +1384,8 @@ struct RcclApi {
   decltype(&ncclGetUniqueId) get_id = nullptr;
   decltype(&ncclCommInitRank) init_rank = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclGetErrorString) err = nullptr;
 };
@@ -1400,6 +1412,8 @@ static RcclApi& rccl() {
   r.get_id = reinterpret_cast<decltype(r.get_id)>(sym("ncclGetUniqueId"));
   r.init_rank = reinterpret_cast<decltype(r.init_rank)>(sym("ncclCommInitRank"));
   r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(sym("ncclAllReduce"));
+  r.reduce_scatter = reinterpret_cast<decltype(r.reduce_scatter)>(sym("ncclReduceScatter"));
+  r.all_gather = reinterpret_cast<decltype(r.all_gather)>(sym("ncclAllGather"));
   r.destroy = reinterpret_cast<decltype(r.destroy)>(sym("ncclCommDestroy"));
   r.err = reinterpret_cast<decltype(r.err)>(sym("ncclGetErrorString"));
   r.h = h;
@@ -1416,7 +1430,120 @@ static RcclApi& rccl() {
 // sacmi/dp.py (DataParallelUpdate over one uninterrupted sequence) with the two
 // all-reduces per update issued here — sum in place on the gradient arena, 1/world
 // applied by the Adam kernels.
+// Sharded (ZeRO-1) form, per range [b, e) of the arena (critic, then actor): the gradients
+// are reduce-scattered in place into chunk r (kShardAlign-float multiples; the last chunk may
+// reach past e — into the next range's gradients, rewritten by its own level later, or into
+// the arena slack), Adam runs on chunk r of the parameters (the layer segments clipped to
+// it), and the parameters are all-gathered in place.  Replicas stay bitwise identical: every
+// chunk is computed by one rank and the gather copies its bits.  Adam moments (M, V) are
+// valid on each rank's own chunks only (sacmi_dp_sync_state gathers them, e.g. before a
+// checkpoint).  Loopback: `world` identical ranks emulated on one GPU — the gradients x world
+// in place, Adam on every rank's chunk in turn (rank 0 alone finalises the losses / ring),
+// the gather an identity.
+#ifndef SACMI_DP_SHARD_DEFAULT
+#define SACMI_DP_SHARD_DEFAULT 0
+#endif
+static bool dp_shard_default(int world) {
+  if (const char* e = std::getenv("SACMI_DP_SHARD")) return std::atoi(e) != 0 && world <= kMaxShardWorld;
+  return SACMI_DP_SHARD_DEFAULT && world >= 2 && world <= kMaxShardWorld;
+}
+
+static int64_t shard_chunk(int64_t n, int world) {
+  return round_up64((n + world - 1) / world, kShardAlign);
+}
+
+static void dp_shard_adam(sacmi_ctx* c, bool critic, int B, int r, bool use_ring) {
+  const int W = c->dp_world;
+  const int64_t b = critic ? c->q_begin : c->pi_begin, e = critic ? c->q_end : c->total;
+  const int64_t ch = shard_chunk(e - b, W), lo = b + r * ch, hi = std::min(e, lo + ch);
+  AdamArgs ad = dp_adam_args(c, critic, B, 1.f / (float)W, use_ring);
+  ad.tgt = nullptr; ad.tgth = nullptr;   // Polyak: its own pass over the gathered critics
+  const AdamArgs full = ad;
+  ad.nseg = 0; ad.total = 0;
+  for (int i = 0; i < full.nseg; ++i) {
+    const int64_t s0 = std::max(full.seg[i].off, lo), s1 = std::min(full.seg[i].off + full.seg[i].n, hi);
+    if (s1 > s0) {
+      ad.seg[ad.nseg++] = AdamSeg{s0, s1 - s0, full.seg[i].step_idx};
+      ad.total += s1 - s0;
+    }
+  }
+  if (!critic && !(c->la_idx >= lo && c->la_idx < hi)) ad.log_alpha_idx = -1;   // (its owner's)
+  if (r != c->dp_rank) { ad.n_losses = 0; ad.loss_ring = nullptr; }   // (loopback's other ranks)
+  launch_adam(ad, c->stream);
+}
+
+static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
+  const int W = c->dp_world;
+  const bool ride = n > 1 && ride_possible(c, B);
+  hipStream_t s = c->stream;
+  auto range = [&](bool critic, int64_t& b, int64_t& e) {
+    b = critic ? c->q_begin : c->pi_begin;
+    e = critic ? c->q_end : c->total;
+  };
+  auto reduce_scatter = [&](bool critic) {
+    (void)mark(c, critic ? "reduce_scatter_critic_grads" : "reduce_scatter_actor_grads");
+    int64_t b, e;
+    range(critic, b, e);
+    const int64_t ch = shard_chunk(e - b, W);
+    float* g = c->G.p + b;
+    if (c->dp_loopback) launch_scale(g, e - b, (float)W, s);
+    else CHECK_RCCL(rccl().reduce_scatter(g, g + c->dp_rank * ch, (size_t)ch, ncclFloat32, ncclSum, c->comm, s));
+  };
+  auto step = [&](bool critic) {   // Adam on the chunk(s), gather, the replicated scalars / shadows
+    (void)mark(c, critic ? "adam_critic_shard" : "adam_actor_shard");
+    if (c->dp_loopback) {
+      for (int r = 0; r < W; ++r) dp_shard_adam(c, critic, B, r, true);
+    } else {
+      dp_shard_adam(c, critic, B, c->dp_rank, true);
+    }
+    int64_t b, e;
+    range(critic, b, e);
+    const int64_t ch = shard_chunk(e - b, W);
+    (void)mark(c, critic ? "all_gather_critic_params" : "all_gather_actor_params");
+    if (!c->dp_loopback) {
+      float* p = c->P.p + b;
+      CHECK_RCCL(rccl().all_gather(p + c->dp_rank * ch, p, (size_t)ch, ncclFloat32, c->comm, s));
+    }
+    if (c->Ph.p) launch_to_bf16(c->Ph.p + b, c->P.p + b, e - b, s);
+    if (!critic && c->cfg.auto_entropy) launch_alpha_sync(c->sc.p, c->P.p + c->la_idx, ~0, s);
+  };
+  // Polyak rides in phase 1's L12 where it can (enqueue_update: polyak_ride), else its own pass
+  const bool pk_ride = std::getenv("SACMI_NO_POLYAK_RIDE") == nullptr && !act16_on(c, B) &&
+                       (int64_t)((B + 31) / 32) * ((c->H + 31) / 32) <= 192;
+  c->dp_sharding_now = true;
+  try {
+    int parity = 0;
+    bool have = false;
+    for (int r = 0; r < n; ++r) {
+      if (r > 0) step(false);                                             // previous actor step
+      enqueue_update(c, B, 1, 1, 1, 1.f, true, parity, have);             // phase 0
+      reduce_scatter(true);
+      step(true);
+      if (!pk_ride && mark(c, "polyak")) {
+        PolyakArgs pk{};
+        pk.T = c->T.p; pk.P = c->P.p + c->q_begin; pk.Th = c->Th.p;
+        pk.n4 = (c->q_end - c->q_begin) / 4; pk.tau = (float)c->cfg.tau; pk.sc = c->sc.p;
+        launch_polyak(pk, s);
+      }
+      const bool rn = ride && r + 1 < n;
+      enqueue_update(c, B, 1, 1, 2, 1.f, true, parity, false, rn);        // phase 1 (no critic Adam)
+      reduce_scatter(false);
+      have = rn;
+      parity = rn ? parity ^ 1 : 0;
+    }
+    step(false);
+  } catch (...) {
+    c->dp_sharding_now = false;
+    throw;
+  }
+  c->dp_sharding_now = false;
+}
+
 static void enqueue_dp(sacmi_ctx* c, int B, int n) {
+  if (c->dp_shard) {
+    enqueue_dp_sharded(c, B, n);
+    return;
+  }
   const float scale = 1.f / (float)c->dp_world;
   const bool ride = n > 1 && ride_possible(c, B);
   auto allreduce = [&](int64_t begin, int64_t end) {
@@ -2223,6 +2350,8 @@ int sacmi_allreduce_init(sacmi_ctx* c, const void* id, int32_t nbytes, int32_t r
     CHECK_RCCL(rccl().init_rank(&comm, world, uid, rank));
     c->comm = comm;
     c->dp_world = world;
+    c->dp_rank = rank;
+    c->dp_shard = dp_shard_default(world);
   });
 }
 
@@ -2233,7 +2362,9 @@ int sacmi_dp_loopback_init(sacmi_ctx* c, int32_t world) {
     REQUIRE(world >= 1 && world <= 1024, SACMI_EVALUE, "world must be in [1, 1024]");
     REQUIRE(!c->comm, SACMI_ESTATE, "communicator already initialised");
     c->dp_world = world;
+    c->dp_rank = 0;
     c->dp_loopback = true;
+    c->dp_shard = dp_shard_default(world);
     destroy_graphs(c);
   });
 }
@@ -2245,6 +2376,14 @@ int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
     REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
     check_device_batch(c, batch);
     REQUIRE(n_updates >= 1 && n_updates <= 256, SACMI_EVALUE, "n_updates must be in [1, 256]");
+    // one rank: nothing to reduce — the fused update (bit-identical to the phase sequence:
+    // test_dp_* world-1 and loopback tests), unless SACMI_DP_PHASES_AT_WORLD1 asks for the
+    // phase sequence and its collectives anyway
+    static const bool phases1 = std::getenv("SACMI_DP_PHASES_AT_WORLD1") != nullptr;
+    if (c->dp_world == 1 && !c->dp_loopback && !phases1) {
+      run_update(c, batch, 1, 1, 7, 1.f, true, n_updates);
+      return;
+    }
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     CHECK_HIP(hipStreamIsCapturing(c->stream, &cap));
     if (!c->use_graphs || cap != hipStreamCaptureStatusNone) {
@@ -2273,6 +2412,43 @@ int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
   });
 }
 
+int sacmi_dp_set_sharded(sacmi_ctx* c, int32_t on) {
+  return guard([&] {
+    pf_touch(c);
+    REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
+    REQUIRE(!on || c->dp_world <= kMaxShardWorld, SACMI_EVALUE, "sharded step: world > 64");
+    c->dp_shard = on != 0;
+    for (auto& kv : c->dp_graphs) (void)hipGraphExecDestroy(kv.second);
+    c->dp_graphs.clear();
+  });
+}
+
+int sacmi_dp_sync_state(sacmi_ctx* c) {
+  return guard([&] {
+    pf_touch(c);
+    REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
+    if (!c->dp_shard || c->dp_loopback || c->dp_world == 1) return;
+    // every rank's chunks of the Adam moments, in place (M and V carry no slack: the last
+    // chunk is gathered through a bounce of the padded size)
+    const int W = c->dp_world;
+    for (int critic = 1; critic >= 0; --critic) {
+      const int64_t b = critic ? c->q_begin : c->pi_begin, e = critic ? c->q_end : c->total;
+      const int64_t ch = shard_chunk(e - b, W);
+      DevBuf<float> tmp;
+      tmp.alloc((size_t)ch * W);
+      for (float* arena : {c->M.p, c->V.p}) {
+        const int64_t lo = b + c->dp_rank * ch, hi = std::min(e, lo + ch);
+        if (hi > lo) CHECK_HIP(hipMemcpyAsync(tmp.p + c->dp_rank * ch, arena + lo, (size_t)(hi - lo) * 4,
+                                              hipMemcpyDeviceToDevice, c->stream));
+        CHECK_RCCL(rccl().all_gather(tmp.p + c->dp_rank * ch, tmp.p, (size_t)ch, ncclFloat32, c->comm, c->stream));
+        CHECK_HIP(hipMemcpyAsync(arena + b, tmp.p, (size_t)(e - b) * 4, hipMemcpyDeviceToDevice, c->stream));
+      }
+      CHECK_HIP(hipStreamSynchronize(c->stream));
+      tmp.release();
+    }
+  });
+}
+
 int sacmi_step_act16(sacmi_ctx* c, int32_t batch, int32_t* out) {
   return guard([&] {
     pf_touch(c); *out = act16_on(c, batch) ? 1 : 0; });
@@ -2283,13 +2459,13 @@ int sacmi_step_ride_possible(sacmi_ctx* c, int32_t batch, int32_t* out) {
 }
 
 int sacmi_grad_arena_numel(sacmi_ctx* c, int64_t* numel) {
-  return guard([&] { *numel = c->total; });
+  return guard([&] { *numel = c->total + kShardSlack; });
 }
 
 int sacmi_attach_grad_arena(sacmi_ctx* c, void* ptr, int64_t numel) {
   return guard([&] {
     pf_touch(c);
-    REQUIRE(ptr && numel == c->total, SACMI_EVALUE, "grad arena must hold exactly grad_arena_numel floats");
+    REQUIRE(ptr && numel == c->total + kShardSlack, SACMI_EVALUE, "grad arena must hold exactly grad_arena_numel floats");
     REQUIRE(((uintptr_t)ptr & 15) == 0, SACMI_EVALUE, "grad arena must be 16-byte aligned");
     CHECK_HIP(hipStreamSynchronize(c->stream));
     CHECK_HIP(hipMemset(ptr, 0, (size_t)numel * 4));

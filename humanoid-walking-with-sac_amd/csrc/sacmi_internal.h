@@ -533,6 +533,19 @@ struct AdamArgs {
 };
 void launch_adam(const AdamArgs& a, hipStream_t s);
 
+// Sharded data-parallel optimizer step (sacmi.hip enqueue_dp, ZeRO-1): each range (critic,
+// actor) is cut into `world` chunks of a kShardAlign-float multiple; rank r reduce-scatters
+// the gradients into chunk r, runs Adam on it and all-gathers the parameters.  P and G carry
+// kShardSlack floats past the arena layout for the last chunk's reach.
+constexpr int kShardAlign = 64;
+constexpr int kMaxShardWorld = 64;
+constexpr int64_t kShardSlack = (int64_t)kShardAlign * kMaxShardWorld;
+// Polyak over the critic arena as its own launch (PolyakArgs: the ride-along form's body)
+void launch_polyak(const PolyakArgs& a, hipStream_t s);
+// alpha = exp(log_alpha) from the parameter arena after the actor all-gather (every rank:
+// only the owner of log_alpha's chunk took its Adam step), unless err & err_skip
+void launch_alpha_sync(DevScalars* sc, const float* log_alpha, int err_skip, hipStream_t s);
+
 void launch_gather(const GatherArgs& a, hipStream_t s);
 
 // Rows sacmi_push left in host-mapped staging for the next synchronous update (the

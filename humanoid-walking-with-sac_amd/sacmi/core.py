@@ -276,8 +276,17 @@ class Context:
         L.call("sacmi_dp_loopback_init", self._h, int(world))
 
     def step_dp(self, batch: int, n_updates: int = 1) -> None:
-        """n complete data-parallel updates (phases + library-issued RCCL all-reduces)."""
+        """n complete data-parallel updates (phases + library-issued RCCL collectives)."""
         L.call("sacmi_step_dp", self._h, int(batch), int(n_updates))
+
+    def dp_set_sharded(self, on: bool) -> None:
+        """Sharded optimizer step (reduce-scatter -> Adam on 1/world -> all-gather) or the
+        all-reduce form of step_dp (include/sacmi.h)."""
+        L.call("sacmi_dp_set_sharded", self._h, 1 if on else 0)
+
+    def dp_sync_state(self) -> None:
+        """Collective: gather the sharded Adam moments on every rank (before reading them)."""
+        L.call("sacmi_dp_sync_state", self._h)
 
     def ride_possible(self, batch: int) -> bool:
         out = ctypes.c_int32()

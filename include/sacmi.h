@@ -258,8 +258,20 @@ int sacmi_allreduce_init(sacmi_ctx* ctx, const void* id, int32_t nbytes, int32_t
  * all-reduce of [actor gradients | dL/dlog_alpha], the last phase 2 at the end; updates
  * 2..n take their minibatch from the previous update's ride-along sampling/gather when
  * the replay allows it.  Captured into one hipGraph per (batch, n_updates); losses land in
- * the loss ring (sacmi_fetch_losses).  Each rank samples its own replay shard. */
+ * the loss ring (sacmi_fetch_losses).  Each rank samples its own replay shard.
+ * Sharded form (the default for 2 <= world <= 64; $SACMI_DP_SHARD=0/1 or
+ * sacmi_dp_set_sharded override): each all-reduce + Adam becomes reduce-scatter -> Adam on
+ * this rank's 1/world chunk of the range -> all-gather of the parameters (ZeRO-1: the Adam
+ * moments stay valid on the rank's own chunks; sacmi_dp_sync_state gathers them).
+ * world == 1: the fused update (nothing to reduce; $SACMI_DP_PHASES_AT_WORLD1 forces the
+ * phase sequence). */
 int sacmi_step_dp(sacmi_ctx* ctx, int32_t batch, int32_t n_updates);
+/* Sharded (1) or all-reduce (0) form of sacmi_step_dp; the same on every rank. */
+int sacmi_dp_set_sharded(sacmi_ctx* ctx, int32_t on);
+/* Collective (every rank): all-gather the sharded Adam moments so that every rank holds
+ * them whole (before sacmi_get_tensor of SACMI_SLOT_ADAM_M / _V, a checkpoint).  No-op
+ * when not sharded. */
+int sacmi_dp_sync_state(sacmi_ctx* ctx);
 /* Test hook for the sequence above on ONE context, no RCCL: every all-reduce becomes an
  * in-place x world over the same gradient range — what `world` ranks holding identical
  * shards would reduce to — while the Adam kernels apply 1/world as in a real run.  For a
@@ -267,6 +279,8 @@ int sacmi_step_dp(sacmi_ctx* ctx, int32_t batch, int32_t n_updates);
  * updates bit for bit: every gradient element, dL/dlog_alpha included, must sit inside an
  * all-reduced range and 1/world must be applied exactly once. */
 int sacmi_dp_loopback_init(sacmi_ctx* ctx, int32_t world);
+/* (Sharded form under loopback: the gradients x world in place, Adam on every rank's chunk
+ * in turn — rank 0's launch alone finalising the losses — and the gather an identity.) */
 
 /* ---- prioritized replay ------------------------------------------------------------ */
 /* PrioritizedReplayBuffer.sample(batch) indices + IS weights; u: NULL -> draw from

@@ -18,3 +18,7 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+# the world-1 RCCL tests exercise the data-parallel phase sequence itself (sacmi_step_dp
+# takes the fused update at world 1 unless asked; the bench does not ask)
+os.environ.setdefault("SACMI_DP_PHASES_AT_WORLD1", "1")

@@ -964,16 +964,20 @@ def test_dlda_fold_matches_unfolded(B, H):
         assert rel(ga[k], gb[k]) <= 1e-5, (k, rel(ga[k], gb[k]))
 
 
+@pytest.mark.parametrize("sharded", [True, False])
 @pytest.mark.parametrize("world", [2, 8])
 @pytest.mark.parametrize("shape", ["config2", "config5_act16"])
-def test_native_dp_loopback_world_k_bitexact(world, shape):
+def test_native_dp_loopback_world_k_bitexact(world, shape, sharded):
     """The library's data-parallel sequence (sacmi_step_dp, sacmi.hip enqueue_dp) with
     world > 1 arithmetic on one GPU: each all-reduce becomes an in-place x world over the
     same range (what `world` ranks with identical shards produce) and Adam applies 1/world.
     Both scalings are exact for a power-of-two world, so the result equals the fused
     updates BIT FOR BIT only if every gradient element — dL/dlog_alpha included — lies
     inside [q_begin, q_end) or [pi_begin, total) and 1/world is applied exactly once
-    (global batch = the ranks' batches concatenated)."""
+    (global batch = the ranks' batches concatenated).
+    sharded: the ZeRO-1 form (reduce-scatter -> Adam on each rank's chunk -> all-gather),
+    every rank's chunk run in turn: the chunks must tile both ranges exactly, and the
+    alpha / loss bookkeeping must happen once."""
     from sacmi import _lib as L
     if shape == "config2":
         cfg, B, dt, nrows, n = SacConfig(376, 17, 512), 256, "fp32", 4000, 4
@@ -990,6 +994,7 @@ def test_native_dp_loopback_world_k_bitexact(world, shape):
         ctx.set_mt(0, key, 624)
         ctxs.append(ctx)
     ctxs[0].dp_loopback_init(world)
+    ctxs[0].dp_set_sharded(sharded)
     ctxs[0].step_dp(B, n)
     fused = np.stack([ctxs[1].step(B) for _ in range(n)])
     ctxs[0].synchronize()
