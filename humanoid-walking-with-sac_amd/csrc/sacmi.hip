@@ -1491,8 +1491,13 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
   };
   auto step = [&](bool critic) {   // Adam on the chunk(s), gather, the replicated scalars / shadows
     (void)mark(c, critic ? "adam_critic_shard" : "adam_actor_shard");
-    if (c->dp_loopback) {
+    // (SACMI_DP_LOOPBACK_ONE_RANK: timing only — rank 0's chunk alone, the per-rank work
+    // of a `world`-rank run minus its collectives; the other chunks are left unstepped)
+    static const bool one_rank = std::getenv("SACMI_DP_LOOPBACK_ONE_RANK") != nullptr;
+    if (c->dp_loopback && !one_rank) {
       for (int r = 0; r < W; ++r) dp_shard_adam(c, critic, B, r, true);
+    } else if (c->dp_loopback) {
+      dp_shard_adam(c, critic, B, 0, true);
     } else {
       dp_shard_adam(c, critic, B, c->dp_rank, true);
     }
@@ -2420,6 +2425,13 @@ int sacmi_dp_set_sharded(sacmi_ctx* c, int32_t on) {
     c->dp_shard = on != 0;
     for (auto& kv : c->dp_graphs) (void)hipGraphExecDestroy(kv.second);
     c->dp_graphs.clear();
+  });
+}
+
+int sacmi_dp_sharded(sacmi_ctx* c, int32_t* on) {
+  return guard([&] {
+    REQUIRE(c && on, SACMI_EVALUE, "null argument");
+    *on = c->dp_shard && (c->dp_world > 1 || c->dp_loopback) ? 1 : 0;
   });
 }
 

@@ -102,6 +102,7 @@ _PROTOS = {
     "sacmi_dp_loopback_init": [c_vp, ctypes.c_int32],
     "sacmi_dp_set_sharded": [c_vp, ctypes.c_int32],
     "sacmi_dp_sync_state": [c_vp],
+    "sacmi_dp_sharded": [c_vp, ctypes.POINTER(ctypes.c_int32)],
     "sacmi_profile_step": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,
                            ctypes.c_int32, c_i32p],
     "sacmi_profile_sites": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, c_f32p, c_f64p,

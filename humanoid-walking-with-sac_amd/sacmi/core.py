@@ -284,6 +284,11 @@ class Context:
         all-reduce form of step_dp (include/sacmi.h)."""
         L.call("sacmi_dp_set_sharded", self._h, 1 if on else 0)
 
+    def dp_sharded(self) -> bool:
+        out = ctypes.c_int32()
+        L.call("sacmi_dp_sharded", self._h, ctypes.byref(out))
+        return bool(out.value)
+
     def dp_sync_state(self) -> None:
         """Collective: gather the sharded Adam moments on every rank (before reading them)."""
         L.call("sacmi_dp_sync_state", self._h)

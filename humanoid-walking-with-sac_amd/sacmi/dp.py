@@ -134,7 +134,10 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     # the library's communicator: the native driver's collectives, and the roofline's
     # timeline of the data-parallel sequence (both paths)
     want_roof = not getattr(args, "no_roofline", False)
-    if native or want_roof:
+    sim = int(getattr(args, "dp_sim_world", 0) or 0)
+    if sim:                                         # one GPU stands in for `sim` ranks
+        ctx.dp_loopback_init(sim)
+    elif native or want_roof:
         _native_comm(ctx, rank, device)
     if native:
         for n in sizes:
@@ -215,6 +218,12 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
             "dp_graph": native,
             "dp_driver": "library (sacmi_step_dp: RCCL issued by libsacmi)" if native
                          else "torch.distributed (RCCL) around sacmi phases",
+            "dp_optimizer_step": ("sharded: reduce-scatter -> Adam on 1/world -> all-gather"
+                                  if ctx.dp_sharded() else "all-reduce -> Adam on every rank"),
+            "simulated_world": sim or None,
+            "simulated_note": (f"one GPU runs rank 0's sequence of a {sim}-rank job, collectives "
+                               "emulated in place (no transfers): the per-rank work minus the "
+                               "collectives" if sim else None),
             "mfma_util_step": round(flops * value / 1e12 / peak / world, 4),
             "replicas_bitwise_equal": replicas_equal,
             "roofline": roof, "cpu_baseline": cpu,

@@ -268,6 +268,7 @@ int sacmi_allreduce_init(sacmi_ctx* ctx, const void* id, int32_t nbytes, int32_t
 int sacmi_step_dp(sacmi_ctx* ctx, int32_t batch, int32_t n_updates);
 /* Sharded (1) or all-reduce (0) form of sacmi_step_dp; the same on every rank. */
 int sacmi_dp_set_sharded(sacmi_ctx* ctx, int32_t on);
+int sacmi_dp_sharded(sacmi_ctx* ctx, int32_t* on);
 /* Collective (every rank): all-gather the sharded Adam moments so that every rank holds
  * them whole (before sacmi_get_tensor of SACMI_SLOT_ADAM_M / _V, a checkpoint).  No-op
  * when not sharded. */
