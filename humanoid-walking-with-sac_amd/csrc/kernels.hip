@@ -137,6 +137,12 @@ struct OpFetch {
 #ifndef SACMI_FETCH_SADDR
 #define SACMI_FETCH_SADDR 0
 #endif
+#ifndef SACMI_A_AUX
+#define SACMI_A_AUX 0           // k_gemm: cache-policy bits of the A-operand loads (experiment)
+#endif
+#ifndef SACMI_B_AUX
+#define SACMI_B_AUX 0
+#endif
 #ifndef SACMI_KCONTIG
 #define SACMI_KCONTIG 0         // k_gemm: contiguous K-chunk ranges per wave (experiment)
 #endif
@@ -165,7 +171,8 @@ __device__ __forceinline__ void row_offs(const float* P, int ld, int row0, int n
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-template <int NT, bool KC, bool H16 = false>
+// AUX: cache-policy bits of the operand loads (SACMI_A_AUX / SACMI_B_AUX: e.g. 2 = nt)
+template <int NT, bool KC, bool H16 = false, int AUX = 0>
 __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, int K,
                                          float (&v)[NT][4]) {
   if constexpr (H16) {
@@ -192,7 +199,13 @@ __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, in
   for (int t = 0; t < NT; ++t) {
     if (KC) {
       const uint32_t o = f.off[t] + (uint32_t)(k < K ? k : 0) * 4u;
-      const float4 x = (SACMI_FETCH_SADDR & 1) ? gld_off<float4>(f.p, o) : buf_ld4(f.r, o);
+      float4 x;
+      if constexpr (AUX != 0) {
+        const f4 y = llvm_raw_buffer_load_v4f32(f.r, (int)o, 0, AUX);
+        x = float4{y[0], y[1], y[2], y[3]};
+      } else {
+        x = (SACMI_FETCH_SADDR & 1) ? gld_off<float4>(f.p, o) : buf_ld4(f.r, o);
+      }
       v[t][0] = (k < K) ? x.x : 0.f;
       v[t][1] = (k + 1 < K) ? x.y : 0.f;
       v[t][2] = (k + 2 < K) ? x.z : 0.f;
@@ -202,7 +215,8 @@ __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, in
       for (int s = 0; s < 4; ++s) {
         const int kk = (k + s < K) ? (k + s) : (K - 1);
         const uint32_t o = f.off[t] + (uint32_t)kk * (uint32_t)ld * 4u;
-        const float x = (SACMI_FETCH_SADDR & 2) ? gld_off<float>(f.p, o) : buf_ld(f.r, o);
+        const float x = AUX ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(f.r, (int)o, 0, AUX))
+                            : (SACMI_FETCH_SADDR & 2) ? gld_off<float>(f.p, o) : buf_ld(f.r, o);
         v[t][s] = (k + s < K) ? x : 0.f;
       }
     }
@@ -331,8 +345,8 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
     auto issue = [&](int jj, float (&av)[MT][4], float (&bv)[NT][4], float (&xv)[4]) {
       jj = jj < nmine ? jj : nmine - 1;   // unconditional: past the end re-reads the last chunk
       const int k = SACMI_CHUNK(jj) * 16 + kl;
-      fetch_op<MT, AKC, A16>(ra, d.lda, k, d.K, av);
-      fetch_op<NT, BKC>(rb, d.ldb, k, d.K, bv);
+      fetch_op<MT, AKC, A16, SACMI_A_AUX>(ra, d.lda, k, d.K, av);
+      fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, bv);
       if constexpr (!AKC) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) xv[s] = buf_ld(rxw, (uint32_t)(k + s < d.K ? k + s : 0) * 4u);
@@ -383,8 +397,8 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       // chunk re-reads that chunk and is skipped below
       const int jj = j + g < nmine ? j + g : nmine - 1;
       const int k = SACMI_CHUNK(jj) * 16 + kl;
-      fetch_op<MT, AKC, A16>(ra, d.lda, k, d.K, a[g]);
-      fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
+      fetch_op<MT, AKC, A16, SACMI_A_AUX>(ra, d.lda, k, d.K, a[g]);
+      fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, b[g]);
       if constexpr (AXF == 1) {          // w3 rows are float4-aligned (parameter arena)
         const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
         xw[g][0] = x.x; xw[g][1] = x.y; xw[g][2] = x.z; xw[g][3] = x.w;
@@ -556,7 +570,8 @@ struct StgOp {
 
 template <int TM, int TN, int KSP, int MG, bool AKC, bool BKC, bool ROWSUM, int AXF, class Pre>
 __device__ __forceinline__ void gemm_core_s(const GemmDesc& d, int m0, int n0, unsigned char* ring,
-                                            float* rsum, float* s_kw, Pre&& pre, bool store_a) {
+                                            float* rsum, float* s_kw, Pre&& pre, bool store_a,
+                                            tl_word* tl = nullptr) {
   constexpr int TMW = TM * MG;
   using G = StgGeo<TMW, TN, KSP>;
   using OA = StgOp<TMW, G::BK, AKC>;
@@ -656,6 +671,9 @@ __device__ __forceinline__ void gemm_core_s(const GemmDesc& d, int m0, int n0, u
     stg_vmwait_n(younger);
     __builtin_amdgcn_s_barrier();          // slab sl landed for every wave; slot (sl - 1) free
     asm volatile("" ::: "memory");
+    if (sl == 0) SACMI_PHASE(tl, 8);
+    if (sl == nslab - 1) SACMI_PHASE(tl, 9);
+    (void)tl;
     const unsigned char* st = ring + (sl % NST) * SLOT;
     const int kb = sl * BK;
     if constexpr (AXF == 1) {
@@ -773,21 +791,22 @@ __device__ __forceinline__ void gemm_core_s(const GemmDesc& d, int m0, int n0, u
 
 template <int TM, int TN, int KSP, int MG, int AXK, class Pre>
 __device__ __forceinline__ void gemm_core_stg(const GemmDesc& d, int m0, int n0, unsigned char* ring,
-                                              float* rsum, float* s_kw, bool rowsum, Pre&& pre) {
+                                              float* rsum, float* s_kw, bool rowsum, Pre&& pre,
+                                              tl_word* tl) {
   if constexpr (AXK == 1) {
     if (d.axk == 1) {
       gemm_core_s<TM, TN, KSP, MG, true, false, false, 1>(d, m0, n0, ring, rsum, s_kw, pre,
-                                                          n0 == 0 && d.ax_out != nullptr);
+                                                          n0 == 0 && d.ax_out != nullptr, tl);
       return;
     }
   }
   if (d.a_kc) {
-    if (d.b_kc) gemm_core_s<TM, TN, KSP, MG, true, true, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
-    else gemm_core_s<TM, TN, KSP, MG, true, false, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
+    if (d.b_kc) gemm_core_s<TM, TN, KSP, MG, true, true, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
+    else gemm_core_s<TM, TN, KSP, MG, true, false, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
   } else {
-    if (d.b_kc) gemm_core_s<TM, TN, KSP, MG, false, true, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
-    else if (rowsum) gemm_core_s<TM, TN, KSP, MG, false, false, true, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
-    else gemm_core_s<TM, TN, KSP, MG, false, false, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false);
+    if (d.b_kc) gemm_core_s<TM, TN, KSP, MG, false, true, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
+    else if (rowsum) gemm_core_s<TM, TN, KSP, MG, false, false, true, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
+    else gemm_core_s<TM, TN, KSP, MG, false, false, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
   }
 }
 
@@ -1250,6 +1269,14 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
     if (bid < batch.total_tiles) return;
   }
 #endif
+  if (bid >= n_tiles && bid == batch.adam_wg) {
+    // the level's scalar Adam work on a workgroup of its own, at once: its inputs (loss
+    // partials, log_alpha's gradient, the scalars) come from earlier levels, and no tile's
+    // workgroup waits behind it (block 0 did it after its tile: +2.6-3 us on the level)
+    const AdamFuse& af = batch.adam;
+    adam_block0(af, af.sc->err, 1.f - af.beta1, 1.f - af.beta2);
+    return;
+  }
   if (bid >= n_tiles) {   // ride-along workgroups (next update's replay work, Polyak)
     if constexpr (gemm_threads<KSPLIT, MG, CORE>() == 1024) {   // the host attaches rides to 1024-thread configs
       const int rb = bid - n_tiles;
@@ -1462,7 +1489,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
                      : (SACMI_PIPE_DW && G == 1 && ADAM && MG == 2) ? 2 : 0;
   SACMI_PHASE(batch.tl, 1);
   if constexpr (CORE == 1)
-    gemm_core_stg<TM, TN, KSPLIT, MG, AXK>(d, m0, n0, ring, rsum, s_kw, rowsum, pre);
+    gemm_core_stg<TM, TN, KSPLIT, MG, AXK>(d, m0, n0, ring, rsum, s_kw, rowsum, pre, batch.tl);
   else
     gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   SACMI_PHASE(batch.tl, 2);
@@ -1619,7 +1646,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
       }
     }
   }
-  if (batch.has_adam && bid == 0) {
+  if (batch.has_adam && batch.adam_wg < 0 && bid == 0) {
     adam_block0(af, err, omb1, omb2);
   }
   SACMI_PHASE(batch.tl, 5);
@@ -1643,6 +1670,13 @@ static int assign_tiles(GemmBatch& b) {
     const double A = (double)d.M * d.K, B = (double)d.N * d.K;
     d.xcd_gr = 0;
     double best = 8 * A + B;      // row-major order
+    // SACMI_XCD_GR (experiment): force the XCD grid (1: every XCD owns column tiles only)
+    static const int force_gr = std::getenv("SACMI_XCD_GR") ? std::atoi(std::getenv("SACMI_XCD_GR")) : 0;
+    if (force_gr > 0 && d.tiles_m % force_gr == 0 && d.tiles_n % (8 / force_gr) == 0) {
+      d.xcd_gr = force_gr;
+      tot += (d.tiles_m * d.tiles_n + 7) & ~7;
+      continue;
+    }
     for (int gr : {1, 2, 4, 8}) {
       const int gc = 8 / gr;
       if (d.tiles_m % gr || d.tiles_n % gc) continue;
@@ -3169,7 +3203,16 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   b = b0;
   if (level_act16(b))
     throw Error{SACMI_ESTATE, "bf16 activation operands on a level outside the batch-4096-class kernels"};
-  const int extra = (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
+  const int extra0 = (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
+  // a fused-Adam level's scalar work on a workgroup of its own, after the tiles and rides
+  // (SACMI_ADAM_WG=1; measured: L13's slowest workgroup 12.3 -> 9.7 us, but the update no
+  // faster — the level's end is its last tile's, and L6 took +0.85 us: off by default)
+  static const bool adam_wg_on = std::getenv("SACMI_ADAM_WG") != nullptr && std::atoi(std::getenv("SACMI_ADAM_WG")) != 0;
+  const bool awg = b.has_adam && adam_wg_on;
+  const int extra = extra0 + (awg ? 1 : 0);
+  b.adam_wg = -1;
+  auto set_awg = [&](int tiles) { if (awg) b.adam_wg = tiles + extra0; };
+  auto grid_for = [&](int tiles) { set_awg(tiles); return tiles + extra; };
   if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > kRideLdsBytes)
     throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_gemm's LDS"};
   int maxk = 0, n_adam = 0;
@@ -3195,21 +3238,21 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   // the batch-256 class on the LDS-staged core (same tile geometries as below)
   if (staged_ok(b) && (dw || (!n_adam && t64 <= 512))) {
     if (dw && t64 <= 256) {
-      if (n_adam) launch_ks<32, 64, 8, 1, true, 0>(b, b.total_tiles + extra, s);
-      else launch_ks<32, 64, 8, 1, false, 0>(b, b.total_tiles + extra, s);
+      if (n_adam) launch_ks<32, 64, 8, 1, true, 0>(b, grid_for(b.total_tiles), s);
+      else launch_ks<32, 64, 8, 1, false, 0>(b, grid_for(b.total_tiles), s);
     } else if (dw) {
       for (int i = 0; i < b.count; ++i)
         if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a 64-row tile level"};
-      const int g = assign_tiles<64, 64>(b) + extra;
+      const int g = grid_for(assign_tiles<64, 64>(b));
       if (n_adam) launch_ks<32, 64, 4, 2, true, 0>(b, g, s);
       else launch_ks<32, 64, 4, 2, false, 0>(b, g, s);
     } else if (axk == 1) {
-      const int g = assign_tiles<32, 32>(b) + extra;
+      const int g = grid_for(assign_tiles<32, 32>(b));
       launch_ks<32, 32, 8, 1, false, 1>(b, g, s);
     } else if (t64 >= 192) {
-      launch_ks<32, 64, 8, 1, false, 0>(b, b.total_tiles + extra, s);
+      launch_ks<32, 64, 8, 1, false, 0>(b, grid_for(b.total_tiles), s);
     } else {
-      const int g = assign_tiles<32, 32>(b) + extra;
+      const int g = grid_for(assign_tiles<32, 32>(b));
       launch_ks<32, 32, 8, 1, false, 0>(b, g, s);
     }
     HIP_LAUNCH_CHECK();
@@ -3217,8 +3260,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   }
   if (dw && t64 <= 256) {
     // one 32x64 tile per CU (policy level): 16 waves, K split 16 ways
-    if (n_adam) launch_k<32, 64, 16, 1, 1, true, 0>(b, b.total_tiles + extra, s);
-    else launch_k<32, 64, 16, 1, 1, false, 0>(b, b.total_tiles + extra, s);
+    if (n_adam) launch_k<32, 64, 16, 1, 1, true, 0>(b, grid_for(b.total_tiles), s);
+    else launch_k<32, 64, 16, 1, 1, false, 0>(b, grid_for(b.total_tiles), s);
   } else if (dw || n_adam || t64 > 512) {
     // more 32x64 tiles than CUs (the twin critic weight gradients; every level at large
     // batch): 64x64 tiles as two 32-row wave groups, each with an 8-way K split — half
@@ -3227,35 +3270,35 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     // 16 waves per CU either as one 1024-thread workgroup (8-way K split per wave group)
     // or as several smaller ones (4- / 2-way): then one workgroup's LDS reduction and
     // epilogue overlap another's operand loads and MFMAs.  Rides attach to 1024 threads.
-    const int g = assign_tiles<64, 64>(b) + extra;
+    const int g = grid_for(assign_tiles<64, 64>(b));
     for (int i = 0; i < b.count; ++i)   // the two-wave-group tiles compute no dL/da partials
       if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a 64-row tile level"};
     if (n_adam) {
-      if (SACMI_DW_KS == 4 && !extra) launch_k<32, 64, 4, 1, 2, true, 0>(b, g, s);
+      if (SACMI_DW_KS == 4 && !extra0) launch_k<32, 64, 4, 1, 2, true, 0>(b, g, s);
       else launch_k<32, 64, 8, 1, 2, true, 0>(b, g, s);
     } else if (axk == 1) {
-      if (SACMI_AXK_KS == 4 && !extra) launch_k<32, 64, 4, 1, 2, false, 1>(b, g, s);
+      if (SACMI_AXK_KS == 4 && !extra0) launch_k<32, 64, 4, 1, 2, false, 1>(b, g, s);
       else launch_k<32, 64, 8, 1, 2, false, 1>(b, g, s);
     } else if (dw) {
       // the plain (data-parallel) form of a weight-gradient level: the fused form's geometry
-      if (SACMI_DW_KS == 4 && !extra) launch_k<32, 64, 4, 1, 2, false, 0>(b, g, s);
+      if (SACMI_DW_KS == 4 && !extra0) launch_k<32, 64, 4, 1, 2, false, 0>(b, g, s);
       else launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
-    } else if (!extra && SACMI_FWD_KS == 2) {
+    } else if (!extra0 && SACMI_FWD_KS == 2) {
       launch_k<32, 64, 2, 1, 2, false, 0>(b, g, s);
-    } else if (!extra && SACMI_FWD_KS == 4) {
+    } else if (!extra0 && SACMI_FWD_KS == 4) {
       launch_k<32, 64, 4, 1, 2, false, 0>(b, g, s);
     } else {
       launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
     }
   } else if (axk == 1) {
     // dh1 / dha1 with the fc3 backward folded in (A transform, coefficient in the epilogue)
-    const int g = assign_tiles<32, 32>(b) + extra;
+    const int g = grid_for(assign_tiles<32, 32>(b));
     launch_k<32, 32, 16, 2, 1, false, 1>(b, g, s);
   } else if (t64 >= 192) {
     // widest tile that still gives one workgroup to most CUs
-    launch_k<32, 64, 16, 2, 1, false, 0>(b, b.total_tiles + extra, s);
+    launch_k<32, 64, 16, 2, 1, false, 0>(b, grid_for(b.total_tiles), s);
   } else {
-    const int g = assign_tiles<32, 32>(b) + extra;
+    const int g = grid_for(assign_tiles<32, 32>(b));
     launch_k<32, 32, 16, 2, 1, false, 0>(b, g, s);
   }
   HIP_LAUNCH_CHECK();

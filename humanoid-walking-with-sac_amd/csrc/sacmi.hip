@@ -897,6 +897,15 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       lv.b.tl = c->tl_cur;
       launch_gemm(lv.b, s);
     }
+    // diagnostic (SACMI_EXP_DUP_LEVELS): the idempotent forward levels launched twice, the
+    // second (site "<name>_dup") with its operands warm in the XCDs' L2 — the level body's
+    // time with L2-resident operands
+    static const bool dup = std::getenv("SACMI_EXP_DUP_LEVELS") != nullptr;
+    if (dup && !lv.b.has_adam && !lv.b.ride.kind && !lv.b.ride.pk_blocks && !lv.b.rows.kind &&
+        mark(c, (name + "_dup").c_str(), level_flops(lv.b), level_bytes(lv.b))) {
+      lv.b.tl = c->tl_cur;
+      launch_gemm(lv.b, s);
+    }
   };
 
   // fused updates whose policy dhp1 level (L12) leaves CUs idle on k_gemm: Polyak rides there
@@ -1441,7 +1450,7 @@ static RcclApi& rccl() {
 // in place, Adam on every rank's chunk in turn (rank 0 alone finalises the losses / ring),
 // the gather an identity.
 #ifndef SACMI_DP_SHARD_DEFAULT
-#define SACMI_DP_SHARD_DEFAULT 0
+#define SACMI_DP_SHARD_DEFAULT 1
 #endif
 static bool dp_shard_default(int world) {
   if (const char* e = std::getenv("SACMI_DP_SHARD")) return std::atoi(e) != 0 && world <= kMaxShardWorld;

@@ -124,7 +124,7 @@ constexpr int kTlEndSlots = 4096;
 // of a stamping kernel also record kTlPhases clocks each (SACMI_PHASE), after the end slots;
 // sacmi_profile_timeline then dumps the raw buffer to $SACMI_DIAG_DUMP (tools/phase_dump.py)
 #ifdef SACMI_DIAG_PHASES
-constexpr int kTlPhases = 8;
+constexpr int kTlPhases = 10;   // 8 / 9: the staged core's first / last slab barrier (wave 0)
 #else
 constexpr int kTlPhases = 0;
 #endif
@@ -401,6 +401,9 @@ struct GemmBatch {
   int total_tiles;
   AdamFuse adam;       // used when any desc has epi >= EPI_ADAM
   int has_adam;
+  int adam_wg;         // k_gemm: the workgroup that runs the level's scalar Adam work (losses,
+                       //   alpha step, loss ring, done word) — an extra workgroup past the
+                       //   tiles and rides (launch_gemm), or -1: block 0 after its tile
   RideAlong ride;      // extra workgroups after the tiles
   RowsFuse rows;       // prologue for axk-1 descs
   int bf16;            // 1: bf16 MFMA operands (fp32 loads rounded to bf16 in registers)

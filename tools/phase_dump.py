@@ -47,6 +47,10 @@ def main(path):
         if nph >= 8 and np.all(ph[:, 6] > 0):   # the last wave's entry / K-loop end
             d["lastin"] = np.median(ph[:, 6] - ph[:, 0]) * 0.01
             d["lastcore"] = np.median(ph[:, 7] - ph[:, 6]) * 0.01
+        if nph >= 10 and np.all(ph[:, 8] > 0):  # staged core: first / last slab barrier
+            d["slab0"] = np.median(ph[:, 8] - ph[:, 1]) * 0.01
+            d["slabs"] = np.median(ph[:, 9] - ph[:, 8]) * 0.01
+            d["lastmma"] = np.median(ph[:, 2] - ph[:, 9]) * 0.01
         acc.setdefault(names[s], []).append(d)
         if SLOW:   # the slowest workgroups of this site's first launch, phase by phase
             bids = np.nonzero(live)[0]
@@ -55,7 +59,8 @@ def main(path):
                 seg = np.diff(ph[r]) * 0.01
                 print(f"  slow {names[s]:28s} wg {bids[r]:4d} start {(ph[r, 0] - start) * 0.01:6.2f} "
                       f"total {tot[r] * 0.01:6.2f} phases " + " ".join(f"{v:5.2f}" for v in seg))
-    keys = ["start", "startmax", "setup", "core0", "wait", "epi", "tail", "wg", "wgmax", "lastin", "lastcore"]
+    keys = ["start", "startmax", "setup", "core0", "wait", "epi", "tail", "wg", "wgmax", "lastin", "lastcore",
+            "slab0", "slabs", "lastmma"]
     print(f"{'site':32s} " + " ".join(f"{k:>8s}" for k in keys))
     for n, lst in acc.items():
         print(f"{n:32s} " + " ".join(f"{np.median([d.get(k, np.nan) for d in lst]):8.2f}" for k in keys))
