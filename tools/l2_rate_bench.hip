@@ -104,12 +104,21 @@ __global__ __launch_bounds__(kThreads) void k_burst(const float* buf, int mall, 
   sink[b * kThreads + threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3] + pad[(threadIdx.x + 1) & 1023];
 }
 
+// a different kernel between two bursts: write-through stores of 1 KB (as the update's levels
+// end), to see whether the next launch still finds the operands in L2
+__global__ void k_touch(float* p) {
+  __hip_atomic_store(p + threadIdx.x, 1.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static float* g_touch = nullptr;
+static int g_between = 0;   // 1: k_touch between the bursts
+
 template <int S>
 static void run(const char* name, const float* buf, unsigned long long* dur, float* sink) {
   std::vector<unsigned long long> h(kWG);
   for (int mall = 0; mall < 2; ++mall) {
     std::vector<double> med;
     for (int rep = 0; rep < 12; ++rep) {
+      if (g_between) hipLaunchKernelGGL(k_touch, dim3(1), dim3(256), 0, 0, g_touch);
       hipLaunchKernelGGL(k_burst<S>, dim3(kWG), dim3(kThreads), 0, 0, buf, mall, dur, sink);
       CHECK(hipGetLastError());
       CHECK(hipDeviceSynchronize());
@@ -120,8 +129,8 @@ static void run(const char* name, const float* buf, unsigned long long* dur, flo
     }
     std::sort(med.begin(), med.end());
     const double us = med[med.size() / 2];
-    printf("%-8s %-4s burst %6.2f us  -> %6.1f GB/s per CU (median CU, median of 10)\n", name, mall ? "mall" : "l2", us,
-           kRegion / us * 1e-3);
+    printf("%-8s %-4s%s burst %6.2f us  -> %6.1f GB/s per CU (median CU, median of 10)\n", name, mall ? "mall" : "l2",
+           g_between ? " +touch" : "", us, kRegion / us * 1e-3);
   }
 }
 
@@ -132,12 +141,15 @@ int main() {
   CHECK(hipMemset(buf, 0, (size_t)kWG * kRegion));
   CHECK(hipMalloc(&sink, (size_t)kWG * kThreads * 4));
   CHECK(hipMalloc(&dur, kWG * 8));
-  run<KC64>("kc64", buf, dur, sink);
-  run<KC32X2>("kc32x2", buf, dur, sink);
-  run<R128>("r128", buf, dur, sink);
-  run<R256>("r256", buf, dur, sink);
-  run<LIN>("lin", buf, dur, sink);
-  run<DMA128>("dma128", buf, dur, sink);
-  run<DMALIN>("dma_lin", buf, dur, sink);
+  CHECK(hipMalloc(&g_touch, 4096));
+  for (g_between = 0; g_between < 2; ++g_between) {
+    run<KC64>("kc64", buf, dur, sink);
+    run<KC32X2>("kc32x2", buf, dur, sink);
+    run<R128>("r128", buf, dur, sink);
+    run<R256>("r256", buf, dur, sink);
+    run<LIN>("lin", buf, dur, sink);
+    run<DMA128>("dma128", buf, dur, sink);
+    run<DMALIN>("dma_lin", buf, dur, sink);
+  }
   return 0;
 }
