@@ -132,6 +132,9 @@ struct OpFetch {
   rsrc_t r;
   const char* p;
   uint32_t off[NT];
+#ifdef SACMI_EXP_LINFETCH
+  bool lin;   // the operand has >= 16 rows: the contiguous-read experiment applies
+#endif
 };
 
 #ifndef SACMI_FETCH_SADDR
@@ -165,6 +168,14 @@ __device__ __forceinline__ void row_offs(const float* P, int ld, int row0, int n
     int row = row0 + t * 16 + (lane & 15);
     row = row < nrows ? row : nrows - 1;
     f.off[t] = KC ? (uint32_t)row * (uint32_t)ld * (H16 ? 2u : 4u) : (uint32_t)row * 4u;
+#ifdef SACMI_EXP_LINFETCH
+    // the 16-row block (kept inside the operand's rows), 16 B per lane
+    f.lin = KC && !H16 && nrows >= 16;
+    if (f.lin) {
+      const int rb = row0 + t * 16 < nrows - 16 ? row0 + t * 16 : nrows - 16;
+      f.off[t] = (uint32_t)rb * (uint32_t)ld * 4u + 16u * (uint32_t)(lane & 63);
+    }
+#endif
   }
 }
 
@@ -198,7 +209,14 @@ __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, in
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (KC) {
+#ifdef SACMI_EXP_LINFETCH
+      // timing experiment only (wrong values): the same 16-row block's bytes read as 1 KB
+      // contiguous per wave-instruction, as an MFMA-packed operand layout would be read
+      const int ch = (k >> 4) < (ld >> 4) - 1 ? (k >> 4) : (ld >> 4) - 1;
+      const uint32_t o = f.lin ? f.off[t] + (uint32_t)ch * 1024u : f.off[t] + (uint32_t)(k < K ? k : 0) * 4u;
+#else
       const uint32_t o = f.off[t] + (uint32_t)(k < K ? k : 0) * 4u;
+#endif
       float4 x;
       if constexpr (AUX != 0) {
         const f4 y = llvm_raw_buffer_load_v4f32(f.r, (int)o, 0, AUX);
@@ -468,6 +486,24 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       v += __shfl_xor(v, 32, 64);
       if (lane < 16) rsum[wave * TM + i * 16 + lane] = v;
     }
+  }
+}
+
+// Tile t of a desc -> (row tile, column tile): row-major, or (xcd_gr) the XCD-blocked order
+// of assign_tiles — XCD x = t & 7 owns a (tiles_m / gr) x (tiles_n / gc) sub-grid.  The
+// divisors come from the host (GemmDesc::pl_*): device integer divisions cost ~0.35 us of
+// dependent scalar code per level (phase stamps, profiles/r04).
+__device__ __forceinline__ void place_tile(const GemmDesc& d, int t, int& tr, int& tc) {
+  const uint32_t n = d.xcd_gr ? (uint32_t)t >> 3 : (uint32_t)t;
+  const int q = d.pl_mag ? (int)__umulhi(n, d.pl_mag) : (int)n;
+  const int r = (int)n - q * d.pl_div;
+  if (d.xcd_gr) {
+    const int x = t & 7;
+    tr = (x >> d.pl_gc_log2) * d.pl_sr + q;
+    tc = (x & ((1 << d.pl_gc_log2) - 1)) * d.pl_div + r;
+  } else {
+    tr = q;
+    tc = r;
   }
 }
 
@@ -1196,7 +1232,7 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
 #define SACMI_PIPE 0
 #endif
 #ifndef SACMI_PIN_EPI
-#define SACMI_PIN_EPI 0         // k_gemm: the epilogue's desc fields in the K loop's round trip (measured: no gain)
+#define SACMI_PIN_EPI 1         // k_gemm: the epilogue's desc fields in the K loop's round trip
 #endif
 #ifndef SACMI_PIPE_DW
 #define SACMI_PIPE_DW 0
@@ -1232,9 +1268,23 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
   int tbeg[kMaxGemms];
 #pragma unroll
   for (int q = 0; q < kMaxGemms; ++q) tbeg[q] = batch.d[q].tile_begin;
-  asm volatile("" :: "s"(tl), "s"(n_tiles), "s"(n_desc));
+  const int adam_wg = batch.adam_wg;
+  asm volatile("" :: "s"(tl), "s"(n_tiles), "s"(n_desc), "s"(adam_wg));
 #pragma unroll
   for (int q = 0; q < kMaxGemms; ++q) asm volatile("" :: "s"(tbeg[q]));
+#if SACMI_PIN_EPI
+  // ... with the level-wide epilogue scalars that do not depend on the desc (the row
+  // prologue's / fused Adam's pointers): otherwise their loads sit behind the desc's
+  if constexpr (AXK == 1) {
+    const RowsFuse& r = batch.rows;
+    asm volatile("" :: "s"(r.part), "s"(r.logp), "s"(r.r), "s"(r.d), "s"(r.kind), "s"(r.nparts),
+                 "s"(r.B), "s"(r.sc), "s"(r.logp_part), "s"(r.n_lp));
+  } else if constexpr (ADAM) {
+    const AdamFuse& a = batch.adam;
+    asm volatile("" :: "s"(a.P), "s"(a.M), "s"(a.V), "s"(a.T), "s"(a.G), "s"(a.t_base), "s"(a.sc),
+                 "s"(a.step_offset));
+  }
+#endif
   const TlMark tl_mark(tl, TL_GEMM);
   SACMI_PHASE(tl, 0);
   SACMI_PHASE_LAST(tl, 6);
@@ -1269,7 +1319,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
     if (bid < batch.total_tiles) return;
   }
 #endif
-  if (bid >= n_tiles && bid == batch.adam_wg) {
+  if (bid >= n_tiles && bid == adam_wg) {
     // the level's scalar Adam work on a workgroup of its own, at once: its inputs (loss
     // partials, log_alpha's gradient, the scalars) come from earlier levels, and no tile's
     // workgroup waits behind it (block 0 did it after its tile: +2.6-3 us on the level)
@@ -1302,7 +1352,8 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
   // loads; the epilogue's fields load lazily, under the MFMAs
   const GemmDesc d = batch.d[p];
 #define SACMI_DESC_PIN_K "s"(d.A), "s"(d.B), "s"(d.M), "s"(d.N), "s"(d.K), "s"(d.lda), "s"(d.ldb), \
-    "s"(d.a_kc), "s"(d.b_kc), "s"(d.tiles_n), "s"(d.tiles_m), "s"(d.xcd_gr)
+    "s"(d.a_kc), "s"(d.b_kc), "s"(d.tiles_n), "s"(d.tiles_m), "s"(d.xcd_gr), "s"(d.pl_div), \
+    "s"(d.pl_mag), "s"(d.pl_gc_log2), "s"(d.pl_sr)
 #if SACMI_PIN_EPI
   // ... and, in the same round trip (one asm statement: every load issued before the one
   // wait), the fields the epilogue's buffer descriptors and scalars are formed from — the
@@ -1327,19 +1378,13 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
 #else
   asm volatile("" :: SACMI_DESC_PIN_K);
 #endif
+  if constexpr (CORE == 0) SACMI_PHASE(batch.tl, 8);   // (diagnostic: the desc has landed)
   const int t = bid - tbeg[p];
   if (t >= d.tiles_m * d.tiles_n) return;   // padding to a multiple of 8 blocks
   int tr, tc;
-  if (d.xcd_gr) {
-    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
-    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
-    tr = (x / gc) * sr + j / sc;
-    tc = (x % gc) * sc + j % sc;
-  } else {
-    tr = t / d.tiles_n;
-    tc = t % d.tiles_n;
-  }
+  place_tile(d, t, tr, tc);
   const int m0 = tr * TMW, n0 = tc * TN;
+  if constexpr (CORE == 0) SACMI_PHASE(batch.tl, 9);   // (diagnostic: the tile is placed)
   const bool rowsum = d.rs_col >= 0 && n0 == 0;
   const AdamFuse& af = batch.adam;
   // Adam bias corrections and the error bits: thread 0 reads them in pre(), behind its
@@ -1685,6 +1730,17 @@ static int assign_tiles(GemmBatch& b) {
     }
     tot += (d.tiles_m * d.tiles_n + 7) & ~7;
   }
+  for (int i = 0; i < b.count; ++i) {   // the placement divisor of every desc
+    GemmDesc& d = b.d[i];
+    const int gc = d.xcd_gr ? 8 / d.xcd_gr : 1;
+    d.pl_div = d.xcd_gr ? d.tiles_n / gc : d.tiles_n;
+    d.pl_gc_log2 = gc == 8 ? 3 : gc == 4 ? 2 : gc == 2 ? 1 : 0;
+    d.pl_sr = d.xcd_gr ? d.tiles_m / d.xcd_gr : 0;
+    // ceil(2^32 / div): mul_hi(n, mag) = n / div exactly for n, div < 2^16
+    if (d.pl_div < 1 || d.pl_div >= 65536 || d.tiles_m * d.tiles_n >= 65536)
+      throw Error{SACMI_ESTATE, "tile grid out of the placement range"};
+    d.pl_mag = d.pl_div == 1 ? 0u : (unsigned)((((uint64_t)1 << 32) + d.pl_div - 1) / d.pl_div);
+  }
   b.total_tiles = tot;
   return tot;
 }
@@ -1810,15 +1866,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
   const int t = bid - d.tile_begin;
   if (t >= d.tiles_m * d.tiles_n) return;
   int tr, tc;
-  if (d.xcd_gr) {
-    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
-    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
-    tr = (x / gc) * sr + j / sc;
-    tc = (x % gc) * sc + j % sc;
-  } else {
-    tr = t / d.tiles_n;
-    tc = t % d.tiles_n;
-  }
+  place_tile(d, t, tr, tc);
   const int m0 = tr * kFBM, n0 = tc * kFBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * (kFBN / 2);
@@ -1950,15 +1998,7 @@ __global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), SACMI_FWD16_OCC) void k_f
   const int t = bid - d.tile_begin;
   if (t >= d.tiles_m * d.tiles_n) return;
   int tr, tc;
-  if (d.xcd_gr) {
-    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
-    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
-    tr = (x / gc) * sr + j / sc;
-    tc = (x % gc) * sc + j % sc;
-  } else {
-    tr = t / d.tiles_n;
-    tc = t % d.tiles_n;
-  }
+  place_tile(d, t, tr, tc);
   const int m0 = tr * kFBM, n0 = tc * kFBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave / WC) * MW, wn = (wave % WC) * NW;
@@ -2118,15 +2158,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void k_fwd16p(GemmBatch batch) {
   const int t = bid - d.tile_begin;
   if (t >= d.tiles_m * d.tiles_n) return;
   int tr, tc;
-  if (d.xcd_gr) {
-    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
-    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
-    tr = (x / gc) * sr + j / sc;
-    tc = (x % gc) * sc + j % sc;
-  } else {
-    tr = t / d.tiles_n;
-    tc = t % d.tiles_n;
-  }
+  place_tile(d, t, tr, tc);
   const int m0 = tr * BM, n0 = tc * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave / WC) * MW, wn = (wave % WC) * NW;
@@ -2659,15 +2691,7 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
   const int t = bid - d.tile_begin;
   if (t >= d.tiles_m * d.tiles_n) return;
   int tr, tc;
-  if (d.xcd_gr) {
-    const int gc = 8 / d.xcd_gr, x = t & 7, j = t >> 3;
-    const int sr = d.tiles_m / d.xcd_gr, sc = d.tiles_n / gc;
-    tr = (x / gc) * sr + j / sc;
-    tc = (x % gc) * sc + j % sc;
-  } else {
-    tr = t / d.tiles_n;
-    tc = t % d.tiles_n;
-  }
+  place_tile(d, t, tr, tc);
   const int m0 = tr * kXBM, n0 = tc * kXBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave / WC) * 32, wn = (wave % WC) * (kXBN / WC);

@@ -240,6 +240,11 @@ struct GemmDesc {
   int tiles_n, tile_begin;
   int tiles_m;         // row blocks
   int xcd_gr;          // >0: XCD-blocked tile order, gr x (8/gr) XCD grid (launch_gemm)
+  // tile placement without a device-side division (assign_tiles): block t of the desc ->
+  // q = t' / pl_div as mul_hi(t', pl_mag) (pl_mag 0: pl_div 1), t' = t (row-major order) or
+  // t >> 3 (XCD grid: sub-grid columns pl_div, sub-grid rows pl_sr, 2^pl_gc_log2 XCD columns)
+  int pl_div, pl_gc_log2, pl_sr;
+  unsigned pl_mag;
   // fc3 dot partials (forward ReLU levels feeding a scalar head): for every row and
   // every 32-column block of this GEMM's output, sum_n relu(y[row][n]) * dotw[n] is
   // written to dotp[row * dotp_ld + n / 32]

@@ -10,6 +10,8 @@
 //   r128    lane l -> row l >> 3, bytes 16 (l & 7): 8 rows x 128 B
 //   r256    lane l -> row l >> 4, bytes 16 (l & 15): 4 rows x 256 B
 //   lin     lane l -> 16 l: 1 KB contiguous
+//   mn4     dword loads, lane l -> row l >> 4, bytes 4 (l & 15): 4 rows x 64 B (k_gemm's
+//           MN-contiguous fragment form: 4x as many wave-instructions of 256 B)
 //   dma128  r128 through LDS-DMA (global_load_lds_dwordx4)
 //   dma_lin lin through LDS-DMA
 // Residency: "l2" = groups of 4 CUs of one XCD read the same 192 KB region (1.5 MB per XCD,
@@ -37,8 +39,9 @@ constexpr int kRowB = 2048;           // a 512-float row
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ f4 raw_ld4(__amdgpu_buffer_rsrc_t r, int off, int soff, int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.v4f32");
+__device__ float raw_ld1(__amdgpu_buffer_rsrc_t r, int off, int soff, int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.f32");
 
-enum Shape { KC64, KC32X2, R128, R256, LIN, DMA128, DMALIN, NSHAPE };
+enum Shape { KC64, KC32X2, R128, R256, LIN, DMA128, DMALIN, MN4, NSHAPE };
 
 // byte offset of lane l's 16 B in wave-instruction q of wave w (inside the CU's region)
 __device__ __forceinline__ int offset(int shape, int w, int q, int l) {
@@ -91,6 +94,18 @@ __global__ __launch_bounds__(kThreads) void k_burst(const float* buf, int mall, 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     acc = lds[w * 128 + l];
+  } else if constexpr (SHAPE == MN4) {
+    // 48 dword instructions of 4 rows x 64 B per wave (the same 12 KB): rows of a 96-row
+    // region, 64-byte column slices
+    float v[4 * kInstr];
+#pragma unroll
+    for (int q = 0; q < 4 * kInstr; ++q) {
+      const int ins = w * 4 * kInstr + q;   // 768 per CU, 256 B each
+      const int rb = (ins % 24) * 4, col = (ins / 24) * 64;
+      v[q] = raw_ld1(r, (rb + (l >> 4)) * kRowB + col + 4 * (l & 15), 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4 * kInstr; ++q) acc[q & 3] += v[q];
   } else {
     f4 v[kInstr];
 #pragma unroll
@@ -150,6 +165,7 @@ int main() {
     run<LIN>("lin", buf, dur, sink);
     run<DMA128>("dma128", buf, dur, sink);
     run<DMALIN>("dma_lin", buf, dur, sink);
+    run<MN4>("mn4", buf, dur, sink);
   }
   return 0;
 }

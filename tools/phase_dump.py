@@ -3,7 +3,8 @@
 a -DSACMI_DIAG_PHASES build).  k_gemm phases (wave 0 of the first 256 workgroups):
 0 entry, 1 setup done (before the K loop), 2 wave 0's K loop + MFMAs done, 3 every wave
 done (the pre-epilogue barrier; incl. the row prologue), 4 epilogue stores issued, 5 exit;
-6 / 7 the last wave's entry and K-loop end (lastin: its entry after wave 0's).
+6 / 7 the last wave's entry and K-loop end (lastin: its entry after wave 0's); 8 / 9 the
+staged core's first / last slab, or (register-direct core) the desc landed / the tile placed.
 usage: tools/phase_dump.py dump.bin"""
 import struct
 import sys
@@ -47,10 +48,16 @@ def main(path):
         if nph >= 8 and np.all(ph[:, 6] > 0):   # the last wave's entry / K-loop end
             d["lastin"] = np.median(ph[:, 6] - ph[:, 0]) * 0.01
             d["lastcore"] = np.median(ph[:, 7] - ph[:, 6]) * 0.01
-        if nph >= 10 and np.all(ph[:, 8] > 0):  # staged core: first / last slab barrier
+        if nph >= 10 and np.all(ph[:, 8] > 0) and np.all(ph[:, 8] >= ph[:, 1]):
+            # staged core: first / last slab barrier
             d["slab0"] = np.median(ph[:, 8] - ph[:, 1]) * 0.01
             d["slabs"] = np.median(ph[:, 9] - ph[:, 8]) * 0.01
             d["lastmma"] = np.median(ph[:, 2] - ph[:, 9]) * 0.01
+        elif nph >= 10 and np.all(ph[:, 8] > 0):
+            # register-direct core: the setup split — desc round trip, tile placement, the rest
+            d["desc"] = np.median(ph[:, 8] - ph[:, 0]) * 0.01
+            d["place"] = np.median(ph[:, 9] - ph[:, 8]) * 0.01
+            d["pre"] = np.median(ph[:, 1] - ph[:, 9]) * 0.01
         acc.setdefault(names[s], []).append(d)
         if SLOW:   # the slowest workgroups of this site's first launch, phase by phase
             bids = np.nonzero(live)[0]
@@ -60,7 +67,7 @@ def main(path):
                 print(f"  slow {names[s]:28s} wg {bids[r]:4d} start {(ph[r, 0] - start) * 0.01:6.2f} "
                       f"total {tot[r] * 0.01:6.2f} phases " + " ".join(f"{v:5.2f}" for v in seg))
     keys = ["start", "startmax", "setup", "core0", "wait", "epi", "tail", "wg", "wgmax", "lastin", "lastcore",
-            "slab0", "slabs", "lastmma"]
+            "slab0", "slabs", "lastmma", "desc", "place", "pre"]
     print(f"{'site':32s} " + " ".join(f"{k:>8s}" for k in keys))
     for n, lst in acc.items():
         print(f"{n:32s} " + " ".join(f"{np.median([d.get(k, np.nan) for d in lst]):8.2f}" for k in keys))
