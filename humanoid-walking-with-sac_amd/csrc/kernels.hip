@@ -935,14 +935,13 @@ __device__ __forceinline__ uint32_t s_ld(sbuf_i4 r, uint32_t byte_off) {
   return (uint32_t)llvm_s_buffer_load_i32(r, (int)byte_off, 0);
 }
 
-__device__ __forceinline__ void adam_block0(const AdamFuse& af, int err, float omb1, float omb2) {
-  __syncthreads();
-  // wave 0 only, on wave-uniform values read by scalar loads (s_ld): the block's tail used
-  // to wait behind its own epilogue stores and then walk a chain of dependent round trips
-  // (loss partials; log_alpha's state and bias corrections; the ring position; done_seq) —
-  // 2.5-4 us past the other workgroups of the Adam levels (phase stamps).  Every value read
-  // here was written by an earlier level.
-  if (threadIdx.x >= 64) return;
+// The fused-Adam level's scalar work (losses, the alpha step, the loss ring, the done word),
+// by ONE wave, on wave-uniform values read by scalar loads (s_ld).  Every value it reads
+// was written by an earlier level, and nothing of the level reads what it writes, so it
+// runs at the level's start (k_gemm, GemmBatch::adam_wg -2: wave 0 of block 0 before its
+// tile) — after the tile it made block 0 the level's last workgroup by 2.7-2.9 us (a chain
+// of dependent round trips, then a system-scope fence; phase stamps, profiles/r04).
+__device__ __forceinline__ void adam_block0_wave(const AdamFuse& af, int err, float omb1, float omb2) {
   const sbuf_i4 rLp = s_rsrc(af.loss_part), rSc = s_rsrc(af.sc);
   const bool alpha = af.log_alpha_idx >= 0 && af.auto_entropy;
   const uint32_t ao = (uint32_t)(alpha ? af.log_alpha_idx : 0) * 4u;
@@ -998,6 +997,12 @@ __device__ __forceinline__ void adam_block0(const AdamFuse& af, int err, float o
     __threadfence_system();                  // the losses and error bits land first
     *reinterpret_cast<volatile int*>(af.done_word) = v;
   }
+}
+// ... after the block's tile (adam_wg -1, or a dedicated workgroup): wave 0
+__device__ __forceinline__ void adam_block0(const AdamFuse& af, int err, float omb1, float omb2) {
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  adam_block0_wave(af, err, omb1, omb2);
 }
 
 // Polyak workgroup w of nw (RideAlong::pk): grid-stride float4 groups of the critic arena,
@@ -1385,6 +1390,15 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
   place_tile(d, t, tr, tc);
   const int m0 = tr * TMW, n0 = tc * TN;
   if constexpr (CORE == 0) SACMI_PHASE(batch.tl, 9);   // (diagnostic: the tile is placed)
+  if constexpr (ADAM) {
+    // the level's scalar Adam work first, on wave 0 of block 0 (adam_block0_wave): the
+    // other waves start their K loops, wave 0 follows ~3 us later, inside the tile's time
+    if (adam_wg == -2 && bid == 0 && threadIdx.x < 64) {
+      const AdamFuse& a = batch.adam;
+      adam_block0_wave(a, (int)s_ld(s_rsrc(a.sc), (uint32_t)offsetof(DevScalars, err)), 1.f - a.beta1,
+                       1.f - a.beta2);
+    }
+  }
   const bool rowsum = d.rs_col >= 0 && n0 == 0;
   const AdamFuse& af = batch.adam;
   // Adam bias corrections and the error bits: thread 0 reads them in pre(), behind its
@@ -1691,7 +1705,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
       }
     }
   }
-  if (batch.has_adam && batch.adam_wg < 0 && bid == 0) {
+  if (batch.has_adam && adam_wg == -1 && bid == 0) {
     adam_block0(af, err, omb1, omb2);
   }
   SACMI_PHASE(batch.tl, 5);
@@ -3228,13 +3242,15 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (level_act16(b))
     throw Error{SACMI_ESTATE, "bf16 activation operands on a level outside the batch-4096-class kernels"};
   const int extra0 = (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
-  // a fused-Adam level's scalar work on a workgroup of its own, after the tiles and rides
-  // (SACMI_ADAM_WG=1; measured: L13's slowest workgroup 12.3 -> 9.7 us, but the update no
-  // faster — the level's end is its last tile's, and L6 took +0.85 us: off by default)
+  // a fused-Adam level's scalar work: by default wave 0 of block 0 before its tile (-2);
+  // SACMI_B0_LATE=1: block 0 after its tile (-1, the round-3 form); SACMI_ADAM_WG=1: a
+  // workgroup of its own past the tiles and rides (measured: the 257th workgroup of L6 / L13
+  // waits for a free CU — L6 +0.85 us, L13 no faster)
   static const bool adam_wg_on = std::getenv("SACMI_ADAM_WG") != nullptr && std::atoi(std::getenv("SACMI_ADAM_WG")) != 0;
+  static const bool b0_late = std::getenv("SACMI_B0_LATE") != nullptr && std::atoi(std::getenv("SACMI_B0_LATE")) != 0;
   const bool awg = b.has_adam && adam_wg_on;
   const int extra = extra0 + (awg ? 1 : 0);
-  b.adam_wg = -1;
+  b.adam_wg = b0_late ? -1 : -2;
   auto set_awg = [&](int tiles) { if (awg) b.adam_wg = tiles + extra0; };
   auto grid_for = [&](int tiles) { set_awg(tiles); return tiles + extra; };
   if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > kRideLdsBytes)

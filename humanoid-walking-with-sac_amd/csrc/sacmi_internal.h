@@ -408,7 +408,8 @@ struct GemmBatch {
   int has_adam;
   int adam_wg;         // k_gemm: the workgroup that runs the level's scalar Adam work (losses,
                        //   alpha step, loss ring, done word) — an extra workgroup past the
-                       //   tiles and rides (launch_gemm), or -1: block 0 after its tile
+                       //   tiles and rides (launch_gemm), -1: block 0 after its tile, or
+                       //   -2: wave 0 of block 0 before its tile
   RideAlong ride;      // extra workgroups after the tiles
   RowsFuse rows;       // prologue for axk-1 descs
   int bf16;            // 1: bf16 MFMA operands (fp32 loads rounded to bf16 in registers)
