@@ -205,7 +205,7 @@ def median_windows(fn, windows):
     return float(np.median(vals)), vals
 
 
-def cpu_baseline(rows, seconds=15.0, warmup=5, batch=BATCH, per=False, n_hidden=2, windows=3):
+def cpu_baseline(rows, seconds=20.0, warmup=5, batch=BATCH, per=False, n_hidden=2, windows=5):
     """The reference update on CPU (oracle torch port, fp32) + the reference's replay
     data path (deque + random.sample, or the prioritized buffer's numpy sampler), timed
     on this host's cores for a bounded number of steps."""
@@ -385,7 +385,7 @@ def parse_args(argv=None):
     ap.add_argument("--windows", type=int, default=0,
                     help="timed windows of --steps updates each (median reported); 0: enough "
                          "windows for >= 2000 timed updates (at least 5)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--updates-per-launch", type=int, default=20,
