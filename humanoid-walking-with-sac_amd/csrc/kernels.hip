@@ -1143,7 +1143,7 @@ __device__ void rows_finish(const RowsFuse& rf, const GemmDesc& d, int m0, bool 
         // every load goes out at once
         const int err = rf.sc->err;
         const bool any = (err & kErrSkipAll) == 0;
-        const bool all = any && (err & ERR_NAN_ACT) == 0;
+        const bool all = any && (err & kErrActLike) == 0;
         for (int i = 0; i < 4; ++i) {
           const bool adv = all || (any && (i == 1 || i == 2));
           rf.sc->step[i] += adv ? 1.0 : 0.0;
@@ -1242,6 +1242,18 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
 #ifndef SACMI_PIPE_DW
 #define SACMI_PIPE_DW 0
 #endif
+
+// data-parallel phase 0: the update's error flags for the critic gradient collective
+// (kDpFlagN; GemmBatch::err_flags).  Every error source of the update ran before this level.
+__device__ __forceinline__ void store_err_flags(const GemmBatch& b) {
+  if (b.err_flags && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int err = *b.err_word;
+    b.err_flags[0] = (err & kErrSkipAll) ? 1.f : 0.f;
+    b.err_flags[1] = (err & kErrActLike) ? 1.f : 0.f;
+    b.err_flags[2] = 0.f;
+    b.err_flags[3] = 0.f;
+  }
+}
 
 // waves per SIMD the register allocation must allow: every wave of the workgroup
 // resident at once, one workgroup per CU
@@ -1708,6 +1720,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
   if (batch.has_adam && adam_wg == -1 && bid == 0) {
     adam_block0(af, err, omb1, omb2);
   }
+  store_err_flags(batch);
   SACMI_PHASE(batch.tl, 5);
 }
 
@@ -2993,6 +3006,7 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
     }
   }
   if (adam && blockIdx.x == 0) adam_block0(af, s_err, omb1, omb2);
+  store_err_flags(batch);
 }
 
 // 1 when the level carries bf16 activation operands (any GemmDesc a16 / b16 / c16 / x16);
@@ -3858,7 +3872,16 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     int64_t p = 0;
     for (int i = 0; i < a.nseg; ++i) { s_prefix[i] = p; p += a.seg[i].n / 4; }
     s_prefix[a.nseg] = p;
-    s_err = a.sc->err;
+    int err = a.sc->err;
+    if (a.err_flags) {
+      // the flags summed over the ranks: a rank that saw a non-finite input makes every rank
+      // void the same steps (block 0 records the remote bits for the rest of the stream)
+      const int rb = (a.err_flags[0] > 0.f ? (int)ERR_REMOTE_SKIP : 0) |
+                     (a.err_flags[1] > 0.f ? (int)ERR_REMOTE_ACT : 0);
+      if (rb && blockIdx.x == 0) atomicOr(&a.sc->err, rb);
+      err |= rb;
+    }
+    s_err = err;
   }
   __syncthreads();
   const float om_b1 = 1.f - a.beta1, om_b2 = 1.f - a.beta2, omtau = 1.f - a.tau;

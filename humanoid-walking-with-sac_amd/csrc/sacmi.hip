@@ -61,6 +61,52 @@ static void registry_remove(uintptr_t base) {
 // the validator self test checks against its own host arrays instead (this thread only)
 static thread_local const std::vector<AllocRec>* g_registry_override = nullptr;
 
+// Host-side bounds check before anything is launched: every element a kernel can touch
+// (incl. the 16-byte over-read of K-contiguous GEMM fetches) must lie in ONE registered
+// allocation.  GEMM levels go through validate(); every other host-launched kernel that
+// writes an arena (conversions, fills, scales, column sets) through the checked launchers
+// below — the bf16 shadow refresh once converted past its shadow's end (round 4).
+static void check_span(const void* p, int64_t max_index, const char* what, int elem_bytes = 4) {
+  if (!p) throw Error{SACMI_ESTATE, std::string("null kernel operand ") + what};
+  const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)(max_index + 1) * elem_bytes;
+  if (g_registry_override) {
+    for (const AllocRec& r : *g_registry_override)
+      if (a >= r.base && e <= r.base + r.bytes) return;
+  } else {
+    std::lock_guard<std::mutex> g(registry_mutex());
+    for (const AllocRec& r : alloc_registry())
+      if (a >= r.base && e <= r.base + r.bytes) return;
+  }
+  throw Error{SACMI_ESTATE, std::string("kernel operand out of bounds: ") + what};
+}
+
+// dst[0, n) = bf16(src[0, n)): both spans inside one allocation each
+static void check_to_bf16(const unsigned short* dst, const float* src, int64_t n) {
+  if (n <= 0) return;
+  check_span(dst, n - 1, "bf16 shadow (conversion destination)", 2);
+  check_span(src, n - 1, "bf16 shadow source");
+}
+static void to_bf16_checked(unsigned short* dst, const float* src, int64_t n, hipStream_t s) {
+  check_to_bf16(dst, src, n);
+  if (n > 0) launch_to_bf16(dst, src, n, s);
+}
+static void scale_checked(float* p, int64_t n, float f, hipStream_t s) {
+  if (n <= 0) return;
+  check_span(p, n - 1, "scaled range");
+  launch_scale(p, n, f, s);
+}
+static void fill_checked(float* p, int64_t n, float v, hipStream_t s) {
+  if (n <= 0) return;
+  check_span(p, n - 1, "filled range");
+  launch_fill(p, n, v, s);
+}
+static void set_column_checked(float* p, int rows, int ld, int col, float v, hipStream_t s) {
+  if (rows <= 0) return;
+  if (col < 0 || col >= ld) throw Error{SACMI_ESTATE, "column outside its row"};
+  check_span(p, (int64_t)(rows - 1) * ld + col, "column set");
+  launch_set_column(p, rows, ld, col, v, s);
+}
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -144,7 +190,15 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> pa;         // dL/da partials [2 * nparts][B][A] (L9 epilogue -> tail)
   sacmi::DevBuf<float> act_h;      // select_action's one-state hidden rows [nh][Hd] (1 at H)
   int pending_step = 0;             // batch of a sacmi_step_launch not yet waited for
-  bool inflight = false;            // updates enqueued since the last full wait
+  // updates enqueued since the last wait.  A synchronous step's wait (step_finish) ends when
+  // the update's done word lands: the fused-Adam levels' block 0 stores it at the START of the
+  // last level, behind its losses — "losses ready", NOT "update complete": that level's Adam
+  // stores may still be in flight.  Safe because every reader the wait releases is either
+  // stream-ordered behind the level (kernels, select_action) or synchronises the stream
+  // itself (tensor / scalar / replay reads), and no host staging (push slots, mailbox) is
+  // read by that level or its rides (a ride's sampler never takes the mailbox: MailboxArgs
+  // go to the update's own sampler launch only)
+  bool inflight = false;
   int pending_done = -1;            // the done word before that launch (step_finish)
   // The next single update's minibatch, drawn ahead: a device-sampled single update
   // (sacmi_step / _async / _launch) also runs the NEXT update's random.sample + gather as
@@ -189,8 +243,9 @@ struct sacmi_ctx {
   int mb_pending = 0;               // rows in it
   bool mb_graph = false;            // the update being enqueued consumes them
   // stream epochs: bumped by every zero-copy push; `done_epoch` = the epoch of the last
-  // completed wait (step / act / synchronize): every earlier launch has finished, so a
-  // staging slot read at an earlier epoch is free without an event (an event record is
+  // completed wait (step / act / synchronize): every earlier launch that reads host staging
+  // has finished (a step's wait: every launch up to its last level's start — see `inflight`),
+  // so a staging slot read at an earlier epoch is free without an event (an event record is
   // one more packet between the push and the update behind it)
   int64_t epoch = 1, done_epoch = 0;
   int push_slot = 0;
@@ -220,6 +275,9 @@ struct sacmi_ctx {
   // 1/world of the parameters, all-gather the parameters (enqueue_dp)
   bool dp_shard = false;
   bool dp_sharding_now = false;   // enqueue_dp is enqueueing a sharded sequence
+  // a sharded step ran at world >= 2: each rank's Adam moments are current on its own chunks
+  // only — reading them (tensors, checkpoints) raises until sacmi_dp_sync_state gathers them
+  bool moments_sharded = false;
   std::map<std::tuple<int, int, int64_t>, hipGraphExec_t> dp_graphs;   // (batch, n, PER fill)
   uint64_t act_calls = 0;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
   // profiling (sacmi_profile_step): one event per launch site
@@ -292,6 +350,11 @@ static void build_layout(sacmi_ctx* c) {
   off = round_up64(off, 64);
   c->q_end = off;
   REQUIRE((c->q_end - c->q_begin) % 4 == 0 && c->q_begin % 4 == 0, SACMI_ESTATE, "critic region not float4-aligned");
+  // kShardSlack floats between the critic and the actor ranges: the data-parallel step's
+  // collective over the critic range reaches past q_end (the sharded form's last chunk, and
+  // the error flags of kDpFlagOff) — into this gap, never into the actor's gradients or
+  // parameters.  The actor range's reach past `total` lands in the arenas' tail slack.
+  off += kShardSlack;
   c->pi_begin = off;
   take(c->p_fc[0], H, S, c->Kp1, S, S, true);
   for (int l = 1; l < c->nh; ++l) take(c->p_fc[l], H, H, c->Hd, H, H, true);
@@ -327,7 +390,9 @@ static void alloc_all(sacmi_ctx* c) {
   c->P.alloc(c->total + kShardSlack); c->G.alloc(c->total + kShardSlack);
   c->M.alloc(c->total); c->V.alloc(c->total);
   c->T.alloc(c->q_end);
-  if (c->bf16) { c->Ph.alloc(c->total); c->Th.alloc(c->q_end); }
+  // (the shadows mirror their arenas element for element, P's slack included: refresh_shadows
+  // converts P.n elements — round 4 sized Ph at `total` and wrote 16 KB past it)
+  if (c->bf16) { c->Ph.alloc(c->P.n); c->Th.alloc(c->T.n); }
   c->sc.alloc(1);
   c->ldo = round_up(S, 4);
   c->ldact = round_up(A, 4);
@@ -386,16 +451,16 @@ static void alloc_all(sacmi_ctx* c) {
   c->lp_part.alloc((size_t)2 * ((2 * Bm + 15) / 16) + 2);   // heads: per-workgroup logp sums
   hipStream_t s = c->stream;
   // constant-1 (bias) columns
-  launch_set_column(c->xq.p, Bm, c->Kx, S, 1.f, s);
-  launch_set_column(c->x2.p, 2 * Bm, c->Kx, S, 1.f, s);
-  launch_set_column(c->xqb.p, Bm, c->Kx, S, 1.f, s);
-  launch_set_column(c->x2b.p, 2 * Bm, c->Kx, S, 1.f, s);
+  set_column_checked(c->xq.p, Bm, c->Kx, S, 1.f, s);
+  set_column_checked(c->x2.p, 2 * Bm, c->Kx, S, 1.f, s);
+  set_column_checked(c->xqb.p, Bm, c->Kx, S, 1.f, s);
+  set_column_checked(c->x2b.p, 2 * Bm, c->Kx, S, 1.f, s);
   for (int l = 0; l < nh; ++l) {
-    launch_set_column(c->hp[l].p, 2 * Bm, c->Hd, H, 1.f, s);
-    launch_set_column(c->act_h.p + (size_t)l * c->Hd, 1, c->Hd, H, 1.f, s);
+    set_column_checked(c->hp[l].p, 2 * Bm, c->Hd, H, 1.f, s);
+    set_column_checked(c->act_h.p + (size_t)l * c->Hd, 1, c->Hd, H, 1.f, s);
     for (auto* b : {&c->hq[l], &c->hqt[l], &c->hqa[l]}) {
-      launch_set_column(b->p, Bm, 2 * c->Hd, H, 1.f, s);
-      launch_set_column(b->p, Bm, 2 * c->Hd, c->Hd + H, 1.f, s);
+      set_column_checked(b->p, Bm, 2 * c->Hd, H, 1.f, s);
+      set_column_checked(b->p, Bm, 2 * c->Hd, c->Hd + H, 1.f, s);
     }
   }
   CHECK_HIP(hipStreamSynchronize(s));
@@ -522,22 +587,10 @@ static GemmDesc gd_dw_h(const float* dY, int ldy, const float* X, int ldx, float
   return d;
 }
 
-// Host-side bounds check of one GEMM before it is ever launched: every element the
-// kernel can touch (incl. the 16-byte over-read of K-contiguous fetches) must lie in
-// one registered allocation, and vector-loaded operands must be 16-byte aligned.
-static void check_span(const void* p, int64_t max_index, const char* what, int elem_bytes = 4) {
-  if (!p) throw Error{SACMI_ESTATE, std::string("null GEMM operand ") + what};
-  const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)(max_index + 1) * elem_bytes;
-  if (g_registry_override) {
-    for (const AllocRec& r : *g_registry_override)
-      if (a >= r.base && e <= r.base + r.bytes) return;
-  } else {
-    std::lock_guard<std::mutex> g(registry_mutex());
-    for (const AllocRec& r : alloc_registry())
-      if (a >= r.base && e <= r.base + r.bytes) return;
-  }
-  throw Error{SACMI_ESTATE, std::string("GEMM operand out of bounds: ") + what};
-}
+// Host-side bounds check of one GEMM before it is ever launched (check_span, defined with
+// the allocation registry above): every element the kernel can touch (incl. the 16-byte
+// over-read of K-contiguous fetches) must lie in one registered allocation, and
+// vector-loaded operands must be 16-byte aligned.
 
 static void validate(const GemmDesc& d) {
   if (d.M <= 0 || d.N <= 0 || d.K <= 0) throw Error{SACMI_ESTATE, "empty GEMM"};
@@ -831,7 +884,9 @@ static AdamArgs dp_adam_args(sacmi_ctx* c, bool critic, int B, float grad_scale,
     ad.tau = (float)c->cfg.tau; ad.step_offset = 1;
     ad.loss_part = c->lpart_c.p; ad.loss_slot0 = 0; ad.n_losses = 2;
     ad.log_alpha_idx = -1; ad.auto_entropy = 0;
-    ad.err_skip = kErrSkipAll; ad.err_nopolyak = ERR_NAN_ACT;
+    ad.err_skip = kErrSkipAll; ad.err_nopolyak = kErrActLike;
+    // every rank's error flags, summed by the critic gradient collective (kDpFlagN)
+    ad.err_flags = c->G.p + c->q_end;
   } else {
     ad.tgt = nullptr; ad.tau = 0.f; ad.step_offset = 0;
     ad.loss_part = c->lpart_a.p; ad.loss_slot0 = 2; ad.n_losses = 1;
@@ -1031,12 +1086,17 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       f.loss_host = c->loss_host_dev;
       f.Ph = c->Ph.p; f.Th = c->Th.p;
       f.loss_div = (float)B; f.log_alpha_idx = -1; f.auto_entropy = 0;
-      f.err_skip = kErrSkipAll; f.err_nopolyak = ERR_NAN_ACT;
+      f.err_skip = kErrSkipAll; f.err_nopolyak = kErrActLike;
     }
     if (ride_b) {   // the next update's random.sample rides in L6 (placement B)
       l6.b.ride.kind = 1; l6.b.ride.nblocks = 1;
       l6.b.ride.tbl_log2 = mt_sample_tbl_log2(B, true);
       l6.b.ride.mt = mt_args(c, B, batch_bufs(c, parity ^ 1));
+    }
+    if (!fuse) {   // data parallel: this update's error flags ride in the critic collective
+      l6.b.err_flags = G + c->q_end;
+      l6.b.err_word = &c->sc.p->err;
+      check_span(l6.b.err_flags, kDpFlagN - 1, "error flags");
     }
     run(l6, fuse ? "gemm_L6_critic_dW_adam" : "gemm_L6_critic_dW1");
   }
@@ -1355,6 +1415,9 @@ static std::string nan_message(const sacmi_ctx* c, int err, int B, const std::st
   if (err & ERR_NAN_PER) m = "probabilities contain NaN (PrioritizedReplayBuffer.sample, replay_buffer.py:64)";
   else if (err & ERR_NAN_TGT) m = normal + "policy.sample(next_state_batch) (sac_imp.py:89)";
   else if (err & (ERR_NAN_ACT | ERR_ABORT)) m = normal + "policy.sample(state_batch) (sac_imp.py:116)";
+  else if (err & (ERR_REMOTE_SKIP | ERR_REMOTE_ACT))
+    m = "non-finite value in another data-parallel rank's update (its update raised ValueError; "
+        "this rank voided the same steps)";
   else m = "non-finite value (error bits " + std::to_string(err) + ")";
   return m + where;
 }
@@ -1441,16 +1504,20 @@ static RcclApi& rccl() {
 // applied by the Adam kernels.
 // Sharded (ZeRO-1) form, per range [b, e) of the arena (critic, then actor): the gradients
 // are reduce-scattered in place into chunk r (kShardAlign-float multiples; the last chunk may
-// reach past e — into the next range's gradients, rewritten by its own level later, or into
-// the arena slack), Adam runs on chunk r of the parameters (the layer segments clipped to
-// it), and the parameters are all-gathered in place.  Replicas stay bitwise identical: every
+// reach past e — into the gap between the critic and actor ranges, or into the arena's tail
+// slack, never into the other range), Adam runs on chunk r of the parameters (the layer
+// segments clipped to it), and the parameters are all-gathered in place.  A reduce-scatter
+// does not deliver the error flags past q_end to every rank, so this form all-reduces them
+// on their own first (kDpFlagN floats; the all-reduce form carries them in its critic range).  Replicas stay bitwise identical: every
 // chunk is computed by one rank and the gather copies its bits.  Adam moments (M, V) are
 // valid on each rank's own chunks only (sacmi_dp_sync_state gathers them, e.g. before a
 // checkpoint).  Loopback: `world` identical ranks emulated on one GPU — the gradients x world
 // in place, Adam on every rank's chunk in turn (rank 0 alone finalises the losses / ring),
 // the gather an identity.
+// Off by default (round 5): the sharded sequence has run only through the loopback emulation,
+// never over real RCCL ranks; SACMI_DP_SHARD=1 or sacmi_dp_set_sharded selects it
 #ifndef SACMI_DP_SHARD_DEFAULT
-#define SACMI_DP_SHARD_DEFAULT 1
+#define SACMI_DP_SHARD_DEFAULT 0
 #endif
 static bool dp_shard_default(int world) {
   if (const char* e = std::getenv("SACMI_DP_SHARD")) return std::atoi(e) != 0 && world <= kMaxShardWorld;
@@ -1459,6 +1526,15 @@ static bool dp_shard_default(int world) {
 
 static int64_t shard_chunk(int64_t n, int world) {
   return round_up64((n + world - 1) / world, kShardAlign);
+}
+
+// Loopback stand-in for the collective over the error flags: `world` identical ranks sum to
+// world x this rank's flags; SACMI_DP_LOOPBACK_REMOTE_ERR=1 (tests) adds another rank whose
+// update saw a non-finite input of the skip-all class
+static void loopback_flags(sacmi_ctx* c, float* f, hipStream_t s) {
+  scale_checked(f, kDpFlagN, (float)c->dp_world, s);
+  const char* e = std::getenv("SACMI_DP_LOOPBACK_REMOTE_ERR");
+  if (e && std::atoi(e) != 0) fill_checked(f, 1, (float)c->dp_world + 1.f, s);
 }
 
 static void dp_shard_adam(sacmi_ctx* c, bool critic, int B, int r, bool use_ring) {
@@ -1490,19 +1566,32 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
     e = critic ? c->q_end : c->total;
   };
   auto reduce_scatter = [&](bool critic) {
-    (void)mark(c, critic ? "reduce_scatter_critic_grads" : "reduce_scatter_actor_grads");
     int64_t b, e;
     range(critic, b, e);
     const int64_t ch = shard_chunk(e - b, W);
     float* g = c->G.p + b;
-    if (c->dp_loopback) launch_scale(g, e - b, (float)W, s);
-    else CHECK_RCCL(rccl().reduce_scatter(g, g + c->dp_rank * ch, (size_t)ch, ncclFloat32, ncclSum, c->comm, s));
+    if (critic) {   // the error flags to every rank (the reduce-scatter delivers chunk r only)
+      (void)mark(c, "allreduce_error_flags");
+      float* f = c->G.p + c->q_end;
+      if (c->dp_loopback) loopback_flags(c, f, s);
+      else CHECK_RCCL(rccl().all_reduce(f, f, (size_t)kDpFlagN, ncclFloat32, ncclSum, c->comm, s));
+    }
+    (void)mark(c, critic ? "reduce_scatter_critic_grads" : "reduce_scatter_actor_grads");
+    // (loopback: the whole span the collective covers, the last chunk's reach included —
+    // the critic's flags past q_end too: already summed above, so the span stops at them)
+    if (c->dp_loopback) {
+      scale_checked(g, std::min(ch * W, critic ? e - b : ch * W), (float)W, s);
+      if (critic && ch * W > e - b + kDpFlagN)
+        scale_checked(g + (e - b) + kDpFlagN, ch * W - (e - b) - kDpFlagN, (float)W, s);
+    } else {
+      CHECK_RCCL(rccl().reduce_scatter(g, g + c->dp_rank * ch, (size_t)ch, ncclFloat32, ncclSum, c->comm, s));
+    }
   };
   auto step = [&](bool critic) {   // Adam on the chunk(s), gather, the replicated scalars / shadows
     (void)mark(c, critic ? "adam_critic_shard" : "adam_actor_shard");
     // (SACMI_DP_LOOPBACK_ONE_RANK: timing only — rank 0's chunk alone, the per-rank work
     // of a `world`-rank run minus its collectives; the other chunks are left unstepped)
-    static const bool one_rank = std::getenv("SACMI_DP_LOOPBACK_ONE_RANK") != nullptr;
+    const bool one_rank = std::getenv("SACMI_DP_LOOPBACK_ONE_RANK") != nullptr;   // (read per capture)
     if (c->dp_loopback && !one_rank) {
       for (int r = 0; r < W; ++r) dp_shard_adam(c, critic, B, r, true);
     } else if (c->dp_loopback) {
@@ -1518,13 +1607,15 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
       float* p = c->P.p + b;
       CHECK_RCCL(rccl().all_gather(p + c->dp_rank * ch, p, (size_t)ch, ncclFloat32, c->comm, s));
     }
-    if (c->Ph.p) launch_to_bf16(c->Ph.p + b, c->P.p + b, e - b, s);
+    if (c->Ph.p) to_bf16_checked(c->Ph.p + b, c->P.p + b, e - b, s);
     if (!critic && c->cfg.auto_entropy) launch_alpha_sync(c->sc.p, c->P.p + c->la_idx, ~0, s);
   };
   // Polyak rides in phase 1's L12 where it can (enqueue_update: polyak_ride), else its own pass
   const bool pk_ride = std::getenv("SACMI_NO_POLYAK_RIDE") == nullptr && !act16_on(c, B) &&
                        (int64_t)((B + 31) / 32) * ((c->H + 31) / 32) <= 192;
   c->dp_sharding_now = true;
+  const bool one_rank_only = std::getenv("SACMI_DP_LOOPBACK_ONE_RANK") != nullptr;
+  if ((!c->dp_loopback && W > 1) || (c->dp_loopback && one_rank_only)) c->moments_sharded = true;
   try {
     int parity = 0;
     bool have = false;
@@ -1561,12 +1652,17 @@ static void enqueue_dp(sacmi_ctx* c, int B, int n) {
   const float scale = 1.f / (float)c->dp_world;
   const bool ride = n > 1 && ride_possible(c, B);
   auto allreduce = [&](int64_t begin, int64_t end) {
-    (void)mark(c, begin == c->q_begin ? "allreduce_critic_grads" : "allreduce_actor_grads");
+    const bool critic = begin == c->q_begin;
+    (void)mark(c, critic ? "allreduce_critic_grads" : "allreduce_actor_grads");
     float* g = c->G.p + begin;
-    if (c->dp_loopback)   // what `world` ranks holding identical shards would all-reduce to
-      launch_scale(g, end - begin, (float)c->dp_world, c->stream);
-    else
-      CHECK_RCCL(rccl().all_reduce(g, g, (size_t)(end - begin), ncclFloat32, ncclSum, c->comm, c->stream));
+    if (c->dp_loopback) {   // what `world` ranks holding identical shards would all-reduce to
+      scale_checked(g, end - begin, (float)c->dp_world, c->stream);
+      if (critic) loopback_flags(c, c->G.p + c->q_end, c->stream);
+    } else {
+      // the critic range carries the error flags past q_end (kDpFlagN)
+      const int64_t n = end - begin + (critic ? kDpFlagN : 0);
+      CHECK_RCCL(rccl().all_reduce(g, g, (size_t)n, ncclFloat32, ncclSum, c->comm, c->stream));
+    }
   };
   int parity = 0;
   bool have = false;
@@ -1668,7 +1764,9 @@ int sacmi_destroy(sacmi_ctx* c) {
   return guard([&] {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    // a fault left by the context's last work is reported by this call (SACMI_EDEVICE), after
+    // the context's resources are released — not discarded
+    const hipError_t sync_err = hipStreamSynchronize(c->stream);
     destroy_graphs(c);
     free_pinned(c);
     if (c->comm) (void)rccl().destroy(c->comm);
@@ -1696,6 +1794,9 @@ int sacmi_destroy(sacmi_ctx* c) {
     if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
     for (hipEvent_t e : c->side_ev) (void)hipEventDestroy(e);
     delete c;
+    if (sync_err != hipSuccess)
+      throw Error{SACMI_EDEVICE, std::string("sacmi_destroy: the context's stream had failed: ") +
+                                     hipGetErrorString(sync_err)};
   });
 }
 
@@ -1724,8 +1825,15 @@ int sacmi_tensor_numel(sacmi_ctx* c, int net, int layer, int part, int64_t* nume
   });
 }
 
+static void require_moments_whole(const sacmi_ctx* c) {
+  REQUIRE(!c->moments_sharded, SACMI_ESTATE,
+          "the Adam moments are sharded across the data-parallel ranks (sharded optimizer step): "
+          "call sacmi_dp_sync_state on every rank before reading or writing them");
+}
+
 static float* slot_base(sacmi_ctx* c, int slot, int net) {
   const bool target = net == SACMI_Q1_TARGET || net == SACMI_Q2_TARGET;
+  if (slot == SACMI_SLOT_ADAM_M || slot == SACMI_SLOT_ADAM_V) require_moments_whole(c);
   if (target) {
     REQUIRE(slot == SACMI_SLOT_PARAM, SACMI_EVALUE, "target nets only have parameters");
     return c->T.p - c->q_begin;
@@ -1742,8 +1850,8 @@ static float* slot_base(sacmi_ctx* c, int slot, int net) {
 // re-derive the bf16 shadows after a host write into the parameter / target arenas
 static void refresh_shadows(sacmi_ctx* c) {
   if (!c->Ph.p) return;
-  launch_to_bf16(c->Ph.p, c->P.p, (int64_t)c->P.n, c->stream);
-  launch_to_bf16(c->Th.p, c->T.p, (int64_t)c->T.n, c->stream);
+  to_bf16_checked(c->Ph.p, c->P.p, (int64_t)c->P.n, c->stream);
+  to_bf16_checked(c->Th.p, c->T.p, (int64_t)c->T.n, c->stream);
   CHECK_HIP(hipStreamSynchronize(c->stream));
 }
 
@@ -1800,8 +1908,8 @@ static void arena_scalar(sacmi_ctx* c, float* arena, int64_t idx, const double* 
 static void scalar_io(sacmi_ctx* c, int which, const double* in, double* out) {
   switch (which) {
     case SACMI_S_LOG_ALPHA: arena_scalar(c, c->P.p, c->la_idx, in, out); return;
-    case SACMI_S_ADAM_M_LOG_ALPHA: arena_scalar(c, c->M.p, c->la_idx, in, out); return;
-    case SACMI_S_ADAM_V_LOG_ALPHA: arena_scalar(c, c->V.p, c->la_idx, in, out); return;
+    case SACMI_S_ADAM_M_LOG_ALPHA: require_moments_whole(c); arena_scalar(c, c->M.p, c->la_idx, in, out); return;
+    case SACMI_S_ADAM_V_LOG_ALPHA: require_moments_whole(c); arena_scalar(c, c->V.p, c->la_idx, in, out); return;
     case SACMI_S_GRAD_LOG_ALPHA: arena_scalar(c, c->G.p, c->la_idx, in, out); return;
     case SACMI_S_GRAPH_COUNT:
       REQUIRE(!in, SACMI_EVALUE, "the graph count is read-only");
@@ -2448,7 +2556,7 @@ int sacmi_dp_sync_state(sacmi_ctx* c) {
   return guard([&] {
     pf_touch(c);
     REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
-    if (!c->dp_shard || c->dp_loopback || c->dp_world == 1) return;
+    if (!c->moments_sharded || c->dp_loopback || c->dp_world == 1) return;
     // every rank's chunks of the Adam moments, in place (M and V carry no slack: the last
     // chunk is gathered through a bounce of the padded size)
     const int W = c->dp_world;
@@ -2467,6 +2575,7 @@ int sacmi_dp_sync_state(sacmi_ctx* c) {
       CHECK_HIP(hipStreamSynchronize(c->stream));
       tmp.release();
     }
+    c->moments_sharded = false;
   });
 }
 
@@ -2511,7 +2620,9 @@ int sacmi_grad_buffer(sacmi_ctx* c, int which, void** ptr, int64_t* numel) {
   return guard([&] {
     pf_touch(c);
     REQUIRE(which == 0 || which == 1, SACMI_EVALUE, "which must be 0 (critic) or 1 (actor)");
-    if (which == 0) { *ptr = c->G.p + c->q_begin; *numel = c->q_end - c->q_begin; }
+    // (the critic range carries the kDpFlagN error flags past q_end: the caller's collective
+    // sums them with the gradients)
+    if (which == 0) { *ptr = c->G.p + c->q_begin; *numel = c->q_end - c->q_begin + kDpFlagN; }
     else { *ptr = c->G.p + c->pi_begin; *numel = c->total - c->pi_begin; }
   });
 }
@@ -2863,7 +2974,7 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     if (!zc) {
       CHECK_HIP(hipMemcpy2DAsync(c->x2.p, (size_t)Kx * 4, src, (size_t)(pinned ? Kx : S) * 4, (size_t)S * 4, n,
                                  hipMemcpyHostToDevice, s));
-      launch_set_column(c->x2.p, n, Kx, S, 1.f, s);   // (a bf16-activation update may have
+      set_column_checked(c->x2.p, n, Kx, S, 1.f, s);   // (a bf16-activation update may have
     }                                                   //  overwritten the fp32 ones column)
     // one state (the env-rate call): the policy forward as GEMVs (k_act_gemv / k_act_heads:
     // a wave per output instead of 32-row level tiles that use one row), fp32, from the
@@ -3012,7 +3123,33 @@ int sacmi_selftest_span_checker(int32_t* n_cases, int32_t* n_passed) {
       }
       pass += ok == k.accept;
     }
-    *n_cases = (int32_t)cases.size();
+    // the host-launched conversions (refresh_shadows / the sharded gather's shadow pass):
+    // an arena of `total` floats plus the data-parallel slack and its bf16 shadow.  Round 4
+    // sized the shadow at `total` and converted the whole arena: 8 KB past the shadow's end
+    const int64_t total = 1000, slack = 64;
+    std::vector<float> arena((size_t)(total + slack));
+    std::vector<unsigned short> shadow_full((size_t)(total + slack)), shadow_short((size_t)total);
+    reg.push_back({(uintptr_t)arena.data(), arena.size() * sizeof(float)});
+    reg.push_back({(uintptr_t)shadow_full.data(), shadow_full.size() * sizeof(unsigned short)});
+    reg.push_back({(uintptr_t)shadow_short.data(), shadow_short.size() * sizeof(unsigned short)});
+    struct Conv { bool accept; unsigned short* dst; const float* src; int64_t n; };
+    const Conv conv[] = {
+        {true, shadow_full.data(), arena.data(), total + slack},     // the whole arena
+        {true, shadow_short.data(), arena.data(), total},            // the layout only
+        {false, shadow_short.data(), arena.data(), total + slack},   // round 4's overrun
+        {true, shadow_full.data() + 64, arena.data() + 64, total + slack - 64},   // a chunk
+        {false, shadow_full.data() + 64, arena.data() + 64, total + slack},       // past both
+    };
+    for (const Conv& k : conv) {
+      bool ok = true;
+      try {
+        check_to_bf16(k.dst, k.src, k.n);
+      } catch (const Error&) {
+        ok = false;
+      }
+      pass += ok == k.accept;
+    }
+    *n_cases = (int32_t)(cases.size() + sizeof(conv) / sizeof(conv[0]));
     *n_passed = pass;
   });
 }

@@ -196,10 +196,24 @@ struct Linear {
 //                the frame has advanced, the numpy stream has not
 //   ERR_ABORT    set once an ERR_NAN_ACT update has taken its critic step: every later
 //                kernel of the stream skips its state writes
+//   ERR_REMOTE_SKIP / ERR_REMOTE_ACT  (data-parallel updates) another rank's update saw a bit
+//                of the skip-all class / ERR_NAN_ACT: every rank then voids the same steps, so
+//                the replicas stay identical (the error flags travel with the critic gradient
+//                collective: kDpFlagN)
 // The host reports and clears them (sacmi_step / sacmi_fetch_losses / sacmi_per_sample).
-enum ErrBits : int { ERR_NAN_TGT = 1, ERR_NAN_ACT = 2, ERR_NAN_PER = 4, ERR_ABORT = 8 };
+enum ErrBits : int { ERR_NAN_TGT = 1, ERR_NAN_ACT = 2, ERR_NAN_PER = 4, ERR_ABORT = 8,
+                     ERR_REMOTE_SKIP = 16, ERR_REMOTE_ACT = 32 };
 // an update that sees any of these takes none of its steps
-constexpr int kErrSkipAll = ERR_NAN_TGT | ERR_NAN_PER | ERR_ABORT;
+constexpr int kErrSkipAll = ERR_NAN_TGT | ERR_NAN_PER | ERR_ABORT | ERR_REMOTE_SKIP;
+// ... and these: the critic step stands, the Polyak / actor / alpha steps do not
+constexpr int kErrActLike = ERR_NAN_ACT | ERR_REMOTE_ACT;
+// Data-parallel error flags: kDpFlagN floats right past the critic range of the gradient arena
+// (in the gap before the actor range), inside the critic gradient collective.  The phase-0
+// weight-gradient level stores flag 0 = (err & kErrSkipAll) != 0, flag 1 = (err & kErrActLike)
+// != 0 (GemmBatch::err_flags); after the sum over ranks the critic Adam ORs ERR_REMOTE_* into
+// the device error word where a flag is positive (AdamArgs::err_flags).  Every error source
+// of an update (heads, PER sampler) runs before that level, so one exchange per update suffices.
+constexpr int kDpFlagN = 4;
 
 // Scalars shared by kernels (device resident, one struct per context).
 struct DevScalars {
@@ -417,6 +431,10 @@ struct GemmBatch {
   int64_t ws_floats;   //   (capacity; launch_gemm falls back when a level needs more)
   tl_word* tl;         // launch timeline slots of this level (kTlPerSite), or null
   int st_wt;           // k_gemm epilogue stores write-through (set by launch_gemm)
+  // data-parallel phase 0's last level: block 0 stores the error flags (kDpFlagN) of
+  // *err_word here, before the critic gradient collective (null: none)
+  float* err_flags;
+  const int* err_word;
 };
 
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked
@@ -538,6 +556,9 @@ struct AdamArgs {
   unsigned short* ph;      // bf16 shadows of p / tgt (bf16 mode) or null
   unsigned short* tgth;
   int err_skip, err_nopolyak;   // as AdamFuse
+  // data-parallel critic step: the error flags summed over the ranks (kDpFlagN), combined into
+  // the error word before the skip test (null: the local word alone)
+  const float* err_flags;
   tl_word* tl;
 };
 void launch_adam(const AdamArgs& a, hipStream_t s);

@@ -248,3 +248,40 @@ def test_nan_split_k_bf16_and_phase_paths():
         sample_indices(mt, 8192, B)              # the first update's draw only
         assert pos1 == mt.pos and np.array_equal(key1, np.asarray(mt.key, np.uint32)), mode
         ctx.close()
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_dp_remote_nan_voids_the_update_on_every_rank(sharded):
+    """Data parallel: a rank whose update sees a non-finite input (another rank, emulated by
+    the loopback's SACMI_DP_LOOPBACK_REMOTE_ERR) makes every rank void the same steps — the
+    error flags travel with the critic gradient collective (csrc/sacmi_internal.h kDpFlagN),
+    so no rank applies a partial update and the replicas stay identical.  This rank's own
+    inputs are finite: its update raises ValueError naming the other rank, takes no step, and
+    the launch's later updates draw nothing (the first update's random.sample only)."""
+    import os
+    from sacmi import Config, Context
+    B = 64
+    ctx = Context(Config(S, A, H, max_batch=B, capacity=4096), 0)
+    rng = np.random.default_rng(8)
+    ctx.push(rng.standard_normal((4096, S)).astype(np.float32),
+             rng.uniform(-0.4, 0.4, (4096, A)).astype(np.float32),
+             rng.standard_normal(4096).astype(np.float32),
+             rng.standard_normal((4096, S)).astype(np.float32), rng.random(4096) < 0.02)
+    ctx.dp_loopback_init(2)
+    ctx.dp_set_sharded(sharded)
+    before = _snapshot(ctx)
+    key0, pos0 = ctx.get_mt(0)
+    os.environ["SACMI_DP_LOOPBACK_REMOTE_ERR"] = "1"
+    try:
+        ctx.step_dp(B, 3)
+        ctx.synchronize()
+    finally:
+        os.environ.pop("SACMI_DP_LOOPBACK_REMOTE_ERR", None)
+    with pytest.raises(ValueError, match="another data-parallel rank"):
+        ctx.fetch_losses(8)
+    _same(before, _snapshot(ctx), before.keys())
+    key1, pos1 = ctx.get_mt(0)
+    mt = MT19937(np.asarray(key0, np.uint32), pos0)
+    sample_indices(mt, 4096, B)
+    assert pos1 == mt.pos and np.array_equal(key1, np.asarray(mt.key, np.uint32))
+    ctx.close()

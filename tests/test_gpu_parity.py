@@ -1086,3 +1086,71 @@ def test_single_updates_drawn_ahead_identical():
     for n in NETS:
         for k in p1[n]:
             assert np.array_equal(p1[n][k], p2[n][k]), (n, k)
+
+
+@pytest.mark.parametrize("world", [3, 5, 6])
+def test_native_dp_loopback_sharded_equals_allreduce_nonpow2(world):
+    """Non-power-of-two worlds (the chunk tiling of the sharded form: chunks of 64-float
+    multiples that do not divide the ranges, the last one reaching into the gap past the
+    critic range / the arena's tail slack): x world then x 1/world is not exact in fp32 there,
+    so the update is not the fused one — but the sharded form (reduce-scatter -> Adam on each
+    rank's chunk -> all-gather, every rank's chunk run in turn) and the all-reduce form apply
+    the same two scalings to every element, and must agree BIT FOR BIT: parameters, Adam
+    moments, log_alpha state, losses."""
+    from sacmi import _lib as L
+    cfg, B, nrows, n = SacConfig(376, 17, 512), 256, 4000, 3
+    params = init_params(cfg, 97, bias_scale=0.05)
+    rows = synthetic_rows(cfg, nrows, 98, state_scale=0.5)
+    key = (np.arange(624, dtype=np.uint64) * 1812433 % (2**32)).astype(np.uint32)
+    ctxs = []
+    for sharded in (True, False):
+        ctx = make_ctx(cfg, max_batch=B, capacity=nrows, seed=5)
+        load_params(ctx, params)
+        ctx.push(*rows)
+        ctx.set_mt(0, key, 624)
+        ctx.dp_loopback_init(world)
+        ctx.dp_set_sharded(sharded)
+        assert ctx.dp_sharded() == sharded
+        ctx.step_dp(B, n)
+        ctx.synchronize()
+        ctxs.append(ctx)
+    a, b = ctxs
+    for nm in NETS:
+        for slot in (("param", "m", "v") if nm in ("policy", "q1", "q2") else ("param",)):
+            x, y = a.get_net(nm, slot), b.get_net(nm, slot)
+            for k in x:
+                assert np.array_equal(x[k], y[k]), (world, nm, slot, k)
+    for sid in (L.S_LOG_ALPHA, L.S_ADAM_M_LOG_ALPHA, L.S_ADAM_V_LOG_ALPHA, L.S_ALPHA, L.S_STEP_POLICY):
+        assert a.get_scalar(sid) == b.get_scalar(sid), sid
+    assert np.array_equal(a.fetch_losses(n), b.fetch_losses(n))
+    for c in ctxs:
+        c.close()
+
+
+def test_dp_sharded_moments_read_guard():
+    """After a sharded optimizer step that leaves other ranks' chunks of the Adam moments
+    stale on this rank (here: the loopback's one-rank timing mode, which steps rank 0's chunk
+    only — what a real world >= 2 rank holds), reading the moments (tensors, the log_alpha
+    moment scalars, hence checkpoints) raises instead of returning stale values; parameters
+    stay readable."""
+    from sacmi import _lib as L
+    cfg, B = SacConfig(24, 4, 64), 64
+    params = init_params(cfg, 99, bias_scale=0.05)
+    rows = synthetic_rows(cfg, 400, 100, state_scale=0.5)
+    ctx = make_ctx(cfg, max_batch=B, capacity=400, seed=5)
+    load_params(ctx, params)
+    ctx.push(*rows)
+    ctx.dp_loopback_init(4)
+    ctx.dp_set_sharded(True)
+    os.environ["SACMI_DP_LOOPBACK_ONE_RANK"] = "1"
+    try:
+        ctx.step_dp(B, 2)
+    finally:
+        os.environ.pop("SACMI_DP_LOOPBACK_ONE_RANK", None)
+    ctx.synchronize()
+    assert all(np.all(np.isfinite(v)) for v in ctx.get_net("q1").values())
+    with pytest.raises(RuntimeError, match="sharded"):
+        ctx.get_net("q1", "m")
+    with pytest.raises(RuntimeError, match="sharded"):
+        ctx.get_scalar(L.S_ADAM_V_LOG_ALPHA)
+    ctx.close()
