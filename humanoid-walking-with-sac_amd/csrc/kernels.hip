@@ -76,6 +76,12 @@ __device__ __forceinline__ rsrc_t make_rsrc(const float* base, uint32_t bytes) {
 __device__ __forceinline__ float buf_ld(rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
+// ... with cache-policy bits (AUX 16 = sc1: L1 bypass, for data another workgroup of the same
+// launch wrote write-through: cdna_hip_programming.md §6 Guideline 16)
+template <int AUX>
+__device__ __forceinline__ float buf_ld_aux(rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, AUX));
+}
 __device__ __forceinline__ void buf_st(rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)off, 0, 0);
 }
@@ -140,6 +146,7 @@ struct OpFetch {
 #ifndef SACMI_FETCH_SADDR
 #define SACMI_FETCH_SADDR 0
 #endif
+constexpr int kLdSc1 = 16;      // raw buffer load cache-policy bits: sc1 (coherent across XCDs)
 #ifndef SACMI_A_AUX
 #define SACMI_A_AUX 0           // k_gemm: cache-policy bits of the A-operand loads (experiment)
 #endif
@@ -306,8 +313,8 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // registers then hold the second buffer instead).  Same chunk order per wave: bitwise
 // identical sums.
 template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
-          int AXF = 0, bool BF16 = false, int PIPE = 0, bool A16 = false, class Pre,
-          class Early = void (*)()>
+          int AXF = 0, bool BF16 = false, int PIPE = 0, bool A16 = false, int AAUX = SACMI_A_AUX,
+          class Pre, class Early = void (*)()>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
                                             float* rsum, Pre&& pre, bool store_a = false,
                                             Early&& early = [] {}) {
@@ -363,7 +370,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
     auto issue = [&](int jj, float (&av)[MT][4], float (&bv)[NT][4], float (&xv)[4]) {
       jj = jj < nmine ? jj : nmine - 1;   // unconditional: past the end re-reads the last chunk
       const int k = SACMI_CHUNK(jj) * 16 + kl;
-      fetch_op<MT, AKC, A16, SACMI_A_AUX>(ra, d.lda, k, d.K, av);
+      fetch_op<MT, AKC, A16, AAUX>(ra, d.lda, k, d.K, av);
       fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, bv);
       if constexpr (!AKC) {
 #pragma unroll
@@ -415,7 +422,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       // chunk re-reads that chunk and is skipped below
       const int jj = j + g < nmine ? j + g : nmine - 1;
       const int k = SACMI_CHUNK(jj) * 16 + kl;
-      fetch_op<MT, AKC, A16, SACMI_A_AUX>(ra, d.lda, k, d.K, a[g]);
+      fetch_op<MT, AKC, A16, AAUX>(ra, d.lda, k, d.K, a[g]);
       fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, b[g]);
       if constexpr (AXF == 1) {          // w3 rows are float4-aligned (parameter arena)
         const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
@@ -510,24 +517,26 @@ __device__ __forceinline__ void place_tile(const GemmDesc& d, int t, int& tr, in
 // layout dispatch (wave-uniform, once per workgroup)
 // AXK: whether this kernel instantiation carries the A-transform path (launch_gemm picks
 // the variant from the level's descs): 1 -> axk 1 descs, 0 -> none.
-template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, int PIPE, class Pre,
+// AAUX: cache-policy bits of the A-operand loads (kg_body's LDAUX)
+template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, int PIPE, int AAUX, class Pre,
           class Early>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
                                           float* rsum, bool rowsum, Pre&& pre, Early&& early) {
+  constexpr int AX = AAUX ? AAUX : SACMI_A_AUX;
   if constexpr (AXK == 1) {
     if (d.axk == 1) {        // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
-      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1, BF16>(
+      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1, BF16, 0, false, AX>(
           d, m0, n0, red, rsum, pre, n0 == 0 && d.ax_out != nullptr, early);
       return;
     }
   }
   if (d.a_kc) {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
-    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
   } else {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
-    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
-    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16, PIPE>(d, m0, n0, red, rsum, pre);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
+    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
   }
 }
 
@@ -1063,7 +1072,7 @@ struct RowsRegs {
   float lpa;                  // actor block 0, wave past the row threads: logp_part[lane]
 };
 
-template <int TMW, int NTH>
+template <int TMW, int NTH, int AUX = 0>
 __device__ __forceinline__ void rows_load(const RowsFuse& rf, const GemmDesc& d, int m0,
                                           RowsRegs& x) {
   const int t = threadIdx.x;
@@ -1085,7 +1094,7 @@ __device__ __forceinline__ void rows_load(const RowsFuse& rf, const GemmDesc& d,
     const uint32_t base = (uint32_t)(((size_t)sl * rf.B + m0 + row) * rf.nparts) * 4u;
 #pragma unroll
     for (int i = 0; i < kRowsPv; ++i)
-      x.pv[i] = buf_ld(rPart, ok && i < rf.nparts ? base + 4u * i : oob);
+      x.pv[i] = buf_ld_aux<AUX>(rPart, ok && i < rf.nparts ? base + 4u * i : oob);
   }
   const int b = m0 + t;
   const uint32_t ob = (uint32_t)((t < TMW && b < rf.B) ? b : 0) * 4u;
@@ -1255,6 +1264,12 @@ __device__ __forceinline__ void store_err_flags(const GemmBatch& b) {
   }
 }
 
+// the policy heads + GaussianPolicy.sample of rows [m0, m0 + TM) (defined with k_heads_sample;
+// k_gemm runs it folded into the last policy hidden layer's level, GemmBatch::heads)
+template <int TN, int KSPLIT, bool H16, int TM, int AAUX>
+__device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int part, float* red,
+                                           float (*lp)[33], float* s_lp);
+
 // waves per SIMD the register allocation must allow: every wave of the workgroup
 // resident at once, one workgroup per CU
 template <int W>
@@ -1272,8 +1287,37 @@ constexpr int stg_ring() {
   if constexpr (CORE == 1) return StgGeo<TMW, TN, KSP>::RING;
   else return 1;
 }
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false, int CORE = 0>
-__global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
+// LDS of one k_gemm configuration (kg_body)
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE>
+constexpr bool kg_heads_fold() {
+  return !ADAM && AXK == 0 && CORE == 0 && !BF16 && MG == 1 && TM == kHeadsFoldTM && TN == 64 &&
+         KSPLIT == 16 && G == 2;
+}
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE>
+struct KgSmem {
+  static constexpr int TMW = TM * MG;
+  static constexpr bool PA = AXK == 1 && MG == 1;
+  static constexpr bool HF = kg_heads_fold<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>();
+  alignas(16) unsigned char ring[stg_ring<CORE, TMW, TN, KSPLIT>()];
+  float red_l[CORE ? 1 : MG * KSPLIT * TM * (TN + 1)];
+  float s_kw[CORE ? kStgKW : 1];
+  float rsum[MG * KSPLIT * TM];
+  AdamScalars s_k;
+  int s_err;
+  float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
+  float s_pa[PA ? TMW * (TN + 1) + TN * 32 : 1];
+  float s_hlp[HF ? kHeadsFoldTM * 33 + kHeadsFoldTM : 1];
+  int s_hlast;
+};
+
+// The body of one k_gemm workgroup: work item `bid_in` of the level (a tile, a ride-along
+// workgroup, the scalar Adam workgroup).  k_gemm runs it as blockIdx.x; the persistent chain
+// kernel (k_chain) runs it for each work item of its cohort.  LDAUX: cache-policy bits of the
+// loads of operands another workgroup of the SAME launch produced (the A operand, the row
+// prologue's dot partials, the ReLU-mask source): sc1 (16) in k_chain, 0 in k_gemm.
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, int LDAUX>
+__device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in,
+                                        KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>& sm) {
   // The scalars that locate this workgroup's work come in ONE kernarg round trip: left to
   // the compiler, each load sat behind a branch on the previous one (timeline pointer, tile
   // count, one desc's tile_begin per loop trip, then the desc's fields as they were used),
@@ -1286,13 +1330,19 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
 #pragma unroll
   for (int q = 0; q < kMaxGemms; ++q) tbeg[q] = batch.d[q].tile_begin;
   const int adam_wg = batch.adam_wg;
-  asm volatile("" :: "s"(tl), "s"(n_tiles), "s"(n_desc), "s"(adam_wg));
+  // (k_chain runs several bodies in one register allocation: there the pins would keep ~40
+  // SGPRs of each level live at once — spills — so it leaves the loads to the compiler)
+  constexpr bool PINS = LDAUX == 0;
+  if constexpr (PINS) {
+    asm volatile("" :: "s"(tl), "s"(n_tiles), "s"(n_desc), "s"(adam_wg));
 #pragma unroll
-  for (int q = 0; q < kMaxGemms; ++q) asm volatile("" :: "s"(tbeg[q]));
+    for (int q = 0; q < kMaxGemms; ++q) asm volatile("" :: "s"(tbeg[q]));
+  }
 #if SACMI_PIN_EPI
   // ... with the level-wide epilogue scalars that do not depend on the desc (the row
   // prologue's / fused Adam's pointers): otherwise their loads sit behind the desc's
-  if constexpr (AXK == 1) {
+  if constexpr (!PINS) {
+  } else if constexpr (AXK == 1) {
     const RowsFuse& r = batch.rows;
     asm volatile("" :: "s"(r.part), "s"(r.logp), "s"(r.r), "s"(r.d), "s"(r.kind), "s"(r.nparts),
                  "s"(r.B), "s"(r.sc), "s"(r.logp_part), "s"(r.n_lp));
@@ -1302,7 +1352,6 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
                  "s"(a.step_offset));
   }
 #endif
-  const TlMark tl_mark(tl, TL_GEMM);
   SACMI_PHASE(tl, 0);
   SACMI_PHASE_LAST(tl, 6);
   constexpr int TMW = TM * MG;
@@ -1311,19 +1360,27 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
   // K vector (ax_w / a_ksc) staging
   constexpr int RING = stg_ring<CORE, TMW, TN, KSPLIT>();
   static_assert(!CORE || RING >= MG * KSPLIT * TM * (TN + 1) * 4, "staged ring holds the partial tiles");
-  __shared__ __attribute__((aligned(16))) unsigned char ring[RING];
-  __shared__ float red_l[CORE ? 1 : MG * KSPLIT * TM * (TN + 1)];
-  __shared__ float s_kw[CORE ? kStgKW : 1];
-  float* const red = CORE ? reinterpret_cast<float*>(ring) : red_l;
-  __shared__ float rsum[MG * KSPLIT * TM];
-  __shared__ AdamScalars s_k;
-  __shared__ int s_err;
-  __shared__ float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
+  // LDS (KgSmem: the caller's, so that a persistent kernel can run several configurations
+  // in one allocation)
+  unsigned char* const ring = sm.ring;
+  float* const red = CORE ? reinterpret_cast<float*>(sm.ring) : sm.red_l;
+  float* const s_kw = sm.s_kw;
+  float* const rsum = sm.rsum;
+  AdamScalars& s_k = sm.s_k;
+  int& s_err = sm.s_err;
+  auto& s_q = sm.s_q;
+  auto& s_coef = sm.s_coef;
+  auto& s_l = sm.s_l;
+  auto& s_dotw = sm.s_dotw;
   // dL/da partials (axk-1 levels of one 32-row wave group): the tile's outputs [TMW][TN+1]
   // and its fc1 action weights [TN][32]
   constexpr bool PA = AXK == 1 && MG == 1;
-  __shared__ float s_pa[PA ? TMW * (TN + 1) + TN * 32 : 1];
-  const int bid = blockIdx.x;
+  float* const s_pa = sm.s_pa;
+  // the policy heads folded into this level (GemmBatch::heads): the fp32 32x64 forward tiles
+  constexpr bool HF = kg_heads_fold<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>();
+  float* const s_hlp = sm.s_hlp;
+  int& s_hlast = sm.s_hlast;
+  const int bid = bid_in;
 #ifdef SACMI_EXP_EMPTY
   if (bid < batch.total_tiles) return;   // timing experiment only: the launch, nothing else
 #endif
@@ -1379,7 +1436,8 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
 #define SACMI_DESC_PIN_E "s"(d.C), "s"(d.aux), "s"(d.ldc), "s"(d.ldaux), "s"(d.epi), "s"(d.bias), \
     "s"(d.bias_ld), "s"(d.dotw), "s"(d.dotp), "s"(d.rs_col), "s"(d.axk), "s"(d.ax_w), "s"(d.ax_out), \
     "s"(d.ax_ld), "s"(d.a_ksc)
-  if constexpr (ADAM) {
+  if constexpr (!PINS) {
+  } else if constexpr (ADAM) {
     const AdamFuse& a = batch.adam;
     asm volatile("" :: SACMI_DESC_PIN_K, SACMI_DESC_PIN_E, "s"(a.P), "s"(a.M), "s"(a.V), "s"(a.T),
                  "s"(a.G), "s"(a.t_base), "s"(a.lr), "s"(a.beta1), "s"(a.beta2), "s"(a.eps),
@@ -1393,7 +1451,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
     asm volatile("" :: SACMI_DESC_PIN_K, SACMI_DESC_PIN_E);
   }
 #else
-  asm volatile("" :: SACMI_DESC_PIN_K);
+  if constexpr (PINS) asm volatile("" :: SACMI_DESC_PIN_K);
 #endif
   if constexpr (CORE == 0) SACMI_PHASE(batch.tl, 8);   // (diagnostic: the desc has landed)
   const int t = bid - tbeg[p];
@@ -1502,7 +1560,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
     // axk 1: the row prologue's loads.  Issued here, behind the operand burst, and
     // consumed after the MFMAs: anything in flight at the k-loop header is waited for by
     // the back-edge's conservative vmcnt on the first iteration.
-    if constexpr (AXK == 1) rows_load<TMW, NTH>(batch.rows, d, m0, rows_x);   // unconditional
+    if constexpr (AXK == 1) rows_load<TMW, NTH, LDAUX>(batch.rows, d, m0, rows_x);   // unconditional
     if constexpr (PA) {   // zero-length range where the level has no partials
       const rsrc_t rPW = make_rsrc(has_pa ? d.pa_w : d.C,
                                    has_pa ? (uint32_t)(((size_t)(d.N - 1) * d.pa_ld + d.pa_A) * 4) : 0u);
@@ -1550,7 +1608,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
         const uint32_t o = !ok ? kOob
                          : d.bias ? (uint32_t)(n * d.bias_ld) * 4u
                                   : (uint32_t)((m0 + row) * d.ldaux + n) * 4u;
-        x0[s] = buf_ld(rX, o);
+        x0[s] = buf_ld_aux<LDAUX>(rX, o);
       }
     }
   };
@@ -1562,7 +1620,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
   if constexpr (CORE == 1)
     gemm_core_stg<TM, TN, KSPLIT, MG, AXK>(d, m0, n0, ring, rsum, s_kw, rowsum, pre, batch.tl);
   else
-    gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE>(d, m0, n0, red, rsum, rowsum, pre, [] {});
+    gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE, LDAUX>(d, m0, n0, red, rsum, rowsum, pre, [] {});
   SACMI_PHASE(batch.tl, 2);
   SACMI_PHASE_LAST(batch.tl, 7);
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
@@ -1683,7 +1741,7 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
         c = row16_sum(c);                 // DPP within each 16-lane row
         c += __shfl_xor(c, 16, 64);       // the two rows of the half wave
         if ((tid & 31) == 0 && m0 + row < d.M)   // block 0 adds the bias: q = sum of blocks
-          d.dotp[(size_t)(m0 + row) * d.dotp_ld + (n0 + col) / 32] = n0 + col == 0 ? c + dotb_x : c;
+          st_pol(d.dotp + (size_t)(m0 + row) * d.dotp_ld + (n0 + col) / 32, n0 + col == 0 ? c + dotb_x : c, wt);
       }
     }
     if constexpr (PA) {   // every tile element, 0 outside the output
@@ -1721,7 +1779,34 @@ __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves
     adam_block0(af, err, omb1, omb2);
   }
   store_err_flags(batch);
+  if constexpr (HF) {
+    // folded heads: the tile's h stores (write-through) acknowledged in every wave, then the
+    // row block's arrival count; its last column tile runs the heads + sample of the block's
+    // 32 rows, reading h with sc1 loads (rows the other tiles stored from other XCDs)
+    if (batch.heads_ticket != nullptr && p == batch.heads_desc) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int* tk = batch.heads_ticket + m0 / kHeadsFoldTM;
+        const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_hlast = old == d.tiles_n - 1;
+        if (old == d.tiles_n - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (s_hlast)
+        heads_rows<48, 16, false, kHeadsFoldTM, kLdSc1>(batch.heads, m0, m0 / kHeadsFoldTM, red,
+                                                         reinterpret_cast<float(*)[33]>(s_hlp),
+                                                         s_hlp + kHeadsFoldTM * 33);
+    }
+  }
   SACMI_PHASE(batch.tl, 5);
+}
+
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false, int CORE = 0>
+__global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_GEMM);
+  __shared__ KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE> sm;
+  kg_body<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, 0>(batch, blockIdx.x, sm);
 }
 
 // Tile order and XCD placement.  Workgroups are dealt round-robin over the 8 XCDs
@@ -3124,6 +3209,8 @@ static bool all_bh(const GemmBatch& b) {
 
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
+  if (b0.heads_ticket && !gemm_level_heads_fold_ok(b0, b0.heads.A))
+    throw Error{SACMI_ESTATE, "policy heads folded into a level outside k_gemm's 32x64 forward tiles"};
   GemmBatch b = b0;
   // Polyak rides (RideAlong::pk) run on k_gemm's 1024-thread configurations only: a level
   // that goes to a split-K / LDS-staged kernel must not carry them
@@ -3400,16 +3487,17 @@ __device__ __forceinline__ float one_minus_tanh2(float x) {
 // go to act as bf16 (the next levels' input columns)
 // TM rows per workgroup (heads_rows_per_wg: 32 at the batch-4096 class — one workgroup
 // per CU covers all rows in one round and the head weights are re-read half as often)
-template <int TN, int KSPLIT, bool H16 = false, int TM = 16>
-__global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) {
-  const TlMark tl_mark(a.tl, TL_HEADS);
-  __shared__ float red[KSPLIT * TM * (TN + 1)];
-  __shared__ float lp[TM][33];
+// rows [m0, m0 + TM) by one 64 * KSPLIT-thread workgroup; part: the row block's slot pair in
+// logp_part; red (KSPLIT * TM * (TN + 1) floats), lp, s_lp: LDS.  AAUX: cache-policy bits of
+// the h loads (k_gemm's folded form reads h rows other workgroups of the same launch wrote:
+// sc1, coherent across the XCDs' L2s)
+template <int TN, int KSPLIT, bool H16, int TM, int AAUX>
+__device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int part, float* red,
+                                           float (*lp)[33], float* s_lp) {
   const int A = a.A;
   GemmDesc d;
   d.A = a.h; d.lda = a.ldh; d.a_kc = 1; d.M = a.rows;
   d.B = a.Wh; d.ldb = a.ldw; d.b_kc = 1; d.N = 2 * A; d.K = a.K;
-  const int m0 = blockIdx.x * TM;
   static_assert(TM * 32 <= 64 * KSPLIT, "one (row, action) element per thread (A <= 32)");
   // element e = threadIdx.x -> (row, action j); its bias values (and stored noise)
   // are loaded while the MFMAs run
@@ -3425,7 +3513,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
     eps_in = buf_ld(make_rsrc(want ? a.eps : a.Wh, want ? 0x7fffffffu : 0u),
                     (uint32_t)((size_t)mm * A + jj) * 4u);
   };
-  gemm_core_l<TM, TN, KSPLIT, 2, true, true, false, 1, 0, false, 0, H16>(d, m0, 0, red, nullptr, pre);
+  gemm_core_l<TM, TN, KSPLIT, 2, true, true, false, 1, 0, false, 0, H16, AAUX>(d, m0, 0, red, nullptr, pre);
   __syncthreads();
   const uint64_t ctr = a.ctr_override ? a.ctr_override : a.sc->noise_counter;
   if (e < TM * A) {
@@ -3475,7 +3563,6 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
     lp[row][j] = lpe;
   }
   __syncthreads();
-  __shared__ float s_lp[TM];
   if (threadIdx.x < TM) {
     const int mm = m0 + threadIdx.x;
     float s = 0.f;
@@ -3493,9 +3580,18 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
         const int mm = m0 + r;
         if (mm < a.rows && (mm >= a.split_row) == (threadIdx.x == 1)) s += s_lp[r];
       }
-      a.logp_part[2 * blockIdx.x + threadIdx.x] = s;
+      a.logp_part[2 * part + threadIdx.x] = s;
     }
   }
+}
+
+template <int TN, int KSPLIT, bool H16 = false, int TM = 16>
+__global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) {
+  const TlMark tl_mark(a.tl, TL_HEADS);
+  __shared__ float red[KSPLIT * TM * (TN + 1)];
+  __shared__ float lp[TM][33];
+  __shared__ float s_lp[TM];
+  heads_rows<TN, KSPLIT, H16, TM, 0>(a, blockIdx.x * TM, blockIdx.x, red, lp, s_lp);
   if (a.done_word) {   // (one workgroup) every store above lands first
     __threadfence_system();
     __syncthreads();
@@ -3722,33 +3818,34 @@ void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream
   HIP_LAUNCH_CHECK();
 }
 
-// The sample backward + dhp2 tail of the actor pass (sac_imp.py:116-125 backward through
-// GaussianPolicy.sample, networks_model1.py:78-99) from the dL/da partials the dha1 level's
-// epilogue wrote (GemmDesc::pa_out): one workgroup per (16-row block, 64-column slab of
-// dhp2).  dL/da = the n_pa column-block partials summed in fixed order; then the same
-// per-element algebra as k_gemm_sample_bwd; the slab-0 workgroups store dhead (the heads'
-// weight-gradient operand); dhp2 = (dhead Whead) * [hp2 > 0] for the slab.  Every
-// workgroup of a row block recomputes the row block's dhead (a few hundred FMAs).
 constexpr int kTailRows = 8, kTailCols = 64, kTailMaxPa = 64;
-__global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_pa, SampleBwdArgs a) {
-  const TlMark tl_mark(a.tl, TL_SAMPLE_TAIL);
-  __shared__ float s_dh[kTailRows][64 + 1];       // dhead rows, zero beyond 2A
-  __shared__ float s_w[64][kTailCols + 1];        // Whead[k][slab columns], k < 2A
+struct TailSmem {
+  float s_dh[kTailRows][64 + 1];       // dhead rows, zero beyond 2A
+  float s_w[64][kTailCols + 1];        // Whead[k][slab columns], k < 2A
+};
+// One unit: rows [m0, m0 + 8) x dhp2 columns [c0, c0 + 64), by the first 256 threads of the
+// workgroup (any others only join its barriers).  slab0: the unit also stores dhead.  AUX:
+// cache-policy bits of the dL/da partial loads (k_chain: sc1 — L9 wrote them in the same launch)
+template <int AUX>
+__device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const SampleBwdArgs& a, int m0,
+                                          int c0, bool slab0, TailSmem& sm) {
+  auto& s_dh = sm.s_dh;
+  auto& s_w = sm.s_w;
   const int A = a.A, B = a.B, K2 = 2 * A;
-  const int m0 = blockIdx.x * kTailRows, c0 = blockIdx.y * kTailCols;
   const int tid = threadIdx.x;
-  // every global load of the kernel goes out first (one round trip): thread e < 8A owns
+  const bool act = tid < 256;
+  // every global load of the unit goes out first (one round trip): thread e < 8A owns
   // (row e / A, action e % A) — its partials, cache and noise; all threads stage a share
   // of the Whead slab and of the ReLU mask.  Buffer loads at out-of-range offsets return
   // 0 without an access, so no load sits behind a guard.
   const int prow = tid / A, pj = tid - prow * A, pm = m0 + prow;
-  const bool own = tid < kTailRows * A && pm < B;
+  const bool own = act && tid < kTailRows * A && pm < B;
   const rsrc_t rP = make_rsrc(pa, (uint32_t)((size_t)n_pa * B * A * 4));
   const uint32_t pstride = (uint32_t)B * (uint32_t)A * 4u, po = (uint32_t)((own ? pm : 0) * A + pj) * 4u;
   float t[kTailMaxPa];
 #pragma unroll
   for (int q = 0; q < kTailMaxPa; ++q)
-    t[q] = buf_ld(rP, own && q < n_pa ? po + (uint32_t)q * pstride : 0xfffffff0u);
+    t[q] = buf_ld_aux<AUX>(rP, own && q < n_pa ? po + (uint32_t)q * pstride : 0xfffffff0u);
   const rsrc_t rC = make_rsrc(a.cache, (uint32_t)((size_t)B * 3 * A * 4));
   const rsrc_t rE = make_rsrc(a.eps, (uint32_t)((size_t)B * A * 4));
   const uint32_t co = own ? (uint32_t)(pm * 3 * A + pj) * 4u : 0xfffffff0u;
@@ -3761,22 +3858,24 @@ __global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_
 #pragma unroll
   for (int q = 0; q < WPT; ++q) {
     const int e = tid + q * 256, k = e / kTailCols, col = c0 + (e - k * kTailCols);
-    wv[q] = buf_ld(rW, k < K2 && col < a.H ? (uint32_t)(k * a.ldw + col) * 4u : 0xfffffff0u);
+    wv[q] = buf_ld(rW, act && k < K2 && col < a.H ? (uint32_t)(k * a.ldw + col) * 4u : 0xfffffff0u);
   }
   // the dhp2 thread layout: row tid / 32 (8 rows), 2 consecutive slab columns
-  const int row = tid >> 5, cq = (tid & 31) * 2, m = m0 + row;
+  const int row = act ? tid >> 5 : 0, cq = (tid & 31) * 2, m = m0 + row;
   const rsrc_t rH = make_rsrc(a.hp2, (uint32_t)(((size_t)(B - 1) * a.ldh + a.H) * 4));
   float mk[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int col = c0 + cq + u;
-    mk[u] = buf_ld(rH, m < B && col < a.H ? (uint32_t)(m * a.ldh + col) * 4u : 0xfffffff0u);
+    mk[u] = buf_ld(rH, act && m < B && col < a.H ? (uint32_t)(m * a.ldh + col) * 4u : 0xfffffff0u);
   }
-  for (int e = tid; e < kTailRows * 65; e += 256) (&s_dh[0][0])[e] = 0.f;
+  if (act) {
+    for (int e = tid; e < kTailRows * 65; e += 256) (&s_dh[0][0])[e] = 0.f;
 #pragma unroll
-  for (int q = 0; q < WPT; ++q) {
-    const int e = tid + q * 256, k = e / kTailCols;
-    s_w[k][e - k * kTailCols] = wv[q];
+    for (int q = 0; q < WPT; ++q) {
+      const int e = tid + q * 256, k = e / kTailCols;
+      s_w[k][e - k * kTailCols] = wv[q];
+    }
   }
   __syncthreads();
   if (own) {
@@ -3792,7 +3891,7 @@ __global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_
     const float dx = G * omy2;
     float dls = dx * eps * sd - glogp;
     if (!(ls_raw >= -20.f && ls_raw <= 2.f)) dls = 0.f;
-    if (blockIdx.y == 0) {
+    if (slab0) {
       a.dhead[(size_t)pm * a.lddh + pj] = dx;
       a.dhead[(size_t)pm * a.lddh + A + pj] = dls;
     }
@@ -3800,19 +3899,34 @@ __global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_
     s_dh[prow][A + pj] = dls;
   }
   __syncthreads();
-  float acc[2] = {0.f, 0.f};
-  for (int k = 0; k < K2; ++k) {
-    const float hk = s_dh[row][k];
-    acc[0] = fmaf(hk, s_w[k][cq], acc[0]);
-    acc[1] = fmaf(hk, s_w[k][cq + 1], acc[1]);
-  }
-  if (m < B) {
+  if (act) {
+    float acc[2] = {0.f, 0.f};
+    for (int k = 0; k < K2; ++k) {
+      const float hk = s_dh[row][k];
+      acc[0] = fmaf(hk, s_w[k][cq], acc[0]);
+      acc[1] = fmaf(hk, s_w[k][cq + 1], acc[1]);
+    }
+    if (m < B) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int col = c0 + cq + u;
-      if (col < a.H) st_wt(a.dhp2 + (size_t)m * a.H + col, mk[u] > 0.f ? acc[u] : 0.f);
+      for (int u = 0; u < 2; ++u) {
+        const int col = c0 + cq + u;
+        if (col < a.H) st_wt(a.dhp2 + (size_t)m * a.H + col, mk[u] > 0.f ? acc[u] : 0.f);
+      }
     }
   }
+}
+
+// The sample backward + dhp2 tail of the actor pass (sac_imp.py:116-125 backward through
+// GaussianPolicy.sample, networks_model1.py:78-99) from the dL/da partials the dha1 level's
+// epilogue wrote (GemmDesc::pa_out): one workgroup per (8-row block, 64-column slab of
+// dhp2).  dL/da = the n_pa column-block partials summed in fixed order; then the same
+// per-element algebra as k_gemm_sample_bwd; the slab-0 workgroups store dhead (the heads'
+// weight-gradient operand); dhp2 = (dhead Whead) * [hp2 > 0] for the slab.  Every
+// workgroup of a row block recomputes the row block's dhead (a few hundred FMAs).
+__global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_pa, SampleBwdArgs a) {
+  const TlMark tl_mark(a.tl, TL_SAMPLE_TAIL);
+  __shared__ TailSmem sm;
+  tail_unit<0>(pa, n_pa, a, blockIdx.x * kTailRows, blockIdx.y * kTailCols, blockIdx.y == 0, sm);
 }
 
 void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, hipStream_t s) {
@@ -3824,9 +3938,198 @@ void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, h
   HIP_LAUNCH_CHECK();
 }
 
+// ---------------------------------------------------------------------------
+// k_chain: the batch-256-class actor pass as one persistent launch (sacmi_internal.h
+// ChainArgs).  256 workgroups of 1024 threads, one per CU; cohort c = blockIdx % 8 owns batch
+// rows [c B/8, (c+1) B/8) in every phase (row-affine tile placement: chain_assign_tiles), so
+// each phase waits only for its own cohort's previous phase.
+constexpr long long kChainSpinTicks = 5000000;   // 50 ms of the 100 MHz clock: a barrier timeout
+
+// Cohort barrier (cdna_hip_programming.md §6 Guideline 16, MI355X_MICROARCH.md hand-off table
+// row 1): every wave's write-through stores acknowledged (vmcnt(0)), a workgroup barrier, ONE
+// agent-scope arrival; the last arriver resets the count and bumps the generation the others
+// poll (relaxed sc1 loads + s_sleep); every later load of the handed-off bytes is an sc1 load
+// (kg_body / tail_unit with LDAUX = sc1).  The generation is read before arriving (its load
+// has returned: vmcnt(0)), so the waiters compare against the value before this round.
+// wait = false: arrive only (the workgroup's next work reads nothing of this phase).  A
+// bounded spin: a timeout sets ERR_CHAIN_TIMEOUT (the host reports a device error) and the
+// workgroup runs on — void outputs, never a hung grid.
+__device__ __forceinline__ void chain_bar(int* cnt, int* gen, int n, int* err, bool wait) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == n - 1) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(gen, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (wait) {
+      const unsigned long long t0 = wall_clock64();
+      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((long long)(wall_clock64() - t0) > kChainSpinTicks) {
+          __hip_atomic_fetch_or(err, (int)ERR_CHAIN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+using ChainKgA = KgSmem<32, 32, 16, 2, 1, false, 0, false, 0>;   // L7, L8, L12 (+ rides)
+using ChainKgB = KgSmem<32, 32, 16, 2, 1, false, 1, false, 0>;   // L9 (row prologue, dL/da)
+union ChainSmem {
+  ChainKgA a;
+  ChainKgB b;
+  TailSmem t;
+};
+
+__global__ __launch_bounds__(1024, 4) void k_chain(const ChainArgs* __restrict__ ca, tl_word* tl) {
+  const TlMark tl_mark(tl, TL_CHAIN);
+  __shared__ ChainSmem sm;
+  const int c = blockIdx.x & (kChainCohorts - 1);
+  const int nmem = gridDim.x / kChainCohorts;
+  int* const sync = ca->sync + c * kChainBars * 32;
+  int* const err = ca->err;
+  auto bar = [&](int b, bool wait) { chain_bar(sync + b * 32, sync + b * 32 + 1, nmem, err, wait); };
+  // each phase reads its arguments through a pointer the compiler cannot see through
+  // (opaque()): no phase's argument loads are hoisted into an earlier phase, where they
+  // would sit in registers across it (SGPR / VGPR spills)
+  // The block is read through the CONSTANT address space: invariant scalar loads, as
+  // k_gemm's kernel argument (a generic pointer's loads behind the barriers' memory clobbers
+  // would be vector loads into VGPRs); the generic pointer handed to kg_body is the cast of
+  // it, which InferAddressSpaces folds back.
+  typedef __attribute__((address_space(4))) const ChainArgs ConstChainArgs;
+  auto opaque = [&]() {
+    ConstChainArgs* p4 = (ConstChainArgs*)ca;
+    asm volatile("" : "+s"(p4));
+    return (const ChainArgs*)p4;
+  };
+  // L7 (updated critics fc1 on [s|1|a~]), L8 (fc2 + fc3 dot partials)
+#pragma unroll 1
+  for (int i = 0; i < 2; ++i) {
+    const GemmBatch& b = opaque()->lv[i];
+    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.a);
+    bar(i, true);
+  }
+  // L9: the actor row prologue + dha1 + the dL/da partials
+  {
+    const GemmBatch& b = opaque()->lv[2];
+    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1>(b, blockIdx.x, sm.b);
+    bar(2, true);
+  }
+  // the sample-backward tail: the cohort's 8-row groups x 64-column dhp2 slabs
+  {
+    const ChainArgs* q = opaque();
+    const int ng = q->tail_groups, units = ng * q->tail_slabs;
+    const int j = blockIdx.x / kChainCohorts;
+    if (j < units) {
+      const int g = j % ng, slab = j / ng;
+      tail_unit<kLdSc1>(q->pa, q->n_pa, q->tail, c * q->rows_per_cohort + g * kTailRows,
+                        slab * kTailCols, slab == 0, sm.t);
+    }
+  }
+  // L12 (dhp1) + the level's rides (the next update's sampler, Polyak): a workgroup whose
+  // items are all rides reads nothing of the chain — it arrives and goes on
+  {
+    const GemmBatch& b = opaque()->lv[3];
+    bar(3, (int)blockIdx.x < b.total_tiles);
+    const int items = b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
+    if ((int)blockIdx.x < items) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.a);
+  }
+}
+
+// 32x32 tiles, XCD-blocked with a row grid of 8: tile t of a desc -> row tile
+// (t & 7) * tm / 8 + q, so workgroup b (b & 7 = cohort) only ever touches its cohort's rows
+bool chain_assign_tiles(GemmBatch& b) {
+  assign_tiles<32, 32>(b);
+  for (int i = 0; i < b.count; ++i) {
+    GemmDesc& d = b.d[i];
+    if (d.tiles_m % kChainCohorts || d.tile_begin % kChainCohorts) return false;
+    d.xcd_gr = kChainCohorts;
+    d.pl_div = d.tiles_n;
+    d.pl_gc_log2 = 0;
+    d.pl_sr = d.tiles_m / kChainCohorts;
+    d.pl_mag = d.pl_div == 1 ? 0u : (unsigned)((((uint64_t)1 << 32) + d.pl_div - 1) / d.pl_div);
+  }
+  return true;
+}
+
+// The grid must be resident at once (its cohorts wait for each other): one workgroup per CU
+// on at least 256 CUs
+bool chain_supported() {
+  static int ok_dev[64] = {};   // 0 unknown, 1 yes, 2 no
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  if (!ok_dev[dev]) {
+    hipDeviceProp_t prop;
+    int per_cu = 0;
+    const bool ok = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount >= kChainGrid &&
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_chain, 1024, 0) == hipSuccess &&
+                    per_cu >= 1;
+    ok_dev[dev] = ok ? 1 : 2;
+  }
+  return ok_dev[dev] == 1;
+}
+
+bool launch_chain(const ChainArgs& h, const ChainArgs* dev, tl_word* tl, hipStream_t s) {
+  if (!chain_supported()) return false;
+  // the configuration k_chain instantiates: fp32 32x32 k_gemm tiles (L9 with the A transform
+  // and the dL/da partials), no fused Adam, no split-K / bf16 activations, rides on L12 only
+  for (int i = 0; i < kChainLevels; ++i) {
+    const GemmBatch& b = h.lv[i];
+    if (b.count < 1 || b.bf16 || b.has_adam || b.heads_ticket || b.err_flags || !b.st_wt)
+      throw Error{SACMI_ESTATE, "k_chain: unsupported level configuration"};
+    if ((b.ride.kind || b.ride.pk_blocks) && i != 3) throw Error{SACMI_ESTATE, "k_chain: rides outside L12"};
+    if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > kRideLdsBytes)
+      throw Error{SACMI_ESTATE, "k_chain: ride-along sampler table exceeds the LDS"};
+    for (int q = 0; q < b.count; ++q) {
+      const GemmDesc& d = b.d[q];
+      if (d.axk != (i == 2 ? 1 : 0) || d.epi >= EPI_ADAM || d.a16 || d.b16 || d.c16 || d.x16 ||
+          d.xcd_gr != kChainCohorts || d.tiles_m % kChainCohorts || (d.pa_out && i != 2))
+        throw Error{SACMI_ESTATE, "k_chain: unsupported GEMM in a chain level"};
+      if (d.M != h.rows_per_cohort * kChainCohorts)
+        throw Error{SACMI_ESTATE, "k_chain: a level's rows differ from the chain's batch"};
+    }
+  }
+  const SampleBwdArgs& a = h.tail;
+  if (2 * a.A > 64 || kTailRows * a.A > 256 || h.n_pa > kTailMaxPa || a.hp2_16 || a.B != h.rows_per_cohort * kChainCohorts ||
+      h.rows_per_cohort % kTailRows || h.tail_groups != h.rows_per_cohort / kTailRows ||
+      h.tail_slabs != (a.H + kTailCols - 1) / kTailCols)
+    throw Error{SACMI_ESTATE, "k_chain: unsupported sample-backward tail"};
+  hipLaunchKernelGGL(k_chain, dim3(kChainGrid), dim3(1024), 0, s, dev, tl);
+  HIP_LAUNCH_CHECK();
+  return true;
+}
+
 bool gemm_level_on_axk16(const GemmBatch& b0) {
   GemmBatch b = b0;
   return SACMI_AXK_LDS16 && axk16_ok(b) >= 0;
+}
+
+// whether launch_gemm takes this forward level on <32, 64, 16, 2, 1> fp32 tiles with
+// write-through stores: the configuration that folds the policy heads (GemmBatch::heads)
+bool gemm_level_heads_fold_ok(const GemmBatch& b0, int A) {
+  if (b0.bf16 || b0.count < 1 || 2 * A > 48 || A < 1) return false;
+  GemmBatch b = b0;
+  if (staged_ok(b) || fwd_big_ok(b)) return false;
+  bool dw = true;
+  int axk = 0, n_adam = 0;
+  int64_t outs = 0;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    dw = dw && !d.a_kc && !d.b_kc;
+    axk = d.axk > axk ? d.axk : axk;
+    n_adam += d.epi >= EPI_ADAM;
+    outs += (int64_t)d.M * d.N;
+    if (d.a16 || d.b16 || d.c16 || d.x16) return false;
+  }
+  const int t64 = assign_tiles<32, 64>(b);
+  // launch_gemm's <32, 64, 16, 2, 1> branch, with write-through stores (st_wt: outs <= 1 M)
+  return !dw && !n_adam && !axk && t64 >= 192 && t64 <= 512 && outs <= (1 << 20);
 }
 
 // launch_gemm's own kernel choice for an axk-1 level, asked ahead of its launch: true when

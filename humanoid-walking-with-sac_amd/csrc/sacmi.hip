@@ -218,6 +218,11 @@ struct sacmi_ctx {
   int nparts = 0;
   sacmi::DevBuf<float> lpart_c, lpart_a, ring, lp_part;
   int ring_slots = 0;
+  // policy heads folded into the last policy hidden layer's level (GemmBatch::heads): the
+  // arrival counts per 32-row block (zero between launches), and the batch size whose
+  // update folds them (the actor phase sizes its log-prob partials from it)
+  sacmi::DevBuf<int> heads_ticket;
+  int heads_fold_B = -1;
   // act scratch
   int act_rows = 0;
   sacmi::DevBuf<float> ax, ah1, ah2, aeps, acache, alogp, aout;
@@ -265,6 +270,17 @@ struct sacmi_ctx {
   sacmi::DevBuf<int32_t> per_owner, per_bad;
   std::map<sacmi::GraphKey, hipGraphExec_t> graphs;
   bool use_graphs = true;
+  // the persistent actor-pass chain (k_chain, sacmi_internal.h ChainArgs): its argument blocks
+  // live in a device pool (larger than a kernel argument); a block registered while a graph is
+  // being captured (own_capture) is uploaded once the capture has ended (chain_flush), before
+  // that graph's first launch.  Blocks are immutable and deduplicated by content.
+  static constexpr int kChainSlots = 48;
+  bool own_capture = false;
+  bool chain_on = true;                      // SACMI_NO_CHAIN at creation: off
+  sacmi::DevBuf<unsigned char> chain_pool;   // kChainSlots x sizeof(ChainArgs)
+  std::vector<std::vector<unsigned char>> chain_host;
+  size_t chain_uploaded = 0;                 // slots [0, chain_uploaded) are on the device
+  sacmi::DevBuf<int> chain_sync;             // cohort barrier words (kChainSyncInts)
   bool G_external = false;
   // native data parallel (sacmi_allreduce_init / sacmi_step_dp)
   ncclComm_t comm = nullptr;
@@ -319,6 +335,51 @@ static void destroy_graphs(sacmi_ctx* c) {
   c->graphs.clear();
   for (auto& kv : c->dp_graphs) (void)hipGraphExecDestroy(kv.second);
   c->dp_graphs.clear();
+  // no graph refers to a chain block any more (every caller has drained the stream)
+  c->chain_host.clear();
+  c->chain_uploaded = 0;
+}
+
+// The device copy of a chain argument block: an existing slot with the same bytes, or a new
+// one (uploaded by chain_flush after the capture); null when the pool is full
+static const ChainArgs* chain_slot(sacmi_ctx* c, const ChainArgs& a) {
+  const unsigned char* bytes = reinterpret_cast<const unsigned char*>(&a);
+  for (size_t i = 0; i < c->chain_host.size(); ++i)
+    if (std::memcmp(c->chain_host[i].data(), bytes, sizeof(ChainArgs)) == 0)
+      return reinterpret_cast<const ChainArgs*>(c->chain_pool.p + i * sizeof(ChainArgs));
+  if (c->chain_host.size() >= (size_t)sacmi_ctx::kChainSlots) return nullptr;
+  c->chain_host.emplace_back(bytes, bytes + sizeof(ChainArgs));
+  return reinterpret_cast<const ChainArgs*>(c->chain_pool.p + (c->chain_host.size() - 1) * sizeof(ChainArgs));
+}
+static void chain_flush(sacmi_ctx* c) {
+  for (size_t i = c->chain_uploaded; i < c->chain_host.size(); ++i)
+    CHECK_HIP(hipMemcpy(c->chain_pool.p + i * sizeof(ChainArgs), c->chain_host[i].data(), sizeof(ChainArgs),
+                        hipMemcpyHostToDevice));
+  c->chain_uploaded = c->chain_host.size();
+}
+
+// Capture whatever `body` enqueues on the context stream into an instantiated graph (thread-
+// local capture mode); chain blocks registered meanwhile are uploaded before it returns
+template <class F>
+static hipGraphExec_t capture_graph(sacmi_ctx* c, F&& body) {
+  hipGraph_t g;
+  CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  c->own_capture = true;
+  try {
+    body();
+  } catch (...) {
+    c->own_capture = false;
+    (void)hipStreamEndCapture(c->stream, &g);
+    throw;
+  }
+  c->own_capture = false;
+  CHECK_HIP(hipStreamEndCapture(c->stream, &g));
+  hipGraphExec_t ex;
+  const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  CHECK_HIP(e);
+  chain_flush(c);
+  return ex;
 }
 
 // ---------------------------------------------------------------------------
@@ -449,6 +510,7 @@ static void alloc_all(sacmi_ctx* c) {
   const int nrb = (Bm + 31) / 32;    // row blocks of the L5 / L9 tiling (loss partials)
   c->lpart_c.alloc((size_t)nrb * 2); c->lpart_a.alloc(nrb);
   c->lp_part.alloc((size_t)2 * ((2 * Bm + 15) / 16) + 2);   // heads: per-workgroup logp sums
+  c->heads_ticket.alloc((size_t)(2 * Bm + kHeadsFoldTM - 1) / kHeadsFoldTM);
   hipStream_t s = c->stream;
   // constant-1 (bias) columns
   set_column_checked(c->xq.p, Bm, c->Kx, S, 1.f, s);
@@ -662,6 +724,13 @@ static void validate_batch(const GemmBatch& b) {
   } else {
     REQUIRE(b.ws_floats == 0, SACMI_ESTATE, "split-K workspace capacity without a workspace");
   }
+}
+
+// the policy heads folded into the last policy hidden layer's level where launch_gemm can
+// (read per enqueue: tests switch it between contexts)
+static bool heads_fold_wanted() {
+  const char* e = std::getenv("SACMI_NO_HEADS_FOLD");
+  return !(e && std::atoi(e) != 0);
 }
 
 struct Level {
@@ -897,6 +966,58 @@ static AdamArgs dp_adam_args(sacmi_ctx* c, bool critic, int B, float grad_scale,
   return ad;
 }
 
+// The actor pass L7 -> L8 -> L9 -> sample-backward tail -> L12 of a fused update as ONE
+// persistent launch (k_chain, sacmi_internal.h ChainArgs): batch 256 (8 cohorts x 32 rows, one
+// tile per workgroup and phase), fp32, two hidden layers with the dL/da fold, inside a graph
+// this context captures (the argument block is uploaded after the capture).  Returns false
+// (nothing enqueued) where it does not apply: the caller launches the levels one by one.
+// SACMI_NO_CHAIN at creation switches it off (the tests' A/B).
+static bool chain_batch_ok(const sacmi_ctx* c, int B) {
+  return c->chain_on && !c->bf16 && c->nh == 2 && B == kChainCohorts * 32 && c->H % 32 == 0 && c->H <= 512 &&
+         !std::getenv("SACMI_NO_DLDA_FOLD") && chain_supported();
+}
+static bool enqueue_chain(sacmi_ctx* c, int B, const Level& l7, const Level& l8, const Level& l9,
+                          const SampleBwdArgs& sb, const Level& l12) {
+  // (site-isolation profiling enumerates the sites outside a capture: the launch chain there)
+  if (!c->own_capture || c->prof_site >= 0 || c->prof_collect || !chain_batch_ok(c, B)) return false;
+  ChainArgs ca;
+  std::memset(&ca, 0, sizeof(ca));
+  const Level* lv[kChainLevels] = {&l7, &l8, &l9, &l12};
+  double flops = 2.0 * B * (2.0 * c->A) * c->H, bytes = 0;   // (the tail's dhp2 product)
+  for (int i = 0; i < kChainLevels; ++i) {
+    GemmBatch b = lv[i]->b;
+    b.bf16 = 0;
+    for (int q = 0; q < b.count; ++q) b.d[q].Bh = nullptr;
+    b.ws = nullptr; b.ws_floats = 0;
+    b.tl = nullptr;
+    b.st_wt = 1;           // write-through epilogue stores: every hand-off's bytes leave L2
+    b.adam_wg = -2;
+    validate_batch(b);
+    if (!chain_assign_tiles(b) || b.total_tiles > kChainGrid) return false;
+    const int items = b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
+    if (items > kChainGrid) return false;
+    flops += level_flops(b);
+    bytes += level_bytes(b);
+    ca.lv[i] = b;
+  }
+  ca.tail = sb;
+  ca.tail.tl = nullptr;
+  ca.pa = c->pa.p; ca.n_pa = 2 * c->nparts;
+  ca.rows_per_cohort = B / kChainCohorts;
+  ca.tail_groups = ca.rows_per_cohort / 8;
+  ca.tail_slabs = (c->H + 63) / 64;
+  if (ca.tail_groups * ca.tail_slabs > kChainGrid / kChainCohorts) return false;
+  ca.sync = c->chain_sync.p;
+  ca.err = &c->sc.p->err;
+  check_span(ca.sync, kChainSyncInts - 1, "chain barrier words");
+  const ChainArgs* dev = chain_slot(c, ca);
+  if (!dev) return false;   // (pool full: the launch chain)
+  if (mark(c, "gemm_chain_L7_L12", flops, bytes)) {
+    if (!launch_chain(ca, dev, c->tl_cur, c->stream)) throw Error{SACMI_ESTATE, "k_chain refused a supported configuration"};
+  }
+  return true;
+}
+
 // parity: which batch buffer set this update uses; have_batch: its indices and rows
 // were produced by the previous update's ride-along work; ride_next: produce the next
 // update's (into the other set) inside this update's L11 / L13 launches.
@@ -977,19 +1098,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     for (int i = 0; i < 2; ++i)
       l1.add(fw(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
     run(l1, "gemm_L1_fc1");
-    // L2 (.. L2b): the remaining hidden layers (K = H, bias in the epilogue); the last one
-    // also accumulates the critic head (fc3 / fc4) dot partials of q1 / q2 (slots 0 / 1)
-    for (int l = 1; l < nh; ++l) {
-      Level lv;
-      lv.add(fw(gd_fwd_h(c->hp[l - 1].p, Hd, W(c->p_fc[l]), Hd, c->hp[l].p, Hd, 2 * B, H, H)));
-      for (int i = 0; i < 2; ++i) {
-        GemmDesc g = fw(gd_fwd_h(E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd, W(q[i][l]), Hd,
-                                 E(c->hq[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
-        lv.add(l == L ? with_dot(g, W(q[i][nh]), i) : g);
-      }
-      run(lv, l == 1 ? "gemm_L2_fc2" : "gemm_L2b_fc3");
-    }
-    // heads + sample for both stacks
+    // heads + sample for both stacks (networks_model1.py:78-99)
     HeadSampleArgs hs{};
     hs.h = c->hp[L].p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
     hs.ldh = Hd; hs.ldw = Hd; hs.eps = c->eps.p; hs.gen_eps = dev_eps; hs.seed = c->cfg.seed;
@@ -1001,7 +1110,31 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     hs.logp_part = c->lp_part.p; hs.split_row = B;    // sums of log pi(a~|s) for dL/dlog_alpha
     // Normal validation of policy.sample(next_state) / policy.sample(state) (sac_imp.py:89,116)
     hs.nan_flag = &c->sc.p->err; hs.nan_bit_lo = ERR_NAN_TGT; hs.nan_bit_hi = ERR_NAN_ACT;
-    if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) {
+    // L2 (.. L2b): the remaining hidden layers (K = H, bias in the epilogue); the last one
+    // also accumulates the critic head (fc3 / fc4) dot partials of q1 / q2 (slots 0 / 1) and,
+    // where its tiles can (gemm_level_heads_fold_ok), runs the heads + sample folded in: the
+    // last column tile of each 32-row block of the policy rows takes them for that block —
+    // one launch and one boundary fewer (SACMI_NO_HEADS_FOLD=1: the separate kernel)
+    bool folded = false;
+    for (int l = 1; l < nh; ++l) {
+      Level lv;
+      lv.add(fw(gd_fwd_h(c->hp[l - 1].p, Hd, W(c->p_fc[l]), Hd, c->hp[l].p, Hd, 2 * B, H, H)));
+      for (int i = 0; i < 2; ++i) {
+        GemmDesc g = fw(gd_fwd_h(E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd, W(q[i][l]), Hd,
+                                 E(c->hq[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
+        lv.add(l == L ? with_dot(g, W(q[i][nh]), i) : g);
+      }
+      lv.b.bf16 = c->bf16 ? 1 : 0;   // (the gate reads the level's MFMA operand type, as run() sets it)
+      if (l == L && heads_fold_wanted() && gemm_level_heads_fold_ok(lv.b, A)) {
+        lv.b.heads = hs;
+        lv.b.heads_desc = 0;   // (the policy desc, added first)
+        lv.b.heads_ticket = c->heads_ticket.p;
+        folded = true;
+      }
+      run(lv, l == 1 ? "gemm_L2_fc2" : "gemm_L2b_fc3");
+    }
+    c->heads_fold_B = folded ? B : -1;
+    if (!folded && mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) {
       hs.tl = c->tl_cur;
       launch_heads_sample(hs, s);
     }
@@ -1111,13 +1244,13 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     }
    }
     // L7/L8 (.. L8b): updated critics on [s|1|a~] (head dot partials: slots 4 / 5)
+    // (the levels of the actor pass are built first, then launched one by one or — fused
+    // batch-256 updates — as the persistent chain k_chain: L7 -> L8 -> L9 -> tail -> L12)
     const float* xa = E(bb.x2, (size_t)B * Kx);
-    {
-      Level l7;
-      for (int i = 0; i < 2; ++i)
-        l7.add(fw(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, E(c->hqa[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
-      run(l7, "gemm_L7_act_fc1");
-    }
+    Level l7;
+    for (int i = 0; i < 2; ++i)
+      l7.add(fw(gd(xa, Kx, 1, W(q[i][0]), Kx, 1, E(c->hqa[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
+    std::vector<Level> l8s;   // L8 (.. L8b)
     for (int l = 1; l < nh; ++l) {
       Level lv;
       for (int i = 0; i < 2; ++i) {
@@ -1125,7 +1258,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
                                  E(c->hqa[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
         lv.add(l == L ? with_dot(g, W(q[i][nh]), 4 + i) : g);
       }
-      run(lv, l == 1 ? "gemm_L8_act_fc2" : "gemm_L8b_act_fc3");
+      l8s.push_back(lv);
     }
     // L9: dha[L-1] = (dha[L] W[L]) * relu'(ha[L-1]), with the actor rows folded in: the
     // prologue finishes qa1, qa2 (dot partials), min (ties 1/2 : 1/2), policy-loss
@@ -1142,7 +1275,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       rf.kind = 2; rf.part = dotp(4); rf.nparts = c->nparts; rf.B = B;
       rf.logp = c->logp.p + B; rf.sc = c->sc.p; rf.loss_part = c->lpart_a.p;
       if (c->cfg.auto_entropy) {
-        rf.alpha_grad = G + c->la_idx; rf.logp_part = c->lp_part.p; rf.n_lp = (2 * B + heads_rows_per_wg(2 * B) - 1) / heads_rows_per_wg(2 * B);
+        rf.alpha_grad = G + c->la_idx; rf.logp_part = c->lp_part.p; {
+          const int tm = c->heads_fold_B == B ? kHeadsFoldTM : heads_rows_per_wg(2 * B);
+          rf.n_lp = (2 * B + tm - 1) / tm;
+        }
         rf.target_entropy = (float)(-A);
       }
     }
@@ -1166,13 +1302,13 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
         check_span(g.pa_out, ((int64_t)(g.pa_base + c->nparts) * B) * A - 1, "pa_out");
       }
     }
-    run(l9, "gemm_L9_act_dh1");
+    std::vector<Level> l9bs;  // L9b (3 hidden layers)
     for (int l = L - 1; l >= 1; --l) {
       Level lv;
       for (int i = 0; i < 2; ++i)
         lv.add(dh(gd(c->dha[l].p + i * H, 2 * H, 1, W(q[i][l]), Hd, 0, c->dha[l - 1].p + i * H, 2 * H,
                      B, H, H, EPI_MASK, E(c->hqa[l - 1].p, (size_t)i * Hd), 2 * Hd)));
-      run(lv, "gemm_L9b_act_dh");
+      l9bs.push_back(lv);
     }
     // L10: dL/da over both critics (K = 2H) + sample backward -> dhead
     GemmDesc da = gd(c->dha[0].p, 2 * H, 1, W(q[0][0]) + S + 1, Kx, 0, nullptr, 0, B, A, 2 * H);
@@ -1187,23 +1323,15 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     sb.hp2_16 = a16;
     check_span(sb.dhp2, (int64_t)B * H - 1, "dhp2");
     check_span(sb.Wh, (int64_t)(2 * A - 1) * Hd + H - 1, "Whead");
-    if (fold_dlda) {
-      if (mark(c, "sample_bwd_tail_dhp2", 2.0 * B * (2.0 * A) * H)) {
-        sb.tl = c->tl_cur;
-        launch_sample_bwd_tail(c->pa.p, 2 * c->nparts, sb, s);
-      }
-    } else if (mark(c, "gemm_L10_dlda_sample_bwd_dhp2", 2.0 * B * A * (2.0 * H) + 2.0 * B * (2.0 * A) * H)) {
-      sb.tl = c->tl_cur;
-      launch_gemm_sample_bwd(da, sb, s);
-    }
     // L11 (3 hidden layers) .. L12: dhp[l-1] = (dhp[l] Wpi[l]) * relu'(hp[l-1]);
     // L13: every policy dW (+ Adam, alpha step, policy loss, loss ring when fused)
     auto pdst = [&](const Linear& l) { return fuse ? P + l.off : dW(l); };
     const int pepi = fuse ? EPI_ADAM : EPI_STORE;
+    std::vector<Level> l11s;
     for (int l = L; l >= 2; --l) {
       Level lv;
       lv.add(dh(gd(c->dhp[l].p, H, 1, W(c->p_fc[l]), Hd, 0, c->dhp[l - 1].p, H, B, H, H, EPI_MASK, hpa(l - 1), Hd)));
-      run(lv, "gemm_L11_pi_dhp");
+      l11s.push_back(lv);
     }
     Level l12, l13;
     l12.add(dh(gd(c->dhp[1].p, H, 1, W(c->p_fc[1]), Hd, 0, c->dhp[0].p, H, B, H, H, EPI_MASK, hpa(0), Hd)));
@@ -1249,7 +1377,24 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l13.b.ride.kind = 2; l13.b.ride.nblocks = 16;
       l13.b.ride.ga = gather_args(c, B, nb2, false);
     }
-    run(l12, "gemm_L12_pi_dhp1");
+    // the persistent chain (k_chain) where it applies, else the launches one by one
+    if (!(fuse && nh == 2 && fold_dlda && enqueue_chain(c, B, l7, l8s[0], l9, sb, l12))) {
+      run(l7, "gemm_L7_act_fc1");
+      for (size_t i = 0; i < l8s.size(); ++i) run(l8s[i], i == 0 ? "gemm_L8_act_fc2" : "gemm_L8b_act_fc3");
+      run(l9, "gemm_L9_act_dh1");
+      for (Level& lv : l9bs) run(lv, "gemm_L9b_act_dh");
+      if (fold_dlda) {
+        if (mark(c, "sample_bwd_tail_dhp2", 2.0 * B * (2.0 * A) * H)) {
+          sb.tl = c->tl_cur;
+          launch_sample_bwd_tail(c->pa.p, 2 * c->nparts, sb, s);
+        }
+      } else if (mark(c, "gemm_L10_dlda_sample_bwd_dhp2", 2.0 * B * A * (2.0 * H) + 2.0 * B * (2.0 * A) * H)) {
+        sb.tl = c->tl_cur;
+        launch_gemm_sample_bwd(da, sb, s);
+      }
+      for (Level& lv : l11s) run(lv, "gemm_L11_pi_dhp");
+      run(l12, "gemm_L12_pi_dhp1");
+    }
     run(l13, fuse ? "gemm_L13_pi_dW_adam" : "gemm_L13_pi_dW1");
   }
   if ((phase_mask & 4) && phase_mask != 7) {
@@ -1374,21 +1519,7 @@ static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_
                use_ring ? c->ring_slots : 0,
                per_graph_len(c), reps};
   auto it = c->graphs.find(key);
-  if (it == c->graphs.end()) {
-    hipGraph_t g;
-    CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    try {
-      enqueue_all();
-    } catch (...) {
-      (void)hipStreamEndCapture(c->stream, &g);
-      throw;
-    }
-    CHECK_HIP(hipStreamEndCapture(c->stream, &g));
-    hipGraphExec_t ex;
-    CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-    CHECK_HIP(hipGraphDestroy(g));
-    it = c->graphs.emplace(key, ex).first;
-  }
+  if (it == c->graphs.end()) it = c->graphs.emplace(key, capture_graph(c, enqueue_all)).first;
   CHECK_HIP(hipGraphLaunch(it->second, c->stream));
 }
 
@@ -1741,6 +1872,11 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
     alloc_all(c.get());
     c->ring_slots = 4096;
     c->ring.alloc((size_t)c->ring_slots * 3);
+    c->chain_on = std::getenv("SACMI_NO_CHAIN") == nullptr;
+    if (c->chain_on) {
+      c->chain_pool.alloc((size_t)sacmi_ctx::kChainSlots * sizeof(ChainArgs));
+      c->chain_sync.alloc(kChainSyncInts);
+    }
     alloc_pinned(c.get());
     DevScalars h{};
     h.alpha = (float)cfg->alpha;
@@ -1785,8 +1921,10 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (int l = 0; l < 3; ++l)
       for (auto* b : {&c->hp[l], &c->hq[l], &c->hqt[l], &c->hqa[l], &c->dhc[l], &c->dha[l], &c->dhp[l]})
         b->release();
+    c->heads_ticket.release();
     c->sc.release(); c->mt.release(); c->mt_backup.release(); c->mt_pf.release(); c->idx32.release(); c->idx64.release();
     c->Ph.release(); c->Th.release();
+    c->chain_pool.release(); c->chain_sync.release();
     c->idx32b.release(); c->idx64b.release();
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
     c->per_u.release(); c->per_uin.release(); c->per_owner.release(); c->per_bad.release();
@@ -2515,21 +2653,8 @@ int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
     }
     const auto key = std::make_tuple((int)batch, (int)n_updates, per_graph_len(c));
     auto it = c->dp_graphs.find(key);
-    if (it == c->dp_graphs.end()) {
-      hipGraph_t g;
-      CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-      try {
-        enqueue_dp(c, batch, n_updates);
-      } catch (...) {
-        (void)hipStreamEndCapture(c->stream, &g);
-        throw;
-      }
-      CHECK_HIP(hipStreamEndCapture(c->stream, &g));
-      hipGraphExec_t ex;
-      CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-      CHECK_HIP(hipGraphDestroy(g));
-      it = c->dp_graphs.emplace(key, ex).first;
-    }
+    if (it == c->dp_graphs.end())
+      it = c->dp_graphs.emplace(key, capture_graph(c, [&] { enqueue_dp(c, batch, n_updates); })).first;
     CHECK_HIP(hipGraphLaunch(it->second, c->stream));
   });
 }
@@ -2582,6 +2707,13 @@ int sacmi_dp_sync_state(sacmi_ctx* c) {
 int sacmi_step_act16(sacmi_ctx* c, int32_t batch, int32_t* out) {
   return guard([&] {
     pf_touch(c); *out = act16_on(c, batch) ? 1 : 0; });
+}
+
+int sacmi_step_chained(sacmi_ctx* c, int32_t batch, int32_t* out) {
+  return guard([&] {
+    REQUIRE(c && out, SACMI_EVALUE, "null argument");
+    *out = chain_batch_ok(c, batch) && c->use_graphs ? 1 : 0;
+  });
 }
 
 int sacmi_step_ride_possible(sacmi_ctx* c, int32_t batch, int32_t* out) {
@@ -2697,19 +2829,13 @@ int sacmi_profile_sites(sacmi_ctx* c, int32_t batch, int32_t reps, char* names_o
     CHECK_HIP(hipEventCreate(&e1));
     for (int i = 0; i < n; ++i) {
       c->prof_site = i;
-      hipGraph_t g;
-      CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      hipGraphExec_t ex;
       try {
-        for (int r = 0; r < reps; ++r) enqueue_update(c, batch, 1, 1, 7, 1.f, false);
+        ex = capture_graph(c, [&] { for (int r = 0; r < reps; ++r) enqueue_update(c, batch, 1, 1, 7, 1.f, false); });
       } catch (...) {
-        (void)hipStreamEndCapture(c->stream, &g);
         c->prof_site = -1;
         throw;
       }
-      CHECK_HIP(hipStreamEndCapture(c->stream, &g));
-      hipGraphExec_t ex;
-      CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-      CHECK_HIP(hipGraphDestroy(g));
       CHECK_HIP(hipGraphLaunch(ex, c->stream));      // warm
       CHECK_HIP(hipEventRecord(e0, c->stream));
       CHECK_HIP(hipGraphLaunch(ex, c->stream));
@@ -2759,18 +2885,8 @@ static void timeline_of(sacmi_ctx* c, int n_updates, F&& enqueue, int32_t max_ke
   try {
     c->tl_dev = buf.p; c->tl_cap = cap; c->tl_sites = 0;
     c->tl_names.clear(); c->tl_flops.clear(); c->tl_bytes.clear();
-    hipGraph_t g;
-    CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    try {
-      enqueue();
-    } catch (...) {
-      (void)hipStreamEndCapture(c->stream, &g);
-      throw;
-    }
-    CHECK_HIP(hipStreamEndCapture(c->stream, &g));
+    ex = capture_graph(c, enqueue);
     c->tl_dev = nullptr; c->tl_cur = nullptr;
-    CHECK_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-    CHECK_HIP(hipGraphDestroy(g));
     CHECK_HIP(hipEventCreate(&e0));
     CHECK_HIP(hipEventCreate(&e1));
     CHECK_HIP(hipGraphLaunch(ex, c->stream));     // warm (its stamps are discarded)

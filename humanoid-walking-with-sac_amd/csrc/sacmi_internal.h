@@ -116,7 +116,7 @@ typedef unsigned long long tl_word;
 enum TlKind : int {
   TL_GEMM = 1, TL_FWD, TL_FWD16, TL_AXK16, TL_DW_PART, TL_DW_PART16, TL_DW_FIN, TL_HEADS,
   TL_SAMPLE_BWD, TL_MT_SAMPLE, TL_GATHER, TL_PER_F1, TL_PER_F2, TL_PER_F2B, TL_PER_F3,
-  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_KINDS
+  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_CHAIN, TL_KINDS
 };
 constexpr int kTlEnd = 4;            // first of the ~end slots
 constexpr int kTlEndSlots = 4096;
@@ -201,10 +201,13 @@ struct Linear {
 //                the replicas stay identical (the error flags travel with the critic gradient
 //                collective: kDpFlagN)
 // The host reports and clears them (sacmi_step / sacmi_fetch_losses / sacmi_per_sample).
+//   ERR_CHAIN_TIMEOUT  a cohort barrier of the persistent chain kernel (k_chain) timed out
+//                (a workgroup never arrived): the chain's outputs are void, every later step of
+//                the stream is skipped, and the host reports a device error (SACMI_EDEVICE)
 enum ErrBits : int { ERR_NAN_TGT = 1, ERR_NAN_ACT = 2, ERR_NAN_PER = 4, ERR_ABORT = 8,
-                     ERR_REMOTE_SKIP = 16, ERR_REMOTE_ACT = 32 };
+                     ERR_REMOTE_SKIP = 16, ERR_REMOTE_ACT = 32, ERR_CHAIN_TIMEOUT = 64 };
 // an update that sees any of these takes none of its steps
-constexpr int kErrSkipAll = ERR_NAN_TGT | ERR_NAN_PER | ERR_ABORT | ERR_REMOTE_SKIP;
+constexpr int kErrSkipAll = ERR_NAN_TGT | ERR_NAN_PER | ERR_ABORT | ERR_REMOTE_SKIP | ERR_CHAIN_TIMEOUT;
 // ... and these: the critic step stands, the Polyak / actor / alpha steps do not
 constexpr int kErrActLike = ERR_NAN_ACT | ERR_REMOTE_ACT;
 // Data-parallel error flags: kDpFlagN floats right past the critic range of the gradient arena
@@ -414,29 +417,6 @@ struct RowsFuse {
 };
 
 constexpr int kMaxGemms = 8;
-struct GemmBatch {
-  GemmDesc d[kMaxGemms];
-  int count;
-  int total_tiles;
-  AdamFuse adam;       // used when any desc has epi >= EPI_ADAM
-  int has_adam;
-  int adam_wg;         // k_gemm: the workgroup that runs the level's scalar Adam work (losses,
-                       //   alpha step, loss ring, done word) — an extra workgroup past the
-                       //   tiles and rides (launch_gemm), -1: block 0 after its tile, or
-                       //   -2: wave 0 of block 0 before its tile
-  RideAlong ride;      // extra workgroups after the tiles
-  RowsFuse rows;       // prologue for axk-1 descs
-  int bf16;            // 1: bf16 MFMA operands (fp32 loads rounded to bf16 in registers)
-  float* ws;           // bf16 deep-K weight-gradient levels: split-K partial workspace
-  int64_t ws_floats;   //   (capacity; launch_gemm falls back when a level needs more)
-  tl_word* tl;         // launch timeline slots of this level (kTlPerSite), or null
-  int st_wt;           // k_gemm epilogue stores write-through (set by launch_gemm)
-  // data-parallel phase 0's last level: block 0 stores the error flags (kDpFlagN) of
-  // *err_word here, before the critic gradient collective (null: none)
-  float* err_flags;
-  const int* err_word;
-};
-
 // Sample-forward epilogue (policy heads): rows [row0, row0+M) of the stacked
 // [target rows ; actor rows] matrix.
 struct HeadSampleArgs {
@@ -470,6 +450,36 @@ struct HeadSampleArgs {
   tl_word* tl;
 };
 
+struct GemmBatch {
+  GemmDesc d[kMaxGemms];
+  int count;
+  int total_tiles;
+  AdamFuse adam;       // used when any desc has epi >= EPI_ADAM
+  int has_adam;
+  int adam_wg;         // k_gemm: the workgroup that runs the level's scalar Adam work (losses,
+                       //   alpha step, loss ring, done word) — an extra workgroup past the
+                       //   tiles and rides (launch_gemm), -1: block 0 after its tile, or
+                       //   -2: wave 0 of block 0 before its tile
+  RideAlong ride;      // extra workgroups after the tiles
+  RowsFuse rows;       // prologue for axk-1 descs
+  int bf16;            // 1: bf16 MFMA operands (fp32 loads rounded to bf16 in registers)
+  float* ws;           // bf16 deep-K weight-gradient levels: split-K partial workspace
+  int64_t ws_floats;   //   (capacity; launch_gemm falls back when a level needs more)
+  tl_word* tl;         // launch timeline slots of this level (kTlPerSite), or null
+  int st_wt;           // k_gemm epilogue stores write-through (set by launch_gemm)
+  // the policy heads + sample folded into the level that produces the last policy hidden
+  // layer (k_gemm's fp32 32x64 forward tiles, gemm_level_heads_fold_ok): the last column
+  // tile of each 32-row block to finish (heads_ticket[row block]: an arrival count, reset
+  // by that tile) runs them for the block's rows
+  HeadSampleArgs heads;
+  int heads_desc;      // the policy desc of the level
+  int* heads_ticket;   // or null: no fold
+  // data-parallel phase 0's last level: block 0 stores the error flags (kDpFlagN) of
+  // *err_word here, before the critic gradient collective (null: none)
+  float* err_flags;
+  const int* err_word;
+};
+
 // Sample-backward epilogue of the dL/da GEMM.
 struct SampleBwdArgs {
   const float* cache;    // actor rows' cache [B, 3A]
@@ -488,9 +498,47 @@ struct SampleBwdArgs {
   tl_word* tl;
 };
 
+// The actor pass of a batch-256-class fused update as ONE persistent launch (k_chain):
+//   L7 (updated critics fc1) -> L8 (fc2 + fc3 dot partials) -> L9 (row prologue + dha1 + dL/da
+//   partials) -> sample-backward tail (dhead, dhp2) -> L12 (dhp1, + the level's rides)
+// (sac_imp.py:116-125 forward / backward through Q(s, a~) and the policy heads).  Every phase
+// is row-local over the batch, so the grid is cut into 8 cohorts of 32 workgroups (blockIdx % 8:
+// one XCD each under the observed round-robin dispatch — for speed only) and cohort c owns batch
+// rows [c B/8, (c+1) B/8) in every phase (k_gemm's XCD-blocked tile placement with a row grid of
+// 8); a cohort barrier (32 arrivals, agent-scope counter) replaces each kernel boundary.
+// Hand-offs follow cdna_hip_programming.md §6 Guideline 16: write-through (sc1) stores, every
+// storing wave's vmcnt(0), one agent-scope arrival per workgroup, sc1 loads of every handed-off
+// byte.  The levels run k_gemm's own workgroup body (kg_body) on the same 32x32 tiles, so the
+// results are those of the launch chain bit for bit.  The argument block lives in device
+// memory (sacmi.hip chain pool: larger than a kernel argument).
+constexpr int kChainLevels = 4;     // L7, L8, L9, L12
+constexpr int kChainBars = 4;       // barriers after L7, L8, L9, the tail
+constexpr int kChainCohorts = 8;
+constexpr int kChainGrid = 256;     // workgroups: one per CU
+struct ChainArgs {
+  GemmBatch lv[kChainLevels];
+  SampleBwdArgs tail;         // the sample backward + dhp2 tail between L9 and L12
+  const float* pa;            // the tail: dL/da partials of L9 (n_pa column blocks)
+  int n_pa;
+  int rows_per_cohort;        // B / 8
+  int tail_groups;            // 8-row groups per cohort (rows_per_cohort / 8)
+  int tail_slabs;             // 64-column slabs of dhp2 (ceil(H / 64))
+  int* sync;                  // [cohort][barrier] x {count, generation}, 128-byte strided
+  int* err;                   // DevScalars::err (ERR_CHAIN_TIMEOUT)
+};
+constexpr int kChainSyncInts = kChainCohorts * kChainBars * 32;
+
 // ---------------------------------------------------------------------------
 // launchers (kernels.hip)
 void launch_gemm(const GemmBatch& batch, hipStream_t s);
+// k_chain over the argument block `dev` (device memory, filled from `host`); host: the same
+// block, validated here.  Returns false (nothing launched) where the device cannot hold the
+// grid at once (fewer than 256 CUs, or the kernel's occupancy below one workgroup per CU)
+bool launch_chain(const ChainArgs& host, const ChainArgs* dev, tl_word* tl, hipStream_t s);
+bool chain_supported();
+// assign k_chain's tile order to a level: 32x32 tiles, XCD-blocked with a row grid of 8
+// (cohort c = tile & 7 owns row tiles [c tm / 8, (c+1) tm / 8)); false where it does not apply
+bool chain_assign_tiles(GemmBatch& b);
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
 
 // select_action for one state (sacmi_act, n = 1): the policy forward as GEMVs.
@@ -534,6 +582,10 @@ void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, h
 bool gemm_level_on_axk16(const GemmBatch& b);
 // whether launch_gemm runs this axk-1 level on the tiles that compute dL/da partials
 bool gemm_level_pa_capable(const GemmBatch& b);
+// whether launch_gemm runs this forward level on the tiles that can fold the policy heads
+// (GemmBatch::heads): fp32 32x64 k_gemm tiles, write-through stores, 2A <= 48
+bool gemm_level_heads_fold_ok(const GemmBatch& b, int A);
+constexpr int kHeadsFoldTM = 32;   // rows per folded heads block (one 32-row tile block)
 
 
 constexpr int kMaxAdamSegs = 8;

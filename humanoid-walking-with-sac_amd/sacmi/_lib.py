@@ -86,6 +86,7 @@ _PROTOS = {
                             ctypes.c_int32, ctypes.c_int32],
     "sacmi_step_ride_possible": [c_vp, ctypes.c_int32, c_i32p],
     "sacmi_step_act16": [c_vp, ctypes.c_int32, c_i32p],
+    "sacmi_step_chained": [c_vp, ctypes.c_int32, c_i32p],
     "sacmi_fetch_losses": [c_vp, c_f32p, ctypes.c_int32, c_i32p],
     "sacmi_step_phase": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float],
     "sacmi_grad_buffer": [c_vp, ctypes.c_int, ctypes.POINTER(c_vp), c_i64p],

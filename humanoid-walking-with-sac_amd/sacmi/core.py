@@ -298,6 +298,13 @@ class Context:
         L.call("sacmi_step_ride_possible", self._h, int(batch), ctypes.byref(out))
         return bool(out.value)
 
+    def chained(self, batch: int) -> bool:
+        """Whether fused updates of this batch run the actor pass as one persistent launch
+        (k_chain, sacmi.h sacmi_step_chained)."""
+        out = ctypes.c_int32()
+        L.call("sacmi_step_chained", self._h, int(batch), ctypes.byref(out))
+        return bool(out.value)
+
     def act16(self, batch: int) -> bool:
         """Whether updates of this batch keep their activations in bf16 (sacmi.h)."""
         out = ctypes.c_int32()

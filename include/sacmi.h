@@ -234,6 +234,12 @@ int sacmi_step_ride_possible(sacmi_ctx* ctx, int32_t batch, int32_t* out);
  * batch-4096 class: hidden layers, minibatch rows and sampled actions; the policy heads
  * then read a bf16-rounded input), else 0. */
 int sacmi_step_act16(sacmi_ctx* ctx, int32_t batch, int32_t* out);
+/* 1 when the fused updates of this batch run their actor pass (sac_imp.py:116-125: the
+ * updated critics' forward, dL/da, the policy heads' and hidden layers' backward) as ONE
+ * persistent launch with cohort barriers instead of five launches (batch 256, fp32, two
+ * hidden layers, a device with >= 256 CUs; SACMI_NO_CHAIN at creation: off), else 0.  The
+ * results are the same bits either way. */
+int sacmi_step_chained(sacmi_ctx* ctx, int32_t batch, int32_t* out);
 int sacmi_grad_buffer(sacmi_ctx* ctx, int which, void** device_ptr, int64_t* numel);
 /* Gradient arena size (floats) and adoption of a caller-allocated device buffer of
  * that size (e.g. a torch tensor), so collectives run on it in place.  Must be on the

@@ -58,6 +58,20 @@ def make_ctx(cfg: SacConfig, max_batch, capacity, **kw):
     return ctx
 
 
+@pytest.fixture(scope="module")
+def nccl_world1():
+    """One 1-rank RCCL process group for the module's data-parallel tests (initialised once,
+    destroyed after the last of them): no process-group teardown / re-init between tests."""
+    import socket
+    import torch.distributed as dist
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+
+
 def load_params(ctx, params):
     for n in NETS:
         ctx.set_net(n, params[n])
@@ -659,16 +673,12 @@ def test_rng_seed_device_rekeys_noise():
 
 @pytest.mark.parametrize("n_hidden,dtype,B", [(2, "fp32", 64), (3, "fp32", 64), (2, "bf16", 64),
                                               (2, "bf16", 2048), (3, "bf16", 2048)])
-def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype, B):
+def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype, B, nccl_world1):
     """sacmi.dp over a 1-rank RCCL group (phases + in-place all-reduce on the adopted
     torch gradient arena) == the fused single-graph update, bit for bit (also for
     networks_model2 and the bf16 compute dtype)."""
-    import socket
-    import torch.distributed as dist
     from sacmi.dp import DataParallelUpdate, GpuBackend
-    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    ctxs, upd = [], None
     try:
         cfg = SacConfig(24, 4, 64, n_hidden=n_hidden)
         params = init_params(cfg, 71, bias_scale=0.05)
@@ -693,7 +703,12 @@ def test_dp_phase_path_matches_fused_step_world1(n_hidden, dtype, B):
                 assert np.array_equal(a[k], b[k]), (n, k)
         assert ctxs[0].get_scalar(0) == ctxs[1].get_scalar(0)
     finally:
-        dist.destroy_process_group()
+        # every context closed (and the updater holding the adopted torch gradient arena
+        # dropped) before the next test, on a drained device
+        torch.cuda.synchronize()
+        del upd
+        for c in ctxs:
+            c.close()
 
 
 BF16_EMU_LOSS_TOL = 1e-4   # relative, vs the oracle emulating the bf16 operands
@@ -885,19 +900,15 @@ def _assert_same_agent(a, b, what):
     assert np.array_equal(a.get_mt(1)[0], b.get_mt(1)[0]), (what, "numpy MT stream")
 
 
-def test_dp_config4_per_shard_world1_matches_fused():
+def test_dp_config4_per_shard_world1_matches_fused(nccl_world1):
     """BASELINE configs[3] per-GPU work (Humanoid S376 A17 H512, fp32, batch 4096, this
     rank's PRIORITIZED replay shard sampled on the device inside phase 0): the data-parallel
     update over a 1-rank RCCL group — eager torch.distributed driver and the library's own
     sacmi_step_dp — equals the fused
     single-GPU update bit for bit (parameters, alpha state, PER frame, numpy MT stream)."""
-    import socket
-    import torch.distributed as dist
     from sacmi.dp import DataParallelUpdate, GpuBackend
     from sacmi import Context
-    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    ctxs, upd = [], None
     try:
         B = 4096
         cfg = SacConfig(376, 17, 512)
@@ -909,6 +920,7 @@ def test_dp_config4_per_shard_world1_matches_fused():
         dev = torch.device("cuda", 0)
         # eager driver: 2 updates vs 2 fused
         a, f = _config4_ctxs(2, cfg, params, rows, prio, key, B)
+        ctxs += [a, f]
         upd = DataParallelUpdate(GpuBackend(a, dev))
         for _ in range(2):
             upd(B)
@@ -919,6 +931,7 @@ def test_dp_config4_per_shard_world1_matches_fused():
         a.close(); f.close()
         # the library-issued collectives
         n, f = _config4_ctxs(2, cfg, params, rows, prio, key, B)
+        ctxs += [n, f]
         n.allreduce_init(Context.allreduce_unique_id(), 0, 1)
         n.step_dp(B, 2)
         n.step_dp(B, 1)
@@ -927,7 +940,10 @@ def test_dp_config4_per_shard_world1_matches_fused():
         n.synchronize()
         _assert_same_agent(n, f, "native dp")
     finally:
-        dist.destroy_process_group()
+        torch.cuda.synchronize()
+        del upd
+        for c in ctxs:
+            c.close()
 
 
 @pytest.mark.parametrize("B,H", [(256, 512), (1024, 512), (1024, 768)])
@@ -962,6 +978,56 @@ def test_dlda_fold_matches_unfolded(B, H):
     assert abs(la[2] - lb[2]) <= 1e-6 * abs(lb[2]) + 1e-9
     for k in gb:
         assert rel(ga[k], gb[k]) <= 1e-5, (k, rel(ga[k], gb[k]))
+
+
+@pytest.mark.parametrize("auto_entropy", [False, True])
+def test_heads_fold_matches_separate_kernel(auto_entropy):
+    """The policy heads + sample folded into the last hidden layer's level (the last column
+    tile of each 32-row block runs them, config-2 shapes) vs the separate heads kernel
+    (SACMI_NO_HEADS_FOLD=1): the heads' outputs are the same sums in the same order, so with
+    a fixed alpha every loss and parameter is bit-identical over single, injected-noise and
+    multi-update launches; with alpha tuning only the log-prob partials are grouped by 32
+    rows instead of 16 — one update then leaves every network bit-identical and log_alpha
+    within fp32 rounding."""
+    cfg = SacConfig(376, 17, 512, automatic_entropy_tuning=auto_entropy)
+    B = 256
+    params = init_params(cfg, 151, bias_scale=0.02)
+    rows = synthetic_rows(cfg, 3000, 152, state_scale=0.1)
+    rng = np.random.default_rng(153)
+    idx = rng.choice(len(rows[2]), B, replace=False)
+    e1 = rng.standard_normal((B, 17)).astype(np.float32)
+    e2 = rng.standard_normal((B, 17)).astype(np.float32)
+    key = (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32)
+    res = []
+    for fold in (True, False):
+        if not fold:
+            os.environ["SACMI_NO_HEADS_FOLD"] = "1"
+        try:
+            ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]))
+            load_params(ctx, params)
+            ctx.push(*rows)
+            ctx.set_mt(0, key, 624)
+            out = [ctx.step(B, idx=idx, eps1=e1, eps2=e2)]
+            if not auto_entropy:
+                out.append(ctx.step(B))
+                ctx.step_many_async(B, 3)
+                out.append(ctx.fetch_losses(3).ravel())
+            st = ctx_state(ctx, cfg)
+            res.append((out, st, ctx_grads(ctx, cfg)))
+            ctx.close()
+        finally:
+            os.environ.pop("SACMI_NO_HEADS_FOLD", None)
+    (oa, sa, ga), (ob, sb, gb) = res
+    for a, b in zip(oa, ob):
+        assert np.array_equal(a, b)
+    for k in sb:
+        if k == "log_alpha" and auto_entropy:
+            assert abs(float(sa[k][0]) - float(sb[k][0])) <= 1e-6 * abs(float(sb[k][0])) + 1e-9
+        else:
+            assert np.array_equal(sa[k], sb[k]), k
+    for k in gb:
+        if not k.startswith("log_alpha"):
+            assert np.array_equal(ga[k], gb[k]), k
 
 
 @pytest.mark.parametrize("sharded", [True, False])
@@ -1154,3 +1220,51 @@ def test_dp_sharded_moments_read_guard():
     with pytest.raises(RuntimeError, match="sharded"):
         ctx.get_scalar(L.S_ADAM_V_LOG_ALPHA)
     ctx.close()
+
+
+@pytest.mark.parametrize("auto_entropy", [True, False])
+def test_chain_matches_launch_sequence(auto_entropy):
+    """The actor pass of a batch-256 fused update as ONE persistent launch (k_chain: L7 ->
+    L8 -> L9 -> sample-backward tail -> L12 with cohort barriers, the next update's sampler and
+    Polyak riding in its L12 phase) against the same levels as five launches
+    (SACMI_NO_CHAIN=1): the same workgroup bodies on the same tiles, so every loss, parameter,
+    gradient, Adam moment, target and the MT stream are bit-identical — over an update with
+    injected indices and noise, device-sampled single updates (drawn ahead) and a 5-update
+    launch (rides into the other batch set)."""
+    cfg = SacConfig(376, 17, 512, automatic_entropy_tuning=auto_entropy)
+    B = 256
+    params = init_params(cfg, 161, bias_scale=0.02)
+    rows = synthetic_rows(cfg, 3000, 162, state_scale=0.1)
+    rng = np.random.default_rng(163)
+    idx = rng.choice(len(rows[2]), B, replace=False)
+    e1 = rng.standard_normal((B, 17)).astype(np.float32)
+    e2 = rng.standard_normal((B, 17)).astype(np.float32)
+    key = (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32)
+    res = []
+    for chain in (True, False):
+        if not chain:
+            os.environ["SACMI_NO_CHAIN"] = "1"
+        try:
+            ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]))
+        finally:
+            os.environ.pop("SACMI_NO_CHAIN", None)
+        assert ctx.chained(B) == chain
+        load_params(ctx, params)
+        ctx.push(*rows)
+        ctx.set_mt(0, key, 624)
+        out = [ctx.step(B, idx=idx, eps1=e1, eps2=e2), ctx.step(B), ctx.step(B)]
+        ctx.step_many_async(B, 5)
+        out.append(ctx.fetch_losses(5).ravel())
+        st = ctx_state(ctx, cfg)
+        mom = {f"{n}.{slot}.{k}": v for n in ("policy", "q1", "q2") for slot in ("m", "v")
+               for k, v in ctx.get_net(n, slot).items()}
+        res.append((out, st, mom, ctx.get_mt(0)))
+        ctx.close()
+    (oa, sa, ma, mta), (ob, sb, mb, mtb) = res
+    for a, b in zip(oa, ob):
+        assert np.array_equal(a, b)
+    for k in sb:
+        assert np.array_equal(sa[k], sb[k]), k
+    for k in mb:
+        assert np.array_equal(ma[k], mb[k]), k
+    assert mta[1] == mtb[1] and np.array_equal(mta[0], mtb[0])
