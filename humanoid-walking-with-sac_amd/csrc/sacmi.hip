@@ -755,6 +755,7 @@ static double level_flops(const GemmBatch& b) {
     f += 2.0 * b.d[i].M * (double)b.d[i].N * b.d[i].K;
     if (b.d[i].pa_out) f += 2.0 * b.d[i].M * (double)b.d[i].N * b.d[i].pa_A;   // dL/da partials
   }
+  if (b.heads_ticket) f += 2.0 * b.heads.rows * (2.0 * b.heads.A) * b.heads.K;   // folded heads
   return f;
 }
 
@@ -2707,6 +2708,28 @@ int sacmi_dp_sync_state(sacmi_ctx* c) {
 int sacmi_step_act16(sacmi_ctx* c, int32_t batch, int32_t* out) {
   return guard([&] {
     pf_touch(c); *out = act16_on(c, batch) ? 1 : 0; });
+}
+
+int sacmi_read_activation(sacmi_ctx* c, int32_t pass, int32_t layer, int32_t batch, float* out,
+                          int64_t numel) {
+  return guard([&] {
+    REQUIRE(c && out, SACMI_EVALUE, "null argument");
+    REQUIRE(pass >= 0 && pass <= 3 && layer >= 0 && layer < c->nh, SACMI_EVALUE, "bad (pass, layer)");
+    REQUIRE(batch >= 1 && batch <= c->Bm, SACMI_EVALUE, "bad batch");
+    REQUIRE(numel == (int64_t)2 * batch * c->H, SACMI_EVALUE, "numel must be 2 * batch * hidden");
+    REQUIRE(!act16_on(c, batch), SACMI_ESTATE, "activations of this batch are stored as bf16");
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    const size_t H4 = (size_t)c->H * 4;
+    if (pass == 3) {
+      CHECK_HIP(hipMemcpy2D(out, H4, c->hp[layer].p, (size_t)c->Hd * 4, H4, (size_t)2 * batch,
+                            hipMemcpyDeviceToHost));
+      return;
+    }
+    const DevBuf<float>& b = pass == 0 ? c->hq[layer] : pass == 1 ? c->hqt[layer] : c->hqa[layer];
+    for (int i = 0; i < 2; ++i)
+      CHECK_HIP(hipMemcpy2D(out + (size_t)i * batch * c->H, H4, b.p + (size_t)i * c->Hd, (size_t)2 * c->Hd * 4, H4,
+                            (size_t)batch, hipMemcpyDeviceToHost));
+  });
 }
 
 int sacmi_step_chained(sacmi_ctx* c, int32_t batch, int32_t* out) {

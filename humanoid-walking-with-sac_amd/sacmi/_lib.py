@@ -87,6 +87,7 @@ _PROTOS = {
     "sacmi_step_ride_possible": [c_vp, ctypes.c_int32, c_i32p],
     "sacmi_step_act16": [c_vp, ctypes.c_int32, c_i32p],
     "sacmi_step_chained": [c_vp, ctypes.c_int32, c_i32p],
+    "sacmi_read_activation": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_f32p, ctypes.c_int64],
     "sacmi_fetch_losses": [c_vp, c_f32p, ctypes.c_int32, c_i32p],
     "sacmi_step_phase": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float],
     "sacmi_grad_buffer": [c_vp, ctypes.c_int, ctypes.POINTER(c_vp), c_i64p],
@@ -121,7 +122,7 @@ TL_KINDS = {1: "k_gemm", 2: "k_fwd", 3: "k_fwd16", 4: "k_axk16", 5: "k_dw_part",
             7: "k_dw_fin", 8: "k_heads_sample", 9: "k_gemm_sample_bwd", 10: "k_mt_sample",
             11: "k_gather", 12: "k_per_f1", 13: "k_per_f2", 14: "k_per_f2b", 15: "k_per_f3",
             16: "k_per_f4", 17: "per_unfused", 18: "k_adam", 19: "k_sample_bwd_tail",
-            20: "k_fwd16p"}
+            20: "k_fwd16p", 21: "k_chain"}
 EXPORTS = tuple(_PROTOS) + ("sacmi_abi_version", "sacmi_last_error")
 
 _lib = None

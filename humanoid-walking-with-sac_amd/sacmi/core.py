@@ -298,6 +298,14 @@ class Context:
         L.call("sacmi_step_ride_possible", self._h, int(batch), ctypes.byref(out))
         return bool(out.value)
 
+    def read_activation(self, pass_: int, layer: int, batch: int) -> np.ndarray:
+        """The last update's hidden activations (sacmi.h sacmi_read_activation): passes 0-2
+        -> [2, batch, hidden] (q1, q2), pass 3 (policy on [s'; s]) -> [2 * batch, hidden]."""
+        H = self.cfg.hidden_dim
+        out = np.zeros(2 * batch * H, np.float32)
+        L.call("sacmi_read_activation", self._h, int(pass_), int(layer), int(batch), L.fptr(out), out.size)
+        return out.reshape((2 * batch, H) if pass_ == 3 else (2, batch, H))
+
     def chained(self, batch: int) -> bool:
         """Whether fused updates of this batch run the actor pass as one persistent launch
         (k_chain, sacmi.h sacmi_step_chained)."""

@@ -240,6 +240,17 @@ int sacmi_step_act16(sacmi_ctx* ctx, int32_t batch, int32_t* out);
  * hidden layers, a device with >= 256 CUs; SACMI_NO_CHAIN at creation: off), else 0.  The
  * results are the same bits either way. */
 int sacmi_step_chained(sacmi_ctx* ctx, int32_t batch, int32_t* out);
+/* Test hook: the hidden activations (post-ReLU) the last update of `batch` rows left in
+ * HBM, hidden layer `layer` (0-based) of pass
+ *   0  the critics on (s, a)            -> [2][batch][hidden]  (q1, then q2)
+ *   1  the target critics on (s', a')   -> [2][batch][hidden]
+ *   2  the updated critics on (s, a~)   -> [2][batch][hidden]
+ *   3  the policy on [s' ; s]           -> [2 * batch][hidden]
+ * (numel = 2 * batch * hidden).  Their signs are the ReLU masks the update's backward used:
+ * the parity tests recompute the fp64 gradient under the GPU's own masks.  SACMI_ESTATE for
+ * bf16-stored activations (sacmi_step_act16). */
+int sacmi_read_activation(sacmi_ctx* ctx, int32_t pass, int32_t layer, int32_t batch, float* out,
+                          int64_t numel);
 int sacmi_grad_buffer(sacmi_ctx* ctx, int which, void** device_ptr, int64_t* numel);
 /* Gradient arena size (floats) and adoption of a caller-allocated device buffer of
  * that size (e.g. a torch tensor), so collectives run on it in place.  Must be on the

@@ -169,6 +169,20 @@ def _n_hidden(p) -> int:
 # already, and the critic head dots read the unrounded epilogue values.
 _ROUND = {"on": False, "act": False}
 
+# Forced ReLU masks (test infrastructure): {(pass tag, hidden layer index): {0,1} tensor of the
+# layer's output shape}.  With a mask given, the layer's output is pre * mask instead of
+# relu(pre), and its backward is masked the same way: the update evaluated in the oracle's
+# precision under ANOTHER evaluation's ReLU decisions (the GPU's: sacmi_read_activation), which
+# separates fp32 summation-order flips of near-zero pre-activations from kernel error.
+# Tags: q1 / q2 (critics on (s, a)), q1t / q2t (targets on (s', a')), pi_s2 / pi_s (policy on
+# s' / s), q1a / q2a (updated critics on (s, a~)).
+_MASKS: dict = {}
+
+
+def _relu(x, tag, i):
+    m = _MASKS.get((tag, i)) if tag else None
+    return F.relu(x) if m is None else x * m.to(x.dtype)
+
 
 def _bf(t):
     return t.to(torch.bfloat16).to(t.dtype)
@@ -201,18 +215,18 @@ def _lin(x, w, b, role):
     return F.linear(x, w, b)
 
 
-def _q_forward(p, state, action):
+def _q_forward(p, state, action, tag=None):
     x = torch.cat([state, action], dim=-1)
     nh = _n_hidden(p)
     for i in range(1, nh + 1):
-        x = F.relu(_lin(x, p[f"fc{i}.weight"], p[f"fc{i}.bias"], "in" if i == 1 else "hid"))
+        x = _relu(_lin(x, p[f"fc{i}.weight"], p[f"fc{i}.bias"], "in" if i == 1 else "hid"), tag, i - 1)
     return _lin(x, p[f"fc{nh + 1}.weight"], p[f"fc{nh + 1}.bias"], "head")
 
 
-def _policy_forward(p, state):
+def _policy_forward(p, state, tag=None):
     x = state
     for i in range(1, _n_hidden(p) + 1):
-        x = F.relu(_lin(x, p[f"fc{i}.weight"], p[f"fc{i}.bias"], "in" if i == 1 else "hid"))
+        x = _relu(_lin(x, p[f"fc{i}.weight"], p[f"fc{i}.bias"], "in" if i == 1 else "hid"), tag, i - 1)
     if _ROUND["on"] and _ROUND["act"]:
         x = x + (_bf(x) - x).detach()
     mean = _lin(x, p["mean.weight"], p["mean.bias"], "head")
@@ -220,8 +234,8 @@ def _policy_forward(p, state):
     return mean, torch.clamp(log_std, -20, 2)
 
 
-def _policy_sample(p, state, eps, scale, bias):
-    mean, log_std = _policy_forward(p, state)
+def _policy_sample(p, state, eps, scale, bias, tag=None):
+    mean, log_std = _policy_forward(p, state, tag)
     std = log_std.exp()
     normal = torch.distributions.Normal(mean, std)
     x_t = mean + eps * std                     # Normal.rsample with injected eps
@@ -258,16 +272,21 @@ class OracleSAC:
         self.alpha = self.cfg.alpha                     # python float until 1st update
 
     def step(self, s, a, r, s2, d, eps1, eps2, bf16_operands: bool = False,
-             bf16_act: bool = False) -> dict:
+             bf16_act: bool = False, masks: dict | None = None) -> dict:
         """``bf16_operands``: emulate compute_dtype=bf16 (see _EmuLinear); ``bf16_act``:
-        with bf16-stored activations (sacmi_step_act16)."""
+        with bf16-stored activations (sacmi_step_act16); ``masks``: forced ReLU masks
+        (see _MASKS: {(tag, layer): array})."""
         _ROUND["on"] = bool(bf16_operands)
         _ROUND["act"] = bool(bf16_act)
+        _MASKS.clear()
+        for k, m in (masks or {}).items():
+            _MASKS[k] = torch.as_tensor(np.asarray(m, dtype=np.float32))
         try:
             return self._step(s, a, r, s2, d, eps1, eps2)
         finally:
             _ROUND["on"] = False
             _ROUND["act"] = False
+            _MASKS.clear()
 
     def _step(self, s, a, r, s2, d, eps1, eps2) -> dict:
         cfg, dt = self.cfg, self.dtype
@@ -279,13 +298,13 @@ class OracleSAC:
         P, Q1, Q2 = self.nets["policy"], self.nets["q1"], self.nets["q2"]
         sc, bi = cfg.action_scale, cfg.action_bias
         with torch.no_grad():
-            na, nlp = _policy_sample(P, next_state, e1, sc, bi)
-            q1n = _q_forward(self.nets["q1_target"], next_state, na)
-            q2n = _q_forward(self.nets["q2_target"], next_state, na)
+            na, nlp = _policy_sample(P, next_state, e1, sc, bi, "pi_s2")
+            q1n = _q_forward(self.nets["q1_target"], next_state, na, "q1t")
+            q2n = _q_forward(self.nets["q2_target"], next_state, na, "q2t")
             value_target = torch.min(q1n, q2n) - self.alpha * nlp
             q_target = reward + (1 - done) * cfg.gamma * value_target
-        q1_loss = F.mse_loss(_q_forward(Q1, state, action), q_target)
-        q2_loss = F.mse_loss(_q_forward(Q2, state, action), q_target)
+        q1_loss = F.mse_loss(_q_forward(Q1, state, action, "q1"), q_target)
+        q2_loss = F.mse_loss(_q_forward(Q2, state, action, "q2"), q_target)
         grads = {}
         self.opt["q1"].zero_grad(); q1_loss.backward()
         grads["q1"] = {k: v.grad.detach().clone() for k, v in Q1.items()}
@@ -294,8 +313,8 @@ class OracleSAC:
         grads["q2"] = {k: v.grad.detach().clone() for k, v in Q2.items()}
         self.opt["q2"].step()
 
-        new_a, logp = _policy_sample(P, state, e2, sc, bi)
-        q_new = torch.min(_q_forward(Q1, state, new_a), _q_forward(Q2, state, new_a))
+        new_a, logp = _policy_sample(P, state, e2, sc, bi, "pi_s")
+        q_new = torch.min(_q_forward(Q1, state, new_a, "q1a"), _q_forward(Q2, state, new_a, "q2a"))
         policy_loss = (self.alpha * logp - q_new).mean()
         self.opt["policy"].zero_grad(); policy_loss.backward()
         grads["policy"] = {k: v.grad.detach().clone() for k, v in P.items()}

@@ -177,3 +177,35 @@ def test_reference_checkpoint_fixture_matches_dropin_layout():
                 p = f"{tag}.{n}.{k}"
                 assert np.array_equal(v.numpy().reshape(-1)[z[p + ".idx"]], z[p + ".val"]), p
         assert torch.is_tensor(ck["alpha"]) and ck["alpha"].requires_grad
+
+
+def test_forced_relu_masks_reproduce_the_unmasked_step():
+    """OracleSAC.step(masks=...) evaluates the update under given ReLU decisions (the GPU's,
+    in tests/test_gpu_parity.py).  Given the oracle's OWN decisions, it is the unmasked step
+    bit for bit; one flipped decision moves the critic loss and the gradients."""
+    import torch
+    from oracle.sac_step import OracleSAC, SacConfig, init_params, synthetic_rows
+    cfg = SacConfig(6, 2, 16)
+    params = init_params(cfg, 3, bias_scale=0.1)
+    s, a, r, s2, d = synthetic_rows(cfg, 8, 4, state_scale=0.5)
+    rng = np.random.default_rng(5)
+    e1, e2 = (rng.standard_normal((8, 2)).astype(np.float32) for _ in range(2))
+    q1 = params["q1"]
+    x = np.concatenate([s, a], 1).astype(np.float64)
+    pre = x @ q1["fc1.weight"].T.astype(np.float64) + q1["fc1.bias"]
+    own = {("q1", 0): (pre > 0).astype(np.float32)}
+    ref = OracleSAC(cfg, params, torch.float64)
+    l_ref = ref.step(s, a, r, s2, d, e1, e2)
+    m = OracleSAC(cfg, params, torch.float64)
+    l_m = m.step(s, a, r, s2, d, e1, e2, masks=own)
+    assert l_ref == l_m
+    for k, v in ref.grads_flat().items():
+        assert np.array_equal(v, m.grads_flat()[k]), k
+    flipped = {("q1", 0): own[("q1", 0)].copy()}
+    i, j = np.argwhere(own[("q1", 0)] > 0)[0]
+    flipped[("q1", 0)][i, j] = 0.0
+    f = OracleSAC(cfg, params, torch.float64)
+    l_f = f.step(s, a, r, s2, d, e1, e2, masks=flipped)
+    assert l_f["q1_loss"] != l_ref["q1_loss"] and l_f["q2_loss"] == l_ref["q2_loss"]
+    g_f, g_r = f.grads_flat()["q1.fc1.weight"], ref.grads_flat()["q1.fc1.weight"]
+    assert not np.array_equal(g_f, g_r)
