@@ -1098,12 +1098,12 @@ __device__ __forceinline__ void rows_load(const RowsFuse& rf, const GemmDesc& d,
   }
   const int b = m0 + t;
   const uint32_t ob = (uint32_t)((t < TMW && b < rf.B) ? b : 0) * 4u;
-  x.alpha = buf_ld(rSc, 0u);
-  x.lp = buf_ld(rLp, ob);
-  x.r = buf_ld(rR, ob);
-  x.d = buf_ld(rD, ob);
+  x.alpha = buf_ld_aux<AUX>(rSc, 0u);
+  x.lp = buf_ld_aux<AUX>(rLp, ob);
+  x.r = buf_ld_aux<AUX>(rR, ob);
+  x.d = buf_ld_aux<AUX>(rD, ob);
   const int lane = t - TMW * nslot;
-  x.lpa = buf_ld(rLpa, (uint32_t)(2 * (lane >= 0 && lane < rf.n_lp ? lane : 0) + 1) * 4u);
+  x.lpa = buf_ld_aux<AUX>(rLpa, (uint32_t)(2 * (lane >= 0 && lane < rf.n_lp ? lane : 0) + 1) * 4u);
 }
 
 template <int TMW, int NTH>
@@ -1783,18 +1783,21 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
     // folded heads: the tile's h stores (write-through) acknowledged in every wave, then the
     // row block's arrival count; its last column tile runs the heads + sample of the block's
     // 32 rows, reading h with sc1 loads (rows the other tiles stored from other XCDs)
-    if (batch.heads_ticket != nullptr && p == batch.heads_desc) {
+    // (the policy rows may come as heads_ndesc descs of d.M rows each, stacked in order: the
+    // target and actor halves of k_chain_a's row-affine L2)
+    if (batch.heads_ticket != nullptr && p >= batch.heads_desc && p < batch.heads_desc + batch.heads_ndesc) {
+      const int hm0 = m0 + (p - batch.heads_desc) * d.M;   // the row in the heads' stacked rows
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
-        int* tk = batch.heads_ticket + m0 / kHeadsFoldTM;
+        int* tk = batch.heads_ticket + hm0 / kHeadsFoldTM;
         const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_hlast = old == d.tiles_n - 1;
         if (old == d.tiles_n - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
       if (s_hlast)
-        heads_rows<48, 16, false, kHeadsFoldTM, kLdSc1>(batch.heads, m0, m0 / kHeadsFoldTM, red,
+        heads_rows<48, 16, false, kHeadsFoldTM, kLdSc1>(batch.heads, hm0, hm0 / kHeadsFoldTM, red,
                                                          reinterpret_cast<float(*)[33]>(s_hlp),
                                                          s_hlp + kHeadsFoldTM * 33);
     }
@@ -3550,8 +3553,8 @@ __device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int 
       const float y = tanhf(x);
       if constexpr (H16)
         reinterpret_cast<unsigned short*>(a.act)[(size_t)m * a.ldact + j] = bf16_bits(y * a.scale + a.bias);
-      else
-        a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
+      else   // (write-through where the same launch reads them back: k_chain_a's L3)
+        st_pol(a.act + (size_t)m * a.ldact + j, y * a.scale + a.bias, AAUX != 0);
       if (a.act_host) a.act_host[(size_t)m * A + j] = y * a.scale + a.bias;
       const float dx = x - mean;
       lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
@@ -3568,7 +3571,7 @@ __device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int 
     float s = 0.f;
     if (mm < a.rows) {
       for (int jj = 0; jj < A; ++jj) s += lp[threadIdx.x][jj];
-      a.logp[mm] = s;
+      st_pol(a.logp + mm, s, AAUX != 0);
     }
     s_lp[threadIdx.x] = s;
   }
@@ -4008,18 +4011,25 @@ __global__ __launch_bounds__(1024, 4) void k_chain(const ChainArgs* __restrict__
     asm volatile("" : "+s"(p4));
     return (const ChainArgs*)p4;
   };
+  // (diagnostic builds, SACMI_DIAG_PHASES: wave 0's clock at every phase boundary — slot 2i+1
+  // after phase i's work, 2i+2 after its barrier; tools/phase_dump.py)
+  SACMI_PHASE(tl, 0);
   // L7 (updated critics fc1 on [s|1|a~]), L8 (fc2 + fc3 dot partials)
 #pragma unroll 1
   for (int i = 0; i < 2; ++i) {
     const GemmBatch& b = opaque()->lv[i];
     if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.a);
+    SACMI_PHASE(tl, 2 * i + 1);
     bar(i, true);
+    SACMI_PHASE(tl, 2 * i + 2);
   }
   // L9: the actor row prologue + dha1 + the dL/da partials
   {
     const GemmBatch& b = opaque()->lv[2];
     if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1>(b, blockIdx.x, sm.b);
+    SACMI_PHASE(tl, 5);
     bar(2, true);
+    SACMI_PHASE(tl, 6);
   }
   // the sample-backward tail: the cohort's 8-row groups x 64-column dhp2 slabs
   {
@@ -4031,21 +4041,77 @@ __global__ __launch_bounds__(1024, 4) void k_chain(const ChainArgs* __restrict__
       tail_unit<kLdSc1>(q->pa, q->n_pa, q->tail, c * q->rows_per_cohort + g * kTailRows,
                         slab * kTailCols, slab == 0, sm.t);
     }
+    SACMI_PHASE(tl, 7);
   }
   // L12 (dhp1) + the level's rides (the next update's sampler, Polyak): a workgroup whose
   // items are all rides reads nothing of the chain — it arrives and goes on
   {
     const GemmBatch& b = opaque()->lv[3];
     bar(3, (int)blockIdx.x < b.total_tiles);
+    SACMI_PHASE(tl, 8);
     const int items = b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
     if ((int)blockIdx.x < items) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.a);
+    SACMI_PHASE(tl, 9);
   }
 }
 
-// 32x32 tiles, XCD-blocked with a row grid of 8: tile t of a desc -> row tile
-// (t & 7) * tm / 8 + q, so workgroup b (b & 7 = cohort) only ever touches its cohort's rows
-bool chain_assign_tiles(GemmBatch& b) {
-  assign_tiles<32, 32>(b);
+// the critic pass (ChainArgs kind 1): L1 / L2 on 32x64 tiles (L2 with the policy heads
+// folded in), L3 / L4 on 32x32, L5 (row prologue, A transform) on 32x32
+using ChainKgW = KgSmem<32, 64, 16, 2, 1, false, 0, false, 0>;
+union ChainSmemA {
+  ChainKgW w;
+  ChainKgA a;
+  ChainKgB b;
+};
+
+__global__ __launch_bounds__(1024, 4) void k_chain_a(const ChainArgs* __restrict__ ca, tl_word* tl) {
+  const TlMark tl_mark(tl, TL_CHAIN_A);
+  __shared__ ChainSmemA sm;
+  const int c = blockIdx.x & (kChainCohorts - 1);
+  const int nmem = gridDim.x / kChainCohorts;
+  typedef __attribute__((address_space(4))) const ChainArgs ConstChainArgs;
+  auto opaque = [&]() {   // (see k_chain)
+    ConstChainArgs* p4 = (ConstChainArgs*)ca;
+    asm volatile("" : "+s"(p4));
+    return (const ChainArgs*)p4;
+  };
+  auto bar = [&](int b) {
+    const ChainArgs* q = opaque();
+    int* const sync = q->sync + c * kChainBars * 32;
+    chain_bar(sync + b * 32, sync + b * 32 + 1, nmem, q->err, true);
+  };
+  SACMI_PHASE(tl, 0);   // (diagnostic builds: as k_chain's)
+  // L1, L2 (+ the heads): 32x64 tiles
+#pragma unroll 1
+  for (int i = 0; i < 2; ++i) {
+    const GemmBatch& b = opaque()->lv[i];
+    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.w);
+    SACMI_PHASE(tl, 2 * i + 1);
+    bar(i);
+    SACMI_PHASE(tl, 2 * i + 2);
+  }
+  // L3, L4 (target critics): 32x32 tiles
+#pragma unroll 1
+  for (int i = 2; i < 4; ++i) {
+    const GemmBatch& b = opaque()->lv[i];
+    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.a);
+    SACMI_PHASE(tl, 2 * i + 1);
+    bar(i);
+    SACMI_PHASE(tl, 2 * i + 2);
+  }
+  // L5: the critic row prologue (targets, MSE gradients, loss partials) + dh1
+  {
+    const GemmBatch& b = opaque()->lv[4];
+    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1>(b, blockIdx.x, sm.b);
+    SACMI_PHASE(tl, 9);
+  }
+}
+
+// 32x32 (TN = 64: 32x64) tiles, XCD-blocked with a row grid of 8: tile t of a desc -> row
+// tile (t & 7) * tm / 8 + q, so workgroup b (b & 7 = cohort) only ever touches its cohort's rows
+bool chain_assign_tiles(GemmBatch& b, int tn) {
+  if (tn == 64) assign_tiles<32, 64>(b);
+  else assign_tiles<32, 32>(b);
   for (int i = 0; i < b.count; ++i) {
     GemmDesc& d = b.d[i];
     if (d.tiles_m % kChainCohorts || d.tile_begin % kChainCohorts) return false;
@@ -4067,16 +4133,45 @@ bool chain_supported() {
   if (!ok_dev[dev]) {
     hipDeviceProp_t prop;
     int per_cu = 0;
+    int per_cu_a = 0;
     const bool ok = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount >= kChainGrid &&
                     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_chain, 1024, 0) == hipSuccess &&
-                    per_cu >= 1;
+                    per_cu >= 1 &&
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_a, k_chain_a, 1024, 0) == hipSuccess &&
+                    per_cu_a >= 1;
     ok_dev[dev] = ok ? 1 : 2;
   }
   return ok_dev[dev] == 1;
 }
 
+bool chain_a_l2_ok(const GemmBatch& b) {
+  return gemm_level_heads_fold_ok(b, b.heads.A);
+}
+
 bool launch_chain(const ChainArgs& h, const ChainArgs* dev, tl_word* tl, hipStream_t s) {
   if (!chain_supported()) return false;
+  if (h.kind == 1) {
+    // the critic pass: fp32 k_gemm bodies, L1 / L2 32x64 (L2 may fold the heads), L3 / L4
+    // 32x32, L5 32x32 with the critic row prologue; no Adam, rides, split-K, bf16
+    for (int i = 0; i < kChainLevels; ++i) {
+      const GemmBatch& b = h.lv[i];
+      if (b.count < 1 || b.bf16 || b.has_adam || b.err_flags || !b.st_wt || b.ride.kind || b.ride.pk_blocks ||
+          (b.heads_ticket && i != 1) || b.total_tiles > kChainGrid)
+        throw Error{SACMI_ESTATE, "k_chain_a: unsupported level configuration"};
+      if (b.heads_ticket && b.heads.A * 2 > 48) throw Error{SACMI_ESTATE, "k_chain_a: heads wider than 48"};
+      for (int q = 0; q < b.count; ++q) {
+        const GemmDesc& d = b.d[q];
+        if (d.axk != (i == 4 ? 1 : 0) || d.epi >= EPI_ADAM || d.a16 || d.b16 || d.c16 || d.x16 || d.pa_out ||
+            d.xcd_gr != kChainCohorts || d.tiles_m % kChainCohorts || d.M != h.rows_per_cohort * kChainCohorts)
+          throw Error{SACMI_ESTATE, "k_chain_a: unsupported GEMM in a chain level"};
+        if (d.tiles_n * (i < 2 ? 64 : 32) < d.N || (i < 2 && d.tiles_n * 32 >= d.N && d.N > 32))
+          throw Error{SACMI_ESTATE, "k_chain_a: a level's tiles differ from the kernel's"};
+      }
+    }
+    hipLaunchKernelGGL(k_chain_a, dim3(kChainGrid), dim3(1024), 0, s, dev, tl);
+    HIP_LAUNCH_CHECK();
+    return true;
+  }
   // the configuration k_chain instantiates: fp32 32x32 k_gemm tiles (L9 with the A transform
   // and the dL/da partials), no fused Adam, no split-K / bf16 activations, rides on L12 only
   for (int i = 0; i < kChainLevels; ++i) {

@@ -977,15 +977,17 @@ static bool chain_batch_ok(const sacmi_ctx* c, int B) {
   return c->chain_on && !c->bf16 && c->nh == 2 && B == kChainCohorts * 32 && c->H % 32 == 0 && c->H <= 512 &&
          !std::getenv("SACMI_NO_DLDA_FOLD") && chain_supported();
 }
-static bool enqueue_chain(sacmi_ctx* c, int B, const Level& l7, const Level& l8, const Level& l9,
-                          const SampleBwdArgs& sb, const Level& l12) {
-  // (site-isolation profiling enumerates the sites outside a capture: the launch chain there)
+// kind 0: the actor pass (L7, L8, L9, the tail `sb`, L12); kind 1: the critic pass (L1 and
+// L2 on 32x64 tiles, L2 carrying the policy heads fold, L3, L4, L5).  (Site-isolation
+// profiling enumerates the sites outside a capture: the launch chain there.)
+static bool enqueue_chain_kind(sacmi_ctx* c, int B, int kind, const Level* const* lv, int n,
+                               const SampleBwdArgs* sb) {
   if (!c->own_capture || c->prof_site >= 0 || c->prof_collect || !chain_batch_ok(c, B)) return false;
   ChainArgs ca;
   std::memset(&ca, 0, sizeof(ca));
-  const Level* lv[kChainLevels] = {&l7, &l8, &l9, &l12};
-  double flops = 2.0 * B * (2.0 * c->A) * c->H, bytes = 0;   // (the tail's dhp2 product)
-  for (int i = 0; i < kChainLevels; ++i) {
+  ca.kind = kind;
+  double flops = kind == 0 ? 2.0 * B * (2.0 * c->A) * c->H : 0.0, bytes = 0;   // (the tail's dhp2 product)
+  for (int i = 0; i < n; ++i) {
     GemmBatch b = lv[i]->b;
     b.bf16 = 0;
     for (int q = 0; q < b.count; ++q) b.d[q].Bh = nullptr;
@@ -994,16 +996,19 @@ static bool enqueue_chain(sacmi_ctx* c, int B, const Level& l7, const Level& l8,
     b.st_wt = 1;           // write-through epilogue stores: every hand-off's bytes leave L2
     b.adam_wg = -2;
     validate_batch(b);
-    if (!chain_assign_tiles(b) || b.total_tiles > kChainGrid) return false;
+    if (!chain_assign_tiles(b, kind == 1 && i < 2 ? 64 : 32) || b.total_tiles > kChainGrid) return false;
     const int items = b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
     if (items > kChainGrid) return false;
+    if (b.heads_ticket && !(kind == 1 && i == 1 && chain_a_l2_ok(b))) return false;
     flops += level_flops(b);
     bytes += level_bytes(b);
     ca.lv[i] = b;
   }
-  ca.tail = sb;
-  ca.tail.tl = nullptr;
-  ca.pa = c->pa.p; ca.n_pa = 2 * c->nparts;
+  if (sb) {
+    ca.tail = *sb;
+    ca.tail.tl = nullptr;
+    ca.pa = c->pa.p; ca.n_pa = 2 * c->nparts;
+  }
   ca.rows_per_cohort = B / kChainCohorts;
   ca.tail_groups = ca.rows_per_cohort / 8;
   ca.tail_slabs = (c->H + 63) / 64;
@@ -1013,10 +1018,15 @@ static bool enqueue_chain(sacmi_ctx* c, int B, const Level& l7, const Level& l8,
   check_span(ca.sync, kChainSyncInts - 1, "chain barrier words");
   const ChainArgs* dev = chain_slot(c, ca);
   if (!dev) return false;   // (pool full: the launch chain)
-  if (mark(c, "gemm_chain_L7_L12", flops, bytes)) {
+  if (mark(c, kind == 0 ? "gemm_chain_L7_L12" : "gemm_chain_L1_L5", flops, bytes)) {
     if (!launch_chain(ca, dev, c->tl_cur, c->stream)) throw Error{SACMI_ESTATE, "k_chain refused a supported configuration"};
   }
   return true;
+}
+static bool enqueue_chain(sacmi_ctx* c, int B, const Level& l7, const Level& l8, const Level& l9,
+                          const SampleBwdArgs& sb, const Level& l12) {
+  const Level* lv[4] = {&l7, &l8, &l9, &l12};
+  return enqueue_chain_kind(c, B, 0, lv, 4, &sb);
 }
 
 // parity: which batch buffer set this update uses; have_batch: its indices and rows
@@ -1093,12 +1103,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     if (!have_batch)   // (have_batch: the previous update's rides / side stream produced them)
       enqueue_sample_gather(c, B, parity, dev_idx != 0, s);
 
-    // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
-    Level l1;
-    l1.add(fw(gd(bb.x2, Kx, 1, W(c->p_fc[0]), c->p_fc[0].ld, 1, c->hp[0].p, Hd, 2 * B, H, S + 1, EPI_RELU)));
-    for (int i = 0; i < 2; ++i)
-      l1.add(fw(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
-    run(l1, "gemm_L1_fc1");
     // heads + sample for both stacks (networks_model1.py:78-99)
     HeadSampleArgs hs{};
     hs.h = c->hp[L].p; hs.Wh = W(c->p_head); hs.rows = 2 * B; hs.A = A; hs.K = H;
@@ -1111,6 +1115,63 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     hs.logp_part = c->lp_part.p; hs.split_row = B;    // sums of log pi(a~|s) for dL/dlog_alpha
     // Normal validation of policy.sample(next_state) / policy.sample(state) (sac_imp.py:89,116)
     hs.nan_flag = &c->sc.p->err; hs.nan_bit_lo = ERR_NAN_TGT; hs.nan_bit_hi = ERR_NAN_ACT;
+    const bool fuse = phase_mask == 7;     // single-GPU update: Adam in the dW epilogues
+    // L5: dh[L-1] = (dh[L] W[L]) * relu'(h[L-1]), with the target / critic-loss rows folded
+    // in: the row prologue finishes q1, q2, qt1, qt2 from the dot partials and gives
+    // dq_i = 2 (q_i - q^) / B; the A operand dh[L] = dq * w_head * [h[L] > 0] is formed
+    // from h[L] on the fly (its coefficient-free rows u stored once by the column-tile-0
+    // workgroups, for the weight gradient of layer L)
+    Level l5;
+    for (int i = 0; i < 2; ++i) {
+      GemmDesc g = gd(E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dhc[L - 1].p + i * H, 2 * H,
+                      B, H, H, EPI_MASK, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd);
+      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]); g.ax_out = c->dhc[L].p + i * H; g.ax_ld = 2 * H;
+      l5.add(dh(g));
+    }
+    {
+      RowsFuse& rf = l5.b.rows;
+      rf.kind = 1; rf.part = dotp(0); rf.nparts = c->nparts; rf.B = B;
+      rf.r = bb.r; rf.d = bb.d; rf.logp = c->logp.p; rf.logp_a = c->logp.p + B;
+      rf.gamma = (float)c->cfg.gamma;
+      rf.sc = c->sc.p; rf.dq = c->dq.p; rf.dq4 = c->dq4.p; rf.loss_part = c->lpart_c.p;
+    }
+    // The critic pass L1 -> L2 (+ heads) -> L3 -> L4 -> L5 as ONE persistent launch
+    // (k_chain_a) where it applies: the policy rows as two row-affine descs (targets'
+    // s', actors' s), so that every cohort holds the a' its target critics read
+    bool chained_a = false;
+    if (nh == 2 && heads_fold_wanted() && chain_batch_ok(c, B)) {
+      Level a1, a2, a3, a4;
+      for (int h2 = 0; h2 < 2; ++h2)
+        a1.add(fw(gd(bb.x2 + (size_t)h2 * B * Kx, Kx, 1, W(c->p_fc[0]), c->p_fc[0].ld, 1, c->hp[0].p + (size_t)h2 * B * Hd,
+                     Hd, B, H, S + 1, EPI_RELU)));
+      for (int i = 0; i < 2; ++i)
+        a1.add(fw(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
+      for (int h2 = 0; h2 < 2; ++h2)
+        a2.add(fw(gd_fwd_h(c->hp[0].p + (size_t)h2 * B * Hd, Hd, W(c->p_fc[1]), Hd, c->hp[1].p + (size_t)h2 * B * Hd, Hd,
+                           B, H, H)));
+      for (int i = 0; i < 2; ++i)
+        a2.add(with_dot(fw(gd_fwd_h(E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, W(q[i][1]), Hd, E(c->hq[1].p, (size_t)i * Hd),
+                                    2 * Hd, B, H, H)), W(q[i][nh]), i));
+      a2.b.heads = hs;
+      a2.b.heads_desc = 0;
+      a2.b.heads_ndesc = 2;
+      a2.b.heads_ticket = c->heads_ticket.p;
+      for (int i = 0; i < 2; ++i)
+        a3.add(fw(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, E(c->hqt[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
+      for (int i = 0; i < 2; ++i)
+        a4.add(with_dot(fw(gd_fwd_h(E(c->hqt[0].p, (size_t)i * Hd), 2 * Hd, Wt(q[i][1]), Hd, E(c->hqt[1].p, (size_t)i * Hd),
+                                    2 * Hd, B, H, H)), Wt(q[i][nh]), 2 + i));
+      const Level* lv[5] = {&a1, &a2, &a3, &a4, &l5};
+      chained_a = enqueue_chain_kind(c, B, 1, lv, 5, nullptr);
+      if (chained_a) c->heads_fold_B = B;
+    }
+    if (!chained_a) {
+    // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
+    Level l1;
+    l1.add(fw(gd(bb.x2, Kx, 1, W(c->p_fc[0]), c->p_fc[0].ld, 1, c->hp[0].p, Hd, 2 * B, H, S + 1, EPI_RELU)));
+    for (int i = 0; i < 2; ++i)
+      l1.add(fw(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
+    run(l1, "gemm_L1_fc1");
     // L2 (.. L2b): the remaining hidden layers (K = H, bias in the epilogue); the last one
     // also accumulates the critic head (fc3 / fc4) dot partials of q1 / q2 (slots 0 / 1) and,
     // where its tiles can (gemm_level_heads_fold_ok), runs the heads + sample folded in: the
@@ -1129,6 +1190,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       if (l == L && heads_fold_wanted() && gemm_level_heads_fold_ok(lv.b, A)) {
         lv.b.heads = hs;
         lv.b.heads_desc = 0;   // (the policy desc, added first)
+        lv.b.heads_ndesc = 1;
         lv.b.heads_ticket = c->heads_ticket.p;
         folded = true;
       }
@@ -1155,26 +1217,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       }
       run(lv, l == 1 ? "gemm_L4_tgt_fc2" : "gemm_L4b_tgt_fc3");
     }
-    // L5: dh[L-1] = (dh[L] W[L]) * relu'(h[L-1]), with the target / critic-loss rows folded
-    // in: the row prologue finishes q1, q2, qt1, qt2 from the dot partials and gives
-    // dq_i = 2 (q_i - q^) / B; the A operand dh[L] = dq * w_head * [h[L] > 0] is formed
-    // from h[L] on the fly (its coefficient-free rows u stored once by the column-tile-0
-    // workgroups, for the weight gradient of layer L)
-    const bool fuse = phase_mask == 7;     // single-GPU update: Adam in the dW epilogues
-    Level l5;
-    for (int i = 0; i < 2; ++i) {
-      GemmDesc g = gd(E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dhc[L - 1].p + i * H, 2 * H,
-                      B, H, H, EPI_MASK, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd);
-      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]); g.ax_out = c->dhc[L].p + i * H; g.ax_ld = 2 * H;
-      l5.add(dh(g));
-    }
-    {
-      RowsFuse& rf = l5.b.rows;
-      rf.kind = 1; rf.part = dotp(0); rf.nparts = c->nparts; rf.B = B;
-      rf.r = bb.r; rf.d = bb.d; rf.logp = c->logp.p; rf.logp_a = c->logp.p + B;
-      rf.gamma = (float)c->cfg.gamma;
-      rf.sc = c->sc.p; rf.dq = c->dq.p; rf.dq4 = c->dq4.p; rf.loss_part = c->lpart_c.p;
-    }
     run(l5, "gemm_L5_critic_dh1");
     // L5b (3 hidden layers): dh[l-1] = (dh[l] W[l]) * relu'(h[l-1]) down to dh[0]
     for (int l = L - 1; l >= 1; --l) {
@@ -1184,6 +1226,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
                      B, H, H, EPI_MASK, E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd)));
       run(lv, "gemm_L5b_critic_dh");
     }
+    }   // (!chained_a)
     // L6: every critic weight gradient: into the gradient arena, or (fused) straight into
     // Adam + Polyak on the parameters.  The hidden weights are read by the dh levels
     // above, so every critic dW runs here — in both modes, so the reduction order (and
@@ -1379,7 +1422,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l13.b.ride.ga = gather_args(c, B, nb2, false);
     }
     // the persistent chain (k_chain) where it applies, else the launches one by one
-    if (!(fuse && nh == 2 && fold_dlda && enqueue_chain(c, B, l7, l8s[0], l9, sb, l12))) {
+    if (!(nh == 2 && fold_dlda && enqueue_chain(c, B, l7, l8s[0], l9, sb, l12))) {
       run(l7, "gemm_L7_act_fc1");
       for (size_t i = 0; i < l8s.size(); ++i) run(l8s[i], i == 0 ? "gemm_L8_act_fc2" : "gemm_L8b_act_fc3");
       run(l9, "gemm_L9_act_dh1");

@@ -116,7 +116,7 @@ typedef unsigned long long tl_word;
 enum TlKind : int {
   TL_GEMM = 1, TL_FWD, TL_FWD16, TL_AXK16, TL_DW_PART, TL_DW_PART16, TL_DW_FIN, TL_HEADS,
   TL_SAMPLE_BWD, TL_MT_SAMPLE, TL_GATHER, TL_PER_F1, TL_PER_F2, TL_PER_F2B, TL_PER_F3,
-  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_CHAIN, TL_KINDS
+  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_CHAIN, TL_CHAIN_A, TL_KINDS
 };
 constexpr int kTlEnd = 4;            // first of the ~end slots
 constexpr int kTlEndSlots = 4096;
@@ -472,7 +472,8 @@ struct GemmBatch {
   // tile of each 32-row block to finish (heads_ticket[row block]: an arrival count, reset
   // by that tile) runs them for the block's rows
   HeadSampleArgs heads;
-  int heads_desc;      // the policy desc of the level
+  int heads_desc;      // the (first) policy desc of the level
+  int heads_ndesc;     // policy descs (stacked rows: desc heads_desc + i holds rows i * M ..)
   int* heads_ticket;   // or null: no fold
   // data-parallel phase 0's last level: block 0 stores the error flags (kDpFlagN) of
   // *err_word here, before the critic gradient collective (null: none)
@@ -511,11 +512,17 @@ struct SampleBwdArgs {
 // byte.  The levels run k_gemm's own workgroup body (kg_body) on the same 32x32 tiles, so the
 // results are those of the launch chain bit for bit.  The argument block lives in device
 // memory (sacmi.hip chain pool: larger than a kernel argument).
-constexpr int kChainLevels = 4;     // L7, L8, L9, L12
-constexpr int kChainBars = 4;       // barriers after L7, L8, L9, the tail
+// The critic pass has the same shape (k_chain_a, kind 1): L1 (policy fc1 on the target and
+// actor halves as two row-affine descs, critics fc1) -> L2 (+ critic fc3 dot partials, + the
+// policy heads and sample folded in: the last column tile of each 32-row block) -> L3 (target
+// critics fc1 on [s'|1|a']) -> L4 (+ target dot partials) -> L5 (critic row prologue + dh1)
+// (sac_imp.py:87-113 up to the critics' backward; L6, their weight gradients, needs every row).
+constexpr int kChainLevels = 5;     // kind 0: L7, L8, L9, L12;  kind 1: L1, L2, L3, L4, L5
+constexpr int kChainBars = 4;       // kind 0: after L7, L8, L9, the tail;  kind 1: after L1-L4
 constexpr int kChainCohorts = 8;
 constexpr int kChainGrid = 256;     // workgroups: one per CU
 struct ChainArgs {
+  int kind;
   GemmBatch lv[kChainLevels];
   SampleBwdArgs tail;         // the sample backward + dhp2 tail between L9 and L12
   const float* pa;            // the tail: dL/da partials of L9 (n_pa column blocks)
@@ -535,10 +542,12 @@ void launch_gemm(const GemmBatch& batch, hipStream_t s);
 // block, validated here.  Returns false (nothing launched) where the device cannot hold the
 // grid at once (fewer than 256 CUs, or the kernel's occupancy below one workgroup per CU)
 bool launch_chain(const ChainArgs& host, const ChainArgs* dev, tl_word* tl, hipStream_t s);
+// whether k_chain_a runs this L2 level (with the heads fold) on its 32x64 tiles
+bool chain_a_l2_ok(const GemmBatch& b);
 bool chain_supported();
 // assign k_chain's tile order to a level: 32x32 tiles, XCD-blocked with a row grid of 8
 // (cohort c = tile & 7 owns row tiles [c tm / 8, (c+1) tm / 8)); false where it does not apply
-bool chain_assign_tiles(GemmBatch& b);
+bool chain_assign_tiles(GemmBatch& b, int tn = 32);
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
 
 // select_action for one state (sacmi_act, n = 1): the policy forward as GEMVs.

@@ -1,0 +1,45 @@
+#!/bin/bash
+# One parameterised GPU session (replaces round 4's one-off gpu_r4*.sh scripts).  Steps, in
+# order, each with its own time limit; the first failure ends the session:
+#   tests    pytest -m gpu (PYTEST_ARGS; SACMI_GRAD_TABLE -> $O/grad_table.jsonl)
+#   smoke    __graft_entry__.smoke()
+#   ab       alternating bench lines without / with AB_ENV (BENCH_ARGS), AB_REPS pairs
+#   configs  bench lines of CONFIGS (default "2 3 5"), BENCH_ARGS appended
+#   dp8      the data-parallel sequence at a simulated world of 8, both optimizer forms
+# usage: STEPS="tests ab" AB_ENV="SACMI_NO_CHAIN=1" TAG=r5b bash tools/gpu_session.sh
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-session}
+mkdir -p $O
+B="python3 bench.py --no-trainer-loop --no-cpu-baseline"
+line() { python3 -c "
+import json; d=json.load(open('$1')); r=d.get('roofline') or {}
+print('$1', d['value'], d['ms_per_step'], r.get('frac'), {k: v for k, v in (r.get('sites_us') or {}).items() if 'L' in k or 'chain' in k})"; }
+for step in ${STEPS:-tests smoke configs}; do
+  case $step in
+    tests)
+      SACMI_GRAD_TABLE=$PWD/$O/grad_table.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 \
+        --timeout-method thread ${PYTEST_ARGS:-} > $O/pytest_gpu.log 2>&1
+      rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; } ;;
+    ab)
+      for r in $(seq 1 ${AB_REPS:-2}); do
+        timeout -k 10 300 $B ${BENCH_ARGS:-} > $O/a$r.json 2> $O/a$r.err || { tail $O/a$r.err; exit 1; }
+        timeout -k 10 300 env ${AB_ENV} $B ${BENCH_ARGS:-} > $O/b$r.json 2> $O/b$r.err || { tail $O/b$r.err; exit 1; }
+      done
+      for f in $O/a*.json $O/b*.json; do line $f; done ;;
+    configs)
+      for c in ${CONFIGS:-2 3 5}; do
+        timeout -k 10 400 $B --config $c ${BENCH_ARGS:-} > $O/c$c.json 2> $O/c$c.err || { tail $O/c$c.err; exit 1; }
+        line $O/c$c.json
+      done ;;
+    dp8)
+      SACMI_DP_SHARD=1 SACMI_DP_LOOPBACK_ONE_RANK=1 timeout -k 10 300 $B --force-dp --dp-sim-world 8 --steps 20 \
+        > $O/dp8_shard.json 2> $O/dp8_shard.err || { tail $O/dp8_shard.err; exit 1; }
+      SACMI_DP_SHARD=0 timeout -k 10 300 $B --force-dp --dp-sim-world 8 --steps 20 > $O/dp8_ar.json 2> $O/dp8_ar.err || { tail $O/dp8_ar.err; exit 1; }
+      line $O/dp8_shard.json; line $O/dp8_ar.json ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -15,6 +15,31 @@ import numpy as np
 SLOW = 0
 
 
+def chain_phases(name, x, words, nph):
+    """k_chain / k_chain_a: wave 0's clock at entry (0), after phase i's work (2i+1) and after
+    its barrier (2i+2), exit (9): per-phase medians (work | barrier wait) and the maxima."""
+    p0 = words - 256 * nph
+    ph = x[p0:p0 + 256 * nph].reshape(256, nph).astype(np.int64)
+    ph = ph[ph[:, 0] > 0]
+    if len(ph) == 0 or nph < 10:
+        return
+    start = int(x[0])
+    print(f"{name}: entry med {np.median(ph[:, 0] - start) * 0.01:.2f} max {np.max(ph[:, 0] - start) * 0.01:.2f} us")
+    for i in range(5):
+        a, b, c = 2 * i, 2 * i + 1, 2 * i + 2
+        if b >= nph:
+            break
+        ok = ph[:, b] > 0
+        work = (ph[ok, b] - ph[ok, a]) * 0.01
+        line = f"  phase {i}: work med {np.median(work):6.2f} max {np.max(work):6.2f}"
+        if c < nph and np.all(ph[ok, c] > 0) and i < 4:
+            wait = (ph[ok, c] - ph[ok, b]) * 0.01
+            line += f" | barrier med {np.median(wait):6.2f} max {np.max(wait):6.2f}"
+            line += f" | phase end (last) {np.max(ph[ok, c] - start) * 0.01:7.2f}"
+        print(line)
+    print(f"  exit med {np.median(ph[:, 9] - start) * 0.01:.2f} max {np.max(ph[:, 9] - start) * 0.01:.2f} us")
+
+
 def main(path):
     raw = open(path, "rb").read()
     sites, per, words, nph = struct.unpack("4q", raw[:32])
@@ -25,6 +50,9 @@ def main(path):
     for s in range(sites):
         k = 0
         x = w[s, k]
+        if x[0] != 2**64 - 1 and int(x[2]) in (21, 22):   # k_chain / k_chain_a (TL_CHAIN, TL_CHAIN_A)
+            chain_phases(names[s], x, words, nph)
+            continue
         if x[0] == 2**64 - 1 or int(x[2]) != 1:      # k_gemm only (TL_GEMM)
             continue
         p0 = words - 256 * nph                        # phase words follow the end slots
