@@ -4174,7 +4174,8 @@ bool launch_chain(const ChainArgs& h, const ChainArgs* dev, tl_word* tl, hipStre
   }
   // the configuration k_chain instantiates: fp32 32x32 k_gemm tiles (L9 with the A transform
   // and the dL/da partials), no fused Adam, no split-K / bf16 activations, rides on L12 only
-  for (int i = 0; i < kChainLevels; ++i) {
+  if (h.kind != 0) throw Error{SACMI_ESTATE, "k_chain: unknown chain kind"};
+  for (int i = 0; i < 4; ++i) {
     const GemmBatch& b = h.lv[i];
     if (b.count < 1 || b.bf16 || b.has_adam || b.heads_ticket || b.err_flags || !b.st_wt)
       throw Error{SACMI_ESTATE, "k_chain: unsupported level configuration"};
