@@ -312,9 +312,13 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
 // right behind chunk 0's loads (PIPE 1) or after the loop (PIPE 2: deep-K levels, whose
 // registers then hold the second buffer instead).  Same chunk order per wave: bitwise
 // identical sums.
+// MIDSPLIT (k_chain's phases, one pass over K: K <= 16 KSPLIT G): every group's B operand
+// (the weights) and transform weights first, then early() — the cohort barrier of the previous
+// phase — then the A operands, which the previous phase wrote: the weights' latency and the
+// setup overlap the barrier.  Otherwise early() runs before any load.
 template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
           int AXF = 0, bool BF16 = false, int PIPE = 0, bool A16 = false, int AAUX = SACMI_A_AUX,
-          class Pre, class Early = void (*)()>
+          bool MIDSPLIT = false, class Pre, class Early = void (*)()>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
                                             float* rsum, Pre&& pre, bool store_a = false,
                                             Early&& early = [] {}) {
@@ -363,7 +367,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   // fall back to full drains)
   const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
                                store_a ? (uint32_t)(((size_t)(d.M - 1) * d.ax_ld + d.K) * 4) : 0u);
-  early();
+  if constexpr (!MIDSPLIT) early();
   if constexpr (PIPE != 0) {
     static_assert(G == 1 && AXF == 0, "pipelined K loop: one chunk per stage, no A transform");
     float a1[MT][4], b1[NT][4], xw1[4];
@@ -413,10 +417,43 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       if constexpr (PIPE == 2) pre();
     }
   } else {
-  if (nmine == 0) pre();
+  if constexpr (MIDSPLIT) {
+    static_assert(PIPE == 0, "MIDSPLIT: register-direct core");
+    if (nmine == 0) {
+      early();
+      pre();
+    } else {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {   // B (and the transform weights), every group
+        const int jj = g < nmine ? g : nmine - 1;
+        const int k = SACMI_CHUNK(jj) * 16 + kl;
+        fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, b[g]);
+        if constexpr (AXF == 1) {
+          const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
+          xw[g][0] = x.x; xw[g][1] = x.y; xw[g][2] = x.z; xw[g][3] = x.w;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      early();
+#pragma unroll
+      for (int g = 0; g < G; ++g) {   // A, every group
+        const int jj = g < nmine ? g : nmine - 1;
+        const int k = SACMI_CHUNK(jj) * 16 + kl;
+        fetch_op<MT, AKC, A16, AAUX>(ra, d.lda, k, d.K, a[g]);
+        if constexpr (AXF != 1 && !AKC) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) xw[g][s] = buf_ld(rxw, (uint32_t)(k + s < d.K ? k + s : 0) * 4u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pre();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (!MIDSPLIT && nmine == 0) pre();
   for (int j = 0; j < nmine; j += G) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
+    for (int g = 0; g < G && !MIDSPLIT; ++g) {
       // unconditional (see fetch_op; a guard, even a wave-uniform one, makes the compiler
       // drain the loads at the end of the guarded block): a group past the wave's last
       // chunk re-reads that chunk and is skipped below
@@ -435,7 +472,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       __builtin_amdgcn_sched_barrier(0);
     }
     // after the LAST operand loads (vmcnt is in order)
-    if (j + G >= nmine) pre();
+    if (!MIDSPLIT && j + G >= nmine) pre();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -517,26 +554,28 @@ __device__ __forceinline__ void place_tile(const GemmDesc& d, int t, int& tr, in
 // layout dispatch (wave-uniform, once per workgroup)
 // AXK: whether this kernel instantiation carries the A-transform path (launch_gemm picks
 // the variant from the level's descs): 1 -> axk 1 descs, 0 -> none.
-// AAUX: cache-policy bits of the A-operand loads (kg_body's LDAUX)
-template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, int PIPE, int AAUX, class Pre,
-          class Early>
+// AAUX: cache-policy bits of the A-operand loads (kg_body's LDAUX); MIDSPLIT: early() is the
+// mid hook of gemm_core_l (k_chain), else it runs first
+template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, int PIPE, int AAUX, bool MIDSPLIT,
+          class Pre, class Early>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
                                           float* rsum, bool rowsum, Pre&& pre, Early&& early) {
   constexpr int AX = AAUX ? AAUX : SACMI_A_AUX;
+  constexpr bool MS = MIDSPLIT;
   if constexpr (AXK == 1) {
     if (d.axk == 1) {        // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
-      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1, BF16, 0, false, AX>(
+      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1, BF16, 0, false, AX, MS>(
           d, m0, n0, red, rsum, pre, n0 == 0 && d.ax_out != nullptr, early);
       return;
     }
   }
   if (d.a_kc) {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
-    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
+    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
   } else {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
-    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
-    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16, PIPE, false, AX>(d, m0, n0, red, rsum, pre);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
+    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
+    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
   }
 }
 
@@ -1315,9 +1354,14 @@ struct KgSmem {
 // kernel (k_chain) runs it for each work item of its cohort.  LDAUX: cache-policy bits of the
 // loads of operands another workgroup of the SAME launch produced (the A operand, the row
 // prologue's dot partials, the ReLU-mask source): sc1 (16) in k_chain, 0 in k_gemm.
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, int LDAUX>
+// MIDSPLIT (k_chain): mid() — the previous phase's cohort barrier — runs inside the K loop's
+// load burst, after the weights' loads and before the A operand's (gemm_core_l), or before a
+// return that loads nothing; every workgroup that calls the body with it reaches it once.
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, int LDAUX,
+          bool MIDSPLIT = false, class Mid = void (*)()>
 __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in,
-                                        KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>& sm) {
+                                        KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>& sm,
+                                        Mid&& mid = [] {}) {
   // The scalars that locate this workgroup's work come in ONE kernarg round trip: left to
   // the compiler, each load sat behind a branch on the previous one (timeline pointer, tile
   // count, one desc's tile_begin per loop trip, then the desc's fields as they were used),
@@ -1393,6 +1437,7 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
     if (bid < batch.total_tiles) return;
   }
 #endif
+  if (bid >= n_tiles && MIDSPLIT) mid();   // (k_chain: rides read nothing of the chain)
   if (bid >= n_tiles && bid == adam_wg) {
     // the level's scalar Adam work on a workgroup of its own, at once: its inputs (loss
     // partials, log_alpha's gradient, the scalars) come from earlier levels, and no tile's
@@ -1455,7 +1500,10 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
 #endif
   if constexpr (CORE == 0) SACMI_PHASE(batch.tl, 8);   // (diagnostic: the desc has landed)
   const int t = bid - tbeg[p];
-  if (t >= d.tiles_m * d.tiles_n) return;   // padding to a multiple of 8 blocks
+  if (t >= d.tiles_m * d.tiles_n) {   // padding to a multiple of 8 blocks
+    if constexpr (MIDSPLIT) mid();
+    return;
+  }
   int tr, tc;
   place_tile(d, t, tr, tc);
   const int m0 = tr * TMW, n0 = tc * TN;
@@ -1620,7 +1668,7 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   if constexpr (CORE == 1)
     gemm_core_stg<TM, TN, KSPLIT, MG, AXK>(d, m0, n0, ring, rsum, s_kw, rowsum, pre, batch.tl);
   else
-    gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE, LDAUX>(d, m0, n0, red, rsum, rowsum, pre, [] {});
+    gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE, LDAUX, MIDSPLIT>(d, m0, n0, red, rsum, rowsum, pre, mid);
   SACMI_PHASE(batch.tl, 2);
   SACMI_PHASE_LAST(batch.tl, 7);
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
@@ -3829,9 +3877,9 @@ struct TailSmem {
 // One unit: rows [m0, m0 + 8) x dhp2 columns [c0, c0 + 64), by the first 256 threads of the
 // workgroup (any others only join its barriers).  slab0: the unit also stores dhead.  AUX:
 // cache-policy bits of the dL/da partial loads (k_chain: sc1 — L9 wrote them in the same launch)
-template <int AUX>
+template <int AUX, class Mid = void (*)()>
 __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const SampleBwdArgs& a, int m0,
-                                          int c0, bool slab0, TailSmem& sm) {
+                                          int c0, bool slab0, TailSmem& sm, Mid&& mid = [] {}) {
   auto& s_dh = sm.s_dh;
   auto& s_w = sm.s_w;
   const int A = a.A, B = a.B, K2 = 2 * A;
@@ -3843,12 +3891,6 @@ __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const Sampl
   // 0 without an access, so no load sits behind a guard.
   const int prow = tid / A, pj = tid - prow * A, pm = m0 + prow;
   const bool own = act && tid < kTailRows * A && pm < B;
-  const rsrc_t rP = make_rsrc(pa, (uint32_t)((size_t)n_pa * B * A * 4));
-  const uint32_t pstride = (uint32_t)B * (uint32_t)A * 4u, po = (uint32_t)((own ? pm : 0) * A + pj) * 4u;
-  float t[kTailMaxPa];
-#pragma unroll
-  for (int q = 0; q < kTailMaxPa; ++q)
-    t[q] = buf_ld_aux<AUX>(rP, own && q < n_pa ? po + (uint32_t)q * pstride : 0xfffffff0u);
   const rsrc_t rC = make_rsrc(a.cache, (uint32_t)((size_t)B * 3 * A * 4));
   const rsrc_t rE = make_rsrc(a.eps, (uint32_t)((size_t)B * A * 4));
   const uint32_t co = own ? (uint32_t)(pm * 3 * A + pj) * 4u : 0xfffffff0u;
@@ -3872,6 +3914,15 @@ __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const Sampl
     const int col = c0 + cq + u;
     mk[u] = buf_ld(rH, act && m < B && col < a.H ? (uint32_t)(m * a.ldh + col) * 4u : 0xfffffff0u);
   }
+  // the dL/da partials the previous phase wrote: after mid() (k_chain's barrier; a no-op in
+  // the standalone kernel, whose loads all went out above)
+  mid();
+  const rsrc_t rP = make_rsrc(pa, (uint32_t)((size_t)n_pa * B * A * 4));
+  const uint32_t pstride = (uint32_t)B * (uint32_t)A * 4u, po = (uint32_t)((own ? pm : 0) * A + pj) * 4u;
+  float t[kTailMaxPa];
+#pragma unroll
+  for (int q = 0; q < kTailMaxPa; ++q)
+    t[q] = buf_ld_aux<AUX>(rP, own && q < n_pa ? po + (uint32_t)q * pstride : 0xfffffff0u);
   if (act) {
     for (int e = tid; e < kTailRows * 65; e += 256) (&s_dh[0][0])[e] = 0.f;
 #pragma unroll
@@ -3948,29 +3999,29 @@ void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, h
 // each phase waits only for its own cohort's previous phase.
 constexpr long long kChainSpinTicks = 5000000;   // 50 ms of the 100 MHz clock: a barrier timeout
 
-// Cohort barrier (cdna_hip_programming.md §6 Guideline 16, MI355X_MICROARCH.md hand-off table
-// row 1): every wave's write-through stores acknowledged (vmcnt(0)), a workgroup barrier, ONE
-// agent-scope arrival; the last arriver resets the count and bumps the generation the others
-// poll (relaxed sc1 loads + s_sleep); every later load of the handed-off bytes is an sc1 load
-// (kg_body / tail_unit with LDAUX = sc1).  The generation is read before arriving (its load
-// has returned: vmcnt(0)), so the waiters compare against the value before this round.
-// wait = false: arrive only (the workgroup's next work reads nothing of this phase).  A
-// bounded spin: a timeout sets ERR_CHAIN_TIMEOUT (the host reports a device error) and the
-// workgroup runs on — void outputs, never a hung grid.
-__device__ __forceinline__ void chain_bar(int* cnt, int* gen, int n, int* err, bool wait) {
+// Cohort barriers (cdna_hip_programming.md §6 Guideline 16, MI355X_MICROARCH.md hand-off table
+// row 1).  Per cohort, 128-byte strided words: [0, kChainBars) the arrivals at barrier b,
+// kChainBars the launch ticket — monotonic and wrapping: every launch adds exactly `nmem` to
+// each, so launch e's barrier b is complete once its word reaches (e + 1) nmem, e read from the
+// ticket each workgroup draws at its start (nothing is ever reset).
+//   chain_phase_end  every wave's write-through stores acknowledged (vmcnt(0)), then a
+//                    workgroup barrier — before the workgroup's arrival is signalled
+//   chain_arrive     ONE agent-scope add (non-returning: issued behind the next phase's weight
+//                    loads, it waits for none of them), then — wait — a poll (relaxed sc1 loads
+//                    + s_sleep) until the cohort has arrived, then a workgroup barrier; every
+//                    later load of handed-off bytes is an sc1 load (kg_body / tail_unit with
+//                    LDAUX = sc1).  A bounded spin: a timeout sets ERR_CHAIN_TIMEOUT (the host
+//                    reports a device error) and the workgroup runs on — void outputs, no hang.
+__device__ __forceinline__ void chain_phase_end() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+}
+__device__ __forceinline__ void chain_arrive(int* cnt, int target, bool wait, int* err) {
   if (threadIdx.x == 0) {
-    const int g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == n - 1) {
-      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(gen, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (wait) {
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wait) {
       const unsigned long long t0 = wall_clock64();
-      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+      while ((int)((unsigned)__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (unsigned)target) < 0) {
         __builtin_amdgcn_s_sleep(1);
         if ((long long)(wall_clock64() - t0) > kChainSpinTicks) {
           __hip_atomic_fetch_or(err, (int)ERR_CHAIN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3981,6 +4032,12 @@ __device__ __forceinline__ void chain_bar(int* cnt, int* gen, int n, int* err, b
   }
   __syncthreads();
 }
+// the launch's completion target of every barrier word (thread 0 only: the others never wait)
+__device__ __forceinline__ int chain_target(int* ticket, int nmem) {
+  if (threadIdx.x != 0) return 0;
+  const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (int)(((unsigned)t & ~(unsigned)(nmem - 1)) + (unsigned)nmem);
+}
 
 using ChainKgA = KgSmem<32, 32, 16, 2, 1, false, 0, false, 0>;   // L7, L8, L12 (+ rides)
 using ChainKgB = KgSmem<32, 32, 16, 2, 1, false, 1, false, 0>;   // L9 (row prologue, dL/da)
@@ -3990,68 +4047,89 @@ union ChainSmem {
   TailSmem t;
 };
 
+// The argument block is read through the CONSTANT address space: invariant scalar loads, as
+// k_gemm's kernel argument (a generic pointer's loads behind the barriers' memory clobbers
+// would be vector loads into VGPRs); the generic pointer handed to kg_body is the cast of it,
+// which InferAddressSpaces folds back.  Each phase reads it through an opaque copy, so no
+// phase's argument loads are hoisted into an earlier one (registers held across it: spills).
+typedef __attribute__((address_space(4))) const ChainArgs ConstChainArgs;
+__device__ __forceinline__ const ChainArgs* chain_args(const ChainArgs* ca) {
+  ConstChainArgs* p4 = (ConstChainArgs*)ca;
+  asm volatile("" : "+s"(p4));
+  return (const ChainArgs*)p4;
+}
+
+// Each phase's weights (and descriptor setup) go out BEFORE the cohort barrier on the
+// previous phase (kg_body / tail_unit MIDSPLIT: the barrier is their mid() hook), so their
+// latency overlaps the wait.  (diagnostic builds, SACMI_DIAG_PHASES: wave 0's clock at entry
+// (slot 0), at the end of phase i (slot i + 1) and right after barrier b's wait (slot 6 + b);
+// tools/phase_dump.py)
 __global__ __launch_bounds__(1024, 4) void k_chain(const ChainArgs* __restrict__ ca, tl_word* tl) {
   const TlMark tl_mark(tl, TL_CHAIN);
   __shared__ ChainSmem sm;
-  const int c = blockIdx.x & (kChainCohorts - 1);
-  const int nmem = gridDim.x / kChainCohorts;
-  int* const sync = ca->sync + c * kChainBars * 32;
-  int* const err = ca->err;
-  auto bar = [&](int b, bool wait) { chain_bar(sync + b * 32, sync + b * 32 + 1, nmem, err, wait); };
-  // each phase reads its arguments through a pointer the compiler cannot see through
-  // (opaque()): no phase's argument loads are hoisted into an earlier phase, where they
-  // would sit in registers across it (SGPR / VGPR spills)
-  // The block is read through the CONSTANT address space: invariant scalar loads, as
-  // k_gemm's kernel argument (a generic pointer's loads behind the barriers' memory clobbers
-  // would be vector loads into VGPRs); the generic pointer handed to kg_body is the cast of
-  // it, which InferAddressSpaces folds back.
-  typedef __attribute__((address_space(4))) const ChainArgs ConstChainArgs;
-  auto opaque = [&]() {
-    ConstChainArgs* p4 = (ConstChainArgs*)ca;
-    asm volatile("" : "+s"(p4));
-    return (const ChainArgs*)p4;
-  };
-  // (diagnostic builds, SACMI_DIAG_PHASES: wave 0's clock at every phase boundary — slot 2i+1
-  // after phase i's work, 2i+2 after its barrier; tools/phase_dump.py)
   SACMI_PHASE(tl, 0);
-  // L7 (updated critics fc1 on [s|1|a~]), L8 (fc2 + fc3 dot partials)
-#pragma unroll 1
-  for (int i = 0; i < 2; ++i) {
-    const GemmBatch& b = opaque()->lv[i];
-    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.a);
-    SACMI_PHASE(tl, 2 * i + 1);
-    bar(i, true);
-    SACMI_PHASE(tl, 2 * i + 2);
+  const int c = blockIdx.x & (kChainCohorts - 1), bid = blockIdx.x;
+  const int nmem = gridDim.x / kChainCohorts;
+  int* const sync = chain_args(ca)->sync + c * (kChainBars + 1) * 32;
+  int* const err = chain_args(ca)->err;
+  const int target = chain_target(sync + kChainBars * 32, nmem);
+  auto arrive = [&](int b, bool wait) {
+    chain_arrive(sync + b * 32, target, wait, err);
+    SACMI_PHASE(tl, 6 + b);
+  };
+  // L7 (updated critics fc1 on [s|1|a~])
+  {
+    const GemmBatch& b = chain_args(ca)->lv[0];
+    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, bid, sm.a);
+    chain_phase_end();
+    SACMI_PHASE(tl, 1);
+  }
+  // L8 (fc2 + fc3 dot partials): barrier 0 behind its weight loads
+  {
+    const GemmBatch& b = chain_args(ca)->lv[1];
+    if (bid < b.total_tiles)
+      kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, [&] { arrive(0, true); });
+    else
+      arrive(0, false);
+    chain_phase_end();
+    SACMI_PHASE(tl, 2);
   }
   // L9: the actor row prologue + dha1 + the dL/da partials
   {
-    const GemmBatch& b = opaque()->lv[2];
-    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1>(b, blockIdx.x, sm.b);
-    SACMI_PHASE(tl, 5);
-    bar(2, true);
-    SACMI_PHASE(tl, 6);
+    const GemmBatch& b = chain_args(ca)->lv[2];
+    if (bid < b.total_tiles)
+      kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1, true>(b, bid, sm.b, [&] { arrive(1, true); });
+    else
+      arrive(1, false);
+    chain_phase_end();
+    SACMI_PHASE(tl, 3);
   }
   // the sample-backward tail: the cohort's 8-row groups x 64-column dhp2 slabs
   {
-    const ChainArgs* q = opaque();
+    const ChainArgs* q = chain_args(ca);
     const int ng = q->tail_groups, units = ng * q->tail_slabs;
-    const int j = blockIdx.x / kChainCohorts;
+    const int j = bid / kChainCohorts;
     if (j < units) {
       const int g = j % ng, slab = j / ng;
       tail_unit<kLdSc1>(q->pa, q->n_pa, q->tail, c * q->rows_per_cohort + g * kTailRows,
-                        slab * kTailCols, slab == 0, sm.t);
+                        slab * kTailCols, slab == 0, sm.t, [&] { arrive(2, true); });
+    } else {
+      arrive(2, false);
     }
-    SACMI_PHASE(tl, 7);
+    chain_phase_end();
+    SACMI_PHASE(tl, 4);
   }
   // L12 (dhp1) + the level's rides (the next update's sampler, Polyak): a workgroup whose
-  // items are all rides reads nothing of the chain — it arrives and goes on
+  // item is a ride reads nothing of the chain — it arrives and goes on
   {
-    const GemmBatch& b = opaque()->lv[3];
-    bar(3, (int)blockIdx.x < b.total_tiles);
-    SACMI_PHASE(tl, 8);
+    const GemmBatch& b = chain_args(ca)->lv[3];
     const int items = b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
-    if ((int)blockIdx.x < items) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.a);
-    SACMI_PHASE(tl, 9);
+    const bool tile = bid < b.total_tiles;
+    if (bid < items)
+      kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, [&] { arrive(3, tile); });
+    else
+      arrive(3, false);
+    SACMI_PHASE(tl, 5);
   }
 }
 
@@ -4067,43 +4145,52 @@ union ChainSmemA {
 __global__ __launch_bounds__(1024, 4) void k_chain_a(const ChainArgs* __restrict__ ca, tl_word* tl) {
   const TlMark tl_mark(tl, TL_CHAIN_A);
   __shared__ ChainSmemA sm;
-  const int c = blockIdx.x & (kChainCohorts - 1);
-  const int nmem = gridDim.x / kChainCohorts;
-  typedef __attribute__((address_space(4))) const ChainArgs ConstChainArgs;
-  auto opaque = [&]() {   // (see k_chain)
-    ConstChainArgs* p4 = (ConstChainArgs*)ca;
-    asm volatile("" : "+s"(p4));
-    return (const ChainArgs*)p4;
-  };
-  auto bar = [&](int b) {
-    const ChainArgs* q = opaque();
-    int* const sync = q->sync + c * kChainBars * 32;
-    chain_bar(sync + b * 32, sync + b * 32 + 1, nmem, q->err, true);
-  };
   SACMI_PHASE(tl, 0);   // (diagnostic builds: as k_chain's)
-  // L1, L2 (+ the heads): 32x64 tiles
-#pragma unroll 1
-  for (int i = 0; i < 2; ++i) {
-    const GemmBatch& b = opaque()->lv[i];
-    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.w);
-    SACMI_PHASE(tl, 2 * i + 1);
-    bar(i);
-    SACMI_PHASE(tl, 2 * i + 2);
+  const int c = blockIdx.x & (kChainCohorts - 1), bid = blockIdx.x;
+  const int nmem = gridDim.x / kChainCohorts;
+  int* const sync = chain_args(ca)->sync + c * (kChainBars + 1) * 32;
+  int* const err = chain_args(ca)->err;
+  const int target = chain_target(sync + kChainBars * 32, nmem);
+  auto arrive = [&](int b, bool wait) {
+    chain_arrive(sync + b * 32, target, wait, err);
+    SACMI_PHASE(tl, 6 + b);
+  };
+  // L1: 32x64 tiles
+  {
+    const GemmBatch& b = chain_args(ca)->lv[0];
+    if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, bid, sm.w);
+    chain_phase_end();
+    SACMI_PHASE(tl, 1);
+  }
+  // L2 (+ the heads): 32x64 tiles, barrier 0 behind its weight loads
+  {
+    const GemmBatch& b = chain_args(ca)->lv[1];
+    if (bid < b.total_tiles)
+      kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.w, [&] { arrive(0, true); });
+    else
+      arrive(0, false);
+    chain_phase_end();
+    SACMI_PHASE(tl, 2);
   }
   // L3, L4 (target critics): 32x32 tiles
 #pragma unroll 1
   for (int i = 2; i < 4; ++i) {
-    const GemmBatch& b = opaque()->lv[i];
-    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, blockIdx.x, sm.a);
-    SACMI_PHASE(tl, 2 * i + 1);
-    bar(i);
-    SACMI_PHASE(tl, 2 * i + 2);
+    const GemmBatch& b = chain_args(ca)->lv[i];
+    if (bid < b.total_tiles)
+      kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, [&] { arrive(i - 1, true); });
+    else
+      arrive(i - 1, false);
+    chain_phase_end();
+    SACMI_PHASE(tl, i + 1);
   }
   // L5: the critic row prologue (targets, MSE gradients, loss partials) + dh1
   {
-    const GemmBatch& b = opaque()->lv[4];
-    if ((int)blockIdx.x < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1>(b, blockIdx.x, sm.b);
-    SACMI_PHASE(tl, 9);
+    const GemmBatch& b = chain_args(ca)->lv[4];
+    if (bid < b.total_tiles)
+      kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1, true>(b, bid, sm.b, [&] { arrive(3, true); });
+    else
+      arrive(3, false);
+    SACMI_PHASE(tl, 5);
   }
 }
 
@@ -4164,6 +4251,7 @@ bool launch_chain(const ChainArgs& h, const ChainArgs* dev, tl_word* tl, hipStre
         if (d.axk != (i == 4 ? 1 : 0) || d.epi >= EPI_ADAM || d.a16 || d.b16 || d.c16 || d.x16 || d.pa_out ||
             d.xcd_gr != kChainCohorts || d.tiles_m % kChainCohorts || d.M != h.rows_per_cohort * kChainCohorts)
           throw Error{SACMI_ESTATE, "k_chain_a: unsupported GEMM in a chain level"};
+        if (d.K > kChainMaxK) throw Error{SACMI_ESTATE, "k_chain_a: K beyond one pass"};
         if (d.tiles_n * (i < 2 ? 64 : 32) < d.N || (i < 2 && d.tiles_n * 32 >= d.N && d.N > 32))
           throw Error{SACMI_ESTATE, "k_chain_a: a level's tiles differ from the kernel's"};
       }
@@ -4189,6 +4277,7 @@ bool launch_chain(const ChainArgs& h, const ChainArgs* dev, tl_word* tl, hipStre
         throw Error{SACMI_ESTATE, "k_chain: unsupported GEMM in a chain level"};
       if (d.M != h.rows_per_cohort * kChainCohorts)
         throw Error{SACMI_ESTATE, "k_chain: a level's rows differ from the chain's batch"};
+      if (d.K > kChainMaxK) throw Error{SACMI_ESTATE, "k_chain: K beyond one pass"};
     }
   }
   const SampleBwdArgs& a = h.tail;

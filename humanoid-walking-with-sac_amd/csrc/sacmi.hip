@@ -276,7 +276,7 @@ struct sacmi_ctx {
   // that graph's first launch.  Blocks are immutable and deduplicated by content.
   static constexpr int kChainSlots = 48;
   bool own_capture = false;
-  bool chain_on = true;                      // SACMI_NO_CHAIN at creation: off
+  bool chain_on = false;                     // SACMI_CHAIN at creation: on
   sacmi::DevBuf<unsigned char> chain_pool;   // kChainSlots x sizeof(ChainArgs)
   std::vector<std::vector<unsigned char>> chain_host;
   size_t chain_uploaded = 0;                 // slots [0, chain_uploaded) are on the device
@@ -974,8 +974,10 @@ static AdamArgs dp_adam_args(sacmi_ctx* c, bool critic, int B, float grad_scale,
 // (nothing enqueued) where it does not apply: the caller launches the levels one by one.
 // SACMI_NO_CHAIN at creation switches it off (the tests' A/B).
 static bool chain_batch_ok(const sacmi_ctx* c, int B) {
-  return c->chain_on && !c->bf16 && c->nh == 2 && B == kChainCohorts * 32 && c->H % 32 == 0 && c->H <= 512 &&
-         !std::getenv("SACMI_NO_DLDA_FOLD") && chain_supported();
+  // (every chain level is one pass over K: K <= kChainMaxK — the critics' fc1 K is S + 1 + A)
+  return c->chain_on && !c->bf16 && c->nh == 2 && B == kChainCohorts * 32 && c->H % 32 == 0 &&
+         c->H <= kChainMaxK && c->S + 1 + c->A <= kChainMaxK && !std::getenv("SACMI_NO_DLDA_FOLD") &&
+         chain_supported();
 }
 // kind 0: the actor pass (L7, L8, L9, the tail `sb`, L12); kind 1: the critic pass (L1 and
 // L2 on 32x64 tiles, L2 carrying the policy heads fold, L3, L4, L5).  (Site-isolation
@@ -1916,7 +1918,10 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
     alloc_all(c.get());
     c->ring_slots = 4096;
     c->ring.alloc((size_t)c->ring_slots * 3);
-    c->chain_on = std::getenv("SACMI_NO_CHAIN") == nullptr;
+    // the persistent chains are opt-in: measured slower than the launch sequence (DESIGN.md
+    // §12a: each cohort barrier + write-through hand-off costs more than a graph's kernel
+    // boundary at these tile sizes)
+    c->chain_on = std::getenv("SACMI_CHAIN") != nullptr && std::getenv("SACMI_NO_CHAIN") == nullptr;
     if (c->chain_on) {
       c->chain_pool.alloc((size_t)sacmi_ctx::kChainSlots * sizeof(ChainArgs));
       c->chain_sync.alloc(kChainSyncInts);

@@ -530,10 +530,11 @@ struct ChainArgs {
   int rows_per_cohort;        // B / 8
   int tail_groups;            // 8-row groups per cohort (rows_per_cohort / 8)
   int tail_slabs;             // 64-column slabs of dhp2 (ceil(H / 64))
-  int* sync;                  // [cohort][barrier] x {count, generation}, 128-byte strided
+  int* sync;                  // [cohort][barrier, ticket], 128-byte strided (k_chain's barriers)
   int* err;                   // DevScalars::err (ERR_CHAIN_TIMEOUT)
 };
-constexpr int kChainSyncInts = kChainCohorts * kChainBars * 32;
+constexpr int kChainMaxK = 16 * 16 * 2;   // one K pass of the chain bodies (16 waves x 2 groups x 16)
+constexpr int kChainSyncInts = kChainCohorts * (kChainBars + 1) * 32;   // + a launch ticket per cohort
 
 // ---------------------------------------------------------------------------
 // launchers (kernels.hip)

@@ -1229,7 +1229,7 @@ def test_chain_matches_launch_sequence(auto_entropy):
     """The actor pass of a batch-256 fused update as ONE persistent launch (k_chain: L7 ->
     L8 -> L9 -> sample-backward tail -> L12 with cohort barriers, the next update's sampler and
     Polyak riding in its L12 phase) against the same levels as five launches
-    (SACMI_NO_CHAIN=1): the same workgroup bodies on the same tiles, so every loss, parameter,
+    (the default; the chain is opt-in, SACMI_CHAIN=1): the same workgroup bodies on the same tiles, so every loss, parameter,
     gradient, Adam moment, target and the MT stream are bit-identical — over an update with
     injected indices and noise, device-sampled single updates (drawn ahead) and a 5-update
     launch (rides into the other batch set)."""
@@ -1244,12 +1244,12 @@ def test_chain_matches_launch_sequence(auto_entropy):
     key = (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32)
     res = []
     for chain in (True, False):
-        if not chain:
-            os.environ["SACMI_NO_CHAIN"] = "1"
+        if chain:
+            os.environ["SACMI_CHAIN"] = "1"
         try:
             ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]))
         finally:
-            os.environ.pop("SACMI_NO_CHAIN", None)
+            os.environ.pop("SACMI_CHAIN", None)
         assert ctx.chained(B) == chain
         load_params(ctx, params)
         ctx.push(*rows)

@@ -6,7 +6,7 @@
 #   ab       alternating bench lines without / with AB_ENV (BENCH_ARGS), AB_REPS pairs
 #   configs  bench lines of CONFIGS (default "2 3 5"), BENCH_ARGS appended
 #   dp8      the data-parallel sequence at a simulated world of 8, both optimizer forms
-# usage: STEPS="tests ab" AB_ENV="SACMI_NO_CHAIN=1" TAG=r5b bash tools/gpu_session.sh
+# usage: STEPS="tests ab" AB_ENV="SACMI_CHAIN=1" TAG=r5b bash tools/gpu_session.sh
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -21,7 +21,7 @@ for step in ${STEPS:-tests smoke configs}; do
     tests)
       SACMI_GRAD_TABLE=$PWD/$O/grad_table.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 \
         --timeout-method thread ${PYTEST_ARGS:-} > $O/pytest_gpu.log 2>&1
-      rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc ;;
+      rc=$?; tail -3 $O/pytest_gpu.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; } ;;
     ab)
@@ -43,3 +43,4 @@ for step in ${STEPS:-tests smoke configs}; do
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
+exit 0

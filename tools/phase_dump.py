@@ -16,28 +16,27 @@ SLOW = 0
 
 
 def chain_phases(name, x, words, nph):
-    """k_chain / k_chain_a: wave 0's clock at entry (0), after phase i's work (2i+1) and after
-    its barrier (2i+2), exit (9): per-phase medians (work | barrier wait) and the maxima."""
+    """k_chain / k_chain_a: wave 0's clock at entry (slot 0), at the end of phase i (slot i+1)
+    and right after the wait of barrier b (slot 6+b, the barrier that opens phase b+1, inside
+    its body: the weights' loads went out before it).  Per phase: the medians / maxima of
+    [phase start -> barrier passed] (weights + wait) and [barrier passed -> phase end]."""
     p0 = words - 256 * nph
     ph = x[p0:p0 + 256 * nph].reshape(256, nph).astype(np.int64)
     ph = ph[ph[:, 0] > 0]
     if len(ph) == 0 or nph < 10:
         return
     start = int(x[0])
-    print(f"{name}: entry med {np.median(ph[:, 0] - start) * 0.01:.2f} max {np.max(ph[:, 0] - start) * 0.01:.2f} us")
-    for i in range(5):
-        a, b, c = 2 * i, 2 * i + 1, 2 * i + 2
-        if b >= nph:
-            break
-        ok = ph[:, b] > 0
-        work = (ph[ok, b] - ph[ok, a]) * 0.01
-        line = f"  phase {i}: work med {np.median(work):6.2f} max {np.max(work):6.2f}"
-        if c < nph and np.all(ph[ok, c] > 0) and i < 4:
-            wait = (ph[ok, c] - ph[ok, b]) * 0.01
-            line += f" | barrier med {np.median(wait):6.2f} max {np.max(wait):6.2f}"
-            line += f" | phase end (last) {np.max(ph[ok, c] - start) * 0.01:7.2f}"
-        print(line)
-    print(f"  exit med {np.median(ph[:, 9] - start) * 0.01:.2f} max {np.max(ph[:, 9] - start) * 0.01:.2f} us")
+    us = lambda v: v * 0.01
+    print(f"{name}: entry med {us(np.median(ph[:, 0] - start)):.2f} max {us(np.max(ph[:, 0] - start)):.2f} us")
+    w0 = us(ph[:, 1] - ph[:, 0])
+    print(f"  phase 0: work med {np.median(w0):6.2f} max {np.max(w0):6.2f} | end (last) {us(np.max(ph[:, 1] - start)):7.2f}")
+    for i in range(1, 5):
+        pre = us(ph[:, 5 + i] - ph[:, i])
+        post = us(ph[:, i + 1] - ph[:, 5 + i])
+        print(f"  phase {i}: to barrier med {np.median(pre):6.2f} max {np.max(pre):6.2f} | "
+              f"after med {np.median(post):6.2f} max {np.max(post):6.2f} | "
+              f"barrier passed (last) {us(np.max(ph[:, 5 + i] - start)):7.2f} | end (last) {us(np.max(ph[:, i + 1] - start)):7.2f}")
+    print(f"  exit med {us(np.median(ph[:, 5] - start)):.2f} max {us(np.max(ph[:, 5] - start)):.2f} us")
 
 
 def main(path):
