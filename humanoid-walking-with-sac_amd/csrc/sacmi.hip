@@ -726,11 +726,15 @@ static void validate_batch(const GemmBatch& b) {
   }
 }
 
-// the policy heads folded into the last policy hidden layer's level where launch_gemm can
+// the policy heads folded into the last policy hidden layer's level where launch_gemm can —
+// opt-in (SACMI_HEADS_FOLD=1): the fold runs the heads behind the level's last tile of each
+// row block, serially, and measured slower than the separate heads launch (config 2: L2
+// 11.1 -> 20.1 us with the fold, 8,850 -> 8,669 steps/s; profiles/r05/heads_fold_ab).
 // (read per enqueue: tests switch it between contexts)
 static bool heads_fold_wanted() {
-  const char* e = std::getenv("SACMI_NO_HEADS_FOLD");
-  return !(e && std::atoi(e) != 0);
+  const char* e = std::getenv("SACMI_HEADS_FOLD");
+  const char* n = std::getenv("SACMI_NO_HEADS_FOLD");
+  return e && std::atoi(e) != 0 && !(n && std::atoi(n) != 0);
 }
 
 struct Level {

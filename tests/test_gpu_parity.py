@@ -986,7 +986,7 @@ def test_dlda_fold_matches_unfolded(B, H):
 def test_heads_fold_matches_separate_kernel(auto_entropy):
     """The policy heads + sample folded into the last hidden layer's level (the last column
     tile of each 32-row block runs them, config-2 shapes) vs the separate heads kernel
-    (SACMI_NO_HEADS_FOLD=1): the heads' outputs are the same sums in the same order, so with
+    (the default; the fold is opt-in, SACMI_HEADS_FOLD=1): the heads' outputs are the same sums in the same order, so with
     a fixed alpha every loss and parameter is bit-identical over single, injected-noise and
     multi-update launches; with alpha tuning only the log-prob partials are grouped by 32
     rows instead of 16 — one update then leaves every network bit-identical and log_alpha
@@ -1002,8 +1002,8 @@ def test_heads_fold_matches_separate_kernel(auto_entropy):
     key = (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32)
     res = []
     for fold in (True, False):
-        if not fold:
-            os.environ["SACMI_NO_HEADS_FOLD"] = "1"
+        if fold:
+            os.environ["SACMI_HEADS_FOLD"] = "1"
         try:
             ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]))
             load_params(ctx, params)
@@ -1018,7 +1018,7 @@ def test_heads_fold_matches_separate_kernel(auto_entropy):
             res.append((out, st, ctx_grads(ctx, cfg)))
             ctx.close()
         finally:
-            os.environ.pop("SACMI_NO_HEADS_FOLD", None)
+            os.environ.pop("SACMI_HEADS_FOLD", None)
     (oa, sa, ga), (ob, sb, gb) = res
     for a, b in zip(oa, ob):
         assert np.array_equal(a, b)
@@ -1224,15 +1224,16 @@ def test_dp_sharded_moments_read_guard():
     ctx.close()
 
 
-@pytest.mark.parametrize("auto_entropy", [True, False])
-def test_chain_matches_launch_sequence(auto_entropy):
+@pytest.mark.parametrize("auto_entropy,fold", [(True, False), (False, False), (True, True)])
+def test_chain_matches_launch_sequence(auto_entropy, fold):
     """The actor pass of a batch-256 fused update as ONE persistent launch (k_chain: L7 ->
     L8 -> L9 -> sample-backward tail -> L12 with cohort barriers, the next update's sampler and
-    Polyak riding in its L12 phase) against the same levels as five launches
-    (the default; the chain is opt-in, SACMI_CHAIN=1): the same workgroup bodies on the same tiles, so every loss, parameter,
-    gradient, Adam moment, target and the MT stream are bit-identical — over an update with
-    injected indices and noise, device-sampled single updates (drawn ahead) and a 5-update
-    launch (rides into the other batch set)."""
+    Polyak riding in its L12 phase) — with the heads fold on, the critic pass too (k_chain_a:
+    L1 -> L2 + heads -> L3 -> L4 -> L5) — against the same levels as launches (the default;
+    the chains are opt-in, SACMI_CHAIN=1): the same workgroup bodies on the same tiles, so
+    every loss, parameter, gradient, Adam moment, target and the MT stream are bit-identical —
+    over an update with injected indices and noise, device-sampled single updates (drawn
+    ahead) and a 5-update launch (rides into the other batch set)."""
     cfg = SacConfig(376, 17, 512, automatic_entropy_tuning=auto_entropy)
     B = 256
     params = init_params(cfg, 161, bias_scale=0.02)
@@ -1244,19 +1245,20 @@ def test_chain_matches_launch_sequence(auto_entropy):
     key = (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32)
     res = []
     for chain in (True, False):
-        if chain:
-            os.environ["SACMI_CHAIN"] = "1"
+        env = dict({"SACMI_HEADS_FOLD": "1"} if fold else {}, **({"SACMI_CHAIN": "1"} if chain else {}))
+        os.environ.update(env)
         try:
             ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]))
+            assert ctx.chained(B) == chain
+            load_params(ctx, params)
+            ctx.push(*rows)
+            ctx.set_mt(0, key, 624)
+            out = [ctx.step(B, idx=idx, eps1=e1, eps2=e2), ctx.step(B), ctx.step(B)]
+            ctx.step_many_async(B, 5)
+            out.append(ctx.fetch_losses(5).ravel())
         finally:
-            os.environ.pop("SACMI_CHAIN", None)
-        assert ctx.chained(B) == chain
-        load_params(ctx, params)
-        ctx.push(*rows)
-        ctx.set_mt(0, key, 624)
-        out = [ctx.step(B, idx=idx, eps1=e1, eps2=e2), ctx.step(B), ctx.step(B)]
-        ctx.step_many_async(B, 5)
-        out.append(ctx.fetch_losses(5).ravel())
+            for k in env:
+                os.environ.pop(k, None)
         st = ctx_state(ctx, cfg)
         mom = {f"{n}.{slot}.{k}": v for n in ("policy", "q1", "q2") for slot in ("m", "v")
                for k, v in ctx.get_net(n, slot).items()}
