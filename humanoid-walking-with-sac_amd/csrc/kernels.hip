@@ -423,17 +423,22 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       early();
       pre();
     } else {
+      auto bload = [&]() {
 #pragma unroll
-      for (int g = 0; g < G; ++g) {   // B (and the transform weights), every group
-        const int jj = g < nmine ? g : nmine - 1;
-        const int k = SACMI_CHUNK(jj) * 16 + kl;
-        fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, b[g]);
-        if constexpr (AXF == 1) {
-          const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
-          xw[g][0] = x.x; xw[g][1] = x.y; xw[g][2] = x.z; xw[g][3] = x.w;
+        for (int g = 0; g < G; ++g) {   // B (and the transform weights), every group
+          const int jj = g < nmine ? g : nmine - 1;
+          const int k = SACMI_CHUNK(jj) * 16 + kl;
+          fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, b[g]);
+          if constexpr (AXF == 1) {
+            const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
+            xw[g][0] = x.x; xw[g][1] = x.y; xw[g][2] = x.z; xw[g][3] = x.w;
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      };
+      // (wave 0 polls the barrier: its weight loads deferred past the wait measured slower,
+      // config 2 chain 42.4 -> 44.5 us — DESIGN.md §12a)
+      bload();
       early();
 #pragma unroll
       for (int g = 0; g < G; ++g) {   // A, every group
@@ -1354,14 +1359,16 @@ struct KgSmem {
 // kernel (k_chain) runs it for each work item of its cohort.  LDAUX: cache-policy bits of the
 // loads of operands another workgroup of the SAME launch produced (the A operand, the row
 // prologue's dot partials, the ReLU-mask source): sc1 (16) in k_chain, 0 in k_gemm.
-// MIDSPLIT (k_chain): mid() — the previous phase's cohort barrier — runs inside the K loop's
-// load burst, after the weights' loads and before the A operand's (gemm_core_l), or before a
-// return that loads nothing; every workgroup that calls the body with it reaches it once.
+// MIDSPLIT (k_chain): mid (ChainWait) — the previous phase's cohort barrier — issues its first
+// poll at entry (mid.issue()) and waits (mid()) inside the K loop's load burst, after the
+// weights' loads and before the A operand's (gemm_core_l), or before a return that loads
+// nothing; every workgroup that calls the body with it reaches both once.
 template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, int LDAUX,
           bool MIDSPLIT = false, class Mid = void (*)()>
 __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in,
                                         KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>& sm,
                                         Mid&& mid = [] {}) {
+  if constexpr (MIDSPLIT) mid.issue();   // (k_chain: the barrier's first poll, ahead of every load)
   // The scalars that locate this workgroup's work come in ONE kernarg round trip: left to
   // the compiler, each load sat behind a branch on the previous one (timeline pointer, tile
   // count, one desc's tile_begin per loop trip, then the desc's fields as they were used),
@@ -3877,9 +3884,10 @@ struct TailSmem {
 // One unit: rows [m0, m0 + 8) x dhp2 columns [c0, c0 + 64), by the first 256 threads of the
 // workgroup (any others only join its barriers).  slab0: the unit also stores dhead.  AUX:
 // cache-policy bits of the dL/da partial loads (k_chain: sc1 — L9 wrote them in the same launch)
-template <int AUX, class Mid = void (*)()>
+template <int AUX, bool MIDSPLIT = false, class Mid = void (*)()>
 __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const SampleBwdArgs& a, int m0,
                                           int c0, bool slab0, TailSmem& sm, Mid&& mid = [] {}) {
+  if constexpr (MIDSPLIT) mid.issue();   // (k_chain: the barrier's first poll, as kg_body's)
   auto& s_dh = sm.s_dh;
   auto& s_w = sm.s_w;
   const int A = a.A, B = a.B, K2 = 2 * A;
@@ -3894,28 +3902,31 @@ __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const Sampl
   const rsrc_t rC = make_rsrc(a.cache, (uint32_t)((size_t)B * 3 * A * 4));
   const rsrc_t rE = make_rsrc(a.eps, (uint32_t)((size_t)B * A * 4));
   const uint32_t co = own ? (uint32_t)(pm * 3 * A + pj) * 4u : 0xfffffff0u;
-  const float omy2 = buf_ld(rC, co), ls_raw = buf_ld(rC, co + (uint32_t)A * 4u),
-              y = buf_ld(rC, co + (uint32_t)(2 * A) * 4u);
-  const float eps = buf_ld(rE, own ? (uint32_t)(pm * A + pj) * 4u : 0xfffffff0u);
   constexpr int WPT = 64 * kTailCols / 256;       // Whead slab elements per thread (k < 64)
   const rsrc_t rW = make_rsrc(a.Wh, (uint32_t)(((size_t)(K2 - 1) * a.ldw + a.H) * 4));
-  float wv[WPT];
-#pragma unroll
-  for (int q = 0; q < WPT; ++q) {
-    const int e = tid + q * 256, k = e / kTailCols, col = c0 + (e - k * kTailCols);
-    wv[q] = buf_ld(rW, act && k < K2 && col < a.H ? (uint32_t)(k * a.ldw + col) * 4u : 0xfffffff0u);
-  }
   // the dhp2 thread layout: row tid / 32 (8 rows), 2 consecutive slab columns
   const int row = act ? tid >> 5 : 0, cq = (tid & 31) * 2, m = m0 + row;
   const rsrc_t rH = make_rsrc(a.hp2, (uint32_t)(((size_t)(B - 1) * a.ldh + a.H) * 4));
-  float mk[2];
+  float omy2, ls_raw, y, eps, wv[WPT], mk[2];
+  auto preload = [&]() {
+    omy2 = buf_ld(rC, co);
+    ls_raw = buf_ld(rC, co + (uint32_t)A * 4u);
+    y = buf_ld(rC, co + (uint32_t)(2 * A) * 4u);
+    eps = buf_ld(rE, own ? (uint32_t)(pm * A + pj) * 4u : 0xfffffff0u);
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int col = c0 + cq + u;
-    mk[u] = buf_ld(rH, act && m < B && col < a.H ? (uint32_t)(m * a.ldh + col) * 4u : 0xfffffff0u);
-  }
+    for (int q = 0; q < WPT; ++q) {
+      const int e = tid + q * 256, k = e / kTailCols, col = c0 + (e - k * kTailCols);
+      wv[q] = buf_ld(rW, act && k < K2 && col < a.H ? (uint32_t)(k * a.ldw + col) * 4u : 0xfffffff0u);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int col = c0 + cq + u;
+      mk[u] = buf_ld(rH, act && m < B && col < a.H ? (uint32_t)(m * a.ldh + col) * 4u : 0xfffffff0u);
+    }
+  };
   // the dL/da partials the previous phase wrote: after mid() (k_chain's barrier; a no-op in
   // the standalone kernel, whose loads all went out above)
+  preload();
   mid();
   const rsrc_t rP = make_rsrc(pa, (uint32_t)((size_t)n_pa * B * A * 4));
   const uint32_t pstride = (uint32_t)B * (uint32_t)A * 4u, po = (uint32_t)((own ? pm : 0) * A + pj) * 4u;
@@ -4004,22 +4015,35 @@ constexpr long long kChainSpinTicks = 5000000;   // 50 ms of the 100 MHz clock: 
 // kChainBars the launch ticket — monotonic and wrapping: every launch adds exactly `nmem` to
 // each, so launch e's barrier b is complete once its word reaches (e + 1) nmem, e read from the
 // ticket each workgroup draws at its start (nothing is ever reset).
-//   chain_phase_end  every wave's write-through stores acknowledged (vmcnt(0)), then a
-//                    workgroup barrier — before the workgroup's arrival is signalled
-//   chain_arrive     ONE agent-scope add (non-returning: issued behind the next phase's weight
-//                    loads, it waits for none of them), then — wait — a poll (relaxed sc1 loads
-//                    + s_sleep) until the cohort has arrived, then a workgroup barrier; every
-//                    later load of handed-off bytes is an sc1 load (kg_body / tail_unit with
-//                    LDAUX = sc1).  A bounded spin: a timeout sets ERR_CHAIN_TIMEOUT (the host
-//                    reports a device error) and the workgroup runs on — void outputs, no hang.
-__device__ __forceinline__ void chain_phase_end() {
+//   chain_end   every wave's write-through stores acknowledged (vmcnt(0)), a workgroup
+//               barrier, then ONE agent-scope add on the phase's barrier word (non-returning)
+//   ChainWait   the next phase's wait on it: issue() — thread 0's first poll load, at the
+//               very start of the phase body, ahead of its weight loads (vmcnt is in order:
+//               the poll's value then does not wait for them) — and operator() after the
+//               weight loads (kg_body / tail_unit MIDSPLIT hook): further polls (relaxed sc1
+//               loads + s_sleep) until the cohort has arrived, then a workgroup barrier; every
+//               later load of handed-off bytes is an sc1 load (LDAUX = sc1).  A bounded spin:
+//               a timeout sets ERR_CHAIN_TIMEOUT (the host reports a device error) and the
+//               workgroup runs on — void outputs, no hang.
+__device__ __forceinline__ void chain_end(int* cnt) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void chain_arrive(int* cnt, int target, bool wait, int* err) {
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wait) {
+struct ChainWait {
+  int* cnt;
+  int target;
+  int* err;
+  bool wait;
+  tl_word* tl;
+  int slot;
+  int v;
+  __device__ __forceinline__ void issue() {
+    if (threadIdx.x == 0 && wait) v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __device__ __forceinline__ void operator()() {
+    if (threadIdx.x == 0 && wait && (int)((unsigned)v - (unsigned)target) < 0) {
       const unsigned long long t0 = wall_clock64();
       while ((int)((unsigned)__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (unsigned)target) < 0) {
         __builtin_amdgcn_s_sleep(1);
@@ -4029,9 +4053,10 @@ __device__ __forceinline__ void chain_arrive(int* cnt, int target, bool wait, in
         }
       }
     }
+    __syncthreads();
+    SACMI_PHASE(tl, slot);
   }
-  __syncthreads();
-}
+};
 // the launch's completion target of every barrier word (thread 0 only: the others never wait)
 __device__ __forceinline__ int chain_target(int* ticket, int nmem) {
   if (threadIdx.x != 0) return 0;
@@ -4073,35 +4098,26 @@ __global__ __launch_bounds__(1024, 4) void k_chain(const ChainArgs* __restrict__
   int* const sync = chain_args(ca)->sync + c * (kChainBars + 1) * 32;
   int* const err = chain_args(ca)->err;
   const int target = chain_target(sync + kChainBars * 32, nmem);
-  auto arrive = [&](int b, bool wait) {
-    chain_arrive(sync + b * 32, target, wait, err);
-    SACMI_PHASE(tl, 6 + b);
-  };
+  auto waiter = [&](int b, bool w) { return ChainWait{sync + b * 32, target, err, w, tl, 6 + b, 0}; };
   // L7 (updated critics fc1 on [s|1|a~])
   {
     const GemmBatch& b = chain_args(ca)->lv[0];
     if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, bid, sm.a);
-    chain_phase_end();
+    chain_end(sync);
     SACMI_PHASE(tl, 1);
   }
   // L8 (fc2 + fc3 dot partials): barrier 0 behind its weight loads
   {
     const GemmBatch& b = chain_args(ca)->lv[1];
-    if (bid < b.total_tiles)
-      kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, [&] { arrive(0, true); });
-    else
-      arrive(0, false);
-    chain_phase_end();
+    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, waiter(0, true));
+    chain_end(sync + 32);
     SACMI_PHASE(tl, 2);
   }
   // L9: the actor row prologue + dha1 + the dL/da partials
   {
     const GemmBatch& b = chain_args(ca)->lv[2];
-    if (bid < b.total_tiles)
-      kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1, true>(b, bid, sm.b, [&] { arrive(1, true); });
-    else
-      arrive(1, false);
-    chain_phase_end();
+    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1, true>(b, bid, sm.b, waiter(1, true));
+    chain_end(sync + 64);
     SACMI_PHASE(tl, 3);
   }
   // the sample-backward tail: the cohort's 8-row groups x 64-column dhp2 slabs
@@ -4111,24 +4127,19 @@ __global__ __launch_bounds__(1024, 4) void k_chain(const ChainArgs* __restrict__
     const int j = bid / kChainCohorts;
     if (j < units) {
       const int g = j % ng, slab = j / ng;
-      tail_unit<kLdSc1>(q->pa, q->n_pa, q->tail, c * q->rows_per_cohort + g * kTailRows,
-                        slab * kTailCols, slab == 0, sm.t, [&] { arrive(2, true); });
-    } else {
-      arrive(2, false);
+      tail_unit<kLdSc1, true>(q->pa, q->n_pa, q->tail, c * q->rows_per_cohort + g * kTailRows,
+                              slab * kTailCols, slab == 0, sm.t, waiter(2, true));
     }
-    chain_phase_end();
+    chain_end(sync + 96);
     SACMI_PHASE(tl, 4);
   }
   // L12 (dhp1) + the level's rides (the next update's sampler, Polyak): a workgroup whose
-  // item is a ride reads nothing of the chain — it arrives and goes on
+  // item is a ride reads nothing of the chain — it does not wait
   {
     const GemmBatch& b = chain_args(ca)->lv[3];
     const int items = b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
-    const bool tile = bid < b.total_tiles;
     if (bid < items)
-      kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, [&] { arrive(3, tile); });
-    else
-      arrive(3, false);
+      kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, waiter(3, bid < b.total_tiles));
     SACMI_PHASE(tl, 5);
   }
 }
@@ -4151,45 +4162,33 @@ __global__ __launch_bounds__(1024, 4) void k_chain_a(const ChainArgs* __restrict
   int* const sync = chain_args(ca)->sync + c * (kChainBars + 1) * 32;
   int* const err = chain_args(ca)->err;
   const int target = chain_target(sync + kChainBars * 32, nmem);
-  auto arrive = [&](int b, bool wait) {
-    chain_arrive(sync + b * 32, target, wait, err);
-    SACMI_PHASE(tl, 6 + b);
-  };
+  auto waiter = [&](int b, bool w) { return ChainWait{sync + b * 32, target, err, w, tl, 6 + b, 0}; };
   // L1: 32x64 tiles
   {
     const GemmBatch& b = chain_args(ca)->lv[0];
     if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, bid, sm.w);
-    chain_phase_end();
+    chain_end(sync);
     SACMI_PHASE(tl, 1);
   }
   // L2 (+ the heads): 32x64 tiles, barrier 0 behind its weight loads
   {
     const GemmBatch& b = chain_args(ca)->lv[1];
-    if (bid < b.total_tiles)
-      kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.w, [&] { arrive(0, true); });
-    else
-      arrive(0, false);
-    chain_phase_end();
+    if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.w, waiter(0, true));
+    chain_end(sync + 32);
     SACMI_PHASE(tl, 2);
   }
   // L3, L4 (target critics): 32x32 tiles
 #pragma unroll 1
   for (int i = 2; i < 4; ++i) {
     const GemmBatch& b = chain_args(ca)->lv[i];
-    if (bid < b.total_tiles)
-      kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, [&] { arrive(i - 1, true); });
-    else
-      arrive(i - 1, false);
-    chain_phase_end();
+    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, waiter(i - 1, true));
+    chain_end(sync + 32 * i);
     SACMI_PHASE(tl, i + 1);
   }
   // L5: the critic row prologue (targets, MSE gradients, loss partials) + dh1
   {
     const GemmBatch& b = chain_args(ca)->lv[4];
-    if (bid < b.total_tiles)
-      kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1, true>(b, bid, sm.b, [&] { arrive(3, true); });
-    else
-      arrive(3, false);
+    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1, true>(b, bid, sm.b, waiter(3, true));
     SACMI_PHASE(tl, 5);
   }
 }
