@@ -3035,6 +3035,324 @@ static int axk16_ok(GemmBatch& b) {
   return assign_tiles<kXBM, kXBN>(b) >= 256 ? ax : -1;
 }
 
+// ---------------------------------------------------------------------------
+// k_axk16p: the act16 batch-4096-class dh levels — k_axk16's math, dh = coef * (A W) *
+// [h > 0] with A = u = [h2 > 0] w3 on the row-prologue levels (AX: L5 / L9) and A = the
+// dh gradient on the plain ones (L12, model2's L5b / L9b / L11) — on k_fwd16p's multi-slab
+// LDS ring: one 16-wave workgroup per CU, BM x 128 tiles, 64-deep slabs filled by LDS-DMA
+// (global_load_lds_dwordx4), NST - 1 slabs in flight across raw barriers with counted
+// vmcnt waits.  k_axk16 stages through registers with one slab in flight: its levels took
+// ~1.6x k_fwd16p's for the same GEMM shape (config 5, round 4: L5 26 us against L4 15 us).
+// Operands in the slot (the DMA image is lane-linear, so every swizzle is on the SOURCE
+// address: LDS position p of row R holds the row's 16-byte chunk p ^ sw(R)):
+//   A, AX: bf16 h2 rows [m][64 k] (128 B), sw = (R >> 1) & 7, read as k_fwd16p's A
+//          (ds_read_b128) and transformed in registers: u = h2 > 0 ? bf16(w3[k]) : 0
+//          (w3 staged in LDS once, fp32 and bf16: the bits k_axk16's staging rounds to);
+//   A, !AX: fp32 gradient rows [m][64 k] (256 B), sw = R & 15, two ds_read_b128 and a
+//          round to bf16 (k_axk16's pack) per fragment;
+//   B: W's [k][n] rows (MN-contiguous: the layer's [out][in]), 128 bf16 columns (256 B) a
+//          k row, sw = 2 (R & 3) ^ 8 ((R >> 3) & 1): conflict-free for ds_read_b64_tr_b16
+//          (lane 4q + p of a 16-lane group: k row q, columns 4p..4p+3).
+// The same MFMAs over the same k blocks as k_axk16 per output element: identical bits.
+// AX: the column-tile-0 workgroup's wn == 0 waves also store u (fp32, ax_out) for the
+// later weight gradient, as k_axk16 — those stores sit in the vmcnt count, so the counted
+// waits include them.  The host runs a level here only without rides, K % 64 == 0,
+// N % 8 == 0, 16-byte aligned operand rows (axk16p_plan).
+#ifndef SACMI_AXK16P
+#define SACMI_AXK16P 1
+#endif
+template <int BM, bool AX>
+__host__ __device__ constexpr int axk16p_stage() { return BM * 64 * (AX ? 2 : 4) + 64 * 256; }
+template <int BM, bool AX>
+__host__ __device__ constexpr int axk16p_stages() { return kPLds / axk16p_stage<BM, AX>(); }
+
+// LDS reads the compiler does not see (k_axk16p's slab reads; see there) and the tie that
+// orders their consumers after an explicit lgkmcnt wait
+typedef __attribute__((address_space(3))) const void lds_cvoid_t;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_cvoid_t*)p; }
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u4v ds_rd128(uint32_t a) {
+  u4v v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+__device__ __forceinline__ u2v ds_rdtr(uint32_t a) {
+  u2v v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+template <class T>
+__device__ __forceinline__ void lds_tie(T& x) { asm volatile("" : "+v"(x)); }
+
+// s_waitcnt vmcnt(ahead * PPW + sts * NS) lgkmcnt(0) for ahead < 3, sts < 4 (immediates)
+template <int PPW, int NS>
+__device__ __forceinline__ void axk16p_wait(int ahead, int sts) {
+  switch (ahead * 4 + sts) {
+    case 0: vm_wait_lgkm0<0>(); break;
+    case 1: vm_wait_lgkm0<NS>(); break;
+    case 2: vm_wait_lgkm0<2 * NS>(); break;
+    case 3: vm_wait_lgkm0<3 * NS>(); break;
+    case 4: vm_wait_lgkm0<PPW>(); break;
+    case 5: vm_wait_lgkm0<PPW + NS>(); break;
+    case 6: vm_wait_lgkm0<PPW + 2 * NS>(); break;
+    case 7: vm_wait_lgkm0<PPW + 3 * NS>(); break;
+    case 8: vm_wait_lgkm0<2 * PPW>(); break;
+    case 9: vm_wait_lgkm0<2 * PPW + NS>(); break;
+    case 10: vm_wait_lgkm0<2 * PPW + 2 * NS>(); break;
+    default: vm_wait_lgkm0<2 * PPW + 3 * NS>(); break;
+  }
+}
+
+template <int BM, bool AX>
+__global__ __launch_bounds__(1024, 1) void k_axk16p(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_AXK16P);
+  constexpr int BN = 128, BK = 64, NWV = 16, WR = 4, WC = 4;
+  constexpr int MW = BM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
+  constexpr int AROW = BK * (AX ? 2 : 4);            // bytes per A slab row
+  constexpr int ABYTES = BM * AROW, STAGE = axk16p_stage<BM, AX>();
+  constexpr int NST = axk16p_stages<BM, AX>();
+  constexpr int APC = ABYTES / 1024, BPC = BK * 256 / 1024;   // 1 KiB pieces per slab
+  constexpr int PPW = (APC + BPC) / NWV, APW = APC / NWV;
+  constexpr int ALPR = AROW / 16;                     // lanes (16-byte chunks) per A row
+  constexpr int NS = AX ? 2 * MI * (BK / 32) : 0;     // u stores per lane per slab
+  static_assert(STAGE == ABYTES + BPC * 1024 && NST >= 3 && NST - 2 <= 2 && APC % NWV == 0 &&
+                BPC % NWV == 0 && MI >= 1 && NT == 2, "k_axk16p geometry");
+  // one LDS object (the ring, then w3 and the row prologue's scratch): with a second
+  // __shared__ variable the compiler put a vmcnt(0) in front of the slab reads
+  constexpr int XW = AX ? 512 * 4 + 512 * 2 : 0, XQ = BM * 4 * 4 + 2 * BM * 4 + BM * 2 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NST * STAGE + XW + XQ];
+  float* const s_w3 = reinterpret_cast<float*>(lds + NST * STAGE);
+  unsigned short* const s_w3b = reinterpret_cast<unsigned short*>(lds + NST * STAGE + 512 * 4);
+  auto s_q = reinterpret_cast<float (*)[4]>(lds + NST * STAGE + XW);
+  auto s_coef = reinterpret_cast<float (*)[BM]>(lds + NST * STAGE + XW + BM * 16);
+  auto s_l = reinterpret_cast<float (*)[2]>(lds + NST * STAGE + XW + BM * 24);
+  const int bid = blockIdx.x;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  int tr, tc;
+  place_tile(d, t, tr, tc);
+  const int m0 = tr * BM, n0 = tc * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WC) * MW, wn = (wave % WC) * NW;
+  const int M = d.M, N = d.N, K = d.K;
+  const bool store_a = AX && n0 == 0 && d.ax_out != nullptr;
+  const bool stw = store_a && wn == 0;                // this wave stores u
+  const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
+                               store_a ? (uint32_t)(((size_t)(M - 1) * d.ax_ld + K) * 4) : 0u);
+  // the row prologue's loads, the w3 vector and the ReLU-mask source go out first (oldest
+  // on the vm queue: retired by the first slab's wait)
+  float w3v = 0.f;
+  if constexpr (AX) w3v = buf_ld(make_rsrc(d.ax_w, (uint32_t)K * 4u), (uint32_t)(tid < K ? tid : 0) * 4u);
+  RowsRegs rows_x{};
+  if constexpr (AX) rows_load<BM, 1024>(batch.rows, d, m0, rows_x);
+  float hm[MI][NT][4];
+  {
+    const rsrc_t rX = make_rsrc(d.aux, (uint32_t)(((size_t)(M - 1) * d.ldaux + N) * 2));
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int col = n0 + wn + j * 16 + (lane & 15);
+          const uint32_t off = row < M && col < N ? (uint32_t)(row * d.ldaux + col) * 2u : 0xfffffff0u;
+          hm[i][j][r] = bf16_lo(buf_ld_u16(rX, off));
+        }
+      }
+  }
+  // DMA sources: wave w moves pieces w + 16 i (A rows first, then B k rows)
+  const unsigned char* src[PPW];
+  int cko[PPW];    // A: the lane's chunk byte offset in its row; B: the lane's k row in the slab
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int pc = wave + NWV * i;
+    if (i < APW) {
+      const int R = pc * (1024 / AROW) + lane / ALPR, pos = lane % ALPR;
+      const int c = AX ? (pos ^ ((R >> 1) & 7)) : (pos ^ (R & 15));
+      const int ra = min(m0 + R, M - 1);
+      src[i] = reinterpret_cast<const unsigned char*>(d.A) + (size_t)ra * d.lda * (AX ? 2 : 4);
+      cko[i] = c * 16;
+    } else {
+      const int R = (pc - APC) * 4 + (lane >> 4), pos = lane & 15;
+      const int c = pos ^ (((R & 3) << 1) ^ (((R >> 3) & 1) << 3));
+      const int n = min(n0 + 8 * c, N - 8);          // (N % 8 == 0: a chunk is all in or out)
+      src[i] = reinterpret_cast<const unsigned char*>(d.Bh) + (size_t)n * 2;
+      cko[i] = R;
+    }
+  }
+  auto issue = [&](int sl) {                          // slab sl into ring slot sl % NST
+    unsigned char* dst = lds + (sl % NST) * STAGE;
+    const int k0 = sl * BK;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave + NWV * i;
+      const unsigned char* g = i < APW ? src[i] + (size_t)k0 * (AX ? 2 : 4) + cko[i]
+                                       : src[i] + (size_t)min(k0 + cko[i], K - 1) * d.ldb * 2;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(dst + pc * 1024), 16, 0, 0);
+    }
+  };
+  f4 acc[MI][NT];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int nslab = K / BK;
+#pragma unroll
+  for (int s2 = 0; s2 < NST - 1; ++s2)
+    if (s2 < nslab) issue(s2);
+  if constexpr (AX) {   // (read after the first slab's barrier; asm stores: see ds_rd128)
+    if (tid < K) {
+      const uint32_t wb16 = __builtin_bit_cast(unsigned short, (__bf16)w3v);
+      asm volatile("ds_write_b32 %0, %1" :: "v"(lds_addr(&s_w3[tid])), "v"(w3v) : "memory");
+      asm volatile("ds_write_b16 %0, %1" :: "v"(lds_addr(&s_w3b[tid])), "v"(wb16) : "memory");
+    }
+  }
+  const int r16 = lane & 15, tq = r16 >> 2, tp = lane & 3, tg = lane >> 4;
+  for (int sl = 0; sl < nslab; ++sl) {
+    // retire slab sl only: younger are the slabs already issued past it and the u stores
+    // of the iterations since it was issued
+    const int ahead = min(NST - 2, nslab - 1 - sl);
+    axk16p_wait<PPW, NS>(ahead, stw ? min(sl, NST - 1) : 0);
+    __builtin_amdgcn_s_barrier();                     // every wave's slab sl landed; slot (sl-1) free
+    asm volatile("" ::: "memory");
+    if (sl + NST - 1 < nslab) issue(sl + NST - 1);
+    const unsigned char* st = lds + (sl % NST) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int kb = sl * BK + kk * 32 + 8 * tg;      // this lane's 8 k of the A fragment
+      // every LDS read here is inline asm (ds_rd128 / ds_rdtr): a compiler-visible LDS read
+      // after the slab's global_load_lds got a vmcnt(0) from the compiler (waiting for the
+      // slabs just issued as well); the lgkmcnt wait is ours (lds_tie)
+      u4v ar[MI][AX ? 1 : 2], wb{}, w0{}, w1{};
+      u2v blo[NT], bhi[NT];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int r = wm + i * 16 + r16;
+        if constexpr (AX) {
+          const int c = kk * 4 + tg;
+          ar[i][0] = ds_rd128(lds_addr(st + r * AROW + ((c ^ ((r >> 1) & 7)) << 4)));
+        } else {
+          const int c = kk * 8 + 2 * tg;
+          ar[i][0] = ds_rd128(lds_addr(st + r * AROW + ((c ^ (r & 15)) << 4)));
+          ar[i][1] = ds_rd128(lds_addr(st + r * AROW + (((c + 1) ^ (r & 15)) << 4)));
+        }
+      }
+      if constexpr (AX) {
+        wb = ds_rd128(lds_addr(&s_w3b[kb]));
+        if (stw) {
+          w0 = ds_rd128(lds_addr(&s_w3[kb]));
+          w1 = ds_rd128(lds_addr(&s_w3[kb + 4]));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int cb = (wn + j * 16 + 4 * tp) >> 3, half = (tp & 1) * 8;
+        const int k0r = kk * 32 + 8 * tg + tq, k1r = k0r + 4;
+        const int p0 = cb ^ (((k0r & 3) << 1) ^ (((k0r >> 3) & 1) << 3));
+        const int p1 = cb ^ (((k1r & 3) << 1) ^ (((k1r >> 3) & 1) << 3));
+        blo[j] = ds_rdtr(lds_addr(st + ABYTES + k0r * 256 + (p0 << 4) + half));
+        bhi[j] = ds_rdtr(lds_addr(st + ABYTES + k1r * 256 + (p1 << 4) + half));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int h = 0; h < (AX ? 1 : 2); ++h) lds_tie(ar[i][h]);
+      lds_tie(wb); lds_tie(w0); lds_tie(w1);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) { lds_tie(blo[j]); lds_tie(bhi[j]); }
+      bf16x8 a[MI], b[NT];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        if constexpr (AX) {
+          const u4v h = ar[i][0];
+          auto sel = [](uint32_t hv, uint32_t wv) {   // per bf16 half: h > 0 ? w : 0
+            return (bf16_lo(hv) > 0.f ? wv & 0xffffu : 0u) | (bf16_hi(hv) > 0.f ? wv & 0xffff0000u : 0u);
+          };
+          const uint4 u = {sel(h.x, wb.x), sel(h.y, wb.y), sel(h.z, wb.z), sel(h.w, wb.w)};
+          a[i] = __builtin_bit_cast(bf16x8, u);
+          if (stw) {   // u rows (fp32) for the weight gradient
+            const float4 f0 = __builtin_bit_cast(float4, w0), f1 = __builtin_bit_cast(float4, w1);
+            const int rr = m0 + wm + i * 16 + r16;
+            const uint32_t o = rr < M ? (uint32_t)(rr * d.ax_ld + kb) * 4u : 0xfffffff0u;
+            buf_st4(rAx, o, f4{bf16_lo(h.x) > 0.f ? f0.x : 0.f, bf16_hi(h.x) > 0.f ? f0.y : 0.f,
+                               bf16_lo(h.y) > 0.f ? f0.z : 0.f, bf16_hi(h.y) > 0.f ? f0.w : 0.f});
+            buf_st4(rAx, rr < M ? o + 16u : 0xfffffff0u,
+                    f4{bf16_lo(h.z) > 0.f ? f1.x : 0.f, bf16_hi(h.z) > 0.f ? f1.y : 0.f,
+                       bf16_lo(h.w) > 0.f ? f1.z : 0.f, bf16_hi(h.w) > 0.f ? f1.w : 0.f});
+          }
+        } else {
+          const u2v lo = pack_bf16x4(__builtin_bit_cast(float4, ar[i][0]));
+          const u2v hi = pack_bf16x4(__builtin_bit_cast(float4, ar[i][1]));
+          const uint4 u = {lo.x, lo.y, hi.x, hi.y};
+          a[i] = __builtin_bit_cast(bf16x8, u);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const uint4 v = {blo[j].x, blo[j].y, bhi[j].x, bhi[j].y};
+        b[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  const bool writer = p == 0 && n0 == 0;
+  if constexpr (AX) rows_finish<BM, 1024>(batch.rows, d, m0, writer, bid == 0, rows_x, s_q, s_coef, s_l);
+  // epilogue: coefficient, ReLU-backward mask, store (k_axk16's op order)
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int lr = wm + i * 16 + (lane >> 4) * 4 + r, row = m0 + lr;
+      const float cf = AX ? s_coef[d.ax_slot][lr] : 1.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = n0 + wn + j * 16 + (lane & 15);
+        float v = acc[i][j][r];
+        if (AX) v *= cf;
+        v = hm[i][j][r] > 0.f ? v : 0.f;
+        if (row < M && col < N) st_big(d.C + (size_t)row * d.ldc + col, v);
+      }
+    }
+  if constexpr (AX) rows_loss<BM>(batch.rows, m0, writer, s_l);
+}
+
+// whether an act16 k_axk16 level (axk16_ok form `ax`) can run on k_axk16p, and its row tile
+// (0: no): bf16 weight shadows, no rides, K % 64 == 0, N % 8 == 0, 16-byte operand rows,
+// one workgroup per CU at least
+// Opt-in (SACMI_AXK16P=1, read per enqueue): bit-identical to k_axk16 but measured slower
+// (config 5, same box, alternating: L5 29.4 vs 26.3 us, L9 25.4 vs 23.2, 3,204 vs 3,268
+// updates/s — profiles/r05/axk16p_ab): the dh levels are not bound by their K loop (the
+// register-staged and the ring kernel take about the same time for the same tiles) but by
+// what surrounds it — 32 MB of fp32 dh and u rows written per critic level
+static int axk16p_plan(GemmBatch& b, int ax) {
+  if (!SACMI_AXK16P || b.ride.kind || b.ride.pk_blocks) return 0;
+  const char* e = std::getenv("SACMI_AXK16P");
+  if (!e || std::atoi(e) == 0) return 0;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    if (!d.Bh || !d.x16 || (d.K % 64) || d.K > 512 || (d.N % 8) || d.N < 8) return 0;
+    if (((uintptr_t)d.A & 15) || ((uintptr_t)d.Bh & 15) || (d.ldb & 7)) return 0;
+    if (ax ? (!d.a16 || (d.lda & 7) || ((uintptr_t)d.ax_w & 15) || (d.ax_out && ((d.ax_ld & 3) || ((uintptr_t)d.ax_out & 15))))
+           : (d.a16 || (d.lda & 3)))
+      return 0;
+  }
+  GemmBatch t = b;   // (b keeps k_axk16's tiles unless this kernel takes the level)
+  if (assign_tiles<128, 128>(t) >= 256) { b = t; return 128; }
+  t = b;
+  if (!ax && assign_tiles<64, 128>(t) >= 256) { b = t; return 64; }
+  return 0;
+}
+
 // NSL: the partial loads each thread issues (= ns where instantiated, else kDwMaxSplit with
 // the loads past ns at an out-of-range offset): no VMEM issue slots for absent splits
 template <int NSL>
@@ -3337,7 +3655,13 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       for (int i = 0; i < b.count; ++i)
         if (b.d[i].c16 || b.d[i].b16 || b.d[i].x16 != form || b.d[i].a16 != (form && b.d[i].axk == 1))
           throw Error{SACMI_ESTATE, "k_axk16: unsupported bf16 activation operand"};
-      if (form) {
+      const int bm = form && bh ? axk16p_plan(b, ax) : 0;
+      if (bm) {   // (axk16p_plan re-tiled the level: its grid)
+        const dim3 pg(b.total_tiles);
+        if (ax) hipLaunchKernelGGL((k_axk16p<128, true>), pg, dim3(1024), 0, s, b);
+        else if (bm == 128) hipLaunchKernelGGL((k_axk16p<128, false>), pg, dim3(1024), 0, s, b);
+        else hipLaunchKernelGGL((k_axk16p<64, false>), pg, dim3(1024), 0, s, b);
+      } else if (form) {
         if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true, true>), grid, blk, 0, s, b);
         else if (ax) hipLaunchKernelGGL((k_axk16<true, false, true>), grid, blk, 0, s, b);
         else if (bh) hipLaunchKernelGGL((k_axk16<false, true, true>), grid, blk, 0, s, b);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One parameterised GPU session (replaces round 4's one-off gpu_r4*.sh scripts).  Steps, in
 # order, each with its own time limit; the first failure ends the session:
-#   tests    pytest -m gpu (PYTEST_ARGS; SACMI_GRAD_TABLE -> $O/grad_table.jsonl)
+#   tests    pytest -m gpu (PYTEST_ARGS, PYTEST_K = a -k expression; SACMI_GRAD_TABLE -> $O/grad_table.jsonl)
 #   smoke    __graft_entry__.smoke()
 #   ab       alternating bench lines without / with AB_ENV (BENCH_ARGS), AB_REPS pairs
 #   configs  bench lines of CONFIGS (default "2 3 5"), BENCH_ARGS appended
@@ -20,7 +20,7 @@ for step in ${STEPS:-tests smoke configs}; do
   case $step in
     tests)
       SACMI_GRAD_TABLE=$PWD/$O/grad_table.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 \
-        --timeout-method thread ${PYTEST_ARGS:-} > $O/pytest_gpu.log 2>&1
+        --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1
       rc=$?; tail -3 $O/pytest_gpu.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; } ;;

@@ -12,7 +12,7 @@ import sys
 def main(path):
     rows = list(csv.DictReader(open(path)))
     tot_ns = calls = 0
-    level = ("sacmi::k_gemm<", "sacmi::k_fwd<", "sacmi::k_fwd16<", "sacmi::k_fwd16p<", "sacmi::k_axk16<", "sacmi::k_dw_part",
+    level = ("sacmi::k_gemm<", "sacmi::k_fwd<", "sacmi::k_fwd16<", "sacmi::k_fwd16p<", "sacmi::k_axk16<", "sacmi::k_axk16p<", "sacmi::k_dw_part",
              "sacmi::k_chain")
     for r in rows:
         name, n, avg = r["Name"], int(r["Calls"]), float(r["AverageNs"])
