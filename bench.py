@@ -121,7 +121,7 @@ def init_agent(ctx, seed):
 # one level carrying its four GEMMs' and the tail's dhp2 FLOPs, k_chain_a (the critic pass
 # L1 -> L2 + heads -> L3 -> L4 -> L5) as one carrying its five GEMMs' and the heads'; a level
 # with the policy heads folded in carries the heads GEMM's FLOPs (sacmi.hip level_flops)
-LEVEL_KERNELS = {"k_gemm", "k_fwd", "k_fwd16", "k_fwd16p", "k_axk16", "k_axk16p", "k_dw_part", "k_dw_part16", "k_dw_fin",
+LEVEL_KERNELS = {"k_gemm", "k_fwd", "k_fwd16", "k_fwd16p", "k_axk16", "k_axk16p", "k_dw_part", "k_dw_part16", "k_dw_fin", "k_dw_fin_p",
                  "k_chain", "k_chain_a"}
 
 

@@ -3470,6 +3470,151 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
   store_err_flags(batch);
 }
 
+// k_dw_fin, pipelined (opt-in, SACMI_DWFIN_P=1 — measured slower: config 5 L6 65.8 vs 63.4 us,
+// L13 42.0 vs 40.5, 3,213 vs 3,246 updates/s, profiles/r05/dwfin_p_ab): the same
+// per-group arithmetic over the same virtual blocks (256 four-column groups each, dealt to
+// the descs in order), but on a grid of at most kDwFinGrid workgroups that loop over them —
+// the next block's loads (partials, parameter, moments, target) are issued before this
+// block's stores, so the level's reads and writes overlap instead of running as one read
+// phase then one write phase across the whole chip (k_dw_fin: ~2.5-2.7 TB/s at config 5,
+// profiles/r05/pmc_c5.json).  Identical bits: each group's sums and updates are k_dw_fin's.
+#ifndef SACMI_DWFIN_GRID
+#define SACMI_DWFIN_GRID 768      // (3 resident per CU at the 11-split form's 138 VGPRs)
+#endif
+constexpr int kDwFinGrid = SACMI_DWFIN_GRID;
+
+template <int NSL>
+__global__ __launch_bounds__(256) void k_dw_fin_p(GemmBatch batch, int ns, int64_t ws_stride, int nvb) {
+  const TlMark tl_mark(batch.tl, TL_DW_FIN_P);
+  __shared__ AdamScalars s_k[3];
+  __shared__ int s_err;
+  const AdamFuse& af = batch.adam;
+  const bool adam = batch.has_adam != 0;
+  if (adam && threadIdx.x < 3) s_k[threadIdx.x] = fuse_scalars(af, threadIdx.x, af.step_offset);
+  if (threadIdx.x == 0) s_err = adam ? af.sc->err : 0;
+  __syncthreads();
+  const bool void_st = (s_err & af.err_skip) != 0;   // (see k_dw_fin)
+  const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
+  const bool wt = batch.st_wt != 0;
+  const uint32_t oob = 0xfffffff0u;
+  // virtual block vb -> its desc q, the desc's first block and its partial-row offset
+  auto locate = [&](int vb, int& q, int& bstart, int64_t& off) {
+    q = batch.count - 1; bstart = 0; off = 0;
+    int acc = 0;
+    bool found = false;
+    int64_t o = 0;
+    for (int qq = 0; qq < batch.count; ++qq) {
+      const int n_el_q = batch.d[qq].M * dw_ncols(batch.d[qq]);
+      const int nb = (n_el_q / 4 + 255) / 256;
+      if (!found && vb < acc + nb) { q = qq; bstart = acc; off = o; found = true; }
+      o += n_el_q;
+      acc += nb;
+    }
+  };
+  struct Ld {
+    float4 t[NSL], pp, mm, vv, tt;
+  };
+  // every load of one block's group, at once; a block past the level (vb >= nvb) or a group
+  // past its desc reads at out-of-range offsets (no access)
+  auto load = [&](int vb, Ld& L) {
+    int q, bstart;
+    int64_t off;
+    locate(vb < nvb ? vb : 0, q, bstart, off);
+    const GemmDesc& d = batch.d[q];
+    const int nc = dw_ncols(d), gpr = nc / 4, n_gr = d.M * gpr;
+    const int g = (vb - bstart) * 256 + threadIdx.x;
+    const bool live = vb < nvb && g < n_gr;
+    const int row = live ? g / gpr : 0, c4 = live ? (g - row * gpr) * 4 : 0;
+    const uint32_t o = (uint32_t)(row * d.ldc + c4) * 4u;
+    const bool pol = d.epi == EPI_ADAM_POLYAK;
+    const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
+    const float* wsd = batch.ws + off;
+    const rsrc_t rWs = make_rsrc(wsd, (uint32_t)(((int64_t)(ns - 1) * ws_stride + (int64_t)n_gr * 4) * 4));
+    const rsrc_t rTg = make_rsrc(adam && pol ? af.T + abase - af.t_base : wsd, adam && pol ? 0x7fffffffu : 0u);
+    const rsrc_t rC = make_rsrc(d.C, 0x7fffffffu);
+    const rsrc_t rM = make_rsrc(adam ? af.M + abase : d.C, adam ? 0x7fffffffu : 0u);
+    const rsrc_t rV = make_rsrc(adam ? af.V + abase : d.C, adam ? 0x7fffffffu : 0u);
+#pragma unroll
+    for (int sp = 0; sp < NSL; ++sp)
+      L.t[sp] = buf_ld4(rWs, live && sp < ns ? (uint32_t)((int64_t)sp * ws_stride + (int64_t)g * 4) * 4u : oob);
+    L.pp = buf_ld4(rC, adam && live ? o : oob);
+    L.mm = buf_ld4(rM, live ? o : oob);
+    L.vv = buf_ld4(rV, live ? o : oob);
+    L.tt = buf_ld4(rTg, pol && live ? o : oob);
+  };
+  // k_dw_fin's arithmetic and stores for one block's group
+  auto finish = [&](int vb, const Ld& L) {
+    int q, bstart;
+    int64_t off;
+    locate(vb, q, bstart, off);
+    const GemmDesc& d = batch.d[q];
+    const int nc = dw_ncols(d), ncr = dw_ncols_real(d), gpr = nc / 4, n_gr = d.M * gpr;
+    const int g = (vb - bstart) * 256 + threadIdx.x;
+    if (g >= n_gr) return;
+    const int row = g / gpr, c4 = (g - row * gpr) * 4;
+    const uint32_t o = (uint32_t)(row * d.ldc + c4) * 4u;
+    const bool pol = d.epi == EPI_ADAM_POLYAK;
+    const bool pol_st = pol && (s_err & af.err_nopolyak) == 0;
+    const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
+    const rsrc_t rC = make_rsrc(d.C, 0x7fffffffu);
+    const rsrc_t rM = make_rsrc(adam ? af.M + abase : d.C, adam ? 0x7fffffffu : 0u);
+    const rsrc_t rV = make_rsrc(adam ? af.V + abase : d.C, adam ? 0x7fffffffu : 0u);
+    const rsrc_t rG = make_rsrc(adam && af.G ? af.G + abase : d.C, adam && af.G ? 0x7fffffffu : 0u);
+    const rsrc_t rT = make_rsrc(adam && pol ? af.T + abase - af.t_base : d.C, adam && pol ? 0x7fffffffu : 0u);
+    float v[4] = {L.t[0].x, L.t[0].y, L.t[0].z, L.t[0].w};
+#pragma unroll
+    for (int sp = 1; sp < NSL; ++sp)
+      if (sp < ns) {
+#pragma clang fp contract(off)
+        v[0] += L.t[sp].x; v[1] += L.t[sp].y; v[2] += L.t[sp].z; v[3] += L.t[sp].w;
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = c4 + j < ncr ? v[j] : 0.f;
+    auto st4 = [&](rsrc_t r, float a0, float a1, float a2, float a3) {
+      if (wt) buf_st4<kStAux>(r, o, f4{a0, a1, a2, a3});
+      else buf_st4<0>(r, o, f4{a0, a1, a2, a3});
+    };
+    if (adam) {
+      float p4[4] = {L.pp.x, L.pp.y, L.pp.z, L.pp.w}, m4[4] = {L.mm.x, L.mm.y, L.mm.z, L.mm.w};
+      float v4[4] = {L.vv.x, L.vv.y, L.vv.z, L.vv.w}, t4[4] = {L.tt.x, L.tt.y, L.tt.z, L.tt.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        adam_elem(p4[j], m4[j], v4[j], v[j], omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
+        t4[j] = polyak(t4[j], p4[j], omtau, af.tau);
+      }
+      if (af.G) st4(rG, v[0], v[1], v[2], v[3]);
+      st4(rC, p4[0], p4[1], p4[2], p4[3]);
+      st4(rM, m4[0], m4[1], m4[2], m4[3]);
+      st4(rV, v4[0], v4[1], v4[2], v4[3]);
+      auto st_bf4 = [&](unsigned short* h, const float (&x)[4]) {   // 4 bf16 shadows, 8 bytes
+        const uint32_t lo = (uint32_t)bf16_bits(x[0]) | ((uint32_t)bf16_bits(x[1]) << 16);
+        const uint32_t hi = (uint32_t)bf16_bits(x[2]) | ((uint32_t)bf16_bits(x[3]) << 16);
+        if (wt) st_wt8(h, 0u, lo, hi);
+        else *reinterpret_cast<uint2*>(h) = make_uint2(lo, hi);
+      };
+      if (af.Ph) st_bf4(af.Ph + abase + o / 4u, p4);
+      if (pol_st) {
+        st4(rT, t4[0], t4[1], t4[2], t4[3]);
+        if (af.Th) st_bf4(af.Th + abase - af.t_base + o / 4u, t4);
+      }
+    } else {
+      st4(rC, v[0], v[1], v[2], v[3]);
+    }
+  };
+  if (!void_st) {
+    Ld cur, nxt;
+    int vb = blockIdx.x;
+    load(vb, cur);
+    for (; vb < nvb; vb += gridDim.x) {
+      load(vb + gridDim.x, nxt);   // (past the level: out-of-range, no access)
+      finish(vb, cur);
+      cur = nxt;
+    }
+  }
+  if (adam && blockIdx.x == 0) adam_block0(af, s_err, omb1, omb2);
+  store_err_flags(batch);
+}
+
 // 1 when the level carries bf16 activation operands (any GemmDesc a16 / b16 / c16 / x16);
 // each kernel that takes them checks the per-desc pattern it supports
 static int level_act16(const GemmBatch& b) {
@@ -3622,6 +3767,27 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       static const bool fin_wt = std::getenv("SACMI_FIN_WT") != nullptr && std::atoi(std::getenv("SACMI_FIN_WT")) != 0;
       b.st_wt = fin_wt ? 1 : 0;
       static const bool nsl = SACMI_DWFIN_NSL && std::getenv("SACMI_NO_DWFIN_NSL") == nullptr;
+      const char* fin_p = std::getenv("SACMI_DWFIN_P");   // (opt-in; read per enqueue: tests switch it)
+      if (nsl && kDwFinEpt == 1 && fin_p && std::atoi(fin_p) != 0) {
+        const dim3 pg(std::min(fin_grid, kDwFinGrid));
+        switch (ns) {
+          case 1: hipLaunchKernelGGL(k_dw_fin_p<1>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 2: hipLaunchKernelGGL(k_dw_fin_p<2>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 3: hipLaunchKernelGGL(k_dw_fin_p<3>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 4: hipLaunchKernelGGL(k_dw_fin_p<4>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 5: hipLaunchKernelGGL(k_dw_fin_p<5>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 6: hipLaunchKernelGGL(k_dw_fin_p<6>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 7: hipLaunchKernelGGL(k_dw_fin_p<7>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 8: hipLaunchKernelGGL(k_dw_fin_p<8>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 9: hipLaunchKernelGGL(k_dw_fin_p<9>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 10: hipLaunchKernelGGL(k_dw_fin_p<10>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 11: hipLaunchKernelGGL(k_dw_fin_p<11>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          case 12: hipLaunchKernelGGL(k_dw_fin_p<12>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+          default: hipLaunchKernelGGL(k_dw_fin_p<kDwMaxSplit>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
+        }
+        HIP_LAUNCH_CHECK();
+        return;
+      }
       switch (nsl ? ns : 0) {
         case 1: hipLaunchKernelGGL(k_dw_fin<1>, fg, fb, 0, s, b, ns, stride); break;
         case 2: hipLaunchKernelGGL(k_dw_fin<2>, fg, fb, 0, s, b, ns, stride); break;

@@ -1,5 +1,7 @@
-"""k_axk16p (the act16 dh levels on an LDS-DMA ring) against k_axk16 (register-staged
-slabs), bit for bit.
+"""Kernel-variant switches of the act16 (batch-4096, bf16) update, each bit for bit against
+the form it replaces.
+
+k_axk16p (the act16 dh levels on an LDS-DMA ring) against k_axk16 (register-staged slabs).
 
 Both kernels accumulate every output element over K in the same order (64-deep slabs in
 increasing k, two 16x16x32 bf16 MFMAs per slab and fragment with the same lane <-> operand
@@ -13,6 +15,11 @@ configs[4] per GPU (NAO S661 A23 H512, batch 4096, bf16): L5 / L9 (row prologue,
 tiles, two critics: 256 workgroups), L12 (plain, one net: 64x128 tiles), and with three
 hidden layers the plain two-critic levels (128x128).  A level that hosts a ride (L12 of an
 update that gathers the next batch) stays on k_axk16.
+
+k_dw_fin_p (the split-K weight gradients' fixed-order sum + Adam + Polyak on a looping grid,
+the next block's loads issued before this block's stores; opt-in, SACMI_DWFIN_P=1, measured
+slower) against k_dw_fin (one group per thread): the same per-group arithmetic, so the same
+bits.
 """
 import os
 
@@ -27,11 +34,11 @@ pytestmark = pytest.mark.gpu
 DH_SITES = ("gemm_L5_critic_dh1", "gemm_L9_act_dh1", "gemm_L12_pi_dhp1")
 
 
-def run_updates(n_hidden, off):
-    """Two injected updates and a 3-update launch at the config-5 shapes; the losses, every
-    tensor of every net (param / grad / Adam m, v) and the dh levels' kernels."""
-    if not off:
-        os.environ["SACMI_AXK16P"] = "1"
+def run_updates(n_hidden, env):
+    """Two injected updates and a 3-update launch at the config-5 shapes under the switches
+    `env`; the losses, every tensor of every net (param / grad / Adam m, v) and the levels'
+    kernels ({site: {(kernel, grid)}})."""
+    os.environ.update(env)
     try:
         cfg = SacConfig(661, 23, 512, n_hidden=n_hidden)
         B = 4096
@@ -61,18 +68,27 @@ def run_updates(n_hidden, off):
         ks, _ = ctx.profile_timeline(B, 2)
         kern = {}
         for k in ks:
-            if k["site"].startswith("gemm_L") and k["kernel"] in ("k_axk16", "k_axk16p"):
+            if k["site"].startswith("gemm_L"):
                 kern.setdefault(k["site"], set()).add((k["kernel"], k["grid"]))
         ctx.close()
         return out, kern
     finally:
-        os.environ.pop("SACMI_AXK16P", None)
+        for k in env:
+            os.environ.pop(k, None)
+
+
+def assert_same(a, b):
+    assert a.keys() == b.keys()
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
 
 
 @pytest.mark.parametrize("n_hidden", [2, 3])
 def test_axk16p_bitexact_vs_axk16(n_hidden):
-    a, ka = run_updates(n_hidden, off=False)
-    b, kb = run_updates(n_hidden, off=True)
+    a, ka = run_updates(n_hidden, {"SACMI_AXK16P": "1"})
+    b, kb = run_updates(n_hidden, {})
+    ka = {s: {v for v in ks if v[0].startswith("k_axk16")} for s, ks in ka.items()}
+    kb = {s: {v for v in ks if v[0].startswith("k_axk16")} for s, ks in kb.items()}
     # the ring kernel ran the two-critic row-prologue levels on one tile per CU ...
     for site in ("gemm_L5_critic_dh1", "gemm_L9_act_dh1"):
         assert ("k_axk16p", 256) in ka[site], (site, ka[site])
@@ -81,6 +97,15 @@ def test_axk16p_bitexact_vs_axk16(n_hidden):
     assert all(kn == "k_axk16" for v in kb.values() for kn, _ in v), kb
     if n_hidden == 3:
         assert sum(kn == "k_axk16p" for v in ka.values() for kn, _ in v) > 3, ka
-    assert a.keys() == b.keys()
-    for k in a:
-        assert np.array_equal(a[k], b[k]), k
+    assert_same(a, b)
+
+
+@pytest.mark.parametrize("n_hidden", [2, 3])
+def test_dw_fin_p_bitexact_vs_dw_fin(n_hidden):
+    a, ka = run_updates(n_hidden, {"SACMI_DWFIN_P": "1"})
+    b, kb = run_updates(n_hidden, {})
+    for site in ("gemm_L6_critic_dW_adam", "gemm_L13_pi_dW_adam"):
+        assert {kn for kn, _ in ka[site]} >= {"k_dw_part16", "k_dw_fin_p"}, (site, ka[site])
+        assert {kn for kn, _ in kb[site]} >= {"k_dw_part16", "k_dw_fin"}, (site, kb[site])
+        assert "k_dw_fin_p" not in {kn for kn, _ in kb[site]}
+    assert_same(a, b)
