@@ -1310,6 +1310,117 @@ __device__ __forceinline__ void store_err_flags(const GemmBatch& b) {
 
 // the policy heads + GaussianPolicy.sample of rows [m0, m0 + TM) (defined with k_heads_sample;
 // k_gemm runs it folded into the last policy hidden layer's level, GemmBatch::heads)
+// ---------------------------------------------------------------------------
+// Philox4x32-10 + Box-Muller (perf-mode policy noise)
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t counter, uint32_t elem) {
+  uint32_t c[4] = {(uint32_t)counter, (uint32_t)(counter >> 32), elem, 0x5ac3u};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float u1 = ((float)c[0] + 0.5f) * 2.3283064365386963e-10f;   // (0,1)
+  const float u2 = ((float)c[1] + 0.5f) * 2.3283064365386963e-10f;
+  return sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+}
+
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;   // math.log(math.sqrt(2*pi))
+
+// 1 - tanh(x)^2 = sech(x)^2 = 4t / (1+t)^2 with t = exp(-2|x|): the reference's
+// `1 - y.pow(2)` (networks_model1.py:93) without its cancellation — for |x| ~ 4 the fp32
+// difference keeps only ~12 good bits, and those few saturated elements dominate the
+// policy gradient through 2y / (1 - y^2) (batch-4096 runs: 1e-4 normwise scatter between
+// fp32 evaluations otherwise; this form tracks the fp64 truth)
+__device__ __forceinline__ float one_minus_tanh2(float x) {
+  const float t = expf(-2.f * fabsf(x));
+  const float u = 1.f + t;
+  return 4.f * t / (u * u);
+}
+
+// one (row m, action j) element of GaussianPolicy.sample from its head sums (bias added):
+// the action, cache and noise stores and the NaN check; returns the element's log-prob term
+template <bool H16, int AAUX>
+__device__ __forceinline__ float heads_elem(const HeadSampleArgs& a, int m, int j, float mean, float ls_raw,
+                                            float eps_in, uint64_t ctr) {
+  const int A = a.A;
+  const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
+  const float sd = expf(ls);
+  // Normal(mean, std) argument validation (networks_model1.py:87): loc must be real (not
+  // NaN) and scale positive — std = exp(clamp(log_std)) is NaN only for a NaN log_std
+  // (torch.clamp keeps NaN; fmaxf above does not, hence the raw value).  evaluate=True
+  // (deterministic) builds no Normal, so nothing is checked there (sac_imp.py:59-65).
+#if defined(SACMI_EXP_NOMFMA) || defined(SACMI_EXP_NOLOAD) || defined(SACMI_EXP_NOADAMIO) || \
+    defined(SACMI_EXP_EMPTY) || defined(SACMI_EXP_DESC) || defined(SACMI_EXP_NOSTORE)
+  if (false) {   // timing experiments compute garbage: never void their updates
+#else
+  if (a.nan_flag && !a.deterministic && (__builtin_isnan(mean) || __builtin_isnan(ls_raw))) {
+#endif
+    const int bit = m < a.split_row ? a.nan_bit_lo : a.nan_bit_hi;
+    if (a.nan_plain) *a.nan_flag = bit;
+    else atomicOr(a.nan_flag, bit);
+  }
+  float eps;
+  if (a.deterministic) {
+    eps = 0.f;
+  } else if (a.gen_eps) {
+    eps = philox_normal(a.seed, ctr, (uint32_t)(m * A + j));
+    a.eps[(size_t)m * A + j] = eps;
+  } else {
+    eps = eps_in;
+  }
+  const float x = a.deterministic ? mean : mean + eps * sd;
+  const float y = tanhf(x);
+  if constexpr (H16)
+    reinterpret_cast<unsigned short*>(a.act)[(size_t)m * a.ldact + j] = bf16_bits(y * a.scale + a.bias);
+  else   // (write-through where the same launch reads them back: k_chain_a's L3)
+    st_pol(a.act + (size_t)m * a.ldact + j, y * a.scale + a.bias, AAUX != 0);
+  if (a.act_host) a.act_host[(size_t)m * A + j] = y * a.scale + a.bias;
+  const float dx = x - mean;
+  float lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
+  const float omy2 = one_minus_tanh2(x);
+  lpe -= logf(a.scale * omy2 + 1e-6f);
+  float* cr = a.cache + (size_t)m * 3 * A;
+  cr[j] = omy2; cr[A + j] = ls_raw; cr[2 * A + j] = y;
+  return lpe;
+}
+
+// rows [m0, m0 + TM): the log-prob row sums from lp (every thread of the workgroup calls it)
+// and the row block's logp_part slot pair
+template <int TM, int AAUX>
+__device__ __forceinline__ void heads_logp(const HeadSampleArgs& a, int m0, int part, float (*lp)[33],
+                                           float* s_lp) {
+  const int A = a.A;
+  __syncthreads();
+  if (threadIdx.x < TM) {
+    const int mm = m0 + threadIdx.x;
+    float s = 0.f;
+    if (mm < a.rows) {
+      for (int jj = 0; jj < A; ++jj) s += lp[threadIdx.x][jj];
+      st_pol(a.logp + mm, s, AAUX != 0);
+    }
+    s_lp[threadIdx.x] = s;
+  }
+  if (a.logp_part) {
+    __syncthreads();
+    if (threadIdx.x < 2) {    // rows below / at-or-above split_row, fixed order
+      float s = 0.f;
+      for (int r = 0; r < TM; ++r) {
+        const int mm = m0 + r;
+        if (mm < a.rows && (mm >= a.split_row) == (threadIdx.x == 1)) s += s_lp[r];
+      }
+      a.logp_part[2 * part + threadIdx.x] = s;
+    }
+  }
+}
+
 template <int TN, int KSPLIT, bool H16, int TM, int AAUX>
 __device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int part, float* red,
                                            float (*lp)[33], float* s_lp);
@@ -1350,7 +1461,7 @@ struct KgSmem {
   int s_err;
   float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
   float s_pa[PA ? TMW * (TN + 1) + TN * 32 : 1];
-  float s_hlp[HF ? kHeadsFoldTM * 33 + kHeadsFoldTM : 1];
+  float s_hlp[HF ? kHeadsFoldTM * (TN + 1) : 1];   // the tile's h (folded heads' partial)
   int s_hlast;
 };
 
@@ -1599,6 +1710,12 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   // CORE 1: the Adam scalars by scalar loads into every wave (lgkmcnt: no vector-memory round
   // trip in front of the slab DMAs, and no LDS store that would wait for them)
   uint32_t skw[5] = {0u, 0u, 0u, 0u, 0u};
+  // folded heads (HF): a policy tile forms its columns' share of the heads (a split-K
+  // partial), so its head-weight columns come in with the epilogue operands
+  const bool hf_mine = HF && batch.heads_ticket != nullptr && p >= batch.heads_desc &&
+                       p < batch.heads_desc + batch.heads_ndesc;
+  constexpr int HWPT = HF ? (48 * TN + NTH - 1) / NTH : 1;   // (2A <= 48)
+  float hw_x[HWPT];
   auto pre = [&]() {
     if constexpr (ADAM && CORE == 1) {
       const sbuf_i4 r = s_rsrc(af.sc);
@@ -1610,6 +1727,17 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
       if (threadIdx.x == 0) {
         s_k = fuse_scalars(af, d.adam_step, af.step_offset);
         s_err = af.sc->err;
+      }
+    }
+    if constexpr (HF) {   // zero-length range where this tile folds nothing
+      const HeadSampleArgs& ha = batch.heads;
+      const int n2 = 2 * ha.A;
+      const rsrc_t rHW = make_rsrc(hf_mine ? ha.Wh : d.C,
+                                   hf_mine ? (uint32_t)(((size_t)(n2 - 1) * ha.ldw + ha.K) * 4) : 0u);
+#pragma unroll
+      for (int q = 0; q < HWPT; ++q) {
+        const int e = tid + q * NTH, j = e / TN, cc = e - j * TN;
+        hw_x[q] = buf_ld(rHW, e < n2 * TN && n0 + cc < ha.K ? (uint32_t)(j * ha.ldw + n0 + cc) * 4u : 0xfffffff0u);
       }
     }
     // axk 1: the row prologue's loads.  Issued here, behind the operand burst, and
@@ -1802,6 +1930,9 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
     if constexpr (PA) {   // every tile element, 0 outside the output
       if (has_pa && s < EPT) s_pa[row * (TN + 1) + col] = ok ? v : 0.f;
     }
+    if constexpr (HF) {   // (the stored h: after the ReLU)
+      if (hf_mine && s < EPT) s_hlp[row * (TN + 1) + col] = ok ? v : 0.f;
+    }
   }
   if (threadIdx.x < 64) SACMI_STAMP(33);
   SACMI_PHASE(batch.tl, 4);
@@ -1835,26 +1966,87 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   }
   store_err_flags(batch);
   if constexpr (HF) {
-    // folded heads: the tile's h stores (write-through) acknowledged in every wave, then the
-    // row block's arrival count; its last column tile runs the heads + sample of the block's
-    // 32 rows, reading h with sc1 loads (rows the other tiles stored from other XCDs)
+    // folded heads, split over the level's column tiles: each policy tile forms its TN
+    // columns' share of every head output of its 32 rows (fixed column order) into
+    // heads_part[row block][column tile] (write-through), acknowledged in every wave, then
+    // the row block's arrival count; the last column tile to arrive sums the shares in column-
+    // tile order (sc1 loads: stored from other XCDs), adds the bias and runs the sample
+    // epilogue (heads_elem: k_heads_sample's per-element algebra) and the log-prob sums.
     // (the policy rows may come as heads_ndesc descs of d.M rows each, stacked in order: the
     // target and actor halves of k_chain_a's row-affine L2)
-    if (batch.heads_ticket != nullptr && p >= batch.heads_desc && p < batch.heads_desc + batch.heads_ndesc) {
+    if (hf_mine) {
+      const HeadSampleArgs& ha = batch.heads;
+      const int A = ha.A, n2 = 2 * A;
       const int hm0 = m0 + (p - batch.heads_desc) * d.M;   // the row in the heads' stacked rows
+      const int rb = hm0 / kHeadsFoldTM, tcol = n0 / TN, ntc = d.tiles_n;
+      static_assert(TMW == kHeadsFoldTM, "one 32-row block per folding tile");
+      __syncthreads();                                     // s_hlp complete; red free
+      float* s_w = red;                                    // [n2][TN + 1]
+#pragma unroll
+      for (int q = 0; q < HWPT; ++q) {
+        const int e = tid + q * NTH;
+        if (e < n2 * TN) s_w[(e / TN) * (TN + 1) + e % TN] = hw_x[q];
+      }
+      __syncthreads();
+      float* part = batch.heads_part + ((size_t)rb * ntc + tcol) * (kHeadsFoldTM * n2);
+      for (int e = tid; e < kHeadsFoldTM * n2; e += NTH) {
+        const int row = e / n2, j = e - row * n2;
+        const float* hr = s_hlp + row * (TN + 1);
+        const float* wr = s_w + j * (TN + 1);
+        float acc = 0.f;
+#pragma unroll 16
+        for (int cc = 0; cc < TN; ++cc) acc = fmaf(hr[cc], wr[cc], acc);
+        st_wt(part + e, acc);
+      }
+      // the finishing tile's bias and noise, loaded by every folding tile before its arrival
+      const int e = tid, row = e / A, j = e - (e / A) * A, m = hm0 + row;
+      const bool live = e < kHeadsFoldTM * A && m < ha.rows;
+      float bm = 0.f, bl = 0.f, eps_in = 0.f;
+      {
+        const int jj = live ? j : 0, mm = live ? m : 0;
+        const rsrc_t rB = make_rsrc(ha.Wh, (uint32_t)(((size_t)(n2 - 1) * ha.ldw + ha.K + 1) * 4));
+        bm = buf_ld(rB, (uint32_t)((size_t)jj * ha.ldw + ha.K) * 4u);
+        bl = buf_ld(rB, (uint32_t)((size_t)(A + jj) * ha.ldw + ha.K) * 4u);
+        const bool want = !ha.deterministic && !ha.gen_eps;
+        eps_in = buf_ld(make_rsrc(want ? ha.eps : ha.Wh, want ? 0x7fffffffu : 0u), (uint32_t)((size_t)mm * A + jj) * 4u);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
-        int* tk = batch.heads_ticket + hm0 / kHeadsFoldTM;
+        int* tk = batch.heads_ticket + rb;
         const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_hlast = old == d.tiles_n - 1;
-        if (old == d.tiles_n - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_hlast = old == ntc - 1;
+        if (old == ntc - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
-      if (s_hlast)
-        heads_rows<48, 16, false, kHeadsFoldTM, kLdSc1>(batch.heads, hm0, hm0 / kHeadsFoldTM, red,
-                                                         reinterpret_cast<float(*)[33]>(s_hlp),
-                                                         s_hlp + kHeadsFoldTM * 33);
+      if (s_hlast) {
+        float (*lp)[33] = reinterpret_cast<float (*)[33]>(red);
+        float* s_lp = red + kHeadsFoldTM * 33;
+        const uint64_t ctr = ha.ctr_override ? ha.ctr_override : ha.sc->noise_counter;
+        if (e < kHeadsFoldTM * A) {
+          float lpe = 0.f;
+          if (live) {
+            // (a buffer descriptor on the row block's base — uniform: a per-lane base would
+            // make the compiler loop over the distinct values — and the row in the offset)
+            const float* p0 = batch.heads_part + (size_t)rb * ntc * (kHeadsFoldTM * n2);
+            const rsrc_t rP = make_rsrc(p0, (uint32_t)((size_t)ntc * kHeadsFoldTM * n2 * 4));
+            float sm[16], sl[16];   // (ntc <= 16: H <= 1024)
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+              const uint32_t o = (uint32_t)((size_t)t * kHeadsFoldTM * n2 + row * n2) * 4u;
+              sm[t] = buf_ld_aux<kLdSc1>(rP, t < ntc ? o + (uint32_t)j * 4u : 0xfffffff0u);
+              sl[t] = buf_ld_aux<kLdSc1>(rP, t < ntc ? o + (uint32_t)(A + j) * 4u : 0xfffffff0u);
+            }
+            float mean = sm[0], ls_raw = sl[0];
+#pragma unroll
+            for (int t = 1; t < 16; ++t)
+              if (t < ntc) { mean += sm[t]; ls_raw += sl[t]; }
+            lpe = heads_elem<false, kLdSc1>(ha, m, j, mean + bm, ls_raw + bl, eps_in, ctr);
+          }
+          lp[row][j] = lpe;
+        }
+        heads_logp<kHeadsFoldTM, kLdSc1>(ha, hm0, rb, lp, s_lp);
+      }
     }
   }
   SACMI_PHASE(batch.tl, 5);
@@ -3994,41 +4186,6 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// Philox4x32-10 + Box-Muller (perf-mode policy noise)
-__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-    c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-  }
-}
-
-__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t counter, uint32_t elem) {
-  uint32_t c[4] = {(uint32_t)counter, (uint32_t)(counter >> 32), elem, 0x5ac3u};
-  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  const float u1 = ((float)c[0] + 0.5f) * 2.3283064365386963e-10f;   // (0,1)
-  const float u2 = ((float)c[1] + 0.5f) * 2.3283064365386963e-10f;
-  return sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
-}
-
-constexpr float kLogSqrt2Pi = 0.91893853320467274178f;   // math.log(math.sqrt(2*pi))
-
-// 1 - tanh(x)^2 = sech(x)^2 = 4t / (1+t)^2 with t = exp(-2|x|): the reference's
-// `1 - y.pow(2)` (networks_model1.py:93) without its cancellation — for |x| ~ 4 the fp32
-// difference keeps only ~12 good bits, and those few saturated elements dominate the
-// policy gradient through 2y / (1 - y^2) (batch-4096 runs: 1e-4 normwise scatter between
-// fp32 evaluations otherwise; this form tracks the fp64 truth)
-__device__ __forceinline__ float one_minus_tanh2(float x) {
-  const float t = expf(-2.f * fabsf(x));
-  const float u = 1.f + t;
-  return 4.f * t / (u * u);
-}
-
-// ---------------------------------------------------------------------------
 // policy heads (mean | log_std) GEMM + GaussianPolicy.sample epilogue
 // (networks_model1.py:65-99, torch distributions/normal.py:83-103)
 // H16 (act16 updates): h is bf16 (widened exactly; Wh fp32, fp32 MFMAs) and the actions
@@ -4069,68 +4226,11 @@ __device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int 
     if (live) {
       const float mean = reduce_partials<TM, TN, KSPLIT>(red, row, j) + bm;
       const float ls_raw = reduce_partials<TM, TN, KSPLIT>(red, row, A + j) + bl;
-      const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
-      const float sd = expf(ls);
-      // Normal(mean, std) argument validation (networks_model1.py:87): loc must be real (not
-      // NaN) and scale positive — std = exp(clamp(log_std)) is NaN only for a NaN log_std
-      // (torch.clamp keeps NaN; fmaxf above does not, hence the raw value).  evaluate=True
-      // (deterministic) builds no Normal, so nothing is checked there (sac_imp.py:59-65).
-#if defined(SACMI_EXP_NOMFMA) || defined(SACMI_EXP_NOLOAD) || defined(SACMI_EXP_NOADAMIO) || \
-    defined(SACMI_EXP_EMPTY) || defined(SACMI_EXP_DESC) || defined(SACMI_EXP_NOSTORE)
-      if (false) {   // timing experiments compute garbage: never void their updates
-#else
-      if (a.nan_flag && !a.deterministic && (__builtin_isnan(mean) || __builtin_isnan(ls_raw))) {
-#endif
-        const int bit = m < a.split_row ? a.nan_bit_lo : a.nan_bit_hi;
-        if (a.nan_plain) *a.nan_flag = bit;
-        else atomicOr(a.nan_flag, bit);
-      }
-      float eps;
-      if (a.deterministic) {
-        eps = 0.f;
-      } else if (a.gen_eps) {
-        eps = philox_normal(a.seed, ctr, (uint32_t)(m * A + j));
-        a.eps[(size_t)m * A + j] = eps;
-      } else {
-        eps = eps_in;
-      }
-      const float x = a.deterministic ? mean : mean + eps * sd;
-      const float y = tanhf(x);
-      if constexpr (H16)
-        reinterpret_cast<unsigned short*>(a.act)[(size_t)m * a.ldact + j] = bf16_bits(y * a.scale + a.bias);
-      else   // (write-through where the same launch reads them back: k_chain_a's L3)
-        st_pol(a.act + (size_t)m * a.ldact + j, y * a.scale + a.bias, AAUX != 0);
-      if (a.act_host) a.act_host[(size_t)m * A + j] = y * a.scale + a.bias;
-      const float dx = x - mean;
-      lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
-      const float omy2 = one_minus_tanh2(x);
-      lpe -= logf(a.scale * omy2 + 1e-6f);
-      float* cr = a.cache + (size_t)m * 3 * A;
-      cr[j] = omy2; cr[A + j] = ls_raw; cr[2 * A + j] = y;
+      lpe = heads_elem<H16, AAUX>(a, m, j, mean, ls_raw, eps_in, ctr);
     }
     lp[row][j] = lpe;
   }
-  __syncthreads();
-  if (threadIdx.x < TM) {
-    const int mm = m0 + threadIdx.x;
-    float s = 0.f;
-    if (mm < a.rows) {
-      for (int jj = 0; jj < A; ++jj) s += lp[threadIdx.x][jj];
-      st_pol(a.logp + mm, s, AAUX != 0);
-    }
-    s_lp[threadIdx.x] = s;
-  }
-  if (a.logp_part) {
-    __syncthreads();
-    if (threadIdx.x < 2) {    // rows below / at-or-above split_row, fixed order
-      float s = 0.f;
-      for (int r = 0; r < TM; ++r) {
-        const int mm = m0 + r;
-        if (mm < a.rows && (mm >= a.split_row) == (threadIdx.x == 1)) s += s_lp[r];
-      }
-      a.logp_part[2 * part + threadIdx.x] = s;
-    }
-  }
+  heads_logp<TM, AAUX>(a, m0, part, lp, s_lp);
 }
 
 template <int TN, int KSPLIT, bool H16 = false, int TM = 16>
@@ -4800,6 +4900,7 @@ bool gemm_level_heads_fold_ok(const GemmBatch& b0, int A) {
     n_adam += d.epi >= EPI_ADAM;
     outs += (int64_t)d.M * d.N;
     if (d.a16 || d.b16 || d.c16 || d.x16) return false;
+    if (d.N > 1024) return false;   // (at most 16 column tiles' shares per row block)
   }
   const int t64 = assign_tiles<32, 64>(b);
   // launch_gemm's <32, 64, 16, 2, 1> branch, with write-through stores (st_wt: outs <= 1 M)

@@ -222,6 +222,7 @@ struct sacmi_ctx {
   // arrival counts per 32-row block (zero between launches), and the batch size whose
   // update folds them (the actor phase sizes its log-prob partials from it)
   sacmi::DevBuf<int> heads_ticket;
+  sacmi::DevBuf<float> heads_part;   // the folded heads' split-K shares (GemmBatch::heads_part)
   int heads_fold_B = -1;
   // act scratch
   int act_rows = 0;
@@ -511,6 +512,7 @@ static void alloc_all(sacmi_ctx* c) {
   c->lpart_c.alloc((size_t)nrb * 2); c->lpart_a.alloc(nrb);
   c->lp_part.alloc((size_t)2 * ((2 * Bm + 15) / 16) + 2);   // heads: per-workgroup logp sums
   c->heads_ticket.alloc((size_t)(2 * Bm + kHeadsFoldTM - 1) / kHeadsFoldTM);
+  c->heads_part.alloc((size_t)(2 * Bm + kHeadsFoldTM - 1) / kHeadsFoldTM * ((c->H + 63) / 64) * kHeadsFoldTM * 2 * c->A);
   hipStream_t s = c->stream;
   // constant-1 (bias) columns
   set_column_checked(c->xq.p, Bm, c->Kx, S, 1.f, s);
@@ -726,11 +728,13 @@ static void validate_batch(const GemmBatch& b) {
   }
 }
 
-// the policy heads folded into the last policy hidden layer's level where launch_gemm can —
-// opt-in (SACMI_HEADS_FOLD=1): the fold runs the heads behind the level's last tile of each
-// row block, serially, and measured slower than the separate heads launch (config 2: L2
-// 11.1 -> 20.1 us with the fold, 8,850 -> 8,669 steps/s; profiles/r05/heads_fold_ab).
-// (read per enqueue: tests switch it between contexts)
+// the policy heads folded into the last policy hidden layer's level where launch_gemm can
+// (gemm_level_heads_fold_ok; kg_body: every policy tile's share of the head sums, the last
+// column tile of a row block sums them and samples) — opt-in, SACMI_HEADS_FOLD=1: both fold
+// forms measured slower than the separate heads launch at config 2 (the last tile running
+// the whole heads GEMM: L2 11.1 -> 20.1 us, 8,850 -> 8,669 steps/s; the split shares:
+// L2 11.8 -> 19.7 us, 8,740 -> 8,644 — profiles/r05/heads_fold_ab, heads_split_ab).  Read per
+// enqueue: tests switch it between contexts.
 static bool heads_fold_wanted() {
   const char* e = std::getenv("SACMI_HEADS_FOLD");
   const char* n = std::getenv("SACMI_NO_HEADS_FOLD");
@@ -1162,6 +1166,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       a2.b.heads_desc = 0;
       a2.b.heads_ndesc = 2;
       a2.b.heads_ticket = c->heads_ticket.p;
+      a2.b.heads_part = c->heads_part.p;
       for (int i = 0; i < 2; ++i)
         a3.add(fw(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, E(c->hqt[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
       for (int i = 0; i < 2; ++i)
@@ -1198,6 +1203,9 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
         lv.b.heads_desc = 0;   // (the policy desc, added first)
         lv.b.heads_ndesc = 1;
         lv.b.heads_ticket = c->heads_ticket.p;
+        lv.b.heads_part = c->heads_part.p;
+        check_span(c->heads_part.p, (int64_t)((2 * B + kHeadsFoldTM - 1) / kHeadsFoldTM) * ((H + 63) / 64) *
+                                        kHeadsFoldTM * 2 * A - 1, "heads_part");
         folded = true;
       }
       run(lv, l == 1 ? "gemm_L2_fc2" : "gemm_L2b_fc3");
@@ -1974,7 +1982,7 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (int l = 0; l < 3; ++l)
       for (auto* b : {&c->hp[l], &c->hq[l], &c->hqt[l], &c->hqa[l], &c->dhc[l], &c->dha[l], &c->dhp[l]})
         b->release();
-    c->heads_ticket.release();
+    c->heads_ticket.release(); c->heads_part.release();
     c->sc.release(); c->mt.release(); c->mt_backup.release(); c->mt_pf.release(); c->idx32.release(); c->idx64.release();
     c->Ph.release(); c->Th.release();
     c->chain_pool.release(); c->chain_sync.release();

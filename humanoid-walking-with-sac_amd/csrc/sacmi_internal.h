@@ -468,13 +468,15 @@ struct GemmBatch {
   tl_word* tl;         // launch timeline slots of this level (kTlPerSite), or null
   int st_wt;           // k_gemm epilogue stores write-through (set by launch_gemm)
   // the policy heads + sample folded into the level that produces the last policy hidden
-  // layer (k_gemm's fp32 32x64 forward tiles, gemm_level_heads_fold_ok): the last column
-  // tile of each 32-row block to finish (heads_ticket[row block]: an arrival count, reset
-  // by that tile) runs them for the block's rows
+  // layer (k_gemm's fp32 32x64 forward tiles, gemm_level_heads_fold_ok): every policy tile
+  // stores its columns' share of the heads (heads_part), and the last column tile of each
+  // 32-row block to arrive (heads_ticket[row block]: an arrival count, reset by that tile)
+  // sums the shares and runs the sample for the block's rows
   HeadSampleArgs heads;
   int heads_desc;      // the (first) policy desc of the level
   int heads_ndesc;     // policy descs (stacked rows: desc heads_desc + i holds rows i * M ..)
   int* heads_ticket;   // or null: no fold
+  float* heads_part;   // [row block][column tile][32][2A]: the tiles' shares of the heads
   // data-parallel phase 0's last level: block 0 stores the error flags (kDpFlagN) of
   // *err_word here, before the critic gradient collective (null: none)
   float* err_flags;
