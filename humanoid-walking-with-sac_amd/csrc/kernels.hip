@@ -1443,16 +1443,18 @@ constexpr int stg_ring() {
   else return 1;
 }
 // LDS of one k_gemm configuration (kg_body)
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE>
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, bool HFOLD = false>
 constexpr bool kg_heads_fold() {
-  return !ADAM && AXK == 0 && CORE == 0 && !BF16 && MG == 1 && TM == kHeadsFoldTM && TN == 64 &&
+  // (an instantiation of its own: the fold's registers and code cost the plain levels of
+  // this tile configuration ~0.6-0.8 us each when compiled in)
+  return HFOLD && !ADAM && AXK == 0 && CORE == 0 && !BF16 && MG == 1 && TM == kHeadsFoldTM && TN == 64 &&
          KSPLIT == 16 && G == 2;
 }
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE>
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, bool HFOLD = false>
 struct KgSmem {
   static constexpr int TMW = TM * MG;
   static constexpr bool PA = AXK == 1 && MG == 1;
-  static constexpr bool HF = kg_heads_fold<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>();
+  static constexpr bool HF = kg_heads_fold<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, HFOLD>();
   alignas(16) unsigned char ring[stg_ring<CORE, TMW, TN, KSPLIT>()];
   float red_l[CORE ? 1 : MG * KSPLIT * TM * (TN + 1)];
   float s_kw[CORE ? kStgKW : 1];
@@ -1475,9 +1477,9 @@ struct KgSmem {
 // weights' loads and before the A operand's (gemm_core_l), or before a return that loads
 // nothing; every workgroup that calls the body with it reaches both once.
 template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, int LDAUX,
-          bool MIDSPLIT = false, class Mid = void (*)()>
+          bool MIDSPLIT = false, bool HFOLD = false, class Mid = void (*)()>
 __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in,
-                                        KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>& sm,
+                                        KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, HFOLD>& sm,
                                         Mid&& mid = [] {}) {
   if constexpr (MIDSPLIT) mid.issue();   // (k_chain: the barrier's first poll, ahead of every load)
   // The scalars that locate this workgroup's work come in ONE kernarg round trip: left to
@@ -1539,7 +1541,7 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   constexpr bool PA = AXK == 1 && MG == 1;
   float* const s_pa = sm.s_pa;
   // the policy heads folded into this level (GemmBatch::heads): the fp32 32x64 forward tiles
-  constexpr bool HF = kg_heads_fold<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE>();
+  constexpr bool HF = kg_heads_fold<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, HFOLD>();
   float* const s_hlp = sm.s_hlp;
   int& s_hlast = sm.s_hlast;
   const int bid = bid_in;
@@ -2052,11 +2054,12 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   SACMI_PHASE(batch.tl, 5);
 }
 
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false, int CORE = 0>
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false, int CORE = 0,
+          bool HFOLD = false>
 __global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_GEMM);
-  __shared__ KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE> sm;
-  kg_body<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, 0>(batch, blockIdx.x, sm);
+  __shared__ KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, HFOLD> sm;
+  kg_body<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, 0, false, HFOLD>(batch, blockIdx.x, sm);
 }
 
 // Tile order and XCD placement.  Workgroups are dealt round-robin over the 8 XCDs
@@ -4176,8 +4179,12 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
     const int g = grid_for(assign_tiles<32, 32>(b));
     launch_k<32, 32, 16, 2, 1, false, 1>(b, g, s);
   } else if (t64 >= 192) {
-    // widest tile that still gives one workgroup to most CUs
-    launch_k<32, 64, 16, 2, 1, false, 0>(b, grid_for(b.total_tiles), s);
+    // widest tile that still gives one workgroup to most CUs (the folded-heads instantiation
+    // where the level carries the fold)
+    if (b.heads_ticket && !b.bf16)
+      hipLaunchKernelGGL((k_gemm<32, 64, 16, 2, 1, false, 0, false, 0, true>), dim3(grid_for(b.total_tiles)), dim3(1024), 0, s, b);
+    else
+      launch_k<32, 64, 16, 2, 1, false, 0>(b, grid_for(b.total_tiles), s);
   } else {
     const int g = grid_for(assign_tiles<32, 32>(b));
     launch_k<32, 32, 16, 2, 1, false, 0>(b, g, s);
@@ -4736,7 +4743,7 @@ __global__ __launch_bounds__(1024, 4) void k_chain(const ChainArgs* __restrict__
 
 // the critic pass (ChainArgs kind 1): L1 / L2 on 32x64 tiles (L2 with the policy heads
 // folded in), L3 / L4 on 32x32, L5 (row prologue, A transform) on 32x32
-using ChainKgW = KgSmem<32, 64, 16, 2, 1, false, 0, false, 0>;
+using ChainKgW = KgSmem<32, 64, 16, 2, 1, false, 0, false, 0, true>;   // (L2 carries the heads)
 union ChainSmemA {
   ChainKgW w;
   ChainKgA a;
@@ -4756,14 +4763,14 @@ __global__ __launch_bounds__(1024, 4) void k_chain_a(const ChainArgs* __restrict
   // L1: 32x64 tiles
   {
     const GemmBatch& b = chain_args(ca)->lv[0];
-    if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, bid, sm.w);
+    if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1, false, true>(b, bid, sm.w);
     chain_end(sync);
     SACMI_PHASE(tl, 1);
   }
   // L2 (+ the heads): 32x64 tiles, barrier 0 behind its weight loads
   {
     const GemmBatch& b = chain_args(ca)->lv[1];
-    if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.w, waiter(0, true));
+    if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1, true, true>(b, bid, sm.w, waiter(0, true));
     chain_end(sync + 32);
     SACMI_PHASE(tl, 2);
   }
