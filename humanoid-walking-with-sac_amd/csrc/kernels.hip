@@ -4481,7 +4481,7 @@ struct TailSmem {
 // One unit: rows [m0, m0 + 8) x dhp2 columns [c0, c0 + 64), by the first 256 threads of the
 // workgroup (any others only join its barriers).  slab0: the unit also stores dhead.  AUX:
 // cache-policy bits of the dL/da partial loads (k_chain: sc1 — L9 wrote them in the same launch)
-template <int AUX, bool MIDSPLIT = false, class Mid = void (*)()>
+template <int AUX, bool MIDSPLIT = false, int NPA = kTailMaxPa, class Mid = void (*)()>
 __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const SampleBwdArgs& a, int m0,
                                           int c0, bool slab0, TailSmem& sm, Mid&& mid = [] {}) {
   if constexpr (MIDSPLIT) mid.issue();   // (k_chain: the barrier's first poll, as kg_body's)
@@ -4527,9 +4527,11 @@ __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const Sampl
   mid();
   const rsrc_t rP = make_rsrc(pa, (uint32_t)((size_t)n_pa * B * A * 4));
   const uint32_t pstride = (uint32_t)B * (uint32_t)A * 4u, po = (uint32_t)((own ? pm : 0) * A + pj) * 4u;
-  float t[kTailMaxPa];
+  // (NPA >= n_pa partial loads per thread: the launcher picks the smallest instantiation, so
+  // no issue slots go to out-of-range loads)
+  float t[NPA];
 #pragma unroll
-  for (int q = 0; q < kTailMaxPa; ++q)
+  for (int q = 0; q < NPA; ++q)
     t[q] = buf_ld_aux<AUX>(rP, own && q < n_pa ? po + (uint32_t)q * pstride : 0xfffffff0u);
   if (act) {
     for (int e = tid; e < kTailRows * 65; e += 256) (&s_dh[0][0])[e] = 0.f;
@@ -4543,7 +4545,7 @@ __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const Sampl
   if (own) {
     float ga = 0.f;                                 // fixed order over the column blocks
 #pragma unroll
-    for (int q = 0; q < kTailMaxPa; ++q)
+    for (int q = 0; q < NPA; ++q)
       if (q < n_pa) ga += t[q];
     const float glogp = a.sc->alpha / (float)B;
     const float ls = fminf(fmaxf(ls_raw, -20.f), 2.f);
@@ -4585,10 +4587,11 @@ __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const Sampl
 // per-element algebra as k_gemm_sample_bwd; the slab-0 workgroups store dhead (the heads'
 // weight-gradient operand); dhp2 = (dhead Whead) * [hp2 > 0] for the slab.  Every
 // workgroup of a row block recomputes the row block's dhead (a few hundred FMAs).
+template <int NPA>
 __global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_pa, SampleBwdArgs a) {
   const TlMark tl_mark(a.tl, TL_SAMPLE_TAIL);
   __shared__ TailSmem sm;
-  tail_unit<0>(pa, n_pa, a, blockIdx.x * kTailRows, blockIdx.y * kTailCols, blockIdx.y == 0, sm);
+  tail_unit<0, false, NPA>(pa, n_pa, a, blockIdx.x * kTailRows, blockIdx.y * kTailCols, blockIdx.y == 0, sm);
 }
 
 void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, hipStream_t s) {
@@ -4596,7 +4599,9 @@ void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, h
     throw Error{SACMI_EVALUE, "sample backward tail: unsupported action_dim / hidden_dim"};
   if (a.hp2_16) throw Error{SACMI_ESTATE, "sample backward tail: bf16 hp2 not supported"};
   const dim3 grid((a.B + kTailRows - 1) / kTailRows, (a.H + kTailCols - 1) / kTailCols);
-  hipLaunchKernelGGL(k_sample_bwd_tail, grid, dim3(256), 0, s, pa, n_pa, a);
+  if (n_pa <= 16) hipLaunchKernelGGL(k_sample_bwd_tail<16>, grid, dim3(256), 0, s, pa, n_pa, a);
+  else if (n_pa <= 32) hipLaunchKernelGGL(k_sample_bwd_tail<32>, grid, dim3(256), 0, s, pa, n_pa, a);
+  else hipLaunchKernelGGL(k_sample_bwd_tail<kTailMaxPa>, grid, dim3(256), 0, s, pa, n_pa, a);
   HIP_LAUNCH_CHECK();
 }
 
