@@ -1393,8 +1393,13 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     }
     Level l12, l13;
     l12.add(dh(gd(c->dhp[1].p, H, 1, W(c->p_fc[1]), Hd, 0, c->dhp[0].p, H, B, H, H, EPI_MASK, hpa(0), Hd)));
-    if (ride_b) {   // ... and its gather in L12 (256 of 512 slots at config 5), a row a wave
-      l12.b.ride.kind = 2; l12.b.ride.nblocks = (B + 7) / 8;   // (8 waves)
+    if (ride_b) {   // ... and its gather in L12, two rows a wave: 256 ride workgroups at config
+      // 5, the slots L12's 256 tiles leave free (512 at 2 per CU) — one round; a row a wave
+      // (512 workgroups, SACMI_RIDE_GATHER_ROWS=8) takes a second round: 3,255 vs 3,282
+      // updates/s (profiles/r05/ride_rows_ab; the ride's 22 MB cost L12 ~8 us either way)
+      const char* rr = std::getenv("SACMI_RIDE_GATHER_ROWS");
+      const int rows_per_block = rr && std::atoi(rr) > 0 ? std::atoi(rr) : 16;   // (8 waves)
+      l12.b.ride.kind = 2; l12.b.ride.nblocks = (B + rows_per_block - 1) / rows_per_block;
       l12.b.ride.ga = gather_args(c, B, batch_bufs(c, parity ^ 1), false);
     }
     // same level structure fused or not: identical reduction order
