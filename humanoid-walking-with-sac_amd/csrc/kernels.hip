@@ -2897,6 +2897,12 @@ __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batc
   // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
   const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
   const bool want_rs = d.rs_col >= 0 && n0 == 0;
+  // axk 2 (act16): A is the bf16 activation h [k][m] and the operand is u = [h > 0] w[m]
+  // (w: ax_w, M % 4 == 0) — the values L5 would have stored as u rows.  Both loads are
+  // issued on every pass, the unused one at an out-of-range offset: no branch around them
+  const bool axt = d.axk == 2;
+  const rsrc_t rAh = make_rsrc(axt ? d.A : d.C, axt ? 0x7fffffffu : 0u);
+  const float4 w3v = axt ? buf_ld4(make_rsrc(d.ax_w, (uint32_t)M * 4u), (uint32_t)ma * 4u) : float4{0.f, 0.f, 0.f, 0.f};
   float4 ga[NI], gb[X16 ? 1 : NI];
   uint2 gbh[X16 ? NI : 1];
   float rs4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -2906,7 +2912,12 @@ __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batc
       const int k = k0 + kr0 + KRP * i;
       const bool kin = k < ke;
       const uint32_t kk = (uint32_t)(kin ? k : 0);   // row 0 always exists (a split may start past K)
-      float4 x = buf_ld4(rA, (kk * (uint32_t)d.lda + (uint32_t)ma) * 4u);
+      const uint32_t ea = kk * (uint32_t)d.lda + (uint32_t)ma;
+      float4 x = buf_ld4(rA, axt ? 0xfffffff0u : ea * 4u);
+      const uint2 hx = buf_ld2(rAh, axt ? ea * 2u : 0xfffffff0u);
+      if (axt)
+        x = make_float4(bf16_lo(hx.x) > 0.f ? w3v.x : 0.f, bf16_hi(hx.x) > 0.f ? w3v.y : 0.f,
+                        bf16_lo(hx.y) > 0.f ? w3v.z : 0.f, bf16_hi(hx.y) > 0.f ? w3v.w : 0.f);
       const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
       // columns past M / N (and rows past this split's K range) contribute zero
       x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
@@ -3827,7 +3838,8 @@ static int dw_split_plan(GemmBatch& b, int64_t* stride) {
   int tiles = 0;
   for (int i = 0; i < b.count; ++i) {
     GemmDesc& d = b.d[i];
-    if (d.a_kc || d.b_kc || d.axk || d.K < 2048) return 0;
+    if (d.a_kc || d.b_kc || d.K < 2048) return 0;
+    if (d.axk && !(d.axk == 2 && b.bf16 && SACMI_DW_LDS16)) return 0;   // (axk 2: k_dw_part16 only)
     if (d.epi != EPI_STORE && d.epi < EPI_ADAM) return 0;
     // k_dw_fin's 4-column groups: the row-sum column is the bias column right after the
     // last output column, and output rows (and their Adam state) are 16-byte aligned with
@@ -3943,7 +3955,7 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
       const int form = level_act16(b);   // act16: every X operand bf16
       for (int i = 0; i < b.count; ++i)
-        if (b.d[i].a16 || b.d[i].c16 || b.d[i].x16 || (form && !b.d[i].b16) || form < 0)
+        if ((b.d[i].a16 && b.d[i].axk != 2) || b.d[i].c16 || b.d[i].x16 || (form && !b.d[i].b16) || form < 0)
           throw Error{SACMI_ESTATE, "split-K weight gradient: unsupported bf16 activation operand"};
       if (form && !(b.bf16 && SACMI_DW_LDS16))
         throw Error{SACMI_ESTATE, "bf16 activation operands need k_dw_part16"};
@@ -4002,6 +4014,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
       return;
     }
     b = b0;
+    for (int i = 0; i < b.count; ++i)   // (no other kernel knows the dW A transform)
+      if (b.d[i].axk == 2) throw Error{SACMI_ESTATE, "dW A transform (axk 2) outside the split-K path"};
   }
   if (SACMI_AXK_LDS16) {
     const int ax = axk16_ok(b);

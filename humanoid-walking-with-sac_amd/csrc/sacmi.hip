@@ -667,8 +667,11 @@ static void validate(const GemmDesc& d) {
   } else {
     // MN-contiguous operands are read 4 columns wide from a 4-aligned start (the split-K
     // dW kernels): the span covers the last such group
-    REQUIRE(!d.a16, SACMI_ESTATE, "bf16 A operands are K-contiguous");
-    check_span(d.A, (int64_t)(d.K - 1) * d.lda + ((d.M - 1) & ~3) + 3, "A");
+    // (bf16 MN-contiguous A: the split-K dW kernel's transformed operand, axk 2 — 4
+    // elements = 8 bytes at a time)
+    REQUIRE(!d.a16 || d.axk == 2, SACMI_ESTATE, "bf16 A operands are K-contiguous");
+    if (d.a16 && (((uintptr_t)d.A & 7) || (d.lda & 3))) throw Error{SACMI_ESTATE, "A misaligned"};
+    check_span(d.A, (int64_t)(d.K - 1) * d.lda + ((d.M - 1) & ~3) + 3, "A", ea);
   }
   if (d.b_kc) {
     REQUIRE(!d.b16, SACMI_ESTATE, "bf16 B operands are row-contiguous (weight-gradient X)");
@@ -683,7 +686,11 @@ static void validate(const GemmDesc& d) {
   if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C", ec);
   if (d.bias) check_span(d.bias, (int64_t)(d.N - 1) * d.bias_ld, "bias");
   REQUIRE(!(d.bias && d.epi == EPI_MASK), SACMI_ESTATE, "GEMM epilogue: bias and mask are exclusive");
-  if (d.axk) {
+  if (d.axk == 2) {   // dW operand u = [A > 0] w[m] (A: bf16 activations [K][M])
+    REQUIRE(!d.a_kc && d.a16 && d.ax_w && d.M % 4 == 0 && !d.ax_out && ((uintptr_t)d.ax_w & 15) == 0,
+            SACMI_ESTATE, "dW A transform needs an MN-contiguous bf16 A and a float4-aligned w");
+    check_span(d.ax_w, d.M - 1, "ax_w");
+  } else if (d.axk) {
     REQUIRE(d.a_kc && !d.b_kc && d.ax_w, SACMI_ESTATE, "A transform needs a K-contiguous A and w");
     check_span(d.ax_w, d.K - 1, "ax_w");
     if (d.ax_out) {
@@ -692,7 +699,7 @@ static void validate(const GemmDesc& d) {
     }
   }
   if (d.a_ksc) {
-    REQUIRE(!d.a_kc && !d.axk, SACMI_ESTATE, "a_ksc needs a row-contiguous A operand");
+    REQUIRE(!d.a_kc && d.axk != 1, SACMI_ESTATE, "a_ksc needs a row-contiguous A operand");
     check_span(d.a_ksc, d.K - 1, "a_ksc");
   }
   if (d.dotp) {
@@ -1131,11 +1138,19 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     // dq_i = 2 (q_i - q^) / B; the A operand dh[L] = dq * w_head * [h[L] > 0] is formed
     // from h[L] on the fly (its coefficient-free rows u stored once by the column-tile-0
     // workgroups, for the weight gradient of layer L)
+    // u rows for layer L's weight gradient (SACMI_DW_U_TRANSFORM=1, read per enqueue, bf16
+    // activations only: none — the split-K kernel forms u = [h[L] > 0] w_head from h[L],
+    // bit-identical; measured slower: L5 24.8 -> 22.1 us but L6 59 -> 75, the part kernel's
+    // staging carrying both loads and the select; profiles/r05/dw_u_ab)
+    const bool u_rows = !act16 || std::getenv("SACMI_DW_U_TRANSFORM") == nullptr;
     Level l5;
     for (int i = 0; i < 2; ++i) {
       GemmDesc g = gd(E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dhc[L - 1].p + i * H, 2 * H,
                       B, H, H, EPI_MASK, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd);
-      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]); g.ax_out = c->dhc[L].p + i * H; g.ax_ld = 2 * H;
+      g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]); g.ax_ld = 2 * H;
+      // the coefficient-free rows u for layer L's weight gradient (or, opt-in with bf16
+      // activations, that gradient forms u = [h[L] > 0] w_head from h[L] itself: axk 2)
+      g.ax_out = u_rows ? c->dhc[L].p + i * H : nullptr;
       l5.add(dh(g));
     }
     {
@@ -1261,6 +1276,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       // weight gradient applies coef = dL/dq_i (dq) as a per-batch-row K-scale
       GemmDesc wl = dwx(gd_dw_h(c->dhc[L].p + i * H, 2 * H, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd,
                                 dst(q[i][L]), Hd, H, H, B, wepi, 1 + i));
+      if (!u_rows) {   // u = [h[L] > 0] w_head formed by the split-K kernel (L5 stored none)
+        wl.A = E(c->hq[L].p, (size_t)i * Hd); wl.lda = 2 * Hd; wl.a16 = 1;
+        wl.axk = 2; wl.ax_w = W(q[i][nh]);
+      }
       wl.a_ksc = c->dq.p + i * B;
       l6.add(wl);
       l6.add(dwx(gd_dw_h(c->dq4.p + (size_t)i * B * 4, 4, E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, dst(q[i][nh]), Hd, 1, H, B,

@@ -16,6 +16,10 @@ tiles, two critics: 256 workgroups), L12 (plain, one net: 64x128 tiles), and wit
 hidden layers the plain two-critic levels (128x128).  A level that hosts a ride (L12 of an
 update that gathers the next batch) stays on k_axk16.
 
+The layer-L weight gradient forming its operand u = [h > 0] w_head from the bf16 activation
+(opt-in, SACMI_DW_U_TRANSFORM=1: L5 stores no u rows; measured slower) against the u rows L5
+stores (the default): the same fp32 values times the same coefficients, so the same bits.
+
 k_dw_fin_p (the split-K weight gradients' fixed-order sum + Adam + Polyak on a looping grid,
 the next block's loads issued before this block's stores; opt-in, SACMI_DWFIN_P=1, measured
 slower) against k_dw_fin (one group per thread): the same per-group arithmetic, so the same
@@ -108,4 +112,11 @@ def test_dw_fin_p_bitexact_vs_dw_fin(n_hidden):
         assert {kn for kn, _ in ka[site]} >= {"k_dw_part16", "k_dw_fin_p"}, (site, ka[site])
         assert {kn for kn, _ in kb[site]} >= {"k_dw_part16", "k_dw_fin"}, (site, kb[site])
         assert "k_dw_fin_p" not in {kn for kn, _ in kb[site]}
+    assert_same(a, b)
+
+
+@pytest.mark.parametrize("n_hidden", [2, 3])
+def test_dw_u_transform_bitexact_vs_u_rows(n_hidden):
+    a, _ = run_updates(n_hidden, {"SACMI_DW_U_TRANSFORM": "1"})
+    b, _ = run_updates(n_hidden, {})
     assert_same(a, b)
