@@ -2846,7 +2846,9 @@ __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
 }
 
 // X16 (act16): the B operand (X: activations / minibatch inputs) is bf16
-template <bool X16 = false>
+// AXT: the level carries a dW A transform (axk 2, opt-in): its own instantiation, so the
+// plain form's staging pass issues no extra load
+template <bool X16 = false, bool AXT = false>
 __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_PART16);
   constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
@@ -2900,7 +2902,7 @@ __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batc
   // axk 2 (act16): A is the bf16 activation h [k][m] and the operand is u = [h > 0] w[m]
   // (w: ax_w, M % 4 == 0) — the values L5 would have stored as u rows.  Both loads are
   // issued on every pass, the unused one at an out-of-range offset: no branch around them
-  const bool axt = d.axk == 2;
+  const bool axt = AXT && d.axk == 2;
   const rsrc_t rAh = make_rsrc(axt ? d.A : d.C, axt ? 0x7fffffffu : 0u);
   const float4 w3v = axt ? buf_ld4(make_rsrc(d.ax_w, (uint32_t)M * 4u), (uint32_t)ma * 4u) : float4{0.f, 0.f, 0.f, 0.f};
   float4 ga[NI], gb[X16 ? 1 : NI];
@@ -2914,10 +2916,12 @@ __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batc
       const uint32_t kk = (uint32_t)(kin ? k : 0);   // row 0 always exists (a split may start past K)
       const uint32_t ea = kk * (uint32_t)d.lda + (uint32_t)ma;
       float4 x = buf_ld4(rA, axt ? 0xfffffff0u : ea * 4u);
-      const uint2 hx = buf_ld2(rAh, axt ? ea * 2u : 0xfffffff0u);
-      if (axt)
-        x = make_float4(bf16_lo(hx.x) > 0.f ? w3v.x : 0.f, bf16_hi(hx.x) > 0.f ? w3v.y : 0.f,
-                        bf16_lo(hx.y) > 0.f ? w3v.z : 0.f, bf16_hi(hx.y) > 0.f ? w3v.w : 0.f);
+      if constexpr (AXT) {
+        const uint2 hx = buf_ld2(rAh, axt ? ea * 2u : 0xfffffff0u);
+        if (axt)
+          x = make_float4(bf16_lo(hx.x) > 0.f ? w3v.x : 0.f, bf16_hi(hx.x) > 0.f ? w3v.y : 0.f,
+                          bf16_lo(hx.y) > 0.f ? w3v.z : 0.f, bf16_hi(hx.y) > 0.f ? w3v.w : 0.f);
+      }
       const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
       // columns past M / N (and rows past this split's K range) contribute zero
       x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
@@ -3959,7 +3963,12 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
           throw Error{SACMI_ESTATE, "split-K weight gradient: unsupported bf16 activation operand"};
       if (form && !(b.bf16 && SACMI_DW_LDS16))
         throw Error{SACMI_ESTATE, "bf16 activation operands need k_dw_part16"};
-      if (b.bf16 && SACMI_DW_LDS16 && form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
+      bool axt = false;
+      for (int i = 0; i < b.count; ++i) axt = axt || b.d[i].axk == 2;
+      if (axt && !(b.bf16 && SACMI_DW_LDS16 && form))
+        throw Error{SACMI_ESTATE, "dW A transform (axk 2) needs k_dw_part16 with bf16 X operands"};
+      if (b.bf16 && SACMI_DW_LDS16 && form && axt) hipLaunchKernelGGL((k_dw_part16<true, true>), dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
+      else if (b.bf16 && SACMI_DW_LDS16 && form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
       else if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
       else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
       else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
