@@ -568,7 +568,7 @@ __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, flo
   constexpr int AX = AAUX ? AAUX : SACMI_A_AUX;
   constexpr bool MS = MIDSPLIT;
   if constexpr (AXK == 1) {
-    if (d.axk == 1) {        // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
+    if (d.axk == 1 && !d.ax_pre) {   // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
       gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1, BF16, 0, false, AX, MS>(
           d, m0, n0, red, rsum, pre, n0 == 0 && d.ax_out != nullptr, early);
       return;
@@ -1671,6 +1671,9 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   const uint32_t span = (uint32_t)(((size_t)(d.M - 1) * d.ldc + (d.rs_col >= ncov ? d.rs_col + 1 : ncov)) * 4);
   const size_t abase = ADAM ? (size_t)(d.C - af.P) : 0;
   const rsrc_t rC = make_rsrc(d.C, span);
+  // u rows (GemmDesc::u_out): a zero-length range where the desc stores none
+  const rsrc_t rU = make_rsrc(d.u_out ? d.u_out : d.C,
+                              d.u_out ? (uint32_t)(((size_t)(d.M - 1) * d.u_ld + d.N) * 4) : 0u);
   // (unused descriptors get a zero-length range: any access through them is dropped)
   const rsrc_t rM = make_rsrc(ADAM ? af.M + abase : d.C, ADAM ? span : 0);
   const rsrc_t rV = make_rsrc(ADAM ? af.V + abase : d.C, ADAM ? span : 0);
@@ -1916,6 +1919,8 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
         if (v == 12345.f)   // timing experiment only: no output stores
 #endif
         buf_st_pol(rC, o, v, wt);
+        if (d.u_out && s < EPT)   // u rows (u_out)
+          buf_st_pol(rU, (uint32_t)((m0 + row) * d.u_ld + n) * 4u, v > 0.f ? s_dotw[col] : 0.f, wt);
       }
     }
     if constexpr (!ADAM) {

@@ -493,7 +493,7 @@ static void alloc_all(sacmi_ctx* c) {
     c->hp[l].alloc((size_t)2 * Bm * c->Hd);
     for (auto* b : {&c->hq[l], &c->hqt[l], &c->hqa[l]}) b->alloc((size_t)Bm * 2 * c->Hd);
     c->dhc[l].alloc((size_t)Bm * 2 * H);
-    if (l < nh - 1) c->dha[l].alloc((size_t)Bm * 2 * H);
+    c->dha[l].alloc((size_t)Bm * 2 * H);   // (dha[L]: the actor pass's u rows, L8's u_out)
     c->dhp[l].alloc((size_t)Bm * H);
   }
   c->eps.alloc((size_t)2 * Bm * A);
@@ -686,6 +686,11 @@ static void validate(const GemmDesc& d) {
   if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C", ec);
   if (d.bias) check_span(d.bias, (int64_t)(d.N - 1) * d.bias_ld, "bias");
   REQUIRE(!(d.bias && d.epi == EPI_MASK), SACMI_ESTATE, "GEMM epilogue: bias and mask are exclusive");
+  if (d.u_out) {
+    REQUIRE(d.dotp && !d.c16 && d.epi == EPI_RELU, SACMI_ESTATE, "u rows come from an fp32 forward level with dot partials");
+    check_span(d.u_out, (int64_t)(d.M - 1) * d.u_ld + d.N - 1, "u_out");
+  }
+  if (d.ax_pre) REQUIRE(d.axk == 1 && !d.ax_out && !d.a16, SACMI_ESTATE, "pre-formed A transform: an fp32 axk-1 GEMM");
   if (d.axk == 2) {   // dW operand u = [A > 0] w[m] (A: bf16 activations [K][M])
     REQUIRE(!d.a_kc && d.a16 && d.ax_w && d.M % 4 == 0 && !d.ax_out && ((uintptr_t)d.ax_w & 15) == 0,
             SACMI_ESTATE, "dW A transform needs an MN-contiguous bf16 A and a float4-aligned w");
@@ -1084,6 +1089,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   };
   // activation buffers: element offsets in the update's activation format
   const bool act16 = act16_on(c, B);
+  // fp32: the critic / actor u rows (u = [h[L] > 0] w_head) stored by the last forward level
+  // (L2 / L8, which holds w_head for its dot partials) and read by L5 / L9 as a plain A
+  // operand — no transform in their K loops, no u stores in L5 (SACMI_NO_PRE_U=1: the
+  // transform form; read per enqueue)
+  const bool pre_u = !c->bf16 && std::getenv("SACMI_PRE_U") != nullptr && std::getenv("SACMI_NO_PRE_U") == nullptr;
   const int a16 = act16 ? 1 : 0;
   auto E = [&](float* base, size_t off) -> float* {
     return act16 ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(base) + off) : base + off;
@@ -1149,8 +1159,10 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
                       B, H, H, EPI_MASK, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd);
       g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]); g.ax_ld = 2 * H;
       // the coefficient-free rows u for layer L's weight gradient (or, opt-in with bf16
-      // activations, that gradient forms u = [h[L] > 0] w_head from h[L] itself: axk 2)
-      g.ax_out = u_rows ? c->dhc[L].p + i * H : nullptr;
+      // activations, that gradient forms u = [h[L] > 0] w_head from h[L] itself: axk 2);
+      // fp32 (pre_u): L2 stored them already, and this level reads them as its A operand
+      g.ax_out = u_rows && !pre_u ? c->dhc[L].p + i * H : nullptr;
+      if (pre_u) { g.A = c->dhc[L].p + i * H; g.lda = 2 * H; g.ax_pre = 1; }
       l5.add(dh(g));
     }
     {
@@ -1210,7 +1222,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       for (int i = 0; i < 2; ++i) {
         GemmDesc g = fw(gd_fwd_h(E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd, W(q[i][l]), Hd,
                                  E(c->hq[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
-        lv.add(l == L ? with_dot(g, W(q[i][nh]), i) : g);
+        if (l == L) {
+          g = with_dot(g, W(q[i][nh]), i);
+          if (pre_u) { g.u_out = c->dhc[L].p + i * H; g.u_ld = 2 * H; }   // (L5's A, L6's u rows)
+        }
+        lv.add(g);
       }
       lv.b.bf16 = c->bf16 ? 1 : 0;   // (the gate reads the level's MFMA operand type, as run() sets it)
       if (l == L && heads_fold_wanted() && gemm_level_heads_fold_ok(lv.b, A)) {
@@ -1333,7 +1349,11 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       for (int i = 0; i < 2; ++i) {
         GemmDesc g = fw(gd_fwd_h(E(c->hqa[l - 1].p, (size_t)i * Hd), 2 * Hd, W(q[i][l]), Hd,
                                  E(c->hqa[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
-        lv.add(l == L ? with_dot(g, W(q[i][nh]), 4 + i) : g);
+        if (l == L) {
+          g = with_dot(g, W(q[i][nh]), 4 + i);
+          if (pre_u) { g.u_out = c->dha[L].p + i * H; g.u_ld = 2 * H; }   // (L9's A)
+        }
+        lv.add(g);
       }
       l8s.push_back(lv);
     }
@@ -1345,6 +1365,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       GemmDesc g = gd(E(c->hqa[L].p, (size_t)i * Hd), 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dha[L - 1].p + i * H, 2 * H,
                       B, H, H, EPI_MASK, E(c->hqa[L - 1].p, (size_t)i * Hd), 2 * Hd);
       g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]);
+      if (pre_u) { g.A = c->dha[L].p + i * H; g.lda = 2 * H; g.ax_pre = 1; }   // (L8 stored u)
       l9.add(dh(g));
     }
     {

@@ -281,6 +281,14 @@ struct GemmDesc {
   const float* ax_w;
   float* ax_out;
   int ax_ld;
+  // ax_pre (axk 1, fp32): A already holds u — the producing level stored it (u_out) — so the
+  // K loop reads it as a plain operand (the row prologue, coefficient and mask stay)
+  int ax_pre;
+  // u_out (a forward level with fc3 dot partials, fp32): also store u(b,n) = [C(b,n) > 0] *
+  // dotw[n] (row stride u_ld) — the next dh level's A operand (ax_pre) and the critic weight
+  // gradient's u rows
+  float* u_out;
+  int u_ld;
   // A row-contiguous only: a(m,k) *= a_ksc[k] (per-K scale, e.g. dh2 = coef (x) u for the
   // critic fc2 weight gradient)
   const float* a_ksc;

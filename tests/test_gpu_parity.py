@@ -1358,3 +1358,47 @@ def test_step_humanoid_b4096_under_gpu_masks(n_hidden):
     bad = {k: e for k, (e, _) in table.items() if e > MASKED_GRAD_TOL}
     assert not bad, bad
     ctx.close()
+
+
+@pytest.mark.parametrize("n_hidden,B", [(2, 256), (3, 256), (2, 4096)])
+def test_pre_formed_u_matches_transform(n_hidden, B):
+    """fp32: the last forward levels (L2 / L8) store u = [h > 0] w_head beside h, and L5 / L9
+    read u as a plain A operand (and L6 reads the same u rows) — against L5 / L9 forming u
+    from h in their K loops (SACMI_NO_PRE_U=1): the same A values, so the same sums: losses,
+    parameters, gradients and Adam moments bit-identical, over injected-noise, device-sampled
+    and multi-update launches."""
+    cfg = SacConfig(376, 17, 512, n_hidden=n_hidden)
+    params = init_params(cfg, 171, bias_scale=0.02)
+    rows = synthetic_rows(cfg, max(3000, B + 1000), 172, state_scale=0.1)
+    rng = np.random.default_rng(173)
+    idx = rng.choice(len(rows[2]), B, replace=False)
+    e1 = rng.standard_normal((B, 17)).astype(np.float32)
+    e2 = rng.standard_normal((B, 17)).astype(np.float32)
+    key = (np.arange(624, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32)
+    res = []
+    for env in ({"SACMI_PRE_U": "1"}, {}):
+        os.environ.update(env)
+        try:
+            ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]))
+            load_params(ctx, params)
+            ctx.push(*rows)
+            ctx.set_mt(0, key, 624)
+            out = [ctx.step(B, idx=idx, eps1=e1, eps2=e2), ctx.step(B)]
+            ctx.step_many_async(B, 3)
+            out.append(ctx.fetch_losses(3).ravel())
+            st = ctx_state(ctx, cfg)
+            g = ctx_grads(ctx, cfg)
+            mom = {f"{n}.{slot}.{k}": v for n in ("policy", "q1", "q2") for slot in ("m", "v")
+                   for k, v in ctx.get_net(n, slot).items()}
+            res.append((out, st, g, mom))
+            ctx.close()
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+    (oa, sa, ga, ma), (ob, sb, gb, mb) = res
+    for a, b in zip(oa, ob):
+        assert np.array_equal(a, b)
+    for d1, d2 in ((sa, sb), (ga, gb), (ma, mb)):
+        assert d1.keys() == d2.keys()
+        for k in d1:
+            assert np.array_equal(d1[k], d2[k]), k
