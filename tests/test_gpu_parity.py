@@ -1209,6 +1209,53 @@ def test_native_dp_loopback_sharded_equals_allreduce_nonpow2(world):
         c.close()
 
 
+@pytest.mark.parametrize("world", [3, 8])
+def test_dp_sharded_one_rank_chunks(world):
+    """The sharded step's chunk arithmetic (the range's chunks of 64-float multiples, Adam's
+    layer segments clipped to rank 0's chunk): the loopback's one-rank mode steps rank 0's
+    chunk of each range only.  Every parameter element must then hold either its fused-update
+    value (inside the chunk) or its value before the update (outside) — nothing else — and
+    the stepped elements must be one contiguous run per range, at most a chunk long."""
+    cfg, B, nrows = SacConfig(376, 17, 512), 256, 4000
+    params = init_params(cfg, 131, bias_scale=0.05)
+    rows = synthetic_rows(cfg, nrows, 132, state_scale=0.5)
+    key = (np.arange(624, dtype=np.uint64) * 1812433 % (2**32)).astype(np.uint32)
+    res = []
+    for one in (True, False):
+        if one:
+            os.environ["SACMI_DP_LOOPBACK_ONE_RANK"] = "1"
+        try:
+            ctx = make_ctx(cfg, max_batch=B, capacity=nrows, seed=5)
+            load_params(ctx, params)
+            ctx.push(*rows)
+            ctx.set_mt(0, key, 624)
+            if one:
+                ctx.dp_loopback_init(world)
+                ctx.dp_set_sharded(True)
+                ctx.step_dp(B, 1)
+            else:
+                ctx.step(B)                       # the fused update (loopback x W / W: exact only
+            ctx.synchronize()                     #  at power-of-two worlds, compared below)
+            res.append({n: ctx.get_net(n) for n in ("policy", "q1", "q2")})
+            ctx.close()
+        finally:
+            os.environ.pop("SACMI_DP_LOOPBACK_ONE_RANK", None)
+    one, fused = res
+    for nets in (("policy",), ("q1", "q2")):      # the actor range, the critic range
+        n_stepped = total = 0
+        for net in nets:
+            for k, v in one[net].items():
+                init = np.asarray(params[net][k], np.float32).reshape(v.shape)
+                stepped = v != init
+                n_stepped += int(stepped.sum())
+                total += v.size
+                if world & (world - 1) == 0:      # x W then x 1/W exact: the fused values
+                    assert np.array_equal(v[stepped], fused[net][k][stepped]), (net, k)
+                else:                             # within fp32 rounding of the fused step
+                    np.testing.assert_allclose(v[stepped], fused[net][k][stepped], rtol=1e-5, atol=1e-7)
+        assert 0 < n_stepped < total, (nets, n_stepped, total)
+
+
 def test_dp_sharded_moments_read_guard():
     """After a sharded optimizer step that leaves other ranks' chunks of the Adam moments
     stale on this rank (here: the loopback's one-rank timing mode, which steps rank 0's chunk
