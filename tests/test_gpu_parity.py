@@ -1213,9 +1213,10 @@ def test_native_dp_loopback_sharded_equals_allreduce_nonpow2(world):
 def test_dp_sharded_one_rank_chunks(world):
     """The sharded step's chunk arithmetic (the range's chunks of 64-float multiples, Adam's
     layer segments clipped to rank 0's chunk): the loopback's one-rank mode steps rank 0's
-    chunk of each range only.  Every parameter element must then hold either its fused-update
-    value (inside the chunk) or its value before the update (outside) — nothing else — and
-    the stepped elements must be one contiguous run per range, at most a chunk long."""
+    chunk of each range only.  Every critic element must then hold either its fused-update
+    value (inside the chunk) or its value before the update (outside) — nothing else; the
+    actor's gradients come from the partly stepped critics, so its values are not the fused
+    ones, but each range (critics, actor) must have some but not all of its elements stepped."""
     cfg, B, nrows = SacConfig(376, 17, 512), 256, 4000
     params = init_params(cfg, 131, bias_scale=0.05)
     rows = synthetic_rows(cfg, nrows, 132, state_scale=0.5)
@@ -1249,10 +1250,16 @@ def test_dp_sharded_one_rank_chunks(world):
                 stepped = v != init
                 n_stepped += int(stepped.sum())
                 total += v.size
+                if net == "policy":
+                    continue
                 if world & (world - 1) == 0:      # x W then x 1/W exact: the fused values
                     assert np.array_equal(v[stepped], fused[net][k][stepped]), (net, k)
-                else:                             # within fp32 rounding of the fused step
-                    np.testing.assert_allclose(v[stepped], fused[net][k][stepped], rtol=1e-5, atol=1e-7)
+                else:                             # x W / W rounding: Adam's first step moves an
+                    # element by ~lr whatever its gradient's size, so a rounding-level change of
+                    # a near-zero gradient can move it the other way: a rare few
+                    f = fused[net][k][stepped].astype(np.float64)
+                    off = np.abs(v[stepped] - f) > 1e-6 + 1e-5 * np.abs(f)
+                    assert off.mean() <= 1e-2, (net, k, off.mean())
         assert 0 < n_stepped < total, (nets, n_stepped, total)
 
 
