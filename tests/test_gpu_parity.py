@@ -1250,7 +1250,7 @@ def test_dp_sharded_one_rank_chunks(world):
                 stepped = v != init
                 n_stepped += int(stepped.sum())
                 total += v.size
-                if net == "policy":
+                if net == "policy" or not stepped.any():
                     continue
                 if world & (world - 1) == 0:      # x W then x 1/W exact: the fused values
                     assert np.array_equal(v[stepped], fused[net][k][stepped]), (net, k)
