@@ -1913,6 +1913,30 @@ static void enqueue_dp(sacmi_ctx* c, int B, int n) {
   enqueue_update(c, B, 1, 1, 4, scale, true, parity);                   // last phase 2
 }
 
+// Every rank's chunks of the Adam moments onto every rank, in place (collective; a no-op
+// unless a sharded step left them valid on the rank's own chunks only).  M and V carry no
+// slack: the last chunk is gathered through a bounce of the padded size
+static void dp_gather_moments(sacmi_ctx* c) {
+  if (!c->moments_sharded || c->dp_loopback || c->dp_world == 1) return;
+  const int W = c->dp_world;
+  for (int critic = 1; critic >= 0; --critic) {
+    const int64_t b = critic ? c->q_begin : c->pi_begin, e = critic ? c->q_end : c->total;
+    const int64_t ch = shard_chunk(e - b, W);
+    DevBuf<float> tmp;
+    tmp.alloc((size_t)ch * W);
+    for (float* arena : {c->M.p, c->V.p}) {
+      const int64_t lo = b + c->dp_rank * ch, hi = std::min(e, lo + ch);
+      if (hi > lo) CHECK_HIP(hipMemcpyAsync(tmp.p + c->dp_rank * ch, arena + lo, (size_t)(hi - lo) * 4,
+                                            hipMemcpyDeviceToDevice, c->stream));
+      CHECK_RCCL(rccl().all_gather(tmp.p + c->dp_rank * ch, tmp.p, (size_t)ch, ncclFloat32, c->comm, c->stream));
+      CHECK_HIP(hipMemcpyAsync(arena + b, tmp.p, (size_t)(e - b) * 4, hipMemcpyDeviceToDevice, c->stream));
+    }
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    tmp.release();
+  }
+  c->moments_sharded = false;
+}
+
 }  // namespace sacmi
 
 using namespace sacmi;
@@ -2770,6 +2794,9 @@ int sacmi_dp_set_sharded(sacmi_ctx* c, int32_t on) {
     pf_touch(c);
     REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
     REQUIRE(!on || c->dp_world <= kMaxShardWorld, SACMI_EVALUE, "sharded step: world > 64");
+    // leaving the sharded form: the moments whole on every rank first (the all-reduce form
+    // steps every element from this rank's M, V) — a collective, like the switch itself
+    if (!on) dp_gather_moments(c);
     c->dp_shard = on != 0;
     for (auto& kv : c->dp_graphs) (void)hipGraphExecDestroy(kv.second);
     c->dp_graphs.clear();
@@ -2787,26 +2814,7 @@ int sacmi_dp_sync_state(sacmi_ctx* c) {
   return guard([&] {
     pf_touch(c);
     REQUIRE(c->comm || c->dp_loopback, SACMI_ESTATE, "sacmi_allreduce_init has not been called");
-    if (!c->moments_sharded || c->dp_loopback || c->dp_world == 1) return;
-    // every rank's chunks of the Adam moments, in place (M and V carry no slack: the last
-    // chunk is gathered through a bounce of the padded size)
-    const int W = c->dp_world;
-    for (int critic = 1; critic >= 0; --critic) {
-      const int64_t b = critic ? c->q_begin : c->pi_begin, e = critic ? c->q_end : c->total;
-      const int64_t ch = shard_chunk(e - b, W);
-      DevBuf<float> tmp;
-      tmp.alloc((size_t)ch * W);
-      for (float* arena : {c->M.p, c->V.p}) {
-        const int64_t lo = b + c->dp_rank * ch, hi = std::min(e, lo + ch);
-        if (hi > lo) CHECK_HIP(hipMemcpyAsync(tmp.p + c->dp_rank * ch, arena + lo, (size_t)(hi - lo) * 4,
-                                              hipMemcpyDeviceToDevice, c->stream));
-        CHECK_RCCL(rccl().all_gather(tmp.p + c->dp_rank * ch, tmp.p, (size_t)ch, ncclFloat32, c->comm, c->stream));
-        CHECK_HIP(hipMemcpyAsync(arena + b, tmp.p, (size_t)(e - b) * 4, hipMemcpyDeviceToDevice, c->stream));
-      }
-      CHECK_HIP(hipStreamSynchronize(c->stream));
-      tmp.release();
-    }
-    c->moments_sharded = false;
+    dp_gather_moments(c);
   });
 }
 

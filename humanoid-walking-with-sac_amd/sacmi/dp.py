@@ -24,6 +24,7 @@ on torch's current stream, on which the library also runs.
 from __future__ import annotations
 
 import json
+import os
 import time
 
 import numpy as np
@@ -174,17 +175,49 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
 
     dts = [window() for _ in range(args.windows)]
     dt = float(np.median(dts))
-    # replicas must have stayed identical: compare a parameter checksum across ranks
-    w = torch.from_numpy(ctx.get_net("policy")["fc2.weight"]).to(device).double()
-    chk = torch.stack([w.sum(), (w * w).sum()])
-    allchk = [torch.zeros_like(chk) for _ in range(world)]
-    dist.all_gather(allchk, chk)
-    replicas_equal = all(bool(torch.equal(allchk[0], c)) for c in allchk)
+
+    def replicas_equal() -> bool:
+        """replicas must have stayed identical: a parameter checksum across ranks"""
+        w = torch.from_numpy(ctx.get_net("policy")["fc2.weight"]).to(device).double()
+        chk = torch.stack([w.sum(), (w * w).sum()])
+        allchk = [torch.zeros_like(chk) for _ in range(world)]
+        dist.all_gather(allchk, chk)
+        return all(bool(torch.equal(allchk[0], c)) for c in allchk)
+
+    replicas_ok = replicas_equal()
     peak = B.PEAK_BF16_MFMA_TFLOPS if wl["dtype"] == "bf16" else B.PEAK_FP32_MFMA_TFLOPS
     roof = None
     if want_roof:
         # every rank replays the instrumented sequence (its graph holds the collectives)
         roof = B.roofline_object(ctx, args, wl, peak, data_parallel=True)
+        torch.cuda.synchronize()
+    # the other optimizer-step form on the same ranks, after the line's own measurement
+    # (the line is the default form's): per-update time, the collectives' share of the
+    # sequence (timeline gaps) and the replica check — the all-reduce vs the sharded
+    # (ZeRO-1) form over real RCCL ranks (SACMI_BENCH_DP_FORM_AB=0: skipped)
+    form_ab = None
+    phases = world > 1 or sim or os.environ.get("SACMI_DP_PHASES_AT_WORLD1") is not None
+    if native and phases and os.environ.get("SACMI_BENCH_DP_FORM_AB", "1") != "0":
+        was = ctx.dp_sharded()
+        ctx.dp_set_sharded(not was)
+        for n in sizes:
+            ctx.step_dp(args.batch, n)
+        run(args.warmup)
+        torch.cuda.synchronize()
+        adts = [window() for _ in range(max(3, args.windows // 4))]
+        adt = float(np.median(adts))
+        form_ab = {
+            "form": "sharded" if not was else "all-reduce",
+            "ms_per_step": round(1e3 * adt / args.steps, 4),
+            "value": round(world * args.steps / adt, 2),
+            "windows": len(adts),
+            "replicas_bitwise_equal": replicas_equal(),
+        }
+        if want_roof:
+            info = B.timeline_roofline(ctx, args.batch, per_launch, data_parallel=True)
+            form_ab["allreduce_us_per_step"] = round(info["allreduce_us"] / per_launch, 2)
+            form_ab["step_us_timeline"] = round(info["graph_us"] / per_launch, 2)
+        ctx.dp_set_sharded(was)   # (leaving the sharded form gathers the moments: collective)
         torch.cuda.synchronize()
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -225,7 +258,8 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
                                "emulated in place (no transfers): the per-rank work minus the "
                                "collectives" if sim else None),
             "mfma_util_step": round(flops * value / 1e12 / peak / world, 4),
-            "replicas_bitwise_equal": replicas_equal,
+            "replicas_bitwise_equal": replicas_ok,
+            "dp_form_ab": form_ab,
             "roofline": roof, "cpu_baseline": cpu,
             "fill_seconds": round(t_fill, 2),
         }

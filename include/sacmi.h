@@ -276,14 +276,16 @@ int sacmi_allreduce_init(sacmi_ctx* ctx, const void* id, int32_t nbytes, int32_t
  * 2..n take their minibatch from the previous update's ride-along sampling/gather when
  * the replay allows it.  Captured into one hipGraph per (batch, n_updates); losses land in
  * the loss ring (sacmi_fetch_losses).  Each rank samples its own replay shard.
- * Sharded form (the default for 2 <= world <= 64; $SACMI_DP_SHARD=0/1 or
- * sacmi_dp_set_sharded override): each all-reduce + Adam becomes reduce-scatter -> Adam on
+ * Sharded form (opt-in, 2 <= world <= 64: $SACMI_DP_SHARD=1 at sacmi_allreduce_init or
+ * sacmi_dp_set_sharded): each all-reduce + Adam becomes reduce-scatter -> Adam on
  * this rank's 1/world chunk of the range -> all-gather of the parameters (ZeRO-1: the Adam
  * moments stay valid on the rank's own chunks; sacmi_dp_sync_state gathers them).
  * world == 1: the fused update (nothing to reduce; $SACMI_DP_PHASES_AT_WORLD1 forces the
  * phase sequence). */
 int sacmi_step_dp(sacmi_ctx* ctx, int32_t batch, int32_t n_updates);
-/* Sharded (1) or all-reduce (0) form of sacmi_step_dp; the same on every rank. */
+/* Sharded (1) or all-reduce (0) form of sacmi_step_dp; the same on every rank.  Leaving
+ * the sharded form is a collective (every rank): it gathers the Adam moments first, as
+ * sacmi_dp_sync_state does, since the all-reduce form steps every element from them. */
 int sacmi_dp_set_sharded(sacmi_ctx* ctx, int32_t on);
 int sacmi_dp_sharded(sacmi_ctx* ctx, int32_t* on);
 /* Collective (every rank): all-gather the sharded Adam moments so that every rank holds

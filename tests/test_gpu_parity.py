@@ -808,11 +808,15 @@ def test_bf16_compute_vs_emulation(S, A, n_hidden, B):
     ctx_b.close()
 
 
+@pytest.mark.parametrize("sharded", [False, True])
 @pytest.mark.parametrize("n_hidden", [2, 3])
-def test_native_dp_world1_matches_fused(n_hidden):
+def test_native_dp_world1_matches_fused(n_hidden, sharded):
     """sacmi_step_dp: the library's own RCCL data-parallel sequence (phases + in-place
     all-reduces, one captured graph per (batch, n), ride-along sampling) over a 1-rank
-    communicator == the same number of fused single-GPU updates, bit for bit."""
+    communicator == the same number of fused single-GPU updates, bit for bit.
+    sharded: the ZeRO-1 form through real RCCL calls — the error flags' all-reduce, the
+    in-place reduce-scatter into chunk r and the in-place all-gather (at one rank the whole
+    range is the chunk) inside the captured graph."""
     from sacmi import Context
     cfg = SacConfig(24, 4, 64, n_hidden=n_hidden)
     params = init_params(cfg, 91, bias_scale=0.05)
@@ -828,6 +832,7 @@ def test_native_dp_world1_matches_fused(n_hidden):
     uid = Context.allreduce_unique_id()
     assert len(uid) == 128
     ctxs[0].allreduce_init(uid, 0, 1)
+    ctxs[0].dp_set_sharded(sharded)   # (dp_sharded() reads 0 at one rank: the fused path's)
     ctxs[0].step_dp(64, 5)
     ctxs[0].step_dp(64, 1)
     for _ in range(6):
@@ -845,11 +850,13 @@ def test_native_dp_world1_matches_fused(n_hidden):
         ctxs[1].step_dp(64, 1)            # no communicator on this context
 
 
-def test_native_dp_world1_matches_fused_act16():
+@pytest.mark.parametrize("sharded", [False, True])
+def test_native_dp_world1_matches_fused_act16(sharded):
     """The same at config 5's per-GPU shape (NAO S661 A23 H512, batch 4096, bf16): the
     phase-split levels store bf16 activations exactly as the fused ones (act16), the
     split-K weight gradients go through the same k_dw_part16 / k_dw_fin path (plain store
-    + k_adam instead of the fused Adam epilogue): bit for bit after three updates."""
+    + k_adam instead of the fused Adam epilogue): bit for bit after three updates (sharded:
+    the bf16 shadows re-derived after the in-place all-gather)."""
     from sacmi import Context
     cfg = SacConfig(661, 23, 512)
     B = 4096
@@ -865,6 +872,7 @@ def test_native_dp_world1_matches_fused_act16():
         ctxs.append(ctx)
     assert ctxs[0].act16(B)
     ctxs[0].allreduce_init(Context.allreduce_unique_id(), 0, 1)
+    ctxs[0].dp_set_sharded(sharded)
     ctxs[0].step_dp(B, 3)
     fused = np.stack([ctxs[1].step(B) for _ in range(3)])
     ctxs[0].synchronize()
