@@ -1124,7 +1124,9 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
 
   // fused updates whose policy dhp1 level (L12) leaves CUs idle on k_gemm: Polyak rides there
   static const bool pk_env = std::getenv("SACMI_NO_POLYAK_RIDE") == nullptr;
-  const bool polyak_ride = (phase_mask == 7 || (c->dp_sharding_now && (phase_mask & 2))) && pk_env &&
+  // (data-parallel phase 1, both optimizer forms: the critic Adam before L7 leaves the
+  // targets alone — sharded: enqueue_dp's chunk Adam, all-reduce: the one below)
+  const bool polyak_ride = (phase_mask == 7 || (phase_mask & 2)) && pk_env &&
                            !act16 && (int64_t)((B + 31) / 32) * ((H + 31) / 32) <= 192;
   if (phase_mask & 1) {
     if (!have_batch)   // (have_batch: the previous update's rides / side stream produced them)
@@ -1331,7 +1333,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
    if (!fuse && !c->dp_sharding_now) {   // (sharded: enqueue_dp takes the critic step)
     // critic Adam (+ Polyak, + q-loss finalisation)
     AdamArgs ad = dp_adam_args(c, true, B, grad_scale, use_ring);
-    if (mark(c, "adam_critic_polyak")) {
+    if (polyak_ride) { ad.tgt = nullptr; ad.tgth = nullptr; }   // (Polyak: in L12)
+    if (mark(c, polyak_ride ? "adam_critic" : "adam_critic_polyak")) {
       ad.tl = c->tl_cur;
       launch_adam(ad, s);
     }
