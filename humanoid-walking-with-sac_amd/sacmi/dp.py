@@ -199,26 +199,30 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     phases = world > 1 or sim or os.environ.get("SACMI_DP_PHASES_AT_WORLD1") is not None
     if native and phases and os.environ.get("SACMI_BENCH_DP_FORM_AB", "1") != "0":
         was = ctx.dp_sharded()
-        ctx.dp_set_sharded(not was)
-        for n in sizes:
-            ctx.step_dp(args.batch, n)
-        run(args.warmup)
-        torch.cuda.synchronize()
-        adts = [window() for _ in range(max(3, args.windows // 4))]
-        adt = float(np.median(adts))
-        form_ab = {
-            "form": "sharded" if not was else "all-reduce",
-            "ms_per_step": round(1e3 * adt / args.steps, 4),
-            "value": round(world * args.steps / adt, 2),
-            "windows": len(adts),
-            "replicas_bitwise_equal": replicas_equal(),
-        }
-        if want_roof:
-            info = B.timeline_roofline(ctx, args.batch, per_launch, data_parallel=True)
-            form_ab["allreduce_us_per_step"] = round(info["allreduce_us"] / per_launch, 2)
-            form_ab["step_us_timeline"] = round(info["graph_us"] / per_launch, 2)
-        ctx.dp_set_sharded(was)   # (leaving the sharded form gathers the moments: collective)
-        torch.cuda.synchronize()
+        form_ab = {"form": "sharded" if not was else "all-reduce"}
+        try:   # (a failure here is reported in the line, not instead of it)
+            ctx.dp_set_sharded(not was)
+            for n in sizes:
+                ctx.step_dp(args.batch, n)
+            run(args.warmup)
+            torch.cuda.synchronize()
+            adts = [window() for _ in range(max(3, args.windows // 4))]
+            adt = float(np.median(adts))
+            form_ab.update({
+                "ms_per_step": round(1e3 * adt / args.steps, 4),
+                "value": round(world * args.steps / adt, 2),
+                "windows": len(adts),
+                "replicas_bitwise_equal": replicas_equal(),
+            })
+            if want_roof:
+                info = B.timeline_roofline(ctx, args.batch, per_launch, data_parallel=True)
+                form_ab["allreduce_us_per_step"] = round(info["allreduce_us"] / per_launch, 2)
+                form_ab["step_us_timeline"] = round(info["graph_us"] / per_launch, 2)
+            # (leaving the sharded form gathers the moments: a collective)
+            ctx.dp_set_sharded(was)
+            torch.cuda.synchronize()
+        except Exception as e:   # noqa: BLE001 — the other form's failure is data for the line
+            form_ab["error"] = f"{type(e).__name__}: {e}"[:300]
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         n_cpu = min(fill * world, 1_000_000)
