@@ -1695,6 +1695,8 @@ struct RcclApi {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclReduceScatter) reduce_scatter = nullptr;
   decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclGetErrorString) err = nullptr;
 };
@@ -1723,6 +1725,8 @@ static RcclApi& rccl() {
   r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(sym("ncclAllReduce"));
   r.reduce_scatter = reinterpret_cast<decltype(r.reduce_scatter)>(sym("ncclReduceScatter"));
   r.all_gather = reinterpret_cast<decltype(r.all_gather)>(sym("ncclAllGather"));
+  r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
+  r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
   r.destroy = reinterpret_cast<decltype(r.destroy)>(sym("ncclCommDestroy"));
   r.err = reinterpret_cast<decltype(r.err)>(sym("ncclGetErrorString"));
   r.h = h;
@@ -1807,7 +1811,11 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
     range(critic, b, e);
     const int64_t ch = shard_chunk(e - b, W);
     float* g = c->G.p + b;
-    if (critic) {   // the error flags to every rank (the reduce-scatter delivers chunk r only)
+    // the critic's error flags to every rank (the reduce-scatter delivers chunk r only): an
+    // all-reduce of their own, in one RCCL group with the reduce-scatter (one launch)
+    const bool group = critic && !c->dp_loopback;
+    if (group) CHECK_RCCL(rccl().group_start());
+    if (critic) {
       (void)mark(c, "allreduce_error_flags");
       float* f = c->G.p + c->q_end;
       if (c->dp_loopback) loopback_flags(c, f, s);
@@ -1823,6 +1831,7 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
     } else {
       CHECK_RCCL(rccl().reduce_scatter(g, g + c->dp_rank * ch, (size_t)ch, ncclFloat32, ncclSum, c->comm, s));
     }
+    if (group) CHECK_RCCL(rccl().group_end());
   };
   auto step = [&](bool critic) {   // Adam on the chunk(s), gather, the replicated scalars / shadows
     (void)mark(c, critic ? "adam_critic_shard" : "adam_actor_shard");
