@@ -294,6 +294,89 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 GEMM on bf16 MFMA: the three-way split ("x6").  gfx950's fp32 MFMA issues at 1/16
+// of the bf16 rate and has no xf32 form.  Every fp32 operand x is cut EXACTLY into three
+// bf16 parts x = h + m + l by truncation (h = the top 8 significant bits, m the next 8 of
+// the remainder, l the rest — at most 8 bits, so l is a bf16 with no rounding; both
+// subtractions are exact in fp32).  a·b is then the 9 cross products of the parts; the
+// products are exact in the fp32 accumulator (8 x 8 significant bits), and the three
+// dropped ones (m·l, l·m, l·l) are below 2^-25 |a b| — under fp32's own unit roundoff, so
+// the result is as accurate as the fp32 FMA chain (different rounding, not bit-identical).
+// Two 16-deep fragment chunks (lane group g holds k = c0*16 + 4g .. +3 and c1*16 + 4g ..
+// +3 of its row, the same for both operands) form the 8 bf16 k of one
+// v_mfma_f32_16x16x32_bf16 operand; per 32 k and 16x16 block 6 MFMAs of 16 cycles
+// replace 8 fp32 MFMAs of 32 cycles.  Small terms first into the accumulator.
+#ifndef SACMI_X6
+#define SACMI_X6 0       // measured slower at config 2 (profiles/r06/x6_ab)
+#endif
+#ifndef SACMI_X6_EXP
+#define SACMI_X6_EXP 0   // timing builds only (wrong values): 1 no B split, 2 no split at all
+#endif
+typedef __bf16 x6_bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int x6_u4 __attribute__((ext_vector_type(4)));
+
+// bf16 bits of the upper halves of (lo, hi) packed as one dword (lo in bits 0-15)
+__device__ __forceinline__ uint32_t x6_pack_hi(uint32_t lo, uint32_t hi) {
+  return __builtin_amdgcn_perm(hi, lo, 0x07060302u);
+}
+__device__ __forceinline__ void x6_split(const float (&p)[4], const float (&q)[4], x6_bf16x8& h,
+                                         x6_bf16x8& m, x6_bf16x8& l, bool fake = false) {
+  x6_u4 H, Mw, L;
+  if (fake) {   // timing experiment (SACMI_X6_EXP): every part = the top part (finite values,
+                // 4 perms instead of the split's 44 instructions)
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      H[d] = x6_pack_hi(__float_as_uint(d < 2 ? p[2 * d] : q[2 * d - 4]),
+                        __float_as_uint(d < 2 ? p[2 * d + 1] : q[2 * d - 3]));
+    h = m = l = __builtin_bit_cast(x6_bf16x8, H);
+    return;
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const float x0 = d < 2 ? p[2 * d] : q[2 * d - 4];
+    const float x1 = d < 2 ? p[2 * d + 1] : q[2 * d - 3];
+    const uint32_t u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+    H[d] = x6_pack_hi(u0, u1);
+    const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u);
+    const float r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+    const uint32_t v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+    Mw[d] = x6_pack_hi(v0, v1);
+    const float s0 = r0 - __uint_as_float(v0 & 0xffff0000u);
+    const float s1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+    L[d] = x6_pack_hi(__float_as_uint(s0), __float_as_uint(s1));
+  }
+  h = __builtin_bit_cast(x6_bf16x8, H);
+  m = __builtin_bit_cast(x6_bf16x8, Mw);
+  l = __builtin_bit_cast(x6_bf16x8, L);
+}
+
+template <int MT, int NT>
+__device__ __forceinline__ void mfma_x6(f4 (&acc)[MT][NT], const float (&a0)[MT][4],
+                                        const float (&b0)[NT][4], const float (&a1)[MT][4],
+                                        const float (&b1)[NT][4]) {
+  // the A parts of every row block first (MT <= NT), each B column block's parts split just
+  // before its MFMAs: the parts of one B block live at a time (register pressure)
+  x6_bf16x8 ah[MT], am[MT], al[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) x6_split(a0[i], a1[i], ah[i], am[i], al[i], SACMI_X6_EXP >= 2);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    x6_bf16x8 bh, bm, bl;
+    x6_split(b0[j], b1[j], bh, bm, bl, SACMI_X6_EXP >= 1);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      f4 c = acc[i][j];
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, c, 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, c, 0, 0, 0);
+    }
+  }
+}
+
 // Each wave accumulates chunks wave, wave+KSPLIT, ... of a TM x TN tile and writes
 // its partial sums to red[wave][TM][TN+1].  At batch 256 every operand read is a
 // dependent L2/MALL round trip (~1-2 us), so a wave issues the loads of G chunks at
@@ -479,6 +562,9 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
     // after the LAST operand loads (vmcnt is in order)
     if (!MIDSPLIT && j + G >= nmine) pre();
     __builtin_amdgcn_sched_barrier(0);
+    // fp32 levels with chunk pairs: the x6 split form (mfma_x6) on each pair, fp32 MFMAs on an
+    // unpaired last chunk; the transforms and row sums below work on the fp32 fragments
+    constexpr bool X6P = SACMI_X6 && !BF16 && (G % 2 == 0);
 #pragma unroll
     for (int g = 0; g < G; ++g)
       if (j + g < nmine) {
@@ -508,12 +594,19 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
             for (int i = 0; i < MT; ++i) a[g][i][s] *= f;
           }
         }
-        mfma_chunk<MT, NT, BF16>(acc, a[g], b[g]);
+        if constexpr (!X6P) mfma_chunk<MT, NT, BF16>(acc, a[g], b[g]);
         if (ROWSUM) {
 #pragma unroll
           for (int i = 0; i < MT; ++i) rs[i] += (a[g][i][0] + a[g][i][1]) + (a[g][i][2] + a[g][i][3]);
         }
       }
+    if constexpr (X6P) {
+#pragma unroll
+      for (int g = 0; g < G; g += 2) {
+        if (j + g + 1 < nmine) mfma_x6<MT, NT>(acc, a[g], b[g], a[g + 1], b[g + 1]);
+        else if (j + g < nmine) mfma_chunk<MT, NT, false>(acc, a[g], b[g]);
+      }
+    }
   }
   }   // !PIPE
 #undef SACMI_CHUNK
