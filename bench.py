@@ -116,13 +116,8 @@ def init_agent(ctx, seed):
 
 
 # kernels that run the MLP GEMM levels (the dominant kernel family of the update); L10
-# (k_gemm_sample_bwd: dL/da + the sampling backward) and the heads kernel are not levels.
-# k_chain (the batch-256 actor pass L7 -> L8 -> L9 -> tail -> L12 in one launch) counts as
-# one level carrying its four GEMMs' and the tail's dhp2 FLOPs, k_chain_a (the critic pass
-# L1 -> L2 + heads -> L3 -> L4 -> L5) as one carrying its five GEMMs' and the heads'; a level
-# with the policy heads folded in carries the heads GEMM's FLOPs (sacmi.hip level_flops)
-LEVEL_KERNELS = {"k_gemm", "k_fwd", "k_fwd16", "k_fwd16p", "k_axk16", "k_axk16p", "k_dw_part", "k_dw_part16", "k_dw_fin", "k_dw_fin_p",
-                 "k_chain", "k_chain_a"}
+# (k_gemm_sample_bwd: dL/da + the sampling backward) and the heads kernel are not levels
+LEVEL_KERNELS = {"k_gemm", "k_fwd16", "k_fwd16p", "k_axk16", "k_dw_part16", "k_dw_fin"}
 
 
 def timeline_roofline(ctx, batch, n_updates, data_parallel=False):

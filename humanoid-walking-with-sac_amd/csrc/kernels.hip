@@ -76,12 +76,6 @@ __device__ __forceinline__ rsrc_t make_rsrc(const float* base, uint32_t bytes) {
 __device__ __forceinline__ float buf_ld(rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
-// ... with cache-policy bits (AUX 16 = sc1: L1 bypass, for data another workgroup of the same
-// launch wrote write-through: cdna_hip_programming.md §6 Guideline 16)
-template <int AUX>
-__device__ __forceinline__ float buf_ld_aux(rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, AUX));
-}
 __device__ __forceinline__ void buf_st(rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, (int)off, 0, 0);
 }
@@ -136,31 +130,8 @@ __device__ __forceinline__ void buf_st4(rsrc_t r, uint32_t off, f4 v) {
 template <int NT>
 struct OpFetch {
   rsrc_t r;
-  const char* p;
   uint32_t off[NT];
-#ifdef SACMI_EXP_LINFETCH
-  bool lin;   // the operand has >= 16 rows: the contiguous-read experiment applies
-#endif
 };
-
-#ifndef SACMI_FETCH_SADDR
-#define SACMI_FETCH_SADDR 0
-#endif
-constexpr int kLdSc1 = 16;      // raw buffer load cache-policy bits: sc1 (coherent across XCDs)
-#ifndef SACMI_A_AUX
-#define SACMI_A_AUX 0           // k_gemm: cache-policy bits of the A-operand loads (experiment)
-#endif
-#ifndef SACMI_B_AUX
-#define SACMI_B_AUX 0
-#endif
-#ifndef SACMI_KCONTIG
-#define SACMI_KCONTIG 0         // k_gemm: contiguous K-chunk ranges per wave (experiment)
-#endif
-// global load with a uniform 64-bit base and a 32-bit per-lane byte offset (saddr form)
-template <class T>
-__device__ __forceinline__ T gld_off(const char* base, uint32_t off) {
-  return *reinterpret_cast<const T*>(base + off);
-}
 
 // H16: the operand is stored as bf16 (K-contiguous only: the policy heads' input under
 // act16), fetched 4 k per 8-byte load and widened exactly to fp32
@@ -169,28 +140,18 @@ __device__ __forceinline__ void row_offs(const float* P, int ld, int row0, int n
                                          OpFetch<NT>& f) {
   static_assert(!H16 || KC, "bf16 operands are K-contiguous");
   f.r = make_rsrc(P, 0x7fffffffu);
-  f.p = reinterpret_cast<const char*>(P);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     int row = row0 + t * 16 + (lane & 15);
     row = row < nrows ? row : nrows - 1;
     f.off[t] = KC ? (uint32_t)row * (uint32_t)ld * (H16 ? 2u : 4u) : (uint32_t)row * 4u;
-#ifdef SACMI_EXP_LINFETCH
-    // the 16-row block (kept inside the operand's rows), 16 B per lane
-    f.lin = KC && !H16 && nrows >= 16;
-    if (f.lin) {
-      const int rb = row0 + t * 16 < nrows - 16 ? row0 + t * 16 : nrows - 16;
-      f.off[t] = (uint32_t)rb * (uint32_t)ld * 4u + 16u * (uint32_t)(lane & 63);
-    }
-#endif
   }
 }
 
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// AUX: cache-policy bits of the operand loads (SACMI_A_AUX / SACMI_B_AUX: e.g. 2 = nt)
-template <int NT, bool KC, bool H16 = false, int AUX = 0>
+template <int NT, bool KC, bool H16 = false>
 __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, int K,
                                          float (&v)[NT][4]) {
   if constexpr (H16) {
@@ -205,32 +166,10 @@ __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, in
     }
     return;
   }
-#ifdef SACMI_EXP_NOLOAD
-  // timing experiment only: no operand loads at all (MFMA + epilogue floor)
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) v[t][s] = (float)(k + s + t) * 1e-3f;
-  return;
-#endif
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (KC) {
-#ifdef SACMI_EXP_LINFETCH
-      // timing experiment only (wrong values): the same 16-row block's bytes read as 1 KB
-      // contiguous per wave-instruction, as an MFMA-packed operand layout would be read
-      const int ch = (k >> 4) < (ld >> 4) - 1 ? (k >> 4) : (ld >> 4) - 1;
-      const uint32_t o = f.lin ? f.off[t] + (uint32_t)ch * 1024u : f.off[t] + (uint32_t)(k < K ? k : 0) * 4u;
-#else
-      const uint32_t o = f.off[t] + (uint32_t)(k < K ? k : 0) * 4u;
-#endif
-      float4 x;
-      if constexpr (AUX != 0) {
-        const f4 y = llvm_raw_buffer_load_v4f32(f.r, (int)o, 0, AUX);
-        x = float4{y[0], y[1], y[2], y[3]};
-      } else {
-        x = (SACMI_FETCH_SADDR & 1) ? gld_off<float4>(f.p, o) : buf_ld4(f.r, o);
-      }
+      const float4 x = buf_ld4(f.r, f.off[t] + (uint32_t)(k < K ? k : 0) * 4u);
       v[t][0] = (k < K) ? x.x : 0.f;
       v[t][1] = (k + 1 < K) ? x.y : 0.f;
       v[t][2] = (k + 2 < K) ? x.z : 0.f;
@@ -239,9 +178,7 @@ __device__ __forceinline__ void fetch_op(const OpFetch<NT>& f, int ld, int k, in
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int kk = (k + s < K) ? (k + s) : (K - 1);
-        const uint32_t o = f.off[t] + (uint32_t)kk * (uint32_t)ld * 4u;
-        const float x = AUX ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(f.r, (int)o, 0, AUX))
-                            : (SACMI_FETCH_SADDR & 2) ? gld_off<float>(f.p, o) : buf_ld(f.r, o);
+        const float x = buf_ld(f.r, f.off[t] + (uint32_t)kk * (uint32_t)ld * 4u);
         v[t][s] = (k + s < K) ? x : 0.f;
       }
     }
@@ -264,14 +201,6 @@ __device__ __forceinline__ s4 to_bf16x4(const float (&v)[4]) {
 template <int MT, int NT, bool BF16 = false>
 __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[MT][4],
                                            const float (&b)[NT][4]) {
-#ifdef SACMI_EXP_NOMFMA
-  // timing experiment only: the operands are consumed by one add, no MFMA
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j][0] += a[i][0] + b[j][0];
-  return;
-#endif
   if constexpr (BF16) {
     s4 ab[MT], bb[NT];
 #pragma unroll
@@ -294,89 +223,6 @@ __device__ __forceinline__ void mfma_chunk(f4 (&acc)[MT][NT], const float (&a)[M
   }
 }
 
-// ---------------------------------------------------------------------------
-// fp32 GEMM on bf16 MFMA: the three-way split ("x6").  gfx950's fp32 MFMA issues at 1/16
-// of the bf16 rate and has no xf32 form.  Every fp32 operand x is cut EXACTLY into three
-// bf16 parts x = h + m + l by truncation (h = the top 8 significant bits, m the next 8 of
-// the remainder, l the rest — at most 8 bits, so l is a bf16 with no rounding; both
-// subtractions are exact in fp32).  a·b is then the 9 cross products of the parts; the
-// products are exact in the fp32 accumulator (8 x 8 significant bits), and the three
-// dropped ones (m·l, l·m, l·l) are below 2^-25 |a b| — under fp32's own unit roundoff, so
-// the result is as accurate as the fp32 FMA chain (different rounding, not bit-identical).
-// Two 16-deep fragment chunks (lane group g holds k = c0*16 + 4g .. +3 and c1*16 + 4g ..
-// +3 of its row, the same for both operands) form the 8 bf16 k of one
-// v_mfma_f32_16x16x32_bf16 operand; per 32 k and 16x16 block 6 MFMAs of 16 cycles
-// replace 8 fp32 MFMAs of 32 cycles.  Small terms first into the accumulator.
-#ifndef SACMI_X6
-#define SACMI_X6 0       // measured slower at config 2 (profiles/r06/x6_ab)
-#endif
-#ifndef SACMI_X6_EXP
-#define SACMI_X6_EXP 0   // timing builds only (wrong values): 1 no B split, 2 no split at all
-#endif
-typedef __bf16 x6_bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int x6_u4 __attribute__((ext_vector_type(4)));
-
-// bf16 bits of the upper halves of (lo, hi) packed as one dword (lo in bits 0-15)
-__device__ __forceinline__ uint32_t x6_pack_hi(uint32_t lo, uint32_t hi) {
-  return __builtin_amdgcn_perm(hi, lo, 0x07060302u);
-}
-__device__ __forceinline__ void x6_split(const float (&p)[4], const float (&q)[4], x6_bf16x8& h,
-                                         x6_bf16x8& m, x6_bf16x8& l, bool fake = false) {
-  x6_u4 H, Mw, L;
-  if (fake) {   // timing experiment (SACMI_X6_EXP): every part = the top part (finite values,
-                // 4 perms instead of the split's 44 instructions)
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-      H[d] = x6_pack_hi(__float_as_uint(d < 2 ? p[2 * d] : q[2 * d - 4]),
-                        __float_as_uint(d < 2 ? p[2 * d + 1] : q[2 * d - 3]));
-    h = m = l = __builtin_bit_cast(x6_bf16x8, H);
-    return;
-  }
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const float x0 = d < 2 ? p[2 * d] : q[2 * d - 4];
-    const float x1 = d < 2 ? p[2 * d + 1] : q[2 * d - 3];
-    const uint32_t u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
-    H[d] = x6_pack_hi(u0, u1);
-    const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u);
-    const float r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
-    const uint32_t v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
-    Mw[d] = x6_pack_hi(v0, v1);
-    const float s0 = r0 - __uint_as_float(v0 & 0xffff0000u);
-    const float s1 = r1 - __uint_as_float(v1 & 0xffff0000u);
-    L[d] = x6_pack_hi(__float_as_uint(s0), __float_as_uint(s1));
-  }
-  h = __builtin_bit_cast(x6_bf16x8, H);
-  m = __builtin_bit_cast(x6_bf16x8, Mw);
-  l = __builtin_bit_cast(x6_bf16x8, L);
-}
-
-template <int MT, int NT>
-__device__ __forceinline__ void mfma_x6(f4 (&acc)[MT][NT], const float (&a0)[MT][4],
-                                        const float (&b0)[NT][4], const float (&a1)[MT][4],
-                                        const float (&b1)[NT][4]) {
-  // the A parts of every row block first (MT <= NT), each B column block's parts split just
-  // before its MFMAs: the parts of one B block live at a time (register pressure)
-  x6_bf16x8 ah[MT], am[MT], al[MT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i) x6_split(a0[i], a1[i], ah[i], am[i], al[i], SACMI_X6_EXP >= 2);
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    x6_bf16x8 bh, bm, bl;
-    x6_split(b0[j], b1[j], bh, bm, bl, SACMI_X6_EXP >= 1);
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      f4 c = acc[i][j];
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, c, 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, c, 0, 0, 0);
-    }
-  }
-}
-
 // Each wave accumulates chunks wave, wave+KSPLIT, ... of a TM x TN tile and writes
 // its partial sums to red[wave][TM][TN+1].  At batch 256 every operand read is a
 // dependent L2/MALL round trip (~1-2 us), so a wave issues the loads of G chunks at
@@ -390,21 +236,10 @@ __device__ __forceinline__ void mfma_x6(f4 (&acc)[MT][NT], const float (&a0)[MT]
 // AXF 1: A-operand transform (GemmDesc::axk) applied to the loaded fragments before the
 // MFMAs: a(b,k) = A>0 ? coef[row]*w[k] : 0 with coef in LDS (coef[tile row]); with
 // store_a the transformed fragments are also written to d.ax_out.
-// PIPE (G == 1, AXF == 0): software-pipelined K loop — chunk j+1's loads are in flight
-// while chunk j's MFMAs run (two register buffers); the epilogue operands (pre) go out
-// right behind chunk 0's loads (PIPE 1) or after the loop (PIPE 2: deep-K levels, whose
-// registers then hold the second buffer instead).  Same chunk order per wave: bitwise
-// identical sums.
-// MIDSPLIT (k_chain's phases, one pass over K: K <= 16 KSPLIT G): every group's B operand
-// (the weights) and transform weights first, then early() — the cohort barrier of the previous
-// phase — then the A operands, which the previous phase wrote: the weights' latency and the
-// setup overlap the barrier.  Otherwise early() runs before any load.
 template <int TM, int TN, int KSPLIT, int G, bool AKC, bool BKC, bool ROWSUM, int MG = 1,
-          int AXF = 0, bool BF16 = false, int PIPE = 0, bool A16 = false, int AAUX = SACMI_A_AUX,
-          bool MIDSPLIT = false, class Pre, class Early = void (*)()>
+          int AXF = 0, bool BF16 = false, bool A16 = false, class Pre>
 __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, float* red,
-                                            float* rsum, Pre&& pre, bool store_a = false,
-                                            Early&& early = [] {}) {
+                                            float* rsum, Pre&& pre, bool store_a = false) {
   constexpr int MT = TM / 16, NT = TN / 16;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -426,16 +261,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   row_offs<MT, AKC, A16>(d.A, d.lda, m0, d.M, lane, ra);
   row_offs<NT, BKC>(d.B, d.ldb, n0, d.N, lane, rb);
   const int nch = (d.K + 15) >> 4;
-#if SACMI_KCONTIG
-  // contiguous chunk ranges per wave (chunks ks*cpw .. +cpw-1): a wave reads whole
-  // 128-byte rows of a K-contiguous operand instead of 64-byte halves shared with another wave
-  const int cpw = (nch + KSPLIT - 1) / KSPLIT;
-  const int nmine = nch > ks * cpw ? (nch - ks * cpw < cpw ? nch - ks * cpw : cpw) : 0;
-#define SACMI_CHUNK(jj) (ks * cpw + (jj))
-#else
   const int nmine = nch > ks ? (nch - ks + KSPLIT - 1) / KSPLIT : 0;
-#define SACMI_CHUNK(jj) (ks + (jj) * KSPLIT)
-#endif
   const int kl = 4 * (lane >> 4);
   float a[G][MT][4], b[G][NT][4];
   // per-group side operands: AXF 1 the transform weights w[k..k+3]; !AKC the A K-scale
@@ -450,105 +276,17 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
   // fall back to full drains)
   const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
                                store_a ? (uint32_t)(((size_t)(d.M - 1) * d.ax_ld + d.K) * 4) : 0u);
-  if constexpr (!MIDSPLIT) early();
-  if constexpr (PIPE != 0) {
-    static_assert(G == 1 && AXF == 0, "pipelined K loop: one chunk per stage, no A transform");
-    float a1[MT][4], b1[NT][4], xw1[4];
-    auto issue = [&](int jj, float (&av)[MT][4], float (&bv)[NT][4], float (&xv)[4]) {
-      jj = jj < nmine ? jj : nmine - 1;   // unconditional: past the end re-reads the last chunk
-      const int k = SACMI_CHUNK(jj) * 16 + kl;
-      fetch_op<MT, AKC, A16, AAUX>(ra, d.lda, k, d.K, av);
-      fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, bv);
-      if constexpr (!AKC) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) xv[s] = buf_ld(rxw, (uint32_t)(k + s < d.K ? k + s : 0) * 4u);
-      }
-    };
-    auto consume = [&](float (&av)[MT][4], const float (&bv)[NT][4], const float (&xv)[4]) {
-#pragma clang fp contract(off)
-      if constexpr (!AKC) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const float f = has_ksc ? xv[s] : 1.f;
-#pragma unroll
-          for (int i = 0; i < MT; ++i) av[i][s] *= f;
-        }
-      }
-      mfma_chunk<MT, NT, BF16>(acc, av, bv);
-      if (ROWSUM) {
-#pragma unroll
-        for (int i = 0; i < MT; ++i) rs[i] += (av[i][0] + av[i][1]) + (av[i][2] + av[i][3]);
-      }
-    };
-    if (nmine == 0) {
-      pre();
-    } else {
-      issue(0, a[0], b[0], xw[0]);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (PIPE == 1) pre();
-      __builtin_amdgcn_sched_barrier(0);
-      for (int j = 0; j < nmine; j += 2) {
-        issue(j + 1, a1, b1, xw1);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(a[0], b[0], xw[0]);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(j + 2, a[0], b[0], xw[0]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (j + 1 < nmine) consume(a1, b1, xw1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (PIPE == 2) pre();
-    }
-  } else {
-  if constexpr (MIDSPLIT) {
-    static_assert(PIPE == 0, "MIDSPLIT: register-direct core");
-    if (nmine == 0) {
-      early();
-      pre();
-    } else {
-      auto bload = [&]() {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {   // B (and the transform weights), every group
-          const int jj = g < nmine ? g : nmine - 1;
-          const int k = SACMI_CHUNK(jj) * 16 + kl;
-          fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, b[g]);
-          if constexpr (AXF == 1) {
-            const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
-            xw[g][0] = x.x; xw[g][1] = x.y; xw[g][2] = x.z; xw[g][3] = x.w;
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      };
-      // (wave 0 polls the barrier: its weight loads deferred past the wait measured slower,
-      // config 2 chain 42.4 -> 44.5 us — DESIGN.md §12a)
-      bload();
-      early();
-#pragma unroll
-      for (int g = 0; g < G; ++g) {   // A, every group
-        const int jj = g < nmine ? g : nmine - 1;
-        const int k = SACMI_CHUNK(jj) * 16 + kl;
-        fetch_op<MT, AKC, A16, AAUX>(ra, d.lda, k, d.K, a[g]);
-        if constexpr (AXF != 1 && !AKC) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) xw[g][s] = buf_ld(rxw, (uint32_t)(k + s < d.K ? k + s : 0) * 4u);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      pre();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (!MIDSPLIT && nmine == 0) pre();
+  if (nmine == 0) pre();
   for (int j = 0; j < nmine; j += G) {
 #pragma unroll
-    for (int g = 0; g < G && !MIDSPLIT; ++g) {
+    for (int g = 0; g < G; ++g) {
       // unconditional (see fetch_op; a guard, even a wave-uniform one, makes the compiler
       // drain the loads at the end of the guarded block): a group past the wave's last
       // chunk re-reads that chunk and is skipped below
       const int jj = j + g < nmine ? j + g : nmine - 1;
-      const int k = SACMI_CHUNK(jj) * 16 + kl;
-      fetch_op<MT, AKC, A16, AAUX>(ra, d.lda, k, d.K, a[g]);
-      fetch_op<NT, BKC, false, SACMI_B_AUX>(rb, d.ldb, k, d.K, b[g]);
+      const int k = (ks + jj * KSPLIT) * 16 + kl;
+      fetch_op<MT, AKC, A16>(ra, d.lda, k, d.K, a[g]);
+      fetch_op<NT, BKC>(rb, d.ldb, k, d.K, b[g]);
       if constexpr (AXF == 1) {          // w3 rows are float4-aligned (parameter arena)
         const float4 x = buf_ld4(rxw, (uint32_t)(k < d.K ? k : 0) * 4u);
         xw[g][0] = x.x; xw[g][1] = x.y; xw[g][2] = x.z; xw[g][3] = x.w;
@@ -560,11 +298,8 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
       __builtin_amdgcn_sched_barrier(0);
     }
     // after the LAST operand loads (vmcnt is in order)
-    if (!MIDSPLIT && j + G >= nmine) pre();
+    if (j + G >= nmine) pre();
     __builtin_amdgcn_sched_barrier(0);
-    // fp32 levels with chunk pairs: the x6 split form (mfma_x6) on each pair, fp32 MFMAs on an
-    // unpaired last chunk; the transforms and row sums below work on the fp32 fragments
-    constexpr bool X6P = SACMI_X6 && !BF16 && (G % 2 == 0);
 #pragma unroll
     for (int g = 0; g < G; ++g)
       if (j + g < nmine) {
@@ -573,7 +308,7 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
         // tile configuration's code generation
 #pragma clang fp contract(off)
         if constexpr (AXF == 1) {
-          const int k = SACMI_CHUNK(j + g) * 16 + kl;
+          const int k = (ks + (j + g) * KSPLIT) * 16 + kl;
 #pragma unroll
           for (int i = 0; i < MT; ++i) {
             const int r = mloc + i * 16 + (lane & 15);
@@ -594,22 +329,13 @@ __device__ __forceinline__ void gemm_core_l(const GemmDesc& d, int m0, int n0, f
             for (int i = 0; i < MT; ++i) a[g][i][s] *= f;
           }
         }
-        if constexpr (!X6P) mfma_chunk<MT, NT, BF16>(acc, a[g], b[g]);
+        mfma_chunk<MT, NT, BF16>(acc, a[g], b[g]);
         if (ROWSUM) {
 #pragma unroll
           for (int i = 0; i < MT; ++i) rs[i] += (a[g][i][0] + a[g][i][1]) + (a[g][i][2] + a[g][i][3]);
         }
       }
-    if constexpr (X6P) {
-#pragma unroll
-      for (int g = 0; g < G; g += 2) {
-        if (j + g + 1 < nmine) mfma_x6<MT, NT>(acc, a[g], b[g], a[g + 1], b[g + 1]);
-        else if (j + g < nmine) mfma_chunk<MT, NT, false>(acc, a[g], b[g]);
-      }
-    }
   }
-  }   // !PIPE
-#undef SACMI_CHUNK
   SACMI_STAMP(16 + wave);
   float* my = red + wave * TM * (TN + 1);
   const int rq = (lane >> 4) * 4, cc = lane & 15;
@@ -652,343 +378,23 @@ __device__ __forceinline__ void place_tile(const GemmDesc& d, int t, int& tr, in
 // layout dispatch (wave-uniform, once per workgroup)
 // AXK: whether this kernel instantiation carries the A-transform path (launch_gemm picks
 // the variant from the level's descs): 1 -> axk 1 descs, 0 -> none.
-// AAUX: cache-policy bits of the A-operand loads (kg_body's LDAUX); MIDSPLIT: early() is the
-// mid hook of gemm_core_l (k_chain), else it runs first
-template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, int PIPE, int AAUX, bool MIDSPLIT,
-          class Pre, class Early>
+template <int TM, int TN, int KSPLIT, int G, int MG, int AXK, bool BF16, class Pre>
 __device__ __forceinline__ void gemm_core(const GemmDesc& d, int m0, int n0, float* red,
-                                          float* rsum, bool rowsum, Pre&& pre, Early&& early) {
-  constexpr int AX = AAUX ? AAUX : SACMI_A_AUX;
-  constexpr bool MS = MIDSPLIT;
+                                          float* rsum, bool rowsum, Pre&& pre) {
   if constexpr (AXK == 1) {
-    if (d.axk == 1 && !d.ax_pre) {   // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
-      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1, BF16, 0, false, AX, MS>(
-          d, m0, n0, red, rsum, pre, n0 == 0 && d.ax_out != nullptr, early);
+    if (d.axk == 1) {   // fc3 backward folded into dh1 / dha1 (A = h2, B = W2)
+      gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 1, BF16>(d, m0, n0, red, rsum, pre,
+                                                                    n0 == 0 && d.ax_out != nullptr);
       return;
     }
   }
   if (d.a_kc) {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
-    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, true, true, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, true, false, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
   } else {
-    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
-    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
-    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16, PIPE, false, AX, MS>(d, m0, n0, red, rsum, pre, false, early);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// LDS-staged core (k_gemm CORE 1: the batch-256-class fp32 levels).
-//
-// Why: the register-direct core above reads its operands as 16 rows x 64 bytes per
-// wave-instruction (the 16x16x4 fragment: 4 lane groups x 16 B of each of 16 rows).  Measured
-// per CU with every CU loading at once (tools/l2_rate_bench.hip, profiles/r04/l2_rate.txt),
-// that shape takes 43 GB/s from an L2-resident operand, against ~150 GB/s for 128- to 1024-byte
-// row segments per instruction — the level bodies' "operand delivery" bound (round-3 phase
-// stamps: the last wave's K loop 2.2-2.5x wave 0's).
-//
-// How: the workgroup (16 waves) streams K in slabs of BK = 16 KSP through a ring of NST LDS
-// slots by LDS-DMA (global_load_lds_dwordx4: 1 KB per wave-instruction, 2-8 rows of
-// 128-512 contiguous bytes), slab s + NST - 1 issued right after the barrier that retires
-// slab s (counted vmcnt waits, no drain).  The tile TMW x TN is cut into NSUB sub-tiles of
-// 32 x WN, and the K of each slab into KSP 16-deep parts: wave (sub, part) runs the 16x16x4
-// MFMAs of its sub-tile over its part of every slab, reading fragments from LDS
-// (ds_read_b128 for a K-contiguous operand, 4 x ds_read_b32 for an MN-contiguous one; 16-byte
-// chunks XOR-swizzled by row on the DMA source address: conflict-free).  The KSP partial
-// tiles go to `red` in k_gemm's layout ([row / TM][part][TM][TN + 1]) and k_gemm's epilogue
-// (bias / ReLU / mask / fc3 dots / Adam / rowsum / dL/da partials) runs unchanged.  The ring
-// aliases `red` (the partials are written after the last slab is consumed).
-// Chunks past K are read from a clamped in-row address and zeroed in the fragments (last slab
-// only); rows past M / N read a clamped row and are discarded by the epilogue.
-typedef __attribute__((address_space(3))) void stg_lds_t;
-typedef __attribute__((address_space(1))) const void stg_gbl_t;
-
-template <int N>
-__device__ __forceinline__ void stg_vmwait() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
-}
-// s_waitcnt vmcnt(n) for a wave-uniform n (an immediate per case)
-__device__ __forceinline__ void stg_vmwait_n(int n) {
-  switch (n) {
-    case 0: stg_vmwait<0>(); break;   case 1: stg_vmwait<1>(); break;
-    case 2: stg_vmwait<2>(); break;   case 3: stg_vmwait<3>(); break;
-    case 4: stg_vmwait<4>(); break;   case 5: stg_vmwait<5>(); break;
-    case 6: stg_vmwait<6>(); break;   case 7: stg_vmwait<7>(); break;
-    case 8: stg_vmwait<8>(); break;   case 9: stg_vmwait<9>(); break;
-    case 10: stg_vmwait<10>(); break; case 11: stg_vmwait<11>(); break;
-    case 12: stg_vmwait<12>(); break; case 13: stg_vmwait<13>(); break;
-    case 14: stg_vmwait<14>(); break; default: stg_vmwait<15>(); break;
-  }
-}
-
-constexpr int kStgKW = 1024;     // K words staged for ax_w / a_ksc (launch_gemm checks K)
-constexpr int kStgRing = 144 * 1024;
-
-// geometry of a staged tile: TMW x TN, KSP K parts, 16 waves
-template <int TMW, int TN, int KSP>
-struct StgGeo {
-  static constexpr int NSUB = 16 / KSP, NSM = TMW / 32, NSN = NSUB / NSM;
-  static constexpr int WM = 32, WN = TN / NSN, MI = WM / 16, NJ = WN / 16;
-  static constexpr int BK = 16 * KSP;
-  static constexpr int SLOT = (TMW + TN) * BK * 4;                 // bytes per ring slot
-  static constexpr int NST = kStgRing / SLOT < 4 ? kStgRing / SLOT : 4;
-  static constexpr int RING = NST * SLOT;
-  static_assert(NSUB * KSP == 16 && NSM * 32 == TMW && NSN * NSM == NSUB && NJ * 16 * NSN == TN,
-                "staged tile geometry");
-  static_assert(NST >= 3 && SLOT % (16 * 1024) == 0, "staged ring");
-};
-
-// one operand's slab image: KC -> R rows (M or N) of BK k; MN -> BK rows (k) of R columns
-template <int R, int BK, bool KC>
-struct StgOp {
-  static constexpr int RB = KC ? BK * 4 : R * 4;        // bytes per LDS row
-  static constexpr int NR = KC ? R : BK;                 // LDS rows
-  static constexpr int CPR = RB / 16;                    // 16-byte chunks per row
-  static constexpr int SWZ = (CPR < 16 ? CPR : 16) - 1;  // chunk swizzle mask
-  static constexpr int RPP = 1024 / RB;                  // rows per 1 KB piece
-  static constexpr int BYTES = NR * RB, PIECES = BYTES / 1024;
-  static_assert(RB >= 128 && RB <= 1024 && BYTES % 1024 == 0, "staged operand shape");
-};
-
-template <int TM, int TN, int KSP, int MG, bool AKC, bool BKC, bool ROWSUM, int AXF, class Pre>
-__device__ __forceinline__ void gemm_core_s(const GemmDesc& d, int m0, int n0, unsigned char* ring,
-                                            float* rsum, float* s_kw, Pre&& pre, bool store_a,
-                                            tl_word* tl = nullptr) {
-  constexpr int TMW = TM * MG;
-  using G = StgGeo<TMW, TN, KSP>;
-  using OA = StgOp<TMW, G::BK, AKC>;
-  using OB = StgOp<TN, G::BK, BKC>;
-  constexpr int BK = G::BK, NST = G::NST, SLOT = G::SLOT, MI = G::MI, NJ = G::NJ;
-  constexpr int PPW = (OA::PIECES + OB::PIECES) / 16;
-  static_assert(OA::PIECES + OB::PIECES == SLOT / 1024 && PPW * 16 == SLOT / 1024 && OA::PIECES % 16 == 0,
-                "staged pieces: whole pieces per wave, A pieces first");
-  // store_a (AXF): every workgroup issues the same number of stores per slab (zero-length
-  // descriptor where it stores nothing), so the counted waits are uniform
-  constexpr int SST = AXF == 1 ? (TMW * BK / 4 + 1023) / 1024 : 0;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int sub = wave % G::NSUB, kp = wave / G::NSUB;
-  const int wm = (sub / G::NSN) * G::WM, wn = (sub % G::NSN) * G::WN;
-  const int g4 = lane >> 4, l16 = lane & 15;
-  const int K = d.K;
-  const int nslab = (K + BK - 1) / BK;
-  // staged K vector (AXF: the fc3 weights w; !AKC: the per-k scale, where the desc has one)
-  const bool has_ksc = AXF != 1 && !AKC && d.a_ksc != nullptr;
-  const float* kwsrc = AXF == 1 ? d.ax_w : d.a_ksc;
-  const bool has_kw = AXF == 1 || has_ksc;
-  // the K vector goes global -> LDS by DMA too (a ds_write behind the slab DMAs would wait for
-  // all of them: the compiler orders LDS stores after an LDS-DMA that may alias): one dword a
-  // lane, 64 words a wave, zeros past K (buffer range; zero-length where the level has none)
-  static_assert(kStgKW == 16 * 64, "one K-vector DMA per wave");
-  {
-    const rsrc_t rkw = make_rsrc(has_kw ? kwsrc : d.A, has_kw ? (uint32_t)K * 4u : 0u);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rkw, (stg_lds_t*)(s_kw + wave * 64), 4,
-                                             (uint32_t)(wave * 64 + lane) * 4u, 0, 0, 0);
-  }
-  pre();     // the epilogue's loads: the oldest vector-memory operations of the wave
-  // DMA source of each piece this wave moves: piece pc = wave + 16 q (A pieces first)
-  const char* pbase[PPW];
-  int kofs[PPW];
-#pragma unroll
-  for (int q = 0; q < PPW; ++q) {
-    const int pc = wave + 16 * q;
-    const bool isA = q < OA::PIECES / 16;
-    const int RPP = isA ? OA::RPP : OB::RPP, CPR = isA ? OA::CPR : OB::CPR, SW = isA ? OA::SWZ : OB::SWZ;
-    const bool kc = isA ? AKC : BKC;
-    const int Rr = (isA ? pc : pc - OA::PIECES) * RPP + lane / CPR;   // LDS row
-    const int c = (lane % CPR) ^ (Rr & SW);                           // global chunk it holds
-    const float* base = isA ? d.A : d.B;
-    const int ld = isA ? d.lda : d.ldb;
-    const int lim = isA ? d.M : d.N;
-    const int mn0 = isA ? m0 : n0;
-    if (kc) {   // row mn0 + Rr (clamped), k = slab k0 + 4 c
-      const int row = mn0 + Rr < lim ? mn0 + Rr : lim - 1;
-      pbase[q] = reinterpret_cast<const char*>(base + (size_t)row * ld);
-      kofs[q] = 4 * c;
-    } else {    // k row = slab k0 + Rr (clamped), column mn0 + 4 c (clamped)
-      const int col = mn0 + 4 * c < lim ? mn0 + 4 * c : 0;
-      pbase[q] = reinterpret_cast<const char*>(base + col);
-      kofs[q] = Rr;
-    }
-  }
-  auto issue = [&](int sl) {
-    unsigned char* dst = ring + (sl % NST) * SLOT;
-    const int k0 = sl * BK;
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      const bool isA = q < OA::PIECES / 16;
-      const bool kc = isA ? AKC : BKC;
-      const int ld = isA ? d.lda : d.ldb;
-      const char* g;
-      if (kc) {
-        const int k = k0 + kofs[q];
-        g = pbase[q] + (size_t)(k < K ? k : 0) * 4;
-      } else {
-        const int k = k0 + kofs[q];
-        g = pbase[q] + (size_t)(k < K ? k : K - 1) * ld * 4;
-      }
-      __builtin_amdgcn_global_load_lds((stg_gbl_t*)g, (stg_lds_t*)(dst + (wave + 16 * q) * 1024), 16, 0, 0);
-    }
-  };
-#pragma unroll
-  for (int sl = 0; sl < NST - 1; ++sl)
-    if (sl < nslab) issue(sl);
-  const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
-                               store_a ? (uint32_t)(((size_t)(d.M - 1) * d.ax_ld + d.K) * 4) : 0u);
-  f4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  float rs[MI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i) rs[i] = 0.f;
-  const bool rs_wave = ROWSUM && wn == 0;   // one column of sub-tiles sums the rows
-  for (int sl = 0; sl < nslab; ++sl) {
-    // vector-memory ops issued after slab sl's DMA: the later prologue slabs, then per
-    // iteration i < sl its stores and (while slabs remain) the DMA of slab i + NST - 1
-    int younger = 0;
-    if (sl < NST - 1) younger += ((NST - 2 < nslab - 1 ? NST - 2 : nslab - 1) - sl) * PPW;
-    for (int i = (sl - NST + 2 > 0 ? sl - NST + 2 : 0); i < sl; ++i)
-      younger += SST + (i + NST - 1 < nslab ? PPW : 0);
-    stg_vmwait_n(younger);
-    __builtin_amdgcn_s_barrier();          // slab sl landed for every wave; slot (sl - 1) free
-    asm volatile("" ::: "memory");
-    if (sl == 0) SACMI_PHASE(tl, 8);
-    if (sl == nslab - 1) SACMI_PHASE(tl, 9);
-    (void)tl;
-    const unsigned char* st = ring + (sl % NST) * SLOT;
-    const int kb = sl * BK;
-    if constexpr (AXF == 1) {
-      // u = transformed A rows of this slab, stored by the column-tile-0 workgroups
-#pragma unroll
-      for (int q = 0; q < SST; ++q) {
-        const int e = tid + 1024 * q, row = e / (BK / 4), c = e % (BK / 4);
-        const int k = kb + 4 * c;
-        f4 v = {0.f, 0.f, 0.f, 0.f};
-        if (row < TMW) {
-          const f4 h = *reinterpret_cast<const f4*>(st + row * OA::RB + ((c ^ (row & OA::SWZ)) << 4));
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) v[s2] = (h[s2] > 0.f && k + s2 < K) ? s_kw[k + s2] : 0.f;
-        }
-        const bool ok = row < TMW && m0 + row < d.M && k < K;
-        buf_st4(rAx, ok ? (uint32_t)((m0 + row) * d.ax_ld + k) * 4u : 0xfffffff0u, v);
-      }
-    }
-    if (sl + NST - 1 < nslab) issue(sl + NST - 1);
-    // this wave's 16-deep part of the slab
-    float a[MI][4], b[NJ][4];
-    const int kk = kp * 16 + 4 * g4;       // the lane group's first k inside the slab
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int r = wm + i * 16 + l16;
-      if constexpr (AKC) {
-        const int c = kk >> 2;
-        const f4 x = *reinterpret_cast<const f4*>(st + r * OA::RB + ((c ^ (r & OA::SWZ)) << 4));
-        a[i][0] = x[0]; a[i][1] = x[1]; a[i][2] = x[2]; a[i][3] = x[3];
-      } else {
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          const int R = kk + s2;
-          a[i][s2] = *reinterpret_cast<const float*>(st + R * OA::RB + ((((r >> 2) ^ (R & OA::SWZ))) << 4) + (r & 3) * 4);
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = wn + j * 16 + l16;
-      const unsigned char* sb = st + OA::BYTES;
-      if constexpr (BKC) {
-        const int c = kk >> 2;
-        const f4 x = *reinterpret_cast<const f4*>(sb + n * OB::RB + ((c ^ (n & OB::SWZ)) << 4));
-        b[j][0] = x[0]; b[j][1] = x[1]; b[j][2] = x[2]; b[j][3] = x[3];
-      } else {
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          const int R = kk + s2;
-          b[j][s2] = *reinterpret_cast<const float*>(sb + R * OB::RB + ((((n >> 2) ^ (R & OB::SWZ))) << 4) + (n & 3) * 4);
-        }
-      }
-    }
-    {
-#pragma clang fp contract(off)
-      const int k = kb + kk;
-      if (K - kb < BK) {   // the last, partial slab: k >= K contributes nothing
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          const bool in = k + s2 < K;
-#pragma unroll
-          for (int i = 0; i < MI; ++i) a[i][s2] = in ? a[i][s2] : 0.f;
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) b[j][s2] = in ? b[j][s2] : 0.f;
-        }
-      }
-      if constexpr (AXF == 1) {
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          const float w = s_kw[k + s2 < kStgKW ? k + s2 : 0];
-#pragma unroll
-          for (int i = 0; i < MI; ++i) a[i][s2] = (a[i][s2] > 0.f && k + s2 < K) ? w : 0.f;
-        }
-      } else if constexpr (!AKC) {
-        if (has_ksc) {
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) {
-            const float f = s_kw[k + s2 < kStgKW ? k + s2 : 0];
-#pragma unroll
-            for (int i = 0; i < MI; ++i) a[i][s2] *= f;
-          }
-        }
-      }
-      mfma_chunk<MI, NJ, false>(acc, a, b);
-      if (ROWSUM && rs_wave) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i) rs[i] += (a[i][0] + a[i][1]) + (a[i][2] + a[i][3]);
-      }
-    }
-  }
-  __syncthreads();                          // every wave is past its last ring read
-  // partial tiles into red = the ring: red[((row / TM) * KSP + kp) * TM * (TN + 1) + (row % TM) * (TN + 1) + col]
-  float* red = reinterpret_cast<float*>(ring);
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm + i * 16 + g4 * 4 + r, col = wn + j * 16 + l16;
-        red[((row / TM) * KSP + kp) * TM * (TN + 1) + (row % TM) * (TN + 1) + col] = acc[i][j][r];
-      }
-  if (ROWSUM && rs_wave) {
-    // lanes l, l+16, l+32, l+48 hold the same row: fold the 4 lane groups, fixed order
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      float v = rs[i];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      const int row = wm + i * 16 + lane;
-      if (lane < 16) rsum[((row / TM) * KSP + kp) * TM + row % TM] = v;
-    }
-  }
-}
-
-template <int TM, int TN, int KSP, int MG, int AXK, class Pre>
-__device__ __forceinline__ void gemm_core_stg(const GemmDesc& d, int m0, int n0, unsigned char* ring,
-                                              float* rsum, float* s_kw, bool rowsum, Pre&& pre,
-                                              tl_word* tl) {
-  if constexpr (AXK == 1) {
-    if (d.axk == 1) {
-      gemm_core_s<TM, TN, KSP, MG, true, false, false, 1>(d, m0, n0, ring, rsum, s_kw, pre,
-                                                          n0 == 0 && d.ax_out != nullptr, tl);
-      return;
-    }
-  }
-  if (d.a_kc) {
-    if (d.b_kc) gemm_core_s<TM, TN, KSP, MG, true, true, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
-    else gemm_core_s<TM, TN, KSP, MG, true, false, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
-  } else {
-    if (d.b_kc) gemm_core_s<TM, TN, KSP, MG, false, true, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
-    else if (rowsum) gemm_core_s<TM, TN, KSP, MG, false, false, true, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
-    else gemm_core_s<TM, TN, KSP, MG, false, false, false, 0>(d, m0, n0, ring, rsum, s_kw, pre, false, tl);
+    if (d.b_kc) gemm_core_l<TM, TN, KSPLIT, G, false, true, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
+    else if (rowsum) gemm_core_l<TM, TN, KSPLIT, G, false, false, true, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
+    else gemm_core_l<TM, TN, KSPLIT, G, false, false, false, MG, 0, BF16>(d, m0, n0, red, rsum, pre);
   }
 }
 
@@ -1084,8 +490,7 @@ __device__ __forceinline__ uint32_t s_ld(sbuf_i4 r, uint32_t byte_off) {
 // The fused-Adam level's scalar work (losses, the alpha step, the loss ring, the done word),
 // by ONE wave, on wave-uniform values read by scalar loads (s_ld).  Every value it reads
 // was written by an earlier level, and nothing of the level reads what it writes, so it
-// runs at the level's start (k_gemm, GemmBatch::adam_wg -2: wave 0 of block 0 before its
-// tile) — after the tile it made block 0 the level's last workgroup by 2.7-2.9 us (a chain
+// runs at the level's start (k_gemm: wave 0 of block 0 before its tile) — after the tile it made block 0 the level's last workgroup by 2.7-2.9 us (a chain
 // of dependent round trips, then a system-scope fence; phase stamps, profiles/r04).
 __device__ __forceinline__ void adam_block0_wave(const AdamFuse& af, int err, float omb1, float omb2) {
   const sbuf_i4 rLp = s_rsrc(af.loss_part), rSc = s_rsrc(af.sc);
@@ -1144,7 +549,7 @@ __device__ __forceinline__ void adam_block0_wave(const AdamFuse& af, int err, fl
     *reinterpret_cast<volatile int*>(af.done_word) = v;
   }
 }
-// ... after the block's tile (adam_wg -1, or a dedicated workgroup): wave 0
+// ... after the block's work (the split-K weight-gradient finish, k_dw_fin): wave 0
 __device__ __forceinline__ void adam_block0(const AdamFuse& af, int err, float omb1, float omb2) {
   __syncthreads();
   if (threadIdx.x >= 64) return;
@@ -1209,7 +614,7 @@ struct RowsRegs {
   float lpa;                  // actor block 0, wave past the row threads: logp_part[lane]
 };
 
-template <int TMW, int NTH, int AUX = 0>
+template <int TMW, int NTH>
 __device__ __forceinline__ void rows_load(const RowsFuse& rf, const GemmDesc& d, int m0,
                                           RowsRegs& x) {
   const int t = threadIdx.x;
@@ -1231,16 +636,16 @@ __device__ __forceinline__ void rows_load(const RowsFuse& rf, const GemmDesc& d,
     const uint32_t base = (uint32_t)(((size_t)sl * rf.B + m0 + row) * rf.nparts) * 4u;
 #pragma unroll
     for (int i = 0; i < kRowsPv; ++i)
-      x.pv[i] = buf_ld_aux<AUX>(rPart, ok && i < rf.nparts ? base + 4u * i : oob);
+      x.pv[i] = buf_ld(rPart, ok && i < rf.nparts ? base + 4u * i : oob);
   }
   const int b = m0 + t;
   const uint32_t ob = (uint32_t)((t < TMW && b < rf.B) ? b : 0) * 4u;
-  x.alpha = buf_ld_aux<AUX>(rSc, 0u);
-  x.lp = buf_ld_aux<AUX>(rLp, ob);
-  x.r = buf_ld_aux<AUX>(rR, ob);
-  x.d = buf_ld_aux<AUX>(rD, ob);
+  x.alpha = buf_ld(rSc, 0u);
+  x.lp = buf_ld(rLp, ob);
+  x.r = buf_ld(rR, ob);
+  x.d = buf_ld(rD, ob);
   const int lane = t - TMW * nslot;
-  x.lpa = buf_ld_aux<AUX>(rLpa, (uint32_t)(2 * (lane >= 0 && lane < rf.n_lp ? lane : 0) + 1) * 4u);
+  x.lpa = buf_ld(rLpa, (uint32_t)(2 * (lane >= 0 && lane < rf.n_lp ? lane : 0) + 1) * 4u);
 }
 
 template <int TMW, int NTH>
@@ -1350,45 +755,6 @@ __device__ __forceinline__ void rows_loss(const RowsFuse& rf, int m0, bool write
   }
 }
 
-// LDS-staged 128x128 forward kernel for large-M levels (k_fwd) and its tile threshold
-#ifndef SACMI_FWD_BIG
-#define SACMI_FWD_BIG 1
-#endif
-#ifndef SACMI_DW_SPLIT
-#define SACMI_DW_SPLIT 1
-#endif
-#ifndef SACMI_FWD_BF16_N64
-#define SACMI_FWD_BF16_N64 1
-#endif
-#ifndef SACMI_FWD_BF16_ALL64
-#define SACMI_FWD_BF16_ALL64 0
-#endif
-#ifndef SACMI_FWD_BIG_FP32
-#define SACMI_FWD_BIG_FP32 0
-#endif
-#ifndef SACMI_FWD_BIG_MIN
-#define SACMI_FWD_BIG_MIN 1      // x 256 tiles of 128x128
-#endif
-// K split per wave group of the batch-4096-class tile configurations (tuning knobs)
-#ifndef SACMI_FWD_KS
-#define SACMI_FWD_KS 4
-#endif
-#ifndef SACMI_AXK_KS
-#define SACMI_AXK_KS 4
-#endif
-#ifndef SACMI_DW_KS
-#define SACMI_DW_KS 8
-#endif
-#ifndef SACMI_PIPE
-#define SACMI_PIPE 0
-#endif
-#ifndef SACMI_PIN_EPI
-#define SACMI_PIN_EPI 1         // k_gemm: the epilogue's desc fields in the K loop's round trip
-#endif
-#ifndef SACMI_PIPE_DW
-#define SACMI_PIPE_DW 0
-#endif
-
 // data-parallel phase 0: the update's error flags for the critic gradient collective
 // (kDpFlagN; GemmBatch::err_flags).  Every error source of the update ran before this level.
 __device__ __forceinline__ void store_err_flags(const GemmBatch& b) {
@@ -1440,7 +806,7 @@ __device__ __forceinline__ float one_minus_tanh2(float x) {
 
 // one (row m, action j) element of GaussianPolicy.sample from its head sums (bias added):
 // the action, cache and noise stores and the NaN check; returns the element's log-prob term
-template <bool H16, int AAUX>
+template <bool H16>
 __device__ __forceinline__ float heads_elem(const HeadSampleArgs& a, int m, int j, float mean, float ls_raw,
                                             float eps_in, uint64_t ctr) {
   const int A = a.A;
@@ -1450,12 +816,7 @@ __device__ __forceinline__ float heads_elem(const HeadSampleArgs& a, int m, int 
   // NaN) and scale positive — std = exp(clamp(log_std)) is NaN only for a NaN log_std
   // (torch.clamp keeps NaN; fmaxf above does not, hence the raw value).  evaluate=True
   // (deterministic) builds no Normal, so nothing is checked there (sac_imp.py:59-65).
-#if defined(SACMI_EXP_NOMFMA) || defined(SACMI_EXP_NOLOAD) || defined(SACMI_EXP_NOADAMIO) || \
-    defined(SACMI_EXP_EMPTY) || defined(SACMI_EXP_DESC) || defined(SACMI_EXP_NOSTORE)
-  if (false) {   // timing experiments compute garbage: never void their updates
-#else
   if (a.nan_flag && !a.deterministic && (__builtin_isnan(mean) || __builtin_isnan(ls_raw))) {
-#endif
     const int bit = m < a.split_row ? a.nan_bit_lo : a.nan_bit_hi;
     if (a.nan_plain) *a.nan_flag = bit;
     else atomicOr(a.nan_flag, bit);
@@ -1473,8 +834,8 @@ __device__ __forceinline__ float heads_elem(const HeadSampleArgs& a, int m, int 
   const float y = tanhf(x);
   if constexpr (H16)
     reinterpret_cast<unsigned short*>(a.act)[(size_t)m * a.ldact + j] = bf16_bits(y * a.scale + a.bias);
-  else   // (write-through where the same launch reads them back: k_chain_a's L3)
-    st_pol(a.act + (size_t)m * a.ldact + j, y * a.scale + a.bias, AAUX != 0);
+  else
+    a.act[(size_t)m * a.ldact + j] = y * a.scale + a.bias;
   if (a.act_host) a.act_host[(size_t)m * A + j] = y * a.scale + a.bias;
   const float dx = x - mean;
   float lpe = -(dx * dx) / (2.f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
@@ -1487,7 +848,7 @@ __device__ __forceinline__ float heads_elem(const HeadSampleArgs& a, int m, int 
 
 // rows [m0, m0 + TM): the log-prob row sums from lp (every thread of the workgroup calls it)
 // and the row block's logp_part slot pair
-template <int TM, int AAUX>
+template <int TM>
 __device__ __forceinline__ void heads_logp(const HeadSampleArgs& a, int m0, int part, float (*lp)[33],
                                            float* s_lp) {
   const int A = a.A;
@@ -1497,7 +858,7 @@ __device__ __forceinline__ void heads_logp(const HeadSampleArgs& a, int m0, int 
     float s = 0.f;
     if (mm < a.rows) {
       for (int jj = 0; jj < A; ++jj) s += lp[threadIdx.x][jj];
-      st_pol(a.logp + mm, s, AAUX != 0);
+      a.logp[mm] = s;
     }
     s_lp[threadIdx.x] = s;
   }
@@ -1514,92 +875,47 @@ __device__ __forceinline__ void heads_logp(const HeadSampleArgs& a, int m0, int 
   }
 }
 
-template <int TN, int KSPLIT, bool H16, int TM, int AAUX>
-__device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int part, float* red,
-                                           float (*lp)[33], float* s_lp);
-
-// waves per SIMD the register allocation must allow: every wave of the workgroup
-// resident at once, one workgroup per CU
-template <int W>
-constexpr int gemm_min_waves() { return 4; }   // 16 waves per CU: one 1024- or two 512-thread WGs
 
 // TM x TN per wave group, MG wave groups (workgroup tile MG*TM x TN), K split KSPLIT
 // ways inside each group; ADAM: fused optimizer epilogue (every desc EPI_ADAM*); BF16:
-// bf16 MFMA operands (GemmBatch::bf16), everything around them fp32
-// CORE 0: register-direct operand loads, K split KSPLIT ways across 64*KSPLIT*MG threads;
-// CORE 1: the LDS-staged core (gemm_core_s), 1024 threads, KSPLIT = its K parts (partial tiles)
-template <int KSPLIT, int MG, int CORE>
-constexpr int gemm_threads() { return CORE ? 1024 : 64 * KSPLIT * MG; }
-template <int CORE, int TMW, int TN, int KSP>
-constexpr int stg_ring() {
-  if constexpr (CORE == 1) return StgGeo<TMW, TN, KSP>::RING;
-  else return 1;
-}
+// bf16 MFMA operands (GemmBatch::bf16), everything around them fp32.  64*KSPLIT*MG threads.
+template <int KSPLIT, int MG>
+constexpr int gemm_threads() { return 64 * KSPLIT * MG; }
 // LDS of one k_gemm configuration (kg_body)
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, bool HFOLD = false>
-constexpr bool kg_heads_fold() {
-  // (an instantiation of its own: the fold's registers and code cost the plain levels of
-  // this tile configuration ~0.6-0.8 us each when compiled in)
-  return HFOLD && !ADAM && AXK == 0 && CORE == 0 && !BF16 && MG == 1 && TM == kHeadsFoldTM && TN == 64 &&
-         KSPLIT == 16 && G == 2;
-}
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, bool HFOLD = false>
+template <int TM, int TN, int KSPLIT, int MG, int AXK>
 struct KgSmem {
   static constexpr int TMW = TM * MG;
   static constexpr bool PA = AXK == 1 && MG == 1;
-  static constexpr bool HF = kg_heads_fold<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, HFOLD>();
-  alignas(16) unsigned char ring[stg_ring<CORE, TMW, TN, KSPLIT>()];
-  float red_l[CORE ? 1 : MG * KSPLIT * TM * (TN + 1)];
-  float s_kw[CORE ? kStgKW : 1];
+  float red[MG * KSPLIT * TM * (TN + 1)];
   float rsum[MG * KSPLIT * TM];
   AdamScalars s_k;
   int s_err;
   float s_q[TMW][4], s_coef[2][TMW], s_l[TMW][2], s_dotw[TN];
   float s_pa[PA ? TMW * (TN + 1) + TN * 32 : 1];
-  float s_hlp[HF ? kHeadsFoldTM * (TN + 1) : 1];   // the tile's h (folded heads' partial)
-  int s_hlast;
 };
 
-// The body of one k_gemm workgroup: work item `bid_in` of the level (a tile, a ride-along
-// workgroup, the scalar Adam workgroup).  k_gemm runs it as blockIdx.x; the persistent chain
-// kernel (k_chain) runs it for each work item of its cohort.  LDAUX: cache-policy bits of the
-// loads of operands another workgroup of the SAME launch produced (the A operand, the row
-// prologue's dot partials, the ReLU-mask source): sc1 (16) in k_chain, 0 in k_gemm.
-// MIDSPLIT (k_chain): mid (ChainWait) — the previous phase's cohort barrier — issues its first
-// poll at entry (mid.issue()) and waits (mid()) inside the K loop's load burst, after the
-// weights' loads and before the A operand's (gemm_core_l), or before a return that loads
-// nothing; every workgroup that calls the body with it reaches both once.
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16, int CORE, int LDAUX,
-          bool MIDSPLIT = false, bool HFOLD = false, class Mid = void (*)()>
-__device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in,
-                                        KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, HFOLD>& sm,
-                                        Mid&& mid = [] {}) {
-  if constexpr (MIDSPLIT) mid.issue();   // (k_chain: the barrier's first poll, ahead of every load)
-  // The scalars that locate this workgroup's work come in ONE kernarg round trip: left to
-  // the compiler, each load sat behind a branch on the previous one (timeline pointer, tile
-  // count, one desc's tile_begin per loop trip, then the desc's fields as they were used),
-  // ~1-1.5 us of dependent scalar round trips before the first operand load of every level
-  // (phase stamps, tools/phase_dump.py).  The asm pins force each value into an SGPR
-  // there, so every load is issued before the one wait.
+// The body of one k_gemm workgroup: work item `bid` of the level (a tile, a ride-along
+// workgroup, the scalar Adam workgroup).
+// The scalars that locate this workgroup's work come in ONE kernarg round trip: left to
+// the compiler, each load sat behind a branch on the previous one (timeline pointer, tile
+// count, one desc's tile_begin per loop trip, then the desc's fields as they were used),
+// ~1-1.5 us of dependent scalar round trips before the first operand load of every level
+// (phase stamps, tools/phase_dump.py).  The asm pins force each value into an SGPR
+// there, so every load is issued before the one wait.
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK, bool BF16>
+__device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid,
+                                        KgSmem<TM, TN, KSPLIT, MG, AXK>& sm) {
   tl_word* const tl = batch.tl;
   const int n_tiles = batch.total_tiles, n_desc = batch.count;
   int tbeg[kMaxGemms];
 #pragma unroll
   for (int q = 0; q < kMaxGemms; ++q) tbeg[q] = batch.d[q].tile_begin;
-  const int adam_wg = batch.adam_wg;
-  // (k_chain runs several bodies in one register allocation: there the pins would keep ~40
-  // SGPRs of each level live at once — spills — so it leaves the loads to the compiler)
-  constexpr bool PINS = LDAUX == 0;
-  if constexpr (PINS) {
-    asm volatile("" :: "s"(tl), "s"(n_tiles), "s"(n_desc), "s"(adam_wg));
+  asm volatile("" :: "s"(tl), "s"(n_tiles), "s"(n_desc));
 #pragma unroll
-    for (int q = 0; q < kMaxGemms; ++q) asm volatile("" :: "s"(tbeg[q]));
-  }
-#if SACMI_PIN_EPI
+  for (int q = 0; q < kMaxGemms; ++q) asm volatile("" :: "s"(tbeg[q]));
   // ... with the level-wide epilogue scalars that do not depend on the desc (the row
   // prologue's / fused Adam's pointers): otherwise their loads sit behind the desc's
-  if constexpr (!PINS) {
-  } else if constexpr (AXK == 1) {
+  if constexpr (AXK == 1) {
     const RowsFuse& r = batch.rows;
     asm volatile("" :: "s"(r.part), "s"(r.logp), "s"(r.r), "s"(r.d), "s"(r.kind), "s"(r.nparts),
                  "s"(r.B), "s"(r.sc), "s"(r.logp_part), "s"(r.n_lp));
@@ -1608,20 +924,10 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
     asm volatile("" :: "s"(a.P), "s"(a.M), "s"(a.V), "s"(a.T), "s"(a.G), "s"(a.t_base), "s"(a.sc),
                  "s"(a.step_offset));
   }
-#endif
   SACMI_PHASE(tl, 0);
   SACMI_PHASE_LAST(tl, 6);
   constexpr int TMW = TM * MG;
-  static_assert(!CORE || !BF16, "the staged core is fp32");
-  // CORE 1: the operand ring, which the partial tiles (`red`) alias after the K loop; its
-  // K vector (ax_w / a_ksc) staging
-  constexpr int RING = stg_ring<CORE, TMW, TN, KSPLIT>();
-  static_assert(!CORE || RING >= MG * KSPLIT * TM * (TN + 1) * 4, "staged ring holds the partial tiles");
-  // LDS (KgSmem: the caller's, so that a persistent kernel can run several configurations
-  // in one allocation)
-  unsigned char* const ring = sm.ring;
-  float* const red = CORE ? reinterpret_cast<float*>(sm.ring) : sm.red_l;
-  float* const s_kw = sm.s_kw;
+  float* const red = sm.red;
   float* const rsum = sm.rsum;
   AdamScalars& s_k = sm.s_k;
   int& s_err = sm.s_err;
@@ -1633,34 +939,8 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   // and its fc1 action weights [TN][32]
   constexpr bool PA = AXK == 1 && MG == 1;
   float* const s_pa = sm.s_pa;
-  // the policy heads folded into this level (GemmBatch::heads): the fp32 32x64 forward tiles
-  constexpr bool HF = kg_heads_fold<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, HFOLD>();
-  float* const s_hlp = sm.s_hlp;
-  int& s_hlast = sm.s_hlast;
-  const int bid = bid_in;
-#ifdef SACMI_EXP_EMPTY
-  if (bid < batch.total_tiles) return;   // timing experiment only: the launch, nothing else
-#endif
-#ifdef SACMI_EXP_DESC
-  {   // timing experiment only: the launch + this workgroup's descriptor, then out
-    int pq = 0;
-    for (int q = 1; q < batch.count; ++q)
-      if (bid >= batch.d[q].tile_begin) pq = q;
-    if (bid < batch.total_tiles && batch.d[pq].M == -7) red[threadIdx.x] = 1.f;
-    if (bid < batch.total_tiles) return;
-  }
-#endif
-  if (bid >= n_tiles && MIDSPLIT) mid();   // (k_chain: rides read nothing of the chain)
-  if (bid >= n_tiles && bid == adam_wg) {
-    // the level's scalar Adam work on a workgroup of its own, at once: its inputs (loss
-    // partials, log_alpha's gradient, the scalars) come from earlier levels, and no tile's
-    // workgroup waits behind it (block 0 did it after its tile: +2.6-3 us on the level)
-    const AdamFuse& af = batch.adam;
-    adam_block0(af, af.sc->err, 1.f - af.beta1, 1.f - af.beta2);
-    return;
-  }
   if (bid >= n_tiles) {   // ride-along workgroups (next update's replay work, Polyak)
-    if constexpr (gemm_threads<KSPLIT, MG, CORE>() == 1024) {   // the host attaches rides to 1024-thread configs
+    if constexpr (gemm_threads<KSPLIT, MG>() == 1024) {   // the host attaches rides to 1024-thread configs
       const int rb = bid - n_tiles;
       if (rb >= (batch.ride.kind ? batch.ride.nblocks : 0)) {
         polyak_ride(batch.ride.pk, rb - (batch.ride.kind ? batch.ride.nblocks : 0), batch.ride.pk_blocks);
@@ -1686,7 +966,6 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
 #define SACMI_DESC_PIN_K "s"(d.A), "s"(d.B), "s"(d.M), "s"(d.N), "s"(d.K), "s"(d.lda), "s"(d.ldb), \
     "s"(d.a_kc), "s"(d.b_kc), "s"(d.tiles_n), "s"(d.tiles_m), "s"(d.xcd_gr), "s"(d.pl_div), \
     "s"(d.pl_mag), "s"(d.pl_gc_log2), "s"(d.pl_sr)
-#if SACMI_PIN_EPI
   // ... and, in the same round trip (one asm statement: every load issued before the one
   // wait), the fields the epilogue's buffer descriptors and scalars are formed from — the
   // compiler forms them before the K loop, behind branches on the fields: two or three more
@@ -1694,8 +973,7 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
 #define SACMI_DESC_PIN_E "s"(d.C), "s"(d.aux), "s"(d.ldc), "s"(d.ldaux), "s"(d.epi), "s"(d.bias), \
     "s"(d.bias_ld), "s"(d.dotw), "s"(d.dotp), "s"(d.rs_col), "s"(d.axk), "s"(d.ax_w), "s"(d.ax_out), \
     "s"(d.ax_ld), "s"(d.a_ksc)
-  if constexpr (!PINS) {
-  } else if constexpr (ADAM) {
+  if constexpr (ADAM) {
     const AdamFuse& a = batch.adam;
     asm volatile("" :: SACMI_DESC_PIN_K, SACMI_DESC_PIN_E, "s"(a.P), "s"(a.M), "s"(a.V), "s"(a.T),
                  "s"(a.G), "s"(a.t_base), "s"(a.lr), "s"(a.beta1), "s"(a.beta2), "s"(a.eps),
@@ -1708,23 +986,19 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   } else {
     asm volatile("" :: SACMI_DESC_PIN_K, SACMI_DESC_PIN_E);
   }
-#else
-  if constexpr (PINS) asm volatile("" :: SACMI_DESC_PIN_K);
-#endif
-  if constexpr (CORE == 0) SACMI_PHASE(batch.tl, 8);   // (diagnostic: the desc has landed)
+#undef SACMI_DESC_PIN_K
+#undef SACMI_DESC_PIN_E
+  SACMI_PHASE(batch.tl, 8);   // (diagnostic: the desc has landed)
   const int t = bid - tbeg[p];
-  if (t >= d.tiles_m * d.tiles_n) {   // padding to a multiple of 8 blocks
-    if constexpr (MIDSPLIT) mid();
-    return;
-  }
+  if (t >= d.tiles_m * d.tiles_n) return;   // padding to a multiple of 8 blocks
   int tr, tc;
   place_tile(d, t, tr, tc);
   const int m0 = tr * TMW, n0 = tc * TN;
-  if constexpr (CORE == 0) SACMI_PHASE(batch.tl, 9);   // (diagnostic: the tile is placed)
+  SACMI_PHASE(batch.tl, 9);   // (diagnostic: the tile is placed)
   if constexpr (ADAM) {
     // the level's scalar Adam work first, on wave 0 of block 0 (adam_block0_wave): the
     // other waves start their K loops, wave 0 follows ~3 us later, inside the tile's time
-    if (adam_wg == -2 && bid == 0 && threadIdx.x < 64) {
+    if (bid == 0 && threadIdx.x < 64) {
       const AdamFuse& a = batch.adam;
       adam_block0_wave(a, (int)s_ld(s_rsrc(a.sc), (uint32_t)offsetof(DevScalars, err)), 1.f - a.beta1,
                        1.f - a.beta2);
@@ -1738,7 +1012,7 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   // Element slots: EPT tile outputs per thread (e = tid + s*NTH) plus one slot for the
   // rowsum (bias-gradient) column.  Their epilogue operands (bias, ReLU mask, Adam
   // state) are loaded by pre() while the MFMAs run.
-  constexpr int NTH = gemm_threads<KSPLIT, MG, CORE>(), EPT = TMW * TN / NTH, NS = EPT + 1;
+  constexpr int NTH = gemm_threads<KSPLIT, MG>(), EPT = TMW * TN / NTH, NS = EPT + 1;
   static_assert(TMW * TN % NTH == 0 && TMW <= NTH, "epilogue slot layout");
   const int tid = threadIdx.x;
   // slot s -> (row, col in tile, output column n, valid); recomputed where needed so
@@ -1756,7 +1030,7 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
     n = d.rs_col;
     return rowsum && tid < TMW && m0 + row < d.M;
   };
-  const bool wt = SACMI_WT && batch.st_wt;   // output store policy of this level
+  const bool wt = batch.st_wt != 0;   // output store policy of this level
   const bool pol = d.epi == EPI_ADAM_POLYAK;
   // byte span of this desc's output (tile rows, plus the rowsum column; the fused-Adam
   // 4-column groups reach the row's padding up to a multiple of 4: ldc is one)
@@ -1764,9 +1038,6 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   const uint32_t span = (uint32_t)(((size_t)(d.M - 1) * d.ldc + (d.rs_col >= ncov ? d.rs_col + 1 : ncov)) * 4);
   const size_t abase = ADAM ? (size_t)(d.C - af.P) : 0;
   const rsrc_t rC = make_rsrc(d.C, span);
-  // u rows (GemmDesc::u_out): a zero-length range where the desc stores none
-  const rsrc_t rU = make_rsrc(d.u_out ? d.u_out : d.C,
-                              d.u_out ? (uint32_t)(((size_t)(d.M - 1) * d.u_ld + d.N) * 4) : 0u);
   // (unused descriptors get a zero-length range: any access through them is dropped)
   const rsrc_t rM = make_rsrc(ADAM ? af.M + abase : d.C, ADAM ? span : 0);
   const rsrc_t rV = make_rsrc(ADAM ? af.V + abase : d.C, ADAM ? span : 0);
@@ -1805,43 +1076,17 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   constexpr int PW = PA ? (TN * 32 + NTH - 1) / NTH : 1;
   float paw_x[PW];
   const bool has_pa = PA && d.pa_out != nullptr;
-  // CORE 1: the Adam scalars by scalar loads into every wave (lgkmcnt: no vector-memory round
-  // trip in front of the slab DMAs, and no LDS store that would wait for them)
-  uint32_t skw[5] = {0u, 0u, 0u, 0u, 0u};
-  // folded heads (HF): a policy tile forms its columns' share of the heads (a split-K
-  // partial), so its head-weight columns come in with the epilogue operands
-  const bool hf_mine = HF && batch.heads_ticket != nullptr && p >= batch.heads_desc &&
-                       p < batch.heads_desc + batch.heads_ndesc;
-  constexpr int HWPT = HF ? (48 * TN + NTH - 1) / NTH : 1;   // (2A <= 48)
-  float hw_x[HWPT];
   auto pre = [&]() {
-    if constexpr (ADAM && CORE == 1) {
-      const sbuf_i4 r = s_rsrc(af.sc);
-      const uint32_t o = (uint32_t)(offsetof(DevScalars, beta_pow) + d.adam_step * 16);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) skw[q] = s_ld(r, o + 4u * q);
-      skw[4] = s_ld(r, (uint32_t)offsetof(DevScalars, err));
-    } else if constexpr (ADAM) {
+    if constexpr (ADAM) {
       if (threadIdx.x == 0) {
         s_k = fuse_scalars(af, d.adam_step, af.step_offset);
         s_err = af.sc->err;
       }
     }
-    if constexpr (HF) {   // zero-length range where this tile folds nothing
-      const HeadSampleArgs& ha = batch.heads;
-      const int n2 = 2 * ha.A;
-      const rsrc_t rHW = make_rsrc(hf_mine ? ha.Wh : d.C,
-                                   hf_mine ? (uint32_t)(((size_t)(n2 - 1) * ha.ldw + ha.K) * 4) : 0u);
-#pragma unroll
-      for (int q = 0; q < HWPT; ++q) {
-        const int e = tid + q * NTH, j = e / TN, cc = e - j * TN;
-        hw_x[q] = buf_ld(rHW, e < n2 * TN && n0 + cc < ha.K ? (uint32_t)(j * ha.ldw + n0 + cc) * 4u : 0xfffffff0u);
-      }
-    }
     // axk 1: the row prologue's loads.  Issued here, behind the operand burst, and
     // consumed after the MFMAs: anything in flight at the k-loop header is waited for by
     // the back-edge's conservative vmcnt on the first iteration.
-    if constexpr (AXK == 1) rows_load<TMW, NTH, LDAUX>(batch.rows, d, m0, rows_x);   // unconditional
+    if constexpr (AXK == 1) rows_load<TMW, NTH>(batch.rows, d, m0, rows_x);   // unconditional
     if constexpr (PA) {   // zero-length range where the level has no partials
       const rsrc_t rPW = make_rsrc(has_pa ? d.pa_w : d.C,
                                    has_pa ? (uint32_t)(((size_t)(d.N - 1) * d.pa_ld + d.pa_A) * 4) : 0u);
@@ -1867,13 +1112,8 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
         int row, c4, n;
         const bool ok = group(s, row, c4, n);
         const uint32_t o = ok ? (uint32_t)((m0 + row) * d.ldc + n) * 4u : kOob;
-#ifdef SACMI_EXP_NOADAMIO
-        // timing experiment only: no optimizer-state traffic
-        q0[s] = q1[s] = q2[s] = q3[s] = float4{0.f, 0.f, 0.f, (float)o};
-#else
         q0[s] = buf_ld4(rC, o); q1[s] = buf_ld4(rM, o); q2[s] = buf_ld4(rV, o);
         q3[s] = buf_ld4(rT, o);
-#endif
       }
       int row, col, n;
       const bool ok = slot(EPT, row, col, n);      // the rowsum slot
@@ -1889,19 +1129,12 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
         const uint32_t o = !ok ? kOob
                          : d.bias ? (uint32_t)(n * d.bias_ld) * 4u
                                   : (uint32_t)((m0 + row) * d.ldaux + n) * 4u;
-        x0[s] = buf_ld_aux<LDAUX>(rX, o);
+        x0[s] = buf_ld(rX, o);
       }
     }
   };
-  // the plain (no Adam, no A transform) one-chunk-per-stage configurations pipeline their
-  // K loop (register budget: the Adam and transform variants already sit near 128 VGPRs)
-  constexpr int PIPE = (SACMI_PIPE && G == 1 && !ADAM && AXK == 0) ? 1
-                     : (SACMI_PIPE_DW && G == 1 && ADAM && MG == 2) ? 2 : 0;
   SACMI_PHASE(batch.tl, 1);
-  if constexpr (CORE == 1)
-    gemm_core_stg<TM, TN, KSPLIT, MG, AXK>(d, m0, n0, ring, rsum, s_kw, rowsum, pre, batch.tl);
-  else
-    gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16, PIPE, LDAUX, MIDSPLIT>(d, m0, n0, red, rsum, rowsum, pre, mid);
+  gemm_core<TM, TN, KSPLIT, G, MG, AXK, BF16>(d, m0, n0, red, rsum, rowsum, pre);
   SACMI_PHASE(batch.tl, 2);
   SACMI_PHASE_LAST(batch.tl, 7);
   if (d.dotp && tid < TN) s_dotw[tid] = n0 + tid < d.N ? dotw_x : 0.f;
@@ -1926,15 +1159,8 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
   const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
   // a non-finite policy sample / PER draw of this update (ErrBits): the reference raised
   // before this step (no stores), or after the critic step but before Polyak
-  int err = ADAM ? s_err : 0;
-  AdamScalars k_ad = s_k;
-  if constexpr (ADAM && CORE == 1) {
-    double p1 = __longlong_as_double((long long)((uint64_t)skw[0] | ((uint64_t)skw[1] << 32)));
-    double p2 = __longlong_as_double((long long)((uint64_t)skw[2] | ((uint64_t)skw[3] << 32)));
-    if (af.step_offset) { p1 *= (double)af.beta1; p2 *= (double)af.beta2; }
-    k_ad = AdamScalars{(float)((double)af.lr / (1.0 - p1)), (float)sqrt(1.0 - p2)};
-    err = (int)skw[4];
-  }
+  const int err = ADAM ? s_err : 0;
+  const AdamScalars k_ad = s_k;
   const bool void_st = ADAM && (err & af.err_skip) != 0;
   const bool pol_st = pol && (err & af.err_nopolyak) == 0;
   if constexpr (ADAM) {
@@ -1963,10 +1189,6 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
         if (wt) st_wt8(h, 0u, lo, hi);
         else *reinterpret_cast<uint2*>(h) = make_uint2(lo, hi);
       };
-#ifdef SACMI_EXP_NOADAMIO
-      if (p[0] + m[1] + v[2] + t[3] == 12345.f) st4(rC, p);   // (keeps the math alive)
-      continue;
-#endif
       if (af.G) st4(rG, g);
       st4(rC, p); st4(rM, m); st4(rV, v);
       if (af.Ph) st_bf4(af.Ph + abase + (o >> 2), p);
@@ -2008,12 +1230,7 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
         if (d.bias) v += x0[s];
         if (d.epi == EPI_RELU) v = v <= 0.f ? 0.f : v;   // F.relu: NaN stays NaN
         else if (d.epi == EPI_MASK) v = x0[s] > 0.f ? v : 0.f;
-#ifdef SACMI_EXP_NOSTORE
-        if (v == 12345.f)   // timing experiment only: no output stores
-#endif
         buf_st_pol(rC, o, v, wt);
-        if (d.u_out && s < EPT)   // u rows (u_out)
-          buf_st_pol(rU, (uint32_t)((m0 + row) * d.u_ld + n) * 4u, v > 0.f ? s_dotw[col] : 0.f, wt);
       }
     }
     if constexpr (!ADAM) {
@@ -2029,9 +1246,6 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
     }
     if constexpr (PA) {   // every tile element, 0 outside the output
       if (has_pa && s < EPT) s_pa[row * (TN + 1) + col] = ok ? v : 0.f;
-    }
-    if constexpr (HF) {   // (the stored h: after the ReLU)
-      if (hf_mine && s < EPT) s_hlp[row * (TN + 1) + col] = ok ? v : 0.f;
     }
   }
   if (threadIdx.x < 64) SACMI_STAMP(33);
@@ -2061,103 +1275,16 @@ __device__ __forceinline__ void kg_body(const GemmBatch& batch, const int bid_in
       }
     }
   }
-  if (batch.has_adam && adam_wg == -1 && bid == 0) {
-    adam_block0(af, err, omb1, omb2);
-  }
   store_err_flags(batch);
-  if constexpr (HF) {
-    // folded heads, split over the level's column tiles: each policy tile forms its TN
-    // columns' share of every head output of its 32 rows (fixed column order) into
-    // heads_part[row block][column tile] (write-through), acknowledged in every wave, then
-    // the row block's arrival count; the last column tile to arrive sums the shares in column-
-    // tile order (sc1 loads: stored from other XCDs), adds the bias and runs the sample
-    // epilogue (heads_elem: k_heads_sample's per-element algebra) and the log-prob sums.
-    // (the policy rows may come as heads_ndesc descs of d.M rows each, stacked in order: the
-    // target and actor halves of k_chain_a's row-affine L2)
-    if (hf_mine) {
-      const HeadSampleArgs& ha = batch.heads;
-      const int A = ha.A, n2 = 2 * A;
-      const int hm0 = m0 + (p - batch.heads_desc) * d.M;   // the row in the heads' stacked rows
-      const int rb = hm0 / kHeadsFoldTM, tcol = n0 / TN, ntc = d.tiles_n;
-      static_assert(TMW == kHeadsFoldTM, "one 32-row block per folding tile");
-      __syncthreads();                                     // s_hlp complete; red free
-      float* s_w = red;                                    // [n2][TN + 1]
-#pragma unroll
-      for (int q = 0; q < HWPT; ++q) {
-        const int e = tid + q * NTH;
-        if (e < n2 * TN) s_w[(e / TN) * (TN + 1) + e % TN] = hw_x[q];
-      }
-      __syncthreads();
-      float* part = batch.heads_part + ((size_t)rb * ntc + tcol) * (kHeadsFoldTM * n2);
-      for (int e = tid; e < kHeadsFoldTM * n2; e += NTH) {
-        const int row = e / n2, j = e - row * n2;
-        const float* hr = s_hlp + row * (TN + 1);
-        const float* wr = s_w + j * (TN + 1);
-        float acc = 0.f;
-#pragma unroll 16
-        for (int cc = 0; cc < TN; ++cc) acc = fmaf(hr[cc], wr[cc], acc);
-        st_wt(part + e, acc);
-      }
-      // the finishing tile's bias and noise, loaded by every folding tile before its arrival
-      const int e = tid, row = e / A, j = e - (e / A) * A, m = hm0 + row;
-      const bool live = e < kHeadsFoldTM * A && m < ha.rows;
-      float bm = 0.f, bl = 0.f, eps_in = 0.f;
-      {
-        const int jj = live ? j : 0, mm = live ? m : 0;
-        const rsrc_t rB = make_rsrc(ha.Wh, (uint32_t)(((size_t)(n2 - 1) * ha.ldw + ha.K + 1) * 4));
-        bm = buf_ld(rB, (uint32_t)((size_t)jj * ha.ldw + ha.K) * 4u);
-        bl = buf_ld(rB, (uint32_t)((size_t)(A + jj) * ha.ldw + ha.K) * 4u);
-        const bool want = !ha.deterministic && !ha.gen_eps;
-        eps_in = buf_ld(make_rsrc(want ? ha.eps : ha.Wh, want ? 0x7fffffffu : 0u), (uint32_t)((size_t)mm * A + jj) * 4u);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        int* tk = batch.heads_ticket + rb;
-        const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_hlast = old == ntc - 1;
-        if (old == ntc - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      if (s_hlast) {
-        float (*lp)[33] = reinterpret_cast<float (*)[33]>(red);
-        float* s_lp = red + kHeadsFoldTM * 33;
-        const uint64_t ctr = ha.ctr_override ? ha.ctr_override : ha.sc->noise_counter;
-        if (e < kHeadsFoldTM * A) {
-          float lpe = 0.f;
-          if (live) {
-            // (a buffer descriptor on the row block's base — uniform: a per-lane base would
-            // make the compiler loop over the distinct values — and the row in the offset)
-            const float* p0 = batch.heads_part + (size_t)rb * ntc * (kHeadsFoldTM * n2);
-            const rsrc_t rP = make_rsrc(p0, (uint32_t)((size_t)ntc * kHeadsFoldTM * n2 * 4));
-            float sm[16], sl[16];   // (ntc <= 16: H <= 1024)
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-              const uint32_t o = (uint32_t)((size_t)t * kHeadsFoldTM * n2 + row * n2) * 4u;
-              sm[t] = buf_ld_aux<kLdSc1>(rP, t < ntc ? o + (uint32_t)j * 4u : 0xfffffff0u);
-              sl[t] = buf_ld_aux<kLdSc1>(rP, t < ntc ? o + (uint32_t)(A + j) * 4u : 0xfffffff0u);
-            }
-            float mean = sm[0], ls_raw = sl[0];
-#pragma unroll
-            for (int t = 1; t < 16; ++t)
-              if (t < ntc) { mean += sm[t]; ls_raw += sl[t]; }
-            lpe = heads_elem<false, kLdSc1>(ha, m, j, mean + bm, ls_raw + bl, eps_in, ctr);
-          }
-          lp[row][j] = lpe;
-        }
-        heads_logp<kHeadsFoldTM, kLdSc1>(ha, hm0, rb, lp, s_lp);
-      }
-    }
-  }
   SACMI_PHASE(batch.tl, 5);
 }
 
-template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false, int CORE = 0,
-          bool HFOLD = false>
-__global__ __launch_bounds__((gemm_threads<KSPLIT, MG, CORE>()), (gemm_min_waves<KSPLIT * MG>())) void k_gemm(GemmBatch batch) {
+template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK = 0, bool BF16 = false>
+__global__ __launch_bounds__((gemm_threads<KSPLIT, MG>()), 4) void k_gemm(GemmBatch batch) {
+  // (4 waves per SIMD: 16 waves per CU, one 1024- or two 512-thread workgroups)
   const TlMark tl_mark(batch.tl, TL_GEMM);
-  __shared__ KgSmem<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, HFOLD> sm;
-  kg_body<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16, CORE, 0, false, HFOLD>(batch, blockIdx.x, sm);
+  __shared__ KgSmem<TM, TN, KSPLIT, MG, AXK> sm;
+  kg_body<TM, TN, KSPLIT, G, MG, ADAM, AXK, BF16>(batch, blockIdx.x, sm);
 }
 
 // Tile order and XCD placement.  Workgroups are dealt round-robin over the 8 XCDs
@@ -2178,13 +1305,6 @@ static int assign_tiles(GemmBatch& b) {
     const double A = (double)d.M * d.K, B = (double)d.N * d.K;
     d.xcd_gr = 0;
     double best = 8 * A + B;      // row-major order
-    // SACMI_XCD_GR (experiment): force the XCD grid (1: every XCD owns column tiles only)
-    static const int force_gr = std::getenv("SACMI_XCD_GR") ? std::atoi(std::getenv("SACMI_XCD_GR")) : 0;
-    if (force_gr > 0 && d.tiles_m % force_gr == 0 && d.tiles_n % (8 / force_gr) == 0) {
-      d.xcd_gr = force_gr;
-      tot += (d.tiles_m * d.tiles_n + 7) & ~7;
-      continue;
-    }
     for (int gr : {1, 2, 4, 8}) {
       const int gc = 8 / gr;
       if (d.tiles_m % gr || d.tiles_n % gc) continue;
@@ -2209,18 +1329,14 @@ static int assign_tiles(GemmBatch& b) {
 }
 
 // ---------------------------------------------------------------------------
-// Large-M forward levels (batch-4096 class) in bf16 mode: LDS-staged 128x128 tiles.
+// Large-M forward levels (batch-4096 class) in bf16 mode: LDS-staged 128-row tiles.
 // C = relu(A . W^T [+ b]) with both operands K-contiguous (activations [rows][K],
-// nn.Linear weights [out][K]); [+ per-32-column fc3 dot partials].  Four waves (2x2),
-// each a 64x64 sub-tile over the FULL K (no K split, no partial-tile reduction): the
-// workgroup stages a 32-deep K slab of its 128 A rows and 128 W rows through LDS (double
-// buffered: the next slab's global loads are in flight while this slab's MFMAs run) and
-// every wave reads its fragments from LDS — each operand byte crosses L2->CU once per
-// workgroup instead of once per wave.  Two workgroups per CU.
-constexpr int kFBM = 128, kFBK = 32, kFPad = 4, kFBN128 = 128;
-#ifndef SACMI_FWD_LDS16
-#define SACMI_FWD_LDS16 1       // bf16 mode: k_fwd16 (bf16 LDS slabs, 16x16x32 MFMA)
-#endif
+// nn.Linear weights [out][K]); [+ per-32-column fc3 dot partials].  The waves cover the
+// tile over the FULL K (no K split, no partial-tile reduction): the workgroup stages K
+// slabs of its A rows and W rows through LDS (the next slab's global loads in flight while
+// this slab's MFMAs run) and every wave reads its fragments from LDS — each operand byte
+// crosses L2->CU once per workgroup instead of once per wave.
+constexpr int kFBM = 128, kFBN128 = 128;
 
 __device__ __forceinline__ float swap_adj(float x) {   // lane ^ 1's x (DPP quad_perm 1,0,3,2)
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
@@ -2229,7 +1345,7 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)bf16_bits(lo) | ((uint32_t)bf16_bits(hi) << 16);
 }
 
-// k_fwd / k_fwd16 epilogue: bias, ReLU, store, per-32-column fc3 dot partials.  A wave
+// k_fwd16 / k_fwd16p epilogue: bias, ReLU, store, per-32-column fc3 dot partials.  A wave
 // owns a 64 x (16 NT) sub-tile at (r0, c0); lane holds D[row = (lane >> 4) * 4 + r]
 // [col = lane & 15] of each 16x16 tile.  The operands are loaded before the K loop.
 template <int NT, int MI = 4>
@@ -2315,111 +1431,14 @@ struct FwdEpi {
 };
 
 
-template <bool BF16, int kFBN = 128>
-__global__ __launch_bounds__(256, 2) void k_fwd(GemmBatch batch) {
-  const TlMark tl_mark(batch.tl, TL_FWD);
-  constexpr int NT = kFBN / 32;          // 16-column MFMA tiles per wave (2 x 2 waves)
-  __shared__ __attribute__((aligned(16))) float sA[2][kFBM][kFBK + kFPad];
-  __shared__ __attribute__((aligned(16))) float sB[2][kFBN][kFBK + kFPad];
-  const int bid = blockIdx.x;
-  int p = 0;
-  for (int q = 1; q < batch.count; ++q)
-    if (bid >= batch.d[q].tile_begin) p = q;
-  const GemmDesc& d = batch.d[p];
-  const int t = bid - d.tile_begin;
-  if (t >= d.tiles_m * d.tiles_n) return;
-  int tr, tc;
-  place_tile(d, t, tr, tc);
-  const int m0 = tr * kFBM, n0 = tc * kFBN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (kFBN / 2);
-  const int M = d.M, N = d.N, K = d.K;
-  constexpr int NB = kFBN / 32;          // B rows staged per thread (32 rows per pass)
-  // staging: thread t moves rows (t >> 3) + 32 i (i < 4) at k = 4 (t & 7) of both slabs
-  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
-  uint32_t offA[4], offB[NB];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ra = min(m0 + (tid >> 3) + 32 * i, M - 1);
-    offA[i] = (uint32_t)ra * (uint32_t)d.lda * 4u;
-  }
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int rb = min(n0 + (tid >> 3) + 32 * i, N - 1);
-    offB[i] = (uint32_t)rb * (uint32_t)d.ldb * 4u;
-  }
-  const int kq = 4 * (tid & 7);
-  float4 ga[4], gb[NB];
-  auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
-    x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
-    return x;
-  };
-  auto gload = [&](int k0) {
-    const int k = k0 + kq;
-    const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) gb[i] = zk(buf_ld4(rB, offB[i] + ko), k);
-  };
-  auto swrite = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&sA[buf][(tid >> 3) + 32 * i][kq]) = ga[i];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) *reinterpret_cast<float4*>(&sB[buf][(tid >> 3) + 32 * i][kq]) = gb[i];
-  };
-  f4 acc[4][NT];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  // epilogue operands (bias, dot weights) issued up front: they land under the K loop
-  FwdEpi<NT> ep;
-  ep.load(d, n0 + wn, lane);
-  gload(0);
-  swrite(0);
-  __syncthreads();
-  const int nslab = (K + kFBK - 1) / kFBK;
-  for (int sl = 0; sl < nslab; ++sl) {
-    const int cur = sl & 1;
-    gload((sl + 1 < nslab ? sl + 1 : sl) * kFBK);   // unconditional: the last re-reads its slab
-#pragma unroll
-    for (int kk = 0; kk < kFBK / 16; ++kk) {
-      float a[4][4], b[NT][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float4 x = *reinterpret_cast<const float4*>(&sA[cur][wm + i * 16 + (lane & 15)][kk * 16 + 4 * (lane >> 4)]);
-        a[i][0] = x.x; a[i][1] = x.y; a[i][2] = x.z; a[i][3] = x.w;
-      }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const float4 y = *reinterpret_cast<const float4*>(&sB[cur][wn + j * 16 + (lane & 15)][kk * 16 + 4 * (lane >> 4)]);
-        b[j][0] = y.x; b[j][1] = y.y; b[j][2] = y.z; b[j][3] = y.w;
-      }
-      mfma_chunk<4, NT, BF16>(acc, a, b);
-    }
-    swrite(cur ^ 1);
-    __syncthreads();
-  }
-  ep.store(d, acc, m0 + wm, n0 + wn, lane);
-}
-
 // bf16 mode, bf16 in LDS: the staging rounds every fp32 operand ONCE per workgroup
 // (v_cvt_pk_bf16_f32) and stores [row][k] bf16 slabs 64 deep; a lane's 8 consecutive k
 // of one row are one ds_read_b128 and exactly its v_mfma_f32_16x16x32_bf16 operand
-// (lane l: A[l&15][8(l>>4) + j], B[8(l>>4) + j][l&15]).  Against k_fwd<true>: half the
-// LDS bytes per MFMA, one conversion per element per workgroup instead of per wave, half
-// the MFMA issues, and half the barriers / load round trips per K.  Same tiles, XCD
-// order and epilogue as k_fwd.
+// (lane l: A[l&15][8(l>>4) + j], B[8(l>>4) + j][l&15]): one conversion per element per
+// workgroup instead of per wave, one 16x16x32 MFMA per 32 k.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u2v __attribute__((ext_vector_type(2)));
-#ifndef SACMI_FWD16_BK
-#define SACMI_FWD16_BK 64       // k_fwd16 slab depth (64 or 32)
-#endif
-#ifndef SACMI_FWD16_OCC
-#define SACMI_FWD16_OCC 2       // k_fwd16 workgroups per CU the launch bounds ask for
-#endif
-constexpr int kHBK = SACMI_FWD16_BK, kHPad = 8;
+constexpr int kHBK = 64, kHPad = 8;   // k_fwd16 slab depth, row pad
 
 __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
   const bf16x4 x = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
@@ -2431,16 +1450,11 @@ __device__ __forceinline__ u2v pack_bf16x4(float4 v) {
 // 8 waves (4 per SIMD at two workgroups per CU) hide each other's LDS / barrier latency
 // behind MFMAs: config 5 L1 / L2 28.8 / 25.4 -> 24.8 / 21.1 us, the 64-column levels
 // L3 / L4 / L7 / L8 18.9 / 16.9 -> 16.4 / 14.7 (4 waves: one wave per SIMD per workgroup)
-#ifndef SACMI_FWD16_WAVES
-#define SACMI_FWD16_WAVES 8     // waves per k_fwd16 workgroup at 128-column tiles (4 or 8)
-#endif
-#ifndef SACMI_FWD16_WAVES64
-#define SACMI_FWD16_WAVES64 8   // ... at 64-column tiles (4: 2 x 2 waves of 64x32; 8: 4 x 2 of 32x32)
-#endif
+// (8 waves at either tile width: 128 columns as 2 x 4 waves of 64x32, 64 as 4 x 2 of 32x32)
 template <int kFBN>
-__host__ __device__ constexpr int fwd16_waves() { return kFBN == 128 ? SACMI_FWD16_WAVES : SACMI_FWD16_WAVES64; }
+__host__ __device__ constexpr int fwd16_waves() { return 8; }
 template <int kFBN, bool BH = false, bool AH = false>
-__global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), SACMI_FWD16_OCC) void k_fwd16(GemmBatch batch) {
+__global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), 2) void k_fwd16(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_FWD16);
   // NWV waves as WR x WC, each an MW x NW sub-tile: MI x NT 16x16 MFMA tiles
   constexpr int NWV = fwd16_waves<kFBN>(), WC = kFBN == 128 ? NWV / 2 : 2, WR = NWV / WC;
@@ -2573,12 +1587,6 @@ __global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), SACMI_FWD16_OCC) void k_f
 // 16-byte slots of a 256-byte bank row.  Chunks past K read a clamped in-row address and
 // are zeroed in the fragment registers (last slab only).  Epilogue: FwdEpi (bias, ReLU,
 // fc3 dot partials, bf16 column-pair stores), as k_fwd16.
-#ifndef SACMI_FWD16P
-#define SACMI_FWD16P 1
-#endif
-#ifndef SACMI_FWD16P_WAVES
-#define SACMI_FWD16P_WAVES 16   // k_fwd16p waves per workgroup (8 or 16)
-#endif
 constexpr int kPLds = 144 * 1024;
 template <int BM>
 __host__ __device__ constexpr int fwd16p_stages() { return kPLds / ((BM + 128) * 128); }
@@ -2600,12 +1608,13 @@ __device__ __forceinline__ bf16x8 zero_past(bf16x8 x, int nvalid) {   // keep el
   return __builtin_bit_cast(bf16x8, u);
 }
 
-template <int BM, int NWV = 16>
-__global__ __launch_bounds__(64 * NWV, 1) void k_fwd16p(GemmBatch batch) {
+template <int BM>
+__global__ __launch_bounds__(1024, 1) void k_fwd16p(GemmBatch batch) {
+  constexpr int NWV = 16;
   const TlMark tl_mark(batch.tl, TL_FWD16P);
   constexpr int BN = 128, BK = 64, NST = fwd16p_stages<BM>();
-  // NWV waves as WR x WC: 16 -> 4 x 4 of (BM/4) x 32; 8 -> BM 256: 4 x 2 of 64 x 64, BM 128: 2 x 4 of 64 x 32
-  constexpr int WR = NWV == 16 ? 4 : (BM == 256 ? 4 : 2), WC = NWV / WR;
+  // NWV waves as WR x WC = 4 x 4 of (BM/4) x 32
+  constexpr int WR = 4, WC = NWV / WR;
   constexpr int MW = BM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
   constexpr int ROWB = BK * 2;                       // bytes per LDS row (64 bf16)
   constexpr int STAGE = (BM + BN) * ROWB;
@@ -2730,7 +1739,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void k_fwd16p(GemmBatch batch) {
 // must start 16-byte aligned (the DMA moves 16-byte chunks) and hold round_up(K, 8)
 // elements inside its stride (a chunk straddling K stays in its row).
 static int fwd16p_plan(GemmBatch& b) {
-  if (!SACMI_FWD16P || !b.bf16 || b.ride.kind) return 0;
+  if (!b.bf16 || b.ride.kind) return 0;
   static const bool off = std::getenv("SACMI_NO_FWD16P") != nullptr;
   if (off) return 0;
   for (int i = 0; i < b.count; ++i) {
@@ -2741,8 +1750,7 @@ static int fwd16p_plan(GemmBatch& b) {
     if (k8 > d.lda || k8 > d.ldb || d.K < 1) return 0;
     if ((d.N & 7) || (d.ldc & 7) || ((uintptr_t)d.C & 15)) return 0;   // 16-byte epilogue stores
   }
-  static const bool wt = std::getenv("SACMI_FWD16P_WT") == nullptr || std::atoi(std::getenv("SACMI_FWD16P_WT")) != 0;
-  b.st_wt = wt ? 1 : 0;
+  b.st_wt = 1;   // write-through epilogue stores
   if (assign_tiles<256, 128>(b) >= 256) return 256;
   if (assign_tiles<128, 128>(b) >= 256) return 128;
   return 0;
@@ -2750,34 +1758,17 @@ static int fwd16p_plan(GemmBatch& b) {
 
 // ---------------------------------------------------------------------------
 // Deep-K weight-gradient levels in bf16 mode (batch 4096 class): dW = dY^T X with both
-// operands row-contiguous.  k_dw_part: 128x128 output tiles, K split NS ways across
-// workgroups; each workgroup stages 32-row slabs of dY (128 columns) and X (128 columns)
-// through LDS (double buffered) and writes its partial tile (+ the bias-gradient row-sum
-// partial) to a workspace.  k_dw_fin: one thread per output element sums the NS partials
+// operands row-contiguous.  k_dw_part16: 128x128 output tiles, K split NS ways across
+// workgroups; each workgroup stages slabs of dY (128 columns) and X (128 columns)
+// through LDS and writes its partial tile (+ the bias-gradient row-sum partial) to a
+// workspace.  k_dw_fin: one thread per output element sums the NS partials
 // in fixed order and runs the epilogue (store, or Adam [+ Polyak] with the gradient export
 // and block 0's loss / alpha extras) — both forms of a level take this path, so the
 // fused and the data-parallel updates keep identical bits.
-constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
-#ifndef SACMI_DW_TARGET
-#define SACMI_DW_TARGET 512     // k_dw_part workgroup slots (256 CUs x 2)
-#endif
+constexpr int kDBM = 128, kDBN = 128;
+constexpr int kDwTarget = 512;   // k_dw_part16 workgroup slots (256 CUs x 2)
 constexpr int kDwMaxSplit = 16;
-#ifndef SACMI_DWFIN_EPT
-#define SACMI_DWFIN_EPT 1       // k_dw_fin elements per thread (1, 2, 4 measured alike)
-#endif
-#ifndef SACMI_DWFIN_NSL
-#define SACMI_DWFIN_NSL 1       // k_dw_fin instantiated per split count (0: one 16-load form)
-#endif
-constexpr int kDwFinEpt = SACMI_DWFIN_EPT;
-#ifndef SACMI_DW_SPLIT_FP32
-#define SACMI_DW_SPLIT_FP32 0   // the split-K dW path for fp32 levels too (k_dw_part<false>)
-#endif
-#ifndef SACMI_AXK_LDS16
-#define SACMI_AXK_LDS16 1       // bf16 mode: k_axk16 for the batch-4096-class dh levels
-#endif
-#ifndef SACMI_DW_LDS16
-#define SACMI_DW_LDS16 1        // bf16 mode: k_dw_part16 (bf16 k-major LDS, transposed reads)
-#endif
+constexpr int kDwFinEpt = 1;     // k_dw_fin 4-column groups per thread (1, 2, 4 measured alike)
 
 // workspace layout: partial s of desc p at ws + s * ws_stride + desc_off[p], row-major
 // [M][ncols] with ncols = N (+1 for the row-sum column) rounded up to a multiple of 4: every
@@ -2788,139 +1779,16 @@ __host__ __device__ __forceinline__ int dw_ncols(const GemmDesc& d) { return (dw
 
 // XCD placement of the split-K work (workgroup b runs on XCD b % 8): the split-major work
 // list w = split * tiles + tile is dealt to the XCDs in contiguous eighths, so each XCD's
-// L2 streams the rows of one or two K ranges instead of every range (SACMI_DW_XCD 0: the
-// plain order).  The tile grid is padded to a multiple of 8 workgroups.
-#ifndef SACMI_DW_XCD
-#define SACMI_DW_XCD 1
-#endif
-__host__ __device__ __forceinline__ int dw_grid_tiles(int tiles, int ns) {
-  return SACMI_DW_XCD ? (tiles * ns + 7) / 8 * 8 : tiles * ns;
-}
+// L2 streams the rows of one or two K ranges instead of every range.  The tile grid is
+// padded to a multiple of 8 workgroups.
+__host__ __device__ __forceinline__ int dw_grid_tiles(int tiles, int ns) { return (tiles * ns + 7) / 8 * 8; }
 __device__ __forceinline__ int dw_work_index(int b, int tiles, int ns) {
-  if (!SACMI_DW_XCD) return b;
   const int W = tiles * ns, per = (W + 7) / 8;
   const int w = (b % 8) * per + b / 8;
   return w < W ? w : -1;
 }
 
-template <bool BF16>
-__global__ __launch_bounds__(256, 2) void k_dw_part(GemmBatch batch, int ns, int64_t ws_stride) {
-  const TlMark tl_mark(batch.tl, TL_DW_PART);
-  __shared__ __attribute__((aligned(16))) float sA[2][kDBK][kDBM + kDPad];
-  __shared__ __attribute__((aligned(16))) float sB[2][kDBK][kDBN + kDPad];
-  const int tiles_tot = batch.total_tiles;
-  const int nwg = dw_grid_tiles(tiles_tot, ns);
-  if ((int)blockIdx.x >= nwg) {   // ride-along: the next update's gather
-    const int rb = blockIdx.x - nwg, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int b = rb * 4 + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * 4)
-      gather_row(batch.ride.ga, b, lane, 64);
-    return;
-  }
-  const int wk = dw_work_index(blockIdx.x, tiles_tot, ns);
-  if (wk < 0) return;
-  const int split = wk / tiles_tot, bid = wk % tiles_tot;
-  int p = 0;
-  for (int q = 1; q < batch.count; ++q)
-    if (bid >= batch.d[q].tile_begin) p = q;
-  const GemmDesc& d = batch.d[p];
-  const int t = bid - d.tile_begin;
-  if (t >= d.tiles_m * d.tiles_n) return;
-  const int m0 = (t / d.tiles_n) * kDBM, n0 = (t % d.tiles_n) * kDBN;
-  const int M = d.M, N = d.N, K = d.K;
-  const int kc = ((K + ns - 1) / ns + kDBK - 1) / kDBK * kDBK;
-  const int kb = split * kc, ke = min(K, kb + kc);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  // staging: thread t moves k rows (t >> 5) + 8 i (i < 4), columns 4 (t & 31) .. +3
-  const int c4 = 4 * (tid & 31);
-  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
-  const rsrc_t rS = make_rsrc(d.a_ksc ? d.a_ksc : d.A, d.a_ksc ? (uint32_t)K * 4u : 0u);
-  const bool has_ksc = d.a_ksc != nullptr;
-  // 4-wide operand reads start at a 4-aligned column <= the last one, so they stay inside
-  // a row padded to a multiple of 4; an operand narrower than 4 columns (the fc3 gradient
-  // dq, lda = 1) reads up to 3 floats past its last row: dw_split_plan's caller keeps
-  // that slack allocated (sacmi.hip: dq).  (A per-load scalar fallback under a branch
-  // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
-  const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
-  float4 ga[4], gb[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = k0 + (tid >> 5) + 8 * i;
-      const bool kin = k < ke;
-      const uint32_t kk = (uint32_t)(kin ? k : 0);   // row 0 always exists (a split may start past K)
-      float4 x = buf_ld4(rA, (kk * (uint32_t)d.lda + (uint32_t)ma) * 4u);
-      float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
-      const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
-      // columns past M / N (and rows past this split's K range) contribute zero
-      x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
-      x.z = kin && m0 + c4 + 2 < M ? x.z * f : 0.f; x.w = kin && m0 + c4 + 3 < M ? x.w * f : 0.f;
-      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
-      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
-      ga[i] = x; gb[i] = y;
-    }
-  };
-  auto swrite = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<float4*>(&sA[buf][(tid >> 5) + 8 * i][c4]) = ga[i];
-      *reinterpret_cast<float4*>(&sB[buf][(tid >> 5) + 8 * i][c4]) = gb[i];
-    }
-  };
-  f4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  float rs = 0.f;                       // row sum of A row m0 + tid (tid < 128), this split
-  const bool want_rs = d.rs_col >= 0 && n0 == 0;
-  const int nslab = (ke - kb + kDBK - 1) / kDBK;
-  gload(kb);
-  swrite(0);
-  __syncthreads();
-  for (int sl = 0; sl < nslab; ++sl) {
-    const int cur = sl & 1;
-    gload(kb + (sl + 1 < nslab ? sl + 1 : sl) * kDBK);
-#pragma unroll
-    for (int kk = 0; kk < kDBK / 16; ++kk) {
-      float a[4][4], b[4][4];
-      const int kr = kk * 16 + 4 * (lane >> 4);
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i][s2] = sA[cur][kr + s2][wm + i * 16 + (lane & 15)];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j][s2] = sB[cur][kr + s2][wn + j * 16 + (lane & 15)];
-      }
-      mfma_chunk<4, 4, BF16>(acc, a, b);
-    }
-    if (want_rs && tid < kDBM) {
-#pragma clang fp contract(off)
-      for (int r = 0; r < kDBK; ++r) rs += sA[cur][r][tid];
-    }
-    swrite(cur ^ 1);
-    __syncthreads();
-  }
-  // partial tile (+ row-sum partial) to the workspace
-  int64_t off = 0;
-  for (int q = 0; q < p; ++q) off += (int64_t)batch.d[q].M * dw_ncols(batch.d[q]);
-  float* w = batch.ws + (int64_t)split * ws_stride + off;
-  const int nc = dw_ncols(d);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn + j * 16 + (lane & 15);
-        if (row < M && col < N) st_big(w + (int64_t)row * nc + col, acc[i][j][r]);
-      }
-    }
-  if (want_rs && tid < kDBM && m0 + tid < M) st_big(w + (int64_t)(m0 + tid) * nc + N, rs);
-}
-
-// bf16 mode, bf16 in LDS: k_dw_part with the operands rounded once at staging and kept
+// bf16 mode, bf16 in LDS: the operands are rounded once at staging and kept
 // k-major ([k][128 columns] bf16, 64-deep slabs, rows padded to 272 B).  The 16x16x32
 // operand (lane l: A[l&15][k = 8(l>>4) + j]) is read with two ds_read_b64_tr_b16 per
 // fragment — the hardware transpose delivers 4 k of one column per lane, lane 4q+p of a
@@ -2932,10 +1800,8 @@ typedef short s4t __attribute__((ext_vector_type(4)));
 typedef short s8t __attribute__((ext_vector_type(8)));
 constexpr int kD16K = 64, kD16Pad = 8;
 constexpr int kDw16OpBytes = 2 * kD16K * (kDBM + kD16Pad) * 2;      // one operand, 2 slabs
-#ifndef SACMI_DW16_WAVES
-#define SACMI_DW16_WAVES 8      // waves per k_dw_part16 workgroup (4: 2 x 2 of 64x64; 8: 2 x 4 of 64x32)
-#endif
-constexpr int kDw16Waves = SACMI_DW16_WAVES, kDw16Krp = 64 * kDw16Waves / 32;   // k rows per staging pass
+// waves per k_dw_part16 workgroup: 2 x 4 of 64x32 sub-tiles
+constexpr int kDw16Waves = 8, kDw16Krp = 64 * kDw16Waves / 32;   // k rows per staging pass
 static_assert(kDw16LdsBytes >= 2 * kDw16OpBytes + kDw16Krp * kDBM * 4, "k_dw_part16 LDS layout");
 
 __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
@@ -2944,9 +1810,7 @@ __device__ __forceinline__ s4t lds_tr16(const __bf16* p) {
 }
 
 // X16 (act16): the B operand (X: activations / minibatch inputs) is bf16
-// AXT: the level carries a dW A transform (axk 2, opt-in): its own instantiation, so the
-// plain form's staging pass issues no extra load
-template <bool X16 = false, bool AXT = false>
+template <bool X16 = false>
 __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batch, int ns, int64_t ws_stride) {
   const TlMark tl_mark(batch.tl, TL_DW_PART16);
   constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
@@ -2997,12 +1861,6 @@ __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batc
   // measured L6 74 -> 93 us: the guarded loads drain the load queue.)
   const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
   const bool want_rs = d.rs_col >= 0 && n0 == 0;
-  // axk 2 (act16): A is the bf16 activation h [k][m] and the operand is u = [h > 0] w[m]
-  // (w: ax_w, M % 4 == 0) — the values L5 would have stored as u rows.  Both loads are
-  // issued on every pass, the unused one at an out-of-range offset: no branch around them
-  const bool axt = AXT && d.axk == 2;
-  const rsrc_t rAh = make_rsrc(axt ? d.A : d.C, axt ? 0x7fffffffu : 0u);
-  const float4 w3v = axt ? buf_ld4(make_rsrc(d.ax_w, (uint32_t)M * 4u), (uint32_t)ma * 4u) : float4{0.f, 0.f, 0.f, 0.f};
   float4 ga[NI], gb[X16 ? 1 : NI];
   uint2 gbh[X16 ? NI : 1];
   float rs4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -3013,13 +1871,7 @@ __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batc
       const bool kin = k < ke;
       const uint32_t kk = (uint32_t)(kin ? k : 0);   // row 0 always exists (a split may start past K)
       const uint32_t ea = kk * (uint32_t)d.lda + (uint32_t)ma;
-      float4 x = buf_ld4(rA, axt ? 0xfffffff0u : ea * 4u);
-      if constexpr (AXT) {
-        const uint2 hx = buf_ld2(rAh, axt ? ea * 2u : 0xfffffff0u);
-        if (axt)
-          x = make_float4(bf16_lo(hx.x) > 0.f ? w3v.x : 0.f, bf16_hi(hx.x) > 0.f ? w3v.y : 0.f,
-                          bf16_lo(hx.y) > 0.f ? w3v.z : 0.f, bf16_hi(hx.y) > 0.f ? w3v.w : 0.f);
-      }
+      float4 x = buf_ld4(rA, ea * 4u);
       const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
       // columns past M / N (and rows past this split's K range) contribute zero
       x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
@@ -3138,10 +1990,7 @@ constexpr int kXBM = 64, kXBN = 128, kXBK = 64;
 
 // ACT16 (act16 updates): the ReLU-mask source (aux) is bf16, and so is A where it is the
 // activation whose sign the transform reads (AX); the plain levels' A is a gradient, fp32
-#ifndef SACMI_AXK16_WAVES
-#define SACMI_AXK16_WAVES 8     // waves per k_axk16 workgroup (4: 2 x 2 of 32x64; 8: 2 x 4 of 32x32)
-#endif
-constexpr int kAxWaves = SACMI_AXK16_WAVES;
+constexpr int kAxWaves = 8;   // waves per k_axk16 workgroup: 2 x 4 of 32x32 sub-tiles
 template <bool AX, bool BH = false, bool ACT16 = false>
 __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_AXK16);
@@ -3343,324 +2192,6 @@ static int axk16_ok(GemmBatch& b) {
   return assign_tiles<kXBM, kXBN>(b) >= 256 ? ax : -1;
 }
 
-// ---------------------------------------------------------------------------
-// k_axk16p: the act16 batch-4096-class dh levels — k_axk16's math, dh = coef * (A W) *
-// [h > 0] with A = u = [h2 > 0] w3 on the row-prologue levels (AX: L5 / L9) and A = the
-// dh gradient on the plain ones (L12, model2's L5b / L9b / L11) — on k_fwd16p's multi-slab
-// LDS ring: one 16-wave workgroup per CU, BM x 128 tiles, 64-deep slabs filled by LDS-DMA
-// (global_load_lds_dwordx4), NST - 1 slabs in flight across raw barriers with counted
-// vmcnt waits.  k_axk16 stages through registers with one slab in flight: its levels took
-// ~1.6x k_fwd16p's for the same GEMM shape (config 5, round 4: L5 26 us against L4 15 us).
-// Operands in the slot (the DMA image is lane-linear, so every swizzle is on the SOURCE
-// address: LDS position p of row R holds the row's 16-byte chunk p ^ sw(R)):
-//   A, AX: bf16 h2 rows [m][64 k] (128 B), sw = (R >> 1) & 7, read as k_fwd16p's A
-//          (ds_read_b128) and transformed in registers: u = h2 > 0 ? bf16(w3[k]) : 0
-//          (w3 staged in LDS once, fp32 and bf16: the bits k_axk16's staging rounds to);
-//   A, !AX: fp32 gradient rows [m][64 k] (256 B), sw = R & 15, two ds_read_b128 and a
-//          round to bf16 (k_axk16's pack) per fragment;
-//   B: W's [k][n] rows (MN-contiguous: the layer's [out][in]), 128 bf16 columns (256 B) a
-//          k row, sw = 2 (R & 3) ^ 8 ((R >> 3) & 1): conflict-free for ds_read_b64_tr_b16
-//          (lane 4q + p of a 16-lane group: k row q, columns 4p..4p+3).
-// The same MFMAs over the same k blocks as k_axk16 per output element: identical bits.
-// AX: the column-tile-0 workgroup's wn == 0 waves also store u (fp32, ax_out) for the
-// later weight gradient, as k_axk16 — those stores sit in the vmcnt count, so the counted
-// waits include them.  The host runs a level here only without rides, K % 64 == 0,
-// N % 8 == 0, 16-byte aligned operand rows (axk16p_plan).
-#ifndef SACMI_AXK16P
-#define SACMI_AXK16P 1
-#endif
-template <int BM, bool AX>
-__host__ __device__ constexpr int axk16p_stage() { return BM * 64 * (AX ? 2 : 4) + 64 * 256; }
-template <int BM, bool AX>
-__host__ __device__ constexpr int axk16p_stages() { return kPLds / axk16p_stage<BM, AX>(); }
-
-// LDS reads the compiler does not see (k_axk16p's slab reads; see there) and the tie that
-// orders their consumers after an explicit lgkmcnt wait
-typedef __attribute__((address_space(3))) const void lds_cvoid_t;
-__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_cvoid_t*)p; }
-typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u4v ds_rd128(uint32_t a) {
-  u4v v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
-  return v;
-}
-__device__ __forceinline__ u2v ds_rdtr(uint32_t a) {
-  u2v v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
-  return v;
-}
-template <class T>
-__device__ __forceinline__ void lds_tie(T& x) { asm volatile("" : "+v"(x)); }
-
-// s_waitcnt vmcnt(ahead * PPW + sts * NS) lgkmcnt(0) for ahead < 3, sts < 4 (immediates)
-template <int PPW, int NS>
-__device__ __forceinline__ void axk16p_wait(int ahead, int sts) {
-  switch (ahead * 4 + sts) {
-    case 0: vm_wait_lgkm0<0>(); break;
-    case 1: vm_wait_lgkm0<NS>(); break;
-    case 2: vm_wait_lgkm0<2 * NS>(); break;
-    case 3: vm_wait_lgkm0<3 * NS>(); break;
-    case 4: vm_wait_lgkm0<PPW>(); break;
-    case 5: vm_wait_lgkm0<PPW + NS>(); break;
-    case 6: vm_wait_lgkm0<PPW + 2 * NS>(); break;
-    case 7: vm_wait_lgkm0<PPW + 3 * NS>(); break;
-    case 8: vm_wait_lgkm0<2 * PPW>(); break;
-    case 9: vm_wait_lgkm0<2 * PPW + NS>(); break;
-    case 10: vm_wait_lgkm0<2 * PPW + 2 * NS>(); break;
-    default: vm_wait_lgkm0<2 * PPW + 3 * NS>(); break;
-  }
-}
-
-template <int BM, bool AX>
-__global__ __launch_bounds__(1024, 1) void k_axk16p(GemmBatch batch) {
-  const TlMark tl_mark(batch.tl, TL_AXK16P);
-  constexpr int BN = 128, BK = 64, NWV = 16, WR = 4, WC = 4;
-  constexpr int MW = BM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
-  constexpr int AROW = BK * (AX ? 2 : 4);            // bytes per A slab row
-  constexpr int ABYTES = BM * AROW, STAGE = axk16p_stage<BM, AX>();
-  constexpr int NST = axk16p_stages<BM, AX>();
-  constexpr int APC = ABYTES / 1024, BPC = BK * 256 / 1024;   // 1 KiB pieces per slab
-  constexpr int PPW = (APC + BPC) / NWV, APW = APC / NWV;
-  constexpr int ALPR = AROW / 16;                     // lanes (16-byte chunks) per A row
-  constexpr int NS = AX ? 2 * MI * (BK / 32) : 0;     // u stores per lane per slab
-  static_assert(STAGE == ABYTES + BPC * 1024 && NST >= 3 && NST - 2 <= 2 && APC % NWV == 0 &&
-                BPC % NWV == 0 && MI >= 1 && NT == 2, "k_axk16p geometry");
-  // one LDS object (the ring, then w3 and the row prologue's scratch): with a second
-  // __shared__ variable the compiler put a vmcnt(0) in front of the slab reads
-  constexpr int XW = AX ? 512 * 4 + 512 * 2 : 0, XQ = BM * 4 * 4 + 2 * BM * 4 + BM * 2 * 4;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[NST * STAGE + XW + XQ];
-  float* const s_w3 = reinterpret_cast<float*>(lds + NST * STAGE);
-  unsigned short* const s_w3b = reinterpret_cast<unsigned short*>(lds + NST * STAGE + 512 * 4);
-  auto s_q = reinterpret_cast<float (*)[4]>(lds + NST * STAGE + XW);
-  auto s_coef = reinterpret_cast<float (*)[BM]>(lds + NST * STAGE + XW + BM * 16);
-  auto s_l = reinterpret_cast<float (*)[2]>(lds + NST * STAGE + XW + BM * 24);
-  const int bid = blockIdx.x;
-  int p = 0;
-  for (int q = 1; q < batch.count; ++q)
-    if (bid >= batch.d[q].tile_begin) p = q;
-  const GemmDesc& d = batch.d[p];
-  const int t = bid - d.tile_begin;
-  if (t >= d.tiles_m * d.tiles_n) return;
-  int tr, tc;
-  place_tile(d, t, tr, tc);
-  const int m0 = tr * BM, n0 = tc * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave / WC) * MW, wn = (wave % WC) * NW;
-  const int M = d.M, N = d.N, K = d.K;
-  const bool store_a = AX && n0 == 0 && d.ax_out != nullptr;
-  const bool stw = store_a && wn == 0;                // this wave stores u
-  const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
-                               store_a ? (uint32_t)(((size_t)(M - 1) * d.ax_ld + K) * 4) : 0u);
-  // the row prologue's loads, the w3 vector and the ReLU-mask source go out first (oldest
-  // on the vm queue: retired by the first slab's wait)
-  float w3v = 0.f;
-  if constexpr (AX) w3v = buf_ld(make_rsrc(d.ax_w, (uint32_t)K * 4u), (uint32_t)(tid < K ? tid : 0) * 4u);
-  RowsRegs rows_x{};
-  if constexpr (AX) rows_load<BM, 1024>(batch.rows, d, m0, rows_x);
-  float hm[MI][NT][4];
-  {
-    const rsrc_t rX = make_rsrc(d.aux, (uint32_t)(((size_t)(M - 1) * d.ldaux + N) * 2));
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const int col = n0 + wn + j * 16 + (lane & 15);
-          const uint32_t off = row < M && col < N ? (uint32_t)(row * d.ldaux + col) * 2u : 0xfffffff0u;
-          hm[i][j][r] = bf16_lo(buf_ld_u16(rX, off));
-        }
-      }
-  }
-  // DMA sources: wave w moves pieces w + 16 i (A rows first, then B k rows)
-  const unsigned char* src[PPW];
-  int cko[PPW];    // A: the lane's chunk byte offset in its row; B: the lane's k row in the slab
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int pc = wave + NWV * i;
-    if (i < APW) {
-      const int R = pc * (1024 / AROW) + lane / ALPR, pos = lane % ALPR;
-      const int c = AX ? (pos ^ ((R >> 1) & 7)) : (pos ^ (R & 15));
-      const int ra = min(m0 + R, M - 1);
-      src[i] = reinterpret_cast<const unsigned char*>(d.A) + (size_t)ra * d.lda * (AX ? 2 : 4);
-      cko[i] = c * 16;
-    } else {
-      const int R = (pc - APC) * 4 + (lane >> 4), pos = lane & 15;
-      const int c = pos ^ (((R & 3) << 1) ^ (((R >> 3) & 1) << 3));
-      const int n = min(n0 + 8 * c, N - 8);          // (N % 8 == 0: a chunk is all in or out)
-      src[i] = reinterpret_cast<const unsigned char*>(d.Bh) + (size_t)n * 2;
-      cko[i] = R;
-    }
-  }
-  auto issue = [&](int sl) {                          // slab sl into ring slot sl % NST
-    unsigned char* dst = lds + (sl % NST) * STAGE;
-    const int k0 = sl * BK;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int pc = wave + NWV * i;
-      const unsigned char* g = i < APW ? src[i] + (size_t)k0 * (AX ? 2 : 4) + cko[i]
-                                       : src[i] + (size_t)min(k0 + cko[i], K - 1) * d.ldb * 2;
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(dst + pc * 1024), 16, 0, 0);
-    }
-  };
-  f4 acc[MI][NT];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  const int nslab = K / BK;
-#pragma unroll
-  for (int s2 = 0; s2 < NST - 1; ++s2)
-    if (s2 < nslab) issue(s2);
-  if constexpr (AX) {   // (read after the first slab's barrier; asm stores: see ds_rd128)
-    if (tid < K) {
-      const uint32_t wb16 = __builtin_bit_cast(unsigned short, (__bf16)w3v);
-      asm volatile("ds_write_b32 %0, %1" :: "v"(lds_addr(&s_w3[tid])), "v"(w3v) : "memory");
-      asm volatile("ds_write_b16 %0, %1" :: "v"(lds_addr(&s_w3b[tid])), "v"(wb16) : "memory");
-    }
-  }
-  const int r16 = lane & 15, tq = r16 >> 2, tp = lane & 3, tg = lane >> 4;
-  for (int sl = 0; sl < nslab; ++sl) {
-    // retire slab sl only: younger are the slabs already issued past it and the u stores
-    // of the iterations since it was issued
-    const int ahead = min(NST - 2, nslab - 1 - sl);
-    axk16p_wait<PPW, NS>(ahead, stw ? min(sl, NST - 1) : 0);
-    __builtin_amdgcn_s_barrier();                     // every wave's slab sl landed; slot (sl-1) free
-    asm volatile("" ::: "memory");
-    if (sl + NST - 1 < nslab) issue(sl + NST - 1);
-    const unsigned char* st = lds + (sl % NST) * STAGE;
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      const int kb = sl * BK + kk * 32 + 8 * tg;      // this lane's 8 k of the A fragment
-      // every LDS read here is inline asm (ds_rd128 / ds_rdtr): a compiler-visible LDS read
-      // after the slab's global_load_lds got a vmcnt(0) from the compiler (waiting for the
-      // slabs just issued as well); the lgkmcnt wait is ours (lds_tie)
-      u4v ar[MI][AX ? 1 : 2], wb{}, w0{}, w1{};
-      u2v blo[NT], bhi[NT];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int r = wm + i * 16 + r16;
-        if constexpr (AX) {
-          const int c = kk * 4 + tg;
-          ar[i][0] = ds_rd128(lds_addr(st + r * AROW + ((c ^ ((r >> 1) & 7)) << 4)));
-        } else {
-          const int c = kk * 8 + 2 * tg;
-          ar[i][0] = ds_rd128(lds_addr(st + r * AROW + ((c ^ (r & 15)) << 4)));
-          ar[i][1] = ds_rd128(lds_addr(st + r * AROW + (((c + 1) ^ (r & 15)) << 4)));
-        }
-      }
-      if constexpr (AX) {
-        wb = ds_rd128(lds_addr(&s_w3b[kb]));
-        if (stw) {
-          w0 = ds_rd128(lds_addr(&s_w3[kb]));
-          w1 = ds_rd128(lds_addr(&s_w3[kb + 4]));
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int cb = (wn + j * 16 + 4 * tp) >> 3, half = (tp & 1) * 8;
-        const int k0r = kk * 32 + 8 * tg + tq, k1r = k0r + 4;
-        const int p0 = cb ^ (((k0r & 3) << 1) ^ (((k0r >> 3) & 1) << 3));
-        const int p1 = cb ^ (((k1r & 3) << 1) ^ (((k1r >> 3) & 1) << 3));
-        blo[j] = ds_rdtr(lds_addr(st + ABYTES + k0r * 256 + (p0 << 4) + half));
-        bhi[j] = ds_rdtr(lds_addr(st + ABYTES + k1r * 256 + (p1 << 4) + half));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int h = 0; h < (AX ? 1 : 2); ++h) lds_tie(ar[i][h]);
-      lds_tie(wb); lds_tie(w0); lds_tie(w1);
-#pragma unroll
-      for (int j = 0; j < NT; ++j) { lds_tie(blo[j]); lds_tie(bhi[j]); }
-      bf16x8 a[MI], b[NT];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        if constexpr (AX) {
-          const u4v h = ar[i][0];
-          auto sel = [](uint32_t hv, uint32_t wv) {   // per bf16 half: h > 0 ? w : 0
-            return (bf16_lo(hv) > 0.f ? wv & 0xffffu : 0u) | (bf16_hi(hv) > 0.f ? wv & 0xffff0000u : 0u);
-          };
-          const uint4 u = {sel(h.x, wb.x), sel(h.y, wb.y), sel(h.z, wb.z), sel(h.w, wb.w)};
-          a[i] = __builtin_bit_cast(bf16x8, u);
-          if (stw) {   // u rows (fp32) for the weight gradient
-            const float4 f0 = __builtin_bit_cast(float4, w0), f1 = __builtin_bit_cast(float4, w1);
-            const int rr = m0 + wm + i * 16 + r16;
-            const uint32_t o = rr < M ? (uint32_t)(rr * d.ax_ld + kb) * 4u : 0xfffffff0u;
-            buf_st4(rAx, o, f4{bf16_lo(h.x) > 0.f ? f0.x : 0.f, bf16_hi(h.x) > 0.f ? f0.y : 0.f,
-                               bf16_lo(h.y) > 0.f ? f0.z : 0.f, bf16_hi(h.y) > 0.f ? f0.w : 0.f});
-            buf_st4(rAx, rr < M ? o + 16u : 0xfffffff0u,
-                    f4{bf16_lo(h.z) > 0.f ? f1.x : 0.f, bf16_hi(h.z) > 0.f ? f1.y : 0.f,
-                       bf16_lo(h.w) > 0.f ? f1.z : 0.f, bf16_hi(h.w) > 0.f ? f1.w : 0.f});
-          }
-        } else {
-          const u2v lo = pack_bf16x4(__builtin_bit_cast(float4, ar[i][0]));
-          const u2v hi = pack_bf16x4(__builtin_bit_cast(float4, ar[i][1]));
-          const uint4 u = {lo.x, lo.y, hi.x, hi.y};
-          a[i] = __builtin_bit_cast(bf16x8, u);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const uint4 v = {blo[j].x, blo[j].y, bhi[j].x, bhi[j].y};
-        b[j] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-  }
-  const bool writer = p == 0 && n0 == 0;
-  if constexpr (AX) rows_finish<BM, 1024>(batch.rows, d, m0, writer, bid == 0, rows_x, s_q, s_coef, s_l);
-  // epilogue: coefficient, ReLU-backward mask, store (k_axk16's op order)
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int lr = wm + i * 16 + (lane >> 4) * 4 + r, row = m0 + lr;
-      const float cf = AX ? s_coef[d.ax_slot][lr] : 1.f;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int col = n0 + wn + j * 16 + (lane & 15);
-        float v = acc[i][j][r];
-        if (AX) v *= cf;
-        v = hm[i][j][r] > 0.f ? v : 0.f;
-        if (row < M && col < N) st_big(d.C + (size_t)row * d.ldc + col, v);
-      }
-    }
-  if constexpr (AX) rows_loss<BM>(batch.rows, m0, writer, s_l);
-}
-
-// whether an act16 k_axk16 level (axk16_ok form `ax`) can run on k_axk16p, and its row tile
-// (0: no): bf16 weight shadows, no rides, K % 64 == 0, N % 8 == 0, 16-byte operand rows,
-// one workgroup per CU at least
-// Opt-in (SACMI_AXK16P=1, read per enqueue): bit-identical to k_axk16 but measured slower
-// (config 5, same box, alternating: L5 29.4 vs 26.3 us, L9 25.4 vs 23.2, 3,204 vs 3,268
-// updates/s — profiles/r05/axk16p_ab): the dh levels are not bound by their K loop (the
-// register-staged and the ring kernel take about the same time for the same tiles) but by
-// what surrounds it — 32 MB of fp32 dh and u rows written per critic level
-static int axk16p_plan(GemmBatch& b, int ax) {
-  if (!SACMI_AXK16P || b.ride.kind || b.ride.pk_blocks) return 0;
-  const char* e = std::getenv("SACMI_AXK16P");
-  if (!e || std::atoi(e) == 0) return 0;
-  for (int i = 0; i < b.count; ++i) {
-    const GemmDesc& d = b.d[i];
-    if (!d.Bh || !d.x16 || (d.K % 64) || d.K > 512 || (d.N % 8) || d.N < 8) return 0;
-    if (((uintptr_t)d.A & 15) || ((uintptr_t)d.Bh & 15) || (d.ldb & 7)) return 0;
-    if (ax ? (!d.a16 || (d.lda & 7) || ((uintptr_t)d.ax_w & 15) || (d.ax_out && ((d.ax_ld & 3) || ((uintptr_t)d.ax_out & 15))))
-           : (d.a16 || (d.lda & 3)))
-      return 0;
-  }
-  GemmBatch t = b;   // (b keeps k_axk16's tiles unless this kernel takes the level)
-  if (assign_tiles<128, 128>(t) >= 256) { b = t; return 128; }
-  t = b;
-  if (!ax && assign_tiles<64, 128>(t) >= 256) { b = t; return 64; }
-  return 0;
-}
-
 // NSL: the partial loads each thread issues (= ns where instantiated, else kDwMaxSplit with
 // the loads past ns at an out-of-range offset): no VMEM issue slots for absent splits
 template <int NSL>
@@ -3778,151 +2309,6 @@ __global__ __launch_bounds__(256) void k_dw_fin(GemmBatch batch, int ns, int64_t
   store_err_flags(batch);
 }
 
-// k_dw_fin, pipelined (opt-in, SACMI_DWFIN_P=1 — measured slower: config 5 L6 65.8 vs 63.4 us,
-// L13 42.0 vs 40.5, 3,213 vs 3,246 updates/s, profiles/r05/dwfin_p_ab): the same
-// per-group arithmetic over the same virtual blocks (256 four-column groups each, dealt to
-// the descs in order), but on a grid of at most kDwFinGrid workgroups that loop over them —
-// the next block's loads (partials, parameter, moments, target) are issued before this
-// block's stores, so the level's reads and writes overlap instead of running as one read
-// phase then one write phase across the whole chip (k_dw_fin: ~2.5-2.7 TB/s at config 5,
-// profiles/r05/pmc_c5.json).  Identical bits: each group's sums and updates are k_dw_fin's.
-#ifndef SACMI_DWFIN_GRID
-#define SACMI_DWFIN_GRID 768      // (3 resident per CU at the 11-split form's 138 VGPRs)
-#endif
-constexpr int kDwFinGrid = SACMI_DWFIN_GRID;
-
-template <int NSL>
-__global__ __launch_bounds__(256) void k_dw_fin_p(GemmBatch batch, int ns, int64_t ws_stride, int nvb) {
-  const TlMark tl_mark(batch.tl, TL_DW_FIN_P);
-  __shared__ AdamScalars s_k[3];
-  __shared__ int s_err;
-  const AdamFuse& af = batch.adam;
-  const bool adam = batch.has_adam != 0;
-  if (adam && threadIdx.x < 3) s_k[threadIdx.x] = fuse_scalars(af, threadIdx.x, af.step_offset);
-  if (threadIdx.x == 0) s_err = adam ? af.sc->err : 0;
-  __syncthreads();
-  const bool void_st = (s_err & af.err_skip) != 0;   // (see k_dw_fin)
-  const float omb1 = 1.f - af.beta1, omb2 = 1.f - af.beta2, omtau = 1.f - af.tau;
-  const bool wt = batch.st_wt != 0;
-  const uint32_t oob = 0xfffffff0u;
-  // virtual block vb -> its desc q, the desc's first block and its partial-row offset
-  auto locate = [&](int vb, int& q, int& bstart, int64_t& off) {
-    q = batch.count - 1; bstart = 0; off = 0;
-    int acc = 0;
-    bool found = false;
-    int64_t o = 0;
-    for (int qq = 0; qq < batch.count; ++qq) {
-      const int n_el_q = batch.d[qq].M * dw_ncols(batch.d[qq]);
-      const int nb = (n_el_q / 4 + 255) / 256;
-      if (!found && vb < acc + nb) { q = qq; bstart = acc; off = o; found = true; }
-      o += n_el_q;
-      acc += nb;
-    }
-  };
-  struct Ld {
-    float4 t[NSL], pp, mm, vv, tt;
-  };
-  // every load of one block's group, at once; a block past the level (vb >= nvb) or a group
-  // past its desc reads at out-of-range offsets (no access)
-  auto load = [&](int vb, Ld& L) {
-    int q, bstart;
-    int64_t off;
-    locate(vb < nvb ? vb : 0, q, bstart, off);
-    const GemmDesc& d = batch.d[q];
-    const int nc = dw_ncols(d), gpr = nc / 4, n_gr = d.M * gpr;
-    const int g = (vb - bstart) * 256 + threadIdx.x;
-    const bool live = vb < nvb && g < n_gr;
-    const int row = live ? g / gpr : 0, c4 = live ? (g - row * gpr) * 4 : 0;
-    const uint32_t o = (uint32_t)(row * d.ldc + c4) * 4u;
-    const bool pol = d.epi == EPI_ADAM_POLYAK;
-    const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
-    const float* wsd = batch.ws + off;
-    const rsrc_t rWs = make_rsrc(wsd, (uint32_t)(((int64_t)(ns - 1) * ws_stride + (int64_t)n_gr * 4) * 4));
-    const rsrc_t rTg = make_rsrc(adam && pol ? af.T + abase - af.t_base : wsd, adam && pol ? 0x7fffffffu : 0u);
-    const rsrc_t rC = make_rsrc(d.C, 0x7fffffffu);
-    const rsrc_t rM = make_rsrc(adam ? af.M + abase : d.C, adam ? 0x7fffffffu : 0u);
-    const rsrc_t rV = make_rsrc(adam ? af.V + abase : d.C, adam ? 0x7fffffffu : 0u);
-#pragma unroll
-    for (int sp = 0; sp < NSL; ++sp)
-      L.t[sp] = buf_ld4(rWs, live && sp < ns ? (uint32_t)((int64_t)sp * ws_stride + (int64_t)g * 4) * 4u : oob);
-    L.pp = buf_ld4(rC, adam && live ? o : oob);
-    L.mm = buf_ld4(rM, live ? o : oob);
-    L.vv = buf_ld4(rV, live ? o : oob);
-    L.tt = buf_ld4(rTg, pol && live ? o : oob);
-  };
-  // k_dw_fin's arithmetic and stores for one block's group
-  auto finish = [&](int vb, const Ld& L) {
-    int q, bstart;
-    int64_t off;
-    locate(vb, q, bstart, off);
-    const GemmDesc& d = batch.d[q];
-    const int nc = dw_ncols(d), ncr = dw_ncols_real(d), gpr = nc / 4, n_gr = d.M * gpr;
-    const int g = (vb - bstart) * 256 + threadIdx.x;
-    if (g >= n_gr) return;
-    const int row = g / gpr, c4 = (g - row * gpr) * 4;
-    const uint32_t o = (uint32_t)(row * d.ldc + c4) * 4u;
-    const bool pol = d.epi == EPI_ADAM_POLYAK;
-    const bool pol_st = pol && (s_err & af.err_nopolyak) == 0;
-    const int64_t abase = adam ? (int64_t)(d.C - af.P) : 0;
-    const rsrc_t rC = make_rsrc(d.C, 0x7fffffffu);
-    const rsrc_t rM = make_rsrc(adam ? af.M + abase : d.C, adam ? 0x7fffffffu : 0u);
-    const rsrc_t rV = make_rsrc(adam ? af.V + abase : d.C, adam ? 0x7fffffffu : 0u);
-    const rsrc_t rG = make_rsrc(adam && af.G ? af.G + abase : d.C, adam && af.G ? 0x7fffffffu : 0u);
-    const rsrc_t rT = make_rsrc(adam && pol ? af.T + abase - af.t_base : d.C, adam && pol ? 0x7fffffffu : 0u);
-    float v[4] = {L.t[0].x, L.t[0].y, L.t[0].z, L.t[0].w};
-#pragma unroll
-    for (int sp = 1; sp < NSL; ++sp)
-      if (sp < ns) {
-#pragma clang fp contract(off)
-        v[0] += L.t[sp].x; v[1] += L.t[sp].y; v[2] += L.t[sp].z; v[3] += L.t[sp].w;
-      }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = c4 + j < ncr ? v[j] : 0.f;
-    auto st4 = [&](rsrc_t r, float a0, float a1, float a2, float a3) {
-      if (wt) buf_st4<kStAux>(r, o, f4{a0, a1, a2, a3});
-      else buf_st4<0>(r, o, f4{a0, a1, a2, a3});
-    };
-    if (adam) {
-      float p4[4] = {L.pp.x, L.pp.y, L.pp.z, L.pp.w}, m4[4] = {L.mm.x, L.mm.y, L.mm.z, L.mm.w};
-      float v4[4] = {L.vv.x, L.vv.y, L.vv.z, L.vv.w}, t4[4] = {L.tt.x, L.tt.y, L.tt.z, L.tt.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        adam_elem(p4[j], m4[j], v4[j], v[j], omb1, af.beta2, omb2, af.eps, s_k[d.adam_step]);
-        t4[j] = polyak(t4[j], p4[j], omtau, af.tau);
-      }
-      if (af.G) st4(rG, v[0], v[1], v[2], v[3]);
-      st4(rC, p4[0], p4[1], p4[2], p4[3]);
-      st4(rM, m4[0], m4[1], m4[2], m4[3]);
-      st4(rV, v4[0], v4[1], v4[2], v4[3]);
-      auto st_bf4 = [&](unsigned short* h, const float (&x)[4]) {   // 4 bf16 shadows, 8 bytes
-        const uint32_t lo = (uint32_t)bf16_bits(x[0]) | ((uint32_t)bf16_bits(x[1]) << 16);
-        const uint32_t hi = (uint32_t)bf16_bits(x[2]) | ((uint32_t)bf16_bits(x[3]) << 16);
-        if (wt) st_wt8(h, 0u, lo, hi);
-        else *reinterpret_cast<uint2*>(h) = make_uint2(lo, hi);
-      };
-      if (af.Ph) st_bf4(af.Ph + abase + o / 4u, p4);
-      if (pol_st) {
-        st4(rT, t4[0], t4[1], t4[2], t4[3]);
-        if (af.Th) st_bf4(af.Th + abase - af.t_base + o / 4u, t4);
-      }
-    } else {
-      st4(rC, v[0], v[1], v[2], v[3]);
-    }
-  };
-  if (!void_st) {
-    Ld cur, nxt;
-    int vb = blockIdx.x;
-    load(vb, cur);
-    for (; vb < nvb; vb += gridDim.x) {
-      load(vb + gridDim.x, nxt);   // (past the level: out-of-range, no access)
-      finish(vb, cur);
-      cur = nxt;
-    }
-  }
-  if (adam && blockIdx.x == 0) adam_block0(af, s_err, omb1, omb2);
-  store_err_flags(batch);
-}
-
 // 1 when the level carries bf16 activation operands (any GemmDesc a16 / b16 / c16 / x16);
 // each kernel that takes them checks the per-desc pattern it supports
 static int level_act16(const GemmBatch& b) {
@@ -3931,17 +2317,14 @@ static int level_act16(const GemmBatch& b) {
   return any ? 1 : 0;
 }
 
-// bf16 deep-K weight-gradient levels: split count and workspace need, or 0 (old path)
+// bf16 deep-K weight-gradient levels: split count and workspace need, or 0 (k_gemm)
 static int dw_split_plan(GemmBatch& b, int64_t* stride) {
-  // (rides: the gather on any split-K kernel, the sampler on k_dw_part16 only)
-  if ((!b.bf16 && !SACMI_DW_SPLIT_FP32) || !b.ws || (b.ride.kind == 1 && !(b.bf16 && SACMI_DW_LDS16)))
-    return 0;
+  if (!b.bf16 || !b.ws) return 0;
   int64_t el = 0;
   int tiles = 0;
   for (int i = 0; i < b.count; ++i) {
     GemmDesc& d = b.d[i];
-    if (d.a_kc || d.b_kc || d.K < 2048) return 0;
-    if (d.axk && !(d.axk == 2 && b.bf16 && SACMI_DW_LDS16)) return 0;   // (axk 2: k_dw_part16 only)
+    if (d.a_kc || d.b_kc || d.K < 2048 || d.axk) return 0;
     if (d.epi != EPI_STORE && d.epi < EPI_ADAM) return 0;
     // k_dw_fin's 4-column groups: the row-sum column is the bias column right after the
     // last output column, and output rows (and their Adam state) are 16-byte aligned with
@@ -3962,22 +2345,21 @@ static int dw_split_plan(GemmBatch& b, int64_t* stride) {
   // as many K splits as fit in one pass over the chip's workgroup slots (2 per CU at
   // 67 KB of LDS each): a partial second pass costs a whole slab loop (config 5: a
   // 528-workgroup L6 took 96 us, 440 workgroups 82 us)
-  static const int target = std::getenv("SACMI_DW_TARGET") ? std::atoi(std::getenv("SACMI_DW_TARGET")) : SACMI_DW_TARGET;
-  int ns = target / tiles;
+  int ns = kDwTarget / tiles;
   ns = ns < 1 ? 1 : ns > kDwMaxSplit ? kDwMaxSplit : ns;
   if ((int64_t)ns * el > b.ws_floats) return 0;
   *stride = el;
   return ns;
 }
 
-// whether launch_gemm may run a level on k_fwd: plain forward GEMMs (both operands
-// K-contiguous, store / ReLU epilogue, optional bias and dot partials), no prologue,
-// no rides, and enough 128x128 tiles to fill the chip
+// whether launch_gemm may run a level on k_fwd16 / k_fwd16p: bf16 plain forward GEMMs
+// (both operands K-contiguous, store / ReLU epilogue, optional bias and dot partials), no
+// prologue, no rides, and enough 128-row tiles to fill the chip.  (fp32 levels: the
+// 512-thread K-split k_gemm tiles measured faster — config 3: 1,351 vs 1,229 updates/s;
+// with bf16 MFMAs the levels are operand-traffic bound and the LDS sharing wins — config 5:
+// 1,381 -> 1,458.)
 static bool fwd_big_ok(GemmBatch& b) {
-  // bf16 only: with fp32 operands the 512-thread K-split tiles measured faster (config 3:
-  // 1,351 vs 1,229 updates/s); with bf16 MFMAs the levels are operand-traffic bound and
-  // the LDS sharing wins (config 5: 1,381 -> 1,458)
-  if (b.ride.kind || (!b.bf16 && !SACMI_FWD_BIG_FP32)) return false;
+  if (b.ride.kind || !b.bf16) return false;
   for (int i = 0; i < b.count; ++i) {
     const GemmDesc& d = b.d[i];
     if (!d.a_kc || !d.b_kc || d.axk || d.a_ksc || d.rs_col >= 0) return false;
@@ -3986,12 +2368,11 @@ static bool fwd_big_ok(GemmBatch& b) {
     if (d.dotp && (d.N % 32)) return false;
   }
   // 128-column tiles when they give two workgroups per CU, else 64-column ones
-  if (b.bf16 && (!SACMI_FWD_BF16_N64 || (assign_tiles<kFBM, 128>(b) >= 512 && !SACMI_FWD_BF16_ALL64)))
-    return assign_tiles<kFBM, 128>(b) >= 256 * SACMI_FWD_BIG_MIN;
-  return assign_tiles<kFBM, 64>(b) >= 512 * SACMI_FWD_BIG_MIN;
+  if (assign_tiles<kFBM, 128>(b) >= 512) return true;
+  return assign_tiles<kFBM, 64>(b) >= 512;
 }
 
-// one configuration, fp32 or bf16 MFMA operands (1024 threads)
+// one k_gemm configuration, fp32 or bf16 MFMA operands
 template <int TM, int TN, int KSPLIT, int G, int MG, bool ADAM, int AXK>
 static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
   const dim3 blk(64 * KSPLIT * MG);
@@ -3999,231 +2380,155 @@ static void launch_k(const GemmBatch& b, int grid, hipStream_t s) {
   else hipLaunchKernelGGL((k_gemm<TM, TN, KSPLIT, G, MG, ADAM, AXK, false>), dim3(grid), blk, 0, s, b);
 }
 
-// the LDS-staged core (CORE 1), 1024 threads
-template <int TM, int TN, int KSP, int MG, bool ADAM, int AXK>
-static void launch_ks(const GemmBatch& b, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((k_gemm<TM, TN, KSP, 1, MG, ADAM, AXK, false, 1>), dim3(grid), dim3(1024), 0, s, b);
-}
-
-// whether a level can take the staged core: fp32 operands, 16-byte-aligned rows, every
-// 16-byte chunk a DMA lane reads inside its row (KC: ld >= round4(K); MN: ld >= round4(M|N)),
-// and the K vector it stages (ax_w / a_ksc) within kStgKW
-#ifndef SACMI_STAGED
-#define SACMI_STAGED 0
-#endif
-static bool staged_ok(const GemmBatch& b) {
-  // $SACMI_STAGED=0/1 overrides the build default; SACMI_NO_STAGED forces it off
-  static const bool env = std::getenv("SACMI_NO_STAGED") == nullptr &&
-                          (std::getenv("SACMI_STAGED") ? std::atoi(std::getenv("SACMI_STAGED")) != 0 : SACMI_STAGED != 0);
-  if (!env || b.bf16) return false;
-  for (int i = 0; i < b.count; ++i) {
-    const GemmDesc& d = b.d[i];
-    if (d.a16 || d.b16 || d.c16 || d.x16) return false;
-    if (d.K < 1 || d.K > kStgKW || d.M < 1 || d.N < 1) return false;
-    if (((uintptr_t)d.A & 15) || ((uintptr_t)d.B & 15) || (d.lda & 3) || (d.ldb & 3)) return false;
-    if (d.lda < round_up(d.a_kc ? d.K : d.M, 4) || d.ldb < round_up(d.b_kc ? d.K : d.N, 4)) return false;
-  }
-  return true;
-}
-
-// every desc's B operand has a bf16 shadow (SACMI_BF16_SHADOW 0: never read them)
-#ifndef SACMI_BF16_SHADOW
-#define SACMI_BF16_SHADOW 1
-#endif
+// every desc's B operand has a bf16 shadow
 static bool all_bh(const GemmBatch& b) {
-  if (!SACMI_BF16_SHADOW) return false;
   for (int i = 0; i < b.count; ++i)
     if (!b.d[i].Bh) return false;
   return true;
 }
 
-void launch_gemm(const GemmBatch& b0, hipStream_t s) {
-  if (b0.count == 0) return;
-  if (b0.heads_ticket && !gemm_level_heads_fold_ok(b0, b0.heads.A))
-    throw Error{SACMI_ESTATE, "policy heads folded into a level outside k_gemm's 32x64 forward tiles"};
-  GemmBatch b = b0;
-  // Polyak rides (RideAlong::pk) run on k_gemm's 1024-thread configurations only: a level
-  // that goes to a split-K / LDS-staged kernel must not carry them
-  const Error pk_err{SACMI_ESTATE, "Polyak ride on a level outside k_gemm"};
-  {
-    int64_t stride = 0;
-    const int ns = SACMI_DW_SPLIT ? dw_split_plan(b, &stride) : 0;
-    if (ns > 0) {
-      if (b.ride.pk_blocks) throw pk_err;
-      const int ride = b.ride.kind ? b.ride.nblocks : 0;
-      if (b.ride.kind == 1 &&
-          mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > (size_t)kDw16LdsBytes)
-        throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_dw_part16's LDS"};
-      const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
-      const int form = level_act16(b);   // act16: every X operand bf16
-      for (int i = 0; i < b.count; ++i)
-        if ((b.d[i].a16 && b.d[i].axk != 2) || b.d[i].c16 || b.d[i].x16 || (form && !b.d[i].b16) || form < 0)
-          throw Error{SACMI_ESTATE, "split-K weight gradient: unsupported bf16 activation operand"};
-      if (form && !(b.bf16 && SACMI_DW_LDS16))
-        throw Error{SACMI_ESTATE, "bf16 activation operands need k_dw_part16"};
-      bool axt = false;
-      for (int i = 0; i < b.count; ++i) axt = axt || b.d[i].axk == 2;
-      if (axt && !(b.bf16 && SACMI_DW_LDS16 && form))
-        throw Error{SACMI_ESTATE, "dW A transform (axk 2) needs k_dw_part16 with bf16 X operands"};
-      if (b.bf16 && SACMI_DW_LDS16 && form && axt) hipLaunchKernelGGL((k_dw_part16<true, true>), dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
-      else if (b.bf16 && SACMI_DW_LDS16 && form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
-      else if (b.bf16 && SACMI_DW_LDS16) hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
-      else if (b.bf16) hipLaunchKernelGGL(k_dw_part<true>, dim3(grid), dim3(256), 0, s, b, ns, stride);
-      else hipLaunchKernelGGL(k_dw_part<false>, dim3(grid), dim3(256), 0, s, b, ns, stride);
-      HIP_LAUNCH_CHECK();
-      int fin_grid = 0;                    // k_dw_fin: kDwFinEpt 4-column groups per thread, per desc
-      for (int i = 0; i < b.count; ++i)
-        fin_grid += (b.d[i].M * (dw_ncols(b.d[i]) / 4) + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
-      if (b.tl) b.tl += kTlWords;          // the second kernel of the level
-      const dim3 fg(fin_grid), fb(256);
-      // the fin's stores: plain (SACMI_FIN_WT=1: write-through, measured slower at config 5:
-      // 3,412 -> 3,357 updates/s, the boundary behind the level unchanged)
-      static const bool fin_wt = std::getenv("SACMI_FIN_WT") != nullptr && std::atoi(std::getenv("SACMI_FIN_WT")) != 0;
-      b.st_wt = fin_wt ? 1 : 0;
-      static const bool nsl = SACMI_DWFIN_NSL && std::getenv("SACMI_NO_DWFIN_NSL") == nullptr;
-      const char* fin_p = std::getenv("SACMI_DWFIN_P");   // (opt-in; read per enqueue: tests switch it)
-      if (nsl && kDwFinEpt == 1 && fin_p && std::atoi(fin_p) != 0) {
-        const dim3 pg(std::min(fin_grid, kDwFinGrid));
-        switch (ns) {
-          case 1: hipLaunchKernelGGL(k_dw_fin_p<1>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 2: hipLaunchKernelGGL(k_dw_fin_p<2>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 3: hipLaunchKernelGGL(k_dw_fin_p<3>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 4: hipLaunchKernelGGL(k_dw_fin_p<4>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 5: hipLaunchKernelGGL(k_dw_fin_p<5>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 6: hipLaunchKernelGGL(k_dw_fin_p<6>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 7: hipLaunchKernelGGL(k_dw_fin_p<7>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 8: hipLaunchKernelGGL(k_dw_fin_p<8>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 9: hipLaunchKernelGGL(k_dw_fin_p<9>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 10: hipLaunchKernelGGL(k_dw_fin_p<10>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 11: hipLaunchKernelGGL(k_dw_fin_p<11>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          case 12: hipLaunchKernelGGL(k_dw_fin_p<12>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-          default: hipLaunchKernelGGL(k_dw_fin_p<kDwMaxSplit>, pg, fb, 0, s, b, ns, stride, fin_grid); break;
-        }
+// the split-K weight-gradient level: k_dw_part16 (partials) + k_dw_fin (sum + epilogue)
+static void launch_dw_split(GemmBatch& b, int ns, int64_t stride, hipStream_t s) {
+  if (b.ride.pk_blocks) throw Error{SACMI_ESTATE, "Polyak ride on a level outside k_gemm"};
+  const int ride = b.ride.kind ? b.ride.nblocks : 0;
+  if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > (size_t)kDw16LdsBytes)
+    throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_dw_part16's LDS"};
+  const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
+  const int form = level_act16(b);   // act16: every X operand bf16
+  for (int i = 0; i < b.count; ++i)
+    if (b.d[i].a16 || b.d[i].c16 || b.d[i].x16 || (form && !b.d[i].b16))
+      throw Error{SACMI_ESTATE, "split-K weight gradient: unsupported bf16 activation operand"};
+  if (form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
+  else hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
+  HIP_LAUNCH_CHECK();
+  int fin_grid = 0;                    // k_dw_fin: kDwFinEpt 4-column groups per thread, per desc
+  for (int i = 0; i < b.count; ++i)
+    fin_grid += (b.d[i].M * (dw_ncols(b.d[i]) / 4) + 256 * kDwFinEpt - 1) / (256 * kDwFinEpt);
+  if (b.tl) b.tl += kTlWords;          // the second kernel of the level
+  // the fin's stores are plain (write-through measured slower at config 5: 3,412 -> 3,357
+  // updates/s, the boundary behind the level unchanged)
+  b.st_wt = 0;
+  const dim3 fg(fin_grid), fb(256);
+  switch (ns) {   // one instantiation per split count: no load slots for absent splits
+    case 1: hipLaunchKernelGGL(k_dw_fin<1>, fg, fb, 0, s, b, ns, stride); break;
+    case 2: hipLaunchKernelGGL(k_dw_fin<2>, fg, fb, 0, s, b, ns, stride); break;
+    case 3: hipLaunchKernelGGL(k_dw_fin<3>, fg, fb, 0, s, b, ns, stride); break;
+    case 4: hipLaunchKernelGGL(k_dw_fin<4>, fg, fb, 0, s, b, ns, stride); break;
+    case 5: hipLaunchKernelGGL(k_dw_fin<5>, fg, fb, 0, s, b, ns, stride); break;
+    case 6: hipLaunchKernelGGL(k_dw_fin<6>, fg, fb, 0, s, b, ns, stride); break;
+    case 7: hipLaunchKernelGGL(k_dw_fin<7>, fg, fb, 0, s, b, ns, stride); break;
+    case 8: hipLaunchKernelGGL(k_dw_fin<8>, fg, fb, 0, s, b, ns, stride); break;
+    case 9: hipLaunchKernelGGL(k_dw_fin<9>, fg, fb, 0, s, b, ns, stride); break;
+    case 10: hipLaunchKernelGGL(k_dw_fin<10>, fg, fb, 0, s, b, ns, stride); break;
+    case 11: hipLaunchKernelGGL(k_dw_fin<11>, fg, fb, 0, s, b, ns, stride); break;
+    case 12: hipLaunchKernelGGL(k_dw_fin<12>, fg, fb, 0, s, b, ns, stride); break;
+    default: hipLaunchKernelGGL(k_dw_fin<kDwMaxSplit>, fg, fb, 0, s, b, ns, stride); break;
+  }
+  HIP_LAUNCH_CHECK();
+}
+
+// the batch-4096-class dh level: k_axk16 (axk16_ok form `ax`)
+static void launch_axk16(const GemmBatch& b, int ax, hipStream_t s) {
+  if (b.ride.pk_blocks) throw Error{SACMI_ESTATE, "Polyak ride on a level outside k_gemm"};
+  for (int i = 0; i < b.count; ++i)   // k_axk16 computes no dL/da partials
+    if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a k_axk16 level"};
+  const bool bh = all_bh(b);
+  const dim3 grid(b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0)), blk(64 * kAxWaves);
+  const int form = level_act16(b);   // act16: mask sources (and AX sources) bf16
+  for (int i = 0; i < b.count; ++i)
+    if (b.d[i].c16 || b.d[i].b16 || b.d[i].x16 != form || b.d[i].a16 != (form && b.d[i].axk == 1))
+      throw Error{SACMI_ESTATE, "k_axk16: unsupported bf16 activation operand"};
+  if (form) {
+    if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true, true>), grid, blk, 0, s, b);
+    else if (ax) hipLaunchKernelGGL((k_axk16<true, false, true>), grid, blk, 0, s, b);
+    else if (bh) hipLaunchKernelGGL((k_axk16<false, true, true>), grid, blk, 0, s, b);
+    else hipLaunchKernelGGL((k_axk16<false, false, true>), grid, blk, 0, s, b);
+  } else if (ax && bh) {
+    hipLaunchKernelGGL((k_axk16<true, true>), grid, blk, 0, s, b);
+  } else if (ax) {
+    hipLaunchKernelGGL((k_axk16<true, false>), grid, blk, 0, s, b);
+  } else if (bh) {
+    hipLaunchKernelGGL((k_axk16<false, true>), grid, blk, 0, s, b);
+  } else {
+    hipLaunchKernelGGL((k_axk16<false, false>), grid, blk, 0, s, b);
+  }
+  HIP_LAUNCH_CHECK();
+}
+
+// the batch-4096-class bf16 forward level: k_fwd16p (multi-slab LDS ring) where its plan
+// applies, else k_fwd16.  SACMI_NO_FWD16P (read once): k_fwd16 only — the parity test that
+// holds the two kernels to the same bits (tests/test_gpu_fwd16p.py)
+static void launch_fwd16(GemmBatch& b, hipStream_t s) {
+  if (b.ride.pk_blocks) throw Error{SACMI_ESTATE, "Polyak ride on a level outside k_gemm"};
+  const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
+  const bool bh = all_bh(b);
+  const bool ah = level_act16(b) != 0;   // act16: bf16 input rows and bf16 output
+  if (ah) {
+    for (int i = 0; i < b.count; ++i)
+      if (!b.d[i].a16 || !b.d[i].c16 || b.d[i].b16 || b.d[i].x16 || (b.d[i].N & 1) || (b.d[i].ldc & 1))
+        throw Error{SACMI_ESTATE, "k_fwd16: unsupported bf16 activation operands"};
+    if (bh) {
+      GemmBatch bp = b;
+      const int bm = fwd16p_plan(bp);
+      if (bm) {
+        const dim3 g(bp.total_tiles);
+        if (bm == 256) hipLaunchKernelGGL((k_fwd16p<256>), g, dim3(1024), 0, s, bp);
+        else hipLaunchKernelGGL((k_fwd16p<128>), g, dim3(1024), 0, s, bp);
         HIP_LAUNCH_CHECK();
         return;
       }
-      switch (nsl ? ns : 0) {
-        case 1: hipLaunchKernelGGL(k_dw_fin<1>, fg, fb, 0, s, b, ns, stride); break;
-        case 2: hipLaunchKernelGGL(k_dw_fin<2>, fg, fb, 0, s, b, ns, stride); break;
-        case 3: hipLaunchKernelGGL(k_dw_fin<3>, fg, fb, 0, s, b, ns, stride); break;
-        case 4: hipLaunchKernelGGL(k_dw_fin<4>, fg, fb, 0, s, b, ns, stride); break;
-        case 5: hipLaunchKernelGGL(k_dw_fin<5>, fg, fb, 0, s, b, ns, stride); break;
-        case 6: hipLaunchKernelGGL(k_dw_fin<6>, fg, fb, 0, s, b, ns, stride); break;
-        case 7: hipLaunchKernelGGL(k_dw_fin<7>, fg, fb, 0, s, b, ns, stride); break;
-        case 8: hipLaunchKernelGGL(k_dw_fin<8>, fg, fb, 0, s, b, ns, stride); break;
-        case 9: hipLaunchKernelGGL(k_dw_fin<9>, fg, fb, 0, s, b, ns, stride); break;
-        case 10: hipLaunchKernelGGL(k_dw_fin<10>, fg, fb, 0, s, b, ns, stride); break;
-        case 11: hipLaunchKernelGGL(k_dw_fin<11>, fg, fb, 0, s, b, ns, stride); break;
-        case 12: hipLaunchKernelGGL(k_dw_fin<12>, fg, fb, 0, s, b, ns, stride); break;
-        default: hipLaunchKernelGGL(k_dw_fin<kDwMaxSplit>, fg, fb, 0, s, b, ns, stride); break;
-      }
-      HIP_LAUNCH_CHECK();
-      return;
     }
-    b = b0;
-    for (int i = 0; i < b.count; ++i)   // (no other kernel knows the dW A transform)
-      if (b.d[i].axk == 2) throw Error{SACMI_ESTATE, "dW A transform (axk 2) outside the split-K path"};
   }
-  if (SACMI_AXK_LDS16) {
-    const int ax = axk16_ok(b);
-    if (ax >= 0) {
-      if (b.ride.pk_blocks) throw pk_err;
-      for (int i = 0; i < b.count; ++i)   // k_axk16 computes no dL/da partials
-        if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a k_axk16 level"};
-      const bool bh = all_bh(b);
-      const dim3 grid(b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0)), blk(64 * kAxWaves);
-      const int form = level_act16(b);   // act16: mask sources (and AX sources) bf16
-      if (form < 0) throw Error{SACMI_ESTATE, "k_axk16 level with mixed bf16 activation flags"};
-      for (int i = 0; i < b.count; ++i)
-        if (b.d[i].c16 || b.d[i].b16 || b.d[i].x16 != form || b.d[i].a16 != (form && b.d[i].axk == 1))
-          throw Error{SACMI_ESTATE, "k_axk16: unsupported bf16 activation operand"};
-      const int bm = form && bh ? axk16p_plan(b, ax) : 0;
-      if (bm) {   // (axk16p_plan re-tiled the level: its grid)
-        const dim3 pg(b.total_tiles);
-        if (ax) hipLaunchKernelGGL((k_axk16p<128, true>), pg, dim3(1024), 0, s, b);
-        else if (bm == 128) hipLaunchKernelGGL((k_axk16p<128, false>), pg, dim3(1024), 0, s, b);
-        else hipLaunchKernelGGL((k_axk16p<64, false>), pg, dim3(1024), 0, s, b);
-      } else if (form) {
-        if (ax && bh) hipLaunchKernelGGL((k_axk16<true, true, true>), grid, blk, 0, s, b);
-        else if (ax) hipLaunchKernelGGL((k_axk16<true, false, true>), grid, blk, 0, s, b);
-        else if (bh) hipLaunchKernelGGL((k_axk16<false, true, true>), grid, blk, 0, s, b);
-        else hipLaunchKernelGGL((k_axk16<false, false, true>), grid, blk, 0, s, b);
-      } else if (ax && bh) {
-        hipLaunchKernelGGL((k_axk16<true, true>), grid, blk, 0, s, b);
-      } else if (ax) {
-        hipLaunchKernelGGL((k_axk16<true, false>), grid, blk, 0, s, b);
-      } else if (bh) {
-        hipLaunchKernelGGL((k_axk16<false, true>), grid, blk, 0, s, b);
-      } else {
-        hipLaunchKernelGGL((k_axk16<false, false>), grid, blk, 0, s, b);
-      }
-      HIP_LAUNCH_CHECK();
+  const dim3 g(b.total_tiles), b128(64 * fwd16_waves<128>()), b64(64 * fwd16_waves<64>());
+  if (ah) {
+    if (n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true, true>), g, b128, 0, s, b);
+    else if (bh) hipLaunchKernelGGL((k_fwd16<64, true, true>), g, b64, 0, s, b);
+    else if (n128) hipLaunchKernelGGL((k_fwd16<128, false, true>), g, b128, 0, s, b);
+    else hipLaunchKernelGGL((k_fwd16<64, false, true>), g, b64, 0, s, b);
+  } else {
+    if (n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), g, b128, 0, s, b);
+    else if (bh) hipLaunchKernelGGL((k_fwd16<64, true>), g, b64, 0, s, b);
+    else if (n128) hipLaunchKernelGGL((k_fwd16<128>), g, b128, 0, s, b);
+    else hipLaunchKernelGGL((k_fwd16<64>), g, b64, 0, s, b);
+  }
+  HIP_LAUNCH_CHECK();
+}
+
+void launch_gemm(const GemmBatch& b0, hipStream_t s) {
+  if (b0.count == 0) return;
+  GemmBatch b = b0;
+  {
+    int64_t stride = 0;
+    const int ns = dw_split_plan(b, &stride);
+    if (ns > 0) {
+      launch_dw_split(b, ns, stride, s);
       return;
     }
   }
   b = b0;
-  static const bool fwd_big = SACMI_FWD_BIG && std::getenv("SACMI_NO_FWD_BIG") == nullptr;
-  if (fwd_big && fwd_big_ok(b)) {
-    if (b.ride.pk_blocks) throw pk_err;
-    const bool n128 = b.d[0].tiles_n * kFBN128 >= b.d[0].N && b.d[0].tiles_n == (b.d[0].N + 127) / 128;
-    const bool bh = b.bf16 && all_bh(b);
-    if (level_act16(b)) {   // act16: bf16 input rows and bf16 output (k_fwd16 only)
-      for (int i = 0; i < b.count; ++i)
-        if (!b.d[i].a16 || !b.d[i].c16 || b.d[i].b16 || b.d[i].x16 || (b.d[i].N & 1) || (b.d[i].ldc & 1))
-          throw Error{SACMI_ESTATE, "k_fwd16: unsupported bf16 activation operands"};
-      if (!(b.bf16 && SACMI_FWD_LDS16)) throw Error{SACMI_ESTATE, "bf16 activations need k_fwd16"};
-      if (bh) {
-        GemmBatch bp = b;
-        const int bm = fwd16p_plan(bp);
-        if (bm) {
-          static const int nwv = std::getenv("SACMI_FWD16P_WAVES") ? std::atoi(std::getenv("SACMI_FWD16P_WAVES")) : SACMI_FWD16P_WAVES;
-          const dim3 g(bp.total_tiles);
-          if (bm == 256 && nwv == 8) hipLaunchKernelGGL((k_fwd16p<256, 8>), g, dim3(512), 0, s, bp);
-          else if (bm == 256) hipLaunchKernelGGL((k_fwd16p<256, 16>), g, dim3(1024), 0, s, bp);
-          else if (nwv == 8) hipLaunchKernelGGL((k_fwd16p<128, 8>), g, dim3(512), 0, s, bp);
-          else hipLaunchKernelGGL((k_fwd16p<128, 16>), g, dim3(1024), 0, s, bp);
-          HIP_LAUNCH_CHECK();
-          return;
-        }
-      }
-      if (n128 && bh)hipLaunchKernelGGL((k_fwd16<128, true, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
-      else if (bh) hipLaunchKernelGGL((k_fwd16<64, true, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
-      else if (n128) hipLaunchKernelGGL((k_fwd16<128, false, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
-      else hipLaunchKernelGGL((k_fwd16<64, false, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
-      HIP_LAUNCH_CHECK();
+  {
+    const int ax = axk16_ok(b);
+    if (ax >= 0) {
+      launch_axk16(b, ax, s);
       return;
     }
-    if (b.bf16 && SACMI_FWD_LDS16 && n128 && bh) hipLaunchKernelGGL((k_fwd16<128, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
-    else if (b.bf16 && SACMI_FWD_LDS16 && bh) hipLaunchKernelGGL((k_fwd16<64, true>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
-    else if (b.bf16 && SACMI_FWD_LDS16 && n128) hipLaunchKernelGGL((k_fwd16<128>), dim3(b.total_tiles), dim3(64 * fwd16_waves<128>()), 0, s, b);
-    else if (b.bf16 && SACMI_FWD_LDS16) hipLaunchKernelGGL((k_fwd16<64>), dim3(b.total_tiles), dim3(64 * fwd16_waves<64>()), 0, s, b);
-    else if (b.bf16 && n128) hipLaunchKernelGGL((k_fwd<true, 128>), dim3(b.total_tiles), dim3(256), 0, s, b);
-    else if (b.bf16) hipLaunchKernelGGL((k_fwd<true, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
-    else hipLaunchKernelGGL((k_fwd<false, 64>), dim3(b.total_tiles), dim3(256), 0, s, b);
-    HIP_LAUNCH_CHECK();
+  }
+  b = b0;
+  if (fwd_big_ok(b)) {
+    launch_fwd16(b, s);
     return;
   }
   b = b0;
   if (level_act16(b))
     throw Error{SACMI_ESTATE, "bf16 activation operands on a level outside the batch-4096-class kernels"};
-  const int extra0 = (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
-  // a fused-Adam level's scalar work: by default wave 0 of block 0 before its tile (-2);
-  // SACMI_B0_LATE=1: block 0 after its tile (-1, the round-3 form); SACMI_ADAM_WG=1: a
-  // workgroup of its own past the tiles and rides (measured: the 257th workgroup of L6 / L13
-  // waits for a free CU — L6 +0.85 us, L13 no faster)
-  static const bool adam_wg_on = std::getenv("SACMI_ADAM_WG") != nullptr && std::atoi(std::getenv("SACMI_ADAM_WG")) != 0;
-  static const bool b0_late = std::getenv("SACMI_B0_LATE") != nullptr && std::atoi(std::getenv("SACMI_B0_LATE")) != 0;
-  const bool awg = b.has_adam && adam_wg_on;
-  const int extra = extra0 + (awg ? 1 : 0);
-  b.adam_wg = b0_late ? -1 : -2;
-  auto set_awg = [&](int tiles) { if (awg) b.adam_wg = tiles + extra0; };
-  auto grid_for = [&](int tiles) { set_awg(tiles); return tiles + extra; };
+  // Polyak rides (RideAlong::pk) and the next update's sampler / gather run as extra
+  // workgroups past the tiles, on k_gemm's 1024-thread configurations
+  const int extra = (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
   if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > kRideLdsBytes)
     throw Error{SACMI_ESTATE, "ride-along sampler table exceeds k_gemm's LDS"};
-  int maxk = 0, n_adam = 0;
+  int n_adam = 0;
   int64_t outs = 0;
   for (int i = 0; i < b.count; ++i) {
-    maxk = b.d[i].K > maxk ? b.d[i].K : maxk;
     n_adam += b.d[i].epi >= EPI_ADAM;
     outs += (int64_t)b.d[i].M * b.d[i].N;
   }
@@ -4240,75 +2545,35 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   bool dw = true;
   for (int i = 0; i < b.count; ++i) dw = dw && !b.d[i].a_kc && !b.d[i].b_kc;
   const int t64 = assign_tiles<32, 64>(b);
-  // the batch-256 class on the LDS-staged core (same tile geometries as below)
-  if (staged_ok(b) && (dw || (!n_adam && t64 <= 512))) {
-    if (dw && t64 <= 256) {
-      if (n_adam) launch_ks<32, 64, 8, 1, true, 0>(b, grid_for(b.total_tiles), s);
-      else launch_ks<32, 64, 8, 1, false, 0>(b, grid_for(b.total_tiles), s);
-    } else if (dw) {
-      for (int i = 0; i < b.count; ++i)
-        if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a 64-row tile level"};
-      const int g = grid_for(assign_tiles<64, 64>(b));
-      if (n_adam) launch_ks<32, 64, 4, 2, true, 0>(b, g, s);
-      else launch_ks<32, 64, 4, 2, false, 0>(b, g, s);
-    } else if (axk == 1) {
-      const int g = grid_for(assign_tiles<32, 32>(b));
-      launch_ks<32, 32, 8, 1, false, 1>(b, g, s);
-    } else if (t64 >= 192) {
-      launch_ks<32, 64, 8, 1, false, 0>(b, grid_for(b.total_tiles), s);
-    } else {
-      const int g = grid_for(assign_tiles<32, 32>(b));
-      launch_ks<32, 32, 8, 1, false, 0>(b, g, s);
-    }
-    HIP_LAUNCH_CHECK();
-    return;
-  }
   if (dw && t64 <= 256) {
     // one 32x64 tile per CU (policy level): 16 waves, K split 16 ways
-    if (n_adam) launch_k<32, 64, 16, 1, 1, true, 0>(b, grid_for(b.total_tiles), s);
-    else launch_k<32, 64, 16, 1, 1, false, 0>(b, grid_for(b.total_tiles), s);
+    if (n_adam) launch_k<32, 64, 16, 1, 1, true, 0>(b, b.total_tiles + extra, s);
+    else launch_k<32, 64, 16, 1, 1, false, 0>(b, b.total_tiles + extra, s);
   } else if (dw || n_adam || t64 > 512) {
     // more 32x64 tiles than CUs (the twin critic weight gradients; every level at large
-    // batch): 64x64 tiles as two 32-row wave groups, each with an 8-way K split — half
-    // the operand bytes per FLOP of a 32x64 tile; the epilogue state is prefetched under
-    // the MFMAs
+    // batch): 64x64 tiles as two 32-row wave groups, each with a K split — half the operand
+    // bytes per FLOP of a 32x64 tile; the epilogue state is prefetched under the MFMAs.
     // 16 waves per CU either as one 1024-thread workgroup (8-way K split per wave group)
-    // or as several smaller ones (4- / 2-way): then one workgroup's LDS reduction and
-    // epilogue overlap another's operand loads and MFMAs.  Rides attach to 1024 threads.
-    const int g = grid_for(assign_tiles<64, 64>(b));
+    // or as two 512-thread ones (4-way): then one workgroup's LDS reduction and epilogue
+    // overlap the other's operand loads and MFMAs (the dh and forward levels; the
+    // weight-gradient levels keep the 8-way split).  Rides attach to 1024 threads.
+    const int g = assign_tiles<64, 64>(b) + extra;
     for (int i = 0; i < b.count; ++i)   // the two-wave-group tiles compute no dL/da partials
       if (b.d[i].pa_out) throw Error{SACMI_ESTATE, "dL/da partials requested on a 64-row tile level"};
-    if (n_adam) {
-      if (SACMI_DW_KS == 4 && !extra0) launch_k<32, 64, 4, 1, 2, true, 0>(b, g, s);
-      else launch_k<32, 64, 8, 1, 2, true, 0>(b, g, s);
-    } else if (axk == 1) {
-      if (SACMI_AXK_KS == 4 && !extra0) launch_k<32, 64, 4, 1, 2, false, 1>(b, g, s);
-      else launch_k<32, 64, 8, 1, 2, false, 1>(b, g, s);
-    } else if (dw) {
-      // the plain (data-parallel) form of a weight-gradient level: the fused form's geometry
-      if (SACMI_DW_KS == 4 && !extra0) launch_k<32, 64, 4, 1, 2, false, 0>(b, g, s);
-      else launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
-    } else if (!extra0 && SACMI_FWD_KS == 2) {
-      launch_k<32, 64, 2, 1, 2, false, 0>(b, g, s);
-    } else if (!extra0 && SACMI_FWD_KS == 4) {
-      launch_k<32, 64, 4, 1, 2, false, 0>(b, g, s);
-    } else {
-      launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
-    }
+    if (n_adam) launch_k<32, 64, 8, 1, 2, true, 0>(b, g, s);
+    else if (dw) launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);   // the plain (data-parallel) form
+    else if (axk == 1 && !extra) launch_k<32, 64, 4, 1, 2, false, 1>(b, g, s);
+    else if (axk == 1) launch_k<32, 64, 8, 1, 2, false, 1>(b, g, s);
+    else if (!extra) launch_k<32, 64, 4, 1, 2, false, 0>(b, g, s);
+    else launch_k<32, 64, 8, 1, 2, false, 0>(b, g, s);
   } else if (axk == 1) {
     // dh1 / dha1 with the fc3 backward folded in (A transform, coefficient in the epilogue)
-    const int g = grid_for(assign_tiles<32, 32>(b));
-    launch_k<32, 32, 16, 2, 1, false, 1>(b, g, s);
+    launch_k<32, 32, 16, 2, 1, false, 1>(b, assign_tiles<32, 32>(b) + extra, s);
   } else if (t64 >= 192) {
-    // widest tile that still gives one workgroup to most CUs (the folded-heads instantiation
-    // where the level carries the fold)
-    if (b.heads_ticket && !b.bf16)
-      hipLaunchKernelGGL((k_gemm<32, 64, 16, 2, 1, false, 0, false, 0, true>), dim3(grid_for(b.total_tiles)), dim3(1024), 0, s, b);
-    else
-      launch_k<32, 64, 16, 2, 1, false, 0>(b, grid_for(b.total_tiles), s);
+    // widest tile that still gives one workgroup to most CUs
+    launch_k<32, 64, 16, 2, 1, false, 0>(b, b.total_tiles + extra, s);
   } else {
-    const int g = grid_for(assign_tiles<32, 32>(b));
-    launch_k<32, 32, 16, 2, 1, false, 0>(b, g, s);
+    launch_k<32, 32, 16, 2, 1, false, 0>(b, assign_tiles<32, 32>(b) + extra, s);
   }
   HIP_LAUNCH_CHECK();
 }
@@ -4321,10 +2586,8 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
 // TM rows per workgroup (heads_rows_per_wg: 32 at the batch-4096 class — one workgroup
 // per CU covers all rows in one round and the head weights are re-read half as often)
 // rows [m0, m0 + TM) by one 64 * KSPLIT-thread workgroup; part: the row block's slot pair in
-// logp_part; red (KSPLIT * TM * (TN + 1) floats), lp, s_lp: LDS.  AAUX: cache-policy bits of
-// the h loads (k_gemm's folded form reads h rows other workgroups of the same launch wrote:
-// sc1, coherent across the XCDs' L2s)
-template <int TN, int KSPLIT, bool H16, int TM, int AAUX>
+// logp_part; red (KSPLIT * TM * (TN + 1) floats), lp, s_lp: LDS.
+template <int TN, int KSPLIT, bool H16, int TM>
 __device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int part, float* red,
                                            float (*lp)[33], float* s_lp) {
   const int A = a.A;
@@ -4346,7 +2609,7 @@ __device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int 
     eps_in = buf_ld(make_rsrc(want ? a.eps : a.Wh, want ? 0x7fffffffu : 0u),
                     (uint32_t)((size_t)mm * A + jj) * 4u);
   };
-  gemm_core_l<TM, TN, KSPLIT, 2, true, true, false, 1, 0, false, 0, H16, AAUX>(d, m0, 0, red, nullptr, pre);
+  gemm_core_l<TM, TN, KSPLIT, 2, true, true, false, 1, 0, false, H16>(d, m0, 0, red, nullptr, pre);
   __syncthreads();
   const uint64_t ctr = a.ctr_override ? a.ctr_override : a.sc->noise_counter;
   if (e < TM * A) {
@@ -4354,11 +2617,11 @@ __device__ __forceinline__ void heads_rows(const HeadSampleArgs& a, int m0, int 
     if (live) {
       const float mean = reduce_partials<TM, TN, KSPLIT>(red, row, j) + bm;
       const float ls_raw = reduce_partials<TM, TN, KSPLIT>(red, row, A + j) + bl;
-      lpe = heads_elem<H16, AAUX>(a, m, j, mean, ls_raw, eps_in, ctr);
+      lpe = heads_elem<H16>(a, m, j, mean, ls_raw, eps_in, ctr);
     }
     lp[row][j] = lpe;
   }
-  heads_logp<TM, AAUX>(a, m0, part, lp, s_lp);
+  heads_logp<TM>(a, m0, part, lp, s_lp);
 }
 
 template <int TN, int KSPLIT, bool H16 = false, int TM = 16>
@@ -4367,7 +2630,7 @@ __global__ __launch_bounds__(64 * KSPLIT) void k_heads_sample(HeadSampleArgs a) 
   __shared__ float red[KSPLIT * TM * (TN + 1)];
   __shared__ float lp[TM][33];
   __shared__ float s_lp[TM];
-  heads_rows<TN, KSPLIT, H16, TM, 0>(a, blockIdx.x * TM, blockIdx.x, red, lp, s_lp);
+  heads_rows<TN, KSPLIT, H16, TM>(a, blockIdx.x * TM, blockIdx.x, red, lp, s_lp);
   if (a.done_word) {   // (one workgroup) every store above lands first
     __threadfence_system();
     __syncthreads();
@@ -4600,12 +2863,10 @@ struct TailSmem {
   float s_w[64][kTailCols + 1];        // Whead[k][slab columns], k < 2A
 };
 // One unit: rows [m0, m0 + 8) x dhp2 columns [c0, c0 + 64), by the first 256 threads of the
-// workgroup (any others only join its barriers).  slab0: the unit also stores dhead.  AUX:
-// cache-policy bits of the dL/da partial loads (k_chain: sc1 — L9 wrote them in the same launch)
-template <int AUX, bool MIDSPLIT = false, int NPA = kTailMaxPa, class Mid = void (*)()>
+// workgroup (any others only join its barriers).  slab0: the unit also stores dhead.
+template <int NPA = kTailMaxPa>
 __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const SampleBwdArgs& a, int m0,
-                                          int c0, bool slab0, TailSmem& sm, Mid&& mid = [] {}) {
-  if constexpr (MIDSPLIT) mid.issue();   // (k_chain: the barrier's first poll, as kg_body's)
+                                          int c0, bool slab0, TailSmem& sm) {
   auto& s_dh = sm.s_dh;
   auto& s_w = sm.s_w;
   const int A = a.A, B = a.B, K2 = 2 * A;
@@ -4642,10 +2903,7 @@ __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const Sampl
       mk[u] = buf_ld(rH, act && m < B && col < a.H ? (uint32_t)(m * a.ldh + col) * 4u : 0xfffffff0u);
     }
   };
-  // the dL/da partials the previous phase wrote: after mid() (k_chain's barrier; a no-op in
-  // the standalone kernel, whose loads all went out above)
   preload();
-  mid();
   const rsrc_t rP = make_rsrc(pa, (uint32_t)((size_t)n_pa * B * A * 4));
   const uint32_t pstride = (uint32_t)B * (uint32_t)A * 4u, po = (uint32_t)((own ? pm : 0) * A + pj) * 4u;
   // (NPA >= n_pa partial loads per thread: the launcher picks the smallest instantiation, so
@@ -4653,7 +2911,7 @@ __device__ __forceinline__ void tail_unit(const float* pa, int n_pa, const Sampl
   float t[NPA];
 #pragma unroll
   for (int q = 0; q < NPA; ++q)
-    t[q] = buf_ld_aux<AUX>(rP, own && q < n_pa ? po + (uint32_t)q * pstride : 0xfffffff0u);
+    t[q] = buf_ld(rP, own && q < n_pa ? po + (uint32_t)q * pstride : 0xfffffff0u);
   if (act) {
     for (int e = tid; e < kTailRows * 65; e += 256) (&s_dh[0][0])[e] = 0.f;
 #pragma unroll
@@ -4712,7 +2970,7 @@ template <int NPA>
 __global__ __launch_bounds__(256) void k_sample_bwd_tail(const float* pa, int n_pa, SampleBwdArgs a) {
   const TlMark tl_mark(a.tl, TL_SAMPLE_TAIL);
   __shared__ TailSmem sm;
-  tail_unit<0, false, NPA>(pa, n_pa, a, blockIdx.x * kTailRows, blockIdx.y * kTailCols, blockIdx.y == 0, sm);
+  tail_unit<NPA>(pa, n_pa, a, blockIdx.x * kTailRows, blockIdx.y * kTailCols, blockIdx.y == 0, sm);
 }
 
 void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, hipStream_t s) {
@@ -4726,324 +2984,15 @@ void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, h
   HIP_LAUNCH_CHECK();
 }
 
-// ---------------------------------------------------------------------------
-// k_chain: the batch-256-class actor pass as one persistent launch (sacmi_internal.h
-// ChainArgs).  256 workgroups of 1024 threads, one per CU; cohort c = blockIdx % 8 owns batch
-// rows [c B/8, (c+1) B/8) in every phase (row-affine tile placement: chain_assign_tiles), so
-// each phase waits only for its own cohort's previous phase.
-constexpr long long kChainSpinTicks = 5000000;   // 50 ms of the 100 MHz clock: a barrier timeout
-
-// Cohort barriers (cdna_hip_programming.md §6 Guideline 16, MI355X_MICROARCH.md hand-off table
-// row 1).  Per cohort, 128-byte strided words: [0, kChainBars) the arrivals at barrier b,
-// kChainBars the launch ticket — monotonic and wrapping: every launch adds exactly `nmem` to
-// each, so launch e's barrier b is complete once its word reaches (e + 1) nmem, e read from the
-// ticket each workgroup draws at its start (nothing is ever reset).
-//   chain_end   every wave's write-through stores acknowledged (vmcnt(0)), a workgroup
-//               barrier, then ONE agent-scope add on the phase's barrier word (non-returning)
-//   ChainWait   the next phase's wait on it: issue() — thread 0's first poll load, at the
-//               very start of the phase body, ahead of its weight loads (vmcnt is in order:
-//               the poll's value then does not wait for them) — and operator() after the
-//               weight loads (kg_body / tail_unit MIDSPLIT hook): further polls (relaxed sc1
-//               loads + s_sleep) until the cohort has arrived, then a workgroup barrier; every
-//               later load of handed-off bytes is an sc1 load (LDAUX = sc1).  A bounded spin:
-//               a timeout sets ERR_CHAIN_TIMEOUT (the host reports a device error) and the
-//               workgroup runs on — void outputs, no hang.
-__device__ __forceinline__ void chain_end(int* cnt) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-struct ChainWait {
-  int* cnt;
-  int target;
-  int* err;
-  bool wait;
-  tl_word* tl;
-  int slot;
-  int v;
-  __device__ __forceinline__ void issue() {
-    if (threadIdx.x == 0 && wait) v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  __device__ __forceinline__ void operator()() {
-    if (threadIdx.x == 0 && wait && (int)((unsigned)v - (unsigned)target) < 0) {
-      const unsigned long long t0 = wall_clock64();
-      while ((int)((unsigned)__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (unsigned)target) < 0) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((long long)(wall_clock64() - t0) > kChainSpinTicks) {
-          __hip_atomic_fetch_or(err, (int)ERR_CHAIN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    SACMI_PHASE(tl, slot);
-  }
-};
-// the launch's completion target of every barrier word (thread 0 only: the others never wait)
-__device__ __forceinline__ int chain_target(int* ticket, int nmem) {
-  if (threadIdx.x != 0) return 0;
-  const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (int)(((unsigned)t & ~(unsigned)(nmem - 1)) + (unsigned)nmem);
-}
-
-using ChainKgA = KgSmem<32, 32, 16, 2, 1, false, 0, false, 0>;   // L7, L8, L12 (+ rides)
-using ChainKgB = KgSmem<32, 32, 16, 2, 1, false, 1, false, 0>;   // L9 (row prologue, dL/da)
-union ChainSmem {
-  ChainKgA a;
-  ChainKgB b;
-  TailSmem t;
-};
-
-// The argument block is read through the CONSTANT address space: invariant scalar loads, as
-// k_gemm's kernel argument (a generic pointer's loads behind the barriers' memory clobbers
-// would be vector loads into VGPRs); the generic pointer handed to kg_body is the cast of it,
-// which InferAddressSpaces folds back.  Each phase reads it through an opaque copy, so no
-// phase's argument loads are hoisted into an earlier one (registers held across it: spills).
-typedef __attribute__((address_space(4))) const ChainArgs ConstChainArgs;
-__device__ __forceinline__ const ChainArgs* chain_args(const ChainArgs* ca) {
-  ConstChainArgs* p4 = (ConstChainArgs*)ca;
-  asm volatile("" : "+s"(p4));
-  return (const ChainArgs*)p4;
-}
-
-// Each phase's weights (and descriptor setup) go out BEFORE the cohort barrier on the
-// previous phase (kg_body / tail_unit MIDSPLIT: the barrier is their mid() hook), so their
-// latency overlaps the wait.  (diagnostic builds, SACMI_DIAG_PHASES: wave 0's clock at entry
-// (slot 0), at the end of phase i (slot i + 1) and right after barrier b's wait (slot 6 + b);
-// tools/phase_dump.py)
-__global__ __launch_bounds__(1024, 4) void k_chain(const ChainArgs* __restrict__ ca, tl_word* tl) {
-  const TlMark tl_mark(tl, TL_CHAIN);
-  __shared__ ChainSmem sm;
-  SACMI_PHASE(tl, 0);
-  const int c = blockIdx.x & (kChainCohorts - 1), bid = blockIdx.x;
-  const int nmem = gridDim.x / kChainCohorts;
-  int* const sync = chain_args(ca)->sync + c * (kChainBars + 1) * 32;
-  int* const err = chain_args(ca)->err;
-  const int target = chain_target(sync + kChainBars * 32, nmem);
-  auto waiter = [&](int b, bool w) { return ChainWait{sync + b * 32, target, err, w, tl, 6 + b, 0}; };
-  // L7 (updated critics fc1 on [s|1|a~])
-  {
-    const GemmBatch& b = chain_args(ca)->lv[0];
-    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1>(b, bid, sm.a);
-    chain_end(sync);
-    SACMI_PHASE(tl, 1);
-  }
-  // L8 (fc2 + fc3 dot partials): barrier 0 behind its weight loads
-  {
-    const GemmBatch& b = chain_args(ca)->lv[1];
-    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, waiter(0, true));
-    chain_end(sync + 32);
-    SACMI_PHASE(tl, 2);
-  }
-  // L9: the actor row prologue + dha1 + the dL/da partials
-  {
-    const GemmBatch& b = chain_args(ca)->lv[2];
-    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1, true>(b, bid, sm.b, waiter(1, true));
-    chain_end(sync + 64);
-    SACMI_PHASE(tl, 3);
-  }
-  // the sample-backward tail: the cohort's 8-row groups x 64-column dhp2 slabs
-  {
-    const ChainArgs* q = chain_args(ca);
-    const int ng = q->tail_groups, units = ng * q->tail_slabs;
-    const int j = bid / kChainCohorts;
-    if (j < units) {
-      const int g = j % ng, slab = j / ng;
-      tail_unit<kLdSc1, true>(q->pa, q->n_pa, q->tail, c * q->rows_per_cohort + g * kTailRows,
-                              slab * kTailCols, slab == 0, sm.t, waiter(2, true));
-    }
-    chain_end(sync + 96);
-    SACMI_PHASE(tl, 4);
-  }
-  // L12 (dhp1) + the level's rides (the next update's sampler, Polyak): a workgroup whose
-  // item is a ride reads nothing of the chain — it does not wait
-  {
-    const GemmBatch& b = chain_args(ca)->lv[3];
-    const int items = b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
-    if (bid < items)
-      kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, waiter(3, bid < b.total_tiles));
-    SACMI_PHASE(tl, 5);
-  }
-}
-
-// the critic pass (ChainArgs kind 1): L1 / L2 on 32x64 tiles (L2 with the policy heads
-// folded in), L3 / L4 on 32x32, L5 (row prologue, A transform) on 32x32
-using ChainKgW = KgSmem<32, 64, 16, 2, 1, false, 0, false, 0, true>;   // (L2 carries the heads)
-union ChainSmemA {
-  ChainKgW w;
-  ChainKgA a;
-  ChainKgB b;
-};
-
-__global__ __launch_bounds__(1024, 4) void k_chain_a(const ChainArgs* __restrict__ ca, tl_word* tl) {
-  const TlMark tl_mark(tl, TL_CHAIN_A);
-  __shared__ ChainSmemA sm;
-  SACMI_PHASE(tl, 0);   // (diagnostic builds: as k_chain's)
-  const int c = blockIdx.x & (kChainCohorts - 1), bid = blockIdx.x;
-  const int nmem = gridDim.x / kChainCohorts;
-  int* const sync = chain_args(ca)->sync + c * (kChainBars + 1) * 32;
-  int* const err = chain_args(ca)->err;
-  const int target = chain_target(sync + kChainBars * 32, nmem);
-  auto waiter = [&](int b, bool w) { return ChainWait{sync + b * 32, target, err, w, tl, 6 + b, 0}; };
-  // L1: 32x64 tiles
-  {
-    const GemmBatch& b = chain_args(ca)->lv[0];
-    if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1, false, true>(b, bid, sm.w);
-    chain_end(sync);
-    SACMI_PHASE(tl, 1);
-  }
-  // L2 (+ the heads): 32x64 tiles, barrier 0 behind its weight loads
-  {
-    const GemmBatch& b = chain_args(ca)->lv[1];
-    if (bid < b.total_tiles) kg_body<32, 64, 16, 2, 1, false, 0, false, 0, kLdSc1, true, true>(b, bid, sm.w, waiter(0, true));
-    chain_end(sync + 32);
-    SACMI_PHASE(tl, 2);
-  }
-  // L3, L4 (target critics): 32x32 tiles
-#pragma unroll 1
-  for (int i = 2; i < 4; ++i) {
-    const GemmBatch& b = chain_args(ca)->lv[i];
-    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 0, false, 0, kLdSc1, true>(b, bid, sm.a, waiter(i - 1, true));
-    chain_end(sync + 32 * i);
-    SACMI_PHASE(tl, i + 1);
-  }
-  // L5: the critic row prologue (targets, MSE gradients, loss partials) + dh1
-  {
-    const GemmBatch& b = chain_args(ca)->lv[4];
-    if (bid < b.total_tiles) kg_body<32, 32, 16, 2, 1, false, 1, false, 0, kLdSc1, true>(b, bid, sm.b, waiter(3, true));
-    SACMI_PHASE(tl, 5);
-  }
-}
-
-// 32x32 (TN = 64: 32x64) tiles, XCD-blocked with a row grid of 8: tile t of a desc -> row
-// tile (t & 7) * tm / 8 + q, so workgroup b (b & 7 = cohort) only ever touches its cohort's rows
-bool chain_assign_tiles(GemmBatch& b, int tn) {
-  if (tn == 64) assign_tiles<32, 64>(b);
-  else assign_tiles<32, 32>(b);
-  for (int i = 0; i < b.count; ++i) {
-    GemmDesc& d = b.d[i];
-    if (d.tiles_m % kChainCohorts || d.tile_begin % kChainCohorts) return false;
-    d.xcd_gr = kChainCohorts;
-    d.pl_div = d.tiles_n;
-    d.pl_gc_log2 = 0;
-    d.pl_sr = d.tiles_m / kChainCohorts;
-    d.pl_mag = d.pl_div == 1 ? 0u : (unsigned)((((uint64_t)1 << 32) + d.pl_div - 1) / d.pl_div);
-  }
-  return true;
-}
-
-// The grid must be resident at once (its cohorts wait for each other): one workgroup per CU
-// on at least 256 CUs
-bool chain_supported() {
-  static int ok_dev[64] = {};   // 0 unknown, 1 yes, 2 no
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-  if (!ok_dev[dev]) {
-    hipDeviceProp_t prop;
-    int per_cu = 0;
-    int per_cu_a = 0;
-    const bool ok = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount >= kChainGrid &&
-                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_chain, 1024, 0) == hipSuccess &&
-                    per_cu >= 1 &&
-                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_a, k_chain_a, 1024, 0) == hipSuccess &&
-                    per_cu_a >= 1;
-    ok_dev[dev] = ok ? 1 : 2;
-  }
-  return ok_dev[dev] == 1;
-}
-
-bool chain_a_l2_ok(const GemmBatch& b) {
-  return gemm_level_heads_fold_ok(b, b.heads.A);
-}
-
-bool launch_chain(const ChainArgs& h, const ChainArgs* dev, tl_word* tl, hipStream_t s) {
-  if (!chain_supported()) return false;
-  if (h.kind == 1) {
-    // the critic pass: fp32 k_gemm bodies, L1 / L2 32x64 (L2 may fold the heads), L3 / L4
-    // 32x32, L5 32x32 with the critic row prologue; no Adam, rides, split-K, bf16
-    for (int i = 0; i < kChainLevels; ++i) {
-      const GemmBatch& b = h.lv[i];
-      if (b.count < 1 || b.bf16 || b.has_adam || b.err_flags || !b.st_wt || b.ride.kind || b.ride.pk_blocks ||
-          (b.heads_ticket && i != 1) || b.total_tiles > kChainGrid)
-        throw Error{SACMI_ESTATE, "k_chain_a: unsupported level configuration"};
-      if (b.heads_ticket && b.heads.A * 2 > 48) throw Error{SACMI_ESTATE, "k_chain_a: heads wider than 48"};
-      for (int q = 0; q < b.count; ++q) {
-        const GemmDesc& d = b.d[q];
-        if (d.axk != (i == 4 ? 1 : 0) || d.epi >= EPI_ADAM || d.a16 || d.b16 || d.c16 || d.x16 || d.pa_out ||
-            d.xcd_gr != kChainCohorts || d.tiles_m % kChainCohorts || d.M != h.rows_per_cohort * kChainCohorts)
-          throw Error{SACMI_ESTATE, "k_chain_a: unsupported GEMM in a chain level"};
-        if (d.K > kChainMaxK) throw Error{SACMI_ESTATE, "k_chain_a: K beyond one pass"};
-        if (d.tiles_n * (i < 2 ? 64 : 32) < d.N || (i < 2 && d.tiles_n * 32 >= d.N && d.N > 32))
-          throw Error{SACMI_ESTATE, "k_chain_a: a level's tiles differ from the kernel's"};
-      }
-    }
-    hipLaunchKernelGGL(k_chain_a, dim3(kChainGrid), dim3(1024), 0, s, dev, tl);
-    HIP_LAUNCH_CHECK();
-    return true;
-  }
-  // the configuration k_chain instantiates: fp32 32x32 k_gemm tiles (L9 with the A transform
-  // and the dL/da partials), no fused Adam, no split-K / bf16 activations, rides on L12 only
-  if (h.kind != 0) throw Error{SACMI_ESTATE, "k_chain: unknown chain kind"};
-  for (int i = 0; i < 4; ++i) {
-    const GemmBatch& b = h.lv[i];
-    if (b.count < 1 || b.bf16 || b.has_adam || b.heads_ticket || b.err_flags || !b.st_wt)
-      throw Error{SACMI_ESTATE, "k_chain: unsupported level configuration"};
-    if ((b.ride.kind || b.ride.pk_blocks) && i != 3) throw Error{SACMI_ESTATE, "k_chain: rides outside L12"};
-    if (b.ride.kind == 1 && mt_sample_lds_words(b.ride.tbl_log2, b.ride.mt.setsize) * 4 > kRideLdsBytes)
-      throw Error{SACMI_ESTATE, "k_chain: ride-along sampler table exceeds the LDS"};
-    for (int q = 0; q < b.count; ++q) {
-      const GemmDesc& d = b.d[q];
-      if (d.axk != (i == 2 ? 1 : 0) || d.epi >= EPI_ADAM || d.a16 || d.b16 || d.c16 || d.x16 ||
-          d.xcd_gr != kChainCohorts || d.tiles_m % kChainCohorts || (d.pa_out && i != 2))
-        throw Error{SACMI_ESTATE, "k_chain: unsupported GEMM in a chain level"};
-      if (d.M != h.rows_per_cohort * kChainCohorts)
-        throw Error{SACMI_ESTATE, "k_chain: a level's rows differ from the chain's batch"};
-      if (d.K > kChainMaxK) throw Error{SACMI_ESTATE, "k_chain: K beyond one pass"};
-    }
-  }
-  const SampleBwdArgs& a = h.tail;
-  if (2 * a.A > 64 || kTailRows * a.A > 256 || h.n_pa > kTailMaxPa || a.hp2_16 || a.B != h.rows_per_cohort * kChainCohorts ||
-      h.rows_per_cohort % kTailRows || h.tail_groups != h.rows_per_cohort / kTailRows ||
-      h.tail_slabs != (a.H + kTailCols - 1) / kTailCols)
-    throw Error{SACMI_ESTATE, "k_chain: unsupported sample-backward tail"};
-  hipLaunchKernelGGL(k_chain, dim3(kChainGrid), dim3(1024), 0, s, dev, tl);
-  HIP_LAUNCH_CHECK();
-  return true;
-}
-
 bool gemm_level_on_axk16(const GemmBatch& b0) {
   GemmBatch b = b0;
-  return SACMI_AXK_LDS16 && axk16_ok(b) >= 0;
-}
-
-// whether launch_gemm takes this forward level on <32, 64, 16, 2, 1> fp32 tiles with
-// write-through stores: the configuration that folds the policy heads (GemmBatch::heads)
-bool gemm_level_heads_fold_ok(const GemmBatch& b0, int A) {
-  if (b0.bf16 || b0.count < 1 || 2 * A > 48 || A < 1) return false;
-  GemmBatch b = b0;
-  if (staged_ok(b) || fwd_big_ok(b)) return false;
-  bool dw = true;
-  int axk = 0, n_adam = 0;
-  int64_t outs = 0;
-  for (int i = 0; i < b.count; ++i) {
-    const GemmDesc& d = b.d[i];
-    dw = dw && !d.a_kc && !d.b_kc;
-    axk = d.axk > axk ? d.axk : axk;
-    n_adam += d.epi >= EPI_ADAM;
-    outs += (int64_t)d.M * d.N;
-    if (d.a16 || d.b16 || d.c16 || d.x16) return false;
-    if (d.N > 1024) return false;   // (at most 16 column tiles' shares per row block)
-  }
-  const int t64 = assign_tiles<32, 64>(b);
-  // launch_gemm's <32, 64, 16, 2, 1> branch, with write-through stores (st_wt: outs <= 1 M)
-  return !dw && !n_adam && !axk && t64 >= 192 && t64 <= 512 && outs <= (1 << 20);
+  return axk16_ok(b) >= 0;
 }
 
 // launch_gemm's own kernel choice for an axk-1 level, asked ahead of its launch: true when
 // it runs on the one-wave-group k_gemm tiles (<32, 32, 16, 2, 1, false, 1>: MG == 1, AXK ==
-// 1), the only form that computes dL/da partials.  Mirrors launch_gemm's order: split-K and
-// the LDS-staged forward kernels never take an axk level; k_axk16 (bf16, batch-4096 class);
+// 1), the only form that computes dL/da partials.  Mirrors launch_gemm's order: the split-K
+// and the bf16 forward kernels never take an axk level; k_axk16 (bf16, batch-4096 class);
 // then the 64-row-tile branch (more than 512 32x64 tiles, e.g. batch 1024 with hidden > 512)
 bool gemm_level_pa_capable(const GemmBatch& b0) {
   if (gemm_level_on_axk16(b0)) return false;

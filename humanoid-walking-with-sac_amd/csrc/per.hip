@@ -611,16 +611,12 @@ __global__ void k_per_f2b(PerArgs a) {
   for (int64_t j = 0; j < len; ++j) a.cdf[j] = a.cdf[j] / last;
 }
 
-#ifndef SACMI_PER_F4
-#define SACMI_PER_F4 1          // w /= max(w) in its own kernel (0: F3 last workgroup, fence + counter: 5 us slower)
-#endif
 __global__ __launch_bounds__(256) void k_per_f3(PerArgs a) {
 #pragma clang fp contract(off)
   const TlMark tl_mark(a.tl, TL_PER_F3);
   extern __shared__ int64_t off[];       // [nb] exclusive prefix of the block totals
   __shared__ double top[kTopMax];
   __shared__ int64_t wtot[4];
-  __shared__ int s_last;
   const bool bad = __atomic_load_n(a.bad, __ATOMIC_RELAXED) != 0;
   const int64_t len = per_len(a);
   const int nb = (int)((len + kScanBlock - 1) / kScanBlock);
@@ -681,19 +677,8 @@ __global__ __launch_bounds__(256) void k_per_f3(PerArgs a) {
   for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
   unsigned int* wmax = reinterpret_cast<unsigned int*>(a.bad + 1);
   if ((threadIdx.x & 63) == 0) atomicMax(wmax, m);
-#if SACMI_PER_F4
-  return;            // w /= max(w) in k_per_f4 (the kernel boundary orders the atomics)
-#endif
-  // last workgroup: w /= max(w)
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(a.bad + 3, 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  const float mx = __uint_as_float(__atomic_load_n(wmax, __ATOMIC_RELAXED));
-  for (int i = threadIdx.x; i < a.k; i += blockDim.x)
-    a.w_out[i] = __builtin_nontemporal_load(a.w_out + i) / mx;
+  // w /= max(w) in k_per_f4 (the kernel boundary orders the atomics; a last-workgroup
+  // fence + counter here measured 5 us slower)
 }
 
 __global__ void k_per_f4(PerArgs a) {
@@ -722,7 +707,7 @@ void launch_per_sample(const PerArgs& a, hipStream_t s) {
     const size_t lds3 = (size_t)nb0 * 8;
     ensure_dyn_lds(reinterpret_cast<const void*>(&k_per_f3), lds3);
     hipLaunchKernelGGL(k_per_f3, dim3((a.k + 255) / 256), dim3(256), lds3, s, at(3));
-    if (SACMI_PER_F4) hipLaunchKernelGGL(k_per_f4, dim3((a.k + 255) / 256), dim3(256), 0, s, at(4));
+    hipLaunchKernelGGL(k_per_f4, dim3((a.k + 255) / 256), dim3(256), 0, s, at(4));
     launch_check("PER sample (fused)");
     return;
   }

@@ -217,13 +217,10 @@ struct sacmi_ctx {
   sacmi::DevBuf<float> dw_ws;      // bf16 deep-K weight-gradient split-K partials
   int nparts = 0;
   sacmi::DevBuf<float> lpart_c, lpart_a, ring, lp_part;
+  // the sharded data-parallel form's error flags (kDpFlagN): a buffer of their own, outside
+  // the critic reduce-scatter's reach (the all-reduce form carries them at G + q_end)
+  sacmi::DevBuf<float> dp_flags;
   int ring_slots = 0;
-  // policy heads folded into the last policy hidden layer's level (GemmBatch::heads): the
-  // arrival counts per 32-row block (zero between launches), and the batch size whose
-  // update folds them (the actor phase sizes its log-prob partials from it)
-  sacmi::DevBuf<int> heads_ticket;
-  sacmi::DevBuf<float> heads_part;   // the folded heads' split-K shares (GemmBatch::heads_part)
-  int heads_fold_B = -1;
   // act scratch
   int act_rows = 0;
   sacmi::DevBuf<float> ax, ah1, ah2, aeps, acache, alogp, aout;
@@ -271,17 +268,6 @@ struct sacmi_ctx {
   sacmi::DevBuf<int32_t> per_owner, per_bad;
   std::map<sacmi::GraphKey, hipGraphExec_t> graphs;
   bool use_graphs = true;
-  // the persistent actor-pass chain (k_chain, sacmi_internal.h ChainArgs): its argument blocks
-  // live in a device pool (larger than a kernel argument); a block registered while a graph is
-  // being captured (own_capture) is uploaded once the capture has ended (chain_flush), before
-  // that graph's first launch.  Blocks are immutable and deduplicated by content.
-  static constexpr int kChainSlots = 48;
-  bool own_capture = false;
-  bool chain_on = false;                     // SACMI_CHAIN at creation: on
-  sacmi::DevBuf<unsigned char> chain_pool;   // kChainSlots x sizeof(ChainArgs)
-  std::vector<std::vector<unsigned char>> chain_host;
-  size_t chain_uploaded = 0;                 // slots [0, chain_uploaded) are on the device
-  sacmi::DevBuf<int> chain_sync;             // cohort barrier words (kChainSyncInts)
   bool G_external = false;
   // native data parallel (sacmi_allreduce_init / sacmi_step_dp)
   ncclComm_t comm = nullptr;
@@ -293,8 +279,13 @@ struct sacmi_ctx {
   bool dp_shard = false;
   bool dp_sharding_now = false;   // enqueue_dp is enqueueing a sharded sequence
   // a sharded step ran at world >= 2: each rank's Adam moments are current on its own chunks
-  // only — reading them (tensors, checkpoints) raises until sacmi_dp_sync_state gathers them
+  // only — reading them (tensors, checkpoints) or stepping them (any non-sharded update)
+  // raises until sacmi_dp_sync_state gathers them
   bool moments_sharded = false;
+  // a loopback one-rank timing run (SACMI_DP_LOOPBACK_ONE_RANK) stepped rank 0's chunks
+  // only: the other chunks' moments (and parameters) were never stepped, and no collective
+  // can repair that — the moments stay unreadable for the context's lifetime
+  bool moments_partial = false;
   std::map<std::tuple<int, int, int64_t>, hipGraphExec_t> dp_graphs;   // (batch, n, PER fill)
   uint64_t act_calls = 0;   // gradient arena owned by the caller (sacmi_attach_grad_arena)
   // profiling (sacmi_profile_step): one event per launch site
@@ -336,50 +327,25 @@ static void destroy_graphs(sacmi_ctx* c) {
   c->graphs.clear();
   for (auto& kv : c->dp_graphs) (void)hipGraphExecDestroy(kv.second);
   c->dp_graphs.clear();
-  // no graph refers to a chain block any more (every caller has drained the stream)
-  c->chain_host.clear();
-  c->chain_uploaded = 0;
-}
-
-// The device copy of a chain argument block: an existing slot with the same bytes, or a new
-// one (uploaded by chain_flush after the capture); null when the pool is full
-static const ChainArgs* chain_slot(sacmi_ctx* c, const ChainArgs& a) {
-  const unsigned char* bytes = reinterpret_cast<const unsigned char*>(&a);
-  for (size_t i = 0; i < c->chain_host.size(); ++i)
-    if (std::memcmp(c->chain_host[i].data(), bytes, sizeof(ChainArgs)) == 0)
-      return reinterpret_cast<const ChainArgs*>(c->chain_pool.p + i * sizeof(ChainArgs));
-  if (c->chain_host.size() >= (size_t)sacmi_ctx::kChainSlots) return nullptr;
-  c->chain_host.emplace_back(bytes, bytes + sizeof(ChainArgs));
-  return reinterpret_cast<const ChainArgs*>(c->chain_pool.p + (c->chain_host.size() - 1) * sizeof(ChainArgs));
-}
-static void chain_flush(sacmi_ctx* c) {
-  for (size_t i = c->chain_uploaded; i < c->chain_host.size(); ++i)
-    CHECK_HIP(hipMemcpy(c->chain_pool.p + i * sizeof(ChainArgs), c->chain_host[i].data(), sizeof(ChainArgs),
-                        hipMemcpyHostToDevice));
-  c->chain_uploaded = c->chain_host.size();
 }
 
 // Capture whatever `body` enqueues on the context stream into an instantiated graph (thread-
-// local capture mode); chain blocks registered meanwhile are uploaded before it returns
+// local capture mode)
 template <class F>
 static hipGraphExec_t capture_graph(sacmi_ctx* c, F&& body) {
   hipGraph_t g;
   CHECK_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-  c->own_capture = true;
   try {
     body();
   } catch (...) {
-    c->own_capture = false;
     (void)hipStreamEndCapture(c->stream, &g);
     throw;
   }
-  c->own_capture = false;
   CHECK_HIP(hipStreamEndCapture(c->stream, &g));
   hipGraphExec_t ex;
   const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   CHECK_HIP(e);
-  chain_flush(c);
   return ex;
 }
 
@@ -388,8 +354,7 @@ static void build_layout(sacmi_ctx* c) {
   const int S = c->S, A = c->A, H = c->H;
   // bf16 mode: rows of 8-element multiples, so every bf16 activation / weight-shadow row
   // starts 16-byte aligned (k_fwd16p's LDS-DMA moves 16-byte chunks)
-  int pad = c->bf16 ? 8 : 4;
-  if (c->bf16 && std::getenv("SACMI_ROW_PAD")) pad = std::max(8, std::atoi(std::getenv("SACMI_ROW_PAD")) / 8 * 8);
+  const int pad = c->bf16 ? 8 : 4;
   c->Kx = round_up(S + 1 + A, pad);
   c->Hd = round_up(H + 1, pad);
   c->Kp1 = round_up(S + 1, pad);
@@ -493,7 +458,7 @@ static void alloc_all(sacmi_ctx* c) {
     c->hp[l].alloc((size_t)2 * Bm * c->Hd);
     for (auto* b : {&c->hq[l], &c->hqt[l], &c->hqa[l]}) b->alloc((size_t)Bm * 2 * c->Hd);
     c->dhc[l].alloc((size_t)Bm * 2 * H);
-    c->dha[l].alloc((size_t)Bm * 2 * H);   // (dha[L]: the actor pass's u rows, L8's u_out)
+    c->dha[l].alloc((size_t)Bm * 2 * H);
     c->dhp[l].alloc((size_t)Bm * H);
   }
   c->eps.alloc((size_t)2 * Bm * A);
@@ -511,8 +476,7 @@ static void alloc_all(sacmi_ctx* c) {
   const int nrb = (Bm + 31) / 32;    // row blocks of the L5 / L9 tiling (loss partials)
   c->lpart_c.alloc((size_t)nrb * 2); c->lpart_a.alloc(nrb);
   c->lp_part.alloc((size_t)2 * ((2 * Bm + 15) / 16) + 2);   // heads: per-workgroup logp sums
-  c->heads_ticket.alloc((size_t)(2 * Bm + kHeadsFoldTM - 1) / kHeadsFoldTM);
-  c->heads_part.alloc((size_t)(2 * Bm + kHeadsFoldTM - 1) / kHeadsFoldTM * ((c->H + 63) / 64) * kHeadsFoldTM * 2 * c->A);
+  c->dp_flags.alloc(kDpFlagN);
   hipStream_t s = c->stream;
   // constant-1 (bias) columns
   set_column_checked(c->xq.p, Bm, c->Kx, S, 1.f, s);
@@ -667,10 +631,7 @@ static void validate(const GemmDesc& d) {
   } else {
     // MN-contiguous operands are read 4 columns wide from a 4-aligned start (the split-K
     // dW kernels): the span covers the last such group
-    // (bf16 MN-contiguous A: the split-K dW kernel's transformed operand, axk 2 — 4
-    // elements = 8 bytes at a time)
-    REQUIRE(!d.a16 || d.axk == 2, SACMI_ESTATE, "bf16 A operands are K-contiguous");
-    if (d.a16 && (((uintptr_t)d.A & 7) || (d.lda & 3))) throw Error{SACMI_ESTATE, "A misaligned"};
+    REQUIRE(!d.a16, SACMI_ESTATE, "bf16 A operands are K-contiguous");
     check_span(d.A, (int64_t)(d.K - 1) * d.lda + ((d.M - 1) & ~3) + 3, "A", ea);
   }
   if (d.b_kc) {
@@ -686,16 +647,8 @@ static void validate(const GemmDesc& d) {
   if (d.C) check_span(d.C, (int64_t)(d.M - 1) * d.ldc + std::max(d.N - 1, d.rs_col), "C", ec);
   if (d.bias) check_span(d.bias, (int64_t)(d.N - 1) * d.bias_ld, "bias");
   REQUIRE(!(d.bias && d.epi == EPI_MASK), SACMI_ESTATE, "GEMM epilogue: bias and mask are exclusive");
-  if (d.u_out) {
-    REQUIRE(d.dotp && !d.c16 && d.epi == EPI_RELU, SACMI_ESTATE, "u rows come from an fp32 forward level with dot partials");
-    check_span(d.u_out, (int64_t)(d.M - 1) * d.u_ld + d.N - 1, "u_out");
-  }
-  if (d.ax_pre) REQUIRE(d.axk == 1 && !d.ax_out && !d.a16, SACMI_ESTATE, "pre-formed A transform: an fp32 axk-1 GEMM");
-  if (d.axk == 2) {   // dW operand u = [A > 0] w[m] (A: bf16 activations [K][M])
-    REQUIRE(!d.a_kc && d.a16 && d.ax_w && d.M % 4 == 0 && !d.ax_out && ((uintptr_t)d.ax_w & 15) == 0,
-            SACMI_ESTATE, "dW A transform needs an MN-contiguous bf16 A and a float4-aligned w");
-    check_span(d.ax_w, d.M - 1, "ax_w");
-  } else if (d.axk) {
+  if (d.axk) {
+    REQUIRE(d.axk == 1, SACMI_ESTATE, "unknown A transform");
     REQUIRE(d.a_kc && !d.b_kc && d.ax_w, SACMI_ESTATE, "A transform needs a K-contiguous A and w");
     check_span(d.ax_w, d.K - 1, "ax_w");
     if (d.ax_out) {
@@ -719,7 +672,7 @@ static void validate(const GemmDesc& d) {
 // level is complete (right before its launch):
 //   * Bh, the bf16 shadow of a weight operand: k_fwd16 / k_axk16 / k_gemm<bf16> read it
 //     over exactly B's element range (2 bytes per element, 8-byte vector loads);
-//   * ws, the split-K partial workspace: k_dw_part{,16} write and k_dw_fin reads
+//   * ws, the split-K partial workspace: k_dw_part16 writes and k_dw_fin reads
 //     ws[0, ws_floats) at most (dw_split_plan never plans past ws_floats), so the claimed
 //     capacity must lie inside one allocation.
 static void validate_batch(const GemmBatch& b) {
@@ -738,19 +691,6 @@ static void validate_batch(const GemmBatch& b) {
   } else {
     REQUIRE(b.ws_floats == 0, SACMI_ESTATE, "split-K workspace capacity without a workspace");
   }
-}
-
-// the policy heads folded into the last policy hidden layer's level where launch_gemm can
-// (gemm_level_heads_fold_ok; kg_body: every policy tile's share of the head sums, the last
-// column tile of a row block sums them and samples) — opt-in, SACMI_HEADS_FOLD=1: both fold
-// forms measured slower than the separate heads launch at config 2 (the last tile running
-// the whole heads GEMM: L2 11.1 -> 20.1 us, 8,850 -> 8,669 steps/s; the split shares:
-// L2 11.8 -> 19.7 us, 8,740 -> 8,644 — profiles/r05/heads_fold_ab, heads_split_ab).  Read per
-// enqueue: tests switch it between contexts.
-static bool heads_fold_wanted() {
-  const char* e = std::getenv("SACMI_HEADS_FOLD");
-  const char* n = std::getenv("SACMI_NO_HEADS_FOLD");
-  return e && std::atoi(e) != 0 && !(n && std::atoi(n) != 0);
 }
 
 struct Level {
@@ -775,7 +715,6 @@ static double level_flops(const GemmBatch& b) {
     f += 2.0 * b.d[i].M * (double)b.d[i].N * b.d[i].K;
     if (b.d[i].pa_out) f += 2.0 * b.d[i].M * (double)b.d[i].N * b.d[i].pa_A;   // dL/da partials
   }
-  if (b.heads_ticket) f += 2.0 * b.heads.rows * (2.0 * b.heads.A) * b.heads.K;   // folded heads
   return f;
 }
 
@@ -881,8 +820,7 @@ static MtSampleArgs mt_args(sacmi_ctx* c, int B, const BatchBufs& bb) {
 // on the batch-4096-class kernels (k_fwd16 / k_axk16 / k_dw_part16: launch_gemm refuses
 // anything else), so batch >= 4096 and hidden a multiple of 128, >= 512.
 static bool act16_on(const sacmi_ctx* c, int B) {
-  static const bool env = std::getenv("SACMI_NO_ACT16") == nullptr;
-  return env && c->bf16 && B >= 4096 && c->H >= 512 && c->H % 128 == 0;
+  return c->bf16 && B >= 4096 && c->H >= 512 && c->H % 128 == 0;
 }
 
 static GatherArgs gather_args(sacmi_ctx* c, int B, const BatchBufs& bb, bool per) {
@@ -910,8 +848,7 @@ static bool ride_possible(sacmi_ctx* c, int B) {
 static bool ride_b_possible(sacmi_ctx* c, int B) {
   return c->cfg.replay_kind == SACMI_REPLAY_UNIFORM && c->bf16 && B >= 2048 &&
          mt_sample_lds_words(mt_sample_tbl_log2(B, true), sample_setsize(B)) * 4 <=
-             (size_t)kDw16LdsBytes &&
-         std::getenv("SACMI_NO_RIDE_B") == nullptr;
+             (size_t)kDw16LdsBytes;
 }
 
 // One update's minibatch: device sampling (random.sample or the prioritized sampler, unless
@@ -975,8 +912,9 @@ static AdamArgs dp_adam_args(sacmi_ctx* c, bool critic, int B, float grad_scale,
     ad.loss_part = c->lpart_c.p; ad.loss_slot0 = 0; ad.n_losses = 2;
     ad.log_alpha_idx = -1; ad.auto_entropy = 0;
     ad.err_skip = kErrSkipAll; ad.err_nopolyak = kErrActLike;
-    // every rank's error flags, summed by the critic gradient collective (kDpFlagN)
-    ad.err_flags = c->G.p + c->q_end;
+    // every rank's error flags, summed by the critic gradient collective (kDpFlagN): past the
+    // critic range (all-reduce form), or in their own buffer (sharded form)
+    ad.err_flags = c->dp_sharding_now ? c->dp_flags.p : c->G.p + c->q_end;
   } else {
     ad.tgt = nullptr; ad.tau = 0.f; ad.step_offset = 0;
     ad.loss_part = c->lpart_a.p; ad.loss_slot0 = 2; ad.n_losses = 1;
@@ -987,68 +925,16 @@ static AdamArgs dp_adam_args(sacmi_ctx* c, bool critic, int B, float grad_scale,
   return ad;
 }
 
-// The actor pass L7 -> L8 -> L9 -> sample-backward tail -> L12 of a fused update as ONE
-// persistent launch (k_chain, sacmi_internal.h ChainArgs): batch 256 (8 cohorts x 32 rows, one
-// tile per workgroup and phase), fp32, two hidden layers with the dL/da fold, inside a graph
-// this context captures (the argument block is uploaded after the capture).  Returns false
-// (nothing enqueued) where it does not apply: the caller launches the levels one by one.
-// SACMI_NO_CHAIN at creation switches it off (the tests' A/B).
-static bool chain_batch_ok(const sacmi_ctx* c, int B) {
-  // (every chain level is one pass over K: K <= kChainMaxK — the critics' fc1 K is S + 1 + A)
-  return c->chain_on && !c->bf16 && c->nh == 2 && B == kChainCohorts * 32 && c->H % 32 == 0 &&
-         c->H <= kChainMaxK && c->S + 1 + c->A <= kChainMaxK && !std::getenv("SACMI_NO_DLDA_FOLD") &&
-         chain_supported();
-}
-// kind 0: the actor pass (L7, L8, L9, the tail `sb`, L12); kind 1: the critic pass (L1 and
-// L2 on 32x64 tiles, L2 carrying the policy heads fold, L3, L4, L5).  (Site-isolation
-// profiling enumerates the sites outside a capture: the launch chain there.)
-static bool enqueue_chain_kind(sacmi_ctx* c, int B, int kind, const Level* const* lv, int n,
-                               const SampleBwdArgs* sb) {
-  if (!c->own_capture || c->prof_site >= 0 || c->prof_collect || !chain_batch_ok(c, B)) return false;
-  ChainArgs ca;
-  std::memset(&ca, 0, sizeof(ca));
-  ca.kind = kind;
-  double flops = kind == 0 ? 2.0 * B * (2.0 * c->A) * c->H : 0.0, bytes = 0;   // (the tail's dhp2 product)
-  for (int i = 0; i < n; ++i) {
-    GemmBatch b = lv[i]->b;
-    b.bf16 = 0;
-    for (int q = 0; q < b.count; ++q) b.d[q].Bh = nullptr;
-    b.ws = nullptr; b.ws_floats = 0;
-    b.tl = nullptr;
-    b.st_wt = 1;           // write-through epilogue stores: every hand-off's bytes leave L2
-    b.adam_wg = -2;
-    validate_batch(b);
-    if (!chain_assign_tiles(b, kind == 1 && i < 2 ? 64 : 32) || b.total_tiles > kChainGrid) return false;
-    const int items = b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0) + b.ride.pk_blocks;
-    if (items > kChainGrid) return false;
-    if (b.heads_ticket && !(kind == 1 && i == 1 && chain_a_l2_ok(b))) return false;
-    flops += level_flops(b);
-    bytes += level_bytes(b);
-    ca.lv[i] = b;
-  }
-  if (sb) {
-    ca.tail = *sb;
-    ca.tail.tl = nullptr;
-    ca.pa = c->pa.p; ca.n_pa = 2 * c->nparts;
-  }
-  ca.rows_per_cohort = B / kChainCohorts;
-  ca.tail_groups = ca.rows_per_cohort / 8;
-  ca.tail_slabs = (c->H + 63) / 64;
-  if (ca.tail_groups * ca.tail_slabs > kChainGrid / kChainCohorts) return false;
-  ca.sync = c->chain_sync.p;
-  ca.err = &c->sc.p->err;
-  check_span(ca.sync, kChainSyncInts - 1, "chain barrier words");
-  const ChainArgs* dev = chain_slot(c, ca);
-  if (!dev) return false;   // (pool full: the launch chain)
-  if (mark(c, kind == 0 ? "gemm_chain_L7_L12" : "gemm_chain_L1_L5", flops, bytes)) {
-    if (!launch_chain(ca, dev, c->tl_cur, c->stream)) throw Error{SACMI_ESTATE, "k_chain refused a supported configuration"};
-  }
-  return true;
-}
-static bool enqueue_chain(sacmi_ctx* c, int B, const Level& l7, const Level& l8, const Level& l9,
-                          const SampleBwdArgs& sb, const Level& l12) {
-  const Level* lv[4] = {&l7, &l8, &l9, &l12};
-  return enqueue_chain_kind(c, B, 0, lv, 4, &sb);
+// The Adam moments are whole on this rank: every read of them and every update that steps
+// them from this rank's M, V (any update but the sharded data-parallel sequence) needs it
+static void require_moments_whole(const sacmi_ctx* c) {
+  REQUIRE(!c->moments_partial, SACMI_ESTATE,
+          "the Adam moments of this context were left partly stepped by a loopback one-rank timing "
+          "run (SACMI_DP_LOOPBACK_ONE_RANK: only rank 0's chunks were stepped); they cannot be read "
+          "or stepped any more");
+  REQUIRE(!c->moments_sharded, SACMI_ESTATE,
+          "the Adam moments are sharded across the data-parallel ranks (sharded optimizer step): "
+          "call sacmi_dp_sync_state on every rank before reading or writing them");
 }
 
 // parity: which batch buffer set this update uses; have_batch: its indices and rows
@@ -1058,6 +944,9 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
                            float grad_scale, bool use_ring, int parity = 0,
                            bool have_batch = false, bool ride_next = false) {
   hipStream_t s = c->stream;
+  // every Adam step of this update but the sharded data-parallel form's own (enqueue_dp_sharded
+  // steps this rank's chunks) reads and writes the whole of M, V
+  if ((phase_mask & 6) && !c->dp_sharding_now) require_moments_whole(c);
   c->site_counter = 0;
   const BatchBufs bb = batch_bufs(c, parity);
   // where the next update's sampling + gather ride: L12 / L13 (placement A, batch <= ~2k,
@@ -1089,11 +978,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
   };
   // activation buffers: element offsets in the update's activation format
   const bool act16 = act16_on(c, B);
-  // fp32: the critic / actor u rows (u = [h[L] > 0] w_head) stored by the last forward level
-  // (L2 / L8, which holds w_head for its dot partials) and read by L5 / L9 as a plain A
-  // operand — no transform in their K loops, no u stores in L5 (SACMI_NO_PRE_U=1: the
-  // transform form; read per enqueue)
-  const bool pre_u = !c->bf16 && std::getenv("SACMI_PRE_U") != nullptr && std::getenv("SACMI_NO_PRE_U") == nullptr;
   const int a16 = act16 ? 1 : 0;
   auto E = [&](float* base, size_t off) -> float* {
     return act16 ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(base) + off) : base + off;
@@ -1111,22 +995,12 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       lv.b.tl = c->tl_cur;
       launch_gemm(lv.b, s);
     }
-    // diagnostic (SACMI_EXP_DUP_LEVELS): the idempotent forward levels launched twice, the
-    // second (site "<name>_dup") with its operands warm in the XCDs' L2 — the level body's
-    // time with L2-resident operands
-    static const bool dup = std::getenv("SACMI_EXP_DUP_LEVELS") != nullptr;
-    if (dup && !lv.b.has_adam && !lv.b.ride.kind && !lv.b.ride.pk_blocks && !lv.b.rows.kind &&
-        mark(c, (name + "_dup").c_str(), level_flops(lv.b), level_bytes(lv.b))) {
-      lv.b.tl = c->tl_cur;
-      launch_gemm(lv.b, s);
-    }
   };
 
   // fused updates whose policy dhp1 level (L12) leaves CUs idle on k_gemm: Polyak rides there
-  static const bool pk_env = std::getenv("SACMI_NO_POLYAK_RIDE") == nullptr;
   // (data-parallel phase 1, both optimizer forms: the critic Adam before L7 leaves the
   // targets alone — sharded: enqueue_dp's chunk Adam, all-reduce: the one below)
-  const bool polyak_ride = (phase_mask == 7 || (phase_mask & 2)) && pk_env &&
+  const bool polyak_ride = (phase_mask == 7 || (phase_mask & 2)) &&
                            !act16 && (int64_t)((B + 31) / 32) * ((H + 31) / 32) <= 192;
   if (phase_mask & 1) {
     if (!have_batch)   // (have_batch: the previous update's rides / side stream produced them)
@@ -1150,21 +1024,12 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     // dq_i = 2 (q_i - q^) / B; the A operand dh[L] = dq * w_head * [h[L] > 0] is formed
     // from h[L] on the fly (its coefficient-free rows u stored once by the column-tile-0
     // workgroups, for the weight gradient of layer L)
-    // u rows for layer L's weight gradient (SACMI_DW_U_TRANSFORM=1, read per enqueue, bf16
-    // activations only: none — the split-K kernel forms u = [h[L] > 0] w_head from h[L],
-    // bit-identical; measured slower: L5 24.8 -> 22.1 us but L6 59 -> 75, the part kernel's
-    // staging carrying both loads and the select; profiles/r05/dw_u_ab)
-    const bool u_rows = !act16 || std::getenv("SACMI_DW_U_TRANSFORM") == nullptr;
     Level l5;
     for (int i = 0; i < 2; ++i) {
       GemmDesc g = gd(E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dhc[L - 1].p + i * H, 2 * H,
                       B, H, H, EPI_MASK, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd);
       g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]); g.ax_ld = 2 * H;
-      // the coefficient-free rows u for layer L's weight gradient (or, opt-in with bf16
-      // activations, that gradient forms u = [h[L] > 0] w_head from h[L] itself: axk 2);
-      // fp32 (pre_u): L2 stored them already, and this level reads them as its A operand
-      g.ax_out = u_rows && !pre_u ? c->dhc[L].p + i * H : nullptr;
-      if (pre_u) { g.A = c->dhc[L].p + i * H; g.lda = 2 * H; g.ax_pre = 1; }
+      g.ax_out = c->dhc[L].p + i * H;   // the coefficient-free rows u (layer L's weight gradient)
       l5.add(dh(g));
     }
     {
@@ -1174,38 +1039,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       rf.gamma = (float)c->cfg.gamma;
       rf.sc = c->sc.p; rf.dq = c->dq.p; rf.dq4 = c->dq4.p; rf.loss_part = c->lpart_c.p;
     }
-    // The critic pass L1 -> L2 (+ heads) -> L3 -> L4 -> L5 as ONE persistent launch
-    // (k_chain_a) where it applies: the policy rows as two row-affine descs (targets'
-    // s', actors' s), so that every cohort holds the a' its target critics read
-    bool chained_a = false;
-    if (nh == 2 && heads_fold_wanted() && chain_batch_ok(c, B)) {
-      Level a1, a2, a3, a4;
-      for (int h2 = 0; h2 < 2; ++h2)
-        a1.add(fw(gd(bb.x2 + (size_t)h2 * B * Kx, Kx, 1, W(c->p_fc[0]), c->p_fc[0].ld, 1, c->hp[0].p + (size_t)h2 * B * Hd,
-                     Hd, B, H, S + 1, EPI_RELU)));
-      for (int i = 0; i < 2; ++i)
-        a1.add(fw(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
-      for (int h2 = 0; h2 < 2; ++h2)
-        a2.add(fw(gd_fwd_h(c->hp[0].p + (size_t)h2 * B * Hd, Hd, W(c->p_fc[1]), Hd, c->hp[1].p + (size_t)h2 * B * Hd, Hd,
-                           B, H, H)));
-      for (int i = 0; i < 2; ++i)
-        a2.add(with_dot(fw(gd_fwd_h(E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, W(q[i][1]), Hd, E(c->hq[1].p, (size_t)i * Hd),
-                                    2 * Hd, B, H, H)), W(q[i][nh]), i));
-      a2.b.heads = hs;
-      a2.b.heads_desc = 0;
-      a2.b.heads_ndesc = 2;
-      a2.b.heads_ticket = c->heads_ticket.p;
-      a2.b.heads_part = c->heads_part.p;
-      for (int i = 0; i < 2; ++i)
-        a3.add(fw(gd(bb.x2, Kx, 1, Wt(q[i][0]), Kx, 1, E(c->hqt[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
-      for (int i = 0; i < 2; ++i)
-        a4.add(with_dot(fw(gd_fwd_h(E(c->hqt[0].p, (size_t)i * Hd), 2 * Hd, Wt(q[i][1]), Hd, E(c->hqt[1].p, (size_t)i * Hd),
-                                    2 * Hd, B, H, H)), Wt(q[i][nh]), 2 + i));
-      const Level* lv[5] = {&a1, &a2, &a3, &a4, &l5};
-      chained_a = enqueue_chain_kind(c, B, 1, lv, 5, nullptr);
-      if (chained_a) c->heads_fold_B = B;
-    }
-    if (!chained_a) {
     // L1: policy fc1 on [s2 ; s] (2B rows), critic fc1 (twin) on [s|1|a]
     Level l1;
     l1.add(fw(gd(bb.x2, Kx, 1, W(c->p_fc[0]), c->p_fc[0].ld, 1, c->hp[0].p, Hd, 2 * B, H, S + 1, EPI_RELU)));
@@ -1213,38 +1046,19 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l1.add(fw(gd(bb.xq, Kx, 1, W(q[i][0]), Kx, 1, E(c->hq[0].p, (size_t)i * Hd), 2 * Hd, B, H, S + A + 1, EPI_RELU)));
     run(l1, "gemm_L1_fc1");
     // L2 (.. L2b): the remaining hidden layers (K = H, bias in the epilogue); the last one
-    // also accumulates the critic head (fc3 / fc4) dot partials of q1 / q2 (slots 0 / 1) and,
-    // where its tiles can (gemm_level_heads_fold_ok), runs the heads + sample folded in: the
-    // last column tile of each 32-row block of the policy rows takes them for that block —
-    // one launch and one boundary fewer (SACMI_NO_HEADS_FOLD=1: the separate kernel)
-    bool folded = false;
+    // also accumulates the critic head (fc3 / fc4) dot partials of q1 / q2 (slots 0 / 1)
     for (int l = 1; l < nh; ++l) {
       Level lv;
       lv.add(fw(gd_fwd_h(c->hp[l - 1].p, Hd, W(c->p_fc[l]), Hd, c->hp[l].p, Hd, 2 * B, H, H)));
       for (int i = 0; i < 2; ++i) {
         GemmDesc g = fw(gd_fwd_h(E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd, W(q[i][l]), Hd,
                                  E(c->hq[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
-        if (l == L) {
-          g = with_dot(g, W(q[i][nh]), i);
-          if (pre_u) { g.u_out = c->dhc[L].p + i * H; g.u_ld = 2 * H; }   // (L5's A, L6's u rows)
-        }
+        if (l == L) g = with_dot(g, W(q[i][nh]), i);
         lv.add(g);
-      }
-      lv.b.bf16 = c->bf16 ? 1 : 0;   // (the gate reads the level's MFMA operand type, as run() sets it)
-      if (l == L && heads_fold_wanted() && gemm_level_heads_fold_ok(lv.b, A)) {
-        lv.b.heads = hs;
-        lv.b.heads_desc = 0;   // (the policy desc, added first)
-        lv.b.heads_ndesc = 1;
-        lv.b.heads_ticket = c->heads_ticket.p;
-        lv.b.heads_part = c->heads_part.p;
-        check_span(c->heads_part.p, (int64_t)((2 * B + kHeadsFoldTM - 1) / kHeadsFoldTM) * ((H + 63) / 64) *
-                                        kHeadsFoldTM * 2 * A - 1, "heads_part");
-        folded = true;
       }
       run(lv, l == 1 ? "gemm_L2_fc2" : "gemm_L2b_fc3");
     }
-    c->heads_fold_B = folded ? B : -1;
-    if (!folded && mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) {
+    if (mark(c, "heads_sample", 2.0 * 2 * B * (2.0 * A) * H)) {
       hs.tl = c->tl_cur;
       launch_heads_sample(hs, s);
     }
@@ -1273,7 +1087,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
                      B, H, H, EPI_MASK, E(c->hq[l - 1].p, (size_t)i * Hd), 2 * Hd)));
       run(lv, "gemm_L5b_critic_dh");
     }
-    }   // (!chained_a)
     // L6: every critic weight gradient: into the gradient arena, or (fused) straight into
     // Adam + Polyak on the parameters.  The hidden weights are read by the dh levels
     // above, so every critic dW runs here — in both modes, so the reduction order (and
@@ -1294,10 +1107,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       // weight gradient applies coef = dL/dq_i (dq) as a per-batch-row K-scale
       GemmDesc wl = dwx(gd_dw_h(c->dhc[L].p + i * H, 2 * H, E(c->hq[L - 1].p, (size_t)i * Hd), 2 * Hd,
                                 dst(q[i][L]), Hd, H, H, B, wepi, 1 + i));
-      if (!u_rows) {   // u = [h[L] > 0] w_head formed by the split-K kernel (L5 stored none)
-        wl.A = E(c->hq[L].p, (size_t)i * Hd); wl.lda = 2 * Hd; wl.a16 = 1;
-        wl.axk = 2; wl.ax_w = W(q[i][nh]);
-      }
       wl.a_ksc = c->dq.p + i * B;
       l6.add(wl);
       l6.add(dwx(gd_dw_h(c->dq4.p + (size_t)i * B * 4, 4, E(c->hq[L].p, (size_t)i * Hd), 2 * Hd, dst(q[i][nh]), Hd, 1, H, B,
@@ -1322,7 +1131,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l6.b.ride.mt = mt_args(c, B, batch_bufs(c, parity ^ 1));
     }
     if (!fuse) {   // data parallel: this update's error flags ride in the critic collective
-      l6.b.err_flags = G + c->q_end;
+      l6.b.err_flags = c->dp_sharding_now ? c->dp_flags.p : G + c->q_end;
       l6.b.err_word = &c->sc.p->err;
       check_span(l6.b.err_flags, kDpFlagN - 1, "error flags");
     }
@@ -1340,8 +1149,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     }
    }
     // L7/L8 (.. L8b): updated critics on [s|1|a~] (head dot partials: slots 4 / 5)
-    // (the levels of the actor pass are built first, then launched one by one or — fused
-    // batch-256 updates — as the persistent chain k_chain: L7 -> L8 -> L9 -> tail -> L12)
     const float* xa = E(bb.x2, (size_t)B * Kx);
     Level l7;
     for (int i = 0; i < 2; ++i)
@@ -1352,10 +1159,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       for (int i = 0; i < 2; ++i) {
         GemmDesc g = fw(gd_fwd_h(E(c->hqa[l - 1].p, (size_t)i * Hd), 2 * Hd, W(q[i][l]), Hd,
                                  E(c->hqa[l].p, (size_t)i * Hd), 2 * Hd, B, H, H));
-        if (l == L) {
-          g = with_dot(g, W(q[i][nh]), 4 + i);
-          if (pre_u) { g.u_out = c->dha[L].p + i * H; g.u_ld = 2 * H; }   // (L9's A)
-        }
+        if (l == L) g = with_dot(g, W(q[i][nh]), 4 + i);
         lv.add(g);
       }
       l8s.push_back(lv);
@@ -1368,7 +1172,6 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       GemmDesc g = gd(E(c->hqa[L].p, (size_t)i * Hd), 2 * Hd, 1, W(q[i][L]), Hd, 0, c->dha[L - 1].p + i * H, 2 * H,
                       B, H, H, EPI_MASK, E(c->hqa[L - 1].p, (size_t)i * Hd), 2 * Hd);
       g.axk = 1; g.ax_slot = i; g.ax_w = W(q[i][nh]);
-      if (pre_u) { g.A = c->dha[L].p + i * H; g.lda = 2 * H; g.ax_pre = 1; }   // (L8 stored u)
       l9.add(dh(g));
     }
     {
@@ -1376,10 +1179,8 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       rf.kind = 2; rf.part = dotp(4); rf.nparts = c->nparts; rf.B = B;
       rf.logp = c->logp.p + B; rf.sc = c->sc.p; rf.loss_part = c->lpart_a.p;
       if (c->cfg.auto_entropy) {
-        rf.alpha_grad = G + c->la_idx; rf.logp_part = c->lp_part.p; {
-          const int tm = c->heads_fold_B == B ? kHeadsFoldTM : heads_rows_per_wg(2 * B);
-          rf.n_lp = (2 * B + tm - 1) / tm;
-        }
+        rf.alpha_grad = G + c->la_idx; rf.logp_part = c->lp_part.p;
+        rf.n_lp = (2 * B + heads_rows_per_wg(2 * B) - 1) / heads_rows_per_wg(2 * B);
         rf.target_entropy = (float)(-A);
       }
     }
@@ -1438,10 +1239,9 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
     l12.add(dh(gd(c->dhp[1].p, H, 1, W(c->p_fc[1]), Hd, 0, c->dhp[0].p, H, B, H, H, EPI_MASK, hpa(0), Hd)));
     if (ride_b) {   // ... and its gather in L12, two rows a wave: 256 ride workgroups at config
       // 5, the slots L12's 256 tiles leave free (512 at 2 per CU) — one round; a row a wave
-      // (512 workgroups, SACMI_RIDE_GATHER_ROWS=8) takes a second round: 3,255 vs 3,282
-      // updates/s (profiles/r05/ride_rows_ab; the ride's 22 MB cost L12 ~8 us either way)
-      const char* rr = std::getenv("SACMI_RIDE_GATHER_ROWS");
-      const int rows_per_block = rr && std::atoi(rr) > 0 ? std::atoi(rr) : 16;   // (8 waves)
+      // (512 workgroups) takes a second round: 3,255 vs 3,282 updates/s
+      // (profiles/r05/ride_rows_ab; the ride's 22 MB cost L12 ~8 us either way)
+      const int rows_per_block = 16;   // (8 waves)
       l12.b.ride.kind = 2; l12.b.ride.nblocks = (B + rows_per_block - 1) / rows_per_block;
       l12.b.ride.ga = gather_args(c, B, batch_bufs(c, parity ^ 1), false);
     }
@@ -1483,8 +1283,7 @@ static void enqueue_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int ph
       l13.b.ride.kind = 2; l13.b.ride.nblocks = 16;
       l13.b.ride.ga = gather_args(c, B, nb2, false);
     }
-    // the persistent chain (k_chain) where it applies, else the launches one by one
-    if (!(nh == 2 && fold_dlda && enqueue_chain(c, B, l7, l8s[0], l9, sb, l12))) {
+    {
       run(l7, "gemm_L7_act_fc1");
       for (size_t i = 0; i < l8s.size(); ++i) run(l8s[i], i == 0 ? "gemm_L8_act_fc2" : "gemm_L8b_act_fc3");
       run(l9, "gemm_L9_act_dh1");
@@ -1542,8 +1341,7 @@ static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use
   // workgroups push level workgroups of the chip-filling levels into a second round) and
   // forked beside the levels with free slots (L6 / L12: 422 -> 430-450 us — every
   // cross-stream edge of the graph cost the main chain ~10 us); they ride (placement B)
-  static const bool side_env = std::getenv("SACMI_NO_SIDE_SAMPLE") == nullptr;
-  const bool side = side_env && reps > 1 && dev_idx && !ride &&
+  const bool side = reps > 1 && dev_idx && !ride &&
                     c->cfg.replay_kind == SACMI_REPLAY_PER;
   if (side) {
     if (!c->side_stream) CHECK_HIP(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
@@ -1585,6 +1383,7 @@ static void enqueue_many(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool use
 
 static void run_update(sacmi_ctx* c, int B, int dev_idx, int dev_eps, int phase_mask,
                        float grad_scale, bool use_ring, int reps = 1, PhaseRide pr = {}) {
+  if (phase_mask & 6) require_moments_whole(c);   // (before any state changes; enqueue_update)
   c->pf_save = false;
   if (!c->mb_graph) mb_flush(c);   // (mb_graph: this update's sampler takes them)
   c->inflight = true;
@@ -1748,8 +1547,10 @@ static RcclApi& rccl() {
 // reach past e — into the gap between the critic and actor ranges, or into the arena's tail
 // slack, never into the other range), Adam runs on chunk r of the parameters (the layer
 // segments clipped to it), and the parameters are all-gathered in place.  A reduce-scatter
-// does not deliver the error flags past q_end to every rank, so this form all-reduces them
-// on their own first (kDpFlagN floats; the all-reduce form carries them in its critic range).  Replicas stay bitwise identical: every
+// does not deliver the error flags to every rank, so this form keeps them in a buffer of their
+// own (dp_flags, outside the reduce-scatter's reach) and all-reduces it in the same RCCL group
+// (kDpFlagN floats; the all-reduce form carries them in its critic range).  Replicas stay
+// bitwise identical: every
 // chunk is computed by one rank and the gather copies its bits.  Adam moments (M, V) are
 // valid on each rank's own chunks only (sacmi_dp_sync_state gathers them, e.g. before a
 // checkpoint).  Loopback: `world` identical ranks emulated on one GPU — the gradients x world
@@ -1812,22 +1613,21 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
     const int64_t ch = shard_chunk(e - b, W);
     float* g = c->G.p + b;
     // the critic's error flags to every rank (the reduce-scatter delivers chunk r only): an
-    // all-reduce of their own, in one RCCL group with the reduce-scatter (one launch)
+    // all-reduce of their own buffer (disjoint from the reduce-scatter's span), in one RCCL
+    // group with the reduce-scatter (one launch)
     const bool group = critic && !c->dp_loopback;
     if (group) CHECK_RCCL(rccl().group_start());
     if (critic) {
       (void)mark(c, "allreduce_error_flags");
-      float* f = c->G.p + c->q_end;
+      float* f = c->dp_flags.p;
       if (c->dp_loopback) loopback_flags(c, f, s);
       else CHECK_RCCL(rccl().all_reduce(f, f, (size_t)kDpFlagN, ncclFloat32, ncclSum, c->comm, s));
     }
     (void)mark(c, critic ? "reduce_scatter_critic_grads" : "reduce_scatter_actor_grads");
-    // (loopback: the whole span the collective covers, the last chunk's reach included —
-    // the critic's flags past q_end too: already summed above, so the span stops at them)
+    // (loopback: the whole span the collective covers, the last chunk's reach included)
+    check_span(g, ch * W - 1, "reduce-scatter span");
     if (c->dp_loopback) {
-      scale_checked(g, std::min(ch * W, critic ? e - b : ch * W), (float)W, s);
-      if (critic && ch * W > e - b + kDpFlagN)
-        scale_checked(g + (e - b) + kDpFlagN, ch * W - (e - b) - kDpFlagN, (float)W, s);
+      scale_checked(g, ch * W, (float)W, s);
     } else {
       CHECK_RCCL(rccl().reduce_scatter(g, g + c->dp_rank * ch, (size_t)ch, ncclFloat32, ncclSum, c->comm, s));
     }
@@ -1857,11 +1657,12 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
     if (!critic && c->cfg.auto_entropy) launch_alpha_sync(c->sc.p, c->P.p + c->la_idx, ~0, s);
   };
   // Polyak rides in phase 1's L12 where it can (enqueue_update: polyak_ride), else its own pass
-  const bool pk_ride = std::getenv("SACMI_NO_POLYAK_RIDE") == nullptr && !act16_on(c, B) &&
+  const bool pk_ride = !act16_on(c, B) &&
                        (int64_t)((B + 31) / 32) * ((c->H + 31) / 32) <= 192;
   c->dp_sharding_now = true;
   const bool one_rank_only = std::getenv("SACMI_DP_LOOPBACK_ONE_RANK") != nullptr;
-  if ((!c->dp_loopback && W > 1) || (c->dp_loopback && one_rank_only)) c->moments_sharded = true;
+  if (!c->dp_loopback && W > 1) c->moments_sharded = true;
+  if (c->dp_loopback && one_rank_only && W > 1) c->moments_partial = true;
   try {
     int parity = 0;
     bool have = false;
@@ -1929,6 +1730,7 @@ static void enqueue_dp(sacmi_ctx* c, int B, int n) {
 // unless a sharded step left them valid on the rank's own chunks only).  M and V carry no
 // slack: the last chunk is gathered through a bounce of the padded size
 static void dp_gather_moments(sacmi_ctx* c) {
+  if (c->dp_loopback) c->moments_sharded = false;   // (loopback: every chunk is on this GPU)
   if (!c->moments_sharded || c->dp_loopback || c->dp_world == 1) return;
   const int W = c->dp_world;
   for (int critic = 1; critic >= 0; --critic) {
@@ -2011,14 +1813,6 @@ int sacmi_create(const sacmi_config* cfg, int device, sacmi_ctx** out) {
     alloc_all(c.get());
     c->ring_slots = 4096;
     c->ring.alloc((size_t)c->ring_slots * 3);
-    // the persistent chains are opt-in: measured slower than the launch sequence (DESIGN.md
-    // §12a: each cohort barrier + write-through hand-off costs more than a graph's kernel
-    // boundary at these tile sizes)
-    c->chain_on = std::getenv("SACMI_CHAIN") != nullptr && std::getenv("SACMI_NO_CHAIN") == nullptr;
-    if (c->chain_on) {
-      c->chain_pool.alloc((size_t)sacmi_ctx::kChainSlots * sizeof(ChainArgs));
-      c->chain_sync.alloc(kChainSyncInts);
-    }
     alloc_pinned(c.get());
     DevScalars h{};
     h.alpha = (float)cfg->alpha;
@@ -2056,17 +1850,15 @@ int sacmi_destroy(sacmi_ctx* c) {
     for (auto* b : {&c->P, &c->T, &c->G, &c->M, &c->V, &c->obs, &c->act, &c->rew, &c->obs2,
                     &c->done, &c->prio, &c->xq, &c->x2, &c->r, &c->d, &c->xqb, &c->x2b, &c->rb,
                     &c->db, &c->eps,
-                    &c->cache, &c->logp, &c->dq, &c->dq4, &c->dotp, &c->pa, &c->act_h, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->ax, &c->ah1, &c->ah2,
+                    &c->cache, &c->logp, &c->dq, &c->dq4, &c->dotp, &c->pa, &c->act_h, &c->dw_ws, &c->dhead, &c->lpart_c, &c->lpart_a, &c->ring, &c->lp_part, &c->dp_flags, &c->ax, &c->ah1, &c->ah2,
                     &c->aeps, &c->acache, &c->alogp, &c->aout, &c->stage, &c->per_scr, &c->per_probs,
                     &c->per_chunk, &c->per_w, &c->per_val})
       b->release();
     for (int l = 0; l < 3; ++l)
       for (auto* b : {&c->hp[l], &c->hq[l], &c->hqt[l], &c->hqa[l], &c->dhc[l], &c->dha[l], &c->dhp[l]})
         b->release();
-    c->heads_ticket.release(); c->heads_part.release();
     c->sc.release(); c->mt.release(); c->mt_backup.release(); c->mt_pf.release(); c->idx32.release(); c->idx64.release();
     c->Ph.release(); c->Th.release();
-    c->chain_pool.release(); c->chain_sync.release();
     c->idx32b.release(); c->idx64b.release();
     c->per_q.release(); c->per_blk.release(); c->per_idx.release(); c->per_cdf.release();
     c->per_u.release(); c->per_uin.release(); c->per_owner.release(); c->per_bad.release();
@@ -2105,11 +1897,6 @@ int sacmi_tensor_numel(sacmi_ctx* c, int net, int layer, int part, int64_t* nume
   });
 }
 
-static void require_moments_whole(const sacmi_ctx* c) {
-  REQUIRE(!c->moments_sharded, SACMI_ESTATE,
-          "the Adam moments are sharded across the data-parallel ranks (sharded optimizer step): "
-          "call sacmi_dp_sync_state on every rank before reading or writing them");
-}
 
 static float* slot_base(sacmi_ctx* c, int slot, int net) {
   const bool target = net == SACMI_Q1_TARGET || net == SACMI_Q2_TARGET;
@@ -2294,10 +2081,9 @@ static void push_impl(sacmi_ctx* c, const float* s, const float* a, const float*
   {
     // a few rows while no update is in flight: into the mailbox, for the next synchronous
     // update's sampler (uniform replay; every other path flushes them first)
-    static const bool mb_env = std::getenv("SACMI_NO_PUSH_MAILBOX") == nullptr;
     const int S = c->S, A = c->A;
     const int64_t rowf = 2 * S + A + 2;
-    if (mb_env && c->mb_host && !c->inflight && c->cfg.replay_kind == SACMI_REPLAY_UNIFORM &&
+    if (c->mb_host && !c->inflight && c->cfg.replay_kind == SACMI_REPLAY_UNIFORM &&
         c->mb_pending + n <= sacmi_ctx::kMbRows && c->mb_pending + n <= c->capacity) {
       // (rows pending beyond the capacity would map two rows onto one ring slot in the
       // sampler's scatter, stored in no fixed order: the chunked path's `skip` handles that)
@@ -2576,8 +2362,7 @@ static void run_update_mb(sacmi_ctx* c, int B, int dev_idx, int dev_eps, bool mb
 // The done word's value before a synchronous step's launch: with nothing else in flight, its
 // next change is that update's (step_finish polls for it); -1 otherwise (stream sync)
 static int done_prev(sacmi_ctx* c) {
-  static const bool poll = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
-  if (!poll || c->inflight) return -1;
+  if (c->inflight) return -1;
   return *reinterpret_cast<volatile int*>(c->loss_host + 4);
 }
 
@@ -2835,6 +2620,17 @@ int sacmi_step_act16(sacmi_ctx* c, int32_t batch, int32_t* out) {
     pf_touch(c); *out = act16_on(c, batch) ? 1 : 0; });
 }
 
+int sacmi_read_batch(sacmi_ctx* c, int32_t batch, int64_t* idx, float* eps, int64_t eps_numel) {
+  return guard([&] {
+    REQUIRE(c && idx && eps, SACMI_EVALUE, "null argument");
+    REQUIRE(batch >= 1 && batch <= c->Bm, SACMI_EVALUE, "bad batch");
+    REQUIRE(eps_numel == (int64_t)2 * batch * c->A, SACMI_EVALUE, "eps_numel must be 2 * batch * action_dim");
+    CHECK_HIP(hipStreamSynchronize(c->stream));
+    CHECK_HIP(hipMemcpy(idx, c->idx64.p, (size_t)batch * 8, hipMemcpyDeviceToHost));
+    CHECK_HIP(hipMemcpy(eps, c->eps.p, (size_t)eps_numel * 4, hipMemcpyDeviceToHost));
+  });
+}
+
 int sacmi_read_activation(sacmi_ctx* c, int32_t pass, int32_t layer, int32_t batch, float* out,
                           int64_t numel) {
   return guard([&] {
@@ -2854,13 +2650,6 @@ int sacmi_read_activation(sacmi_ctx* c, int32_t pass, int32_t layer, int32_t bat
     for (int i = 0; i < 2; ++i)
       CHECK_HIP(hipMemcpy2D(out + (size_t)i * batch * c->H, H4, b.p + (size_t)i * c->Hd, (size_t)2 * c->Hd * 4, H4,
                             (size_t)batch, hipMemcpyDeviceToHost));
-  });
-}
-
-int sacmi_step_chained(sacmi_ctx* c, int32_t batch, int32_t* out) {
-  return guard([&] {
-    REQUIRE(c && out, SACMI_EVALUE, "null argument");
-    *out = chain_batch_ok(c, batch) && c->use_graphs ? 1 : 0;
   });
 }
 
@@ -3226,12 +3015,8 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     }
     // zero-copy (default for env-rate calls): fc1 reads the states from the mapped staging
     // (its A operand, the ones column in place) and the heads kernel writes the actions back
-    static const bool zc_env = std::getenv("SACMI_ACT_ZEROCOPY") == nullptr ||
-                               std::getenv("SACMI_ACT_ZEROCOPY")[0] != '0';
-    const bool zc = pinned && zc_env && c->act_host_dev;
-    static const bool gemv_env = std::getenv("SACMI_NO_ACT_GEMV") == nullptr;
-    static const bool poll1 = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
-    const bool gemv = zc && n == 1 && gemv_env && poll1 && A <= 32;
+    const bool zc = pinned && c->act_host_dev;
+    const bool gemv = zc && n == 1 && A <= 32;
     // every path but the one-state GEMVs writes rows of batch set 0's x2 (the states here,
     // the actions from the heads kernel): a batch drawn ahead there is given up first
     if (!gemv) pf_touch(c);
@@ -3302,8 +3087,7 @@ int sacmi_act(sacmi_ctx* c, const float* states, int32_t n, int32_t deterministi
     hs.ctr_override = (1ull << 63) | (++c->act_calls);   // disjoint from update noise
     if (zc) hs.act_host = c->act_host_dev + (h_out - c->act_host);
     // one heads workgroup: the host polls its done word instead of the stream's completion
-    static const bool poll = std::getenv("SACMI_NO_DONE_POLL") == nullptr;
-    const bool poll_wait = poll && zc && n <= heads_rows_per_wg(n);
+    const bool poll_wait = zc && n <= heads_rows_per_wg(n);
     volatile int* done_host = reinterpret_cast<volatile int*>(c->act_nan_host + 1);
     if (poll_wait) {
       hs.done_word = c->act_nan_dev + 1;

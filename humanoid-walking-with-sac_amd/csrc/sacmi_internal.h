@@ -49,25 +49,19 @@ void ensure_dyn_lds(const void* kernel, size_t bytes);
 // Output stores of the update's kernels are write-through (sc1): a kernel then leaves no
 // dirty L2 lines behind, and the end-of-kernel L2 writeback — serialised at the boundary
 // to the next dependent kernel, ~B / 6 TB/s for B dirty bytes — has nothing to do (the
-// Adam levels write 15-30 MB of optimizer state per update).  SACMI_WT 0: plain stores.
-#ifndef SACMI_WT
-#define SACMI_WT 1
-#endif
-constexpr int kStAux = SACMI_WT ? 16 : 0;   // raw buffer store cache-policy bits (16 = sc1)
+// Adam levels write 15-30 MB of optimizer state per update).
+constexpr int kStAux = 16;   // raw buffer store cache-policy bits (16 = sc1)
 // The large-batch bf16 level kernels (k_fwd16 / k_axk16 / k_dw_part16 / k_dw_fin) store
 // tens of MB per launch as one dword per lane: there write-through measured slower (config
 // 5: 415 -> 447 us per update, the kernel bodies grew more than the boundaries shrank), so
-// they keep plain stores (SACMI_WT_BIG 0).
-#ifndef SACMI_WT_BIG
-#define SACMI_WT_BIG 0
-#endif
-template <bool WT = (SACMI_WT != 0), class T>
+// they keep plain stores (st_big).
+template <bool WT = true, class T>
 __device__ __forceinline__ void st_wt(T* p, T v) {
   if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
 template <class T>
-__device__ __forceinline__ void st_big(T* p, T v) { st_wt<SACMI_WT_BIG != 0>(p, v); }
+__device__ __forceinline__ void st_big(T* p, T v) { st_wt<false>(p, v); }
 
 // 16-byte write-through store at a wave-uniform base + per-lane byte offset (raw buffer
 // store; the LLVM intrinsic is bound directly, see kernels.hip buf_ld4)
@@ -116,7 +110,7 @@ typedef unsigned long long tl_word;
 enum TlKind : int {
   TL_GEMM = 1, TL_FWD, TL_FWD16, TL_AXK16, TL_DW_PART, TL_DW_PART16, TL_DW_FIN, TL_HEADS,
   TL_SAMPLE_BWD, TL_MT_SAMPLE, TL_GATHER, TL_PER_F1, TL_PER_F2, TL_PER_F2B, TL_PER_F3,
-  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_CHAIN, TL_CHAIN_A, TL_AXK16P, TL_DW_FIN_P, TL_KINDS
+  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_KINDS
 };
 constexpr int kTlEnd = 4;            // first of the ~end slots
 constexpr int kTlEndSlots = 4096;
@@ -124,7 +118,7 @@ constexpr int kTlEndSlots = 4096;
 // of a stamping kernel also record kTlPhases clocks each (SACMI_PHASE), after the end slots;
 // sacmi_profile_timeline then dumps the raw buffer to $SACMI_DIAG_DUMP (tools/phase_dump.py)
 #ifdef SACMI_DIAG_PHASES
-constexpr int kTlPhases = 10;   // 8 / 9: the staged core's first / last slab barrier (wave 0)
+constexpr int kTlPhases = 10;
 #else
 constexpr int kTlPhases = 0;
 #endif
@@ -201,13 +195,10 @@ struct Linear {
 //                the replicas stay identical (the error flags travel with the critic gradient
 //                collective: kDpFlagN)
 // The host reports and clears them (sacmi_step / sacmi_fetch_losses / sacmi_per_sample).
-//   ERR_CHAIN_TIMEOUT  a cohort barrier of the persistent chain kernel (k_chain) timed out
-//                (a workgroup never arrived): the chain's outputs are void, every later step of
-//                the stream is skipped, and the host reports a device error (SACMI_EDEVICE)
 enum ErrBits : int { ERR_NAN_TGT = 1, ERR_NAN_ACT = 2, ERR_NAN_PER = 4, ERR_ABORT = 8,
-                     ERR_REMOTE_SKIP = 16, ERR_REMOTE_ACT = 32, ERR_CHAIN_TIMEOUT = 64 };
+                     ERR_REMOTE_SKIP = 16, ERR_REMOTE_ACT = 32 };
 // an update that sees any of these takes none of its steps
-constexpr int kErrSkipAll = ERR_NAN_TGT | ERR_NAN_PER | ERR_ABORT | ERR_REMOTE_SKIP | ERR_CHAIN_TIMEOUT;
+constexpr int kErrSkipAll = ERR_NAN_TGT | ERR_NAN_PER | ERR_ABORT | ERR_REMOTE_SKIP;
 // ... and these: the critic step stands, the Polyak / actor / alpha steps do not
 constexpr int kErrActLike = ERR_NAN_ACT | ERR_REMOTE_ACT;
 // Data-parallel error flags: kDpFlagN floats right past the critic range of the gradient arena
@@ -281,14 +272,6 @@ struct GemmDesc {
   const float* ax_w;
   float* ax_out;
   int ax_ld;
-  // ax_pre (axk 1, fp32): A already holds u — the producing level stored it (u_out) — so the
-  // K loop reads it as a plain operand (the row prologue, coefficient and mask stay)
-  int ax_pre;
-  // u_out (a forward level with fc3 dot partials, fp32): also store u(b,n) = [C(b,n) > 0] *
-  // dotw[n] (row stride u_ld) — the next dh level's A operand (ax_pre) and the critic weight
-  // gradient's u rows
-  float* u_out;
-  int u_ld;
   // A row-contiguous only: a(m,k) *= a_ksc[k] (per-K scale, e.g. dh2 = coef (x) u for the
   // critic fc2 weight gradient)
   const float* a_ksc;
@@ -415,7 +398,7 @@ struct RowsFuse {
   DevScalars* sc;
   float* dq;                 // [2][B] out: the per-row head gradients (read by later levels)
   float* dq4;                // [2][B][4]: the same, one per 16-byte row (column 0; the fc3
-                             //   weight gradient's A operand: 16-byte rows for the staged core)
+                             //   weight gradient's A operand)
   float* loss_part;          // critic [row blocks][2] squared errors; actor [row blocks]
   // actor: dL/dlog_alpha = -mean(logp_a + te) (sac_imp.py:128-133) from the heads
   // kernel's per-workgroup logp sums (slot 1 of each of n_lp workgroups)
@@ -464,10 +447,6 @@ struct GemmBatch {
   int total_tiles;
   AdamFuse adam;       // used when any desc has epi >= EPI_ADAM
   int has_adam;
-  int adam_wg;         // k_gemm: the workgroup that runs the level's scalar Adam work (losses,
-                       //   alpha step, loss ring, done word) — an extra workgroup past the
-                       //   tiles and rides (launch_gemm), -1: block 0 after its tile, or
-                       //   -2: wave 0 of block 0 before its tile
   RideAlong ride;      // extra workgroups after the tiles
   RowsFuse rows;       // prologue for axk-1 descs
   int bf16;            // 1: bf16 MFMA operands (fp32 loads rounded to bf16 in registers)
@@ -475,16 +454,6 @@ struct GemmBatch {
   int64_t ws_floats;   //   (capacity; launch_gemm falls back when a level needs more)
   tl_word* tl;         // launch timeline slots of this level (kTlPerSite), or null
   int st_wt;           // k_gemm epilogue stores write-through (set by launch_gemm)
-  // the policy heads + sample folded into the level that produces the last policy hidden
-  // layer (k_gemm's fp32 32x64 forward tiles, gemm_level_heads_fold_ok): every policy tile
-  // stores its columns' share of the heads (heads_part), and the last column tile of each
-  // 32-row block to arrive (heads_ticket[row block]: an arrival count, reset by that tile)
-  // sums the shares and runs the sample for the block's rows
-  HeadSampleArgs heads;
-  int heads_desc;      // the (first) policy desc of the level
-  int heads_ndesc;     // policy descs (stacked rows: desc heads_desc + i holds rows i * M ..)
-  int* heads_ticket;   // or null: no fold
-  float* heads_part;   // [row block][column tile][32][2A]: the tiles' shares of the heads
   // data-parallel phase 0's last level: block 0 stores the error flags (kDpFlagN) of
   // *err_word here, before the critic gradient collective (null: none)
   float* err_flags;
@@ -509,56 +478,9 @@ struct SampleBwdArgs {
   tl_word* tl;
 };
 
-// The actor pass of a batch-256-class fused update as ONE persistent launch (k_chain):
-//   L7 (updated critics fc1) -> L8 (fc2 + fc3 dot partials) -> L9 (row prologue + dha1 + dL/da
-//   partials) -> sample-backward tail (dhead, dhp2) -> L12 (dhp1, + the level's rides)
-// (sac_imp.py:116-125 forward / backward through Q(s, a~) and the policy heads).  Every phase
-// is row-local over the batch, so the grid is cut into 8 cohorts of 32 workgroups (blockIdx % 8:
-// one XCD each under the observed round-robin dispatch — for speed only) and cohort c owns batch
-// rows [c B/8, (c+1) B/8) in every phase (k_gemm's XCD-blocked tile placement with a row grid of
-// 8); a cohort barrier (32 arrivals, agent-scope counter) replaces each kernel boundary.
-// Hand-offs follow cdna_hip_programming.md §6 Guideline 16: write-through (sc1) stores, every
-// storing wave's vmcnt(0), one agent-scope arrival per workgroup, sc1 loads of every handed-off
-// byte.  The levels run k_gemm's own workgroup body (kg_body) on the same 32x32 tiles, so the
-// results are those of the launch chain bit for bit.  The argument block lives in device
-// memory (sacmi.hip chain pool: larger than a kernel argument).
-// The critic pass has the same shape (k_chain_a, kind 1): L1 (policy fc1 on the target and
-// actor halves as two row-affine descs, critics fc1) -> L2 (+ critic fc3 dot partials, + the
-// policy heads and sample folded in: the last column tile of each 32-row block) -> L3 (target
-// critics fc1 on [s'|1|a']) -> L4 (+ target dot partials) -> L5 (critic row prologue + dh1)
-// (sac_imp.py:87-113 up to the critics' backward; L6, their weight gradients, needs every row).
-constexpr int kChainLevels = 5;     // kind 0: L7, L8, L9, L12;  kind 1: L1, L2, L3, L4, L5
-constexpr int kChainBars = 4;       // kind 0: after L7, L8, L9, the tail;  kind 1: after L1-L4
-constexpr int kChainCohorts = 8;
-constexpr int kChainGrid = 256;     // workgroups: one per CU
-struct ChainArgs {
-  int kind;
-  GemmBatch lv[kChainLevels];
-  SampleBwdArgs tail;         // the sample backward + dhp2 tail between L9 and L12
-  const float* pa;            // the tail: dL/da partials of L9 (n_pa column blocks)
-  int n_pa;
-  int rows_per_cohort;        // B / 8
-  int tail_groups;            // 8-row groups per cohort (rows_per_cohort / 8)
-  int tail_slabs;             // 64-column slabs of dhp2 (ceil(H / 64))
-  int* sync;                  // [cohort][barrier, ticket], 128-byte strided (k_chain's barriers)
-  int* err;                   // DevScalars::err (ERR_CHAIN_TIMEOUT)
-};
-constexpr int kChainMaxK = 16 * 16 * 2;   // one K pass of the chain bodies (16 waves x 2 groups x 16)
-constexpr int kChainSyncInts = kChainCohorts * (kChainBars + 1) * 32;   // + a launch ticket per cohort
-
 // ---------------------------------------------------------------------------
 // launchers (kernels.hip)
 void launch_gemm(const GemmBatch& batch, hipStream_t s);
-// k_chain over the argument block `dev` (device memory, filled from `host`); host: the same
-// block, validated here.  Returns false (nothing launched) where the device cannot hold the
-// grid at once (fewer than 256 CUs, or the kernel's occupancy below one workgroup per CU)
-bool launch_chain(const ChainArgs& host, const ChainArgs* dev, tl_word* tl, hipStream_t s);
-// whether k_chain_a runs this L2 level (with the heads fold) on its 32x64 tiles
-bool chain_a_l2_ok(const GemmBatch& b);
-bool chain_supported();
-// assign k_chain's tile order to a level: 32x32 tiles, XCD-blocked with a row grid of 8
-// (cohort c = tile & 7 owns row tiles [c tm / 8, (c+1) tm / 8)); false where it does not apply
-bool chain_assign_tiles(GemmBatch& b, int tn = 32);
 void launch_heads_sample(const HeadSampleArgs& a, hipStream_t s);
 
 // select_action for one state (sacmi_act, n = 1): the policy forward as GEMVs.
@@ -588,10 +510,7 @@ struct ActHeadsArgs {
 };
 void launch_act_heads(const ActHeadsArgs& a, hipStream_t s);
 // rows per heads workgroup (and per log-prob partial): 32 from 8192 stacked rows on
-#ifndef SACMI_HEADS_TM32
-#define SACMI_HEADS_TM32 1
-#endif
-inline int heads_rows_per_wg(int rows) { return SACMI_HEADS_TM32 && rows >= 8192 ? 32 : 16; }
+inline int heads_rows_per_wg(int rows) { return rows >= 8192 ? 32 : 16; }
 // dst[i] = bf16(src[i]) (round to nearest even), the parameter shadows of bf16 mode
 void launch_to_bf16(unsigned short* dst, const float* src, int64_t n, hipStream_t s);
 void launch_gemm_sample_bwd(const GemmDesc& d, const SampleBwdArgs& a, hipStream_t s);
@@ -602,10 +521,6 @@ void launch_sample_bwd_tail(const float* pa, int n_pa, const SampleBwdArgs& a, h
 bool gemm_level_on_axk16(const GemmBatch& b);
 // whether launch_gemm runs this axk-1 level on the tiles that compute dL/da partials
 bool gemm_level_pa_capable(const GemmBatch& b);
-// whether launch_gemm runs this forward level on the tiles that can fold the policy heads
-// (GemmBatch::heads): fp32 32x64 k_gemm tiles, write-through stores, 2A <= 48
-bool gemm_level_heads_fold_ok(const GemmBatch& b, int A);
-constexpr int kHeadsFoldTM = 32;   // rows per folded heads block (one 32-row tile block)
 
 
 constexpr int kMaxAdamSegs = 8;

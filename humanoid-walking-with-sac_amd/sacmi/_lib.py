@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACMI_LIB_PATH") or os.path.join(_HERE, "libsacmi.so")   # override: tuning builds
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_f32p = ctypes.POINTER(ctypes.c_float)
 c_f64p = ctypes.POINTER(ctypes.c_double)
@@ -86,8 +86,8 @@ _PROTOS = {
                             ctypes.c_int32, ctypes.c_int32],
     "sacmi_step_ride_possible": [c_vp, ctypes.c_int32, c_i32p],
     "sacmi_step_act16": [c_vp, ctypes.c_int32, c_i32p],
-    "sacmi_step_chained": [c_vp, ctypes.c_int32, c_i32p],
     "sacmi_read_activation": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_f32p, ctypes.c_int64],
+    "sacmi_read_batch": [c_vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), c_f32p, ctypes.c_int64],
     "sacmi_fetch_losses": [c_vp, c_f32p, ctypes.c_int32, c_i32p],
     "sacmi_step_phase": [c_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float],
     "sacmi_grad_buffer": [c_vp, ctypes.c_int, ctypes.POINTER(c_vp), c_i64p],
@@ -122,7 +122,7 @@ TL_KINDS = {1: "k_gemm", 2: "k_fwd", 3: "k_fwd16", 4: "k_axk16", 5: "k_dw_part",
             7: "k_dw_fin", 8: "k_heads_sample", 9: "k_gemm_sample_bwd", 10: "k_mt_sample",
             11: "k_gather", 12: "k_per_f1", 13: "k_per_f2", 14: "k_per_f2b", 15: "k_per_f3",
             16: "k_per_f4", 17: "per_unfused", 18: "k_adam", 19: "k_sample_bwd_tail",
-            20: "k_fwd16p", 21: "k_chain", 22: "k_chain_a", 23: "k_axk16p", 24: "k_dw_fin_p"}
+            20: "k_fwd16p"}
 EXPORTS = tuple(_PROTOS) + ("sacmi_abi_version", "sacmi_last_error")
 
 _lib = None

@@ -306,12 +306,16 @@ class Context:
         L.call("sacmi_read_activation", self._h, int(pass_), int(layer), int(batch), L.fptr(out), out.size)
         return out.reshape((2 * batch, H) if pass_ == 3 else (2, batch, H))
 
-    def chained(self, batch: int) -> bool:
-        """Whether fused updates of this batch run the actor pass as one persistent launch
-        (k_chain, sacmi.h sacmi_step_chained)."""
-        out = ctypes.c_int32()
-        L.call("sacmi_step_chained", self._h, int(batch), ctypes.byref(out))
-        return bool(out.value)
+    def read_batch(self, batch: int):
+        """(idx[batch] int64, eps[2 * batch, A] float32) of the last device-sampled update of
+        `batch` rows in batch set 0 (sacmi.h sacmi_read_batch): eps rows [0, batch) noise of
+        policy.sample(next_state), rows [batch, 2 batch) of policy.sample(state)."""
+        A = self.cfg.action_dim
+        idx = np.zeros(batch, np.int64)
+        eps = np.zeros(2 * batch * A, np.float32)
+        L.call("sacmi_read_batch", self._h, int(batch),
+               idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), L.fptr(eps), eps.size)
+        return idx, eps.reshape(2 * batch, A)
 
     def act16(self, batch: int) -> bool:
         """Whether updates of this batch keep their activations in bf16 (sacmi.h)."""

@@ -137,6 +137,11 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     want_roof = not getattr(args, "no_roofline", False)
     sim = int(getattr(args, "dp_sim_world", 0) or 0)
     if sim:                                         # one GPU stands in for `sim` ranks
+        # rank 0's work only, in BOTH optimizer forms: the sharded form's Adam on rank 0's
+        # chunk (SACMI_DP_LOOPBACK_ONE_RANK, read at each capture) — without it the loopback
+        # steps all `sim` chunks in turn, sim x a rank's optimizer work (round 5's dp_form_ab
+        # legs differed by 42 % for that reason alone)
+        os.environ["SACMI_DP_LOOPBACK_ONE_RANK"] = "1"
         ctx.dp_loopback_init(sim)
     elif native or want_roof:
         _native_comm(ctx, rank, device)
@@ -200,29 +205,47 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     if native and phases and os.environ.get("SACMI_BENCH_DP_FORM_AB", "1") != "0":
         was = ctx.dp_sharded()
         form_ab = {"form": "sharded" if not was else "all-reduce"}
-        try:   # (a failure here is reported in the line, not instead of it)
+        # the switch and the first launch of each graph (its capture) are where one rank can
+        # fail alone: every rank learns the outcome before any collective of the other form
+        # runs, so all go on or all skip together (a rank that raised while the others wait
+        # inside a collective would hang them)
+        err = None
+        try:
             ctx.dp_set_sharded(not was)
-            for n in sizes:
-                ctx.step_dp(args.batch, n)
-            run(args.warmup)
-            torch.cuda.synchronize()
-            adts = [window() for _ in range(max(3, args.windows // 4))]
-            adt = float(np.median(adts))
-            form_ab.update({
-                "ms_per_step": round(1e3 * adt / args.steps, 4),
-                "value": round(world * args.steps / adt, 2),
-                "windows": len(adts),
-                "replicas_bitwise_equal": replicas_equal(),
-            })
-            if want_roof:
-                info = B.timeline_roofline(ctx, args.batch, per_launch, data_parallel=True)
-                form_ab["allreduce_us_per_step"] = round(info["allreduce_us"] / per_launch, 2)
-                form_ab["step_us_timeline"] = round(info["graph_us"] / per_launch, 2)
-            # (leaving the sharded form gathers the moments: a collective)
-            ctx.dp_set_sharded(was)
-            torch.cuda.synchronize()
-        except Exception as e:   # noqa: BLE001 — the other form's failure is data for the line
-            form_ab["error"] = f"{type(e).__name__}: {e}"[:300]
+        except Exception as e:   # noqa: BLE001
+            err = e
+        bad = torch.tensor([0.0 if err is None else 1.0], device=device)
+        dist.all_reduce(bad)
+        if float(bad.item()) > 0:
+            form_ab["error"] = (f"{type(err).__name__}: {err}" if err is not None
+                                else "another rank could not switch")[:300]
+            if err is None:
+                ctx.dp_set_sharded(was)       # (leaving the sharded form: a collective — every
+                                              #  rank that switched does this)
+        else:
+            # (a failure from here on, inside the other form's collectives, is re-raised: the
+            # ranks cannot be kept in step past it; the original form is restored first)
+            try:
+                for n in sizes:
+                    ctx.step_dp(args.batch, n)
+                run(args.warmup)
+                torch.cuda.synchronize()
+                adts = [window() for _ in range(max(3, args.windows // 4))]
+                adt = float(np.median(adts))
+                form_ab.update({
+                    "ms_per_step": round(1e3 * adt / args.steps, 4),
+                    "value": round(world * args.steps / adt, 2),
+                    "windows": len(adts),
+                    "replicas_bitwise_equal": replicas_equal(),
+                })
+                if want_roof:
+                    info = B.timeline_roofline(ctx, args.batch, per_launch, data_parallel=True)
+                    form_ab["allreduce_us_per_step"] = round(info["allreduce_us"] / per_launch, 2)
+                    form_ab["step_us_timeline"] = round(info["graph_us"] / per_launch, 2)
+            finally:
+                # (leaving the sharded form gathers the moments: a collective)
+                ctx.dp_set_sharded(was)
+                torch.cuda.synchronize()
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         n_cpu = min(fill * world, 1_000_000)
@@ -260,7 +283,8 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
             "simulated_world": sim or None,
             "simulated_note": (f"one GPU runs rank 0's sequence of a {sim}-rank job, collectives "
                                "emulated in place (no transfers): the per-rank work minus the "
-                               "collectives" if sim else None),
+                               "collectives (the sharded form's Adam on rank 0's chunk only, "
+                               "SACMI_DP_LOOPBACK_ONE_RANK)" if sim else None),
             "mfma_util_step": round(flops * value / 1e12 / peak / world, 4),
             "replicas_bitwise_equal": replicas_ok,
             "dp_form_ab": form_ab,

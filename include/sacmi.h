@@ -38,7 +38,9 @@
 extern "C" {
 #endif
 
-#define SACMI_ABI_VERSION 2
+/* ABI 3 (round 6): sacmi_step_chained removed (the persistent-chain kernels are gone);
+ * sacmi_grad_buffer(0)'s view documents its trailing error-flag words (kDpFlagN). */
+#define SACMI_ABI_VERSION 3
 
 enum sacmi_status {
   SACMI_OK = 0,
@@ -234,12 +236,6 @@ int sacmi_step_ride_possible(sacmi_ctx* ctx, int32_t batch, int32_t* out);
  * batch-4096 class: hidden layers, minibatch rows and sampled actions; the policy heads
  * then read a bf16-rounded input), else 0. */
 int sacmi_step_act16(sacmi_ctx* ctx, int32_t batch, int32_t* out);
-/* 1 when the fused updates of this batch run their actor pass (sac_imp.py:116-125: the
- * updated critics' forward, dL/da, the policy heads' and hidden layers' backward) as ONE
- * persistent launch with cohort barriers instead of five launches (batch 256, fp32, two
- * hidden layers, a device with >= 256 CUs; SACMI_NO_CHAIN at creation: off), else 0.  The
- * results are the same bits either way. */
-int sacmi_step_chained(sacmi_ctx* ctx, int32_t batch, int32_t* out);
 /* Test hook: the hidden activations (post-ReLU) the last update of `batch` rows left in
  * HBM, hidden layer `layer` (0-based) of pass
  *   0  the critics on (s, a)            -> [2][batch][hidden]  (q1, then q2)
@@ -251,6 +247,18 @@ int sacmi_step_chained(sacmi_ctx* ctx, int32_t batch, int32_t* out);
  * bf16-stored activations (sacmi_step_act16). */
 int sacmi_read_activation(sacmi_ctx* ctx, int32_t pass, int32_t layer, int32_t batch, float* out,
                           int64_t numel);
+/* Test hook: the minibatch of the last device-sampled update of `batch` rows that used batch
+ * set 0 (every single update, and the first of a multi-update graph): its replay indices
+ * (idx[batch]: deque positions, or ring slots for PER) and the policy noise it drew
+ * (eps[2 * batch * action_dim]: rows [0, batch) for policy.sample(next_state), rows [batch,
+ * 2 batch) for policy.sample(state), sac_imp.py:89,116). */
+int sacmi_read_batch(sacmi_ctx* ctx, int32_t batch, int64_t* idx, float* eps, int64_t eps_numel);
+/* The gradient range a phase-split update's collective covers, in the gradient arena:
+ * which = 0 the critic range [q1 | q2] FOLLOWED BY 4 error-flag floats (kDpFlagN: flag 0 =
+ * this update saw a skip-all non-finite input, flag 1 = an actor-batch one, 2-3 zero) — they
+ * travel with the critic all-reduce so that every rank voids the same steps; a grad norm or
+ * clip over this view must exclude the last 4 floats.  which = 1 the actor range [policy |
+ * log_alpha]. */
 int sacmi_grad_buffer(sacmi_ctx* ctx, int which, void** device_ptr, int64_t* numel);
 /* Gradient arena size (floats) and adoption of a caller-allocated device buffer of
  * that size (e.g. a torch tensor), so collectives run on it in place.  Must be on the

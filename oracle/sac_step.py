@@ -313,7 +313,22 @@ class OracleSAC:
         grads["q2"] = {k: v.grad.detach().clone() for k, v in Q2.items()}
         self.opt["q2"].step()
 
-        new_a, logp = _policy_sample(P, state, e2, sc, bi, "pi_s")
+        policy_loss = self._actor(state, e2, grads)
+        with torch.no_grad():
+            tau = cfg.tau
+            for src, dst in (("q1", "q1_target"), ("q2", "q2_target")):
+                for k in q_keys(cfg.n_hidden):
+                    t = self.nets[dst][k]
+                    t.copy_(t * (1.0 - tau) + self.nets[src][k] * tau)
+        self.last_grads = grads
+        return {"q1_loss": q1_loss.item(), "q2_loss": q2_loss.item(),
+                "policy_loss": policy_loss.item()}
+
+    def _actor(self, state, e2, grads):
+        """The actor and alpha blocks (sac_imp.py:116-135) on the agent's current critics."""
+        cfg = self.cfg
+        P, Q1, Q2 = self.nets["policy"], self.nets["q1"], self.nets["q2"]
+        new_a, logp = _policy_sample(P, state, e2, cfg.action_scale, cfg.action_bias, "pi_s")
         q_new = torch.min(_q_forward(Q1, state, new_a, "q1a"), _q_forward(Q2, state, new_a, "q2a"))
         policy_loss = (self.alpha * logp - q_new).mean()
         self.opt["policy"].zero_grad(); policy_loss.backward()
@@ -326,15 +341,17 @@ class OracleSAC:
             grads["log_alpha"] = self.log_alpha.grad.detach().clone()
             self.opt["alpha"].step()
             self.alpha = self.log_alpha.exp()
-        with torch.no_grad():
-            tau = cfg.tau
-            for src, dst in (("q1", "q1_target"), ("q2", "q2_target")):
-                for k in q_keys(cfg.n_hidden):
-                    t = self.nets[dst][k]
-                    t.copy_(t * (1.0 - tau) + self.nets[src][k] * tau)
+        return policy_loss
+
+    def actor_step(self, s, eps2) -> float:
+        """The actor and alpha blocks of one update_parameters call alone (sac_imp.py:116-135),
+        on the agent's CURRENT critics: the reference for an update whose critic step happened
+        elsewhere (the sharded data-parallel chunk tests load the partly stepped critics)."""
+        T = lambda x: torch.as_tensor(np.asarray(x, dtype=np.float32)).to(self.dtype)
+        grads = {}
+        loss = self._actor(T(s), T(eps2), grads)
         self.last_grads = grads
-        return {"q1_loss": q1_loss.item(), "q2_loss": q2_loss.item(),
-                "policy_loss": policy_loss.item()}
+        return loss.item()
 
     # -- snapshots ------------------------------------------------------------
     def state(self) -> dict:

@@ -5,8 +5,3 @@ cd "$(dirname "$0")/.."
 F="-O3 -std=c++17 --offload-arch=gfx950 -Ihumanoid-walking-with-sac_amd/csrc -Iinclude"
 /opt/rocm/bin/hipcc $F tools/gemm_bench.hip -o tools/gemm_bench
 /opt/rocm/bin/hipcc $F -DSACMI_DIAG_STAMPS tools/gemm_bench.hip -o tools/gemm_stamps
-/opt/rocm/bin/hipcc $F -DSACMI_EXP_NOLOAD tools/gemm_bench.hip -o tools/gemm_bench_noload &
-/opt/rocm/bin/hipcc $F -DSACMI_FETCH_SADDR=1 tools/gemm_bench.hip -o tools/gemm_bench_s1 &
-/opt/rocm/bin/hipcc $F -DSACMI_FETCH_SADDR=3 tools/gemm_bench.hip -o tools/gemm_bench_s3 &
-wait
-

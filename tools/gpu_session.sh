@@ -8,7 +8,7 @@
 #   dp8      the data-parallel sequence at a simulated world of 8, both optimizer forms
 #   dpab     the data-parallel bench at one rank over real RCCL with the phase sequence forced
 #            (SACMI_DP_PHASES_AT_WORLD1): the line's form and the other one (dp_form_ab)
-# usage: STEPS="tests ab" AB_ENV="SACMI_CHAIN=1" TAG=r5b bash tools/gpu_session.sh
+# usage: STEPS="tests ab" AB_ENV="SACMI_NO_GRAPH=1" TAG=r6b bash tools/gpu_session.sh
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -40,7 +40,7 @@ for step in ${STEPS:-tests smoke configs}; do
     dp8)
       SACMI_DP_SHARD=1 SACMI_DP_LOOPBACK_ONE_RANK=1 timeout -k 10 300 $B --force-dp --dp-sim-world 8 --steps 20 \
         > $O/dp8_shard.json 2> $O/dp8_shard.err || { tail $O/dp8_shard.err; exit 1; }
-      SACMI_DP_SHARD=0 timeout -k 10 300 $B --force-dp --dp-sim-world 8 --steps 20 > $O/dp8_ar.json 2> $O/dp8_ar.err || { tail $O/dp8_ar.err; exit 1; }
+      SACMI_DP_SHARD=0 SACMI_DP_LOOPBACK_ONE_RANK=1 timeout -k 10 300 $B --force-dp --dp-sim-world 8 --steps 20 > $O/dp8_ar.json 2> $O/dp8_ar.err || { tail $O/dp8_ar.err; exit 1; }
       line $O/dp8_shard.json; line $O/dp8_ar.json
       python3 -c "import json; [print(f, json.load(open(f))['dp_form_ab']) for f in ('$O/dp8_shard.json', '$O/dp8_ar.json')]" ;;
     dpab)

@@ -4,7 +4,7 @@ a -DSACMI_DIAG_PHASES build).  k_gemm phases (wave 0 of the first 256 workgroups
 0 entry, 1 setup done (before the K loop), 2 wave 0's K loop + MFMAs done, 3 every wave
 done (the pre-epilogue barrier; incl. the row prologue), 4 epilogue stores issued, 5 exit;
 6 / 7 the last wave's entry and K-loop end (lastin: its entry after wave 0's); 8 / 9 the
-staged core's first / last slab, or (register-direct core) the desc landed / the tile placed.
+desc landed / the tile placed.
 usage: tools/phase_dump.py dump.bin"""
 import struct
 import sys
@@ -13,30 +13,6 @@ import numpy as np
 
 
 SLOW = 0
-
-
-def chain_phases(name, x, words, nph):
-    """k_chain / k_chain_a: wave 0's clock at entry (slot 0), at the end of phase i (slot i+1)
-    and right after the wait of barrier b (slot 6+b, the barrier that opens phase b+1, inside
-    its body: the weights' loads went out before it).  Per phase: the medians / maxima of
-    [phase start -> barrier passed] (weights + wait) and [barrier passed -> phase end]."""
-    p0 = words - 256 * nph
-    ph = x[p0:p0 + 256 * nph].reshape(256, nph).astype(np.int64)
-    ph = ph[ph[:, 0] > 0]
-    if len(ph) == 0 or nph < 10:
-        return
-    start = int(x[0])
-    us = lambda v: v * 0.01
-    print(f"{name}: entry med {us(np.median(ph[:, 0] - start)):.2f} max {us(np.max(ph[:, 0] - start)):.2f} us")
-    w0 = us(ph[:, 1] - ph[:, 0])
-    print(f"  phase 0: work med {np.median(w0):6.2f} max {np.max(w0):6.2f} | end (last) {us(np.max(ph[:, 1] - start)):7.2f}")
-    for i in range(1, 5):
-        pre = us(ph[:, 5 + i] - ph[:, i])
-        post = us(ph[:, i + 1] - ph[:, 5 + i])
-        print(f"  phase {i}: to barrier med {np.median(pre):6.2f} max {np.max(pre):6.2f} | "
-              f"after med {np.median(post):6.2f} max {np.max(post):6.2f} | "
-              f"barrier passed (last) {us(np.max(ph[:, 5 + i] - start)):7.2f} | end (last) {us(np.max(ph[:, i + 1] - start)):7.2f}")
-    print(f"  exit med {us(np.median(ph[:, 5] - start)):.2f} max {us(np.max(ph[:, 5] - start)):.2f} us")
 
 
 def main(path):
@@ -49,9 +25,6 @@ def main(path):
     for s in range(sites):
         k = 0
         x = w[s, k]
-        if x[0] != 2**64 - 1 and int(x[2]) in (21, 22):   # k_chain / k_chain_a (TL_CHAIN, TL_CHAIN_A)
-            chain_phases(names[s], x, words, nph)
-            continue
         if x[0] == 2**64 - 1 or int(x[2]) != 1:      # k_gemm only (TL_GEMM)
             continue
         p0 = words - 256 * nph                        # phase words follow the end slots

@@ -12,8 +12,7 @@ import sys
 def main(path):
     rows = list(csv.DictReader(open(path)))
     tot_ns = calls = 0
-    level = ("sacmi::k_gemm<", "sacmi::k_fwd<", "sacmi::k_fwd16<", "sacmi::k_fwd16p<", "sacmi::k_axk16<", "sacmi::k_axk16p<", "sacmi::k_dw_part",
-             "sacmi::k_chain")
+    level = ("sacmi::k_gemm<", "sacmi::k_fwd16<", "sacmi::k_fwd16p<", "sacmi::k_axk16<", "sacmi::k_dw_part")
     for r in rows:
         name, n, avg = r["Name"], int(r["Calls"]), float(r["AverageNs"])
         print(f"{name[:72]:72s} {n:7d} {avg / 1e3:9.2f} us  {float(r['Percentage']):6.2f}%")
@@ -23,7 +22,7 @@ def main(path):
         elif "sacmi::k_dw_fin" in name:
             tot_ns += avg * n                   # second kernel of a split-K level
     if calls:
-        print(f"\nGEMM levels (k_gemm all tile configs + k_fwd* + k_axk16 + k_dw_part*/k_dw_fin + k_chain): "
+        print(f"\nGEMM levels (k_gemm all tile configs + k_fwd16* + k_axk16 + k_dw_part16/k_dw_fin): "
               f"{calls} levels, mean {tot_ns / calls / 1e3:.3f} us")
 
 
