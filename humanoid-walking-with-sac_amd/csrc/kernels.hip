@@ -3022,6 +3022,37 @@ __device__ __forceinline__ float wave_sum(float v) {
 // and 16-byte aligned), + optional Polyak target update (sac_imp.py:146-152) + loss
 // finalisation + the scalar log_alpha step and alpha = exp(log_alpha)
 // (sac_imp.py:128-135) + the loss ring slot of this update.
+// The scalar work runs on a workgroup of its own, the grid's last, from the kernel's start:
+// its inputs (loss partials, log_alpha's gradient and state, the scalars) come from earlier
+// kernels and no element reads what it writes — after block 0's elements it put a chain of
+// dependent round trips at the end of the kernel (the fused levels moved it the same way,
+// adam_block0_wave).  The element blocks are the grid's first gridDim.x - 1.
+__device__ __forceinline__ void adam_scalar_tail(const AdamArgs& a, float om_b1, float om_b2) {
+  if (threadIdx.x == 0 && a.log_alpha_idx >= 0 && a.auto_entropy) {
+    const AdamScalars k = adam_scalars(a, 3);
+    const int64_t i = a.log_alpha_idx;
+    float p = a.p[i], m = a.m[i], v = a.v[i];
+    adam_elem(p, m, v, a.g[i] * a.grad_scale, om_b1, a.beta2, om_b2, a.eps, k);
+    a.p[i] = p; a.m[i] = m; a.v[i] = v;
+    a.sc->alpha = expf(p);
+    a.sc->alpha_is_tensor = 1;
+  }
+  if (threadIdx.x < a.n_losses) {
+    float s = 0.f;
+    for (int w = 0; w < a.n_part; ++w) s += a.loss_part[w * a.n_losses + threadIdx.x];
+    a.sc->losses[a.loss_slot0 + threadIdx.x] = s / a.loss_div;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && a.loss_ring) {
+    const int64_t pos = a.sc->loss_ring_pos;
+    const int64_t q = pos % a.ring;
+    a.loss_ring[q * 3 + 0] = a.sc->losses[0];
+    a.loss_ring[q * 3 + 1] = a.sc->losses[1];
+    a.loss_ring[q * 3 + 2] = a.sc->losses[2];
+    a.sc->loss_ring_pos = pos + 1;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
   const TlMark tl_mark(a.tl, TL_ADAM);
   __shared__ AdamScalars s_k[kMaxAdamSegs];
@@ -3048,6 +3079,11 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
   // a non-finite policy sample / PER draw of this update (ErrBits, see k_gemm): no step,
   // or (critic, actor-batch NaN) the step without Polyak
   const int err = s_err;
+  const unsigned nel = gridDim.x - 1;   // element workgroups; the last one: the scalar work
+  if (blockIdx.x == nel) {
+    if (!err) adam_scalar_tail(a, om_b1, om_b2);
+    return;
+  }
   if (err & a.err_skip) return;
   const bool pol = a.tgt && (err & a.err_nopolyak) == 0;
   const int64_t total4 = s_prefix[a.nseg];
@@ -3057,7 +3093,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
                rV = make_rsrc(a.v, 0x7fffffffu),
                rT = make_rsrc(a.tgt ? a.tgt : a.p, a.tgt ? 0x7fffffffu : 0u);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total4;
-       e += (int64_t)gridDim.x * blockDim.x) {
+       e += (int64_t)nel * blockDim.x) {
     int sg = 0;
     for (int q = 1; q < a.nseg; ++q)
       if (e >= s_prefix[q]) sg = q;
@@ -3095,30 +3131,6 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
       }
     }
   }
-  if (blockIdx.x != 0 || err) return;
-  if (threadIdx.x == 0 && a.log_alpha_idx >= 0 && a.auto_entropy) {
-    const AdamScalars k = adam_scalars(a, 3);
-    const int64_t i = a.log_alpha_idx;
-    float p = a.p[i], m = a.m[i], v = a.v[i];
-    adam_elem(p, m, v, a.g[i] * a.grad_scale, om_b1, a.beta2, om_b2, a.eps, k);
-    a.p[i] = p; a.m[i] = m; a.v[i] = v;
-    a.sc->alpha = expf(p);
-    a.sc->alpha_is_tensor = 1;
-  }
-  if (threadIdx.x < a.n_losses) {
-    float s = 0.f;
-    for (int w = 0; w < a.n_part; ++w) s += a.loss_part[w * a.n_losses + threadIdx.x];
-    a.sc->losses[a.loss_slot0 + threadIdx.x] = s / a.loss_div;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && a.loss_ring) {
-    const int64_t pos = a.sc->loss_ring_pos;
-    const int64_t q = pos % a.ring;
-    a.loss_ring[q * 3 + 0] = a.sc->losses[0];
-    a.loss_ring[q * 3 + 1] = a.sc->losses[1];
-    a.loss_ring[q * 3 + 2] = a.sc->losses[2];
-    a.sc->loss_ring_pos = pos + 1;
-  }
 }
 
 void launch_adam(const AdamArgs& a, hipStream_t s) {
@@ -3127,7 +3139,8 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
   int64_t blocks = (total4 + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  // + the scalar-work workgroup (the grid's last)
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks + 1), dim3(256), 0, s, a);
   HIP_LAUNCH_CHECK();
 }
 

@@ -8,6 +8,9 @@
 #   dp8      the data-parallel sequence at a simulated world of 8, both optimizer forms
 #   dpab     the data-parallel bench at one rank over real RCCL with the phase sequence forced
 #            (SACMI_DP_PHASES_AT_WORLD1): the line's form and the other one (dp_form_ab)
+#   pmcb     the bound-analysis PMC passes (tools/gpu_pmc_bound.sh) of CONFIGS_PMCB ("5 3")
+#   prof     the round's profile set (tools/gpu_profile.sh: PMC passes of CONFIGS, the
+#            rocprofv3 kernel-trace summary of the driver's config-2 command)
 # usage: STEPS="tests ab" AB_ENV="SACMI_NO_GRAPH=1" TAG=r6b bash tools/gpu_session.sh
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -48,6 +51,13 @@ for step in ${STEPS:-tests smoke configs}; do
         || { tail $O/dp1_ab.err; exit 1; }
       line $O/dp1_ab.json
       python3 -c "import json; d=json.load(open('$O/dp1_ab.json')); print(d['dp_optimizer_step'], d['replicas_bitwise_equal'], d['dp_form_ab'])" ;;
+    pmcb)
+      for c in ${CONFIGS_PMCB:-5 3}; do
+        bash tools/gpu_pmc_bound.sh c$c --config $c --steps 20 --warmup 5 --profile-only || exit 1
+        cp gpurun_out/pmc_bound_c$c.json gpurun_out/pmc_bound_c$c.txt $O/ || exit 1
+      done ;;
+    prof)
+      TAG=${TAG:-session} bash tools/gpu_profile.sh || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
