@@ -925,16 +925,21 @@ static AdamArgs dp_adam_args(sacmi_ctx* c, bool critic, int B, float grad_scale,
   return ad;
 }
 
-// The Adam moments are whole on this rank: every read of them and every update that steps
-// them from this rank's M, V (any update but the sharded data-parallel sequence) needs it
+// The Adam moments are whole on this rank: every update that steps them from this rank's M, V
+// (any update but the sharded data-parallel sequence) needs it.  (A loopback one-rank timing
+// context, moments_partial, may go on stepping: its state is a timing artifact either way;
+// reads of it raise, require_moments_readable.)
 static void require_moments_whole(const sacmi_ctx* c) {
-  REQUIRE(!c->moments_partial, SACMI_ESTATE,
-          "the Adam moments of this context were left partly stepped by a loopback one-rank timing "
-          "run (SACMI_DP_LOOPBACK_ONE_RANK: only rank 0's chunks were stepped); they cannot be read "
-          "or stepped any more");
   REQUIRE(!c->moments_sharded, SACMI_ESTATE,
           "the Adam moments are sharded across the data-parallel ranks (sharded optimizer step): "
           "call sacmi_dp_sync_state on every rank before reading or writing them");
+}
+static void require_moments_readable(const sacmi_ctx* c) {
+  REQUIRE(!c->moments_partial, SACMI_ESTATE,
+          "the Adam moments of this context were left partly stepped by a loopback one-rank timing "
+          "run (SACMI_DP_LOOPBACK_ONE_RANK: only rank 0's chunks were stepped); they cannot be read "
+          "any more");
+  require_moments_whole(c);
 }
 
 // parity: which batch buffer set this update uses; have_batch: its indices and rows
@@ -1900,7 +1905,7 @@ int sacmi_tensor_numel(sacmi_ctx* c, int net, int layer, int part, int64_t* nume
 
 static float* slot_base(sacmi_ctx* c, int slot, int net) {
   const bool target = net == SACMI_Q1_TARGET || net == SACMI_Q2_TARGET;
-  if (slot == SACMI_SLOT_ADAM_M || slot == SACMI_SLOT_ADAM_V) require_moments_whole(c);
+  if (slot == SACMI_SLOT_ADAM_M || slot == SACMI_SLOT_ADAM_V) require_moments_readable(c);
   if (target) {
     REQUIRE(slot == SACMI_SLOT_PARAM, SACMI_EVALUE, "target nets only have parameters");
     return c->T.p - c->q_begin;
@@ -1975,8 +1980,8 @@ static void arena_scalar(sacmi_ctx* c, float* arena, int64_t idx, const double* 
 static void scalar_io(sacmi_ctx* c, int which, const double* in, double* out) {
   switch (which) {
     case SACMI_S_LOG_ALPHA: arena_scalar(c, c->P.p, c->la_idx, in, out); return;
-    case SACMI_S_ADAM_M_LOG_ALPHA: require_moments_whole(c); arena_scalar(c, c->M.p, c->la_idx, in, out); return;
-    case SACMI_S_ADAM_V_LOG_ALPHA: require_moments_whole(c); arena_scalar(c, c->V.p, c->la_idx, in, out); return;
+    case SACMI_S_ADAM_M_LOG_ALPHA: require_moments_readable(c); arena_scalar(c, c->M.p, c->la_idx, in, out); return;
+    case SACMI_S_ADAM_V_LOG_ALPHA: require_moments_readable(c); arena_scalar(c, c->V.p, c->la_idx, in, out); return;
     case SACMI_S_GRAD_LOG_ALPHA: arena_scalar(c, c->G.p, c->la_idx, in, out); return;
     case SACMI_S_GRAPH_COUNT:
       REQUIRE(!in, SACMI_EVALUE, "the graph count is read-only");
