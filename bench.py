@@ -393,10 +393,11 @@ def parse_args(argv=None):
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel path even at world size 1 (overhead check)")
     ap.add_argument("--dp-sim-world", type=int, default=0,
-                    help="with --force-dp: one GPU runs the data-parallel sequence of a W-rank job "
-                         "through the loopback hook (collectives emulated in place; with "
-                         "SACMI_DP_LOOPBACK_ONE_RANK=1 only rank 0's optimizer chunk: that rank's "
-                         "work minus the collectives)")
+                    help="with --force-dp: one GPU runs rank 0's data-parallel sequence of a "
+                         "W-rank job through the loopback hook in its one-rank timing mode "
+                         "(SACMI_DP_LOOPBACK_ONE_RANK: the sharded Adam on rank 0's chunk, the "
+                         "collectives returning the rank's own gradient, no stand-in kernels): "
+                         "that rank's work minus the collectives")
     ap.add_argument("--dp-native", action="store_true",
                     help="(default) data parallel through sacmi_step_dp: the library issues "
                          "the RCCL all-reduces inside its own captured graph")

@@ -1571,6 +1571,16 @@ static bool dp_shard_default(int world) {
   return SACMI_DP_SHARD_DEFAULT && world >= 2 && world <= kMaxShardWorld;
 }
 
+// The loopback's one-rank timing mode (SACMI_DP_LOOPBACK_ONE_RANK, read at each capture): the
+// sequence of ONE rank of a `world`-rank job minus its collectives — the sharded Adam on rank 0's
+// chunk only, and no stand-in kernels for the collectives (a real rank moves its bytes over xGMI
+// instead: the driver's N > 1 lines).  Each collective then returns this rank's own gradient, so
+// Adam applies no 1/world (grad_scale 1): rank 0's chunks take exactly the fused update's values
+// at any world (test_dp_sharded_one_rank_chunks)
+static bool loopback_one_rank(const sacmi_ctx* c) {
+  return c->dp_loopback && std::getenv("SACMI_DP_LOOPBACK_ONE_RANK") != nullptr;
+}
+
 static int64_t shard_chunk(int64_t n, int world) {
   return round_up64((n + world - 1) / world, kShardAlign);
 }
@@ -1588,7 +1598,7 @@ static void dp_shard_adam(sacmi_ctx* c, bool critic, int B, int r, bool use_ring
   const int W = c->dp_world;
   const int64_t b = critic ? c->q_begin : c->pi_begin, e = critic ? c->q_end : c->total;
   const int64_t ch = shard_chunk(e - b, W), lo = b + r * ch, hi = std::min(e, lo + ch);
-  AdamArgs ad = dp_adam_args(c, critic, B, 1.f / (float)W, use_ring);
+  AdamArgs ad = dp_adam_args(c, critic, B, loopback_one_rank(c) ? 1.f : 1.f / (float)W, use_ring);
   ad.tgt = nullptr; ad.tgth = nullptr;   // Polyak: its own pass over the gathered critics
   const AdamArgs full = ad;
   ad.nseg = 0; ad.total = 0;
@@ -1622,17 +1632,18 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
     // group with the reduce-scatter (one launch)
     const bool group = critic && !c->dp_loopback;
     if (group) CHECK_RCCL(rccl().group_start());
+    const bool one = loopback_one_rank(c);
     if (critic) {
       (void)mark(c, "allreduce_error_flags");
       float* f = c->dp_flags.p;
-      if (c->dp_loopback) loopback_flags(c, f, s);
-      else CHECK_RCCL(rccl().all_reduce(f, f, (size_t)kDpFlagN, ncclFloat32, ncclSum, c->comm, s));
+      if (c->dp_loopback && !one) loopback_flags(c, f, s);
+      else if (!c->dp_loopback) CHECK_RCCL(rccl().all_reduce(f, f, (size_t)kDpFlagN, ncclFloat32, ncclSum, c->comm, s));
     }
     (void)mark(c, critic ? "reduce_scatter_critic_grads" : "reduce_scatter_actor_grads");
     // (loopback: the whole span the collective covers, the last chunk's reach included)
     check_span(g, ch * W - 1, "reduce-scatter span");
     if (c->dp_loopback) {
-      scale_checked(g, ch * W, (float)W, s);
+      if (!one) scale_checked(g, ch * W, (float)W, s);
     } else {
       CHECK_RCCL(rccl().reduce_scatter(g, g + c->dp_rank * ch, (size_t)ch, ncclFloat32, ncclSum, c->comm, s));
     }
@@ -1642,7 +1653,7 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
     (void)mark(c, critic ? "adam_critic_shard" : "adam_actor_shard");
     // (SACMI_DP_LOOPBACK_ONE_RANK: timing only — rank 0's chunk alone, the per-rank work
     // of a `world`-rank run minus its collectives; the other chunks are left unstepped)
-    const bool one_rank = std::getenv("SACMI_DP_LOOPBACK_ONE_RANK") != nullptr;   // (read per capture)
+    const bool one_rank = loopback_one_rank(c);
     if (c->dp_loopback && !one_rank) {
       for (int r = 0; r < W; ++r) dp_shard_adam(c, critic, B, r, true);
     } else if (c->dp_loopback) {
@@ -1665,9 +1676,8 @@ static void enqueue_dp_sharded(sacmi_ctx* c, int B, int n) {
   const bool pk_ride = !act16_on(c, B) &&
                        (int64_t)((B + 31) / 32) * ((c->H + 31) / 32) <= 192;
   c->dp_sharding_now = true;
-  const bool one_rank_only = std::getenv("SACMI_DP_LOOPBACK_ONE_RANK") != nullptr;
   if (!c->dp_loopback && W > 1) c->moments_sharded = true;
-  if (c->dp_loopback && one_rank_only && W > 1) c->moments_partial = true;
+  if (loopback_one_rank(c) && W > 1) c->moments_partial = true;
   try {
     int parity = 0;
     bool have = false;
@@ -1701,15 +1711,17 @@ static void enqueue_dp(sacmi_ctx* c, int B, int n) {
     enqueue_dp_sharded(c, B, n);
     return;
   }
-  const float scale = 1.f / (float)c->dp_world;
+  const float scale = loopback_one_rank(c) ? 1.f : 1.f / (float)c->dp_world;   // (see there)
   const bool ride = n > 1 && ride_possible(c, B);
   auto allreduce = [&](int64_t begin, int64_t end) {
     const bool critic = begin == c->q_begin;
     (void)mark(c, critic ? "allreduce_critic_grads" : "allreduce_actor_grads");
     float* g = c->G.p + begin;
     if (c->dp_loopback) {   // what `world` ranks holding identical shards would all-reduce to
-      scale_checked(g, end - begin, (float)c->dp_world, c->stream);
-      if (critic) loopback_flags(c, c->G.p + c->q_end, c->stream);
+      if (!loopback_one_rank(c)) {
+        scale_checked(g, end - begin, (float)c->dp_world, c->stream);
+        if (critic) loopback_flags(c, c->G.p + c->q_end, c->stream);
+      }
     } else {
       // the critic range carries the error flags past q_end (kDpFlagN)
       const int64_t n = end - begin + (critic ? kDpFlagN : 0);

@@ -137,10 +137,11 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
     want_roof = not getattr(args, "no_roofline", False)
     sim = int(getattr(args, "dp_sim_world", 0) or 0)
     if sim:                                         # one GPU stands in for `sim` ranks
-        # rank 0's work only, in BOTH optimizer forms: the sharded form's Adam on rank 0's
-        # chunk (SACMI_DP_LOOPBACK_ONE_RANK, read at each capture) — without it the loopback
-        # steps all `sim` chunks in turn, sim x a rank's optimizer work (round 5's dp_form_ab
-        # legs differed by 42 % for that reason alone)
+        # rank 0's work only, in BOTH optimizer forms (SACMI_DP_LOOPBACK_ONE_RANK, read at each
+        # capture): the sharded form's Adam on rank 0's chunk, the collectives returning the
+        # rank's own gradient with no stand-in kernels — without it the loopback steps all
+        # `sim` chunks in turn, sim x a rank's optimizer work (round 5's dp_form_ab legs
+        # differed by 42 % for that reason alone), and scales the gradients in place
         os.environ["SACMI_DP_LOOPBACK_ONE_RANK"] = "1"
         ctx.dp_loopback_init(sim)
     elif native or want_roof:
@@ -282,9 +283,10 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
                                   if ctx.dp_sharded() else "all-reduce -> Adam on every rank"),
             "simulated_world": sim or None,
             "simulated_note": (f"one GPU runs rank 0's sequence of a {sim}-rank job, collectives "
-                               "emulated in place (no transfers): the per-rank work minus the "
-                               "collectives (the sharded form's Adam on rank 0's chunk only, "
-                               "SACMI_DP_LOOPBACK_ONE_RANK)" if sim else None),
+                               "returning the rank's own gradient (no transfers, no stand-in "
+                               "kernels; the sharded form's Adam on rank 0's chunk: "
+                               "SACMI_DP_LOOPBACK_ONE_RANK): the per-rank work minus the "
+                               "collectives" if sim else None),
             "mfma_util_step": round(flops * value / 1e12 / peak / world, 4),
             "replicas_bitwise_equal": replicas_ok,
             "dp_form_ab": form_ab,

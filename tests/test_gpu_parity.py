@@ -1160,10 +1160,8 @@ def test_dp_sharded_one_rank_chunks(world):
     chunk of each range only, and each range must have some but not all of its elements
     stepped.
     * Critic range: every element holds its fused-update value (inside the chunk) or its
-      value before the update (outside).  Power-of-two worlds: bit for bit (x W then x 1/W
-      is exact); otherwise the stepped deltas are graded against the fused ones with
-      split_flips (Adam's first step is ~lr * sign(g): the x W / W rounding may flip a
-      near-zero gradient's sign, nothing else moves).
+      value before the update (outside), bit for bit at any world (the one-rank mode's
+      collectives return the rank's own gradient, and Adam applies no 1/world).
     * Actor range: its gradient comes from the PARTLY stepped critics (sac_imp.py:116-125
       reads the critics after their step).  Reference: the oracle's actor block
       (OracleSAC.actor_step, sac_imp.py:116-135) in fp64 and fp32 on those same critics (read
@@ -1204,15 +1202,8 @@ def test_dp_sharded_one_rank_chunks(world):
             stepped = v != init[net][k]
             n_stepped += int(stepped.sum())
             total += v.size
-            if not stepped.any():
-                continue
-            if world & (world - 1) == 0:
+            if stepped.any():
                 assert np.array_equal(v[stepped], fused[net][k][stepped]), (net, k)
-            else:
-                d = v[stepped].astype(np.float64) - init[net][k][stepped]
-                d_f = fused[net][k][stepped].astype(np.float64) - init[net][k][stepped]
-                e, f = split_flips(d, d_f)
-                assert f <= max(2, int(0.002 * d.size)) and e <= GRAD_TOL, (net, k, e, f)
     assert 0 < n_stepped < total, ("critics", n_stepped, total)
     # the actor range, against the oracle's actor block on the same partly stepped critics
     shapes = param_shapes(cfg)
