@@ -1566,6 +1566,13 @@ static RcclApi& rccl() {
 #ifndef SACMI_DP_SHARD_DEFAULT
 #define SACMI_DP_SHARD_DEFAULT 0
 #endif
+// SACMI_DP_PHASES_AT_WORLD1: a one-rank RCCL job runs the phase sequence and its collectives
+// (and so the sharded form when selected) instead of the fused update
+static bool dp_phases_at_world1() {
+  static const bool on = std::getenv("SACMI_DP_PHASES_AT_WORLD1") != nullptr;
+  return on;
+}
+
 static bool dp_shard_default(int world) {
   if (const char* e = std::getenv("SACMI_DP_SHARD")) return std::atoi(e) != 0 && world <= kMaxShardWorld;
   return SACMI_DP_SHARD_DEFAULT && world >= 2 && world <= kMaxShardWorld;
@@ -2583,8 +2590,7 @@ int sacmi_step_dp(sacmi_ctx* c, int32_t batch, int32_t n_updates) {
     // one rank: nothing to reduce — the fused update (bit-identical to the phase sequence:
     // test_dp_* world-1 and loopback tests), unless SACMI_DP_PHASES_AT_WORLD1 asks for the
     // phase sequence and its collectives anyway
-    static const bool phases1 = std::getenv("SACMI_DP_PHASES_AT_WORLD1") != nullptr;
-    if (c->dp_world == 1 && !c->dp_loopback && !phases1) {
+    if (c->dp_world == 1 && !c->dp_loopback && !dp_phases_at_world1()) {
       run_update(c, batch, 1, 1, 7, 1.f, true, n_updates);
       return;
     }
@@ -2620,7 +2626,7 @@ int sacmi_dp_set_sharded(sacmi_ctx* c, int32_t on) {
 int sacmi_dp_sharded(sacmi_ctx* c, int32_t* on) {
   return guard([&] {
     REQUIRE(c && on, SACMI_EVALUE, "null argument");
-    *on = c->dp_shard && (c->dp_world > 1 || c->dp_loopback) ? 1 : 0;
+    *on = c->dp_shard && (c->dp_world > 1 || c->dp_loopback || dp_phases_at_world1()) ? 1 : 0;
   });
 }
 

@@ -47,7 +47,7 @@ for step in ${STEPS:-tests smoke configs}; do
       line $O/dp8_shard.json; line $O/dp8_ar.json
       python3 -c "import json; [print(f, json.load(open(f))['dp_form_ab']) for f in ('$O/dp8_shard.json', '$O/dp8_ar.json')]" ;;
     dpab)
-      SACMI_DP_PHASES_AT_WORLD1=1 timeout -k 10 300 $B --force-dp --steps 20 > $O/dp1_ab.json 2> $O/dp1_ab.err \
+      env ${DPAB_ENV:-} SACMI_DP_PHASES_AT_WORLD1=1 timeout -k 10 300 $B --force-dp --steps 20 > $O/dp1_ab.json 2> $O/dp1_ab.err \
         || { tail $O/dp1_ab.err; exit 1; }
       line $O/dp1_ab.json
       python3 -c "import json; d=json.load(open('$O/dp1_ab.json')); print(d['dp_optimizer_step'], d['replicas_bitwise_equal'], d['dp_form_ab'])" ;;
