@@ -2040,9 +2040,31 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
   float4 ga[NAI], gb[BH ? 1 : NBI], gw;
   uint2 gh[BH ? NBI : 1];               // BH: W from its bf16 shadow
   const rsrc_t rBh = make_rsrc(BH ? reinterpret_cast<const float*>(d.Bh) : d.B, 0x7fffffffu);
+  // a tile wholly inside N and a slab wholly inside K stage without the edge masks (rows past
+  // M read the clamped last row, as in the masked form; their outputs are never stored)
+  const bool n_in = n0 + kXBN <= N;
   auto gload = [&](int k0) {
     const int k = k0 + kq;
     const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
+    if (n_in && k0 + kXBK <= K) {
+#pragma unroll
+      for (int i = 0; i < NAI; ++i) {
+        if constexpr (A16) {
+          const uint2 h = buf_ld2(rA, offA[i] + ko / 2u);
+          ga[i] = make_float4(bf16_lo(h.x), bf16_hi(h.x), bf16_lo(h.y), bf16_hi(h.y));
+        } else {
+          ga[i] = buf_ld4(rA, offA[i] + ko);
+        }
+      }
+      gw = buf_ld4(rW, ko);
+#pragma unroll
+      for (int i = 0; i < NBI; ++i) {
+        const uint32_t e = (uint32_t)(k0 + kr0 + BKP * i) * (uint32_t)d.ldb + (uint32_t)nb;
+        if constexpr (BH) gh[i] = buf_ld2(rBh, e * 2u);
+        else gb[i] = buf_ld4(rB, e * 4u);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NAI; ++i) {
       if constexpr (A16) {   // (only the sign is read: exact widening)
@@ -2073,11 +2095,15 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
   };
   auto swrite = [&](int buf, int k0, bool fresh) {
     const int k = k0 + kq;
+    const bool k_in = k0 + kXBK <= K;
 #pragma unroll
     for (int i = 0; i < NAI; ++i) {
       // u = [h2 > 0] w3 (exact fp32 values: w3 or 0), rounded to bf16 for the MFMAs
       const float4 a = ga[i];
-      const float4 u = AX ? make_float4(a.x > 0.f && k < K ? gw.x : 0.f, a.y > 0.f && k + 1 < K ? gw.y : 0.f,
+      const float4 u = k_in ? (AX ? make_float4(a.x > 0.f ? gw.x : 0.f, a.y > 0.f ? gw.y : 0.f,
+                                                a.z > 0.f ? gw.z : 0.f, a.w > 0.f ? gw.w : 0.f)
+                                  : a)
+                     : AX ? make_float4(a.x > 0.f && k < K ? gw.x : 0.f, a.y > 0.f && k + 1 < K ? gw.y : 0.f,
                                         a.z > 0.f && k + 2 < K ? gw.z : 0.f, a.w > 0.f && k + 3 < K ? gw.w : 0.f)
                           : make_float4(k < K ? a.x : 0.f, k + 1 < K ? a.y : 0.f,
                                         k + 2 < K ? a.z : 0.f, k + 3 < K ? a.w : 0.f);
