@@ -7,7 +7,9 @@
 #   configs  bench lines of CONFIGS (default "2 3 5"), BENCH_ARGS appended
 #   dp8      the data-parallel sequence at a simulated world of 8, both optimizer forms
 #   dpab     the data-parallel bench at one rank over real RCCL with the phase sequence forced
-#            (SACMI_DP_PHASES_AT_WORLD1): the line's form and the other one (dp_form_ab)
+#            (SACMI_DP_PHASES_AT_WORLD1): the line's form and the other one (dp_form_ab);
+#            dpabr the same with the sharded form as the line's
+#   driver   `python3 bench.py` with no arguments (the driver's round-end line)
 #   pmcb     the bound-analysis PMC passes (tools/gpu_pmc_bound.sh) of CONFIGS_PMCB ("5 3")
 #   prof     the round's profile set (tools/gpu_profile.sh: PMC passes of CONFIGS, the
 #            rocprofv3 kernel-trace summary of the driver's config-2 command)
@@ -46,11 +48,16 @@ for step in ${STEPS:-tests smoke configs}; do
       SACMI_DP_SHARD=0 SACMI_DP_LOOPBACK_ONE_RANK=1 timeout -k 10 300 $B --force-dp --dp-sim-world 8 --steps 20 > $O/dp8_ar.json 2> $O/dp8_ar.err || { tail $O/dp8_ar.err; exit 1; }
       line $O/dp8_shard.json; line $O/dp8_ar.json
       python3 -c "import json; [print(f, json.load(open(f))['dp_form_ab']) for f in ('$O/dp8_shard.json', '$O/dp8_ar.json')]" ;;
-    dpab)
-      env ${DPAB_ENV:-} SACMI_DP_PHASES_AT_WORLD1=1 timeout -k 10 300 $B --force-dp --steps 20 > $O/dp1_ab.json 2> $O/dp1_ab.err \
-        || { tail $O/dp1_ab.err; exit 1; }
-      line $O/dp1_ab.json
-      python3 -c "import json; d=json.load(open('$O/dp1_ab.json')); print(d['dp_optimizer_step'], d['replicas_bitwise_equal'], d['dp_form_ab'])" ;;
+    dpab|dpabr)
+      # dpabr: the same with the sharded form as the line's (the all-reduce form the other leg)
+      f=dp1_ab; e=""; if [ $step = dpabr ]; then f=dp1_abr; e="SACMI_DP_SHARD=1"; fi
+      env $e SACMI_DP_PHASES_AT_WORLD1=1 timeout -k 10 300 $B --force-dp --steps 20 > $O/$f.json 2> $O/$f.err \
+        || { tail $O/$f.err; exit 1; }
+      line $O/$f.json
+      python3 -c "import json; d=json.load(open('$O/$f.json')); print(d['dp_optimizer_step'], d['replicas_bitwise_equal'], d['dp_form_ab'])" ;;
+    driver)   # the driver's own round-end command (defaults: trainer loop and cpu_baseline included)
+      timeout -k 10 600 python3 bench.py > $O/driver_bench.json 2> $O/driver_bench.err || { tail $O/driver_bench.err; exit 1; }
+      line $O/driver_bench.json ;;
     pmcb)
       for c in ${CONFIGS_PMCB:-5 3}; do
         bash tools/gpu_pmc_bound.sh c$c --config $c --steps 20 --warmup 5 --profile-only || exit 1
