@@ -248,7 +248,8 @@ def run_dp_bench(args, rank: int, world: int, local_rank: int, emit=print):
                 ctx.dp_set_sharded(was)
                 torch.cuda.synchronize()
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    # (the CPU baseline is timed on rank 0 at N = 1 only: the N > 1 lines carry none)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         n_cpu = min(fill * world, 1_000_000)
         cpu_rows = tuple(x[:n_cpu] for x in B.synth(n_cpu, 7, S, A))
         cpu = B.cpu_baseline(cpu_rows, seconds=args.cpu_seconds, batch=args.batch, per=per,
