@@ -1572,6 +1572,163 @@ __global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), 2) void k_fwd16(GemmBatch
 }
 
 // ---------------------------------------------------------------------------
+// fp32 forward levels of the batch-4096 class on bf16 MFMA: the exact three-way split
+// ("x6").  gfx950 has no xf32 MFMA and its fp32 MFMA issues at 1/16 of the bf16 rate.  Each
+// fp32 operand x is cut EXACTLY into three bf16 parts x = h + m + l by truncation (h: the
+// top 8 significant bits; m: the next 8 of the remainder; l: the rest, at most 8 bits — both
+// subtractions exact in fp32), once per workgroup as the slab is staged, into three bf16 LDS
+// planes per operand.  a.b is then 9 cross products of exact parts; the 6 kept (hh, hm, mh,
+// mm, hl, lh) are exact in the fp32 accumulator, the 3 dropped (ml, lm, ll) are below
+// 2^-25 |a b| — under fp32's own unit roundoff: the result is as accurate as the fp32 MFMA
+// chain (rounded differently, not bit-identical).  Per 32 k and 16x16 block: 6
+// v_mfma_f32_16x16x32_bf16 (16 cycles each) for 8 v_mfma_f32_16x16x4_f32 (32 each).
+// Round 6's register-split form at batch 256 (profiles/r06/x6_ab) paid the split per wave
+// per fragment; here it is paid once per staged element.
+// Tiles 128 x BN (BN 128 or 64), 8 waves as 4 x 2 sub-tiles of 32 x BN/2, full K in 32-deep
+// slabs; one LDS buffer (the next slab's fp32 loads in flight in registers under the MFMAs,
+// two barriers a slab) so that two workgroups share a CU.  Epilogue: k_fwd16's (bias, ReLU,
+// fc3 dot partials, fp32 stores).
+constexpr int kX6K = 32, kX6Pad = 8, kX6Waves = 8;
+
+// the three bf16 parts of four fp32 values, each part as four packed bf16 (k order kept)
+__device__ __forceinline__ void x6_split4(float4 v, u2v& h, u2v& m, u2v& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t ph[2], pm[2], pl[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const float x0 = x[2 * d], x1 = x[2 * d + 1];
+    const uint32_t u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+    ph[d] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+    const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u);
+    const float r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+    const uint32_t v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+    pm[d] = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+    const float s0 = r0 - __uint_as_float(v0 & 0xffff0000u);
+    const float s1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+    pl[d] = __builtin_amdgcn_perm(__float_as_uint(s1), __float_as_uint(s0), 0x07060302u);
+  }
+  h = u2v{ph[0], ph[1]}; m = u2v{pm[0], pm[1]}; l = u2v{pl[0], pl[1]};
+}
+
+template <int BN>
+__global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_FWD_X6);
+  constexpr int NWV = kX6Waves, WC = 2, WR = NWV / WC;
+  constexpr int MW = kFBM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
+  static_assert(NT >= 2 && MI >= 1, "a wave covers whole 32-column dot blocks");
+  constexpr int LDR = kX6K + kX6Pad;     // bf16 per LDS row (80 B)
+  constexpr int TPR = kX6K / 4;          // staging threads per row (4 k each)
+  constexpr int RPP = 64 * NWV / TPR;    // rows per staging pass
+  constexpr int NA = kFBM / RPP, NB = BN / RPP;
+  static_assert(NA >= 1 && NB >= 1, "staging passes");
+  __shared__ __attribute__((aligned(16))) __bf16 sA[3][kFBM][LDR];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[3][BN][LDR];
+  const int bid = blockIdx.x;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  int tr, tc;
+  place_tile(d, t, tr, tc);
+  const int m0 = tr * kFBM, n0 = tc * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WC) * MW, wn = (wave % WC) * NW;
+  const int M = d.M, N = d.N, K = d.K;
+  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
+  uint32_t offA[NA], offB[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i)
+    offA[i] = (uint32_t)min(m0 + tid / TPR + RPP * i, M - 1) * (uint32_t)d.lda * 4u;
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    offB[i] = (uint32_t)min(n0 + tid / TPR + RPP * i, N - 1) * (uint32_t)d.ldb * 4u;
+  const int kq = 4 * (tid % TPR);
+  float4 ga[NA], gb[NB];
+  auto zk = [&](float4 x, int k) {    // elements past K read the row's next columns: zeroed
+    x.x = k < K ? x.x : 0.f; x.y = k + 1 < K ? x.y : 0.f; x.z = k + 2 < K ? x.z : 0.f; x.w = k + 3 < K ? x.w : 0.f;
+    return x;
+  };
+  auto gload = [&](int k0) {
+    const int k = k0 + kq;
+    const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) ga[i] = zk(buf_ld4(rA, offA[i] + ko), k);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) gb[i] = zk(buf_ld4(rB, offB[i] + ko), k);
+  };
+  auto swrite = [&]() {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      u2v h, m, l;
+      x6_split4(ga[i], h, m, l);
+      const int r = tid / TPR + RPP * i;
+      *reinterpret_cast<u2v*>(&sA[0][r][kq]) = h;
+      *reinterpret_cast<u2v*>(&sA[1][r][kq]) = m;
+      *reinterpret_cast<u2v*>(&sA[2][r][kq]) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      u2v h, m, l;
+      x6_split4(gb[i], h, m, l);
+      const int r = tid / TPR + RPP * i;
+      *reinterpret_cast<u2v*>(&sB[0][r][kq]) = h;
+      *reinterpret_cast<u2v*>(&sB[1][r][kq]) = m;
+      *reinterpret_cast<u2v*>(&sB[2][r][kq]) = l;
+    }
+  };
+  f4 acc[MI][NT];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  FwdEpi<NT, MI> ep;
+  ep.load(d, n0 + wn, lane);
+  gload(0);
+  swrite();
+  __syncthreads();
+  const int nslab = (K + kX6K - 1) / kX6K;
+  const int kc = 8 * (lane >> 4);
+  for (int sl = 0; sl < nslab; ++sl) {
+    if (sl + 1 < nslab) gload((sl + 1) * kX6K);
+    // the A parts of every row block, then each B column block's parts just before its
+    // MFMAs (one B block's parts live at a time); small terms first into the accumulator
+    bf16x8 ah[MI], am[MI], al[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int r = wm + i * 16 + (lane & 15);
+      ah[i] = *reinterpret_cast<const bf16x8*>(&sA[0][r][kc]);
+      am[i] = *reinterpret_cast<const bf16x8*>(&sA[1][r][kc]);
+      al[i] = *reinterpret_cast<const bf16x8*>(&sA[2][r][kc]);
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int r = wn + j * 16 + (lane & 15);
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(&sB[0][r][kc]);
+      const bf16x8 bm = *reinterpret_cast<const bf16x8*>(&sB[1][r][kc]);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&sB[2][r][kc]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        f4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, c, 0, 0, 0);
+      }
+    }
+    if (sl + 1 < nslab) {
+      __syncthreads();   // every wave's fragment reads of this slab done
+      swrite();
+      __syncthreads();
+    }
+  }
+  ep.store(d, acc, m0 + wm, n0 + wn, lane);
+}
+
+// ---------------------------------------------------------------------------
 // k_fwd16p: the act16 forward levels (bf16 activations AND bf16 weight shadows) with a
 // multi-slab LDS ring filled by LDS-DMA (global_load_lds_dwordx4: no VGPR per slab in
 // flight).  k_fwd16 keeps one slab in flight per workgroup (its register stage), and at
@@ -2520,6 +2677,32 @@ static void launch_fwd16(GemmBatch& b, hipStream_t s) {
   HIP_LAUNCH_CHECK();
 }
 
+// whether launch_gemm may run an fp32 level on k_fwd_x6: plain forward GEMMs (both operands
+// K-contiguous and 16-byte aligned, store / ReLU epilogue, optional bias and dot partials),
+// no prologue, no rides, and two 128-row tiles per CU (128 columns wide where that gives
+// them, else 64).  The tile assignment of the chosen width is left in b.
+static bool fwd_x6_ok(GemmBatch& b) {
+  if (b.ride.kind || b.ride.pk_blocks || b.bf16 || b.has_adam) return false;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    if (!d.a_kc || !d.b_kc || d.axk || d.a_ksc || d.rs_col >= 0 || d.pa_out) return false;
+    if (d.a16 || d.b16 || d.c16 || d.x16) return false;
+    if (((uintptr_t)d.A & 15) || (d.lda & 3) || ((uintptr_t)d.B & 15) || (d.ldb & 3)) return false;
+    if (d.epi != EPI_RELU && d.epi != EPI_STORE) return false;
+    if (d.dotp && (d.N % 32)) return false;
+  }
+  if (assign_tiles<kFBM, 128>(b) >= 512) return true;
+  return assign_tiles<kFBM, 64>(b) >= 512;
+}
+
+static void launch_fwd_x6(const GemmBatch& b, hipStream_t s) {
+  const bool n128 = b.d[0].tiles_n == (b.d[0].N + 127) / 128;
+  const dim3 g(b.total_tiles), blk(64 * kX6Waves);
+  if (n128) hipLaunchKernelGGL(k_fwd_x6<128>, g, blk, 0, s, b);
+  else hipLaunchKernelGGL(k_fwd_x6<64>, g, blk, 0, s, b);
+  HIP_LAUNCH_CHECK();
+}
+
 void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (b0.count == 0) return;
   GemmBatch b = b0;
@@ -2542,6 +2725,11 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   b = b0;
   if (fwd_big_ok(b)) {
     launch_fwd16(b, s);
+    return;
+  }
+  b = b0;
+  if (fwd_x6_ok(b)) {
+    launch_fwd_x6(b, s);
     return;
   }
   b = b0;
