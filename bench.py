@@ -117,7 +117,7 @@ def init_agent(ctx, seed):
 
 # kernels that run the MLP GEMM levels (the dominant kernel family of the update); L10
 # (k_gemm_sample_bwd: dL/da + the sampling backward) and the heads kernel are not levels
-LEVEL_KERNELS = {"k_gemm", "k_fwd_x6", "k_fwd16", "k_fwd16p", "k_axk16", "k_dw_part16", "k_dw_fin"}
+LEVEL_KERNELS = {"k_gemm", "k_fwd_x6", "k_fwd16", "k_fwd16p", "k_axk16", "k_axk_x6", "k_dw_part16", "k_dw_part_x6", "k_dw_fin"}
 
 
 def timeline_roofline(ctx, batch, n_updates, data_parallel=False):

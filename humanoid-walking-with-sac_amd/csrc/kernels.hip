@@ -2133,6 +2133,181 @@ __global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part16(GemmBatch batc
   }
 }
 
+// fp32 mode, batch-4096 class: the deep-K weight-gradient partials on bf16 MFMA with the
+// exact three-way split (k_fwd_x6's form on k_dw_part16's structure): 128x128 output tiles,
+// K (the batch) split NS ways across workgroups, 32-deep slabs of dY (x the K-scale) and X
+// cut once per workgroup into three bf16 planes each, [k][column] in LDS and read transposed
+// (ds_read_b64_tr_b16); the bias-gradient row sums from the unrounded fp32 staging registers;
+// the partial tile to the workspace for k_dw_fin.  One LDS buffer (the next slab's fp32 loads
+// in registers), two workgroups per CU.
+constexpr int kDX6K = 32;
+__global__ __launch_bounds__(64 * kDw16Waves, 2) void k_dw_part_x6(GemmBatch batch, int ns, int64_t ws_stride) {
+  const TlMark tl_mark(batch.tl, TL_DW_PART_X6);
+  constexpr int LDR = kDBM + kD16Pad;          // bf16 per LDS k row (272 B)
+  constexpr int PL = kDX6K * LDR;              // one plane
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kDw16LdsBytes];
+  __bf16* const sAp = reinterpret_cast<__bf16*>(lds_raw);              // [3][kDX6K][LDR]
+  __bf16* const sBp = sAp + 3 * PL;
+  auto& s_rs = *reinterpret_cast<float (*)[kDw16Krp][kDBM]>(lds_raw + 6 * PL * 2);
+  static_assert(6 * PL * 2 + kDw16Krp * kDBM * 4 <= kDw16LdsBytes, "k_dw_part_x6 LDS layout");
+  constexpr int NWV = kDw16Waves, WC = NWV / 2, NJ = kDBN / WC / 16;   // 2 x WC waves of 64 x (128 / WC)
+  constexpr int KRP = kDw16Krp, NI = kDX6K / KRP;                      // staging: KRP k rows a pass
+  static_assert(NI >= 1, "k_dw_part_x6 staging");
+  const int tiles_tot = batch.total_tiles;
+  const int nwg = dw_grid_tiles(tiles_tot, ns);
+  if ((int)blockIdx.x >= nwg) {   // ride-along: the next update's sampling or gather
+    const int rb = blockIdx.x - nwg, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (batch.ride.kind == 1) {
+      if (rb == 0) mt_sample_body(batch.ride.mt, batch.ride.tbl_log2, reinterpret_cast<uint32_t*>(lds_raw));
+    } else {
+      for (int b = rb * NWV + wave; b < batch.ride.ga.B; b += batch.ride.nblocks * NWV)
+        gather_row(batch.ride.ga, b, lane, 64);
+    }
+    return;
+  }
+  const int wk = dw_work_index(blockIdx.x, tiles_tot, ns);
+  if (wk < 0) return;
+  const int split = wk / tiles_tot, bid = wk % tiles_tot;
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  const int m0 = (t / d.tiles_n) * kDBM, n0 = (t % d.tiles_n) * kDBN;
+  const int M = d.M, N = d.N, K = d.K;
+  // the split's K range in whole 64-deep units (k_dw_part16's ranges: the same partition)
+  const int kc = ((K + ns - 1) / ns + kD16K - 1) / kD16K * kD16K;
+  const int kb = split * kc, ke = min(K, kb + kc);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WC) * 64, wn = (wave % WC) * (kDBN / WC);
+  const int c4 = 4 * (tid & 31), kr0 = tid >> 5;
+  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
+  const rsrc_t rS = make_rsrc(d.a_ksc ? d.a_ksc : d.A, d.a_ksc ? (uint32_t)K * 4u : 0u);
+  const bool has_ksc = d.a_ksc != nullptr;
+  const int ma = min(m0 + c4, (M - 1) & ~3), nb = min(n0 + c4, (N - 1) & ~3);
+  const bool want_rs = d.rs_col >= 0 && n0 == 0;
+  float4 ga[NI], gb[NI];
+  float rs4[4] = {0.f, 0.f, 0.f, 0.f};
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int k = k0 + kr0 + KRP * i;
+      const bool kin = k < ke;
+      const uint32_t kk = (uint32_t)(kin ? k : 0);
+      float4 x = buf_ld4(rA, (kk * (uint32_t)d.lda + (uint32_t)ma) * 4u);
+      const float f = has_ksc ? buf_ld(rS, kk * 4u) : 1.f;
+      x.x = kin && m0 + c4 < M ? x.x * f : 0.f;     x.y = kin && m0 + c4 + 1 < M ? x.y * f : 0.f;
+      x.z = kin && m0 + c4 + 2 < M ? x.z * f : 0.f; x.w = kin && m0 + c4 + 3 < M ? x.w * f : 0.f;
+      ga[i] = x;
+      float4 y = buf_ld4(rB, (kk * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
+      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+      gb[i] = y;
+    }
+  };
+  auto swrite = [&]() {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r = kr0 + KRP * i;
+      u2v h, m, l;
+      x6_split4(ga[i], h, m, l);
+      *reinterpret_cast<u2v*>(sAp + 0 * PL + r * LDR + c4) = h;
+      *reinterpret_cast<u2v*>(sAp + 1 * PL + r * LDR + c4) = m;
+      *reinterpret_cast<u2v*>(sAp + 2 * PL + r * LDR + c4) = l;
+      x6_split4(gb[i], h, m, l);
+      *reinterpret_cast<u2v*>(sBp + 0 * PL + r * LDR + c4) = h;
+      *reinterpret_cast<u2v*>(sBp + 1 * PL + r * LDR + c4) = m;
+      *reinterpret_cast<u2v*>(sBp + 2 * PL + r * LDR + c4) = l;
+    }
+    if (want_rs) {
+#pragma clang fp contract(off)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        rs4[0] += ga[i].x; rs4[1] += ga[i].y; rs4[2] += ga[i].z; rs4[3] += ga[i].w;
+      }
+    }
+  };
+  f4 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int nslab = (ke - kb + kDX6K - 1) / kDX6K;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = lane >> 4;
+  const int kr = 8 * tg + tq;
+  auto frag = [&](const __bf16* plane, int col) {   // transposed 16x32 fragment at column col
+    const s4t lo = lds_tr16(plane + kr * LDR + col);
+    const s4t hi = lds_tr16(plane + (kr + 4) * LDR + col);
+    const s8t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  if (nslab > 0) {
+    gload(kb);
+    swrite();
+    __syncthreads();
+  }
+  for (int sl = 0; sl < nslab; ++sl) {
+    if (sl + 1 < nslab) gload(kb + (sl + 1) * kDX6K);
+    bf16x8 ah[4], am[4], al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = wm + i * 16 + 4 * tp;
+      ah[i] = frag(sAp, col);
+      am[i] = frag(sAp + PL, col);
+      al[i] = frag(sAp + 2 * PL, col);
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = wn + j * 16 + 4 * tp;
+      const bf16x8 bh = frag(sBp, col), bm = frag(sBp + PL, col), bl = frag(sBp + 2 * PL, col);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, c, 0, 0, 0);
+      }
+    }
+    if (sl + 1 < nslab) {
+      __syncthreads();   // every wave's fragment reads of this slab done
+      swrite();
+      __syncthreads();
+    }
+  }
+  // partial tile (+ row-sum partial) to the workspace
+  int64_t off = 0;
+  for (int q = 0; q < p; ++q) off += (int64_t)batch.d[q].M * dw_ncols(batch.d[q]);
+  float* w = batch.ws + (int64_t)split * ws_stride + off;
+  const int nc = dw_ncols(d);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wn + j * 16 + (lane & 15);
+        if (row < M && col < N) st_big(w + (int64_t)row * nc + col, acc[i][j][r]);
+      }
+    }
+  if (want_rs) {
+    __syncthreads();
+    s_rs[kr0][c4] = rs4[0]; s_rs[kr0][c4 + 1] = rs4[1];
+    s_rs[kr0][c4 + 2] = rs4[2]; s_rs[kr0][c4 + 3] = rs4[3];
+    __syncthreads();
+    if (tid < kDBM && m0 + tid < M) {
+#pragma clang fp contract(off)
+      float v = s_rs[0][tid];
+      for (int g = 1; g < KRP; ++g) v += s_rs[g][tid];
+      st_big(w + (int64_t)(m0 + tid) * nc + N, v);
+    }
+  }
+}
+
 // bf16 mode, batch-4096 class: the row-prologue dh levels (L5 / L9 and their model2
 // form) on LDS-staged 64x128 tiles.  dh[b][n] = coef[b] * sum_k u[b][k] W[k][n] * [h[b][n] > 0]
 // with u[b][k] = h2[b][k] > 0 ? w3[k] : 0 formed at staging (the coefficient-free rows u
@@ -2355,6 +2530,221 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
   if constexpr (AX) rows_loss<kXBM>(batch.rows, m0, writer, s_l);
 }
 
+// fp32 dh levels of the batch-4096 class on bf16 MFMA with the exact three-way split
+// (k_fwd_x6's form on k_axk16's structure): dh[b][n] = coef[b] * sum_k u[b][k] W[k][n] *
+// [h[b][n] > 0] with u = [h2 > 0] w3 formed at staging (its exact fp32 rows stored by the
+// column-tile-0 workgroups for the layer's weight gradient; the row prologue and coefficients
+// as k_axk16 / k_gemm's, so the losses and dq bits do not depend on the kernel), or (AX =
+// false) the plain dh = (dY W) * [h > 0].  64 x 128 tiles, 8 waves of 32 x 32, 32-deep slabs
+// split once per workgroup into three bf16 planes per operand: A [row][k], B = W k-major
+// [k][n] read transposed (ds_read_b64_tr_b16); one LDS buffer, two workgroups per CU.
+constexpr int kXX6K = 32;
+template <bool AX>
+__global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
+  const TlMark tl_mark(batch.tl, TL_AXK_X6);
+  constexpr int LDA_ = kXX6K + 8;       // [row][k] bf16, 80-B rows
+  constexpr int LDB_ = kXBN + 8;        // [k][n] bf16, 272-B rows
+  __shared__ __attribute__((aligned(16))) __bf16 sA[3][kXBM][LDA_];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[3][kXX6K][LDB_];
+  __shared__ float s_q[kXBM][4], s_coef[2][kXBM], s_l[kXBM][2];
+  constexpr int NWV = kAxWaves, NTH = 64 * NWV, WC = NWV / 2, NJ = kXBN / WC / 16;
+  constexpr int TPRA = kXX6K / 4, ARP = NTH / TPRA, NAI = kXBM / ARP;   // A staging
+  constexpr int BKP = NTH / 32, NBI = kXX6K / BKP;                      // B staging
+  static_assert(NAI >= 1 && NBI >= 1 && NJ == 2, "k_axk_x6 staging");
+  const int bid = blockIdx.x;
+  if (bid >= batch.total_tiles) {   // ride-along: the next update's gather, a row a wave
+    const int wv = (bid - batch.total_tiles) * NWV + (int)(threadIdx.x >> 6), nwv = batch.ride.nblocks * NWV;
+    for (int b0 = wv; b0 < batch.ride.ga.B; b0 += nwv)
+      gather_rows_wave<1, 3>(batch.ride.ga, b0, nwv, threadIdx.x & 63);
+    return;
+  }
+  int p = 0;
+  for (int q = 1; q < batch.count; ++q)
+    if (bid >= batch.d[q].tile_begin) p = q;
+  const GemmDesc& d = batch.d[p];
+  const int t = bid - d.tile_begin;
+  if (t >= d.tiles_m * d.tiles_n) return;
+  int tr, tc;
+  place_tile(d, t, tr, tc);
+  const int m0 = tr * kXBM, n0 = tc * kXBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WC) * 32, wn = (wave % WC) * (kXBN / WC);
+  const int M = d.M, N = d.N, K = d.K;
+  const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
+  const rsrc_t rW = make_rsrc(AX ? d.ax_w : d.A, AX ? (uint32_t)K * 4u : 0u);
+  const bool store_a = AX && n0 == 0 && d.ax_out != nullptr;
+  const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
+                               store_a ? (uint32_t)(((size_t)(M - 1) * d.ax_ld + K) * 4) : 0u);
+  // A staging: rows tid / TPRA + ARP i at k = 4 (tid % TPRA); B staging: k rows
+  // (tid >> 5) + BKP i at columns 4 (tid & 31)
+  const int kq = 4 * (tid % TPRA), c4 = 4 * (tid & 31), kr0 = tid >> 5;
+  uint32_t offA[NAI];
+#pragma unroll
+  for (int i = 0; i < NAI; ++i)
+    offA[i] = (uint32_t)min(m0 + tid / TPRA + ARP * i, M - 1) * (uint32_t)d.lda * 4u;
+  const int nb = min(n0 + c4, N - 1);
+  float4 ga[NAI], gb[NBI], gw;
+  auto gload = [&](int k0) {
+    const int k = k0 + kq;
+    const uint32_t ko = (uint32_t)(k < K ? k : 0) * 4u;
+#pragma unroll
+    for (int i = 0; i < NAI; ++i) ga[i] = buf_ld4(rA, offA[i] + ko);
+    gw = buf_ld4(rW, ko);
+#pragma unroll
+    for (int i = 0; i < NBI; ++i) {
+      const int kb = k0 + kr0 + BKP * i;
+      const bool kin = kb < K;
+      float4 y = buf_ld4(rB, ((uint32_t)(kin ? kb : 0) * (uint32_t)d.ldb + (uint32_t)nb) * 4u);
+      y.x = kin && n0 + c4 < N ? y.x : 0.f;         y.y = kin && n0 + c4 + 1 < N ? y.y : 0.f;
+      y.z = kin && n0 + c4 + 2 < N ? y.z : 0.f;     y.w = kin && n0 + c4 + 3 < N ? y.w : 0.f;
+      gb[i] = y;
+    }
+  };
+  auto swrite = [&](int k0, bool fresh) {
+    const int k = k0 + kq;
+#pragma unroll
+    for (int i = 0; i < NAI; ++i) {
+      // u = [h2 > 0] w3 (exact fp32 values: w3 or 0)
+      const float4 a = ga[i];
+      const float4 u = AX ? make_float4(a.x > 0.f && k < K ? gw.x : 0.f, a.y > 0.f && k + 1 < K ? gw.y : 0.f,
+                                        a.z > 0.f && k + 2 < K ? gw.z : 0.f, a.w > 0.f && k + 3 < K ? gw.w : 0.f)
+                          : make_float4(k < K ? a.x : 0.f, k + 1 < K ? a.y : 0.f,
+                                        k + 2 < K ? a.z : 0.f, k + 3 < K ? a.w : 0.f);
+      const int r = tid / TPRA + ARP * i;
+      u2v h, m, l;
+      x6_split4(u, h, m, l);
+      *reinterpret_cast<u2v*>(&sA[0][r][kq]) = h;
+      *reinterpret_cast<u2v*>(&sA[1][r][kq]) = m;
+      *reinterpret_cast<u2v*>(&sA[2][r][kq]) = l;
+      if (fresh) {
+        const int rr = m0 + r;
+        buf_st4(rAx, (rr < M && k < K) ? (uint32_t)(rr * d.ax_ld + k) * 4u : 0xfffffff0u,
+                f4{u.x, u.y, u.z, u.w});
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NBI; ++i) {
+      u2v h, m, l;
+      x6_split4(gb[i], h, m, l);
+      *reinterpret_cast<u2v*>(&sB[0][kr0 + BKP * i][c4]) = h;
+      *reinterpret_cast<u2v*>(&sB[1][kr0 + BKP * i][c4]) = m;
+      *reinterpret_cast<u2v*>(&sB[2][kr0 + BKP * i][c4]) = l;
+    }
+  };
+  f4 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  // the row prologue's loads and the ReLU-mask source, behind the first slab's loads
+  RowsRegs rows_x{};
+  if constexpr (AX) rows_load<kXBM, NTH>(batch.rows, d, m0, rows_x);
+  float hm[2][NJ][4];
+  {
+    const rsrc_t rX = make_rsrc(d.aux, (uint32_t)(((size_t)(M - 1) * d.ldaux + N) * 4u));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int col = n0 + wn + j * 16 + (lane & 15);
+          hm[i][j][r] = buf_ld(rX, row < M && col < N ? (uint32_t)(row * d.ldaux + col) * 4u : 0xfffffff0u);
+        }
+      }
+  }
+  swrite(0, store_a);
+  __syncthreads();
+  const int nslab = (K + kXX6K - 1) / kXX6K;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = lane >> 4;
+  const int kc = 8 * tg;
+  for (int sl = 0; sl < nslab; ++sl) {
+    if (sl + 1 < nslab) gload((sl + 1) * kXX6K);
+    bf16x8 ah[2], am[2], al[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = wm + i * 16 + (lane & 15);
+      ah[i] = *reinterpret_cast<const bf16x8*>(&sA[0][r][kc]);
+      am[i] = *reinterpret_cast<const bf16x8*>(&sA[1][r][kc]);
+      al[i] = *reinterpret_cast<const bf16x8*>(&sA[2][r][kc]);
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      bf16x8 bp[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const s4t lo = lds_tr16(&sB[q][kc + tq][wn + j * 16 + 4 * tp]);
+        const s4t hi = lds_tr16(&sB[q][kc + tq + 4][wn + j * 16 + 4 * tp]);
+        const s8t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        bp[q] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bp[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bp[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bp[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bp[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bp[1], c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bp[0], c, 0, 0, 0);
+      }
+    }
+    if (sl + 1 < nslab) {
+      __syncthreads();   // every wave's fragment reads of this slab done
+      swrite((sl + 1) * kXX6K, store_a);
+      __syncthreads();
+    }
+  }
+  const bool writer = p == 0 && n0 == 0;
+  if constexpr (AX) rows_finish<kXBM, NTH>(batch.rows, d, m0, writer, bid == 0, rows_x, s_q, s_coef, s_l);
+  // epilogue: coefficient, ReLU-backward mask, store (k_gemm's op order)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int lr = wm + i * 16 + (lane >> 4) * 4 + r, row = m0 + lr;
+      const float cf = AX ? s_coef[d.ax_slot][lr] : 1.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wn + j * 16 + (lane & 15);
+        float v = acc[i][j][r];
+        if (AX) v *= cf;
+        v = hm[i][j][r] > 0.f ? v : 0.f;
+        if (row < M && col < N) st_big(d.C + (size_t)row * d.ldc + col, v);
+      }
+    }
+  if constexpr (AX) rows_loss<kXBM>(batch.rows, m0, writer, s_l);
+}
+
+// whether launch_gemm may run an fp32 level on k_axk_x6: k_axk16's level form in fp32 mode
+// (-1: no; 1: the row-prologue form; 0: the plain dh form)
+static int axk_x6_ok(GemmBatch& b) {
+  if (b.bf16 || (b.ride.kind && b.ride.kind != 2) || b.ride.pk_blocks || b.has_adam) return -1;
+  const int ax = b.d[0].axk == 1 ? 1 : 0;
+  if (ax != (b.rows.kind != 0 ? 1 : 0)) return -1;
+  for (int i = 0; i < b.count; ++i) {
+    const GemmDesc& d = b.d[i];
+    if (d.axk != ax || !d.a_kc || d.b_kc || d.epi != EPI_MASK || d.bias || d.dotp || d.a_ksc ||
+        d.rs_col >= 0 || d.pa_out || d.a16 || d.b16 || d.c16 || d.x16)
+      return -1;
+    if (((uintptr_t)d.A & 15) || (d.lda & 3) || ((uintptr_t)d.B & 15) || (d.ldb & 3) ||
+        (ax && ((uintptr_t)d.ax_w & 15)) || (d.N & 3))
+      return -1;
+  }
+  // two workgroups per CU: a one-net level (the policy's dhp1, 256 tiles) measured slower
+  // than its k_gemm form (config 3 L12 28.0-29.5 vs 27.1-27.2 us)
+  return assign_tiles<kXBM, kXBN>(b) >= 512 ? ax : -1;
+}
+
+static void launch_axk_x6(const GemmBatch& b, int ax, hipStream_t s) {
+  const dim3 grid(b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0)), blk(64 * kAxWaves);
+  if (ax) hipLaunchKernelGGL(k_axk_x6<true>, grid, blk, 0, s, b);
+  else hipLaunchKernelGGL(k_axk_x6<false>, grid, blk, 0, s, b);
+  HIP_LAUNCH_CHECK();
+}
+
 // whether launch_gemm may run a level on k_axk16: bf16, every desc a row-prologue dh GEMM
 // (A transform, K-contiguous A, MN-contiguous 16-B aligned B, mask epilogue), no rides,
 // and at least one 64x128 tile per CU
@@ -2502,7 +2892,7 @@ static int level_act16(const GemmBatch& b) {
 
 // bf16 deep-K weight-gradient levels: split count and workspace need, or 0 (k_gemm)
 static int dw_split_plan(GemmBatch& b, int64_t* stride) {
-  if (!b.bf16 || !b.ws) return 0;
+  if (!b.ws) return 0;   // (bf16: k_dw_part16; fp32: k_dw_part_x6)
   int64_t el = 0;
   int tiles = 0;
   for (int i = 0; i < b.count; ++i) {
@@ -2579,9 +2969,10 @@ static void launch_dw_split(GemmBatch& b, int ns, int64_t stride, hipStream_t s)
   const int grid = dw_grid_tiles(b.total_tiles, ns) + ride;
   const int form = level_act16(b);   // act16: every X operand bf16
   for (int i = 0; i < b.count; ++i)
-    if (b.d[i].a16 || b.d[i].c16 || b.d[i].x16 || (form && !b.d[i].b16))
+    if (b.d[i].a16 || b.d[i].c16 || b.d[i].x16 || (form && !b.d[i].b16) || (!b.bf16 && b.d[i].b16))
       throw Error{SACMI_ESTATE, "split-K weight gradient: unsupported bf16 activation operand"};
-  if (form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
+  if (!b.bf16) hipLaunchKernelGGL(k_dw_part_x6, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
+  else if (form) hipLaunchKernelGGL(k_dw_part16<true>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
   else hipLaunchKernelGGL(k_dw_part16<false>, dim3(grid), dim3(64 * kDw16Waves), 0, s, b, ns, stride);
   HIP_LAUNCH_CHECK();
   int fin_grid = 0;                    // k_dw_fin: kDwFinEpt 4-column groups per thread, per desc
@@ -2731,6 +3122,14 @@ void launch_gemm(const GemmBatch& b0, hipStream_t s) {
   if (fwd_x6_ok(b)) {
     launch_fwd_x6(b, s);
     return;
+  }
+  b = b0;
+  {
+    const int ax = axk_x6_ok(b);
+    if (ax >= 0) {
+      launch_axk_x6(b, ax, s);
+      return;
+    }
   }
   b = b0;
   if (level_act16(b))

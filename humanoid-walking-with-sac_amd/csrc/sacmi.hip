@@ -469,7 +469,7 @@ static void alloc_all(sacmi_ctx* c) {
   c->dq4.alloc((size_t)2 * Bm * 4);    // dq one value per 16-byte row (pads stay 0)
   c->nparts = (H + 31) / 32;
   // split-K dW partials (kernels.hip; bf16 only: the fp32 levels measured slower split)
-  if (c->bf16 && Bm >= 2048) c->dw_ws.alloc((size_t)16 * c->total);
+  if (Bm >= 2048) c->dw_ws.alloc((size_t)16 * c->total);   // (split-K partials: bf16 and x6 levels)
   c->dotp.alloc((size_t)6 * Bm * c->nparts);
   c->pa.alloc((size_t)2 * c->nparts * Bm * A);
   c->dhead.alloc((size_t)Bm * c->lddh);

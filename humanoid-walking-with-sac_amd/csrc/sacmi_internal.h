@@ -108,9 +108,9 @@ inline int64_t round_up64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // Null pointer (every production graph): no instruction beyond the test.
 typedef unsigned long long tl_word;
 enum TlKind : int {
-  TL_GEMM = 1, TL_FWD_X6, TL_FWD16, TL_AXK16, TL_DW_PART, TL_DW_PART16, TL_DW_FIN, TL_HEADS,
+  TL_GEMM = 1, TL_FWD_X6, TL_FWD16, TL_AXK16, TL_AXK_X6, TL_DW_PART16, TL_DW_FIN, TL_HEADS,
   TL_SAMPLE_BWD, TL_MT_SAMPLE, TL_GATHER, TL_PER_F1, TL_PER_F2, TL_PER_F2B, TL_PER_F3,
-  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_KINDS
+  TL_PER_F4, TL_PER_UNFUSED, TL_ADAM, TL_SAMPLE_TAIL, TL_FWD16P, TL_DW_PART_X6, TL_KINDS
 };
 constexpr int kTlEnd = 4;            // first of the ~end slots
 constexpr int kTlEndSlots = 4096;

@@ -118,11 +118,11 @@ _PROTOS = {
                                   c_f64p],
 }
 # kernel kinds of the launch timeline (TlKind, csrc/sacmi_internal.h)
-TL_KINDS = {1: "k_gemm", 2: "k_fwd_x6", 3: "k_fwd16", 4: "k_axk16", 5: "k_dw_part", 6: "k_dw_part16",
+TL_KINDS = {1: "k_gemm", 2: "k_fwd_x6", 3: "k_fwd16", 4: "k_axk16", 5: "k_axk_x6", 6: "k_dw_part16",
             7: "k_dw_fin", 8: "k_heads_sample", 9: "k_gemm_sample_bwd", 10: "k_mt_sample",
             11: "k_gather", 12: "k_per_f1", 13: "k_per_f2", 14: "k_per_f2b", 15: "k_per_f3",
             16: "k_per_f4", 17: "per_unfused", 18: "k_adam", 19: "k_sample_bwd_tail",
-            20: "k_fwd16p"}
+            20: "k_fwd16p", 21: "k_dw_part_x6"}
 EXPORTS = tuple(_PROTOS) + ("sacmi_abi_version", "sacmi_last_error")
 
 _lib = None

@@ -29,7 +29,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LEVEL = ("k_gemm<", "k_fwd_x6<", "k_fwd16<", "k_fwd16p<", "k_axk16<", "k_dw_part16")
+LEVEL = ("k_gemm<", "k_fwd_x6<", "k_fwd16<", "k_fwd16p<", "k_axk16<", "k_axk_x6<", "k_dw_part16", "k_dw_part_x6")
 
 
 def csrc_digest(root=ROOT):
