@@ -1588,7 +1588,14 @@ __global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), 2) void k_fwd16(GemmBatch
 // slabs; one LDS buffer (the next slab's fp32 loads in flight in registers under the MFMAs,
 // two barriers a slab) so that two workgroups share a CU.  Epilogue: k_fwd16's (bias, ReLU,
 // fc3 dot partials, fp32 stores).
-constexpr int kX6K = 32, kX6Pad = 8, kX6Waves = 8;
+// LDS rows of 48 bf16 (24 dwords): the ds_read_b128 fragment reads of a 16-row block hit 16
+// distinct 4-bank slots in each of the instruction's 16-lane groups; 40 bf16 rows put two
+// fragments on one slot in half of them.  Measured (profiles/r06/x6_lds_rows_ab): the dh
+// levels and the 64-wide forward tiles gain ~1 us each, the 128-wide forward tiles of L1
+// lose 7-8 us (L2 gains 2) — those keep 40 bf16 rows
+constexpr int kX6K = 32, kX6Waves = 8;
+template <int BN> constexpr int x6_pad() { return BN == 128 ? 8 : 16; }
+constexpr int kX6Pad = 16;
 
 // the three bf16 parts of four fp32 values, each part as four packed bf16 (k order kept)
 __device__ __forceinline__ void x6_split4(float4 v, u2v& h, u2v& m, u2v& l) {
@@ -1610,13 +1617,26 @@ __device__ __forceinline__ void x6_split4(float4 v, u2v& h, u2v& m, u2v& l) {
   h = u2v{ph[0], ph[1]}; m = u2v{pm[0], pm[1]}; l = u2v{pl[0], pl[1]};
 }
 
+#ifndef SACMI_X6_EXP
+#define SACMI_X6_EXP 0   // timing builds only (wrong values): 1 B not split, 2 neither operand
+#endif
+template <bool FAKE>
+__device__ __forceinline__ void x6_split4x(float4 v, u2v& h, u2v& m, u2v& l) {
+  if constexpr (FAKE) {
+    h = u2v{__builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x07060302u),
+            __builtin_amdgcn_perm(__float_as_uint(v.w), __float_as_uint(v.z), 0x07060302u)};
+    m = l = h;
+  } else {
+    x6_split4(v, h, m, l);
+  }
+}
 template <int BN>
 __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_FWD_X6);
   constexpr int NWV = kX6Waves, WC = 2, WR = NWV / WC;
   constexpr int MW = kFBM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
   static_assert(NT >= 2 && MI >= 1, "a wave covers whole 32-column dot blocks");
-  constexpr int LDR = kX6K + kX6Pad;     // bf16 per LDS row (80 B)
+  constexpr int LDR = kX6K + x6_pad<BN>();   // bf16 per LDS row
   constexpr int TPR = kX6K / 4;          // staging threads per row (4 k each)
   constexpr int RPP = 64 * NWV / TPR;    // rows per staging pass
   constexpr int NA = kFBM / RPP, NB = BN / RPP;
@@ -1662,7 +1682,7 @@ __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       u2v h, m, l;
-      x6_split4(ga[i], h, m, l);
+      x6_split4x<SACMI_X6_EXP >= 2>(ga[i], h, m, l);
       const int r = tid / TPR + RPP * i;
       *reinterpret_cast<u2v*>(&sA[0][r][kq]) = h;
       *reinterpret_cast<u2v*>(&sA[1][r][kq]) = m;
@@ -1671,7 +1691,7 @@ __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       u2v h, m, l;
-      x6_split4(gb[i], h, m, l);
+      x6_split4x<SACMI_X6_EXP >= 1>(gb[i], h, m, l);
       const int r = tid / TPR + RPP * i;
       *reinterpret_cast<u2v*>(&sB[0][r][kq]) = h;
       *reinterpret_cast<u2v*>(&sB[1][r][kq]) = m;
@@ -2542,7 +2562,7 @@ constexpr int kXX6K = 32;
 template <bool AX>
 __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_AXK_X6);
-  constexpr int LDA_ = kXX6K + 8;       // [row][k] bf16, 80-B rows
+  constexpr int LDA_ = kXX6K + kX6Pad;  // [row][k] bf16, 96-B rows (k_fwd_x6's)
   constexpr int LDB_ = kXBN + 8;        // [k][n] bf16, 272-B rows
   __shared__ __attribute__((aligned(16))) __bf16 sA[3][kXBM][LDA_];
   __shared__ __attribute__((aligned(16))) __bf16 sB[3][kXX6K][LDB_];

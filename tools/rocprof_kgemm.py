@@ -12,7 +12,7 @@ import sys
 def main(path):
     rows = list(csv.DictReader(open(path)))
     tot_ns = calls = 0
-    level = ("sacmi::k_gemm<", "sacmi::k_fwd_x6<", "sacmi::k_fwd16<", "sacmi::k_fwd16p<", "sacmi::k_axk16<", "sacmi::k_dw_part")
+    level = ("sacmi::k_gemm<", "sacmi::k_fwd_x6<", "sacmi::k_fwd16<", "sacmi::k_fwd16p<", "sacmi::k_axk16<", "sacmi::k_axk_x6<", "sacmi::k_dw_part")
     for r in rows:
         name, n, avg = r["Name"], int(r["Calls"]), float(r["AverageNs"])
         print(f"{name[:72]:72s} {n:7d} {avg / 1e3:9.2f} us  {float(r['Percentage']):6.2f}%")
