@@ -1617,19 +1617,6 @@ __device__ __forceinline__ void x6_split4(float4 v, u2v& h, u2v& m, u2v& l) {
   h = u2v{ph[0], ph[1]}; m = u2v{pm[0], pm[1]}; l = u2v{pl[0], pl[1]};
 }
 
-#ifndef SACMI_X6_EXP
-#define SACMI_X6_EXP 0   // timing builds only (wrong values): 1 B not split, 2 neither operand
-#endif
-template <bool FAKE>
-__device__ __forceinline__ void x6_split4x(float4 v, u2v& h, u2v& m, u2v& l) {
-  if constexpr (FAKE) {
-    h = u2v{__builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x07060302u),
-            __builtin_amdgcn_perm(__float_as_uint(v.w), __float_as_uint(v.z), 0x07060302u)};
-    m = l = h;
-  } else {
-    x6_split4(v, h, m, l);
-  }
-}
 template <int BN>
 __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_FWD_X6);
@@ -1682,7 +1669,7 @@ __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       u2v h, m, l;
-      x6_split4x<SACMI_X6_EXP >= 2>(ga[i], h, m, l);
+      x6_split4(ga[i], h, m, l);
       const int r = tid / TPR + RPP * i;
       *reinterpret_cast<u2v*>(&sA[0][r][kq]) = h;
       *reinterpret_cast<u2v*>(&sA[1][r][kq]) = m;
@@ -1691,7 +1678,7 @@ __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       u2v h, m, l;
-      x6_split4x<SACMI_X6_EXP >= 1>(gb[i], h, m, l);
+      x6_split4(gb[i], h, m, l);
       const int r = tid / TPR + RPP * i;
       *reinterpret_cast<u2v*>(&sB[0][r][kq]) = h;
       *reinterpret_cast<u2v*>(&sB[1][r][kq]) = m;
