@@ -22,7 +22,7 @@ def main(path):
         elif "sacmi::k_dw_fin" in name:
             tot_ns += avg * n                   # second kernel of a split-K level
     if calls:
-        print(f"\nGEMM levels (k_gemm all tile configs + k_fwd16* + k_axk16 + k_dw_part16/k_dw_fin): "
+        print(f"\nGEMM levels (k_gemm all tile configs + k_fwd_x6 / k_fwd16* + k_axk16 / k_axk_x6 + k_dw_part* / k_dw_fin): "
               f"{calls} levels, mean {tot_ns / calls / 1e3:.3f} us")
 
 
