@@ -1368,9 +1368,11 @@ def gpu_relu_masks(ctx, cfg, B):
     return masks
 
 
-@pytest.mark.parametrize("n_hidden", [2, 3])
-def test_step_humanoid_b4096_under_gpu_masks(n_hidden):
-    """Batch 4096 (BASELINE configs[2] shapes) at the 1e-5 gradient bar: the fp64 truth is
+@pytest.mark.parametrize("n_hidden,B", [(2, 4096), (3, 4096), (2, 3000)])
+def test_step_humanoid_b4096_under_gpu_masks(n_hidden, B):
+    """Batch 4096 (BASELINE configs[2] shapes) at the 1e-5 gradient bar — and batch 3000, whose
+    row counts are no multiple of the x6 kernels' 128-row tiles (k_fwd_x6's clamped rows, the
+    split-K ranges of k_dw_part_x6; the dh levels fall back to k_gemm): the fp64 truth is
     recomputed under the GPU's OWN ReLU masks (read back from the activations the update left
     in HBM).  Where test_step_humanoid_b4096_vs_oracle needs its ReLU-flip allowances
     (q1.fc1.weight 2.9e-4 against plain fp64), the flips are the whole story if every gradient
@@ -1379,7 +1381,6 @@ def test_step_humanoid_b4096_under_gpu_masks(n_hidden):
     cfg = SacConfig(376, 17, 512, n_hidden=n_hidden)
     params = init_params(cfg, 101, bias_scale=0.02)
     rows = synthetic_rows(cfg, 6000, 102, state_scale=0.1)
-    B = 4096
     ctx = make_ctx(cfg, max_batch=B, capacity=len(rows[2]))
     load_params(ctx, params)
     ctx.push(*rows)
@@ -1403,7 +1404,7 @@ def test_step_humanoid_b4096_under_gpu_masks(n_hidden):
     for i, k in enumerate(("q1_loss", "q2_loss", "policy_loss")):
         assert abs(lg[i] - lm[k]) <= LOSS_TOL * max(abs(lm[k]), 1e-3), (k, lg[i], lm[k])
     table = {k: (rel(gg[k], v), rel(gg[k], g64[k])) for k, v in gm.items()}
-    report_grad_errors(f"humanoid B4096 n_hidden {n_hidden} under the GPU's ReLU masks", MASKED_GRAD_TOL, table,
+    report_grad_errors(f"humanoid B{B} n_hidden {n_hidden} under the GPU's ReLU masks", MASKED_GRAD_TOL, table,
                        second="gpu_vs_plain_fp64", strict=True)
     bad = {k: e for k, (e, _) in table.items() if e > MASKED_GRAD_TOL}
     assert not bad, bad
