@@ -47,7 +47,10 @@ CONFIGS = {
                      "replay (HBM ring, device random.sample)"),
     3: dict(S=376, A=17, H=512, batch=4096, replay="per", dtype="fp32",
             workload="BASELINE configs[2]: Humanoid-v5 shapes, hidden=512, batch=4096, prioritized "
-                     "replay resident in HBM (device np.random.choice over prios**alpha)"),
+                     "replay resident in HBM (device np.random.choice over prios**alpha); fp32 "
+                     "GEMM levels on bf16 MFMA with each fp32 operand split exactly into three "
+                     "bf16 parts (6 cross products, fp32 accumulation: the x6 form, DESIGN §13j) "
+                     "except the policy dhp1 level and the sample backward (fp32 MFMA)"),
     5: dict(S=661, A=23, H=512, batch=4096, replay="uniform", dtype="bf16",
             workload="BASELINE configs[4] per GPU: NAO-walk shapes (obs 661, act 23), hidden=512, "
                      "batch=4096, uniform replay, auto-entropy on, bf16 MFMA operands (fp32 "
