@@ -2545,19 +2545,20 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
 // false) the plain dh = (dY W) * [h > 0].  64 x 128 tiles, 8 waves of 32 x 32, 32-deep slabs
 // split once per workgroup into three bf16 planes per operand: A [row][k], B = W k-major
 // [k][n] read transposed (ds_read_b64_tr_b16); one LDS buffer, two workgroups per CU.
+// (BN: the tile width — 128, or 64 for a one-net level, which then gets two workgroups per CU)
 constexpr int kXX6K = 32;
-template <bool AX>
+template <bool AX, int BN = kXBN>
 __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_AXK_X6);
   constexpr int LDA_ = kXX6K + kX6Pad;  // [row][k] bf16, 96-B rows (k_fwd_x6's)
-  constexpr int LDB_ = kXBN + 8;        // [k][n] bf16, 272-B rows
+  constexpr int LDB_ = BN + 8;          // [k][n] bf16
   __shared__ __attribute__((aligned(16))) __bf16 sA[3][kXBM][LDA_];
   __shared__ __attribute__((aligned(16))) __bf16 sB[3][kXX6K][LDB_];
   __shared__ float s_q[kXBM][4], s_coef[2][kXBM], s_l[kXBM][2];
-  constexpr int NWV = kAxWaves, NTH = 64 * NWV, WC = NWV / 2, NJ = kXBN / WC / 16;
+  constexpr int NWV = kAxWaves, NTH = 64 * NWV, WC = NWV / 2, NJ = BN / WC / 16;
   constexpr int TPRA = kXX6K / 4, ARP = NTH / TPRA, NAI = kXBM / ARP;   // A staging
-  constexpr int BKP = NTH / 32, NBI = kXX6K / BKP;                      // B staging
-  static_assert(NAI >= 1 && NBI >= 1 && NJ == 2, "k_axk_x6 staging");
+  constexpr int TPRB = BN / 4, BKP = NTH / TPRB, NBI = kXX6K / BKP;     // B staging
+  static_assert(NAI >= 1 && NBI >= 1 && NJ >= 1, "k_axk_x6 staging");
   const int bid = blockIdx.x;
   if (bid >= batch.total_tiles) {   // ride-along: the next update's gather, a row a wave
     const int wv = (bid - batch.total_tiles) * NWV + (int)(threadIdx.x >> 6), nwv = batch.ride.nblocks * NWV;
@@ -2573,9 +2574,9 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
   if (t >= d.tiles_m * d.tiles_n) return;
   int tr, tc;
   place_tile(d, t, tr, tc);
-  const int m0 = tr * kXBM, n0 = tc * kXBN;
+  const int m0 = tr * kXBM, n0 = tc * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave / WC) * 32, wn = (wave % WC) * (kXBN / WC);
+  const int wm = (wave / WC) * 32, wn = (wave % WC) * (BN / WC);
   const int M = d.M, N = d.N, K = d.K;
   const rsrc_t rA = make_rsrc(d.A, 0x7fffffffu), rB = make_rsrc(d.B, 0x7fffffffu);
   const rsrc_t rW = make_rsrc(AX ? d.ax_w : d.A, AX ? (uint32_t)K * 4u : 0u);
@@ -2583,8 +2584,8 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
   const rsrc_t rAx = make_rsrc(store_a ? d.ax_out : d.C,
                                store_a ? (uint32_t)(((size_t)(M - 1) * d.ax_ld + K) * 4) : 0u);
   // A staging: rows tid / TPRA + ARP i at k = 4 (tid % TPRA); B staging: k rows
-  // (tid >> 5) + BKP i at columns 4 (tid & 31)
-  const int kq = 4 * (tid % TPRA), c4 = 4 * (tid & 31), kr0 = tid >> 5;
+  // tid / TPRB + BKP i at columns 4 (tid % TPRB)
+  const int kq = 4 * (tid % TPRA), c4 = 4 * (tid % TPRB), kr0 = tid / TPRB;
   uint32_t offA[NAI];
 #pragma unroll
   for (int i = 0; i < NAI; ++i)
@@ -2726,7 +2727,7 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
 }
 
 // whether launch_gemm may run an fp32 level on k_axk_x6: k_axk16's level form in fp32 mode
-// (-1: no; 1: the row-prologue form; 0: the plain dh form)
+// (-1: no; else bit 0: the row-prologue form, bit 1: 64-wide tiles)
 static int axk_x6_ok(GemmBatch& b) {
   if (b.bf16 || (b.ride.kind && b.ride.kind != 2) || b.ride.pk_blocks || b.has_adam) return -1;
   const int ax = b.d[0].axk == 1 ? 1 : 0;
@@ -2740,15 +2741,21 @@ static int axk_x6_ok(GemmBatch& b) {
         (ax && ((uintptr_t)d.ax_w & 15)) || (d.N & 3))
       return -1;
   }
-  // two workgroups per CU: a one-net level (the policy's dhp1, 256 tiles) measured slower
-  // than its k_gemm form (config 3 L12 28.0-29.5 vs 27.1-27.2 us)
-  return assign_tiles<kXBM, kXBN>(b) >= 512 ? ax : -1;
+  // two workgroups per CU: 128-wide tiles where they give 512, else 64-wide ones (a one-net
+  // level: the policy's dhp1; at 128 wide its 256 tiles measured slower than its k_gemm
+  // form, config 3 L12 28.0-29.5 vs 27.1-27.2 us)
+  if (assign_tiles<kXBM, kXBN>(b) >= 512) return ax;
+  return assign_tiles<kXBM, 64>(b) >= 512 ? ax | 2 : -1;
 }
 
-static void launch_axk_x6(const GemmBatch& b, int ax, hipStream_t s) {
+static void launch_axk_x6(const GemmBatch& b, int form, hipStream_t s) {
   const dim3 grid(b.total_tiles + (b.ride.kind ? b.ride.nblocks : 0)), blk(64 * kAxWaves);
-  if (ax) hipLaunchKernelGGL(k_axk_x6<true>, grid, blk, 0, s, b);
-  else hipLaunchKernelGGL(k_axk_x6<false>, grid, blk, 0, s, b);
+  switch (form) {
+    case 0: hipLaunchKernelGGL((k_axk_x6<false>), grid, blk, 0, s, b); break;
+    case 1: hipLaunchKernelGGL((k_axk_x6<true>), grid, blk, 0, s, b); break;
+    case 2: hipLaunchKernelGGL((k_axk_x6<false, 64>), grid, blk, 0, s, b); break;
+    default: hipLaunchKernelGGL((k_axk_x6<true, 64>), grid, blk, 0, s, b); break;
+  }
   HIP_LAUNCH_CHECK();
 }
 
