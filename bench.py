@@ -50,7 +50,7 @@ CONFIGS = {
                      "replay resident in HBM (device np.random.choice over prios**alpha); fp32 "
                      "GEMM levels on bf16 MFMA with each fp32 operand split exactly into three "
                      "bf16 parts (6 cross products, fp32 accumulation: the x6 form, DESIGN §13j) "
-                     "except the policy dhp1 level and the sample backward (fp32 MFMA)"),
+                     "except the policy heads and the sample backward (fp32 MFMA)"),
     5: dict(S=661, A=23, H=512, batch=4096, replay="uniform", dtype="bf16",
             workload="BASELINE configs[4] per GPU: NAO-walk shapes (obs 661, act 23), hidden=512, "
                      "batch=4096, uniform replay, auto-entropy on, bf16 MFMA operands (fp32 "
