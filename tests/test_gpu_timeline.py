@@ -80,3 +80,36 @@ def test_timeline_of_the_data_parallel_sequence():
         pa, pb = a.get_net(n), b.get_net(n)
         for k in pa:
             assert np.array_equal(pa[k], pb[k]), (n, k)
+
+
+@pytest.mark.parametrize("B,x6", [(4096, True), (256, False)])
+def test_fp32_level_kernels_by_batch_class(B, x6):
+    """Which kernel runs each fp32 GEMM level: at batch 4096 the forward levels
+    on k_fwd_x6, the dh levels (critic / actor dh1, policy dhp1) on k_axk_x6 and the weight
+    gradients split-K on k_dw_part_x6 + k_dw_fin — the x6 path must be the one the batch-4096
+    parity tests and bench lines exercise, not a silent k_gemm fallback; at batch 256 every
+    level stays on the fp32 MFMA k_gemm."""
+    from sacmi import Config, Context
+    cfg = SacConfig(376, 17, 512)
+    params = init_params(cfg, 11, bias_scale=0.02)
+    c = Context(Config(376, 17, 512, max_batch=B, capacity=6000, seed=3), 0)
+    for n in NETS:
+        c.set_net(n, params[n])
+    c.push(*synthetic_rows(cfg, 6000, 12, state_scale=0.1))
+    ks, _ = c.profile_timeline(B, 1)
+    by_site = {}
+    for k in ks:
+        by_site.setdefault(k["site"], []).append(k["kernel"])
+    want = {"gemm_L1_fc1": ["k_fwd_x6"], "gemm_L2_fc2": ["k_fwd_x6"], "gemm_L3_tgt_fc1": ["k_fwd_x6"],
+            "gemm_L4_tgt_fc2": ["k_fwd_x6"], "gemm_L7_act_fc1": ["k_fwd_x6"], "gemm_L8_act_fc2": ["k_fwd_x6"],
+            "gemm_L5_critic_dh1": ["k_axk_x6"], "gemm_L9_act_dh1": ["k_axk_x6"], "gemm_L12_pi_dhp1": ["k_axk_x6"],
+            "gemm_L6_critic_dW_adam": ["k_dw_part_x6", "k_dw_fin"],
+            "gemm_L13_pi_dW_adam": ["k_dw_part_x6", "k_dw_fin"]}
+    for site, kernels in want.items():
+        got = by_site.get(site)
+        assert got, (site, sorted(by_site))
+        if x6:
+            assert got == kernels, (site, got)
+        else:
+            assert got == ["k_gemm"], (site, got)
+    c.close()
