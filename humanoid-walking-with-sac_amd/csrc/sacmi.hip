@@ -353,11 +353,13 @@ static hipGraphExec_t capture_graph(sacmi_ctx* c, F&& body) {
 static void build_layout(sacmi_ctx* c) {
   const int S = c->S, A = c->A, H = c->H;
   // bf16 mode: rows of 8-element multiples, so every bf16 activation / weight-shadow row
-  // starts 16-byte aligned (k_fwd16p's LDS-DMA moves 16-byte chunks).  fp32 contexts of the
-  // batch-4096 class: whole 128-byte rows (the x6 kernels stage 128-byte row segments per
-  // slab: config 3 1,883-1,889 -> 1,912-1,924 updates/s); the batch-256 class keeps 16-byte
-  // rows (128-byte ones cost config 2 6 %: 8,968-8,993 -> 8,420-8,435, profiles/r06/row_pad_ab)
-  const int pad = c->bf16 ? 8 : c->Bm >= 2048 ? 32 : 4;
+  // starts 16-byte aligned (k_fwd16p's LDS-DMA moves 16-byte chunks).  Contexts of the
+  // batch-4096 class: whole 128-byte rows of either width (the level kernels stage 128-byte
+  // row segments per slab: config 3 1,883-1,889 -> 1,912-1,924 updates/s; config 5 3,331-3,381
+  // -> 3,407-3,469, the forward levels 1-2 us each faster, profiles/r06/row_pad_ab and
+  // row_pad_bf16_ab); the batch-256 class keeps 16-byte rows (128-byte ones cost config 2 6 %:
+  // 8,968-8,993 -> 8,420-8,435)
+  const int pad = c->Bm >= 2048 ? (c->bf16 ? 64 : 32) : (c->bf16 ? 8 : 4);
   c->Kx = round_up(S + 1 + A, pad);
   c->Hd = round_up(H + 1, pad);
   c->Kp1 = round_up(S + 1, pad);
