@@ -357,9 +357,10 @@ static void build_layout(sacmi_ctx* c) {
   // batch-4096 class: whole 128-byte rows of either width (the level kernels stage 128-byte
   // row segments per slab: config 3 1,883-1,889 -> 1,912-1,924 updates/s; config 5 3,331-3,381
   // -> 3,407-3,469, the forward levels 1-2 us each faster, profiles/r06/row_pad_ab and
-  // row_pad_bf16_ab); the batch-256 class keeps 16-byte rows (128-byte ones cost config 2 6 %:
-  // 8,968-8,993 -> 8,420-8,435)
-  const int pad = c->Bm >= 2048 ? (c->bf16 ? 64 : 32) : (c->bf16 ? 8 : 4);
+  // row_pad_bf16_ab); the fp32 batch-256 class takes 32-byte rows (config 2: 16-byte 8,992-9,018,
+  // 32-byte 9,043-9,093, 64-byte 8,972-8,979 steps/s, profiles/r06/row_pad_small_ab; 128-byte
+  // ones cost 6 %: 8,968-8,993 -> 8,420-8,435)
+  const int pad = c->Bm >= 2048 ? (c->bf16 ? 64 : 32) : 8;
   c->Kx = round_up(S + 1 + A, pad);
   c->Hd = round_up(H + 1, pad);
   c->Kp1 = round_up(S + 1, pad);
