@@ -1588,13 +1588,12 @@ __global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), 2) void k_fwd16(GemmBatch
 // slabs; one LDS buffer (the next slab's fp32 loads in flight in registers under the MFMAs,
 // two barriers a slab) so that two workgroups share a CU.  Epilogue: k_fwd16's (bias, ReLU,
 // fc3 dot partials, fp32 stores).
-// LDS rows of 48 bf16 (24 dwords): the ds_read_b128 fragment reads of a 16-row block hit 16
-// distinct 4-bank slots in each of the instruction's 16-lane groups; 40 bf16 rows put two
-// fragments on one slot in half of them.  Measured (profiles/r06/x6_lds_rows_ab): the dh
-// levels and the 64-wide forward tiles gain ~1 us each, the 128-wide forward tiles of L1
-// lose 7-8 us (L2 gains 2) — those keep 40 bf16 rows
+// LDS rows: k_axk_x6's A planes 48 bf16 (24 dwords), so that the ds_read_b128 fragment reads
+// of a 16-row block hit 16 distinct 4-bank slots in each of the instruction's 16-lane groups
+// (40 bf16 rows put two fragments on one slot in half of them; profiles/r06/x6_lds_rows_ab);
+// k_fwd_x6's planes unpadded 32-bf16 rows with an XOR chunk swizzle (below), conflict-free
+// for the reads and the staging stores alike and 20-25 % less LDS
 constexpr int kX6K = 32, kX6Waves = 8;
-template <int BN> constexpr int x6_pad() { return BN == 128 ? 8 : 16; }
 constexpr int kX6Pad = 16;
 
 // the three bf16 parts of four fp32 values, each part as four packed bf16 (k order kept)
@@ -1623,13 +1622,17 @@ __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
   constexpr int NWV = kX6Waves, WC = 2, WR = NWV / WC;
   constexpr int MW = kFBM / WR, MI = MW / 16, NW = BN / WC, NT = NW / 16;
   static_assert(NT >= 2 && MI >= 1, "a wave covers whole 32-column dot blocks");
-  constexpr int LDR = kX6K + x6_pad<BN>();   // bf16 per LDS row
+  // 64-B rows, each row's 16-B k chunks stored at chunk ^ ((row >> 2) & 2): the 16 lanes of
+  // every ds_read_b128 lane group on 16 distinct 4-bank slots, the two rows of each
+  // ds_write_b64 lane group on all 32 banks (profiles/r06/x6_swizzle_ab)
+  constexpr int LDR = kX6K;
   constexpr int TPR = kX6K / 4;          // staging threads per row (4 k each)
   constexpr int RPP = 64 * NWV / TPR;    // rows per staging pass
   constexpr int NA = kFBM / RPP, NB = BN / RPP;
   static_assert(NA >= 1 && NB >= 1, "staging passes");
   __shared__ __attribute__((aligned(16))) __bf16 sA[3][kFBM][LDR];
   __shared__ __attribute__((aligned(16))) __bf16 sB[3][BN][LDR];
+  auto cw = [](int r, int k) { return (((k >> 3) ^ ((r >> 2) & 2)) << 3) | (k & 7); };
   const int bid = blockIdx.x;
   int p = 0;
   for (int q = 1; q < batch.count; ++q)
@@ -1670,19 +1673,19 @@ __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
     for (int i = 0; i < NA; ++i) {
       u2v h, m, l;
       x6_split4(ga[i], h, m, l);
-      const int r = tid / TPR + RPP * i;
-      *reinterpret_cast<u2v*>(&sA[0][r][kq]) = h;
-      *reinterpret_cast<u2v*>(&sA[1][r][kq]) = m;
-      *reinterpret_cast<u2v*>(&sA[2][r][kq]) = l;
+      const int r = tid / TPR + RPP * i, c = cw(r, kq);
+      *reinterpret_cast<u2v*>(&sA[0][r][c]) = h;
+      *reinterpret_cast<u2v*>(&sA[1][r][c]) = m;
+      *reinterpret_cast<u2v*>(&sA[2][r][c]) = l;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       u2v h, m, l;
       x6_split4(gb[i], h, m, l);
-      const int r = tid / TPR + RPP * i;
-      *reinterpret_cast<u2v*>(&sB[0][r][kq]) = h;
-      *reinterpret_cast<u2v*>(&sB[1][r][kq]) = m;
-      *reinterpret_cast<u2v*>(&sB[2][r][kq]) = l;
+      const int r = tid / TPR + RPP * i, c = cw(r, kq);
+      *reinterpret_cast<u2v*>(&sB[0][r][c]) = h;
+      *reinterpret_cast<u2v*>(&sB[1][r][c]) = m;
+      *reinterpret_cast<u2v*>(&sB[2][r][c]) = l;
     }
   };
   f4 acc[MI][NT];
@@ -1696,7 +1699,7 @@ __global__ __launch_bounds__(64 * kX6Waves, 2) void k_fwd_x6(GemmBatch batch) {
   swrite();
   __syncthreads();
   const int nslab = (K + kX6K - 1) / kX6K;
-  const int kc = 8 * (lane >> 4);
+  const int kc = cw(lane & 15, 8 * (lane >> 4));   // (row blocks start at multiples of 16)
   for (int sl = 0; sl < nslab; ++sl) {
     if (sl + 1 < nslab) gload((sl + 1) * kX6K);
     // the A parts of every row block, then each B column block's parts just before its
@@ -2547,10 +2550,19 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
 // [k][n] read transposed (ds_read_b64_tr_b16); one LDS buffer, two workgroups per CU.
 // (BN: the tile width — 128, or 64 for a one-net level, which then gets two workgroups per CU)
 constexpr int kXX6K = 32;
+#ifndef SACMI_AXS
+#define SACMI_AXS 0
+#endif
 template <bool AX, int BN = kXBN>
 __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_AXK_X6);
+#if SACMI_AXS
+  constexpr int LDA_ = kXX6K;           // [row][k] bf16, 64-B rows, k_fwd_x6's chunk swizzle
+  auto cw = [](int r, int k) { return (((k >> 3) ^ ((r >> 2) & 2)) << 3) | (k & 7); };
+#else
   constexpr int LDA_ = kXX6K + kX6Pad;  // [row][k] bf16, 96-B rows (k_fwd_x6's)
+  auto cw = [](int, int k) { return k; };
+#endif
   constexpr int LDB_ = BN + 8;          // [k][n] bf16
   __shared__ __attribute__((aligned(16))) __bf16 sA[3][kXBM][LDA_];
   __shared__ __attribute__((aligned(16))) __bf16 sB[3][kXX6K][LDB_];
@@ -2621,9 +2633,9 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
       const int r = tid / TPRA + ARP * i;
       u2v h, m, l;
       x6_split4(u, h, m, l);
-      *reinterpret_cast<u2v*>(&sA[0][r][kq]) = h;
-      *reinterpret_cast<u2v*>(&sA[1][r][kq]) = m;
-      *reinterpret_cast<u2v*>(&sA[2][r][kq]) = l;
+      *reinterpret_cast<u2v*>(&sA[0][r][cw(r, kq)]) = h;
+      *reinterpret_cast<u2v*>(&sA[1][r][cw(r, kq)]) = m;
+      *reinterpret_cast<u2v*>(&sA[2][r][cw(r, kq)]) = l;
       if (fresh) {
         const int rr = m0 + r;
         buf_st4(rAx, (rr < M && k < K) ? (uint32_t)(rr * d.ax_ld + k) * 4u : 0xfffffff0u,
@@ -2667,16 +2679,16 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
   __syncthreads();
   const int nslab = (K + kXX6K - 1) / kXX6K;
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg = lane >> 4;
-  const int kc = 8 * tg;
+  const int kc = 8 * tg, kca = cw(lane & 15, kc);
   for (int sl = 0; sl < nslab; ++sl) {
     if (sl + 1 < nslab) gload((sl + 1) * kXX6K);
     bf16x8 ah[2], am[2], al[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r = wm + i * 16 + (lane & 15);
-      ah[i] = *reinterpret_cast<const bf16x8*>(&sA[0][r][kc]);
-      am[i] = *reinterpret_cast<const bf16x8*>(&sA[1][r][kc]);
-      al[i] = *reinterpret_cast<const bf16x8*>(&sA[2][r][kc]);
+      ah[i] = *reinterpret_cast<const bf16x8*>(&sA[0][r][kca]);
+      am[i] = *reinterpret_cast<const bf16x8*>(&sA[1][r][kca]);
+      al[i] = *reinterpret_cast<const bf16x8*>(&sA[2][r][kca]);
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
