@@ -1588,13 +1588,11 @@ __global__ __launch_bounds__(64 * fwd16_waves<kFBN>(), 2) void k_fwd16(GemmBatch
 // slabs; one LDS buffer (the next slab's fp32 loads in flight in registers under the MFMAs,
 // two barriers a slab) so that two workgroups share a CU.  Epilogue: k_fwd16's (bias, ReLU,
 // fc3 dot partials, fp32 stores).
-// LDS rows: k_axk_x6's A planes 48 bf16 (24 dwords), so that the ds_read_b128 fragment reads
-// of a 16-row block hit 16 distinct 4-bank slots in each of the instruction's 16-lane groups
-// (40 bf16 rows put two fragments on one slot in half of them; profiles/r06/x6_lds_rows_ab);
-// k_fwd_x6's planes unpadded 32-bf16 rows with an XOR chunk swizzle (below), conflict-free
-// for the reads and the staging stores alike and 20-25 % less LDS
+// LDS rows (k_fwd_x6's planes and k_axk_x6's A planes): unpadded 32-bf16 rows with an XOR
+// chunk swizzle (below), conflict-free for the ds_read_b128 fragment reads and the staging
+// stores alike, and 20-30 % less LDS than the padded 40 / 48-bf16 rows they replace
+// (profiles/r06/x6_lds_rows_ab, x6_swizzle_ab)
 constexpr int kX6K = 32, kX6Waves = 8;
-constexpr int kX6Pad = 16;
 
 // the three bf16 parts of four fp32 values, each part as four packed bf16 (k order kept)
 __device__ __forceinline__ void x6_split4(float4 v, u2v& h, u2v& m, u2v& l) {
@@ -2550,19 +2548,12 @@ __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk16(GemmBatch batch) {
 // [k][n] read transposed (ds_read_b64_tr_b16); one LDS buffer, two workgroups per CU.
 // (BN: the tile width — 128, or 64 for a one-net level, which then gets two workgroups per CU)
 constexpr int kXX6K = 32;
-#ifndef SACMI_AXS
-#define SACMI_AXS 0
-#endif
 template <bool AX, int BN = kXBN>
 __global__ __launch_bounds__(64 * kAxWaves, 2) void k_axk_x6(GemmBatch batch) {
   const TlMark tl_mark(batch.tl, TL_AXK_X6);
-#if SACMI_AXS
-  constexpr int LDA_ = kXX6K;           // [row][k] bf16, 64-B rows, k_fwd_x6's chunk swizzle
+  // [row][k] bf16, 64-B rows with k_fwd_x6's chunk swizzle (profiles/r06/x6_swizzle_ab)
+  constexpr int LDA_ = kXX6K;
   auto cw = [](int r, int k) { return (((k >> 3) ^ ((r >> 2) & 2)) << 3) | (k & 7); };
-#else
-  constexpr int LDA_ = kXX6K + kX6Pad;  // [row][k] bf16, 96-B rows (k_fwd_x6's)
-  auto cw = [](int, int k) { return k; };
-#endif
   constexpr int LDB_ = BN + 8;          // [k][n] bf16
   __shared__ __attribute__((aligned(16))) __bf16 sA[3][kXBM][LDA_];
   __shared__ __attribute__((aligned(16))) __bf16 sB[3][kXX6K][LDB_];
